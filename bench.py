@@ -1,0 +1,287 @@
+#!/usr/bin/env python3
+"""Benchmark: windowed GROUP BY records/s on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over the configured workload: reset the
+operator's HBM state, push every batch of the (HBM-resident, synthetic) input
+through libhstream_gpu and drain each batch's changelog into HBM. Default
+workload = BASELINE config C2 (tumbling 60 s COUNT/SUM/AVG/MIN/MAX, 100M
+records, 64K uniform keys, batches of 2^24), which fits one GPU.
+
+Multi-GPU: launched by torch.distributed.run, one process per GPU; every rank
+ingests its own C2-sized slice (weak scaling) and the library exchanges
+records by key hash over RCCL, so each GPU owns its key range's state.
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--config", default="C2")
+    p.add_argument("--records", type=int, default=0, help="records per rank per step (default: the config's N)")
+    p.add_argument("--batch", type=int, default=0, help="records per push (default: the config's batch)")
+    p.add_argument("--emit", default="per_batch", choices=["per_batch", "per_record", "none"])
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget (0 = skip)")
+    p.add_argument("--traffic-csv", default="", help="rocprofv3 --pmc counter CSV to fill roofline.traffic")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from hstream_amd import abi, datagen
+    from hstream_amd.engine import Engine, comm_unique_id
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = datagen.CONFIGS[args.config]
+    n_rank = args.records or cfg.n
+    batch = args.batch or min(cfg.batch, n_rank)
+    emit = {"per_batch": abi.HSG_EMIT_PER_BATCH, "per_record": abi.HSG_EMIT_PER_RECORD,
+            "none": abi.HSG_EMIT_NONE}[args.emit]
+
+    comm_id = None
+    if world > 1:
+        idt = torch.zeros(abi.HSG_COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            idt.copy_(torch.frombuffer(bytearray(comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(idt, 0)
+        comm_id = bytes(idt.cpu().numpy().tobytes())
+    eng = Engine(device=local, rank=rank, nranks=world, comm_id=comm_id, batch_capacity=batch)
+
+    # state sized for the config: distinct (key, window) groups over the whole run
+    windows = 3_600_000 // (cfg.advance_ms or cfg.size_ms or 60_000) + 2 if cfg.window_kind != abi.HSG_SESSION else 1
+    groups = min(cfg.keys, n_rank * world) * windows
+    spec = cfg.spec(emit, state_capacity=max(1 << 16, groups))
+    op = eng.op(spec)
+    f64 = spec.agg_is_f64()
+
+    # synthetic input resident in HBM before timing: this rank's slice of every step
+    data = datagen.generate_torch(cfg, n_rank, device=dev, start=rank * n_rank, total=n_rank * world)
+    keys, ts = data["key_id"], data["ts"]
+    cols = data["cols"] if spec.col_types else []
+    pieces = [(s, min(batch, n_rank - s)) for s in range(0, n_rank, batch)]
+    out_cap = max(1, eng_out_capacity(op))
+    outs = {
+        "key_id": torch.empty(out_cap, dtype=torch.int32, device=dev),
+        "win_start": torch.empty(out_cap, dtype=torch.int64, device=dev),
+        "win_end": torch.empty(out_cap, dtype=torch.int64, device=dev),
+        "src_index": torch.empty(out_cap, dtype=torch.int64, device=dev),
+        "aggs": [torch.empty(out_cap, dtype=torch.float64 if f else torch.int64, device=dev) for f in f64],
+    }
+    drain_dev = make_device_drain(op, outs, out_cap)
+
+    def step():
+        op.reset()
+        wm = -1
+        for s, m in pieces:
+            wm = op.push(keys[s:s + m], ts[s:s + m], [c[s:s + m] for c in cols], None, watermark=wm,
+                         mem=abi.HSG_MEM_DEVICE)
+            if emit != abi.HSG_EMIT_NONE:
+                drain_dev()
+        return wm
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    st0 = op.stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st1 = op.stats()
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    total_records = n_rank * world * args.steps
+    value = total_records / elapsed
+
+    # roofline of the dominant kernel (window assignment + hash aggregation)
+    launches = st1["agg_kernel_launches"] - st0["agg_kernel_launches"]
+    agg_s = (st1["agg_kernel_ms"] - st0["agg_kernel_ms"]) / 1e3
+    n_slots = len(spec_state_slots(spec))
+    ncol = len(spec.col_types)
+    rec_bytes = 4 + 8 + 8 * ncol
+    row_bytes = 8 + 8 * n_slots
+    touched = st1["touched_total"] - st0["touched_total"]
+    owned = (st1["records_owned"] - st0["records_owned"])
+    alg_bytes = owned * rec_bytes + 2 * touched * row_bytes
+    achieved = (alg_bytes / agg_s / 1e9) if agg_s > 0 else 0.0
+    traffic = traffic_from_csv(args.traffic_csv, launches) if args.traffic_csv else None
+    roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+            "kernel": "k_tw_agg", "alg_bytes_per_launch": int(alg_bytes / max(1, launches)),
+            "avg_launch_ms": round(agg_s * 1e3 / max(1, launches), 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(cfg, spec, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "records/sec windowed GROUP BY",
+            "value": round(value, 1),
+            "unit": "records/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64" if cfg.col_type == abi.HSG_F64 else "int64",
+            "data": "synthetic",
+            "config": {"workload": f"{cfg.name}: {workload_text(cfg)}", "records_per_gpu": n_rank,
+                       "batch": batch, "keys": cfg.keys, "emit": args.emit,
+                       "parallelism": f"key-hash sharded x{world}" if world > 1 else "single GPU"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "agg_kernel_share": round(agg_s / elapsed, 4) if elapsed > 0 else None,
+            "pairs_per_step": int((st1["pairs_total"] - st0["pairs_total"]) / max(1, args.steps)),
+            "touched_per_step": int(touched / max(1, args.steps)),
+        }
+        print(json.dumps(line), flush=True)
+    op.close()
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def workload_text(cfg):
+    from hstream_amd import abi
+    kind = {abi.HSG_TUMBLING: f"tumbling {cfg.size_ms // 1000}s", abi.HSG_HOPPING:
+            f"hopping {cfg.size_ms // 1000}s/{cfg.advance_ms // 1000}s", abi.HSG_SESSION:
+            f"session gap {cfg.gap_ms // 1000}s", abi.HSG_UNWINDOWED: "unwindowed"}[cfg.window_kind]
+    names = {0: "COUNT(*)", 1: "COUNT", 2: "SUM", 3: "MIN", 4: "MAX", 5: "AVG", 6: "LAST"}
+    aggs = "/".join(names[k] for k, _ in cfg.aggs)
+    return f"{kind} {aggs}, {cfg.keys} keys{' zipf ' + str(cfg.zipf) if cfg.zipf else ' uniform'}"
+
+
+def eng_out_capacity(op):
+    # enough for the rows one batch can emit (per-batch: touched groups)
+    from hstream_amd import abi
+    spec = op.spec
+    if spec.emit_mode == abi.HSG_EMIT_NONE:
+        return 1
+    return op.engine.batch_capacity * op.engine.nranks * (
+        -(-spec.size_ms // spec.advance_ms) if spec.window_kind == abi.HSG_HOPPING else 1)
+
+
+def make_device_drain(op, outs, cap):
+    import ctypes as C
+    from hstream_amd import abi
+    agg_ptrs = (C.c_void_p * max(1, len(outs["aggs"])))(*[t.data_ptr() for t in outs["aggs"]])
+    rows = abi.hsg_rows(capacity=cap, mem=abi.HSG_MEM_DEVICE, n_aggs=len(outs["aggs"]),
+                        key_id=outs["key_id"].data_ptr(), win_start=outs["win_start"].data_ptr(),
+                        win_end=outs["win_end"].data_ptr(), src_index=outs["src_index"].data_ptr(),
+                        aggs=C.cast(agg_ptrs, C.POINTER(C.c_void_p)))
+    got = C.c_uint64(0)
+
+    def drain():
+        rc = op._lib.hsg_drain(op._h, C.byref(rows), C.byref(got))
+        if rc != abi.HSG_OK:
+            raise abi.HStreamGpuError(rc, "hsg_drain")
+        return got.value
+
+    drain.keep = (agg_ptrs, rows, outs)
+    return drain
+
+
+def spec_state_slots(spec):
+    """State words per group (mirrors build_program in csrc/hsg_api.cpp)."""
+    from hstream_amd import abi
+    slots = []
+    for kind, col in spec.aggs:
+        isf = kind != abi.HSG_COUNT_ALL and spec.col_types[col] == abi.HSG_F64
+        if kind == abi.HSG_COUNT_ALL:
+            need = [("cnt_all", 0)]
+        elif kind == abi.HSG_COUNT:
+            need = [("cnt", col)]
+        elif kind == abi.HSG_AVG:
+            need = [("sum", col), ("cnt", col)]
+        elif kind == abi.HSG_LAST:
+            need = [("lseq", col), ("lval", col)]
+        else:
+            need = [({2: "sum", 3: "min", 4: "max"}[kind], col, isf)]
+        for s in need:
+            if s not in slots:
+                slots.append(s)
+    return slots
+
+
+def traffic_from_csv(path, launches):
+    """Sum FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE over k_tw_agg rows of a
+    rocprofv3 --pmc counter_collection.csv, per launch, in bytes."""
+    import csv
+    fetch = write = 0.0
+    n = set()
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if "k_tw_agg" not in r.get("Kernel_Name", ""):
+                continue
+            n.add(r.get("Dispatch_Id"))
+            name, val = r.get("Counter_Name"), float(r.get("Counter_Value", 0))
+            if name == "FETCH_SIZE":
+                fetch += val
+            elif name == "WRITE_SIZE":
+                write += val
+    if not n:
+        return None
+    return int((2 * fetch + write) * 1024 / len(n))
+
+
+def cpu_baseline(cfg, spec, seconds):
+    """The oracle (sequential restatement, ordered-map store) on a bounded sample
+    of the same workload, single thread, on this host."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from hstream_amd import abi, datagen
+    o = pyoracle.OracleOp(spec, faithful_sessions=True)
+    chunk = 1 << 18
+    done = 0
+    wm = -1
+    t_used = 0.0
+    while t_used < seconds and done < cfg.n:
+        h = datagen.generate(cfg, n=chunk, start=done, total=cfg.n)
+        t0 = time.perf_counter()
+        wm = o.push(h["key_id"], h["ts"], h["cols"] if spec.col_types else [], None, watermark=wm)
+        if spec.emit_mode != abi.HSG_EMIT_NONE:
+            o.drain()
+        t_used += time.perf_counter() - t0
+        done += chunk
+    o.close()
+    return {"value": round(done / t_used, 1), "unit": "records/s", "cores": 1, "kind": "port",
+            "sample": f"first {done} records of {cfg.name} (same generator), oracle/hsoracle.cpp ordered-map "
+                      f"restatement, 1 thread, {os.cpu_count()} host CPUs visible"}
+
+
+if __name__ == "__main__":
+    main()

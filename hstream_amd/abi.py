@@ -1,0 +1,172 @@
+"""ctypes mirror of include/hstream_gpu.h (structs, enums, status codes).
+
+Kept in one place so the product binding (``hstream_amd.engine``) and the test
+oracle binding (``oracle/pyoracle.py``) describe the exact same ABI.
+"""
+import ctypes as C
+
+HSG_OK = 0
+HSG_E_INVALID = -1
+HSG_E_OOM = -2
+HSG_E_CAPACITY = -3
+HSG_E_DEVICE = -4
+HSG_E_COMM = -5
+HSG_E_RANGE = -6
+
+STATUS_NAMES = {
+    HSG_OK: "HSG_OK",
+    HSG_E_INVALID: "HSG_E_INVALID",
+    HSG_E_OOM: "HSG_E_OOM",
+    HSG_E_CAPACITY: "HSG_E_CAPACITY",
+    HSG_E_DEVICE: "HSG_E_DEVICE",
+    HSG_E_COMM: "HSG_E_COMM",
+    HSG_E_RANGE: "HSG_E_RANGE",
+}
+
+HSG_KEY_NONE = 0xFFFFFFFF
+HSG_COMM_ID_BYTES = 128
+HSG_DEFAULT_GRACE_MS = 86400000
+
+# hsg_window_kind
+HSG_TUMBLING = 0
+HSG_HOPPING = 1
+HSG_SESSION = 2
+HSG_UNWINDOWED = 3
+
+# hsg_emit_mode
+HSG_EMIT_PER_RECORD = 0
+HSG_EMIT_PER_BATCH = 1
+HSG_EMIT_NONE = 2
+
+# hsg_col_type
+HSG_I64 = 0
+HSG_F64 = 1
+
+# hsg_agg_kind
+HSG_COUNT_ALL = 0
+HSG_COUNT = 1
+HSG_SUM = 2
+HSG_MIN = 3
+HSG_MAX = 4
+HSG_AVG = 5
+HSG_LAST = 6
+
+# hsg_mem
+HSG_MEM_HOST = 0
+HSG_MEM_DEVICE = 1
+
+
+class hsg_engine_config(C.Structure):
+    _fields_ = [
+        ("device", C.c_int32),
+        ("rank", C.c_int32),
+        ("nranks", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("comm_id", C.POINTER(C.c_uint8)),
+        ("batch_capacity", C.c_uint64),
+    ]
+
+
+class hsg_agg(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("column", C.c_int32)]
+
+
+class hsg_op_config(C.Structure):
+    _fields_ = [
+        ("window_kind", C.c_int32),
+        ("emit_mode", C.c_int32),
+        ("size_ms", C.c_int64),
+        ("advance_ms", C.c_int64),
+        ("gap_ms", C.c_int64),
+        ("grace_ms", C.c_int64),
+        ("n_cols", C.c_int32),
+        ("n_aggs", C.c_int32),
+        ("col_types", C.POINTER(C.c_int32)),
+        ("aggs", C.POINTER(hsg_agg)),
+        ("state_capacity", C.c_uint64),
+        ("out_capacity", C.c_uint64),
+    ]
+
+
+class hsg_batch(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint64),
+        ("mem", C.c_int32),
+        ("n_cols", C.c_int32),
+        ("key_id", C.c_void_p),
+        ("ts", C.c_void_p),
+        ("cols", C.POINTER(C.c_void_p)),
+        ("valid", C.POINTER(C.c_void_p)),
+    ]
+
+
+class hsg_rows(C.Structure):
+    _fields_ = [
+        ("capacity", C.c_uint64),
+        ("mem", C.c_int32),
+        ("n_aggs", C.c_int32),
+        ("key_id", C.c_void_p),
+        ("win_start", C.c_void_p),
+        ("win_end", C.c_void_p),
+        ("src_index", C.c_void_p),
+        ("aggs", C.POINTER(C.c_void_p)),
+    ]
+
+
+class hsg_stats(C.Structure):
+    _fields_ = [
+        ("batches", C.c_uint64),
+        ("records", C.c_uint64),
+        ("records_owned", C.c_uint64),
+        ("pairs", C.c_uint64),
+        ("late_dropped", C.c_uint64),
+        ("touched", C.c_uint64),
+        ("state_rows", C.c_uint64),
+        ("pending_rows", C.c_uint64),
+        ("last_batch_ms", C.c_double),
+        ("agg_kernel_ms", C.c_double),
+        ("agg_kernel_launches", C.c_uint64),
+        ("exchange_ms", C.c_double),
+        ("exchange_bytes", C.c_uint64),
+        ("pairs_total", C.c_uint64),
+        ("touched_total", C.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+# Every symbol include/hstream_gpu.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = [
+    "hsg_comm_unique_id",
+    "hsg_engine_create",
+    "hsg_engine_destroy",
+    "hsg_engine_last_error",
+    "hsg_op_create",
+    "hsg_op_destroy",
+    "hsg_op_reset",
+    "hsg_last_error",
+    "hsg_push_batch",
+    "hsg_pending_rows",
+    "hsg_drain",
+    "hsg_state_rows",
+    "hsg_dump_state",
+    "hsg_op_stats",
+]
+
+
+class HStreamGpuError(RuntimeError):
+    """Raised for a negative status; mirrors the reference's HStreamError (Error.hs:11-18)."""
+
+    def __init__(self, status, message=""):
+        self.status = status
+        name = STATUS_NAMES.get(status, str(status))
+        super().__init__(f"{name}: {message}" if message else name)
+
+
+def agg_output_is_f64(kind, col_type):
+    if kind in (HSG_COUNT_ALL, HSG_COUNT):
+        return False
+    if kind == HSG_AVG:
+        return True
+    return col_type == HSG_F64

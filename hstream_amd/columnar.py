@@ -1,0 +1,251 @@
+"""Columnar batch / changelog-row marshalling for the C ABI.
+
+Backend-neutral: ``OpSpec`` describes one windowed GROUP BY operator (what the
+reference builds with timeWindowedBy/sessionWindowedBy + aggregate,
+hstream-sql/src/HStream/SQL/Codegen.hs:479-521) and ``OpHandle`` drives any
+library exporting the hsg_op_* call shapes under some symbol prefix. The
+product binding (hstream_amd.engine) uses it over libhstream_gpu; the test
+oracle binding (oracle/pyoracle.py) uses it over the CPU restatement.
+"""
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+
+
+@dataclass
+class OpSpec:
+    window_kind: int
+    emit_mode: int = abi.HSG_EMIT_PER_BATCH
+    size_ms: int = 0
+    advance_ms: int = 0
+    gap_ms: int = 0
+    grace_ms: int = abi.HSG_DEFAULT_GRACE_MS
+    col_types: Sequence[int] = ()
+    aggs: Sequence[Tuple[int, int]] = ()  # (hsg_agg_kind, column)
+    state_capacity: int = 0
+    out_capacity: int = 0
+
+    def agg_is_f64(self) -> List[bool]:
+        out = []
+        for kind, col in self.aggs:
+            ct = self.col_types[col] if kind not in (abi.HSG_COUNT_ALL,) and 0 <= col < len(self.col_types) else abi.HSG_I64
+            out.append(abi.agg_output_is_f64(kind, ct))
+        return out
+
+    def to_config(self):
+        n_cols = len(self.col_types)
+        col_arr = (C.c_int32 * max(1, n_cols))(*self.col_types)
+        agg_arr = (abi.hsg_agg * max(1, len(self.aggs)))(*[abi.hsg_agg(k, c) for k, c in self.aggs])
+        adv = self.advance_ms if self.window_kind == abi.HSG_HOPPING else self.size_ms
+        cfg = abi.hsg_op_config(
+            window_kind=self.window_kind,
+            emit_mode=self.emit_mode,
+            size_ms=self.size_ms,
+            advance_ms=adv,
+            gap_ms=self.gap_ms,
+            grace_ms=self.grace_ms,
+            n_cols=n_cols,
+            n_aggs=len(self.aggs),
+            col_types=C.cast(col_arr, C.POINTER(C.c_int32)),
+            aggs=C.cast(agg_arr, C.POINTER(abi.hsg_agg)),
+            state_capacity=self.state_capacity,
+            out_capacity=self.out_capacity,
+        )
+        return cfg, (col_arr, agg_arr)
+
+
+def _is_torch(x):
+    return type(x).__module__.startswith("torch")
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if _is_torch(x):
+        return x.data_ptr()
+    return x.ctypes.data
+
+
+def make_batch(key_id, ts, cols=(), valid=None, mem=None):
+    """Build an hsg_batch over numpy arrays (host) or torch tensors (device).
+
+    Returns (hsg_batch, keepalive). Arrays must be contiguous: key_id uint32 /
+    int32, ts int64, cols int64 or float64, valid uint8 (or None = all present).
+    """
+    if mem is None:
+        mem = abi.HSG_MEM_DEVICE if (_is_torch(ts) and ts.is_cuda) else abi.HSG_MEM_HOST
+    keep = [key_id, ts]
+    if not _is_torch(ts):
+        key_id = np.ascontiguousarray(key_id, dtype=np.uint32)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        cols = [np.ascontiguousarray(c) for c in cols]
+        if valid is not None:
+            valid = [None if v is None else np.ascontiguousarray(v, dtype=np.uint8) for v in valid]
+        keep = [key_id, ts, cols, valid]
+    else:
+        keep.append(cols)
+        keep.append(valid)
+    n = int(ts.shape[0])
+    ncols = len(cols)
+    col_ptrs = (C.c_void_p * max(1, ncols))(*[_ptr(c) for c in cols])
+    keep.append(col_ptrs)
+    valid_ptrs = None
+    if valid is not None:
+        valid_ptrs = (C.c_void_p * max(1, ncols))(*[_ptr(v) for v in valid])
+        keep.append(valid_ptrs)
+    b = abi.hsg_batch(
+        n=n,
+        mem=mem,
+        n_cols=ncols,
+        key_id=_ptr(key_id),
+        ts=_ptr(ts),
+        cols=C.cast(col_ptrs, C.POINTER(C.c_void_p)),
+        valid=C.cast(valid_ptrs, C.POINTER(C.c_void_p)) if valid_ptrs is not None else None,
+    )
+    return b, keep
+
+
+@dataclass
+class Rows:
+    """Columnar changelog / state rows (host numpy arrays)."""
+
+    key_id: np.ndarray
+    win_start: np.ndarray
+    win_end: np.ndarray
+    src_index: np.ndarray
+    aggs: List[np.ndarray] = field(default_factory=list)
+
+    def __len__(self):
+        return int(self.key_id.shape[0])
+
+    def sorted(self, by_src=False):
+        """Rows in a canonical order: (src_index, win_start) or (key, win_start, win_end)."""
+        if by_src:
+            order = np.lexsort((self.win_start, self.src_index))
+        else:
+            order = np.lexsort((self.win_end, self.win_start, self.key_id))
+        return Rows(self.key_id[order], self.win_start[order], self.win_end[order],
+                    self.src_index[order], [a[order] for a in self.aggs])
+
+    def tuples(self):
+        out = []
+        for i in range(len(self)):
+            out.append((int(self.key_id[i]), int(self.win_start[i]), int(self.win_end[i]),
+                        tuple(a[i].item() for a in self.aggs)))
+        return out
+
+
+def alloc_rows(n: int, agg_is_f64: Sequence[bool]):
+    n = int(n)
+    arrs = Rows(
+        key_id=np.zeros(n, dtype=np.uint32),
+        win_start=np.zeros(n, dtype=np.int64),
+        win_end=np.zeros(n, dtype=np.int64),
+        src_index=np.zeros(n, dtype=np.int64),
+        aggs=[np.zeros(n, dtype=np.float64 if f else np.int64) for f in agg_is_f64],
+    )
+    agg_ptrs = (C.c_void_p * max(1, len(agg_is_f64)))(*[a.ctypes.data for a in arrs.aggs])
+    rows = abi.hsg_rows(
+        capacity=n,
+        mem=abi.HSG_MEM_HOST,
+        n_aggs=len(agg_is_f64),
+        key_id=arrs.key_id.ctypes.data,
+        win_start=arrs.win_start.ctypes.data,
+        win_end=arrs.win_end.ctypes.data,
+        src_index=arrs.src_index.ctypes.data,
+        aggs=C.cast(agg_ptrs, C.POINTER(C.c_void_p)),
+    )
+    return rows, arrs, agg_ptrs
+
+
+def truncate(rows: Rows, n: int) -> Rows:
+    return Rows(rows.key_id[:n], rows.win_start[:n], rows.win_end[:n], rows.src_index[:n],
+                [a[:n] for a in rows.aggs])
+
+
+class OpHandle:
+    """Drives one operator through a library exposing <prefix>_push_batch etc."""
+
+    def __init__(self, lib, prefix: str, handle, spec: OpSpec):
+        self._lib = lib
+        self._p = prefix
+        self._h = handle
+        self.spec = spec
+        self._f64 = spec.agg_is_f64()
+
+    def _fn(self, name):
+        return getattr(self._lib, f"{self._p}_{name}")
+
+    def _check(self, rc, what):
+        if rc != abi.HSG_OK:
+            msg = self._fn("last_error")(self._h)
+            msg = msg.decode() if msg else ""
+            raise abi.HStreamGpuError(rc, f"{what}: {msg}")
+
+    def push(self, key_id, ts, cols=(), valid=None, watermark=-1, mem=None) -> int:
+        b, keep = make_batch(key_id, ts, cols, valid, mem)
+        wm = C.c_int64(watermark)
+        rc = self._fn("push_batch")(self._h, C.byref(b), C.byref(wm))
+        del keep
+        self._check(rc, "push_batch")
+        return wm.value
+
+    def pending(self) -> int:
+        n = C.c_uint64(0)
+        self._check(self._fn("pending_rows")(self._h, C.byref(n)), "pending_rows")
+        return n.value
+
+    def drain(self) -> Rows:
+        n = self.pending()
+        rows, arrs, keep = alloc_rows(n, self._f64)
+        got = C.c_uint64(0)
+        self._check(self._fn("drain")(self._h, C.byref(rows), C.byref(got)), "drain")
+        return truncate(arrs, got.value)
+
+    def dump_state(self) -> Rows:
+        n = C.c_uint64(0)
+        self._check(self._fn("state_rows")(self._h, C.byref(n)), "state_rows")
+        rows, arrs, keep = alloc_rows(n.value, self._f64)
+        got = C.c_uint64(0)
+        self._check(self._fn("dump_state")(self._h, C.byref(rows), C.byref(got)), "dump_state")
+        return truncate(arrs, got.value)
+
+    def reset(self):
+        self._check(self._fn("op_reset")(self._h), "op_reset")
+
+    def close(self):
+        if self._h:
+            self._fn("op_destroy")(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def declare_op_functions(lib, prefix):
+    """Set ctypes signatures for the <prefix>_op functions shared by both libraries."""
+    vp = C.c_void_p
+    P = C.POINTER
+    getattr(lib, f"{prefix}_op_destroy").argtypes = [vp]
+    getattr(lib, f"{prefix}_op_destroy").restype = None
+    getattr(lib, f"{prefix}_op_reset").argtypes = [vp]
+    getattr(lib, f"{prefix}_op_reset").restype = C.c_int
+    getattr(lib, f"{prefix}_last_error").argtypes = [vp]
+    getattr(lib, f"{prefix}_last_error").restype = C.c_char_p
+    getattr(lib, f"{prefix}_push_batch").argtypes = [vp, P(abi.hsg_batch), P(C.c_int64)]
+    getattr(lib, f"{prefix}_push_batch").restype = C.c_int
+    getattr(lib, f"{prefix}_pending_rows").argtypes = [vp, P(C.c_uint64)]
+    getattr(lib, f"{prefix}_pending_rows").restype = C.c_int
+    getattr(lib, f"{prefix}_drain").argtypes = [vp, P(abi.hsg_rows), P(C.c_uint64)]
+    getattr(lib, f"{prefix}_drain").restype = C.c_int
+    getattr(lib, f"{prefix}_state_rows").argtypes = [vp, P(C.c_uint64)]
+    getattr(lib, f"{prefix}_state_rows").restype = C.c_int
+    getattr(lib, f"{prefix}_dump_state").argtypes = [vp, P(abi.hsg_rows), P(C.c_uint64)]
+    getattr(lib, f"{prefix}_dump_state").restype = C.c_int

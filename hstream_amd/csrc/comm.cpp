@@ -1,0 +1,49 @@
+// RCCL communicator owned by the engine (one per process and GPU).
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <string>
+
+#include "hsg_kernels.h"
+
+namespace hsg {
+
+struct Comm {
+  ncclComm_t comm = nullptr;
+  int rank = 0;
+  int nranks = 1;
+};
+
+static_assert(sizeof(ncclUniqueId) <= HSG_COMM_ID_BYTES, "ncclUniqueId larger than HSG_COMM_ID_BYTES");
+
+int comm_unique_id(uint8_t *out) {
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return HSG_E_COMM;
+  memset(out, 0, HSG_COMM_ID_BYTES);
+  memcpy(out, &id, sizeof(id));
+  return HSG_OK;
+}
+
+int comm_create(const uint8_t *id_bytes, int rank, int nranks, int device, Comm **out, std::string &err) {
+  ncclUniqueId id;
+  memcpy(&id, id_bytes, sizeof(id));
+  Comm *c = new Comm();
+  c->rank = rank;
+  c->nranks = nranks;
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+  if (r != ncclSuccess) {
+    err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+    delete c;
+    return HSG_E_COMM;
+  }
+  *out = c;
+  return HSG_OK;
+}
+
+void comm_destroy(Comm *c) {
+  if (!c) return;
+  if (c->comm) ncclCommDestroy(c->comm);
+  delete c;
+}
+
+}  // namespace hsg

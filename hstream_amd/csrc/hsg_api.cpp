@@ -1,0 +1,410 @@
+// libhstream_gpu host runtime: the C ABI of include/hstream_gpu.h.
+//
+// One hsg_engine per process and GPU (device selection, RCCL communicator);
+// one hsg_op per windowed GROUP BY operator. Each op owns a HIP stream, its
+// HBM state (hash table of (key, window) rows, or the session arena), staging
+// buffers for host batches and an HBM changelog buffer drained by hsg_drain.
+// Every entry point catches everything: no C++ exception crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "hsg_internal.h"
+#include "hsg_ops.h"
+
+using namespace hsg;
+
+// ---------------------------------------------------------------------------
+// error helpers
+// ---------------------------------------------------------------------------
+#define HIP_TRY(obj, expr)                                                         \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess) {                                                        \
+      (obj)->err = std::string(#expr) + ": " + hipGetErrorString(_e);              \
+      return _e == hipErrorOutOfMemory ? HSG_E_OOM : HSG_E_DEVICE;                 \
+    }                                                                              \
+  } while (0)
+
+namespace {
+
+int fail(std::string &err, int code, const std::string &msg) {
+  err = msg;
+  return code;
+}
+
+uint64_t next_pow2(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+double now_ms() {
+  using namespace std::chrono;
+  return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// program (aggregates -> state slots -> output columns)
+// ---------------------------------------------------------------------------
+namespace hsg {
+
+int build_program(const hsg_op_config &cfg, const std::vector<int32_t> &col_types, const std::vector<hsg_agg> &aggs,
+                  Program &prog, std::string &err) {
+  memset(&prog, 0, sizeof(prog));
+  auto find_slot = [&](int op, int col) -> int {
+    for (int s = 0; s < prog.n_slots; ++s)
+      if (prog.slot_op[s] == op && prog.slot_col[s] == col) return s;
+    return -1;
+  };
+  auto add_slot = [&](int op, int col) -> int {
+    int s = find_slot(op, col);
+    if (s >= 0) return s;
+    if (prog.n_slots >= kMaxSlots) return -1;
+    prog.slot_op[prog.n_slots] = op;
+    prog.slot_col[prog.n_slots] = col;
+    return prog.n_slots++;
+  };
+  if ((int)aggs.size() > kMaxAggs) return fail(err, HSG_E_INVALID, "too many aggregates (max 16)");
+  for (size_t j = 0; j < aggs.size(); ++j) {
+    const hsg_agg &g = aggs[j];
+    int a = -1, b = 0, kind = O_I64;
+    bool isf = g.kind != HSG_COUNT_ALL && col_types[g.column] == HSG_F64;
+    int c = g.kind == HSG_COUNT_ALL ? 0 : g.column;
+    switch (g.kind) {
+      case HSG_COUNT_ALL: a = add_slot(S_CNT_ALL, 0); break;
+      case HSG_COUNT: a = add_slot(S_CNT, c); break;
+      case HSG_SUM: a = add_slot(isf ? S_SUM_F : S_SUM_I, c); kind = isf ? O_F64 : O_I64; break;
+      case HSG_MIN: a = add_slot(isf ? S_MIN_F : S_MIN_I, c); kind = isf ? O_F64_ORD : O_I64; break;
+      case HSG_MAX: a = add_slot(isf ? S_MAX_F : S_MAX_I, c); kind = isf ? O_F64_ORD : O_I64; break;
+      case HSG_AVG:
+        a = add_slot(isf ? S_SUM_F : S_SUM_I, c);
+        b = add_slot(S_CNT, c);
+        kind = isf ? O_AVG_F : O_AVG_I;
+        break;
+      case HSG_LAST: {
+        if (cfg.window_kind == HSG_SESSION)
+          return fail(err, HSG_E_INVALID, "HSG_LAST is not supported for session windows");
+        int s = find_slot(S_LAST_SEQ, c);
+        if (s < 0) {
+          if (prog.n_slots + 2 > kMaxSlots) return fail(err, HSG_E_INVALID, "too many state slots");
+          s = add_slot(S_LAST_SEQ, c);
+          prog.slot_op[prog.n_slots] = S_LAST_VAL;
+          prog.slot_col[prog.n_slots] = c;
+          prog.n_slots++;
+        }
+        a = s + 1;
+        kind = isf ? O_F64 : O_I64;
+        break;
+      }
+      default: return fail(err, HSG_E_INVALID, "bad aggregate kind");
+    }
+    if (a < 0 || b < 0) return fail(err, HSG_E_INVALID, "too many state slots");
+    prog.out_kind[j] = kind;
+    prog.out_a[j] = a;
+    prog.out_b[j] = b;
+  }
+  prog.n_out = (int)aggs.size();
+  return HSG_OK;
+}
+
+}  // namespace hsg
+
+// ---------------------------------------------------------------------------
+// engine
+// ---------------------------------------------------------------------------
+struct hsg_engine {
+  int device = 0;
+  int rank = 0;
+  int nranks = 1;
+  uint64_t batch_cap = 0;
+  std::string err;
+  std::mutex mu;  // guards the communicator
+  Comm *comm = nullptr;
+};
+
+extern "C" int hsg_comm_unique_id(uint8_t *out, size_t len) {
+  try {
+    if (!out || len < HSG_COMM_ID_BYTES) return HSG_E_INVALID;
+    return comm_unique_id(out);
+  } catch (...) {
+    return HSG_E_DEVICE;
+  }
+}
+
+extern "C" int hsg_engine_create(const hsg_engine_config *cfg, hsg_engine **out) {
+  try {
+    if (!cfg || !out) return HSG_E_INVALID;
+    *out = nullptr;
+    if (cfg->nranks < 1 || cfg->rank < 0 || cfg->rank >= cfg->nranks) return HSG_E_INVALID;
+    if (cfg->nranks > 1 && !cfg->comm_id) return HSG_E_INVALID;
+    if (cfg->batch_capacity == 0) return HSG_E_INVALID;
+    hsg_engine *e = new (std::nothrow) hsg_engine();
+    if (!e) return HSG_E_OOM;
+    int dev = cfg->device;
+    if (dev < 0) {
+      if (hipGetDevice(&dev) != hipSuccess) { delete e; return HSG_E_DEVICE; }
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || dev >= ndev) { delete e; return HSG_E_DEVICE; }
+    if (hipSetDevice(dev) != hipSuccess) { delete e; return HSG_E_DEVICE; }
+    e->device = dev;
+    e->rank = cfg->rank;
+    e->nranks = cfg->nranks;
+    e->batch_cap = cfg->batch_capacity;
+    if (cfg->nranks > 1 || cfg->comm_id) {
+      int rc = comm_create(cfg->comm_id, cfg->rank, cfg->nranks, dev, &e->comm, e->err);
+      if (rc != HSG_OK) { delete e; return rc; }
+    }
+    *out = e;
+    return HSG_OK;
+  } catch (...) {
+    return HSG_E_DEVICE;
+  }
+}
+
+extern "C" void hsg_engine_destroy(hsg_engine *e) {
+  if (!e) return;
+  try {
+    hipSetDevice(e->device);
+    if (e->comm) comm_destroy(e->comm);
+  } catch (...) {
+  }
+  delete e;
+}
+
+extern "C" const char *hsg_engine_last_error(const hsg_engine *e) { return e ? e->err.c_str() : "null engine"; }
+
+// ---------------------------------------------------------------------------
+// op
+// ---------------------------------------------------------------------------
+struct hsg_op {
+  hsg_engine *eng = nullptr;
+  hsg_op_config cfg;
+  std::vector<int32_t> col_types;
+  std::vector<hsg_agg> aggs;
+  Program prog;
+  OpDevice dev;  // every HBM buffer + stream + events (hsg_ops.h)
+  std::string err;
+  uint64_t pending = 0;
+  uint64_t state_rows = 0;
+  uint32_t batch_id = 0;
+  uint64_t rec_base = 0;
+  hsg_stats stats;
+};
+
+static int validate_config(const hsg_op_config *c, std::string &err) {
+  if (!c) return fail(err, HSG_E_INVALID, "null config");
+  if (c->window_kind < HSG_TUMBLING || c->window_kind > HSG_UNWINDOWED) return fail(err, HSG_E_INVALID, "bad window_kind");
+  if (c->emit_mode < HSG_EMIT_PER_RECORD || c->emit_mode > HSG_EMIT_NONE) return fail(err, HSG_E_INVALID, "bad emit_mode");
+  if (c->window_kind == HSG_TUMBLING || c->window_kind == HSG_HOPPING) {
+    if (c->size_ms <= 0) return fail(err, HSG_E_INVALID, "size_ms must be > 0");
+    if (c->window_kind == HSG_HOPPING && c->advance_ms <= 0) return fail(err, HSG_E_INVALID, "advance_ms must be > 0");
+  }
+  if (c->window_kind == HSG_SESSION && c->gap_ms < 0) return fail(err, HSG_E_INVALID, "gap_ms must be >= 0");
+  if (c->n_aggs <= 0 || !c->aggs) return fail(err, HSG_E_INVALID, "no aggregates");
+  if (c->n_cols < 0 || c->n_cols > kMaxCols || (c->n_cols > 0 && !c->col_types))
+    return fail(err, HSG_E_INVALID, "bad value columns (max 8)");
+  for (int i = 0; i < c->n_cols; ++i)
+    if (c->col_types[i] != HSG_I64 && c->col_types[i] != HSG_F64) return fail(err, HSG_E_INVALID, "bad column type");
+  for (int j = 0; j < c->n_aggs; ++j) {
+    const hsg_agg &g = c->aggs[j];
+    if (g.kind < HSG_COUNT_ALL || g.kind > HSG_LAST) return fail(err, HSG_E_INVALID, "bad aggregate kind");
+    if (g.kind != HSG_COUNT_ALL && (g.column < 0 || g.column >= c->n_cols))
+      return fail(err, HSG_E_INVALID, "aggregate column out of range");
+  }
+  return HSG_OK;
+}
+
+uint64_t hsg_windows_per_record(const hsg_op_config &c) {
+  if (c.window_kind == HSG_HOPPING) return (uint64_t)((c.size_ms + c.advance_ms - 1) / c.advance_ms);
+  return 1;
+}
+
+extern "C" int hsg_op_create(hsg_engine *eng, const hsg_op_config *cfg, hsg_op **out) {
+  try {
+    if (!eng || !out) return HSG_E_INVALID;
+    *out = nullptr;
+    int rc = validate_config(cfg, eng->err);
+    if (rc != HSG_OK) return rc;
+    hsg_op *op = new (std::nothrow) hsg_op();
+    if (!op) return HSG_E_OOM;
+    op->eng = eng;
+    op->cfg = *cfg;
+    op->col_types.assign(cfg->col_types, cfg->col_types + cfg->n_cols);
+    op->aggs.assign(cfg->aggs, cfg->aggs + cfg->n_aggs);
+    op->cfg.col_types = nullptr;
+    op->cfg.aggs = nullptr;
+    if (op->cfg.window_kind == HSG_TUMBLING) op->cfg.advance_ms = op->cfg.size_ms;
+    memset(&op->stats, 0, sizeof(op->stats));
+    rc = build_program(op->cfg, op->col_types, op->aggs, op->prog, eng->err);
+    if (rc != HSG_OK) { delete op; return rc; }
+    if (hipSetDevice(eng->device) != hipSuccess) { delete op; return HSG_E_DEVICE; }
+    rc = op_device_init(op->dev, op->cfg, op->prog, eng->batch_cap, eng->nranks, hsg_windows_per_record(op->cfg),
+                        eng->err);
+    if (rc != HSG_OK) {
+      op_device_free(op->dev);
+      delete op;
+      return rc;
+    }
+    *out = op;
+    return HSG_OK;
+  } catch (const std::bad_alloc &) {
+    return HSG_E_OOM;
+  } catch (...) {
+    return HSG_E_DEVICE;
+  }
+}
+
+extern "C" void hsg_op_destroy(hsg_op *op) {
+  if (!op) return;
+  try {
+    hipSetDevice(op->eng->device);
+    op_device_free(op->dev);
+  } catch (...) {
+  }
+  delete op;
+}
+
+extern "C" const char *hsg_last_error(const hsg_op *op) { return op ? op->err.c_str() : "null op"; }
+
+extern "C" int hsg_op_reset(hsg_op *op) {
+  try {
+    if (!op) return HSG_E_INVALID;
+    HIP_TRY(op, hipSetDevice(op->eng->device));
+    int rc = op_device_reset(op->dev, op->cfg, op->prog, op->err);
+    if (rc != HSG_OK) return rc;
+    op->pending = 0;
+    op->state_rows = 0;
+    op->rec_base = 0;
+    memset(&op->stats, 0, sizeof(op->stats));
+    return HSG_OK;
+  } catch (...) {
+    return HSG_E_DEVICE;
+  }
+}
+
+extern "C" int hsg_push_batch(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark) {
+  try {
+    if (!op) return HSG_E_INVALID;
+    if (!b || !inout_watermark) return fail(op->err, HSG_E_INVALID, "null batch or watermark");
+    if (b->n_cols != op->cfg.n_cols) return fail(op->err, HSG_E_INVALID, "batch n_cols != op n_cols");
+    if (b->mem != HSG_MEM_HOST && b->mem != HSG_MEM_DEVICE) return fail(op->err, HSG_E_INVALID, "bad batch mem");
+    if (b->n > op->eng->batch_cap)
+      return fail(op->err, HSG_E_CAPACITY, "batch larger than the engine's batch_capacity");
+    if (b->n && (!b->key_id || !b->ts)) return fail(op->err, HSG_E_INVALID, "null key_id / ts");
+    for (int c = 0; c < b->n_cols; ++c)
+      if (b->n && (!b->cols || !b->cols[c])) return fail(op->err, HSG_E_INVALID, "null value column");
+    HIP_TRY(op, hipSetDevice(op->eng->device));
+    double t0 = now_ms();
+    PushResult res;
+    PushArgs args;
+    args.batch = b;
+    args.wm_in = *inout_watermark;
+    args.batch_id = ++op->batch_id;
+    args.rec_base = op->rec_base;
+    args.pending = op->pending;
+    args.comm = op->eng->comm;
+    args.rank = op->eng->rank;
+    args.nranks = op->eng->nranks;
+    std::unique_lock<std::mutex> lk(op->eng->mu, std::defer_lock);
+    if (op->eng->comm) lk.lock();
+    int rc = op_push(op->dev, op->cfg, op->prog, args, res, op->err);
+    if (lk.owns_lock()) lk.unlock();
+    if (rc != HSG_OK && rc != HSG_E_RANGE && rc != HSG_E_OOM) return rc;
+    // state was mutated: account for what happened even on OOM / RANGE
+    *inout_watermark = res.wm_out;
+    op->pending += res.out_rows;
+    op->state_rows = res.state_rows;
+    op->rec_base += res.global_records;
+    op->stats.batches += 1;
+    op->stats.records += b->n;
+    op->stats.records_owned += res.owned;
+    op->stats.pairs = res.pairs;
+    op->stats.late_dropped = res.late;
+    op->stats.touched = res.touched;
+    op->stats.pairs_total += res.pairs;
+    op->stats.touched_total += res.touched;
+    op->stats.state_rows = op->state_rows;
+    op->stats.pending_rows = op->pending;
+    op->stats.last_batch_ms = now_ms() - t0;
+    op->stats.agg_kernel_ms += res.agg_ms;
+    op->stats.agg_kernel_launches += res.agg_launches;
+    op->stats.exchange_ms += res.exchange_ms;
+    op->stats.exchange_bytes += res.exchange_bytes;
+    return rc;
+  } catch (const std::bad_alloc &) {
+    return HSG_E_OOM;
+  } catch (...) {
+    if (op) op->err = "unexpected exception";
+    return HSG_E_DEVICE;
+  }
+}
+
+extern "C" int hsg_pending_rows(const hsg_op *op, uint64_t *n) {
+  if (!op || !n) return HSG_E_INVALID;
+  *n = op->pending;
+  return HSG_OK;
+}
+
+static int check_rows(hsg_op *op, const hsg_rows *out) {
+  if (!out) return fail(op->err, HSG_E_INVALID, "null rows");
+  if (out->n_aggs != op->cfg.n_aggs) return fail(op->err, HSG_E_INVALID, "rows n_aggs != op n_aggs");
+  if (out->mem != HSG_MEM_HOST && out->mem != HSG_MEM_DEVICE) return fail(op->err, HSG_E_INVALID, "bad rows mem");
+  return HSG_OK;
+}
+
+extern "C" int hsg_drain(hsg_op *op, hsg_rows *out, uint64_t *n_out) {
+  try {
+    if (!op || !n_out) return HSG_E_INVALID;
+    int rc = check_rows(op, out);
+    if (rc != HSG_OK) return rc;
+    *n_out = op->pending;
+    if (out->capacity < op->pending) return fail(op->err, HSG_E_CAPACITY, "drain: rows capacity < pending rows");
+    HIP_TRY(op, hipSetDevice(op->eng->device));
+    rc = op_copy_rows(op->dev, op->dev.out, 0, op->pending, op->cfg.n_aggs, out, op->err);
+    if (rc != HSG_OK) return rc;
+    op->pending = 0;
+    op->stats.pending_rows = 0;
+    return HSG_OK;
+  } catch (...) {
+    return HSG_E_DEVICE;
+  }
+}
+
+extern "C" int hsg_state_rows(hsg_op *op, uint64_t *n) {
+  if (!op || !n) return HSG_E_INVALID;
+  *n = op->state_rows;
+  return HSG_OK;
+}
+
+extern "C" int hsg_dump_state(hsg_op *op, hsg_rows *out, uint64_t *n_out) {
+  try {
+    if (!op || !n_out) return HSG_E_INVALID;
+    int rc = check_rows(op, out);
+    if (rc != HSG_OK) return rc;
+    *n_out = op->state_rows;
+    if (out->capacity < op->state_rows) return fail(op->err, HSG_E_CAPACITY, "dump: rows capacity < state rows");
+    HIP_TRY(op, hipSetDevice(op->eng->device));
+    uint64_t n = 0;
+    rc = op_dump(op->dev, op->cfg, op->prog, out, &n, op->err);
+    *n_out = n;
+    return rc;
+  } catch (...) {
+    return HSG_E_DEVICE;
+  }
+}
+
+extern "C" int hsg_op_stats(const hsg_op *op, hsg_stats *out) {
+  if (!op || !out) return HSG_E_INVALID;
+  *out = op->stats;
+  return HSG_OK;
+}

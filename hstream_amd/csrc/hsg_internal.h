@@ -1,0 +1,190 @@
+// Internal definitions shared by the host runtime (hsg_api.cpp) and the gfx950
+// kernels (*.hip) of libhstream_gpu. Not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hstream_gpu.h"
+
+namespace hsg {
+
+constexpr int kMaxCols = 8;
+constexpr int kMaxAggs = 16;
+constexpr int kMaxSlots = 24;   // per-group state words (8 B each)
+constexpr uint64_t kEmpty = ~0ull;
+
+// One 8-byte state word per slot; the op of each slot is fixed at op creation.
+enum SlotOp : int32_t {
+  S_CNT_ALL = 0,  // += 1                               (COUNT(*))
+  S_CNT = 1,      // += present(col)                    (COUNT(col), AVG denominator)
+  S_SUM_I = 2,    // += v (wrapping int64)              (SUM / AVG numerator of an i64 column)
+  S_SUM_F = 3,    // += v (f64)                         (SUM / AVG numerator of an f64 column)
+  S_MIN_I = 4,    // min, identity INT64_MAX
+  S_MAX_I = 5,    // max, identity INT64_MIN
+  S_MIN_F = 6,    // min over order-preserving u64 image of the f64, identity img(2^63)
+  S_MAX_F = 7,    // max over order-preserving u64 image, identity img(-2^63)
+  S_LAST_SEQ = 8, // max over (global record seq + 1) of present records
+  S_LAST_VAL = 9, // value of the record named by the LAST_SEQ slot just before it
+};
+
+// Output column j = f(slot a [, slot b]).
+enum OutKind : int32_t {
+  O_I64 = 0,      // slot a as int64
+  O_F64 = 1,      // slot a as f64 bits
+  O_F64_ORD = 2,  // slot a holds the order-preserving image of an f64
+  O_AVG_I = 3,    // (double)slot a (i64 sum) / slot b (count)
+  O_AVG_F = 4,    // slot a (f64 sum) / slot b (count)
+};
+
+struct Program {
+  int32_t n_slots;
+  int32_t n_out;
+  int32_t slot_op[kMaxSlots];
+  int32_t slot_col[kMaxSlots];
+  int32_t out_kind[kMaxAggs];
+  int32_t out_a[kMaxAggs];
+  int32_t out_b[kMaxAggs];
+};
+
+// u64 division by an invariant divisor (Granlund–Montgomery), exact for all n.
+struct Divider {
+  uint64_t d;
+  uint64_t m;
+  int32_t sh1;
+  int32_t sh2;
+};
+
+__host__ __device__ inline uint64_t umulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(a, b);
+#else
+  return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+__host__ __device__ inline uint64_t udiv(const Divider &v, uint64_t n) {
+  uint64_t t = umulhi64(v.m, n);
+  return (t + ((n - t) >> v.sh1)) >> v.sh2;
+}
+
+inline Divider make_divider(uint64_t d) {
+  Divider v;
+  v.d = d;
+  int l = 0;
+  while (l < 64 && (1ull << l) < d) ++l;  // l = ceil(log2 d)
+  unsigned __int128 two_l = (unsigned __int128)1 << l;
+  unsigned __int128 m = (((unsigned __int128)1 << 64) * (two_l - d)) / d + 1;
+  v.m = (uint64_t)m;
+  v.sh1 = l < 1 ? l : 1;
+  v.sh2 = l - 1 > 0 ? l - 1 : 0;
+  return v;
+}
+
+// Device-side per-op scalars (one 256-byte block, zeroed / set per batch).
+struct DevScalars {
+  int64_t wm_out;        // watermark after the batch
+  int64_t k_epoch;       // window index represented by k_rel = 0
+  uint32_t epoch_set;
+  uint32_t err;          // bit0 OOM, bit1 RANGE
+  uint64_t pairs;        // accepted (record, window) updates
+  uint64_t late;         // rejected by grace
+  uint64_t out_rows;     // rows appended to the changelog this batch
+  uint64_t touched;
+  uint64_t live;         // dump: rows found
+  uint64_t min_ts_valid; // reserved
+  uint64_t scratch[23];
+};
+static_assert(sizeof(DevScalars) == 256, "DevScalars layout");
+
+constexpr uint32_t ERR_OOM = 1u;
+constexpr uint32_t ERR_RANGE = 2u;
+
+// Changelog / dump rows in HBM, columnar.
+struct OutCols {
+  uint32_t *key;
+  int64_t *ws;
+  int64_t *we;
+  int64_t *src;
+  int64_t *agg[kMaxAggs];  // 8-byte words (i64 or f64 bits)
+};
+
+struct Batch {
+  uint64_t n;
+  const uint32_t *key;
+  const int64_t *ts;
+  const int64_t *col[kMaxCols];  // i64 or f64 bits
+  const uint8_t *valid[kMaxCols];
+};
+
+// Time-window (tumbling / hopping / unwindowed) hash state in HBM.
+struct TwTable {
+  uint64_t *keys;   // [cap] group key = key_id << 32 | (k - k_epoch); kEmpty = free
+  int64_t *aggs;    // [cap][n_slots]
+  uint32_t *stamp;  // [cap] id of the last batch that touched the group
+  uint64_t mask;    // cap - 1
+};
+
+struct TwParams {
+  int32_t kind;     // hsg_window_kind
+  int32_t batch_id;
+  int64_t size;
+  int64_t adv;
+  int64_t grace;
+  int64_t wm_in;
+  uint64_t rec_base; // global seq of record 0 of this batch
+  Divider div;
+};
+
+__device__ __host__ inline uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+// Order-preserving map f64 -> u64 (total order on non-NaN values).
+__device__ __host__ inline uint64_t f64_ord(double d) {
+  uint64_t u = __builtin_bit_cast(uint64_t, d);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __host__ inline double f64_unord(uint64_t o) {
+  uint64_t u = (o & 0x8000000000000000ull) ? (o & 0x7fffffffffffffffull) : ~o;
+  return __builtin_bit_cast(double, u);
+}
+
+inline int64_t slot_identity(int32_t op) {
+  switch (op) {
+    case S_MIN_I: return INT64_MAX;
+    case S_MAX_I: return INT64_MIN;
+    case S_MIN_F: return (int64_t)f64_ord((double)INT64_MAX);
+    case S_MAX_F: return (int64_t)f64_ord((double)INT64_MIN);
+    default: return 0;
+  }
+}
+
+// ---- kernel launchers (defined in the .hip files) --------------------------
+void launch_fill_u64(hipStream_t s, uint64_t *p, uint64_t n, uint64_t v);
+void launch_fill_rows(hipStream_t s, int64_t *aggs, uint64_t rows, const Program &prog);
+void launch_fill_u32(hipStream_t s, uint32_t *p, uint64_t n, uint32_t v);
+
+// stream time: tile maxima -> exclusive tile prefix (+ epoch init)
+void launch_tile_stats(hipStream_t s, const Batch &b, int64_t *tile_max, int64_t *tile_min, uint64_t n_tiles);
+void launch_tile_scan(hipStream_t s, const int64_t *tile_max, const int64_t *tile_min, int64_t *tile_prefix,
+                      uint64_t n_tiles, int64_t wm_in, int64_t adv, bool set_epoch, DevScalars *sc);
+
+// time windows, atomic hash aggregation (per-batch / none modes)
+void launch_tw_agg(hipStream_t s, const Batch &b, const TwParams &p, const TwTable &t, const Program &prog,
+                   const int64_t *tile_prefix, DevScalars *sc);
+// scan the table: emit rows whose stamp == batch_id (mode 0) or every live row (mode 1)
+void launch_tw_scan_emit(hipStream_t s, const TwTable &t, uint64_t cap, const Program &prog, const TwParams &p,
+                         const Batch &b, int mode, OutCols out, uint64_t out_base, uint64_t out_cap,
+                         DevScalars *sc, uint64_t *counter);
+
+constexpr int kTileThreads = 256;
+constexpr int kRecPerThread = 4;
+constexpr int kTileRecords = kTileThreads * kRecPerThread;
+
+}  // namespace hsg

@@ -1,0 +1,108 @@
+// Device-side operator state and the host orchestration entry points used by
+// hsg_api.cpp. Not part of the ABI.
+#pragma once
+
+#include <string>
+
+#include "hsg_internal.h"
+
+namespace hsg {
+
+struct Comm;  // RCCL communicator wrapper (comm.cpp)
+
+int comm_unique_id(uint8_t *out);
+int comm_create(const uint8_t *id, int rank, int nranks, int device, Comm **out, std::string &err);
+void comm_destroy(Comm *c);
+
+// Session store in HBM (k_session.hip): per-key session lists in an arena.
+struct SessTable {
+  uint32_t *keys;      // [cap] key id, kEmpty32 = free
+  uint64_t *list_off;  // [cap] arena offset (in sessions) of the key's list
+  uint32_t *list_len;  // [cap]
+  uint32_t *list_cap;  // [cap]
+  uint64_t mask;
+  // arena, structure of arrays: start, end, stamp and n_slots agg words per session
+  int64_t *a_start;
+  int64_t *a_end;
+  uint32_t *a_stamp;
+  int64_t *a_aggs;     // [arena_cap][n_slots]
+  uint64_t arena_cap;
+};
+
+struct OpDevice {
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr, ev_d = nullptr;
+  DevScalars *sc = nullptr;     // device
+  DevScalars *h_sc = nullptr;   // pinned host mirror
+  uint64_t batch_cap = 0;       // records this op can take in one push (after exchange)
+  uint64_t wpr = 1;             // max windows per record
+  uint64_t n_tiles_cap = 0;
+  int64_t *tile_max = nullptr, *tile_min = nullptr, *tile_prefix = nullptr;
+  // staging (host batches, exchange receive side)
+  uint32_t *st_key = nullptr;
+  int64_t *st_ts = nullptr;
+  int64_t *st_col[kMaxCols] = {};
+  uint8_t *st_valid[kMaxCols] = {};
+  int64_t *st_seq = nullptr;    // global record seq of received records (multi-GPU)
+  int64_t *st_wm = nullptr;     // per-record watermark of received records (multi-GPU)
+  // time windows
+  TwTable tw = {};
+  uint64_t cap = 0;             // table slots
+  // sessions
+  SessTable ss = {};
+  uint64_t *arena_top = nullptr;  // device bump pointer
+  // changelog buffer
+  OutCols out = {};
+  uint64_t out_cap = 0;
+  // per-record / session scratch (sort + scan)
+  void *scratch = nullptr;
+  uint64_t scratch_bytes = 0;
+  // exchange buffers (multi-GPU)
+  void *xsend = nullptr;
+  void *xrecv = nullptr;
+  uint64_t xbytes = 0;
+  uint64_t *h_counts = nullptr;   // pinned [2 * nranks]
+  uint64_t *d_counts = nullptr;
+  int nranks = 1;
+  int n_cols = 0;
+  int32_t col_types[kMaxCols] = {};
+};
+
+struct PushArgs {
+  const hsg_batch *batch = nullptr;
+  int64_t wm_in = -1;
+  uint32_t batch_id = 0;
+  uint64_t rec_base = 0;  // global seq of this batch's first record (all ranks)
+  uint64_t pending = 0;
+  Comm *comm = nullptr;
+  int rank = 0;
+  int nranks = 1;
+};
+
+struct PushResult {
+  int64_t wm_out = -1;
+  uint64_t out_rows = 0;
+  uint64_t pairs = 0;
+  uint64_t late = 0;
+  uint64_t touched = 0;
+  uint64_t state_rows = 0;
+  uint64_t owned = 0;           // records aggregated here after the exchange
+  uint64_t global_records = 0;  // records in this batch over all ranks
+  double agg_ms = 0;
+  uint64_t agg_launches = 0;
+  double exchange_ms = 0;
+  uint64_t exchange_bytes = 0;
+};
+
+int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t batch_cap, int nranks,
+                   uint64_t wpr, std::string &err);
+void op_device_free(OpDevice &d);
+int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err);
+int op_push(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, PushResult &r,
+            std::string &err);
+int op_copy_rows(OpDevice &d, const OutCols &src, uint64_t from, uint64_t n, int n_aggs, const hsg_rows *out,
+                 std::string &err);
+int op_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hsg_rows *out, uint64_t *n_out,
+            std::string &err);
+
+}  // namespace hsg

@@ -1,0 +1,435 @@
+// gfx950 kernels for tumbling / hopping / unwindowed GROUP BY (per-batch and
+// state-only modes): stream-time scan, window assignment fused with the HBM
+// open-addressing (key, window) hash aggregation, and the touched-row emit /
+// dump scans.
+//
+// Semantics follow the reference's per-record processor, restated for a batch:
+//   windowsFor      hstream-processing/.../Stream/TimeWindowedStream.hs:105-117
+//   grace check     TimeWindowedStream.hs:88-92 with stream time Processor.hs:139
+//   state update    TimeWindowedStream.hs:93-100 (ksGet / aggF / ksPut)
+//   SQL aggregates  hstream-sql/src/HStream/SQL/Codegen.hs:399-469
+// The aggregates used here (COUNT/SUM/MIN/MAX and LAST by record order) are
+// commutative per group, so applying a batch's updates in any order gives the
+// reference's final state; the exact per-record changelog is produced by the
+// sort-based path in k_perrecord.hip.
+#include "hsg_internal.h"
+
+namespace hsg {
+
+// ---------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------
+__device__ inline int64_t wave_max_i64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    int64_t u = __shfl_xor(v, o, 64);
+    v = u > v ? u : v;
+  }
+  return v;
+}
+__device__ inline int64_t wave_min_i64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    int64_t u = __shfl_xor(v, o, 64);
+    v = u < v ? u : v;
+  }
+  return v;
+}
+__device__ inline uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// inclusive max-scan across the 64 lanes of a wave
+__device__ inline int64_t wave_incl_max(int64_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int64_t u = __shfl_up(v, o, 64);
+    if (lane >= o) v = u > v ? u : v;
+  }
+  return v;
+}
+__device__ inline uint64_t wave_incl_sum(uint64_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint64_t u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+__device__ inline int64_t slot_identity_dev(int32_t op) {
+  switch (op) {
+    case S_MIN_I: return INT64_MAX;
+    case S_MAX_I: return INT64_MIN;
+    case S_MIN_F: return (int64_t)f64_ord(9223372036854775807.0);
+    case S_MAX_F: return (int64_t)f64_ord(-9223372036854775808.0);
+    default: return 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fills
+// ---------------------------------------------------------------------------
+__global__ void k_fill_u64(uint64_t *__restrict__ p, uint64_t n, uint64_t v) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+__global__ void k_fill_u32(uint32_t *__restrict__ p, uint64_t n, uint32_t v) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+__global__ void k_fill_rows(int64_t *__restrict__ aggs, uint64_t rows, Program prog) {
+  const uint64_t total = rows * (uint64_t)prog.n_slots;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x)
+    aggs[i] = slot_identity_dev(prog.slot_op[i % prog.n_slots]);
+}
+
+static unsigned grid_for(uint64_t n, unsigned tpb) {
+  uint64_t g = (n + tpb - 1) / tpb;
+  if (g > 4096) g = 4096;
+  if (g == 0) g = 1;
+  return (unsigned)g;
+}
+
+void launch_fill_u64(hipStream_t s, uint64_t *p, uint64_t n, uint64_t v) {
+  if (n) hipLaunchKernelGGL(k_fill_u64, dim3(grid_for(n, 256)), dim3(256), 0, s, p, n, v);
+}
+void launch_fill_u32(hipStream_t s, uint32_t *p, uint64_t n, uint32_t v) {
+  if (n) hipLaunchKernelGGL(k_fill_u32, dim3(grid_for(n, 256)), dim3(256), 0, s, p, n, v);
+}
+void launch_fill_rows(hipStream_t s, int64_t *aggs, uint64_t rows, const Program &prog) {
+  if (rows && prog.n_slots)
+    hipLaunchKernelGGL(k_fill_rows, dim3(grid_for(rows * prog.n_slots, 256)), dim3(256), 0, s, aggs, rows, prog);
+}
+
+// ---------------------------------------------------------------------------
+// stream time (Processor.hs:139): per-tile max of every record's ts, then an
+// exclusive prefix max over tiles seeded with the incoming watermark.
+// Tile t covers records [t*kTileRecords, (t+1)*kTileRecords), record
+// (r, thread) = t*kTileRecords + r*kTileThreads + thread.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kTileThreads) void k_tile_stats(Batch b, int64_t *__restrict__ tmax,
+                                                             int64_t *__restrict__ tmin) {
+  __shared__ int64_t smax[kTileThreads / 64], smin[kTileThreads / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kTileRecords;
+  int64_t mx = INT64_MIN, mn = INT64_MAX;
+#pragma unroll
+  for (int r = 0; r < kRecPerThread; ++r) {
+    uint64_t i = base + (uint64_t)r * kTileThreads + threadIdx.x;
+    if (i < b.n) {
+      int64_t t = b.ts[i];
+      mx = t > mx ? t : mx;
+      if (b.key[i] != HSG_KEY_NONE && t >= 0) mn = t < mn ? t : mn;
+    }
+  }
+  mx = wave_max_i64(mx);
+  mn = wave_min_i64(mn);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { smax[w] = mx; smin[w] = mn; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < kTileThreads / 64; ++k) {
+      mx = smax[k] > mx ? smax[k] : mx;
+      mn = smin[k] < mn ? smin[k] : mn;
+    }
+    tmax[blockIdx.x] = mx;
+    tmin[blockIdx.x] = mn;
+  }
+}
+
+// One workgroup: tile_prefix[t] = max(wm_in, tile_max[0..t-1]); sc->wm_out; epoch.
+__global__ __launch_bounds__(1024) void k_tile_scan(const int64_t *__restrict__ tmax, const int64_t *__restrict__ tmin,
+                                                    int64_t *__restrict__ tprefix, uint64_t n_tiles, int64_t wm_in,
+                                                    int64_t adv, int set_epoch, DevScalars *sc) {
+  __shared__ int64_t swave[16];
+  __shared__ int64_t swmin[16];
+  const uint64_t per = (n_tiles + 1023) / 1024;
+  const uint64_t lo = threadIdx.x * per;
+  const uint64_t hi = lo + per < n_tiles ? lo + per : n_tiles;
+  int64_t local = INT64_MIN, lmin = INT64_MAX;
+  for (uint64_t t = lo; t < hi; ++t) {
+    local = tmax[t] > local ? tmax[t] : local;
+    lmin = tmin[t] < lmin ? tmin[t] : lmin;
+  }
+  // exclusive scan of thread totals across the block
+  int64_t incl = wave_incl_max(local);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 63) swave[w] = incl;
+  int64_t wmn = wave_min_i64(lmin);
+  if (lane == 0) swmin[w] = wmn;
+  __syncthreads();
+  int64_t before = wm_in;
+  for (int k = 0; k < w; ++k) before = swave[k] > before ? swave[k] : before;
+  int64_t excl = __shfl_up(incl, 1, 64);
+  if (lane > 0) before = excl > before ? excl : before;
+  int64_t run = before;
+  for (uint64_t t = lo; t < hi; ++t) {
+    tprefix[t] = run;
+    run = tmax[t] > run ? tmax[t] : run;
+  }
+  if (threadIdx.x == 0) {
+    int64_t all = wm_in, amin = INT64_MAX;
+    for (int k = 0; k < 16; ++k) {
+      all = swave[k] > all ? swave[k] : all;
+      amin = swmin[k] < amin ? swmin[k] : amin;
+    }
+    sc->wm_out = all;
+    if (set_epoch && !sc->epoch_set && amin != INT64_MAX) {
+      int64_t k0 = amin / adv - (int64_t)(1ll << 31);
+      sc->k_epoch = k0 > 0 ? k0 : 0;
+      sc->epoch_set = 1;
+    }
+  }
+}
+
+void launch_tile_stats(hipStream_t s, const Batch &b, int64_t *tile_max, int64_t *tile_min, uint64_t n_tiles) {
+  if (n_tiles) hipLaunchKernelGGL(k_tile_stats, dim3((unsigned)n_tiles), dim3(kTileThreads), 0, s, b, tile_max, tile_min);
+}
+void launch_tile_scan(hipStream_t s, const int64_t *tile_max, const int64_t *tile_min, int64_t *tile_prefix,
+                      uint64_t n_tiles, int64_t wm_in, int64_t adv, bool set_epoch, DevScalars *sc) {
+  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, tile_max, tile_min, tile_prefix, n_tiles, wm_in, adv,
+                     set_epoch ? 1 : 0, sc);
+}
+
+// ---------------------------------------------------------------------------
+// the hash table
+// ---------------------------------------------------------------------------
+// Returns the slot of group g, inserting it if absent; -1 when the table is full.
+// A plain load is only a hint (a stale EMPTY costs one failed CAS); the CAS
+// result is authoritative, and a slot moves EMPTY -> g at most once.
+__device__ inline int64_t tw_find_or_insert(const TwTable &t, uint64_t g, uint32_t &fresh) {
+  uint64_t s = mix64(g) & t.mask;
+  for (uint64_t probe = 0; probe <= t.mask; ++probe) {
+    uint64_t cur = t.keys[s];
+    if (cur == g) return (int64_t)s;
+    if (cur == kEmpty) {
+      uint64_t old = atomicCAS((unsigned long long *)&t.keys[s], (unsigned long long)kEmpty, (unsigned long long)g);
+      if (old == kEmpty) { fresh += 1; return (int64_t)s; }
+      if (old == g) return (int64_t)s;
+    }
+    s = (s + 1) & t.mask;
+  }
+  return -1;
+}
+
+__device__ inline bool rec_present(const Batch &b, int c, uint64_t i) {
+  return b.valid[c] == nullptr || b.valid[c][i] != 0;
+}
+
+__device__ inline void apply_slots(const Program &prog, int64_t *__restrict__ row, const Batch &b, uint64_t i,
+                                   uint64_t seq1) {
+  for (int s = 0; s < prog.n_slots; ++s) {
+    const int op = prog.slot_op[s];
+    const int c = prog.slot_col[s];
+    unsigned long long *u = (unsigned long long *)(row + s);
+    switch (op) {
+      case S_CNT_ALL: atomicAdd(u, 1ull); break;
+      case S_CNT: if (rec_present(b, c, i)) atomicAdd(u, 1ull); break;
+      case S_SUM_I: if (rec_present(b, c, i)) atomicAdd(u, (unsigned long long)b.col[c][i]); break;
+      case S_SUM_F:
+        if (rec_present(b, c, i)) unsafeAtomicAdd((double *)(row + s), __builtin_bit_cast(double, b.col[c][i]));
+        break;
+      case S_MIN_I: if (rec_present(b, c, i)) atomicMin((long long *)(row + s), (long long)b.col[c][i]); break;
+      case S_MAX_I: if (rec_present(b, c, i)) atomicMax((long long *)(row + s), (long long)b.col[c][i]); break;
+      case S_MIN_F:
+        if (rec_present(b, c, i)) atomicMin(u, (unsigned long long)f64_ord(__builtin_bit_cast(double, b.col[c][i])));
+        break;
+      case S_MAX_F:
+        if (rec_present(b, c, i)) atomicMax(u, (unsigned long long)f64_ord(__builtin_bit_cast(double, b.col[c][i])));
+        break;
+      case S_LAST_SEQ: if (rec_present(b, c, i)) atomicMax(u, (unsigned long long)seq1); break;
+      default: break;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// window assignment + hash aggregation, one tile of kTileRecords per workgroup
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kTileThreads) void k_tw_agg(Batch b, TwParams p, TwTable t, Program prog,
+                                                         const int64_t *__restrict__ tprefix, DevScalars *sc) {
+  __shared__ int64_t swave[kTileThreads / 64];
+  __shared__ uint64_t sred[3][kTileThreads / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kTileRecords;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t k_epoch = sc->k_epoch;
+
+  // 1) stream time per record: inclusive prefix max in arrival order
+  uint32_t key[kRecPerThread];
+  int64_t ts[kRecPerThread], wm[kRecPerThread];
+  int64_t carry = tprefix[blockIdx.x];
+#pragma unroll
+  for (int r = 0; r < kRecPerThread; ++r) {
+    uint64_t i = base + (uint64_t)r * kTileThreads + threadIdx.x;
+    bool in = i < b.n;
+    key[r] = in ? b.key[i] : HSG_KEY_NONE;
+    ts[r] = in ? b.ts[i] : INT64_MIN;
+  }
+#pragma unroll
+  for (int r = 0; r < kRecPerThread; ++r) {
+    int64_t incl = wave_incl_max(ts[r]);
+    if (lane == 63) swave[w] = incl;
+    __syncthreads();
+    int64_t before = carry;
+    for (int k = 0; k < w; ++k) before = swave[k] > before ? swave[k] : before;
+    wm[r] = incl > before ? incl : before;
+    int64_t tot = carry;
+    for (int k = 0; k < kTileThreads / 64; ++k) tot = swave[k] > tot ? swave[k] : tot;
+    carry = tot;
+    __syncthreads();
+  }
+
+  // 2) windows + hash aggregation
+  uint64_t pairs = 0, late = 0;
+  uint32_t fresh = 0, err = 0;
+  const bool unwin = p.kind == HSG_UNWINDOWED;
+#pragma unroll 1
+  for (int r = 0; r < kRecPerThread; ++r) {
+    if (key[r] == HSG_KEY_NONE) continue;
+    const uint64_t i = base + (uint64_t)r * kTileThreads + threadIdx.x;
+    uint64_t k_lo, k_hi;
+    if (unwin) {
+      k_lo = 0; k_hi = 0;
+    } else {
+      if (ts[r] < 0) continue;  // windowsFor yields no window for ts < 0
+      int64_t t0 = (int64_t)((uint64_t)ts[r] - (uint64_t)p.size + (uint64_t)p.adv);
+      if (t0 < 0) t0 = 0;
+      k_lo = udiv(p.div, (uint64_t)t0);
+      k_hi = udiv(p.div, (uint64_t)ts[r]);
+    }
+    for (uint64_t k = k_lo; k <= k_hi; ++k) {
+      if (!unwin) {
+        int64_t ws = (int64_t)(k * (uint64_t)p.adv);
+        int64_t we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
+        if (!(wm[r] < (int64_t)((uint64_t)we + (uint64_t)p.grace))) { late += 1; continue; }
+      }
+      int64_t krel = (int64_t)k - k_epoch;
+      if (krel < 0 || krel > 0xFFFFFFFFll) { err |= ERR_RANGE; continue; }
+      uint64_t g = ((uint64_t)key[r] << 32) | (uint64_t)krel;
+      int64_t slot = tw_find_or_insert(t, g, fresh);
+      if (slot < 0) { err |= ERR_OOM; continue; }
+      apply_slots(prog, t.aggs + (uint64_t)slot * prog.n_slots, b, i, p.rec_base + i + 1);
+      t.stamp[slot] = (uint32_t)p.batch_id;
+      pairs += 1;
+    }
+  }
+
+  // 3) per-workgroup counters
+  pairs = wave_sum_u64(pairs);
+  late = wave_sum_u64(late);
+  uint64_t fr = wave_sum_u64(fresh);
+  uint64_t anyerr = __ballot(err != 0);
+  if (lane == 0) { sred[0][w] = pairs; sred[1][w] = late; sred[2][w] = fr; }
+  if (anyerr && err) atomicOr(&sc->err, err);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t a = 0, l = 0, f = 0;
+    for (int k = 0; k < kTileThreads / 64; ++k) { a += sred[0][k]; l += sred[1][k]; f += sred[2][k]; }
+    if (a) atomicAdd((unsigned long long *)&sc->pairs, (unsigned long long)a);
+    if (l) atomicAdd((unsigned long long *)&sc->late, (unsigned long long)l);
+    if (f) atomicAdd((unsigned long long *)&sc->live, (unsigned long long)f);
+  }
+}
+
+void launch_tw_agg(hipStream_t s, const Batch &b, const TwParams &p, const TwTable &t, const Program &prog,
+                   const int64_t *tile_prefix, DevScalars *sc) {
+  uint64_t tiles = (b.n + kTileRecords - 1) / kTileRecords;
+  if (tiles) hipLaunchKernelGGL(k_tw_agg, dim3((unsigned)tiles), dim3(kTileThreads), 0, s, b, p, t, prog, tile_prefix, sc);
+}
+
+// ---------------------------------------------------------------------------
+// row emission: mode 0 = groups touched by this batch (per-batch changelog and
+// LAST fix-up), mode 1 = every live group (ksDump), mode 2 = LAST fix-up only
+// ---------------------------------------------------------------------------
+__device__ inline int64_t out_value(const Program &prog, int j, const int64_t *row) {
+  const int64_t a = row[prog.out_a[j]];
+  switch (prog.out_kind[j]) {
+    case O_F64_ORD: return __builtin_bit_cast(int64_t, f64_unord((uint64_t)a));
+    case O_AVG_I: {
+      int64_t c = row[prog.out_b[j]];
+      double d = c ? (double)a / (double)c : __builtin_nan("");
+      return __builtin_bit_cast(int64_t, d);
+    }
+    case O_AVG_F: {
+      int64_t c = row[prog.out_b[j]];
+      double d = c ? __builtin_bit_cast(double, a) / (double)c : __builtin_nan("");
+      return __builtin_bit_cast(int64_t, d);
+    }
+    default: return a;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_tw_scan_emit(TwTable t, uint64_t cap, Program prog, TwParams p, Batch b,
+                                                      int mode, OutCols out, uint64_t out_base, uint64_t out_cap,
+                                                      DevScalars *sc, uint64_t *counter) {
+  __shared__ uint64_t swave[4];
+  __shared__ uint64_t sbase;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t k_epoch = sc->k_epoch;
+  const bool unwin = p.kind == HSG_UNWINDOWED;
+  for (uint64_t blk = blockIdx.x * 256ull; blk < cap; blk += (uint64_t)gridDim.x * 256ull) {
+    const uint64_t s = blk + threadIdx.x;
+    bool hit = false;
+    uint64_t g = kEmpty;
+    if (s < cap) {
+      g = t.keys[s];
+      if (mode == 1) hit = g != kEmpty;
+      else hit = g != kEmpty && t.stamp[s] == (uint32_t)p.batch_id;
+    }
+    int64_t *row = t.aggs + s * (uint64_t)prog.n_slots;
+    if (hit && mode != 1) {
+      // LAST fix-up: the record that won LAST_SEQ belongs to this batch
+      for (int q = 0; q < prog.n_slots; ++q) {
+        if (prog.slot_op[q] != S_LAST_SEQ) continue;
+        uint64_t seq1 = (uint64_t)row[q];
+        if (seq1 > p.rec_base && seq1 - 1 - p.rec_base < b.n)
+          row[q + 1] = b.col[prog.slot_col[q]][seq1 - 1 - p.rec_base];
+      }
+    }
+    if (mode == 2) continue;
+    uint64_t f = hit ? 1 : 0;
+    uint64_t incl = wave_incl_sum(f);
+    if (lane == 63) swave[w] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t tot = swave[0] + swave[1] + swave[2] + swave[3];
+      sbase = tot ? atomicAdd((unsigned long long *)counter, (unsigned long long)tot) : 0;
+    }
+    __syncthreads();
+    uint64_t off = sbase + incl - f;
+    for (int k = 0; k < w; ++k) off += swave[k];
+    if (hit) {
+      uint64_t o = out_base + off;
+      if (o < out_cap) {
+        out.key[o] = (uint32_t)(g >> 32);
+        int64_t ws = 0, we = 0;
+        if (!unwin) {
+          int64_t k = k_epoch + (int64_t)(g & 0xFFFFFFFFull);
+          ws = (int64_t)((uint64_t)k * (uint64_t)p.adv);
+          we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
+        }
+        out.ws[o] = ws;
+        out.we[o] = we;
+        out.src[o] = -1;
+        for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, row);
+      } else {
+        atomicOr(&sc->err, ERR_OOM);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+void launch_tw_scan_emit(hipStream_t s, const TwTable &t, uint64_t cap, const Program &prog, const TwParams &p,
+                         const Batch &b, int mode, OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc,
+                         uint64_t *counter) {
+  uint64_t blocks = (cap + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_tw_scan_emit, dim3((unsigned)blocks), dim3(256), 0, s, t, cap, prog, p, b, mode, out, out_base,
+                     out_cap, sc, counter);
+}
+
+}  // namespace hsg

@@ -1,0 +1,397 @@
+// Host orchestration of one operator's batch on its HIP stream: staging, the
+// stream-time scan, the aggregation kernels, changelog bookkeeping, dumps.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+
+#include "hsg_internal.h"
+#include "hsg_ops.h"
+#include "hsg_kernels.h"
+
+namespace hsg {
+
+#define DTRY(expr)                                                          \
+  do {                                                                      \
+    hipError_t _e = (expr);                                                 \
+    if (_e != hipSuccess) {                                                 \
+      err = std::string(#expr) + ": " + hipGetErrorString(_e);              \
+      return _e == hipErrorOutOfMemory ? HSG_E_OOM : HSG_E_DEVICE;          \
+    }                                                                       \
+  } while (0)
+
+static uint64_t next_pow2(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+template <typename T>
+static hipError_t dalloc(T **p, uint64_t count) {
+  if (count == 0) count = 1;
+  return hipMalloc((void **)p, count * sizeof(T));
+}
+
+template <typename T>
+static void dfree(T *&p) {
+  if (p) hipFree((void *)p);
+  p = nullptr;
+}
+
+static bool has_last(const Program &prog) {
+  for (int s = 0; s < prog.n_slots; ++s)
+    if (prog.slot_op[s] == S_LAST_SEQ) return true;
+  return false;
+}
+
+static int alloc_out(OutCols &o, uint64_t cap, int n_aggs, std::string &err) {
+  DTRY(dalloc(&o.key, cap));
+  DTRY(dalloc(&o.ws, cap));
+  DTRY(dalloc(&o.we, cap));
+  DTRY(dalloc(&o.src, cap));
+  for (int j = 0; j < n_aggs; ++j) DTRY(dalloc(&o.agg[j], cap));
+  return HSG_OK;
+}
+
+static void free_out(OutCols &o) {
+  dfree(o.key);
+  dfree(o.ws);
+  dfree(o.we);
+  dfree(o.src);
+  for (int j = 0; j < kMaxAggs; ++j) dfree(o.agg[j]);
+}
+
+int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err) {
+  DTRY(hipMemsetAsync(d.sc, 0, sizeof(DevScalars), d.stream));
+  if (cfg.window_kind == HSG_SESSION) {
+    launch_fill_u32(d.stream, d.ss.keys, d.cap, 0xFFFFFFFFu);
+    DTRY(hipMemsetAsync(d.arena_top, 0, sizeof(uint64_t), d.stream));
+  } else {
+    launch_fill_u64(d.stream, d.tw.keys, d.cap, kEmpty);
+    launch_fill_rows(d.stream, d.tw.aggs, d.cap, prog);
+    DTRY(hipMemsetAsync(d.tw.stamp, 0, d.cap * sizeof(uint32_t), d.stream));
+    if (cfg.window_kind == HSG_UNWINDOWED) {
+      // one implicit window: k = 0, epoch fixed at 0
+      DevScalars init;
+      memset(&init, 0, sizeof(init));
+      init.epoch_set = 1;
+      memcpy(d.h_sc, &init, sizeof(init));
+      DTRY(hipMemcpyAsync(d.sc, d.h_sc, sizeof(DevScalars), hipMemcpyHostToDevice, d.stream));
+    }
+  }
+  DTRY(hipGetLastError());
+  DTRY(hipStreamSynchronize(d.stream));
+  return HSG_OK;
+}
+
+int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t batch_cap, int nranks,
+                   uint64_t wpr, std::string &err) {
+  d.nranks = nranks;
+  d.n_cols = cfg.n_cols;
+  d.wpr = wpr;
+  // after a key exchange a rank can receive up to nranks * batch_cap records
+  d.batch_cap = batch_cap * (uint64_t)nranks;
+  DTRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  DTRY(hipEventCreate(&d.ev_a));
+  DTRY(hipEventCreate(&d.ev_b));
+  DTRY(hipEventCreate(&d.ev_c));
+  DTRY(hipEventCreate(&d.ev_d));
+  DTRY(dalloc(&d.sc, 1));
+  DTRY(hipHostMalloc((void **)&d.h_sc, sizeof(DevScalars), hipHostMallocDefault));
+  d.n_tiles_cap = (d.batch_cap + kTileRecords - 1) / kTileRecords + 1;
+  DTRY(dalloc(&d.tile_max, d.n_tiles_cap));
+  DTRY(dalloc(&d.tile_min, d.n_tiles_cap));
+  DTRY(dalloc(&d.tile_prefix, d.n_tiles_cap));
+  DTRY(dalloc(&d.st_key, d.batch_cap));
+  DTRY(dalloc(&d.st_ts, d.batch_cap));
+  for (int c = 0; c < cfg.n_cols; ++c) {
+    DTRY(dalloc(&d.st_col[c], d.batch_cap));
+    DTRY(dalloc(&d.st_valid[c], d.batch_cap));
+  }
+  uint64_t rows = cfg.state_capacity ? cfg.state_capacity : (1ull << 21);
+  d.cap = next_pow2(rows * 2);  // load factor <= 1/2
+  if (cfg.window_kind == HSG_SESSION) {
+    int rc = session_device_init(d, cfg, prog, rows, err);
+    if (rc != HSG_OK) return rc;
+  } else {
+    DTRY(dalloc(&d.tw.keys, d.cap));
+    DTRY(dalloc(&d.tw.aggs, d.cap * (uint64_t)prog.n_slots));
+    DTRY(dalloc(&d.tw.stamp, d.cap));
+    d.tw.mask = d.cap - 1;
+  }
+  // changelog capacity
+  uint64_t oc = cfg.out_capacity;
+  if (!oc && cfg.emit_mode != HSG_EMIT_NONE) {
+    oc = d.batch_cap * wpr;
+    if (cfg.emit_mode == HSG_EMIT_PER_BATCH && cfg.window_kind != HSG_SESSION && oc > d.cap) oc = d.cap;
+  }
+  d.out_cap = oc;
+  int rc = alloc_out(d.out, d.out_cap, cfg.n_aggs, err);
+  if (rc != HSG_OK) return rc;
+  if (cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.window_kind == HSG_SESSION) {
+    rc = perrecord_device_init(d, cfg, prog, err);
+    if (rc != HSG_OK) return rc;
+  }
+  if (nranks > 1) {
+    rc = exchange_device_init(d, cfg, batch_cap, err);
+    if (rc != HSG_OK) return rc;
+  }
+  return op_device_reset(d, cfg, prog, err);
+}
+
+void op_device_free(OpDevice &d) {
+  if (d.stream) hipStreamSynchronize(d.stream);
+  dfree(d.sc);
+  if (d.h_sc) hipHostFree(d.h_sc);
+  d.h_sc = nullptr;
+  dfree(d.tile_max);
+  dfree(d.tile_min);
+  dfree(d.tile_prefix);
+  dfree(d.st_key);
+  dfree(d.st_ts);
+  for (int c = 0; c < kMaxCols; ++c) {
+    dfree(d.st_col[c]);
+    dfree(d.st_valid[c]);
+  }
+  dfree(d.st_seq);
+  dfree(d.st_wm);
+  dfree(d.tw.keys);
+  dfree(d.tw.aggs);
+  dfree(d.tw.stamp);
+  dfree(d.ss.keys);
+  dfree(d.ss.list_off);
+  dfree(d.ss.list_len);
+  dfree(d.ss.list_cap);
+  dfree(d.ss.a_start);
+  dfree(d.ss.a_end);
+  dfree(d.ss.a_stamp);
+  dfree(d.ss.a_aggs);
+  dfree(d.arena_top);
+  free_out(d.out);
+  if (d.scratch) hipFree(d.scratch);
+  d.scratch = nullptr;
+  if (d.xsend) hipFree(d.xsend);
+  if (d.xrecv) hipFree(d.xrecv);
+  d.xsend = d.xrecv = nullptr;
+  dfree(d.d_counts);
+  if (d.h_counts) hipHostFree(d.h_counts);
+  d.h_counts = nullptr;
+  if (d.ev_a) hipEventDestroy(d.ev_a);
+  if (d.ev_b) hipEventDestroy(d.ev_b);
+  if (d.ev_c) hipEventDestroy(d.ev_c);
+  if (d.ev_d) hipEventDestroy(d.ev_d);
+  d.ev_a = d.ev_b = d.ev_c = d.ev_d = nullptr;
+  if (d.stream) hipStreamDestroy(d.stream);
+  d.stream = nullptr;
+}
+
+// Resolve the batch into device pointers, copying host arrays into staging.
+int stage_batch(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err) {
+  memset(&kb, 0, sizeof(kb));
+  kb.n = b->n;
+  const uint64_t n = b->n;
+  if (b->mem == HSG_MEM_DEVICE) {
+    kb.key = b->key_id;
+    kb.ts = b->ts;
+    for (int c = 0; c < b->n_cols; ++c) {
+      kb.col[c] = (const int64_t *)b->cols[c];
+      kb.valid[c] = (b->valid && b->valid[c]) ? b->valid[c] : nullptr;
+    }
+    return HSG_OK;
+  }
+  if (n) {
+    DTRY(hipMemcpyAsync(d.st_key, b->key_id, n * 4, hipMemcpyHostToDevice, d.stream));
+    DTRY(hipMemcpyAsync(d.st_ts, b->ts, n * 8, hipMemcpyHostToDevice, d.stream));
+  }
+  kb.key = d.st_key;
+  kb.ts = d.st_ts;
+  for (int c = 0; c < b->n_cols; ++c) {
+    if (n) DTRY(hipMemcpyAsync(d.st_col[c], b->cols[c], n * 8, hipMemcpyHostToDevice, d.stream));
+    kb.col[c] = d.st_col[c];
+    if (b->valid && b->valid[c]) {
+      if (n) DTRY(hipMemcpyAsync(d.st_valid[c], b->valid[c], n, hipMemcpyHostToDevice, d.stream));
+      kb.valid[c] = d.st_valid[c];
+    }
+  }
+  return HSG_OK;
+}
+
+TwParams make_tw_params(const hsg_op_config &cfg, const PushArgs &a) {
+  TwParams p;
+  memset(&p, 0, sizeof(p));
+  p.kind = cfg.window_kind;
+  p.batch_id = (int32_t)a.batch_id;
+  p.size = cfg.size_ms;
+  p.adv = cfg.window_kind == HSG_HOPPING ? cfg.advance_ms : (cfg.size_ms > 0 ? cfg.size_ms : 1);
+  p.grace = cfg.grace_ms;
+  p.wm_in = a.wm_in;
+  p.rec_base = a.rec_base;
+  p.div = make_divider((uint64_t)p.adv);
+  return p;
+}
+
+// Stream time for a batch in arrival order: per-tile maxima, exclusive tile
+// prefix (seeded with wm_in), epoch initialisation.
+void launch_stream_time(OpDevice &d, const hsg_op_config &cfg, const Batch &kb, int64_t wm_in, int64_t adv) {
+  uint64_t tiles = (kb.n + kTileRecords - 1) / kTileRecords;
+  launch_tile_stats(d.stream, kb, d.tile_max, d.tile_min, tiles);
+  launch_tile_scan(d.stream, d.tile_max, d.tile_min, d.tile_prefix, tiles, wm_in, adv,
+                   cfg.window_kind == HSG_TUMBLING || cfg.window_kind == HSG_HOPPING, d.sc);
+}
+
+int fetch_scalars(OpDevice &d, std::string &err) {
+  DTRY(hipMemcpyAsync(d.h_sc, d.sc, sizeof(DevScalars), hipMemcpyDeviceToHost, d.stream));
+  DTRY(hipStreamSynchronize(d.stream));
+  DTRY(hipGetLastError());
+  return HSG_OK;
+}
+
+int clear_batch_scalars(OpDevice &d, std::string &err) {
+  // err, pairs, late, out_rows, touched (offsets 20..55); wm/epoch/live persist
+  DTRY(hipMemsetAsync((char *)d.sc + offsetof(DevScalars, err), 0,
+                      offsetof(DevScalars, live) - offsetof(DevScalars, err), d.stream));
+  return HSG_OK;
+}
+
+static int status_from_err(uint32_t e, std::string &err) {
+  if (e & ERR_OOM) {
+    err = "HBM state table / arena full (raise state_capacity)";
+    return HSG_E_OOM;
+  }
+  if (e & ERR_RANGE) {
+    err = "window index outside the op's 2^32-window span around its first batch";
+    return HSG_E_RANGE;
+  }
+  return HSG_OK;
+}
+
+int finish_batch(OpDevice &d, int64_t wm_in, uint64_t n, PushResult &r, std::string &err) {
+  int rc = fetch_scalars(d, err);
+  if (rc != HSG_OK) return rc;
+  const DevScalars &s = *d.h_sc;
+  r.wm_out = n ? s.wm_out : wm_in;
+  r.pairs = s.pairs;
+  r.late = s.late;
+  r.out_rows = s.out_rows;
+  r.touched = s.touched;
+  r.state_rows = s.live;
+  return status_from_err(s.err, err);
+}
+
+static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
+                            const Batch &kb, PushResult &r, std::string &err) {
+  TwParams p = make_tw_params(cfg, a);
+  int rc = clear_batch_scalars(d, err);
+  if (rc != HSG_OK) return rc;
+  if (kb.n) {
+    launch_stream_time(d, cfg, kb, a.wm_in, p.adv);
+    DTRY(hipEventRecord(d.ev_a, d.stream));
+    launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, d.sc);
+    DTRY(hipEventRecord(d.ev_b, d.stream));
+    int mode = cfg.emit_mode == HSG_EMIT_PER_BATCH ? 0 : (has_last(prog) ? 2 : -1);
+    if (mode >= 0)
+      launch_tw_scan_emit(d.stream, d.tw, d.cap, prog, p, kb, mode, d.out, a.pending, d.out_cap, d.sc,
+                          (uint64_t *)&d.sc->out_rows);
+    DTRY(hipGetLastError());
+  }
+  rc = finish_batch(d, a.wm_in, kb.n, r, err);
+  if (kb.n) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, d.ev_a, d.ev_b) == hipSuccess) r.agg_ms = ms;
+    r.agg_launches = 1;
+  }
+  r.touched = r.out_rows;
+  return rc;
+}
+
+int op_push(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, PushResult &r,
+            std::string &err) {
+  const hsg_batch *b = a.batch;
+  // the changelog must have room for the worst case of this batch
+  if (cfg.emit_mode != HSG_EMIT_NONE) {
+    uint64_t bound = b->n * (uint64_t)a.nranks * d.wpr;
+    if (cfg.emit_mode == HSG_EMIT_PER_BATCH && cfg.window_kind != HSG_SESSION && bound > d.cap) bound = d.cap;
+    if (a.pending + bound > d.out_cap) {
+      err = "changelog buffer full: drain before pushing (out_capacity)";
+      return HSG_E_CAPACITY;
+    }
+  }
+  if (a.nranks > 1) return push_sharded(d, cfg, prog, a, r, err);
+  Batch kb;
+  int rc = stage_batch(d, b, kb, err);
+  if (rc != HSG_OK) return rc;
+  r.owned = kb.n;
+  r.global_records = kb.n;
+  return push_local(d, cfg, prog, a, kb, nullptr, nullptr, r, err);
+}
+
+// Aggregate an already-staged (and, for multi-GPU, already-exchanged) batch.
+// seq / rec_wm, when given, carry each record's global sequence number and the
+// watermark it saw in the global arrival order (computed before the exchange).
+int push_local(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, const Batch &kb,
+               const int64_t *seq, const int64_t *rec_wm, PushResult &r, std::string &err) {
+  if (cfg.window_kind == HSG_SESSION) return push_session(d, cfg, prog, a, kb, seq, r, err);
+  if (cfg.emit_mode == HSG_EMIT_PER_RECORD) return push_time_perrecord(d, cfg, prog, a, kb, seq, rec_wm, r, err);
+  if (seq || rec_wm) return push_time_atomic_sharded(d, cfg, prog, a, kb, seq, rec_wm, r, err);
+  return push_time_atomic(d, cfg, prog, a, kb, r, err);
+}
+
+int op_copy_rows(OpDevice &d, const OutCols &src, uint64_t from, uint64_t n, int n_aggs, const hsg_rows *out,
+                 std::string &err) {
+  if (n == 0) return HSG_OK;
+  hipMemcpyKind k = out->mem == HSG_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+  if (out->key_id) DTRY(hipMemcpyAsync(out->key_id, src.key + from, n * 4, k, d.stream));
+  if (out->win_start) DTRY(hipMemcpyAsync(out->win_start, src.ws + from, n * 8, k, d.stream));
+  if (out->win_end) DTRY(hipMemcpyAsync(out->win_end, src.we + from, n * 8, k, d.stream));
+  if (out->src_index) DTRY(hipMemcpyAsync(out->src_index, src.src + from, n * 8, k, d.stream));
+  for (int j = 0; j < n_aggs; ++j)
+    if (out->aggs && out->aggs[j]) DTRY(hipMemcpyAsync(out->aggs[j], src.agg[j] + from, n * 8, k, d.stream));
+  DTRY(hipStreamSynchronize(d.stream));
+  return HSG_OK;
+}
+
+int op_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hsg_rows *out, uint64_t *n_out,
+            std::string &err) {
+  int rc = fetch_scalars(d, err);
+  if (rc != HSG_OK) return rc;
+  uint64_t live = d.h_sc->live;
+  *n_out = 0;
+  if (live == 0) return HSG_OK;
+  OutCols tmp;
+  memset(&tmp, 0, sizeof(tmp));
+  rc = alloc_out(tmp, live, cfg.n_aggs, err);
+  if (rc == HSG_OK) {
+    uint64_t *counter = nullptr;
+    if (hipMalloc((void **)&counter, 8) != hipSuccess) {
+      free_out(tmp);
+      err = "hipMalloc counter";
+      return HSG_E_DEVICE;
+    }
+    hipMemsetAsync(counter, 0, 8, d.stream);
+    if (cfg.window_kind == HSG_SESSION) {
+      launch_session_dump(d, cfg, prog, tmp, live, counter);
+    } else {
+      PushArgs a;
+      TwParams p = make_tw_params(cfg, a);
+      Batch none;
+      memset(&none, 0, sizeof(none));
+      launch_tw_scan_emit(d.stream, d.tw, d.cap, prog, p, none, 1, tmp, 0, live, d.sc, counter);
+    }
+    uint64_t got = 0;
+    hipMemcpyAsync(&got, counter, 8, hipMemcpyDeviceToHost, d.stream);
+    hipError_t e = hipStreamSynchronize(d.stream);
+    hipFree(counter);
+    if (e != hipSuccess) {
+      free_out(tmp);
+      err = std::string("dump: ") + hipGetErrorString(e);
+      return HSG_E_DEVICE;
+    }
+    if (got > live) got = live;
+    rc = op_copy_rows(d, tmp, 0, got, cfg.n_aggs, out, err);
+    *n_out = got;
+  }
+  free_out(tmp);
+  return rc;
+}
+
+}  // namespace hsg

@@ -1,0 +1,108 @@
+"""ctypes binding of libhstream_gpu (the product path).
+
+Loads the in-tree ``hstream_amd/libhstream_gpu.so``; there is no fallback of
+any kind: if the library is missing or the GPU is absent, constructing an
+Engine raises.
+"""
+import ctypes as C
+import os
+
+from . import abi
+from .columnar import OpHandle, OpSpec, declare_op_functions
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhstream_gpu.so")
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libhstream_gpu.so and declare every exported signature."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"libhstream_gpu.so not found at {path}: run __graft_entry__.build() "
+            "(the GPU path has no fallback)")
+    L = C.CDLL(path)
+    vp = C.c_void_p
+    P = C.POINTER
+    L.hsg_comm_unique_id.argtypes = [P(C.c_uint8), C.c_size_t]
+    L.hsg_comm_unique_id.restype = C.c_int
+    L.hsg_engine_create.argtypes = [P(abi.hsg_engine_config), P(vp)]
+    L.hsg_engine_create.restype = C.c_int
+    L.hsg_engine_destroy.argtypes = [vp]
+    L.hsg_engine_destroy.restype = None
+    L.hsg_engine_last_error.argtypes = [vp]
+    L.hsg_engine_last_error.restype = C.c_char_p
+    L.hsg_op_create.argtypes = [vp, P(abi.hsg_op_config), P(vp)]
+    L.hsg_op_create.restype = C.c_int
+    L.hsg_op_stats.argtypes = [vp, P(abi.hsg_stats)]
+    L.hsg_op_stats.restype = C.c_int
+    declare_op_functions(L, "hsg")
+    _lib = L
+    return L
+
+
+def comm_unique_id() -> bytes:
+    L = load_library()
+    buf = (C.c_uint8 * abi.HSG_COMM_ID_BYTES)()
+    rc = L.hsg_comm_unique_id(buf, abi.HSG_COMM_ID_BYTES)
+    if rc != abi.HSG_OK:
+        raise abi.HStreamGpuError(rc, "hsg_comm_unique_id")
+    return bytes(buf)
+
+
+class Engine:
+    """One per process and GPU (hsg_engine_create)."""
+
+    def __init__(self, device=0, rank=0, nranks=1, comm_id=None, batch_capacity=1 << 24):
+        L = load_library()
+        self._lib = L
+        self._id_buf = None
+        cfg = abi.hsg_engine_config(device=device, rank=rank, nranks=nranks, reserved0=0,
+                                    comm_id=None, batch_capacity=batch_capacity)
+        if comm_id is not None:
+            self._id_buf = (C.c_uint8 * abi.HSG_COMM_ID_BYTES)(*comm_id[: abi.HSG_COMM_ID_BYTES])
+            cfg.comm_id = C.cast(self._id_buf, P_u8)
+        h = C.c_void_p()
+        rc = L.hsg_engine_create(C.byref(cfg), C.byref(h))
+        if rc != abi.HSG_OK:
+            raise abi.HStreamGpuError(rc, "hsg_engine_create")
+        self._h = h
+        self.device, self.rank, self.nranks, self.batch_capacity = device, rank, nranks, batch_capacity
+
+    def op(self, spec: OpSpec) -> "GpuOp":
+        return GpuOp(self, spec)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.hsg_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+P_u8 = C.POINTER(C.c_uint8)
+
+
+class GpuOp(OpHandle):
+    """One windowed GROUP BY operator on the GPU (hsg_op_create)."""
+
+    def __init__(self, engine: Engine, spec: OpSpec):
+        cfg, keep = spec.to_config()
+        h = C.c_void_p()
+        rc = engine._lib.hsg_op_create(engine._h, C.byref(cfg), C.byref(h))
+        if rc != abi.HSG_OK:
+            msg = engine._lib.hsg_engine_last_error(engine._h)
+            raise abi.HStreamGpuError(rc, f"hsg_op_create: {msg.decode() if msg else ''}")
+        self.engine = engine  # keep the engine alive while the op lives
+        super().__init__(engine._lib, "hsg", h, spec)
+
+    def stats(self) -> dict:
+        s = abi.hsg_stats()
+        self._check(self._lib.hsg_op_stats(self._h, C.byref(s)), "op_stats")
+        return s.as_dict()

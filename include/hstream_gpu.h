@@ -1,0 +1,210 @@
+/*
+ * hstream_gpu.h — C ABI of libhstream_gpu, the MI355X (gfx950) engine behind
+ * HStreamDB's windowed GROUP BY operators.
+ *
+ * What it replaces (reference = Yu-zh/hstream @ 2025-01-17, paths relative to
+ * its root):
+ *
+ *   hsg_op_create (HSG_TUMBLING / HSG_HOPPING)
+ *       TimeWindowedStream.aggregate / count
+ *         hstream-processing/src/HStream/Processing/Stream/TimeWindowedStream.hs:32-70
+ *       with the window spec of mkTumblingWindow / mkHoppingWindow
+ *         .../Stream/TimeWindows.hs:23-43
+ *   hsg_op_create (HSG_SESSION)
+ *       SessionWindowedStream.aggregate / count
+ *         .../Stream/SessionWindowedStream.hs:33-72, mkSessionWindows SessionWindows.hs:25-30
+ *   hsg_op_create (HSG_UNWINDOWED)
+ *       GroupedStream.aggregate / count  .../Stream/GroupedStream.hs:35-87
+ *   hsg_push_batch
+ *       the per-record processors TimeWindowedStream.aggregateProcessor (:72-117),
+ *       SessionWindowedStream.aggregateProcessor (:74-118),
+ *       GroupedStream.aggregateProcessor (:71-87), driven for a whole poll batch
+ *       instead of record by record by runTask (Processor.hs:128-144), with the
+ *       stream-time update of Processor.hs:139 / Processor/Internal.hs:160-166.
+ *   hsg_drain
+ *       the `forward` of every updated (key, window) row (TimeWindowedStream.hs:101,
+ *       SessionWindowedStream.hs:97,118, GroupedStream.hs:87).
+ *   hsg_dump_state
+ *       ksDump / ssDump (Store.hs:59,81 and :143,238-241) used by views
+ *       (hstream/src/HStream/Server/Handler.hs:274-321).
+ *   hsg_agg kinds
+ *       the SQL aggregate components of hstream-sql/src/HStream/SQL/Codegen.hs:399-469
+ *       (COUNT(*), COUNT(col), SUM, MIN, MAX, non-aggregate passthrough = HSG_LAST)
+ *       plus AVG, which the reference rejects at codegen (Codegen.hs:462) and which
+ *       this ABI defines as SUM(col) / COUNT(col).
+ *
+ * Conventions (mirroring the reference's own FFI, hstream-store cbits and
+ * common/HStream/Stats.hs): opaque handles freed by *_destroy functions that
+ * are usable as ForeignPtr finalizers, plain pointers + sizes, int status codes
+ * (0 = OK, negative = error), no C++ exception crosses the ABI, a per-handle
+ * last-error string. Calls on one op handle must be serialized by the caller;
+ * distinct op handles may be used concurrently from different OS threads.
+ * hsg_push_batch blocks until the GPU work is done: bind it as a *safe* ccall.
+ */
+#ifndef HSTREAM_GPU_H
+#define HSTREAM_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes --------------------------------------------------------- */
+#define HSG_OK           0
+#define HSG_E_INVALID   (-1) /* bad argument / unsupported combination           */
+#define HSG_E_OOM       (-2) /* HBM state table or session arena full            */
+#define HSG_E_CAPACITY  (-3) /* batch larger than capacity / changelog not drained / out buffer too small */
+#define HSG_E_DEVICE    (-4) /* HIP runtime error                                */
+#define HSG_E_COMM      (-5) /* RCCL error                                       */
+#define HSG_E_RANGE     (-6) /* window index outside the op's 2^32-window span   */
+
+/* key id reserved for records that only advance stream time (filtered by WHERE,
+ * failed decode, aggregate type error): Processor.hs:139 updates the task
+ * timestamp before the topology runs, so such records still move the watermark. */
+#define HSG_KEY_NONE 0xFFFFFFFFu
+
+#define HSG_COMM_ID_BYTES 128
+
+/* grace used by every reference window spec: 24 h (TimeWindows.hs:34,42; SessionWindows.hs:29) */
+#define HSG_DEFAULT_GRACE_MS 86400000LL
+
+enum hsg_window_kind {
+  HSG_TUMBLING   = 0, /* mkTumblingWindow size            (advance = size)      */
+  HSG_HOPPING    = 1, /* mkHoppingWindow size advance                           */
+  HSG_SESSION    = 2, /* mkSessionWindows gap (grace unused, as in the reference) */
+  HSG_UNWINDOWED = 3  /* GroupedStream.aggregate: one implicit window per key   */
+};
+
+enum hsg_emit_mode {
+  HSG_EMIT_PER_RECORD = 0, /* exact reference changelog: one row per (record, accepted window),
+                              arrival order, windows in ascending start              */
+  HSG_EMIT_PER_BATCH  = 1, /* one row per group touched by the batch = the last per-record
+                              row of that group; order unspecified                     */
+  HSG_EMIT_NONE       = 2  /* state only (views)                                       */
+};
+
+enum hsg_col_type { HSG_I64 = 0, HSG_F64 = 1 };
+
+enum hsg_agg_kind {
+  HSG_COUNT_ALL = 0, /* COUNT(*)   Codegen.hs:404-411, DSL count TimeWindowedStream.hs:59-70 */
+  HSG_COUNT     = 1, /* COUNT(col) Codegen.hs:412-422: +1 when the field is present          */
+  HSG_SUM       = 2, /* SUM(col)   Codegen.hs:423-435                                        */
+  HSG_MIN       = 3, /* MIN(col)   Codegen.hs:449-461, identity maxBound::Int                */
+  HSG_MAX       = 4, /* MAX(col)   Codegen.hs:436-448, identity minBound::Int                */
+  HSG_AVG       = 5, /* SUM(col)/COUNT(col) as f64 (NaN when COUNT(col) = 0)                 */
+  HSG_LAST      = 6  /* non-aggregate SELECT column, Codegen.hs:463-469 (time windows and
+                        unwindowed only)                                                     */
+};
+
+enum hsg_mem { HSG_MEM_HOST = 0, HSG_MEM_DEVICE = 1 };
+
+typedef struct hsg_engine hsg_engine;
+typedef struct hsg_op hsg_op;
+
+typedef struct {
+  int32_t device;          /* HIP device ordinal; -1 = the calling thread's current device */
+  int32_t rank;            /* this process's rank in the key-sharded group                */
+  int32_t nranks;          /* 1 = single GPU, no communicator                              */
+  int32_t reserved0;
+  const uint8_t *comm_id;  /* HSG_COMM_ID_BYTES from hsg_comm_unique_id() on rank 0, shared
+                              out of band; NULL when nranks == 1                            */
+  uint64_t batch_capacity; /* max records per hsg_push_batch on this rank                   */
+} hsg_engine_config;
+
+typedef struct {
+  int32_t kind;   /* hsg_agg_kind                                  */
+  int32_t column; /* value column index; ignored for HSG_COUNT_ALL */
+} hsg_agg;
+
+typedef struct {
+  int32_t window_kind;     /* hsg_window_kind                                            */
+  int32_t emit_mode;       /* hsg_emit_mode                                              */
+  int64_t size_ms;         /* TUMBLING / HOPPING window size  (twSizeMs)                 */
+  int64_t advance_ms;      /* HOPPING advance (twAdvanceMs); TUMBLING: = size_ms         */
+  int64_t gap_ms;          /* SESSION inactivity gap (swInactivityGap)                   */
+  int64_t grace_ms;        /* twGraceMs; use HSG_DEFAULT_GRACE_MS for reference parity  */
+  int32_t n_cols;          /* value columns carried by every batch                       */
+  int32_t n_aggs;
+  const int32_t *col_types;/* n_cols hsg_col_type                                        */
+  const hsg_agg *aggs;     /* n_aggs output aggregates, in output order                  */
+  uint64_t state_capacity; /* HBM state rows (groups or sessions); 0 = engine default    */
+  uint64_t out_capacity;   /* changelog rows buffered in HBM between drains; 0 = default */
+} hsg_op_config;
+
+/* One micro-batch in columnar form, records in arrival order. */
+typedef struct {
+  uint64_t n;
+  int32_t mem;                  /* hsg_mem of every pointer below                        */
+  int32_t n_cols;               /* must equal the op's n_cols                            */
+  const uint32_t *key_id;       /* dictionary-encoded group-by key, HSG_KEY_NONE = skip   */
+  const int64_t *ts;            /* event timestamp, ms (record header publish time)      */
+  const void *const *cols;      /* n_cols arrays of int64_t or double                    */
+  const uint8_t *const *valid;  /* n_cols presence arrays (1 byte/record, 0 = field absent);
+                                   NULL or a NULL entry = all present                    */
+} hsg_batch;
+
+/* Columnar changelog / state rows. */
+typedef struct {
+  uint64_t capacity;   /* rows every array can hold                                    */
+  int32_t mem;         /* hsg_mem of every pointer below                               */
+  int32_t n_aggs;      /* must equal the op's n_aggs                                   */
+  uint32_t *key_id;
+  int64_t *win_start;  /* time windows: window start; sessions: session start          */
+  int64_t *win_end;    /* time windows: start + size; sessions: session end (inclusive) */
+  int64_t *src_index;  /* per-record mode: global index of the producing record; else -1 */
+  void *const *aggs;   /* n_aggs arrays: int64_t (COUNT*, SUM/MIN/MAX/LAST of i64) or double */
+} hsg_rows;
+
+typedef struct {
+  uint64_t batches;           /* batches pushed since create/reset                     */
+  uint64_t records;           /* records pushed (this rank's ingest)                    */
+  uint64_t records_owned;     /* records aggregated on this rank after the key exchange */
+  uint64_t pairs;             /* accepted (record, window) updates, last batch          */
+  uint64_t late_dropped;      /* (record, window) pairs rejected by grace, last batch   */
+  uint64_t touched;           /* groups / sessions touched, last batch                  */
+  uint64_t state_rows;        /* live groups / sessions                                 */
+  uint64_t pending_rows;      /* changelog rows waiting for hsg_drain                   */
+  double   last_batch_ms;     /* wall time of the last hsg_push_batch                   */
+  double   agg_kernel_ms;     /* cumulative device time of the dominant kernel          */
+  uint64_t agg_kernel_launches;
+  double   exchange_ms;       /* cumulative device time of the key exchange             */
+  uint64_t exchange_bytes;    /* cumulative bytes this rank sent to peers               */
+  uint64_t pairs_total;       /* cumulative accepted (record, window) updates           */
+  uint64_t touched_total;     /* cumulative groups / sessions touched (summed per batch) */
+} hsg_stats;
+
+/* ---- engine: one per process and GPU ---------------------------------------- */
+int  hsg_comm_unique_id(uint8_t *out, size_t len);
+int  hsg_engine_create(const hsg_engine_config *cfg, hsg_engine **out);
+void hsg_engine_destroy(hsg_engine *eng);
+const char *hsg_engine_last_error(const hsg_engine *eng);
+
+/* ---- operator: one per windowed GROUP BY -------------------------------------- */
+int  hsg_op_create(hsg_engine *eng, const hsg_op_config *cfg, hsg_op **out);
+void hsg_op_destroy(hsg_op *op);
+int  hsg_op_reset(hsg_op *op);            /* drop all state and pending rows          */
+const char *hsg_last_error(const hsg_op *op);
+
+/* Process one batch. *inout_watermark is the task's stream time (initially -1,
+ * Processor/Internal.hs:151); it is read as the value before the batch and
+ * overwritten with the value after it (max over all ranks' records). */
+int  hsg_push_batch(hsg_op *op, const hsg_batch *batch, int64_t *inout_watermark);
+
+int  hsg_pending_rows(const hsg_op *op, uint64_t *n);
+/* Move up to out->capacity pending changelog rows into out (oldest first). If
+ * the pending rows do not fit, copies nothing, sets *n_out to the number
+ * pending and returns HSG_E_CAPACITY. */
+int  hsg_drain(hsg_op *op, hsg_rows *out, uint64_t *n_out);
+
+int  hsg_state_rows(hsg_op *op, uint64_t *n);
+/* Copy every live state row (views). Same capacity rule as hsg_drain. */
+int  hsg_dump_state(hsg_op *op, hsg_rows *out, uint64_t *n_out);
+
+int  hsg_op_stats(const hsg_op *op, hsg_stats *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HSTREAM_GPU_H */

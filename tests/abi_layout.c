@@ -1,0 +1,17 @@
+/* Prints sizeof / offsetof of the ABI structs; tests/test_abi.py compares them
+ * with the ctypes mirror in hstream_amd/abi.py. */
+#include <stddef.h>
+#include <stdio.h>
+#include "../include/hstream_gpu.h"
+#define F(T, m) printf("%s.%s %zu\n", #T, #m, offsetof(T, m))
+#define S(T) printf("%s %zu\n", #T, sizeof(T))
+int main(void) {
+  S(hsg_engine_config); F(hsg_engine_config, comm_id); F(hsg_engine_config, batch_capacity);
+  S(hsg_agg);
+  S(hsg_op_config); F(hsg_op_config, size_ms); F(hsg_op_config, grace_ms); F(hsg_op_config, n_cols);
+  F(hsg_op_config, col_types); F(hsg_op_config, aggs); F(hsg_op_config, state_capacity); F(hsg_op_config, out_capacity);
+  S(hsg_batch); F(hsg_batch, key_id); F(hsg_batch, ts); F(hsg_batch, cols); F(hsg_batch, valid);
+  S(hsg_rows); F(hsg_rows, key_id); F(hsg_rows, win_start); F(hsg_rows, src_index); F(hsg_rows, aggs);
+  S(hsg_stats); F(hsg_stats, last_batch_ms); F(hsg_stats, exchange_bytes); F(hsg_stats, touched_total);
+  return 0;
+}

@@ -1,0 +1,171 @@
+"""GPU parity: libhstream_gpu (through the C ABI) against the CPU oracle on the
+same seeded inputs. Integer aggregates, keys and window bounds bit-exact; f64
+SUM/AVG within 1e-6 relative (util.F64_RTOL)."""
+import numpy as np
+import pytest
+
+import pyoracle
+from hstream_amd import abi, datagen
+from hstream_amd.columnar import OpSpec
+from util import ALL_AGG_SETS, gen_small, load_kat, rows_equal, run_kat_case
+
+pytestmark = pytest.mark.gpu
+
+KAT = load_kat()
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need cuda:0"
+    from hstream_amd.engine import Engine
+    e = Engine(device=0, batch_capacity=1 << 22)
+    yield e
+    e.close()
+
+
+def _pair(eng, spec):
+    return eng.op(spec), pyoracle.OracleOp(spec)
+
+
+def _drive(eng, spec, batches, check_rows=True):
+    g, o = _pair(eng, spec)
+    f64 = spec.agg_is_f64()
+    wg = wo = -1
+    for bi, (key, ts, cols, valid) in enumerate(batches):
+        wg = g.push(key, ts, cols, valid, watermark=wg)
+        wo = o.push(key, ts, cols, valid, watermark=wo)
+        assert wg == wo, f"batch {bi}: watermark {wg} != {wo}"
+        if spec.emit_mode != abi.HSG_EMIT_NONE and check_rows:
+            rg, ro = g.drain(), o.drain()
+            rows_equal(rg, ro, f64, ordered=spec.emit_mode == abi.HSG_EMIT_PER_RECORD, what=f"changelog batch {bi}")
+    rows_equal(g.dump_state(), o.dump_state(), f64, what="state dump")
+    return g, o
+
+
+@pytest.mark.parametrize("case", KAT["cases"], ids=lambda c: c["name"])
+def test_reference_kat_gpu(eng, case):
+    run_kat_case(case, lambda spec: eng.op(spec))
+
+
+def _time_specs(modes):
+    out = []
+    for aggname, col_types in (("count", []), ("full_i64", [abi.HSG_I64]), ("mixed", [abi.HSG_I64, abi.HSG_F64])):
+        for kind, kw in ((abi.HSG_TUMBLING, dict(size_ms=10_000)),
+                         (abi.HSG_HOPPING, dict(size_ms=10_000, advance_ms=3_000)),
+                         (abi.HSG_HOPPING, dict(size_ms=60_000, advance_ms=5_000)),
+                         (abi.HSG_UNWINDOWED, {})):
+            for mode in modes:
+                out.append(pytest.param(OpSpec(kind, mode, col_types=col_types, aggs=ALL_AGG_SETS[aggname], **kw),
+                                        id=f"{aggname}-k{kind}-s{kw.get('size_ms', 0)}-m{mode}"))
+    return out
+
+
+@pytest.mark.parametrize("spec", _time_specs([abi.HSG_EMIT_PER_BATCH, abi.HSG_EMIT_NONE, abi.HSG_EMIT_PER_RECORD]))
+def test_time_windows_messy_batches(eng, spec):
+    ncols = len(spec.col_types)
+    batches = []
+    for bi in range(3):
+        key, ts, cols, valid = gen_small(1000 + bi, 5000, 37, col_types=spec.col_types or (abi.HSG_I64,),
+                                         span=100_000, base=10_000_000 + bi * 100_000)
+        batches.append((key, ts, cols[:ncols], valid[:ncols]))
+    _drive(eng, spec, batches)
+
+
+@pytest.mark.parametrize("mode", [abi.HSG_EMIT_PER_BATCH, abi.HSG_EMIT_PER_RECORD])
+def test_edge_batches(eng, mode):
+    spec = OpSpec(abi.HSG_HOPPING, mode, size_ms=7, advance_ms=3, col_types=[abi.HSG_I64],
+                  aggs=ALL_AGG_SETS["full_i64"])
+    e = np.array([], dtype=np.int64)
+    batches = [
+        (np.array([], dtype=np.uint32), e, [e], None),                                  # empty
+        (np.full(4, abi.HSG_KEY_NONE, np.uint32), np.array([5, 9, 1, 2]), [np.arange(4)], None),  # only NONE
+        (np.zeros(3, np.uint32), np.array([-5, -1, -100]), [np.arange(3)], None),     # only negative ts
+        (np.array([0, 1, 0, 1, 2], np.uint32), np.array([10, 13, 12, 0, 6]), [np.array([5, -3, 7, 1, 0])],
+         [np.array([1, 1, 0, 1, 1], np.uint8)]),                                        # size % adv != 0
+        (np.array([3, 3], np.uint32), np.array([2**31, 11]), [np.array([1, 2])], None),  # jump then late
+    ]
+    _drive(eng, spec, batches)
+
+
+def test_grace_boundary(eng):
+    """Window [0,10000) of a record is accepted iff stream time < 10000 + grace."""
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=10_000, aggs=[(abi.HSG_COUNT_ALL, 0)])
+    g = abi.HSG_DEFAULT_GRACE_MS
+    key = np.zeros(4, np.uint32)
+    ts = np.array([10_000 + g - 1, 5, 10_000 + g, 6])  # second record accepted, fourth rejected
+    _drive(eng, spec, [(key, ts, [], None)])
+
+
+def test_device_resident_batch(eng):
+    import torch
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=60_000, col_types=[abi.HSG_I64],
+                  aggs=datagen.C_AGGS_FULL)
+    key, ts, cols, valid = gen_small(5, 100_000, 1000, span=600_000)
+    g, o = _pair(eng, spec)
+    dk = torch.from_numpy(key.view(np.int32)).cuda()
+    dt = torch.from_numpy(ts).cuda()
+    dc = [torch.from_numpy(c).cuda() for c in cols]
+    dv = [torch.from_numpy(v).cuda() for v in valid]
+    wg = g.push(dk, dt, dc, dv, watermark=-1)
+    wo = o.push(key, ts, cols, valid, watermark=-1)
+    assert wg == wo
+    rows_equal(g.drain(), o.drain(), spec.agg_is_f64())
+    rows_equal(g.dump_state(), o.dump_state(), spec.agg_is_f64())
+
+
+@pytest.mark.parametrize("name", ["C1", "C2", "C2f", "C3"])
+def test_configs_reduced(eng, name):
+    """The BASELINE configs' window specs and aggregates at sizes the oracle finishes in seconds."""
+    cfg = datagen.CONFIGS[name]
+    n = {"C1": 1_000_000, "C2": 2_000_000, "C2f": 1_000_000, "C3": 300_000}[name]
+    spec = cfg.spec(abi.HSG_EMIT_PER_BATCH)
+    batches = []
+    bsz = min(n, 1 << 20)
+    for s in range(0, n, bsz):
+        h = datagen.generate(cfg, n=min(bsz, n - s), start=s, total=n)
+        batches.append((h["key_id"], h["ts"], h["cols"] if spec.col_types else [], None))
+    _drive(eng, spec, batches)
+
+
+def test_state_table_full_raises(eng):
+    spec = OpSpec(abi.HSG_UNWINDOWED, abi.HSG_EMIT_NONE, aggs=[(abi.HSG_COUNT_ALL, 0)], state_capacity=16)
+    g = eng.op(spec)
+    key = np.arange(1000, dtype=np.uint32)
+    with pytest.raises(abi.HStreamGpuError) as ei:
+        g.push(key, np.zeros(1000, np.int64), [], None)
+    assert ei.value.status == abi.HSG_E_OOM
+
+
+def test_changelog_must_be_drained(eng):
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_RECORD, size_ms=1000, aggs=[(abi.HSG_COUNT_ALL, 0)],
+                  out_capacity=10)
+    g = eng.op(spec)
+    g.push(np.zeros(8, np.uint32), np.arange(8, dtype=np.int64), [], None)
+    with pytest.raises(abi.HStreamGpuError) as ei:
+        g.push(np.zeros(8, np.uint32), np.arange(8, dtype=np.int64), [], None)
+    assert ei.value.status == abi.HSG_E_CAPACITY
+    assert len(g.drain()) == 8
+    g.push(np.zeros(8, np.uint32), np.arange(8, dtype=np.int64), [], None)
+
+
+def test_reset_clears_state(eng):
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=1000, aggs=[(abi.HSG_COUNT_ALL, 0)])
+    g = eng.op(spec)
+    g.push(np.zeros(8, np.uint32), np.arange(8, dtype=np.int64), [], None)
+    assert len(g.dump_state()) == 1
+    g.reset()
+    assert len(g.dump_state()) == 0
+    g.push(np.zeros(2, np.uint32), np.arange(2, dtype=np.int64), [], None)
+    assert g.dump_state().tuples() == [(0, 0, 1000, (2,))]
+
+
+def test_window_span_limit_is_reported(eng):
+    """Window indices are kept relative to the first batch in 32 bits; a record
+    2^32 advances away is refused with HSG_E_RANGE, never silently dropped."""
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_NONE, size_ms=3, aggs=[(abi.HSG_COUNT_ALL, 0)])
+    g = eng.op(spec)
+    g.push(np.zeros(1, np.uint32), np.array([10], np.int64), [], None)
+    with pytest.raises(abi.HStreamGpuError) as ei:
+        g.push(np.zeros(1, np.uint32), np.array([3 * 2**33], np.int64), [], None)
+    assert ei.value.status == abi.HSG_E_RANGE
