@@ -282,10 +282,12 @@ extern "C" int hsg_op_reset(hsg_op *op) {
     HIP_TRY(op, hipSetDevice(op->eng->device));
     int rc = op_device_reset(op->dev, op->cfg, op->prog, op->err);
     if (rc != HSG_OK) return rc;
+    // counters in hsg_stats are cumulative since create; only the state goes
     op->pending = 0;
     op->state_rows = 0;
     op->rec_base = 0;
-    memset(&op->stats, 0, sizeof(op->stats));
+    op->stats.state_rows = 0;
+    op->stats.pending_rows = 0;
     return HSG_OK;
   } catch (...) {
     return HSG_E_DEVICE;

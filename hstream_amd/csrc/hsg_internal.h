@@ -175,13 +175,17 @@ void launch_tile_stats(hipStream_t s, const Batch &b, int64_t *tile_max, int64_t
 void launch_tile_scan(hipStream_t s, const int64_t *tile_max, const int64_t *tile_min, int64_t *tile_prefix,
                       uint64_t n_tiles, int64_t wm_in, int64_t adv, bool set_epoch, DevScalars *sc);
 
-// time windows, atomic hash aggregation (per-batch / none modes)
+// time windows, atomic hash aggregation (per-batch / none modes). rec_wm / seq
+// (optional) carry per-record stream time and global sequence after a key
+// exchange; last_pass = the LAST-value resolution pass.
 void launch_tw_agg(hipStream_t s, const Batch &b, const TwParams &p, const TwTable &t, const Program &prog,
-                   const int64_t *tile_prefix, DevScalars *sc);
+                   const int64_t *tile_prefix, const int64_t *rec_wm, const int64_t *seq, DevScalars *sc,
+                   bool last_pass);
 // scan the table: emit rows whose stamp == batch_id (mode 0) or every live row (mode 1)
 void launch_tw_scan_emit(hipStream_t s, const TwTable &t, uint64_t cap, const Program &prog, const TwParams &p,
-                         const Batch &b, int mode, OutCols out, uint64_t out_base, uint64_t out_cap,
-                         DevScalars *sc, uint64_t *counter);
+                         int mode, OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc,
+                         uint64_t *counter);
+unsigned grid_for(uint64_t n, unsigned tpb);
 
 constexpr int kTileThreads = 256;
 constexpr int kRecPerThread = 4;

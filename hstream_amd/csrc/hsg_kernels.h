@@ -22,9 +22,6 @@ int push_local(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const
 int perrecord_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err);
 int push_time_perrecord(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
                         const Batch &kb, const int64_t *seq, const int64_t *rec_wm, PushResult &r, std::string &err);
-int push_time_atomic_sharded(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
-                             const Batch &kb, const int64_t *seq, const int64_t *rec_wm, PushResult &r,
-                             std::string &err);
 
 // sessions (session.cpp / k_session.hip)
 int session_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t rows, std::string &err);

@@ -5,6 +5,7 @@
 #include <string>
 
 #include "hsg_internal.h"
+#include "hsg_perrecord.h"
 
 namespace hsg {
 
@@ -55,6 +56,7 @@ struct OpDevice {
   OutCols out = {};
   uint64_t out_cap = 0;
   // per-record / session scratch (sort + scan)
+  PrBuffers pr = {};
   void *scratch = nullptr;
   uint64_t scratch_bytes = 0;
   // exchange buffers (multi-GPU)
@@ -62,6 +64,7 @@ struct OpDevice {
   void *xrecv = nullptr;
   uint64_t xbytes = 0;
   uint64_t *h_counts = nullptr;   // pinned [2 * nranks]
+  uint64_t *h_tmp = nullptr;      // pinned [8] small host<->device scalars
   uint64_t *d_counts = nullptr;
   int nranks = 1;
   int n_cols = 0;

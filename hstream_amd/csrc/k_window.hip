@@ -8,67 +8,14 @@
 //   grace check     TimeWindowedStream.hs:88-92 with stream time Processor.hs:139
 //   state update    TimeWindowedStream.hs:93-100 (ksGet / aggF / ksPut)
 //   SQL aggregates  hstream-sql/src/HStream/SQL/Codegen.hs:399-469
-// The aggregates used here (COUNT/SUM/MIN/MAX and LAST by record order) are
-// commutative per group, so applying a batch's updates in any order gives the
-// reference's final state; the exact per-record changelog is produced by the
-// sort-based path in k_perrecord.hip.
-#include "hsg_internal.h"
+// The aggregates (COUNT/SUM/MIN/MAX, and LAST resolved by global arrival
+// sequence) are commutative per group, so applying a batch's updates in any
+// order gives the reference's final state; the exact per-record changelog is
+// produced by the sort-based path in k_perrecord.hip.
+#include "hsg_dev.h"
+#include "hsg_tw.h"
 
 namespace hsg {
-
-// ---------------------------------------------------------------------------
-// small device helpers
-// ---------------------------------------------------------------------------
-__device__ inline int64_t wave_max_i64(int64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    int64_t u = __shfl_xor(v, o, 64);
-    v = u > v ? u : v;
-  }
-  return v;
-}
-__device__ inline int64_t wave_min_i64(int64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    int64_t u = __shfl_xor(v, o, 64);
-    v = u < v ? u : v;
-  }
-  return v;
-}
-__device__ inline uint64_t wave_sum_u64(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-// inclusive max-scan across the 64 lanes of a wave
-__device__ inline int64_t wave_incl_max(int64_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int64_t u = __shfl_up(v, o, 64);
-    if (lane >= o) v = u > v ? u : v;
-  }
-  return v;
-}
-__device__ inline uint64_t wave_incl_sum(uint64_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint64_t u = __shfl_up(v, o, 64);
-    if (lane >= o) v += u;
-  }
-  return v;
-}
-
-__device__ inline int64_t slot_identity_dev(int32_t op) {
-  switch (op) {
-    case S_MIN_I: return INT64_MAX;
-    case S_MAX_I: return INT64_MIN;
-    case S_MIN_F: return (int64_t)f64_ord(9223372036854775807.0);
-    case S_MAX_F: return (int64_t)f64_ord(-9223372036854775808.0);
-    default: return 0;
-  }
-}
 
 // ---------------------------------------------------------------------------
 // fills
@@ -87,7 +34,7 @@ __global__ void k_fill_rows(int64_t *__restrict__ aggs, uint64_t rows, Program p
     aggs[i] = slot_identity_dev(prog.slot_op[i % prog.n_slots]);
 }
 
-static unsigned grid_for(uint64_t n, unsigned tpb) {
+unsigned grid_for(uint64_t n, unsigned tpb) {
   uint64_t g = (n + tpb - 1) / tpb;
   if (g > 4096) g = 4096;
   if (g == 0) g = 1;
@@ -154,7 +101,6 @@ __global__ __launch_bounds__(1024) void k_tile_scan(const int64_t *__restrict__ 
     local = tmax[t] > local ? tmax[t] : local;
     lmin = tmin[t] < lmin ? tmin[t] : lmin;
   }
-  // exclusive scan of thread totals across the block
   int64_t incl = wave_incl_max(local);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (lane == 63) swave[w] = incl;
@@ -195,30 +141,8 @@ void launch_tile_scan(hipStream_t s, const int64_t *tile_max, const int64_t *til
 }
 
 // ---------------------------------------------------------------------------
-// the hash table
+// window assignment + hash aggregation, one tile of kTileRecords per workgroup
 // ---------------------------------------------------------------------------
-// Returns the slot of group g, inserting it if absent; -1 when the table is full.
-// A plain load is only a hint (a stale EMPTY costs one failed CAS); the CAS
-// result is authoritative, and a slot moves EMPTY -> g at most once.
-__device__ inline int64_t tw_find_or_insert(const TwTable &t, uint64_t g, uint32_t &fresh) {
-  uint64_t s = mix64(g) & t.mask;
-  for (uint64_t probe = 0; probe <= t.mask; ++probe) {
-    uint64_t cur = t.keys[s];
-    if (cur == g) return (int64_t)s;
-    if (cur == kEmpty) {
-      uint64_t old = atomicCAS((unsigned long long *)&t.keys[s], (unsigned long long)kEmpty, (unsigned long long)g);
-      if (old == kEmpty) { fresh += 1; return (int64_t)s; }
-      if (old == g) return (int64_t)s;
-    }
-    s = (s + 1) & t.mask;
-  }
-  return -1;
-}
-
-__device__ inline bool rec_present(const Batch &b, int c, uint64_t i) {
-  return b.valid[c] == nullptr || b.valid[c][i] != 0;
-}
-
 __device__ inline void apply_slots(const Program &prog, int64_t *__restrict__ row, const Batch &b, uint64_t i,
                                    uint64_t seq1) {
   for (int s = 0; s < prog.n_slots; ++s) {
@@ -246,84 +170,75 @@ __device__ inline void apply_slots(const Program &prog, int64_t *__restrict__ ro
   }
 }
 
-// ---------------------------------------------------------------------------
-// window assignment + hash aggregation, one tile of kTileRecords per workgroup
-// ---------------------------------------------------------------------------
+// LAST resolution: the record whose sequence won LAST_SEQ writes LAST_VAL.
+__device__ inline void apply_last(const Program &prog, int64_t *__restrict__ row, const Batch &b, uint64_t i,
+                                  uint64_t seq1) {
+  for (int s = 0; s < prog.n_slots; ++s) {
+    if (prog.slot_op[s] != S_LAST_SEQ) continue;
+    const int c = prog.slot_col[s];
+    if (rec_present(b, c, i) && (uint64_t)row[s] == seq1) row[s + 1] = b.col[c][i];
+  }
+}
+
+// pass 0 = aggregate, pass 1 = LAST resolution (lookups only)
+template <int PASS>
 __global__ __launch_bounds__(kTileThreads) void k_tw_agg(Batch b, TwParams p, TwTable t, Program prog,
-                                                         const int64_t *__restrict__ tprefix, DevScalars *sc) {
-  __shared__ int64_t swave[kTileThreads / 64];
+                                                         const int64_t *__restrict__ tprefix,
+                                                         const int64_t *__restrict__ rec_wm,
+                                                         const int64_t *__restrict__ seq, DevScalars *sc) {
   __shared__ uint64_t sred[3][kTileThreads / 64];
   const uint64_t base = (uint64_t)blockIdx.x * kTileRecords;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t k_epoch = sc->k_epoch;
 
-  // 1) stream time per record: inclusive prefix max in arrival order
   uint32_t key[kRecPerThread];
   int64_t ts[kRecPerThread], wm[kRecPerThread];
-  int64_t carry = tprefix[blockIdx.x];
 #pragma unroll
   for (int r = 0; r < kRecPerThread; ++r) {
     uint64_t i = base + (uint64_t)r * kTileThreads + threadIdx.x;
     bool in = i < b.n;
     key[r] = in ? b.key[i] : HSG_KEY_NONE;
     ts[r] = in ? b.ts[i] : INT64_MIN;
+    if (rec_wm) wm[r] = in ? rec_wm[i] : INT64_MIN;
   }
-#pragma unroll
-  for (int r = 0; r < kRecPerThread; ++r) {
-    int64_t incl = wave_incl_max(ts[r]);
-    if (lane == 63) swave[w] = incl;
-    __syncthreads();
-    int64_t before = carry;
-    for (int k = 0; k < w; ++k) before = swave[k] > before ? swave[k] : before;
-    wm[r] = incl > before ? incl : before;
-    int64_t tot = carry;
-    for (int k = 0; k < kTileThreads / 64; ++k) tot = swave[k] > tot ? swave[k] : tot;
-    carry = tot;
-    __syncthreads();
-  }
+  // 1) stream time per record (or the one computed before a key exchange)
+  if (!rec_wm) tile_stream_time(ts, tprefix[blockIdx.x], wm);
 
   // 2) windows + hash aggregation
   uint64_t pairs = 0, late = 0;
   uint32_t fresh = 0, err = 0;
-  const bool unwin = p.kind == HSG_UNWINDOWED;
 #pragma unroll 1
   for (int r = 0; r < kRecPerThread; ++r) {
     if (key[r] == HSG_KEY_NONE) continue;
     const uint64_t i = base + (uint64_t)r * kTileThreads + threadIdx.x;
     uint64_t k_lo, k_hi;
-    if (unwin) {
-      k_lo = 0; k_hi = 0;
-    } else {
-      if (ts[r] < 0) continue;  // windowsFor yields no window for ts < 0
-      int64_t t0 = (int64_t)((uint64_t)ts[r] - (uint64_t)p.size + (uint64_t)p.adv);
-      if (t0 < 0) t0 = 0;
-      k_lo = udiv(p.div, (uint64_t)t0);
-      k_hi = udiv(p.div, (uint64_t)ts[r]);
-    }
+    if (!record_windows(p, ts[r], k_lo, k_hi)) continue;
+    const uint64_t seq1 = (seq ? (uint64_t)seq[i] : p.rec_base + i) + 1;
     for (uint64_t k = k_lo; k <= k_hi; ++k) {
-      if (!unwin) {
-        int64_t ws = (int64_t)(k * (uint64_t)p.adv);
-        int64_t we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
-        if (!(wm[r] < (int64_t)((uint64_t)we + (uint64_t)p.grace))) { late += 1; continue; }
-      }
+      if (!window_accepted(p, k, wm[r])) { late += 1; continue; }
       int64_t krel = (int64_t)k - k_epoch;
       if (krel < 0 || krel > 0xFFFFFFFFll) { err |= ERR_RANGE; continue; }
       uint64_t g = ((uint64_t)key[r] << 32) | (uint64_t)krel;
-      int64_t slot = tw_find_or_insert(t, g, fresh);
-      if (slot < 0) { err |= ERR_OOM; continue; }
-      apply_slots(prog, t.aggs + (uint64_t)slot * prog.n_slots, b, i, p.rec_base + i + 1);
-      t.stamp[slot] = (uint32_t)p.batch_id;
-      pairs += 1;
+      if (PASS == 0) {
+        int64_t slot = tw_find_or_insert(t, g, fresh);
+        if (slot < 0) { err |= ERR_OOM; continue; }
+        apply_slots(prog, t.aggs + (uint64_t)slot * prog.n_slots, b, i, seq1);
+        t.stamp[slot] = (uint32_t)p.batch_id;
+        pairs += 1;
+      } else {
+        int64_t slot = tw_find(t, g);
+        if (slot >= 0) apply_last(prog, t.aggs + (uint64_t)slot * prog.n_slots, b, i, seq1);
+      }
     }
   }
+  if (PASS != 0) return;
 
   // 3) per-workgroup counters
   pairs = wave_sum_u64(pairs);
   late = wave_sum_u64(late);
   uint64_t fr = wave_sum_u64(fresh);
-  uint64_t anyerr = __ballot(err != 0);
   if (lane == 0) { sred[0][w] = pairs; sred[1][w] = late; sred[2][w] = fr; }
-  if (anyerr && err) atomicOr(&sc->err, err);
+  if (err) atomicOr(&sc->err, err);
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t a = 0, l = 0, f = 0;
@@ -335,35 +250,24 @@ __global__ __launch_bounds__(kTileThreads) void k_tw_agg(Batch b, TwParams p, Tw
 }
 
 void launch_tw_agg(hipStream_t s, const Batch &b, const TwParams &p, const TwTable &t, const Program &prog,
-                   const int64_t *tile_prefix, DevScalars *sc) {
+                   const int64_t *tile_prefix, const int64_t *rec_wm, const int64_t *seq, DevScalars *sc,
+                   bool last_pass) {
   uint64_t tiles = (b.n + kTileRecords - 1) / kTileRecords;
-  if (tiles) hipLaunchKernelGGL(k_tw_agg, dim3((unsigned)tiles), dim3(kTileThreads), 0, s, b, p, t, prog, tile_prefix, sc);
+  if (!tiles) return;
+  if (last_pass)
+    hipLaunchKernelGGL(k_tw_agg<1>, dim3((unsigned)tiles), dim3(kTileThreads), 0, s, b, p, t, prog, tile_prefix,
+                       rec_wm, seq, sc);
+  else
+    hipLaunchKernelGGL(k_tw_agg<0>, dim3((unsigned)tiles), dim3(kTileThreads), 0, s, b, p, t, prog, tile_prefix,
+                       rec_wm, seq, sc);
 }
 
 // ---------------------------------------------------------------------------
-// row emission: mode 0 = groups touched by this batch (per-batch changelog and
-// LAST fix-up), mode 1 = every live group (ksDump), mode 2 = LAST fix-up only
+// row emission: mode 0 = groups touched by this batch (per-batch changelog),
+// mode 1 = every live group (ksDump)
 // ---------------------------------------------------------------------------
-__device__ inline int64_t out_value(const Program &prog, int j, const int64_t *row) {
-  const int64_t a = row[prog.out_a[j]];
-  switch (prog.out_kind[j]) {
-    case O_F64_ORD: return __builtin_bit_cast(int64_t, f64_unord((uint64_t)a));
-    case O_AVG_I: {
-      int64_t c = row[prog.out_b[j]];
-      double d = c ? (double)a / (double)c : __builtin_nan("");
-      return __builtin_bit_cast(int64_t, d);
-    }
-    case O_AVG_F: {
-      int64_t c = row[prog.out_b[j]];
-      double d = c ? __builtin_bit_cast(double, a) / (double)c : __builtin_nan("");
-      return __builtin_bit_cast(int64_t, d);
-    }
-    default: return a;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_tw_scan_emit(TwTable t, uint64_t cap, Program prog, TwParams p, Batch b,
-                                                      int mode, OutCols out, uint64_t out_base, uint64_t out_cap,
+__global__ __launch_bounds__(256) void k_tw_scan_emit(TwTable t, uint64_t cap, Program prog, TwParams p, int mode,
+                                                      OutCols out, uint64_t out_base, uint64_t out_cap,
                                                       DevScalars *sc, uint64_t *counter) {
   __shared__ uint64_t swave[4];
   __shared__ uint64_t sbase;
@@ -379,17 +283,7 @@ __global__ __launch_bounds__(256) void k_tw_scan_emit(TwTable t, uint64_t cap, P
       if (mode == 1) hit = g != kEmpty;
       else hit = g != kEmpty && t.stamp[s] == (uint32_t)p.batch_id;
     }
-    int64_t *row = t.aggs + s * (uint64_t)prog.n_slots;
-    if (hit && mode != 1) {
-      // LAST fix-up: the record that won LAST_SEQ belongs to this batch
-      for (int q = 0; q < prog.n_slots; ++q) {
-        if (prog.slot_op[q] != S_LAST_SEQ) continue;
-        uint64_t seq1 = (uint64_t)row[q];
-        if (seq1 > p.rec_base && seq1 - 1 - p.rec_base < b.n)
-          row[q + 1] = b.col[prog.slot_col[q]][seq1 - 1 - p.rec_base];
-      }
-    }
-    if (mode == 2) continue;
+    const int64_t *row = t.aggs + s * (uint64_t)prog.n_slots;
     uint64_t f = hit ? 1 : 0;
     uint64_t incl = wave_incl_sum(f);
     if (lane == 63) swave[w] = incl;
@@ -424,11 +318,11 @@ __global__ __launch_bounds__(256) void k_tw_scan_emit(TwTable t, uint64_t cap, P
 }
 
 void launch_tw_scan_emit(hipStream_t s, const TwTable &t, uint64_t cap, const Program &prog, const TwParams &p,
-                         const Batch &b, int mode, OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc,
+                         int mode, OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc,
                          uint64_t *counter) {
   uint64_t blocks = (cap + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(k_tw_scan_emit, dim3((unsigned)blocks), dim3(256), 0, s, t, cap, prog, p, b, mode, out, out_base,
+  hipLaunchKernelGGL(k_tw_scan_emit, dim3((unsigned)blocks), dim3(256), 0, s, t, cap, prog, p, mode, out, out_base,
                      out_cap, sc, counter);
 }
 

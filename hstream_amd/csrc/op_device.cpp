@@ -8,6 +8,8 @@
 #include "hsg_internal.h"
 #include "hsg_ops.h"
 #include "hsg_kernels.h"
+#include "hsg_session.h"
+#include "hsg_sort.h"
 
 namespace hsg {
 
@@ -64,7 +66,7 @@ static void free_out(OutCols &o) {
 int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err) {
   DTRY(hipMemsetAsync(d.sc, 0, sizeof(DevScalars), d.stream));
   if (cfg.window_kind == HSG_SESSION) {
-    launch_fill_u32(d.stream, d.ss.keys, d.cap, 0xFFFFFFFFu);
+    launch_ss_reset(d.stream, d.ss, d.cap);
     DTRY(hipMemsetAsync(d.arena_top, 0, sizeof(uint64_t), d.stream));
   } else {
     launch_fill_u64(d.stream, d.tw.keys, d.cap, kEmpty);
@@ -175,6 +177,8 @@ void op_device_free(OpDevice &d) {
   d.xsend = d.xrecv = nullptr;
   dfree(d.d_counts);
   if (d.h_counts) hipHostFree(d.h_counts);
+  if (d.h_tmp) hipHostFree(d.h_tmp);
+  d.h_tmp = nullptr;
   d.h_counts = nullptr;
   if (d.ev_a) hipEventDestroy(d.ev_a);
   if (d.ev_b) hipEventDestroy(d.ev_b);
@@ -279,18 +283,21 @@ int finish_batch(OpDevice &d, int64_t wm_in, uint64_t n, PushResult &r, std::str
 }
 
 static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
-                            const Batch &kb, PushResult &r, std::string &err) {
+                            const Batch &kb, const int64_t *seq, const int64_t *rec_wm, PushResult &r,
+                            std::string &err) {
   TwParams p = make_tw_params(cfg, a);
   int rc = clear_batch_scalars(d, err);
   if (rc != HSG_OK) return rc;
   if (kb.n) {
+    // stream time (and the window epoch on the first batch); after a key exchange
+    // the per-record stream time arrives in rec_wm and only the epoch is used
     launch_stream_time(d, cfg, kb, a.wm_in, p.adv);
     DTRY(hipEventRecord(d.ev_a, d.stream));
-    launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, d.sc);
+    launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, false);
     DTRY(hipEventRecord(d.ev_b, d.stream));
-    int mode = cfg.emit_mode == HSG_EMIT_PER_BATCH ? 0 : (has_last(prog) ? 2 : -1);
-    if (mode >= 0)
-      launch_tw_scan_emit(d.stream, d.tw, d.cap, prog, p, kb, mode, d.out, a.pending, d.out_cap, d.sc,
+    if (has_last(prog)) launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, true);
+    if (cfg.emit_mode == HSG_EMIT_PER_BATCH)
+      launch_tw_scan_emit(d.stream, d.tw, d.cap, prog, p, 0, d.out, a.pending, d.out_cap, d.sc,
                           (uint64_t *)&d.sc->out_rows);
     DTRY(hipGetLastError());
   }
@@ -332,8 +339,7 @@ int push_local(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const
                const int64_t *seq, const int64_t *rec_wm, PushResult &r, std::string &err) {
   if (cfg.window_kind == HSG_SESSION) return push_session(d, cfg, prog, a, kb, seq, r, err);
   if (cfg.emit_mode == HSG_EMIT_PER_RECORD) return push_time_perrecord(d, cfg, prog, a, kb, seq, rec_wm, r, err);
-  if (seq || rec_wm) return push_time_atomic_sharded(d, cfg, prog, a, kb, seq, rec_wm, r, err);
-  return push_time_atomic(d, cfg, prog, a, kb, r, err);
+  return push_time_atomic(d, cfg, prog, a, kb, seq, rec_wm, r, err);
 }
 
 int op_copy_rows(OpDevice &d, const OutCols &src, uint64_t from, uint64_t n, int n_aggs, const hsg_rows *out,
@@ -373,9 +379,7 @@ int op_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hs
     } else {
       PushArgs a;
       TwParams p = make_tw_params(cfg, a);
-      Batch none;
-      memset(&none, 0, sizeof(none));
-      launch_tw_scan_emit(d.stream, d.tw, d.cap, prog, p, none, 1, tmp, 0, live, d.sc, counter);
+      launch_tw_scan_emit(d.stream, d.tw, d.cap, prog, p, 1, tmp, 0, live, d.sc, counter);
     }
     uint64_t got = 0;
     hipMemcpyAsync(&got, counter, 8, hipMemcpyDeviceToHost, d.stream);

@@ -202,6 +202,8 @@ int  hsg_state_rows(hsg_op *op, uint64_t *n);
 /* Copy every live state row (views). Same capacity rule as hsg_drain. */
 int  hsg_dump_state(hsg_op *op, hsg_rows *out, uint64_t *n_out);
 
+/* Counters are cumulative since hsg_op_create (hsg_op_reset keeps them);
+ * "last batch" fields describe the most recent hsg_push_batch. */
 int  hsg_op_stats(const hsg_op *op, hsg_stats *out);
 
 #ifdef __cplusplus
