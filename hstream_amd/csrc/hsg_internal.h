@@ -181,10 +181,18 @@ void launch_tile_scan(hipStream_t s, const int64_t *tile_max, const int64_t *til
 void launch_tw_agg(hipStream_t s, const Batch &b, const TwParams &p, const TwTable &t, const Program &prog,
                    const int64_t *tile_prefix, const int64_t *rec_wm, const int64_t *seq, DevScalars *sc,
                    bool last_pass);
-// scan the table: emit rows whose stamp == batch_id (mode 0) or every live row (mode 1)
-void launch_tw_scan_emit(hipStream_t s, const TwTable &t, uint64_t cap, const Program &prog, const TwParams &p,
-                         int mode, OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc,
-                         uint64_t *counter);
+// emit rows whose stamp == batch_id (mode 0) or every live row (mode 1) in slot
+// order; *total (device) receives the row count
+constexpr uint64_t kEmitChunk = 4096;
+struct EmitScratch {
+  uint32_t *cnt;     // [emit_chunks(cap)]
+  uint64_t *off;     // [emit_chunks(cap)]
+  uint64_t *partial; // scan partials
+};
+uint64_t emit_chunks(uint64_t cap);
+void launch_tw_emit(hipStream_t s, const TwTable &t, uint64_t cap, const Program &prog, const TwParams &p, int mode,
+                    OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc, const EmitScratch &es,
+                    uint64_t *total);
 unsigned grid_for(uint64_t n, unsigned tpb);
 
 constexpr int kTileThreads = 256;

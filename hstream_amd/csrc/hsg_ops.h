@@ -49,6 +49,7 @@ struct OpDevice {
   // time windows
   TwTable tw = {};
   uint64_t cap = 0;             // table slots
+  EmitScratch emit = {};
   // sessions
   SessTable ss = {};
   uint64_t *arena_top = nullptr;  // device bump pointer

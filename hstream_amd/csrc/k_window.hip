@@ -13,6 +13,7 @@
 // order gives the reference's final state; the exact per-record changelog is
 // produced by the sort-based path in k_perrecord.hip.
 #include "hsg_dev.h"
+#include "hsg_sort.h"
 #include "hsg_tw.h"
 
 namespace hsg {
@@ -264,66 +265,80 @@ void launch_tw_agg(hipStream_t s, const Batch &b, const TwParams &p, const TwTab
 
 // ---------------------------------------------------------------------------
 // row emission: mode 0 = groups touched by this batch (per-batch changelog),
-// mode 1 = every live group (ksDump)
+// mode 1 = every live group (ksDump). Deterministic: per-chunk counts, an
+// exclusive scan, then rows written in slot order (no shared counter).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_tw_scan_emit(TwTable t, uint64_t cap, Program prog, TwParams p, int mode,
-                                                      OutCols out, uint64_t out_base, uint64_t out_cap,
-                                                      DevScalars *sc, uint64_t *counter) {
+__device__ inline bool tw_hit(const TwTable &t, uint64_t s, uint64_t cap, int mode, uint32_t batch_id) {
+  if (s >= cap) return false;
+  uint64_t g = t.keys[s];
+  if (g == kEmpty) return false;
+  return mode == 1 || t.stamp[s] == batch_id;
+}
+
+__global__ __launch_bounds__(256) void k_tw_emit_count(TwTable t, uint64_t cap, int mode, uint32_t batch_id,
+                                                       uint32_t *cnt) {
+  __shared__ uint64_t sw[4];
+  const uint64_t c0 = (uint64_t)blockIdx.x * kEmitChunk;
+  uint64_t h = 0;
+  for (uint64_t s = c0 + threadIdx.x; s < c0 + kEmitChunk; s += 256) h += tw_hit(t, s, cap, mode, batch_id);
+  h = wave_sum_u64(h);
+  if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = (uint32_t)(sw[0] + sw[1] + sw[2] + sw[3]);
+}
+
+__global__ __launch_bounds__(256) void k_tw_emit_rows(TwTable t, uint64_t cap, Program prog, TwParams p, int mode,
+                                                      const uint64_t *off, OutCols out, uint64_t out_base,
+                                                      uint64_t out_cap, DevScalars *sc) {
   __shared__ uint64_t swave[4];
-  __shared__ uint64_t sbase;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t k_epoch = sc->k_epoch;
   const bool unwin = p.kind == HSG_UNWINDOWED;
-  for (uint64_t blk = blockIdx.x * 256ull; blk < cap; blk += (uint64_t)gridDim.x * 256ull) {
+  const uint64_t c0 = (uint64_t)blockIdx.x * kEmitChunk;
+  uint64_t run = off[blockIdx.x];
+  for (uint64_t blk = c0; blk < c0 + kEmitChunk; blk += 256) {
     const uint64_t s = blk + threadIdx.x;
-    bool hit = false;
-    uint64_t g = kEmpty;
-    if (s < cap) {
-      g = t.keys[s];
-      if (mode == 1) hit = g != kEmpty;
-      else hit = g != kEmpty && t.stamp[s] == (uint32_t)p.batch_id;
-    }
-    const int64_t *row = t.aggs + s * (uint64_t)prog.n_slots;
+    const bool hit = tw_hit(t, s, cap, mode, (uint32_t)p.batch_id);
     uint64_t f = hit ? 1 : 0;
     uint64_t incl = wave_incl_sum(f);
     if (lane == 63) swave[w] = incl;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      uint64_t tot = swave[0] + swave[1] + swave[2] + swave[3];
-      sbase = tot ? atomicAdd((unsigned long long *)counter, (unsigned long long)tot) : 0;
-    }
+    uint64_t o = run + incl - f;
+    for (int k = 0; k < w; ++k) o += swave[k];
+    run += swave[0] + swave[1] + swave[2] + swave[3];
     __syncthreads();
-    uint64_t off = sbase + incl - f;
-    for (int k = 0; k < w; ++k) off += swave[k];
-    if (hit) {
-      uint64_t o = out_base + off;
-      if (o < out_cap) {
-        out.key[o] = (uint32_t)(g >> 32);
-        int64_t ws = 0, we = 0;
-        if (!unwin) {
-          int64_t k = k_epoch + (int64_t)(g & 0xFFFFFFFFull);
-          ws = (int64_t)((uint64_t)k * (uint64_t)p.adv);
-          we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
-        }
-        out.ws[o] = ws;
-        out.we[o] = we;
-        out.src[o] = -1;
-        for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, row);
-      } else {
-        atomicOr(&sc->err, ERR_OOM);
-      }
+    if (!hit) continue;
+    o += out_base;
+    if (o >= out_cap) {
+      atomicOr(&sc->err, ERR_OOM);
+      continue;
     }
-    __syncthreads();
+    const uint64_t g = t.keys[s];
+    const int64_t *row = t.aggs + s * (uint64_t)prog.n_slots;
+    out.key[o] = (uint32_t)(g >> 32);
+    int64_t ws = 0, we = 0;
+    if (!unwin) {
+      int64_t k = k_epoch + (int64_t)(g & 0xFFFFFFFFull);
+      ws = (int64_t)((uint64_t)k * (uint64_t)p.adv);
+      we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
+    }
+    out.ws[o] = ws;
+    out.we[o] = we;
+    out.src[o] = -1;
+    for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, row);
   }
 }
 
-void launch_tw_scan_emit(hipStream_t s, const TwTable &t, uint64_t cap, const Program &prog, const TwParams &p,
-                         int mode, OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc,
-                         uint64_t *counter) {
-  uint64_t blocks = (cap + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(k_tw_scan_emit, dim3((unsigned)blocks), dim3(256), 0, s, t, cap, prog, p, mode, out, out_base,
-                     out_cap, sc, counter);
+uint64_t emit_chunks(uint64_t cap) { return (cap + kEmitChunk - 1) / kEmitChunk; }
+
+void launch_tw_emit(hipStream_t s, const TwTable &t, uint64_t cap, const Program &prog, const TwParams &p, int mode,
+                    OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc, const EmitScratch &es,
+                    uint64_t *total) {
+  uint64_t nb = emit_chunks(cap);
+  hipLaunchKernelGGL(k_tw_emit_count, dim3((unsigned)nb), dim3(256), 0, s, t, cap, mode, (uint32_t)p.batch_id, es.cnt);
+  scan_excl_u32(s, es.cnt, es.off, nb, es.partial, total);
+  hipLaunchKernelGGL(k_tw_emit_rows, dim3((unsigned)nb), dim3(256), 0, s, t, cap, prog, p, mode, es.off, out, out_base,
+                     out_cap, sc);
 }
 
 }  // namespace hsg

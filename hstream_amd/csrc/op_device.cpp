@@ -120,6 +120,10 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
     DTRY(dalloc(&d.tw.aggs, d.cap * (uint64_t)prog.n_slots));
     DTRY(dalloc(&d.tw.stamp, d.cap));
     d.tw.mask = d.cap - 1;
+    uint64_t nb = emit_chunks(d.cap);
+    DTRY(dalloc(&d.emit.cnt, nb));
+    DTRY(dalloc(&d.emit.off, nb));
+    DTRY(dalloc(&d.emit.partial, scan_partials_needed(nb) + 8));
   }
   // changelog capacity
   uint64_t oc = cfg.out_capacity;
@@ -160,6 +164,9 @@ void op_device_free(OpDevice &d) {
   dfree(d.tw.keys);
   dfree(d.tw.aggs);
   dfree(d.tw.stamp);
+  dfree(d.emit.cnt);
+  dfree(d.emit.off);
+  dfree(d.emit.partial);
   dfree(d.ss.keys);
   dfree(d.ss.list_off);
   dfree(d.ss.list_len);
@@ -297,8 +304,8 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     DTRY(hipEventRecord(d.ev_b, d.stream));
     if (has_last(prog)) launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, true);
     if (cfg.emit_mode == HSG_EMIT_PER_BATCH)
-      launch_tw_scan_emit(d.stream, d.tw, d.cap, prog, p, 0, d.out, a.pending, d.out_cap, d.sc,
-                          (uint64_t *)&d.sc->out_rows);
+      launch_tw_emit(d.stream, d.tw, d.cap, prog, p, 0, d.out, a.pending, d.out_cap, d.sc, d.emit,
+                     (uint64_t *)&d.sc->out_rows);
     DTRY(hipGetLastError());
   }
   rc = finish_batch(d, a.wm_in, kb.n, r, err);
@@ -379,7 +386,7 @@ int op_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hs
     } else {
       PushArgs a;
       TwParams p = make_tw_params(cfg, a);
-      launch_tw_scan_emit(d.stream, d.tw, d.cap, prog, p, 1, tmp, 0, live, d.sc, counter);
+      launch_tw_emit(d.stream, d.tw, d.cap, prog, p, 1, tmp, 0, live, d.sc, d.emit, counter);
     }
     uint64_t got = 0;
     hipMemcpyAsync(&got, counter, 8, hipMemcpyDeviceToHost, d.stream);
