@@ -1,18 +1,11 @@
 // RCCL communicator owned by the engine (one per process and GPU).
-#include <rccl/rccl.h>
-
 #include <cstring>
 #include <string>
 
+#include "hsg_exchange.h"
 #include "hsg_kernels.h"
 
 namespace hsg {
-
-struct Comm {
-  ncclComm_t comm = nullptr;
-  int rank = 0;
-  int nranks = 1;
-};
 
 static_assert(sizeof(ncclUniqueId) <= HSG_COMM_ID_BYTES, "ncclUniqueId larger than HSG_COMM_ID_BYTES");
 
@@ -25,6 +18,10 @@ int comm_unique_id(uint8_t *out) {
 }
 
 int comm_create(const uint8_t *id_bytes, int rank, int nranks, int device, Comm **out, std::string &err) {
+  if (nranks > kMaxRanks) {
+    err = "too many ranks";
+    return HSG_E_INVALID;
+  }
   ncclUniqueId id;
   memcpy(&id, id_bytes, sizeof(id));
   Comm *c = new Comm();

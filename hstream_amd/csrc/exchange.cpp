@@ -1,0 +1,220 @@
+// Multi-GPU key exchange over RCCL (xGMI on an MI355X node).
+//
+// Every rank ingests its own slice of each global batch; slices are ordered by
+// rank in the global arrival order. Per batch:
+//   1. local: tile maxima of ts, owner = hash(key) mod G, stable partition
+//   2. one ncclAllGather of [max ts, min ts, n, has_valid, counts[G]] per rank
+//      -> global watermark, each rank's stream-time carry and sequence base,
+//      the all-to-all-v sizes, and whether any record can be late at all
+//   3. (only if some record can be late) per-record stream time in global order
+//   4. pack -> ncclAllToAllv -> unpack: each rank now holds, in global arrival
+//      order, every record whose key it owns
+//   5. the single-GPU path aggregates them with their global sequence numbers
+//      (and stream times), so results equal one GPU fed the whole batch.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "hsg_exchange.h"
+#include "hsg_kernels.h"
+#include "hsg_sort.h"
+
+namespace hsg {
+
+#define DTRY(expr)                                                          \
+  do {                                                                      \
+    hipError_t _e = (expr);                                                 \
+    if (_e != hipSuccess) {                                                 \
+      err = std::string(#expr) + ": " + hipGetErrorString(_e);              \
+      return _e == hipErrorOutOfMemory ? HSG_E_OOM : HSG_E_DEVICE;          \
+    }                                                                       \
+  } while (0)
+
+#define NTRY(expr)                                                          \
+  do {                                                                      \
+    ncclResult_t _r = (expr);                                               \
+    if (_r != ncclSuccess) {                                                \
+      err = std::string(#expr) + ": " + ncclGetErrorString(_r);             \
+      return HSG_E_COMM;                                                    \
+    }                                                                       \
+  } while (0)
+
+static int info_words(int G) { return 4 + G; }
+
+static XLayout layout_for(const hsg_op_config &cfg, bool has_seq, bool has_wm, bool has_valid) {
+  XLayout L;
+  L.ncols = cfg.n_cols;
+  L.has_seq = has_seq;
+  L.has_wm = has_wm;
+  L.has_valid = has_valid;
+  L.words = 2 + cfg.n_cols + (has_seq ? 1 : 0) + (has_wm ? 1 : 0);
+  return L;
+}
+
+int exchange_device_init(OpDevice &d, const hsg_op_config &cfg, uint64_t batch_cap, std::string &err) {
+  XBuffers *x = new XBuffers();
+  memset(x, 0, sizeof(*x));
+  d.x = x;
+  const int G = d.nranks;
+  const uint64_t n = batch_cap;
+  const uint64_t max_words = 2 + cfg.n_cols + 2;
+  x->batch = n;
+  DTRY(hipMalloc((void **)&x->owner, n * 4 + 4));
+  DTRY(hipMalloc((void **)&x->idx, n * 4 + 4));
+  DTRY(hipMalloc((void **)&x->k1, n * 4 + 4));
+  DTRY(hipMalloc((void **)&x->v1, n * 4 + 4));
+  DTRY(hipMalloc(&x->sort_scratch, sort_scratch_bytes(n)));
+  DTRY(hipMalloc((void **)&x->hist, (kMaxRanks + 1) * 8));
+  DTRY(hipMalloc((void **)&x->info, info_words(G) * 8));
+  DTRY(hipMalloc((void **)&x->info_all, (uint64_t)G * info_words(G) * 8));
+  DTRY(hipHostMalloc((void **)&x->h_info, (uint64_t)G * info_words(G) * 8, hipHostMallocDefault));
+  DTRY(hipMalloc((void **)&x->wm_local, n * 8 + 8));
+  DTRY(hipMalloc((void **)&x->send, n * max_words * 8 + 8));
+  DTRY(hipMalloc((void **)&x->recv, (uint64_t)G * n * max_words * 8 + 8));
+  DTRY(hipMalloc((void **)&d.st_seq, (uint64_t)G * n * 8 + 8));
+  DTRY(hipMalloc((void **)&d.st_wm, (uint64_t)G * n * 8 + 8));
+  if (!d.h_tmp) DTRY(hipHostMalloc((void **)&d.h_tmp, 8 * sizeof(uint64_t), hipHostMallocDefault));
+  return HSG_OK;
+}
+
+void exchange_device_free(OpDevice &d) {
+  XBuffers *x = d.x;
+  if (!x) return;
+  hipFree(x->owner);
+  hipFree(x->idx);
+  hipFree(x->k1);
+  hipFree(x->v1);
+  hipFree(x->sort_scratch);
+  hipFree(x->hist);
+  hipFree(x->info);
+  hipFree(x->info_all);
+  hipHostFree(x->h_info);
+  hipFree(x->wm_local);
+  hipFree(x->send);
+  hipFree(x->recv);
+  delete x;
+  d.x = nullptr;
+}
+
+int push_sharded(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, PushResult &r,
+                 std::string &err) {
+  XBuffers &x = *d.x;
+  const int G = a.nranks, me = a.rank;
+  const int IW = info_words(G);
+  ncclComm_t comm = a.comm->comm;
+  hipStream_t s = d.stream;
+  if (a.batch->n > x.batch) {
+    err = "batch larger than batch_capacity";
+    return HSG_E_CAPACITY;
+  }
+  // 1. stage this rank's slice and compute local facts
+  Batch kb;
+  int rc = stage_batch(d, a.batch, kb, err);
+  if (rc != HSG_OK) return rc;
+  bool has_valid = false;
+  for (int c = 0; c < cfg.n_cols; ++c) has_valid = has_valid || kb.valid[c] != nullptr;
+  const uint64_t n = kb.n;
+  const uint64_t tiles = (n + kTileRecords - 1) / kTileRecords;
+  DTRY(hipEventRecord(d.ev_c, s));
+  launch_tile_stats(s, kb, d.tile_max, d.tile_min, tiles);
+  launch_x_minmax(s, d.tile_max, d.tile_min, tiles, n, has_valid ? 1 : 0, x.info);
+  DTRY(hipMemsetAsync(x.hist, 0, (kMaxRanks + 1) * 8, s));
+  launch_x_owner(s, kb, (uint32_t)G, x.owner, x.idx, x.hist);
+  DTRY(hipMemcpyAsync(x.info + 4, x.hist, (uint64_t)G * 8, hipMemcpyDeviceToDevice, s));
+  // stable partition by owner: one 8-bit radix pass of (owner, record index)
+  int which = radix_sort_pairs(s, x.owner, x.idx, x.k1, x.v1, n, 8, x.sort_scratch);
+  const uint32_t *sidx = which ? x.v1 : x.idx;
+  // 2. all-gather the per-rank facts
+  NTRY(ncclAllGather(x.info, x.info_all, IW, ncclInt64, comm, s));
+  DTRY(hipMemcpyAsync(x.h_info, x.info_all, (uint64_t)G * IW * 8, hipMemcpyDeviceToHost, s));
+  DTRY(hipStreamSynchronize(s));
+  const int64_t *H = x.h_info;
+  int64_t wm_global = a.wm_in, carry = a.wm_in, min_ts = INT64_MAX;
+  uint64_t seq_base = a.rec_base, total = 0;
+  bool any_valid = false;
+  for (int q = 0; q < G; ++q) {
+    const int64_t *I = H + (uint64_t)q * IW;
+    if (I[2] > 0) {
+      wm_global = I[0] > wm_global ? I[0] : wm_global;
+      if (q < me) carry = I[0] > carry ? I[0] : carry;
+      min_ts = I[1] < min_ts ? I[1] : min_ts;
+    }
+    if (q < me) seq_base += (uint64_t)I[2];
+    total += (uint64_t)I[2];
+    any_valid = any_valid || I[3] != 0;
+  }
+  // can any (record, window) be rejected by grace? every window of a record at
+  // ts t ends after t, so none is when stream time never exceeds t + grace
+  const bool time_win = cfg.window_kind == HSG_TUMBLING || cfg.window_kind == HSG_HOPPING;
+  const bool may_be_late =
+      time_win && min_ts != INT64_MAX && wm_global > (int64_t)((uint64_t)min_ts + (uint64_t)cfg.grace_ms);
+  const bool need_seq = cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.window_kind == HSG_SESSION ||
+                        [&] {
+                          for (int q = 0; q < prog.n_slots; ++q)
+                            if (prog.slot_op[q] == S_LAST_SEQ) return true;
+                          return false;
+                        }();
+  XLayout L = layout_for(cfg, need_seq, may_be_late, any_valid);
+  // 3. per-record stream time in the global order (rare)
+  if (may_be_late) {
+    launch_tile_scan(s, d.tile_max, d.tile_min, d.tile_prefix, tiles, carry, 1, false, d.sc);
+    launch_x_recwm(s, kb, d.tile_prefix, x.wm_local);
+  }
+  // 4. exchange
+  std::vector<size_t> scount(G), sdispl(G), rcount(G), rdispl(G);
+  uint64_t so = 0, ro = 0;
+  for (int q = 0; q < G; ++q) {
+    scount[q] = (size_t)H[(uint64_t)me * IW + 4 + q] * L.words;
+    sdispl[q] = so;
+    so += scount[q];
+    rcount[q] = (size_t)H[(uint64_t)q * IW + 4 + me] * L.words;
+    rdispl[q] = ro;
+    ro += rcount[q];
+  }
+  const uint64_t m_send = so / L.words, m_recv = ro / L.words;
+  if (m_recv > d.batch_cap) {
+    err = "received more records than the op's capacity";
+    return HSG_E_CAPACITY;
+  }
+  launch_x_pack(s, kb, L, sidx, m_send, seq_base, x.wm_local, x.send);
+  NTRY(ncclAllToAllv(x.send, scount.data(), sdispl.data(), x.recv, rcount.data(), rdispl.data(), ncclUint64, comm,
+                     s));
+  XStaging st;
+  memset(&st, 0, sizeof(st));
+  // received records reuse the op's staging arrays (the local slice is packed already)
+  st.key = d.st_key;
+  st.ts = d.st_ts;
+  for (int c = 0; c < cfg.n_cols; ++c) {
+    st.col[c] = d.st_col[c];
+    st.valid[c] = d.st_valid[c];
+  }
+  st.seq = d.st_seq;
+  st.wm = d.st_wm;
+  launch_x_unpack(s, L, x.recv, m_recv, st);
+  DTRY(hipEventRecord(d.ev_d, s));
+  DTRY(hipGetLastError());
+  // 5. aggregate the owned records
+  Batch rb;
+  memset(&rb, 0, sizeof(rb));
+  rb.n = m_recv;
+  rb.key = d.st_key;
+  rb.ts = d.st_ts;
+  for (int c = 0; c < cfg.n_cols; ++c) {
+    rb.col[c] = d.st_col[c];
+    rb.valid[c] = any_valid ? d.st_valid[c] : nullptr;
+  }
+  PushArgs la = a;
+  la.wm_in = carry;  // any value <= the records' stream times keeps grace exact
+  rc = push_local(d, cfg, prog, la, rb, need_seq ? d.st_seq : nullptr, may_be_late ? d.st_wm : nullptr, r, err);
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, d.ev_c, d.ev_d) == hipSuccess) r.exchange_ms = ms;
+  r.exchange_bytes = (uint64_t)(so - scount[me]) * 8;
+  r.wm_out = wm_global;
+  r.owned = m_recv;
+  r.global_records = total;
+  return rc;
+}
+
+}  // namespace hsg

@@ -248,7 +248,8 @@ extern "C" int hsg_op_create(hsg_engine *eng, const hsg_op_config *cfg, hsg_op *
     rc = build_program(op->cfg, op->col_types, op->aggs, op->prog, eng->err);
     if (rc != HSG_OK) { delete op; return rc; }
     if (hipSetDevice(eng->device) != hipSuccess) { delete op; return HSG_E_DEVICE; }
-    rc = op_device_init(op->dev, op->cfg, op->prog, eng->batch_cap, eng->nranks, hsg_windows_per_record(op->cfg),
+    rc = op_device_init(op->dev, op->cfg, op->prog, eng->batch_cap, eng->nranks, eng->comm != nullptr,
+                        hsg_windows_per_record(op->cfg),
                         eng->err);
     if (rc != HSG_OK) {
       op_device_free(op->dev);

@@ -1,0 +1,57 @@
+// Multi-GPU key exchange (k_exchange.hip, exchange.cpp). Not part of the ABI.
+#pragma once
+
+#include <rccl/rccl.h>
+
+#include "hsg_internal.h"
+#include "hsg_ops.h"
+
+namespace hsg {
+
+constexpr int kMaxRanks = 64;
+
+struct Comm {
+  ncclComm_t comm = nullptr;
+  int rank = 0;
+  int nranks = 1;
+};
+
+struct XLayout {
+  int32_t words;     // 8-byte words per record
+  int32_t ncols;
+  int32_t has_seq;
+  int32_t has_wm;
+  int32_t has_valid;
+};
+
+struct XStaging {
+  uint32_t *key;
+  int64_t *ts;
+  int64_t *col[kMaxCols];
+  uint8_t *valid[kMaxCols];
+  int64_t *seq;
+  int64_t *wm;
+};
+
+struct XBuffers {
+  uint32_t *owner, *idx, *k1, *v1;  // [batch] partition sort
+  void *sort_scratch;
+  uint64_t *hist;                    // [kMaxRanks + 1]
+  int64_t *info;                     // [4 + kMaxRanks] this rank: max, min, n, has_valid, counts[G]
+  int64_t *info_all;                 // [G * (4 + kMaxRanks)]
+  int64_t *h_info;                   // pinned mirror of info_all
+  int64_t *wm_local;                 // [batch] per-record stream time before the exchange
+  uint64_t *send;                    // [batch * max words]
+  uint64_t *recv;                    // [G * batch * max words]
+  uint64_t batch;                    // per-rank push capacity
+};
+
+void launch_x_minmax(hipStream_t s, const int64_t *tmax, const int64_t *tmin, uint64_t n_tiles, uint64_t n,
+                     int has_valid, int64_t *info);
+void launch_x_owner(hipStream_t s, const Batch &b, uint32_t G, uint32_t *owner, uint32_t *idx, uint64_t *hist);
+void launch_x_recwm(hipStream_t s, const Batch &b, const int64_t *tprefix, int64_t *wm);
+void launch_x_pack(hipStream_t s, const Batch &b, const XLayout &L, const uint32_t *sidx, uint64_t m,
+                   uint64_t seq_base, const int64_t *wm, uint64_t *send);
+void launch_x_unpack(hipStream_t s, const XLayout &L, const uint64_t *recv, uint64_t m, const XStaging &st);
+
+}  // namespace hsg

@@ -32,6 +32,7 @@ void launch_session_dump(OpDevice &d, const hsg_op_config &cfg, const Program &p
 
 // multi-GPU key exchange (exchange.cpp / k_exchange.hip)
 int exchange_device_init(OpDevice &d, const hsg_op_config &cfg, uint64_t batch_cap, std::string &err);
+void exchange_device_free(OpDevice &d);
 int push_sharded(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, PushResult &r,
                  std::string &err);
 

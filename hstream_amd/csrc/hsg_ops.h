@@ -9,7 +9,8 @@
 
 namespace hsg {
 
-struct Comm;  // RCCL communicator wrapper (comm.cpp)
+struct Comm;      // RCCL communicator wrapper (hsg_exchange.h)
+struct XBuffers;  // exchange scratch (hsg_exchange.h)
 
 int comm_unique_id(uint8_t *out);
 int comm_create(const uint8_t *id, int rank, int nranks, int device, Comm **out, std::string &err);
@@ -66,6 +67,7 @@ struct OpDevice {
   uint64_t xbytes = 0;
   uint64_t *h_counts = nullptr;   // pinned [2 * nranks]
   uint64_t *h_tmp = nullptr;      // pinned [8] small host<->device scalars
+  XBuffers *x = nullptr;          // key exchange (engines with a communicator)
   uint64_t *d_counts = nullptr;
   int nranks = 1;
   int n_cols = 0;
@@ -98,7 +100,7 @@ struct PushResult {
   uint64_t exchange_bytes = 0;
 };
 
-int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t batch_cap, int nranks,
+int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t batch_cap, int nranks, bool sharded,
                    uint64_t wpr, std::string &err);
 void op_device_free(OpDevice &d);
 int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err);

@@ -86,7 +86,7 @@ int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, 
   return HSG_OK;
 }
 
-int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t batch_cap, int nranks,
+int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t batch_cap, int nranks, bool sharded,
                    uint64_t wpr, std::string &err) {
   d.nranks = nranks;
   d.n_cols = cfg.n_cols;
@@ -138,7 +138,7 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
     rc = perrecord_device_init(d, cfg, prog, err);
     if (rc != HSG_OK) return rc;
   }
-  if (nranks > 1) {
+  if (sharded) {
     rc = exchange_device_init(d, cfg, batch_cap, err);
     if (rc != HSG_OK) return rc;
   }
@@ -147,6 +147,7 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
 
 void op_device_free(OpDevice &d) {
   if (d.stream) hipStreamSynchronize(d.stream);
+  exchange_device_free(d);
   dfree(d.sc);
   if (d.h_sc) hipHostFree(d.h_sc);
   d.h_sc = nullptr;
@@ -330,7 +331,7 @@ int op_push(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const Pu
       return HSG_E_CAPACITY;
     }
   }
-  if (a.nranks > 1) return push_sharded(d, cfg, prog, a, r, err);
+  if (a.comm) return push_sharded(d, cfg, prog, a, r, err);
   Batch kb;
   int rc = stage_batch(d, b, kb, err);
   if (rc != HSG_OK) return rc;

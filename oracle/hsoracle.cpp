@@ -193,7 +193,7 @@ static void emit_row(Op &op, uint32_t key, int64_t ws, int64_t we, int64_t src, 
 }
 
 // ---- time-windowed and grouped aggregation ---------------------------------
-static int push_time(Op &op, const hsg_batch *b, int64_t *wm) {
+static int push_time(Op &op, const hsg_batch *b, int64_t *wm, const int64_t *rec_wm, const int64_t *seq) {
   const bool unwin = op.cfg.window_kind == HSG_UNWINDOWED;
   const int64_t size = op.cfg.size_ms;
   const int64_t adv = op.cfg.window_kind == HSG_TUMBLING ? op.cfg.size_ms : op.cfg.advance_ms;
@@ -210,7 +210,10 @@ static int push_time(Op &op, const hsg_batch *b, int64_t *wm) {
     uint32_t key = b->key_id[i];
     if (key == HSG_KEY_NONE) continue;
     RecView rv{b, i};
-    int64_t src = (int64_t)(op.records + i);
+    int64_t src = seq ? seq[i] : (int64_t)(op.records + i);
+    // sharded-protocol tests hand in the stream time each record saw in the
+    // global arrival order
+    const int64_t wr = rec_wm ? rec_wm[i] : w;
     if (unwin) {  // GroupedStream.aggregateProcessor (GroupedStream.hs:79-87)
       auto it = op.kv.find({0, key});
       if (it == op.kv.end()) it = op.kv.emplace(std::make_pair((int64_t)0, key), acc_init(op)).first;
@@ -227,7 +230,7 @@ static int push_time(Op &op, const hsg_batch *b, int64_t *wm) {
     windows_for(ts, size, adv, starts);  // TimeWindowedStream.hs:86
     for (int64_t ws : starts) {
       int64_t we = wadd(ws, size);
-      if (!(w < wadd(we, grace))) continue;  // :92, "Skipping record for expired window."
+      if (!(wr < wadd(we, grace))) continue;  // :92, "Skipping record for expired window."
       auto it = op.kv.find({ws, key});
       if (it == op.kv.end()) it = op.kv.emplace(std::make_pair(ws, key), acc_init(op)).first;
       acc_apply(op, it->second, rv);  // :96-100
@@ -290,7 +293,7 @@ static void find_sessions_fast(Op &op, uint32_t key, int64_t lo, int64_t hi, std
   for (auto r = rev.rbegin(); r != rev.rend(); ++r) out.push_back(*r);
 }
 
-static int push_session(Op &op, const hsg_batch *b, int64_t *wm) {
+static int push_session(Op &op, const hsg_batch *b, int64_t *wm, const int64_t *seq) {
   const int64_t gap = op.cfg.gap_ms;
   const int mode = op.cfg.emit_mode;
   std::set<std::tuple<uint32_t, int64_t, int64_t>> touched;  // (key, start, end)
@@ -319,7 +322,7 @@ static int push_session(Op &op, const hsg_batch *b, int64_t *wm) {
     if (op.faithful_sessions) op.ss[e][key][s] = acc;  // ssPut
     else op.ssf[key][s] = {e, acc};
     touched.insert({key, s, e});
-    if (mode == HSG_EMIT_PER_RECORD) emit_row(op, key, s, e, (int64_t)(op.records + i), acc);
+    if (mode == HSG_EMIT_PER_RECORD) emit_row(op, key, s, e, seq ? seq[i] : (int64_t)(op.records + i), acc);
   }
   if (mode == HSG_EMIT_PER_BATCH) {
     for (auto &t : touched) {
@@ -430,17 +433,21 @@ int hso_op_reset(hso_op *h) {
 
 const char *hso_last_error(const hso_op *h) { return ((const Op *)h)->err.c_str(); }
 
-int hso_push_batch(hso_op *h, const hsg_batch *b, int64_t *wm) {
+// rec_wm / seq (optional): per-record stream time and global sequence number,
+// used by the tests that restate the multi-GPU sharding protocol.
+int hso_push_batch_ex(hso_op *h, const hsg_batch *b, int64_t *wm, const int64_t *rec_wm, const int64_t *seq) {
   Op *op = (Op *)h;
   if (!b || !wm) { op->err = "null argument"; return HSG_E_INVALID; }
   if (b->mem != HSG_MEM_HOST) { op->err = "oracle takes host batches only"; return HSG_E_INVALID; }
   if (b->n_cols != (int32_t)op->col_types.size()) { op->err = "n_cols mismatch"; return HSG_E_INVALID; }
   if (b->n && (!b->key_id || !b->ts)) { op->err = "null key/ts"; return HSG_E_INVALID; }
-  int rc = op->cfg.window_kind == HSG_SESSION ? push_session(*op, b, wm) : push_time(*op, b, wm);
+  int rc = op->cfg.window_kind == HSG_SESSION ? push_session(*op, b, wm, seq) : push_time(*op, b, wm, rec_wm, seq);
   op->records += b->n;
   op->batches += 1;
   return rc;
 }
+
+int hso_push_batch(hso_op *h, const hsg_batch *b, int64_t *wm) { return hso_push_batch_ex(h, b, wm, nullptr, nullptr); }
 
 int hso_pending_rows(const hso_op *h, uint64_t *n) {
   const Op *op = (const Op *)h;

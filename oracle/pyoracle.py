@@ -8,6 +8,8 @@ import ctypes as C
 import os
 import subprocess
 
+import numpy as np
+
 from hstream_amd import abi
 from hstream_amd.columnar import OpHandle, OpSpec, declare_op_functions
 
@@ -35,6 +37,9 @@ def lib():
         L.hso_op_create_ex.restype = C.c_int
         L.hso_windows_for.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.POINTER(C.c_int64), C.c_int]
         L.hso_windows_for.restype = C.c_int
+        L.hso_push_batch_ex.argtypes = [C.c_void_p, C.POINTER(abi.hsg_batch), C.POINTER(C.c_int64), C.c_void_p,
+                                        C.c_void_p]
+        L.hso_push_batch_ex.restype = C.c_int
         _lib = L
     return _lib
 
@@ -48,6 +53,20 @@ class OracleOp(OpHandle):
         if rc != abi.HSG_OK:
             raise abi.HStreamGpuError(rc, "hso_op_create")
         super().__init__(L, "hso", h, spec)
+
+    def push_ex(self, key_id, ts, cols=(), valid=None, watermark=-1, rec_wm=None, seq=None):
+        """push with explicit per-record stream time / global sequence numbers."""
+        from hstream_amd.columnar import make_batch
+        b, keep = make_batch(key_id, ts, cols, valid)
+        rw = None if rec_wm is None else np.ascontiguousarray(rec_wm, dtype=np.int64)
+        sq = None if seq is None else np.ascontiguousarray(seq, dtype=np.int64)
+        wm = C.c_int64(watermark)
+        rc = self._lib.hso_push_batch_ex(self._h, C.byref(b), C.byref(wm),
+                                         None if rw is None else rw.ctypes.data,
+                                         None if sq is None else sq.ctypes.data)
+        del keep
+        self._check(rc, "push_batch_ex")
+        return wm.value
 
 
 def windows_for(ts, size, adv):

@@ -169,3 +169,53 @@ def test_window_span_limit_is_reported(eng):
     with pytest.raises(abi.HStreamGpuError) as ei:
         g.push(np.zeros(1, np.uint32), np.array([3 * 2**33], np.int64), [], None)
     assert ei.value.status == abi.HSG_E_RANGE
+
+
+# ---------------------------------------------------------------------------
+# the multi-GPU exchange path (owner partition, RCCL all-gather + all-to-all-v,
+# unpack, sequence numbers, stream-time carry) driven through a 1-rank
+# communicator: every record is exchanged with itself
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def xeng():
+    import torch
+    assert torch.cuda.is_available()
+    from hstream_amd.engine import Engine, comm_unique_id
+    e = Engine(device=0, rank=0, nranks=1, comm_id=comm_unique_id(), batch_capacity=1 << 20)
+    yield e
+    e.close()
+
+
+def _x_specs():
+    out = []
+    for kind, kw in ((abi.HSG_TUMBLING, dict(size_ms=10_000)), (abi.HSG_HOPPING, dict(size_ms=10_000, advance_ms=3_000)),
+                     (abi.HSG_UNWINDOWED, {}), (abi.HSG_SESSION, dict(gap_ms=2_000))):
+        aggs = [a for a in ALL_AGG_SETS["mixed"] if not (kind == abi.HSG_SESSION and a[0] == abi.HSG_LAST)]
+        for mode in (abi.HSG_EMIT_PER_BATCH, abi.HSG_EMIT_PER_RECORD, abi.HSG_EMIT_NONE):
+            out.append(pytest.param(OpSpec(kind, mode, col_types=[abi.HSG_I64, abi.HSG_F64], aggs=aggs, **kw),
+                                    id=f"k{kind}-m{mode}"))
+    return out
+
+
+@pytest.mark.parametrize("late", [False, True], ids=["no_late", "late"])
+@pytest.mark.parametrize("spec", _x_specs())
+def test_exchange_path_single_rank(xeng, spec, late):
+    batches = []
+    for bi in range(3):
+        key, ts, cols, valid = gen_small(2000 + bi, 4000, 29, col_types=spec.col_types, span=60_000,
+                                         base=5_000_000 + bi * 60_000, very_late=late)
+        batches.append((key, ts, cols, valid))
+    g = xeng.op(spec)
+    o = pyoracle.OracleOp(spec)
+    f64 = spec.agg_is_f64()
+    wg = wo = -1
+    for bi, (key, ts, cols, valid) in enumerate(batches):
+        wg = g.push(key, ts, cols, valid, watermark=wg)
+        wo = o.push(key, ts, cols, valid, watermark=wo)
+        assert wg == wo
+        if spec.emit_mode != abi.HSG_EMIT_NONE:
+            rows_equal(g.drain(), o.drain(), f64, ordered=spec.emit_mode == abi.HSG_EMIT_PER_RECORD,
+                       what=f"batch {bi}")
+    rows_equal(g.dump_state(), o.dump_state(), f64, what="state")
+    st = g.stats()
+    assert st["records_owned"] == sum(int((b[0] != abi.HSG_KEY_NONE).sum()) for b in batches)

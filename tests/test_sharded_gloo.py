@@ -1,0 +1,190 @@
+"""CPU, world_size 2 over gloo: the multi-GPU sharding protocol of
+hstream_amd/csrc/exchange.cpp restated with torch.distributed and checked
+against one oracle fed the whole batch.
+
+Protocol per global batch (rank r ingests slice r; slices are in rank order):
+  all-gather (max ts, min keyed ts, n) -> global watermark, stream-time carry
+  of rank r = max(wm_in, max ts of ranks < r), sequence base = sum of n of
+  ranks < r, and whether any record may be late (stream time > min ts + grace);
+  owner = hash(key) mod G; all-to-all of (key, ts, cols, valid, seq[, wm]);
+  each rank aggregates its owned records in global order.
+The per-rank aggregation here is the oracle, so this checks the protocol's
+claims (exact stream time and sequence numbers after the exchange, disjoint
+key ownership), not the GPU kernels (tests/test_gpu_parity.py does that)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from hstream_amd import abi
+from hstream_amd.columnar import OpSpec
+from util import ALL_AGG_SETS, gen_small
+
+M64 = (1 << 64) - 1
+
+
+def mix64(x):
+    x = np.asarray(x, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = x ^ (x >> np.uint64(33))
+        x = x * np.uint64(0xFF51AFD7ED558CCD)
+        x = x ^ (x >> np.uint64(33))
+        x = x * np.uint64(0xC4CEB9FE1A85EC53)
+        x = x ^ (x >> np.uint64(33))
+    return x
+
+
+def owner_of(key, G):
+    return (mix64(np.asarray(key, np.uint64) ^ np.uint64(0x5BD1E9955BD1E995)) % np.uint64(G)).astype(np.int64)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+SPECS = {
+    "hopping": OpSpec(abi.HSG_HOPPING, abi.HSG_EMIT_PER_RECORD, size_ms=10_000, advance_ms=3_000,
+                      col_types=[abi.HSG_I64, abi.HSG_F64], aggs=ALL_AGG_SETS["mixed"]),
+    "tumbling_batch": OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=10_000,
+                             col_types=[abi.HSG_I64, abi.HSG_F64], aggs=ALL_AGG_SETS["mixed"]),
+    "session": OpSpec(abi.HSG_SESSION, abi.HSG_EMIT_PER_RECORD, gap_ms=2_000, col_types=[abi.HSG_I64, abi.HSG_F64],
+                      aggs=[a for a in ALL_AGG_SETS["mixed"] if a[0] != abi.HSG_LAST]),
+}
+
+
+def _batches(G, late):
+    out = []
+    for bi in range(3):
+        slices = []
+        for r in range(G):
+            slices.append(gen_small(500 + 10 * bi + r, 1500, 23, col_types=(abi.HSG_I64, abi.HSG_F64),
+                                    span=30_000, base=2_000_000 + bi * 30_000 + r * 7_000, very_late=late))
+        out.append(slices)
+    return out
+
+
+def _worker(rank, G, port, spec_name, late, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=G)
+    import pyoracle
+    spec = SPECS[spec_name]
+    op = pyoracle.OracleOp(spec)
+    wm = -1
+    rec_base = 0
+    results = []
+    for slices in _batches(G, late):
+        key, ts, cols, valid = slices[rank]
+        keyed = key != abi.HSG_KEY_NONE
+        mn = int(ts[keyed & (ts >= 0)].min()) if (keyed & (ts >= 0)).any() else np.iinfo(np.int64).max
+        facts = torch.tensor([int(ts.max()) if len(ts) else np.iinfo(np.int64).min, mn, len(ts)], dtype=torch.int64)
+        allf = [torch.zeros(3, dtype=torch.int64) for _ in range(G)]
+        dist.all_gather(allf, facts)
+        allf = [f.tolist() for f in allf]
+        carry = max([wm] + [f[0] for q_, f in enumerate(allf) if q_ < rank and f[2] > 0])
+        wm_global = max([wm] + [f[0] for f in allf if f[2] > 0])
+        min_ts = min(f[1] for f in allf if f[2] > 0)
+        seq_base = rec_base + sum(f[2] for q_, f in enumerate(allf) if q_ < rank)
+        total = sum(f[2] for f in allf)
+        time_win = spec.window_kind in (abi.HSG_TUMBLING, abi.HSG_HOPPING)
+        may_be_late = time_win and wm_global > min_ts + spec.grace_ms
+        rec_wm = np.maximum.accumulate(np.concatenate([[carry], ts]))[1:]
+        seq = seq_base + np.arange(len(ts), dtype=np.int64)
+        own = np.where(keyed, owner_of(key, G), G)
+        # stable partition by owner, drop HSG_KEY_NONE
+        order = np.argsort(own, kind="stable")
+        order = order[own[order] < G]
+        counts = np.bincount(own[own < G], minlength=G)
+        rows = np.stack([key.astype(np.int64), ts, cols[0], cols[1].view(np.int64), valid[0].astype(np.int64),
+                         valid[1].astype(np.int64), seq, rec_wm], axis=1)[order]
+        send = torch.from_numpy(np.ascontiguousarray(rows)).reshape(-1)
+        cnt_t = torch.from_numpy(counts.astype(np.int64))
+        rcnt = torch.zeros(G, dtype=torch.int64)
+        dist.all_to_all_single(rcnt, cnt_t)
+        recv = torch.zeros(int(rcnt.sum()) * 8, dtype=torch.int64)
+        dist.all_to_all_single(recv, send, [int(c) * 8 for c in rcnt], [int(c) * 8 for c in counts])
+        got = recv.reshape(-1, 8).numpy()
+        r_key = got[:, 0].astype(np.uint32)
+        r_cols = [got[:, 2].copy(), got[:, 3].copy().view(np.float64)]
+        r_valid = [got[:, 4].astype(np.uint8), got[:, 5].astype(np.uint8)]
+        op.push_ex(r_key, got[:, 1].copy(), r_cols, r_valid, watermark=carry,
+                   rec_wm=got[:, 7].copy() if may_be_late else None, seq=got[:, 6].copy())
+        wm = wm_global
+        rec_base += total
+        rows_out = op.drain() if spec.emit_mode != abi.HSG_EMIT_NONE else None
+        results.append(None if rows_out is None else rows_out.tuples_with_src() if hasattr(rows_out, "tuples_with_src")
+                       else [(int(rows_out.key_id[i]), int(rows_out.win_start[i]), int(rows_out.win_end[i]),
+                              int(rows_out.src_index[i]), tuple(a[i].item() for a in rows_out.aggs))
+                             for i in range(len(rows_out))])
+    state = op.dump_state().tuples()
+    q.put((rank, wm, results, state))
+    dist.destroy_process_group()
+
+
+def _single(spec_name, G, late):
+    import pyoracle
+    spec = SPECS[spec_name]
+    op = pyoracle.OracleOp(spec)
+    wm = -1
+    results = []
+    for slices in _batches(G, late):
+        key = np.concatenate([s[0] for s in slices])
+        ts = np.concatenate([s[1] for s in slices])
+        cols = [np.concatenate([s[2][c] for s in slices]) for c in range(2)]
+        valid = [np.concatenate([s[3][c] for s in slices]) for c in range(2)]
+        wm = op.push(key, ts, cols, valid, watermark=wm)
+        r = op.drain()
+        results.append([(int(r.key_id[i]), int(r.win_start[i]), int(r.win_end[i]), int(r.src_index[i]),
+                         tuple(a[i].item() for a in r.aggs)) for i in range(len(r))])
+    return wm, results, op.dump_state().tuples()
+
+
+def _close(a, b):
+    for x, y in zip(a, b):
+        if isinstance(x, float) or isinstance(y, float):
+            if not (np.isnan(x) and np.isnan(y)) and abs(x - y) > 1e-9 * max(1.0, abs(x), abs(y)):
+                return False
+        elif x != y:
+            return False
+    return True
+
+
+@pytest.mark.parametrize("late", [False, True], ids=["no_late", "late"])
+@pytest.mark.parametrize("spec_name", list(SPECS))
+def test_two_rank_protocol_equals_single_stream(spec_name, late):
+    G = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, G, port, spec_name, late, q)) for r in range(G)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=240) for _ in range(G)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    outs.sort()
+    wm1, res1, st1 = _single(spec_name, G, late)
+    assert all(o[1] == wm1 for o in outs)
+    # union of the ranks' state = the single-stream state, keys disjoint
+    keys = [set(k for k, *_ in o[3]) for o in outs]
+    assert not (keys[0] & keys[1])
+    merged = sorted(outs[0][3] + outs[1][3])
+    assert len(merged) == len(st1)
+    for a, b in zip(merged, sorted(st1)):
+        assert a[:3] == b[:3] and _close(a[3], b[3]), (a, b)
+    # changelogs: per-record rows carry the global sequence; merged by (src, start)
+    for bi in range(len(res1)):
+        rows = sorted(outs[0][2][bi] + outs[1][2][bi], key=lambda t: (t[3], t[1], t[0], t[2]))
+        ref = sorted(res1[bi], key=lambda t: (t[3], t[1], t[0], t[2]))
+        assert len(rows) == len(ref)
+        for a, b in zip(rows, ref):
+            assert a[:4] == b[:4] and _close(a[4], b[4]), (a, b)
