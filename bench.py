@@ -35,6 +35,7 @@ def parse():
     p.add_argument("--emit", default="per_batch", choices=["per_batch", "per_record", "none"])
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget (0 = skip)")
     p.add_argument("--traffic-csv", default="", help="rocprofv3 --pmc counter CSV to fill roofline.traffic")
+    p.add_argument("--force-exchange", action="store_true", help="N=1 through the RCCL exchange path")
     return p.parse_args()
 
 
@@ -68,20 +69,29 @@ def main():
             idt.copy_(torch.frombuffer(bytearray(comm_unique_id()), dtype=torch.uint8))
         dist.broadcast(idt, 0)
         comm_id = bytes(idt.cpu().numpy().tobytes())
+    elif args.force_exchange:
+        comm_id = comm_unique_id()  # 1-rank communicator: the exchange path with itself
     eng = Engine(device=local, rank=rank, nranks=world, comm_id=comm_id, batch_capacity=batch)
 
     # state sized for the config: distinct (key, window) groups over the whole run
     windows = 3_600_000 // (cfg.advance_ms or cfg.size_ms or 60_000) + 2 if cfg.window_kind != abi.HSG_SESSION else 1
     groups = min(cfg.keys, n_rank * world) * windows
+    if cfg.window_kind == abi.HSG_SESSION:
+        groups = n_rank * world  # at most one session per record
     spec = cfg.spec(emit, state_capacity=max(1 << 16, groups))
     op = eng.op(spec)
     f64 = spec.agg_is_f64()
 
     # synthetic input resident in HBM before timing: this rank's slice of every step
-    data = datagen.generate_torch(cfg, n_rank, device=dev, start=rank * n_rank, total=n_rank * world)
-    keys, ts = data["key_id"], data["ts"]
-    cols = data["cols"] if spec.col_types else []
+    # every global batch = world consecutive pieces of `batch` records; rank r
+    # ingests piece r of each (the C3 layout: a contiguous 1/G of every batch)
     pieces = [(s, min(batch, n_rank - s)) for s in range(0, n_rank, batch)]
+    parts = [datagen.generate_torch(cfg, m, device=dev, start=s * world + rank * m, total=n_rank * world)
+             for s, m in pieces]
+    keys = torch.cat([p["key_id"] for p in parts])
+    ts = torch.cat([p["ts"] for p in parts])
+    cols = [torch.cat([p["cols"][0] for p in parts])] if spec.col_types else []
+    del parts
     out_cap = max(1, eng_out_capacity(op))
     outs = {
         "key_id": torch.empty(out_cap, dtype=torch.int32, device=dev),
@@ -141,6 +151,19 @@ def main():
             "kernel": "k_tw_agg", "alg_bytes_per_launch": int(alg_bytes / max(1, launches)),
             "avg_launch_ms": round(agg_s * 1e3 / max(1, launches), 4)}
 
+    xchg = None
+    if world > 1 or args.force_exchange:
+        xb = st1["exchange_bytes"] - st0["exchange_bytes"]
+        xs = (st1["exchange_ms"] - st0["exchange_ms"]) / 1e3
+        xt = torch.tensor([float(xb), xs], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(xt, op=dist.ReduceOp.SUM)
+        xb_all, xs_sum = float(xt[0]), float(xt[1])
+        links = world * (world - 1) * 153e9  # xGMI: 7 links x ~153 GB/s per GPU, one per peer pair
+        xchg = {"bytes_per_step": int(xb_all / args.steps), "device_ms_per_step_per_rank":
+                round(xs_sum * 1e3 / args.steps / world, 3),
+                "xgmi_frac": round(xb_all / elapsed / links, 6) if world > 1 else None}
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(cfg, spec, args.cpu_seconds)
@@ -164,6 +187,7 @@ def main():
                        "parallelism": f"key-hash sharded x{world}" if world > 1 else "single GPU"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "exchange": xchg,
             "agg_kernel_share": round(agg_s / elapsed, 4) if elapsed > 0 else None,
             "pairs_per_step": int((st1["pairs_total"] - st0["pairs_total"]) / max(1, args.steps)),
             "touched_per_step": int(touched / max(1, args.steps)),
