@@ -5,6 +5,7 @@
 #include <string>
 
 #include "hsg_internal.h"
+#include "hsg_part.h"
 #include "hsg_perrecord.h"
 
 namespace hsg {
@@ -51,6 +52,11 @@ struct OpDevice {
   TwTable tw = {};
   uint64_t cap = 0;             // table slots
   EmitScratch emit = {};
+  // partitioned aggregation (hsg_part.h)
+  PartBuffers part = {};
+  void *part_mem = nullptr;
+  bool use_part = false;
+  int np_log2 = 10;             // partitions of the next batch (adapted per batch)
   // sessions
   SessTable ss = {};
   uint64_t *arena_top = nullptr;  // device bump pointer

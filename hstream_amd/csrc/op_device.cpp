@@ -2,6 +2,7 @@
 // stream-time scan, the aggregation kernels, changelog bookkeeping, dumps.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -61,6 +62,60 @@ static void free_out(OutCols &o) {
   dfree(o.we);
   dfree(o.src);
   for (int j = 0; j < kMaxAggs; ++j) dfree(o.agg[j]);
+}
+
+// Partitioned-aggregation scratch, carved from one allocation.
+int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err) {
+  PartBuffers &pb = d.part;
+  const uint64_t n = d.batch_cap;
+  const uint64_t tiles = part_tiles(n) + 1;
+  const uint64_t nh = (1ull << kPartMaxLog2) * tiles;
+  bool last = has_last(prog);
+  uint64_t off = 0;
+  auto take = [&](uint64_t bytes) {
+    off = (off + 255) & ~255ull;
+    uint64_t o = off;
+    off += bytes ? bytes : 1;
+    return o;
+  };
+  uint64_t o_hist = take(nh * 4), o_off = take((nh + 1) * 8), o_part = take((scan_partials_needed(nh) + 8) * 8);
+  uint64_t o_total = take(64), o_key = take(n * 4), o_krel = take(n * 4), o_nwin = take(n * 4);
+  uint64_t o_col[kMaxCols], o_valid[kMaxCols];
+  for (int c = 0; c < cfg.n_cols; ++c) {
+    o_col[c] = take(n * 8);
+    o_valid[c] = take(n);
+  }
+  uint64_t o_seq = take(last ? n * 8 : 8), o_chunk = take(((1ull << kPartMaxLog2) + 1) * 4);
+  DTRY(hipMalloc(&d.part_mem, off));
+  char *m = (char *)d.part_mem;
+  pb.hist = (uint32_t *)(m + o_hist);
+  pb.off = (uint64_t *)(m + o_off);
+  pb.partial = (uint64_t *)(m + o_part);
+  pb.total = (uint64_t *)(m + o_total);
+  pb.key = (uint32_t *)(m + o_key);
+  pb.krel = (uint32_t *)(m + o_krel);
+  pb.nwin = (uint32_t *)(m + o_nwin);
+  for (int c = 0; c < kMaxCols; ++c) {
+    pb.col[c] = c < cfg.n_cols ? (int64_t *)(m + o_col[c]) : nullptr;
+    pb.valid[c] = c < cfg.n_cols ? (uint8_t *)(m + o_valid[c]) : nullptr;
+  }
+  pb.seq1 = (int64_t *)(m + o_seq);
+  pb.chunk_start = (uint32_t *)(m + o_chunk);
+  pb.n_cap = n;
+  pb.tiles_cap = tiles;
+  return HSG_OK;
+}
+
+// Partitions for the next batch: about half an LDS table of groups per bucket,
+// and buckets of at least a few thousand records.
+static void adapt_partitions(OpDevice &d, const Program &prog, uint64_t groups, uint64_t n) {
+  const uint64_t per = part_lds_entries(prog) / 2;
+  uint64_t want = (groups + per - 1) / per;
+  uint64_t cap_by_n = n / 2048 > 1 ? n / 2048 : 1;
+  if (want > cap_by_n) want = cap_by_n;
+  int l = 0;
+  while ((1ull << l) < want && l < kPartMaxLog2) ++l;
+  d.np_log2 = l < 4 ? 4 : l;
 }
 
 int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err) {
@@ -137,6 +192,13 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
   if (cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.window_kind == HSG_SESSION) {
     rc = perrecord_device_init(d, cfg, prog, err);
     if (rc != HSG_OK) return rc;
+  } else if (part_supported(prog)) {
+    const char *env = getenv("HSG_AGG");
+    d.use_part = !(env && strcmp(env, "atomic") == 0);
+    if (d.use_part) {
+      rc = part_device_init(d, cfg, prog, err);
+      if (rc != HSG_OK) return rc;
+    }
   }
   if (sharded) {
     rc = exchange_device_init(d, cfg, batch_cap, err);
@@ -180,6 +242,8 @@ void op_device_free(OpDevice &d) {
   free_out(d.out);
   if (d.scratch) hipFree(d.scratch);
   d.scratch = nullptr;
+  if (d.part_mem) hipFree(d.part_mem);
+  d.part_mem = nullptr;
   if (d.xsend) hipFree(d.xsend);
   if (d.xrecv) hipFree(d.xrecv);
   d.xsend = d.xrecv = nullptr;
@@ -262,6 +326,7 @@ int clear_batch_scalars(OpDevice &d, std::string &err) {
   // err, pairs, late, out_rows, touched (offsets 20..55); wm/epoch/live persist
   DTRY(hipMemsetAsync((char *)d.sc + offsetof(DevScalars, err), 0,
                       offsetof(DevScalars, live) - offsetof(DevScalars, err), d.stream));
+  DTRY(hipMemsetAsync((char *)d.sc + offsetof(DevScalars, scratch), 0, 8 * sizeof(uint64_t), d.stream));
   return HSG_OK;
 }
 
@@ -301,7 +366,21 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     // the per-record stream time arrives in rec_wm and only the epoch is used
     launch_stream_time(d, cfg, kb, a.wm_in, p.adv);
     DTRY(hipEventRecord(d.ev_a, d.stream));
-    launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, false);
+    if (d.use_part) {
+      PartParams pp;
+      memset(&pp, 0, sizeof(pp));
+      pp.np_log2 = d.np_log2;
+      for (int c = 0; c < cfg.n_cols; ++c) pp.has_valid |= kb.valid[c] != nullptr;
+      pp.has_seq = has_last(prog);
+      pp.tiles = part_tiles(kb.n);
+      const uint64_t nh = (1ull << pp.np_log2) * pp.tiles;
+      launch_part_hist(d.stream, kb, p, pp, d.tile_prefix, rec_wm, d.part, d.sc);
+      scan_excl_u32(d.stream, d.part.hist, d.part.off, nh, d.part.partial, d.part.off + nh);
+      launch_part_scatter(d.stream, kb, p, pp, d.tile_prefix, rec_wm, seq, d.part, d.sc);
+      launch_part_agg(d.stream, prog, p, pp, d.tw, d.part, kb.n, d.sc);
+    } else {
+      launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, false);
+    }
     DTRY(hipEventRecord(d.ev_b, d.stream));
     if (has_last(prog)) launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, true);
     if (cfg.emit_mode == HSG_EMIT_PER_BATCH)
@@ -314,8 +393,9 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     float ms = 0;
     if (hipEventElapsedTime(&ms, d.ev_a, d.ev_b) == hipSuccess) r.agg_ms = ms;
     r.agg_launches = 1;
+    if (d.use_part) adapt_partitions(d, prog, d.h_sc->scratch[0], kb.n);
   }
-  r.touched = r.out_rows;
+  r.touched = cfg.emit_mode == HSG_EMIT_PER_BATCH ? r.out_rows : d.h_sc->scratch[0];
   return rc;
 }
 
