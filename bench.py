@@ -75,7 +75,8 @@ def main():
 
     # state sized for the config: distinct (key, window) groups over the whole run
     windows = 3_600_000 // (cfg.advance_ms or cfg.size_ms or 60_000) + 2 if cfg.window_kind != abi.HSG_SESSION else 1
-    groups = min(cfg.keys, n_rank * world) * windows
+    wpr = -(-cfg.size_ms // cfg.advance_ms) if cfg.window_kind == abi.HSG_HOPPING else 1
+    groups = min(cfg.keys * windows, n_rank * world * wpr)
     if cfg.window_kind == abi.HSG_SESSION:
         groups = n_rank * world  # at most one session per record
     spec = cfg.spec(emit, state_capacity=max(1 << 16, groups))

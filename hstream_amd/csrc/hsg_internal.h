@@ -92,8 +92,9 @@ struct DevScalars {
   uint64_t out_rows;     // rows appended to the changelog this batch
   uint64_t touched;
   uint64_t live;         // dump: rows found
-  uint64_t min_ts_valid; // reserved
-  uint64_t scratch[23];
+  uint32_t no_late;      // this batch: no (record, window) can fail the grace check
+  uint32_t pad0;
+  uint64_t scratch[23];  // [0] groups flushed (partition path), [1] touched-list length
 };
 static_assert(sizeof(DevScalars) == 256, "DevScalars layout");
 
@@ -172,8 +173,10 @@ void launch_fill_u32(hipStream_t s, uint32_t *p, uint64_t n, uint32_t v);
 
 // stream time: tile maxima -> exclusive tile prefix (+ epoch init)
 void launch_tile_stats(hipStream_t s, const Batch &b, int64_t *tile_max, int64_t *tile_min, uint64_t n_tiles);
+// grace >= 0: also decide sc->no_late for a time-window op
 void launch_tile_scan(hipStream_t s, const int64_t *tile_max, const int64_t *tile_min, int64_t *tile_prefix,
-                      uint64_t n_tiles, int64_t wm_in, int64_t adv, bool set_epoch, DevScalars *sc);
+                      uint64_t n_tiles, int64_t wm_in, int64_t adv, bool set_epoch, DevScalars *sc,
+                      int64_t grace = -1);
 
 // time windows, atomic hash aggregation (per-batch / none modes). rec_wm / seq
 // (optional) carry per-record stream time and global sequence after a key

@@ -8,37 +8,38 @@
 namespace hsg {
 
 constexpr int kPartThreads = 256;
-constexpr int kPartItems = 16;
-constexpr int kPartTile = kPartThreads * kPartItems;  // records per partition-pass workgroup
-constexpr int kPartMaxLog2 = 12;                      // up to 4096 partitions
-constexpr int kAggThreads = 512;
+constexpr int kPartMaxLog2 = 11;                      // up to 2048 partitions
+constexpr int kAggThreads = 1024;
+constexpr int kPartMaxWords = 11;                     // 2 + 8 columns + seq
 constexpr uint64_t kAggChunk = 16384;                 // records per aggregation workgroup
 
+// A partitioned record is `words` 8-byte words:
+//   [key | krel << 32] [nwin | valid bits << 32] [col 0 .. C-1] [seq + 1]?
+// krel = first accepted window relative to the epoch, nwin = accepted windows.
 struct PartBuffers {
-  uint32_t *hist;     // [np * tiles] bucket-major per-tile counts
-  uint64_t *off;      // [np * tiles + 1] exclusive prefix
-  uint64_t *partial;  // scan partials
-  uint64_t *total;    // [4] device scalars
-  uint32_t *key;      // [n] partitioned records
-  uint32_t *krel;     // [n] first accepted window, relative to the epoch
-  uint32_t *nwin;     // [n] accepted windows (consecutive from krel)
-  int64_t *col[kMaxCols];
-  uint8_t *valid[kMaxCols];
-  int64_t *seq1;      // [n] global sequence + 1 (LAST only)
-  uint32_t *chunk_start;  // [4097] first aggregation workgroup of each bucket
+  uint32_t *hist;         // [np * tiles] bucket-major per-tile counts
+  uint64_t *off;          // [np * tiles + 1] exclusive prefix
+  uint64_t *partial;      // scan partials
+  uint64_t *rec;          // [n * words] partitioned records
+  uint32_t *chunk_start;  // [np + 1] first aggregation workgroup of each bucket
+  uint32_t *touched;      // [table slots] groups first touched by this batch (length: sc->scratch[1])
   uint64_t n_cap;
-  uint64_t tiles_cap;
 };
 
 struct PartParams {
   int32_t np_log2;    // partitions = 1 << np_log2
   int32_t has_valid;
   int32_t has_seq;
+  int32_t words;
+  int32_t tile;       // records per partition-pass workgroup (1024, 2048 or 4096)
   int32_t pad;
   uint64_t tiles;     // partition-pass tiles of this batch
 };
 
-uint64_t part_tiles(uint64_t n);
+inline int part_words(int n_cols, bool has_seq) { return 2 + n_cols + (has_seq ? 1 : 0); }
+inline int part_tile_for(int words) { return words <= 3 ? 4096 : words <= 7 ? 2048 : 1024; }
+inline uint64_t part_tiles(uint64_t n, int tile) { return (n + tile - 1) / tile; }
+
 void launch_part_hist(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp,
                       const int64_t *tprefix, const int64_t *rec_wm, const PartBuffers &pb, DevScalars *sc);
 void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp,
@@ -48,6 +49,9 @@ void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const
 bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, const PartParams &pp, const TwTable &t,
                      const PartBuffers &pb, uint64_t n, DevScalars *sc);
 bool part_supported(const Program &prog);
+// per-batch changelog rows of the groups in pb.touched
+void launch_part_emit(hipStream_t s, const TwTable &t, const Program &prog, const TwParams &p, const PartBuffers &pb,
+                      OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc);
 inline uint64_t part_lds_entries(const Program &prog) {
   return prog.n_slots <= 2 ? 4096 : prog.n_slots <= 6 ? 2048 : 1024;
 }

@@ -4,8 +4,10 @@
 //            window (bucket = top bits of hash(key): every window of a key
 //            lands in one bucket)
 //   scan     bucket-major exclusive prefix -> bucket ranges
-//   scatter  partitioned columnar copy: key, first accepted window, window
-//            count, values (+ presence, + sequence when LAST is asked for)
+//   scatter  each tile is bucket-sorted in LDS, then every bucket's run is
+//            written by consecutive lanes as packed 8-byte-word records
+//            [key|krel<<32][nwin|valid<<32][cols][seq+1]? (coalesced stores;
+//            scattering 4-8 B fields per record directly ran at ~280 GB/s)
 //   agg      one workgroup per <= kAggChunk records of a bucket: LDS hash table
 //            of the chunk's groups fed by LDS atomics, then one flush per group
 //            into the HBM table -- plain read-modify-write when the workgroup is
@@ -21,7 +23,7 @@
 
 namespace hsg {
 
-uint64_t part_tiles(uint64_t n) { return (n + kPartTile - 1) / kPartTile; }
+constexpr uint16_t kNoBucket = 0xFFFF;
 
 __device__ inline uint32_t bucket_of(uint32_t key, int np_log2) {
   return np_log2 ? (uint32_t)(mix64((uint64_t)key * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull) >> (64 - np_log2))
@@ -55,25 +57,28 @@ __device__ inline bool part_record(const TwParams &p, int64_t k_epoch, uint32_t 
   return true;
 }
 
-// Shared walk over the 4 stream-time sub-tiles of one partition tile.
-template <int PASS>
-__global__ __launch_bounds__(kPartThreads) void k_part(Batch b, TwParams p, PartParams pp,
-                                                       const int64_t *__restrict__ tprefix,
-                                                       const int64_t *__restrict__ rec_wm,
-                                                       const int64_t *__restrict__ seq, PartBuffers pb,
-                                                       DevScalars *sc) {
-  __shared__ uint32_t cnt[1 << kPartMaxLog2];
-  __shared__ uint64_t sred[2][kPartThreads / 64];
-  const int nb = 1 << pp.np_log2;
-  for (int i = threadIdx.x; i < nb; i += kPartThreads) cnt[i] = 0;
-  __syncthreads();
-  const int64_t k_epoch = sc->k_epoch;
-  uint64_t late = 0;
-  uint32_t err = 0;
-  constexpr int kSub = kPartTile / kTileRecords;
+// XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs, so
+// give workgroups b, b+8, b+16, ... (one XCD) consecutive tiles; a bucket's
+// runs from consecutive tiles are adjacent in the output. Speed only.
+__device__ inline uint64_t xcd_tile(uint64_t blk, uint64_t tiles) {
+  const uint64_t per = tiles / 8, full = per * 8;
+  if (blk >= full) return blk;
+  return (blk & 7) * per + (blk >> 3);
+}
+
+// Walk the T records of one partition tile in stream-time sub-tiles; calls
+// f(j, i, key, krel, nwin) for every record with >= 1 accepted window, where
+// j = tile-local index and i = batch index. Block-wide (barriers inside).
+template <int T, typename F>
+__device__ inline void walk_tile(const Batch &b, const TwParams &p, const PartParams &pp,
+                                 const int64_t *__restrict__ tprefix, const int64_t *__restrict__ rec_wm,
+                                 uint64_t tile, int64_t k_epoch, uint64_t &late, uint32_t &err, F f,
+                                 bool no_late) {
+  constexpr int kSub = T / kTileRecords;
   for (int sub = 0; sub < kSub; ++sub) {
-    const uint64_t st = (uint64_t)blockIdx.x * kSub + sub;  // stream-time tile
+    const uint64_t st = tile * kSub + sub;  // stream-time tile
     const uint64_t base = st * kTileRecords;
+    if (base >= b.n) break;  // uniform across the workgroup
     uint32_t key[kRecPerThread];
     int64_t ts[kRecPerThread], wm[kRecPerThread];
 #pragma unroll
@@ -83,64 +88,159 @@ __global__ __launch_bounds__(kPartThreads) void k_part(Batch b, TwParams p, Part
       key[r] = in ? b.key[i] : HSG_KEY_NONE;
       ts[r] = in ? b.ts[i] : INT64_MIN;
       if (rec_wm) wm[r] = in ? rec_wm[i] : INT64_MIN;
+      if (no_late && !rec_wm) wm[r] = INT64_MIN;  // every window is accepted: skip the scan
     }
-    if (base >= b.n) break;  // uniform across the workgroup
-    if (!rec_wm) tile_stream_time(ts, tprefix[st], wm);
+    if (!rec_wm && !no_late) tile_stream_time(ts, tprefix[st], wm);
 #pragma unroll
     for (int r = 0; r < kRecPerThread; ++r) {
-      const uint64_t i = base + (uint64_t)r * kTileThreads + threadIdx.x;
       uint32_t krel, nwin;
-      uint64_t lt = 0;
-      if (!part_record(p, k_epoch, key[r], ts[r], wm[r], krel, nwin, lt, err)) {
-        late += lt;
-        continue;
-      }
-      late += lt;
-      const uint32_t bk = bucket_of(key[r], pp.np_log2);
-      if (PASS == 0) {
-        atomicAdd(&cnt[bk], 1u);
-      } else {
-        const uint32_t rank = atomicAdd(&cnt[bk], 1u);
-        const uint64_t o = pb.off[(uint64_t)bk * pp.tiles + blockIdx.x] + rank;
-        pb.key[o] = key[r];
-        pb.krel[o] = krel;
-        pb.nwin[o] = nwin;
-        for (int c = 0; c < kMaxCols; ++c) {
-          if (!b.col[c]) break;
-          pb.col[c][o] = b.col[c][i];
-          if (pp.has_valid) pb.valid[c][o] = b.valid[c] ? b.valid[c][i] : (uint8_t)1;
-        }
-        if (pp.has_seq) pb.seq1[o] = (seq ? seq[i] : (int64_t)(p.rec_base + i)) + 1;
-      }
-    }
-  }
-  __syncthreads();
-  if (PASS == 0) {
-    for (int i = threadIdx.x; i < nb; i += kPartThreads) pb.hist[(uint64_t)i * pp.tiles + blockIdx.x] = cnt[i];
-    late = wave_sum_u64(late);
-    if ((threadIdx.x & 63) == 0) sred[0][threadIdx.x >> 6] = late;
-    if (err) atomicOr(&sc->err, err);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint64_t l = 0;
-      for (int k = 0; k < kPartThreads / 64; ++k) l += sred[0][k];
-      if (l) atomicAdd((unsigned long long *)&sc->late, (unsigned long long)l);
+      if (!part_record(p, k_epoch, key[r], ts[r], wm[r], krel, nwin, late, err)) continue;
+      const int j = sub * kTileRecords + r * kTileThreads + threadIdx.x;
+      f(j, base + (uint64_t)r * kTileThreads + threadIdx.x, key[r], krel, nwin);
     }
   }
 }
 
+template <int T>
+__global__ __launch_bounds__(kPartThreads) void k_part_hist(Batch b, TwParams p, PartParams pp,
+                                                            const int64_t *__restrict__ tprefix,
+                                                            const int64_t *__restrict__ rec_wm, PartBuffers pb,
+                                                            DevScalars *sc) {
+  __shared__ uint32_t cnt[1 << kPartMaxLog2];
+  __shared__ uint64_t sred[kPartThreads / 64];
+  const int nb = 1 << pp.np_log2;
+  const uint64_t tile = xcd_tile(blockIdx.x, pp.tiles);
+  for (int i = threadIdx.x; i < nb; i += kPartThreads) cnt[i] = 0;
+  __syncthreads();
+  uint64_t late = 0;
+  uint32_t err = 0;
+  walk_tile<T>(b, p, pp, tprefix, rec_wm, tile, sc->k_epoch, late, err,
+               [&](int, uint64_t, uint32_t key, uint32_t, uint32_t) { atomicAdd(&cnt[bucket_of(key, pp.np_log2)], 1u); },
+               sc->no_late != 0);
+  __syncthreads();
+  for (int i = threadIdx.x; i < nb; i += kPartThreads) pb.hist[(uint64_t)i * pp.tiles + tile] = cnt[i];
+  late = wave_sum_u64(late);
+  if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = late;
+  if (err) atomicOr(&sc->err, err);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t l = 0;
+    for (int k = 0; k < kPartThreads / 64; ++k) l += sred[k];
+    if (l) atomicAdd((unsigned long long *)&sc->late, (unsigned long long)l);
+  }
+}
+
+template <int T, int WMAX>
+__global__ __launch_bounds__(kPartThreads) void k_part_scatter(Batch b, TwParams p, PartParams pp,
+                                                               const int64_t *__restrict__ tprefix,
+                                                               const int64_t *__restrict__ rec_wm,
+                                                               const int64_t *__restrict__ seq, PartBuffers pb,
+                                                               DevScalars *sc) {
+  __shared__ uint64_t stage[T * WMAX];
+  __shared__ uint16_t lbk[T];
+  __shared__ uint16_t sidx[T];
+  __shared__ uint32_t lstart[1 << kPartMaxLog2];
+  __shared__ uint32_t cursor[1 << kPartMaxLog2];
+  __shared__ uint64_t goff[1 << kPartMaxLog2];
+  __shared__ uint32_t swave[kPartThreads / 64];
+  const int nb = 1 << pp.np_log2;
+  const int W = pp.words;
+  const int C = W - 2 - pp.has_seq;
+  const uint64_t tile = xcd_tile(blockIdx.x, pp.tiles);
+  for (int i = threadIdx.x; i < nb; i += kPartThreads) cursor[i] = 0;
+  for (int j = threadIdx.x; j < T; j += kPartThreads) lbk[j] = kNoBucket;
+  __syncthreads();
+  // 1) records -> LDS in arrival order, bucket histogram
+  uint64_t late = 0;
+  uint32_t err = 0;
+  walk_tile<T>(b, p, pp, tprefix, rec_wm, tile, sc->k_epoch, late, err,
+               [&](int j, uint64_t i, uint32_t key, uint32_t krel, uint32_t nwin) {
+                 const uint32_t bk = bucket_of(key, pp.np_log2);
+                 uint64_t vb = 0;
+                 uint64_t *w = &stage[j * WMAX];
+                 for (int c = 0; c < C; ++c) {
+                   w[2 + c] = (uint64_t)b.col[c][i];
+                   if (pp.has_valid && b.valid[c] && !b.valid[c][i]) continue;
+                   vb |= 1ull << c;
+                 }
+                 w[0] = (uint64_t)key | ((uint64_t)krel << 32);
+                 w[1] = (uint64_t)nwin | (vb << 32);
+                 if (pp.has_seq) w[2 + C] = (uint64_t)((seq ? seq[i] : (int64_t)(p.rec_base + i)) + 1);
+                 lbk[j] = (uint16_t)bk;
+                 atomicAdd(&cursor[bk], 1u);
+               },
+               sc->no_late != 0);
+  __syncthreads();
+  // 2) tile-local exclusive scan of the histogram; global run starts
+  const int per = (nb + kPartThreads - 1) / kPartThreads;
+  const int lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
+  uint32_t loc = 0;
+  for (int k = lo; k < hi; ++k) loc += cursor[k];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t incl = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) swave[wv] = incl;
+  __syncthreads();
+  uint32_t run = incl - loc;
+  for (int k = 0; k < wv; ++k) run += swave[k];
+  for (int k = lo; k < hi; ++k) {
+    lstart[k] = run;
+    run += cursor[k];
+    cursor[k] = 0;
+    goff[k] = pb.off[(uint64_t)k * pp.tiles + tile];
+  }
+  const uint32_t placed = swave[0] + swave[1] + swave[2] + swave[3];
+  __syncthreads();
+  // 3) bucket-sorted order of the staged records
+  for (int j = threadIdx.x; j < T; j += kPartThreads) {
+    const uint16_t bk = lbk[j];
+    if (bk == kNoBucket) continue;
+    sidx[lstart[bk] + atomicAdd(&cursor[bk], 1u)] = (uint16_t)j;
+  }
+  __syncthreads();
+  // 4) coalesced write-out: consecutive lanes write consecutive words of a run
+  const uint32_t inv = (1u << 20) / (uint32_t)W + 1;  // t / W for t < 16384, W <= 64
+  const uint32_t total = placed * (uint32_t)W;
+  for (uint32_t t = threadIdx.x; t < total; t += kPartThreads) {
+    const uint32_t q = (uint32_t)(((uint64_t)t * inv) >> 20);
+    const uint32_t w = t - q * (uint32_t)W;
+    const uint16_t j = sidx[q];
+    const uint16_t bk = lbk[j];
+    const uint64_t dest = goff[bk] + (q - lstart[bk]);
+    pb.rec[dest * W + w] = stage[j * WMAX + w];
+  }
+}
+
+template <int T>
+static void hist_launch(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp, const int64_t *tprefix,
+                        const int64_t *rec_wm, const PartBuffers &pb, DevScalars *sc) {
+  hipLaunchKernelGGL(k_part_hist<T>, dim3((unsigned)pp.tiles), dim3(kPartThreads), 0, s, b, p, pp, tprefix, rec_wm,
+                     pb, sc);
+}
+
 void launch_part_hist(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp,
                       const int64_t *tprefix, const int64_t *rec_wm, const PartBuffers &pb, DevScalars *sc) {
-  if (pp.tiles)
-    hipLaunchKernelGGL(k_part<0>, dim3((unsigned)pp.tiles), dim3(kPartThreads), 0, s, b, p, pp, tprefix, rec_wm,
-                       nullptr, pb, sc);
+  if (!pp.tiles) return;
+  if (pp.tile == 4096) hist_launch<4096>(s, b, p, pp, tprefix, rec_wm, pb, sc);
+  else if (pp.tile == 2048) hist_launch<2048>(s, b, p, pp, tprefix, rec_wm, pb, sc);
+  else hist_launch<1024>(s, b, p, pp, tprefix, rec_wm, pb, sc);
 }
+
 void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp,
                          const int64_t *tprefix, const int64_t *rec_wm, const int64_t *seq, const PartBuffers &pb,
                          DevScalars *sc) {
-  if (pp.tiles)
-    hipLaunchKernelGGL(k_part<1>, dim3((unsigned)pp.tiles), dim3(kPartThreads), 0, s, b, p, pp, tprefix, rec_wm, seq,
-                       pb, sc);
+  if (!pp.tiles) return;
+  const dim3 g((unsigned)pp.tiles), t(kPartThreads);
+  if (pp.tile == 4096)
+    hipLaunchKernelGGL((k_part_scatter<4096, 3>), g, t, 0, s, b, p, pp, tprefix, rec_wm, seq, pb, sc);
+  else if (pp.tile == 2048)
+    hipLaunchKernelGGL((k_part_scatter<2048, 7>), g, t, 0, s, b, p, pp, tprefix, rec_wm, seq, pb, sc);
+  else
+    hipLaunchKernelGGL((k_part_scatter<1024, 11>), g, t, 0, s, b, p, pp, tprefix, rec_wm, seq, pb, sc);
 }
 
 // ---------------------------------------------------------------------------
@@ -183,30 +283,60 @@ __global__ __launch_bounds__(1024) void k_part_chunks(const uint64_t *off, uint6
 // ---------------------------------------------------------------------------
 // LDS aggregation of one chunk
 // ---------------------------------------------------------------------------
-__device__ inline void lds_apply(const Program &prog, int64_t *__restrict__ row, const PartBuffers &pb, bool has_valid,
-                                 uint64_t i) {
+// One partitioned record: word 1 (window count + presence bits) in a register,
+// columns / sequence read from HBM (same cache line as words 0-1 mostly).
+struct PRec {
+  const uint64_t *w;
+  uint64_t w1;
+  int C;
+  __device__ bool present(int c) const { return (w1 >> (32 + c)) & 1ull; }
+  __device__ int64_t col(int c) const { return (int64_t)w[2 + c]; }
+  __device__ int64_t seq1() const { return (int64_t)w[2 + C]; }
+};
+
+// contribution of the record to slot s (identity when absent)
+__device__ inline int64_t prec_elem(const Program &prog, int s, const PRec &r) {
+  const int op = prog.slot_op[s];
+  const int c = prog.slot_col[s];
+  if (op == S_CNT_ALL) return 1;
+  if (op == S_LAST_VAL) return 0;
+  if (!r.present(c)) return slot_identity_dev(op);
+  switch (op) {
+    case S_CNT: return 1;
+    case S_SUM_I:
+    case S_SUM_F:
+    case S_MIN_I:
+    case S_MAX_I: return r.col(c);
+    case S_MIN_F:
+    case S_MAX_F: return (int64_t)f64_ord(__builtin_bit_cast(double, r.col(c)));
+    case S_LAST_SEQ: return r.seq1();
+    default: return 0;
+  }
+}
+
+__device__ inline void lds_apply(const Program &prog, int64_t *__restrict__ row, const PRec &r) {
   for (int s = 0; s < prog.n_slots; ++s) {
     const int op = prog.slot_op[s];
-    const int c = prog.slot_col[s];
-    const bool present = op == S_CNT_ALL || !has_valid || pb.valid[c][i];
-    if (!present) continue;
+    if (op == S_LAST_VAL) continue;
+    if (op != S_CNT_ALL && !r.present(prog.slot_col[s])) continue;
+    const int64_t x = prec_elem(prog, s, r);
     unsigned long long *u = (unsigned long long *)(row + s);
     switch (op) {
       case S_CNT_ALL:
-      case S_CNT: atomicAdd(u, 1ull); break;
-      case S_SUM_I: atomicAdd(u, (unsigned long long)pb.col[c][i]); break;
-      case S_SUM_F: unsafeAtomicAdd((double *)(row + s), __builtin_bit_cast(double, pb.col[c][i])); break;
-      case S_MIN_I: atomicMin((long long *)(row + s), (long long)pb.col[c][i]); break;
-      case S_MAX_I: atomicMax((long long *)(row + s), (long long)pb.col[c][i]); break;
-      case S_MIN_F: atomicMin(u, (unsigned long long)f64_ord(__builtin_bit_cast(double, pb.col[c][i]))); break;
-      case S_MAX_F: atomicMax(u, (unsigned long long)f64_ord(__builtin_bit_cast(double, pb.col[c][i]))); break;
-      case S_LAST_SEQ: atomicMax(u, (unsigned long long)pb.seq1[i]); break;
+      case S_CNT:
+      case S_SUM_I: atomicAdd(u, (unsigned long long)x); break;
+      case S_SUM_F: unsafeAtomicAdd((double *)(row + s), __builtin_bit_cast(double, x)); break;
+      case S_MIN_I: atomicMin((long long *)(row + s), (long long)x); break;
+      case S_MAX_I: atomicMax((long long *)(row + s), (long long)x); break;
+      case S_MIN_F: atomicMin(u, (unsigned long long)x); break;
+      case S_MAX_F:
+      case S_LAST_SEQ: atomicMax(u, (unsigned long long)x); break;
       default: break;
     }
   }
 }
 
-// HBM-side combine of a finished LDS row (v) into state row `row`.
+// HBM-side combine of a finished row of partial aggregates (v) into `row`.
 __device__ inline void flush_row(const Program &prog, int64_t *__restrict__ row, const int64_t *v, bool exclusive) {
   for (int s = 0; s < prog.n_slots; ++s) {
     const int op = prog.slot_op[s];
@@ -235,14 +365,17 @@ __device__ inline void flush_row(const Program &prog, int64_t *__restrict__ row,
 
 template <int MS, int E>
 __global__ __launch_bounds__(kAggThreads) void k_part_agg(Program prog, TwParams p, PartParams pp, TwTable t,
-                                                          PartBuffers pb, const uint32_t *__restrict__ chunk_start,
-                                                          DevScalars *sc) {
+                                                          PartBuffers pb, DevScalars *sc) {
   __shared__ uint64_t lkey[E];
   __shared__ int64_t lagg[E * MS];
   __shared__ uint32_t lfill;
   __shared__ uint32_t sb, sc0, sc1;
   __shared__ uint64_t sred[3][kAggThreads / 64];
+  __shared__ uint32_t ltouch[E];  // slots this workgroup touched first in this batch
+  __shared__ uint32_t ltn;
+  __shared__ uint64_t lbase;
   const int nb = 1 << pp.np_log2;
+  const uint32_t *chunk_start = pb.chunk_start;
   if (threadIdx.x == 0) {
     // find this workgroup's bucket: chunk_start[b] <= blockIdx.x < chunk_start[b + 1]
     uint32_t w = blockIdx.x;
@@ -256,6 +389,7 @@ __global__ __launch_bounds__(kAggThreads) void k_part_agg(Program prog, TwParams
     sc0 = chunk_start[lo];
     sc1 = chunk_start[lo + 1];
     lfill = 0;
+    ltn = 0;
   }
   for (int e = threadIdx.x; e < E; e += kAggThreads) {
     lkey[e] = kEmpty;
@@ -270,13 +404,27 @@ __global__ __launch_bounds__(kAggThreads) void k_part_agg(Program prog, TwParams
   const bool exclusive = (sc1 - sc0) == 1;
   const uint64_t r0 = b0 + c * kAggChunk, r1 = r0 + kAggChunk < b1 ? r0 + kAggChunk : b1;
   const uint32_t limit = (uint32_t)(E * 3 / 4);
-  const bool has_valid = pp.has_valid != 0;
+  const int W = pp.words;
+  const int C = W - 2 - pp.has_seq;
   uint64_t pairs = 0;
   uint32_t fresh = 0, err = 0;
-  for (uint64_t i = r0 + threadIdx.x; i < r1; i += kAggThreads) {
-    const uint32_t key = pb.key[i];
-    const uint32_t krel = pb.krel[i];
-    const uint32_t nw = pb.nwin[i];
+  constexpr int kU = 4;  // records loaded per thread before any is processed
+  for (uint64_t i0 = r0 + threadIdx.x; i0 < r1; i0 += (uint64_t)kAggThreads * kU) {
+    uint64_t b0[kU], b1[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint64_t i = i0 + (uint64_t)u * kAggThreads;
+      b0[u] = i < r1 ? pb.rec[i * W] : 0;
+      b1[u] = i < r1 ? pb.rec[i * W + 1] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+    const uint64_t i = i0 + (uint64_t)u * kAggThreads;
+    if (i >= r1) break;
+    const PRec r{pb.rec + i * W, b1[u], C};
+    const uint64_t w0 = b0[u];
+    const uint32_t key = (uint32_t)w0, krel = (uint32_t)(w0 >> 32);
+    const uint32_t nw = (uint32_t)b1[u];
     pairs += nw;
     for (uint32_t j = 0; j < nw; ++j) {
       const uint64_t g = ((uint64_t)key << 32) | (uint64_t)(krel + j);
@@ -298,36 +446,19 @@ __global__ __launch_bounds__(kAggThreads) void k_part_agg(Program prog, TwParams
         h = (h + 1) & (E - 1);
       }
       if (e >= 0) {
-        lds_apply(prog, &lagg[e * MS], pb, has_valid, i);
+        lds_apply(prog, &lagg[e * MS], r);
       } else {
         // overflow: straight to the HBM table
         int64_t slot = tw_find_or_insert(t, g, fresh);
         if (slot < 0) { err |= ERR_OOM; continue; }
         int64_t v[MS];
-        identity_row<MS>(prog, v);
 #pragma unroll
-        for (int s = 0; s < MS; ++s) {
-          if (s >= prog.n_slots) break;
-          const int op = prog.slot_op[s];
-          const int cc = prog.slot_col[s];
-          const bool present = op == S_CNT_ALL || !has_valid || pb.valid[cc][i];
-          if (!present) continue;
-          switch (op) {
-            case S_CNT_ALL:
-            case S_CNT: v[s] = 1; break;
-            case S_SUM_I:
-            case S_SUM_F:
-            case S_MIN_I:
-            case S_MAX_I: v[s] = pb.col[cc][i]; break;
-            case S_MIN_F:
-            case S_MAX_F: v[s] = (int64_t)f64_ord(__builtin_bit_cast(double, pb.col[cc][i])); break;
-            case S_LAST_SEQ: v[s] = pb.seq1[i]; break;
-            default: break;
-          }
-        }
+        for (int s = 0; s < MS; ++s) v[s] = s < prog.n_slots ? prec_elem(prog, s, r) : 0;
         flush_row(prog, t.aggs + (uint64_t)slot * prog.n_slots, v, false);
-        t.stamp[slot] = (uint32_t)p.batch_id;
+        if (atomicExch(&t.stamp[slot], (uint32_t)p.batch_id) != (uint32_t)p.batch_id)
+          pb.touched[atomicAdd((unsigned long long *)&sc->scratch[1], 1ull)] = (uint32_t)slot;
       }
+    }
     }
   }
   __syncthreads();
@@ -343,8 +474,20 @@ __global__ __launch_bounds__(kAggThreads) void k_part_agg(Program prog, TwParams
 #pragma unroll
     for (int s = 0; s < MS; ++s) v[s] = lagg[e * MS + s];
     flush_row(prog, t.aggs + (uint64_t)slot * prog.n_slots, v, exclusive);
-    t.stamp[slot] = (uint32_t)p.batch_id;
+    // first touch of the group in this batch -> touched list (per-batch changelog)
+    bool first;
+    if (exclusive) {
+      first = t.stamp[slot] != (uint32_t)p.batch_id;
+      if (first) t.stamp[slot] = (uint32_t)p.batch_id;
+    } else {
+      first = atomicExch(&t.stamp[slot], (uint32_t)p.batch_id) != (uint32_t)p.batch_id;
+    }
+    if (first) ltouch[atomicAdd(&ltn, 1u)] = (uint32_t)slot;
   }
+  __syncthreads();
+  if (threadIdx.x == 0) lbase = ltn ? atomicAdd((unsigned long long *)&sc->scratch[1], (unsigned long long)ltn) : 0;
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q < ltn; q += kAggThreads) pb.touched[lbase + q] = ltouch[q];
   pairs = wave_sum_u64(pairs);
   uint64_t fr = wave_sum_u64(fresh);
   groups = wave_sum_u64(groups);
@@ -370,25 +513,52 @@ __global__ __launch_bounds__(kAggThreads) void k_part_agg(Program prog, TwParams
 
 bool part_supported(const Program &prog) { return prog.n_slots <= 8; }
 
+// per-batch changelog: one row per group in the touched list
+__global__ __launch_bounds__(256) void k_part_emit(TwTable t, Program prog, TwParams p, PartBuffers pb, OutCols out,
+                                                   uint64_t out_base, uint64_t out_cap, DevScalars *sc) {
+  const uint64_t n = sc->scratch[1];
+  const int64_t k_epoch = sc->k_epoch;
+  const bool unwin = p.kind == HSG_UNWINDOWED;
+  if (blockIdx.x == 0 && threadIdx.x == 0) sc->out_rows = n;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < n; q += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t o = out_base + q;
+    if (o >= out_cap) {
+      atomicOr(&sc->err, ERR_OOM);
+      break;
+    }
+    const uint32_t s = pb.touched[q];
+    const uint64_t g = t.keys[s];
+    const int64_t *row = t.aggs + (uint64_t)s * prog.n_slots;
+    out.key[o] = (uint32_t)(g >> 32);
+    int64_t ws = 0, we = 0;
+    if (!unwin) {
+      int64_t k = k_epoch + (int64_t)(g & 0xFFFFFFFFull);
+      ws = (int64_t)((uint64_t)k * (uint64_t)p.adv);
+      we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
+    }
+    out.ws[o] = ws;
+    out.we[o] = we;
+    out.src[o] = -1;
+    for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, row);
+  }
+}
+
+void launch_part_emit(hipStream_t s, const TwTable &t, const Program &prog, const TwParams &p, const PartBuffers &pb,
+                      OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc) {
+  hipLaunchKernelGGL(k_part_emit, dim3(2048), dim3(256), 0, s, t, prog, p, pb, out, out_base, out_cap, sc);
+}
+
 bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, const PartParams &pp, const TwTable &t,
                      const PartBuffers &pb, uint64_t n, DevScalars *sc) {
   if (!part_supported(prog)) return false;
   const uint64_t nb = 1ull << pp.np_log2;
-  uint32_t *chunk_start = pb.chunk_start;
-  hipLaunchKernelGGL(k_part_chunks, dim3(1), dim3(1024), 0, s, pb.off, pp.tiles, pp.np_log2, chunk_start);
+  hipLaunchKernelGGL(k_part_chunks, dim3(1), dim3(1024), 0, s, pb.off, pp.tiles, pp.np_log2, pb.chunk_start);
   const uint64_t grid = nb + n / kAggChunk + 1;
-  if (prog.n_slots <= 2)
-    hipLaunchKernelGGL((k_part_agg<2, 4096>), dim3((unsigned)grid), dim3(kAggThreads), 0, s, prog, p, pp, t, pb,
-                       chunk_start, sc);
-  else if (prog.n_slots <= 4)
-    hipLaunchKernelGGL((k_part_agg<4, 2048>), dim3((unsigned)grid), dim3(kAggThreads), 0, s, prog, p, pp, t, pb,
-                       chunk_start, sc);
-  else if (prog.n_slots <= 6)
-    hipLaunchKernelGGL((k_part_agg<6, 2048>), dim3((unsigned)grid), dim3(kAggThreads), 0, s, prog, p, pp, t, pb,
-                       chunk_start, sc);
-  else
-    hipLaunchKernelGGL((k_part_agg<8, 1024>), dim3((unsigned)grid), dim3(kAggThreads), 0, s, prog, p, pp, t, pb,
-                       chunk_start, sc);
+  const dim3 g((unsigned)grid), th(kAggThreads);
+  if (prog.n_slots <= 2) hipLaunchKernelGGL((k_part_agg<2, 4096>), g, th, 0, s, prog, p, pp, t, pb, sc);
+  else if (prog.n_slots <= 4) hipLaunchKernelGGL((k_part_agg<4, 2048>), g, th, 0, s, prog, p, pp, t, pb, sc);
+  else if (prog.n_slots <= 6) hipLaunchKernelGGL((k_part_agg<6, 2048>), g, th, 0, s, prog, p, pp, t, pb, sc);
+  else hipLaunchKernelGGL((k_part_agg<8, 1024>), g, th, 0, s, prog, p, pp, t, pb, sc);
   return true;
 }
 

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_stats(Batch b, int64_t *_
 // One workgroup: tile_prefix[t] = max(wm_in, tile_max[0..t-1]); sc->wm_out; epoch.
 __global__ __launch_bounds__(1024) void k_tile_scan(const int64_t *__restrict__ tmax, const int64_t *__restrict__ tmin,
                                                     int64_t *__restrict__ tprefix, uint64_t n_tiles, int64_t wm_in,
-                                                    int64_t adv, int set_epoch, DevScalars *sc) {
+                                                    int64_t adv, int set_epoch, int64_t grace, DevScalars *sc) {
   __shared__ int64_t swave[16];
   __shared__ int64_t swmin[16];
   const uint64_t per = (n_tiles + 1023) / 1024;
@@ -124,6 +124,12 @@ __global__ __launch_bounds__(1024) void k_tile_scan(const int64_t *__restrict__ 
       amin = swmin[k] < amin ? swmin[k] : amin;
     }
     sc->wm_out = all;
+    // every window of a record at ts t ends after t, so no window of this
+    // batch can fail the grace check while stream time <= min ts + grace
+    if (grace >= 0)
+      sc->no_late = (amin == INT64_MAX || amin > INT64_MAX - grace || all <= amin + grace) ? 1u : 0u;
+    else
+      sc->no_late = 0;
     if (set_epoch && !sc->epoch_set && amin != INT64_MAX) {
       int64_t k0 = amin / adv - (int64_t)(1ll << 31);
       sc->k_epoch = k0 > 0 ? k0 : 0;
@@ -136,9 +142,10 @@ void launch_tile_stats(hipStream_t s, const Batch &b, int64_t *tile_max, int64_t
   if (n_tiles) hipLaunchKernelGGL(k_tile_stats, dim3((unsigned)n_tiles), dim3(kTileThreads), 0, s, b, tile_max, tile_min);
 }
 void launch_tile_scan(hipStream_t s, const int64_t *tile_max, const int64_t *tile_min, int64_t *tile_prefix,
-                      uint64_t n_tiles, int64_t wm_in, int64_t adv, bool set_epoch, DevScalars *sc) {
+                      uint64_t n_tiles, int64_t wm_in, int64_t adv, bool set_epoch, DevScalars *sc,
+                      int64_t grace) {
   hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, tile_max, tile_min, tile_prefix, n_tiles, wm_in, adv,
-                     set_epoch ? 1 : 0, sc);
+                     set_epoch ? 1 : 0, grace, sc);
 }
 
 // ---------------------------------------------------------------------------

@@ -68,9 +68,9 @@ static void free_out(OutCols &o) {
 int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err) {
   PartBuffers &pb = d.part;
   const uint64_t n = d.batch_cap;
-  const uint64_t tiles = part_tiles(n) + 1;
+  const int words = part_words(cfg.n_cols, has_last(prog));
+  const uint64_t tiles = part_tiles(n, part_tile_for(words)) + 1;
   const uint64_t nh = (1ull << kPartMaxLog2) * tiles;
-  bool last = has_last(prog);
   uint64_t off = 0;
   auto take = [&](uint64_t bytes) {
     off = (off + 255) & ~255ull;
@@ -79,30 +79,17 @@ int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog,
     return o;
   };
   uint64_t o_hist = take(nh * 4), o_off = take((nh + 1) * 8), o_part = take((scan_partials_needed(nh) + 8) * 8);
-  uint64_t o_total = take(64), o_key = take(n * 4), o_krel = take(n * 4), o_nwin = take(n * 4);
-  uint64_t o_col[kMaxCols], o_valid[kMaxCols];
-  for (int c = 0; c < cfg.n_cols; ++c) {
-    o_col[c] = take(n * 8);
-    o_valid[c] = take(n);
-  }
-  uint64_t o_seq = take(last ? n * 8 : 8), o_chunk = take(((1ull << kPartMaxLog2) + 1) * 4);
+  uint64_t o_rec = take(n * words * 8), o_chunk = take(((1ull << kPartMaxLog2) + 1) * 4);
+  uint64_t o_touch = take(d.cap * 4);
   DTRY(hipMalloc(&d.part_mem, off));
   char *m = (char *)d.part_mem;
   pb.hist = (uint32_t *)(m + o_hist);
   pb.off = (uint64_t *)(m + o_off);
   pb.partial = (uint64_t *)(m + o_part);
-  pb.total = (uint64_t *)(m + o_total);
-  pb.key = (uint32_t *)(m + o_key);
-  pb.krel = (uint32_t *)(m + o_krel);
-  pb.nwin = (uint32_t *)(m + o_nwin);
-  for (int c = 0; c < kMaxCols; ++c) {
-    pb.col[c] = c < cfg.n_cols ? (int64_t *)(m + o_col[c]) : nullptr;
-    pb.valid[c] = c < cfg.n_cols ? (uint8_t *)(m + o_valid[c]) : nullptr;
-  }
-  pb.seq1 = (int64_t *)(m + o_seq);
+  pb.rec = (uint64_t *)(m + o_rec);
   pb.chunk_start = (uint32_t *)(m + o_chunk);
+  pb.touched = (uint32_t *)(m + o_touch);
   pb.n_cap = n;
-  pb.tiles_cap = tiles;
   return HSG_OK;
 }
 
@@ -111,6 +98,10 @@ int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog,
 static void adapt_partitions(OpDevice &d, const Program &prog, uint64_t groups, uint64_t n) {
   const uint64_t per = part_lds_entries(prog) / 2;
   uint64_t want = (groups + per - 1) / per;
+  // and buckets of about half a chunk, so nearly every bucket is owned by one
+  // workgroup (plain read-modify-write flush)
+  const uint64_t by_size = (2 * n + kAggChunk - 1) / kAggChunk;
+  if (by_size > want) want = by_size;
   uint64_t cap_by_n = n / 2048 > 1 ? n / 2048 : 1;
   if (want > cap_by_n) want = cap_by_n;
   int l = 0;
@@ -311,8 +302,9 @@ TwParams make_tw_params(const hsg_op_config &cfg, const PushArgs &a) {
 void launch_stream_time(OpDevice &d, const hsg_op_config &cfg, const Batch &kb, int64_t wm_in, int64_t adv) {
   uint64_t tiles = (kb.n + kTileRecords - 1) / kTileRecords;
   launch_tile_stats(d.stream, kb, d.tile_max, d.tile_min, tiles);
-  launch_tile_scan(d.stream, d.tile_max, d.tile_min, d.tile_prefix, tiles, wm_in, adv,
-                   cfg.window_kind == HSG_TUMBLING || cfg.window_kind == HSG_HOPPING, d.sc);
+  const bool tw = cfg.window_kind == HSG_TUMBLING || cfg.window_kind == HSG_HOPPING;
+  launch_tile_scan(d.stream, d.tile_max, d.tile_min, d.tile_prefix, tiles, wm_in, adv, tw, d.sc,
+                   tw ? (cfg.grace_ms >= 0 ? cfg.grace_ms : 0) : -1);
 }
 
 int fetch_scalars(OpDevice &d, std::string &err) {
@@ -372,7 +364,9 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       pp.np_log2 = d.np_log2;
       for (int c = 0; c < cfg.n_cols; ++c) pp.has_valid |= kb.valid[c] != nullptr;
       pp.has_seq = has_last(prog);
-      pp.tiles = part_tiles(kb.n);
+      pp.words = part_words(cfg.n_cols, pp.has_seq);
+      pp.tile = part_tile_for(pp.words);
+      pp.tiles = part_tiles(kb.n, pp.tile);
       const uint64_t nh = (1ull << pp.np_log2) * pp.tiles;
       launch_part_hist(d.stream, kb, p, pp, d.tile_prefix, rec_wm, d.part, d.sc);
       scan_excl_u32(d.stream, d.part.hist, d.part.off, nh, d.part.partial, d.part.off + nh);
@@ -383,9 +377,13 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     }
     DTRY(hipEventRecord(d.ev_b, d.stream));
     if (has_last(prog)) launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, true);
-    if (cfg.emit_mode == HSG_EMIT_PER_BATCH)
-      launch_tw_emit(d.stream, d.tw, d.cap, prog, p, 0, d.out, a.pending, d.out_cap, d.sc, d.emit,
-                     (uint64_t *)&d.sc->out_rows);
+    if (cfg.emit_mode == HSG_EMIT_PER_BATCH) {
+      if (d.use_part)
+        launch_part_emit(d.stream, d.tw, prog, p, d.part, d.out, a.pending, d.out_cap, d.sc);
+      else
+        launch_tw_emit(d.stream, d.tw, d.cap, prog, p, 0, d.out, a.pending, d.out_cap, d.sc, d.emit,
+                       (uint64_t *)&d.sc->out_rows);
+    }
     DTRY(hipGetLastError());
   }
   rc = finish_batch(d, a.wm_in, kb.n, r, err);
