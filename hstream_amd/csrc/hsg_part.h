@@ -23,6 +23,7 @@ struct PartBuffers {
   uint64_t *rec;          // [n * words] partitioned records
   uint32_t *chunk_start;  // [np + 1] first aggregation workgroup of each bucket
   uint32_t *touched;      // [table slots] groups first touched by this batch (length: sc->scratch[1])
+  int64_t *wm;            // [n] per-record stream time (written only when late records are possible)
   uint64_t n_cap;
 };
 
@@ -37,13 +38,17 @@ struct PartParams {
 };
 
 inline int part_words(int n_cols, bool has_seq) { return 2 + n_cols + (has_seq ? 1 : 0); }
-inline int part_tile_for(int words) { return words <= 3 ? 4096 : words <= 7 ? 2048 : 1024; }
+constexpr int kPartTileRecs = 4096;                   // records per partition-pass workgroup
+inline int part_tile_for(int) { return kPartTileRecs; }
 inline uint64_t part_tiles(uint64_t n, int tile) { return (n + tile - 1) / tile; }
 
-void launch_part_hist(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp,
-                      const int64_t *tprefix, const int64_t *rec_wm, const PartBuffers &pb, DevScalars *sc);
+// per-record stream time into wm unless sc->no_late (decided by launch_tile_scan)
+void launch_part_recwm(hipStream_t s, const Batch &b, const int64_t *tprefix, const DevScalars *sc, int64_t *wm);
+// rec_wm: per-record stream time from a key exchange (else own_wm / none)
+void launch_part_hist(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp, const int64_t *rec_wm,
+                      const int64_t *own_wm, const PartBuffers &pb, DevScalars *sc);
 void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp,
-                         const int64_t *tprefix, const int64_t *rec_wm, const int64_t *seq, const PartBuffers &pb,
+                         const int64_t *rec_wm, const int64_t *own_wm, const int64_t *seq, const PartBuffers &pb,
                          DevScalars *sc);
 // returns false when the op's slot count has no LDS variant (caller falls back)
 bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, const PartParams &pp, const TwTable &t,

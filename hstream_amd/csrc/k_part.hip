@@ -66,113 +66,126 @@ __device__ inline uint64_t xcd_tile(uint64_t blk, uint64_t tiles) {
   return (blk & 7) * per + (blk >> 3);
 }
 
-// Walk the T records of one partition tile in stream-time sub-tiles; calls
-// f(j, i, key, krel, nwin) for every record with >= 1 accepted window, where
-// j = tile-local index and i = batch index. Block-wide (barriers inside).
-template <int T, typename F>
-__device__ inline void walk_tile(const Batch &b, const TwParams &p, const PartParams &pp,
-                                 const int64_t *__restrict__ tprefix, const int64_t *__restrict__ rec_wm,
-                                 uint64_t tile, int64_t k_epoch, uint64_t &late, uint32_t &err, F f,
-                                 bool no_late) {
-  constexpr int kSub = T / kTileRecords;
-  for (int sub = 0; sub < kSub; ++sub) {
-    const uint64_t st = tile * kSub + sub;  // stream-time tile
-    const uint64_t base = st * kTileRecords;
-    if (base >= b.n) break;  // uniform across the workgroup
-    uint32_t key[kRecPerThread];
-    int64_t ts[kRecPerThread], wm[kRecPerThread];
+// Per-record stream time in arrival order, only when some record of the batch
+// may fail the grace check (sc->no_late == 0); otherwise every workgroup exits.
+__global__ __launch_bounds__(kTileThreads) void k_part_recwm(Batch b, const int64_t *__restrict__ tprefix,
+                                                             const DevScalars *sc, int64_t *__restrict__ wm_out) {
+  if (sc->no_late) return;  // uniform
+  const uint64_t base = (uint64_t)blockIdx.x * kTileRecords;
+  int64_t ts[kRecPerThread], wm[kRecPerThread];
 #pragma unroll
-    for (int r = 0; r < kRecPerThread; ++r) {
-      uint64_t i = base + (uint64_t)r * kTileThreads + threadIdx.x;
-      bool in = i < b.n;
-      key[r] = in ? b.key[i] : HSG_KEY_NONE;
-      ts[r] = in ? b.ts[i] : INT64_MIN;
-      if (rec_wm) wm[r] = in ? rec_wm[i] : INT64_MIN;
-      if (no_late && !rec_wm) wm[r] = INT64_MIN;  // every window is accepted: skip the scan
-    }
-    if (!rec_wm && !no_late) tile_stream_time(ts, tprefix[st], wm);
+  for (int r = 0; r < kRecPerThread; ++r) {
+    uint64_t i = base + (uint64_t)r * kTileThreads + threadIdx.x;
+    ts[r] = i < b.n ? b.ts[i] : INT64_MIN;
+  }
+  tile_stream_time(ts, tprefix[blockIdx.x], wm);
 #pragma unroll
-    for (int r = 0; r < kRecPerThread; ++r) {
-      uint32_t krel, nwin;
-      if (!part_record(p, k_epoch, key[r], ts[r], wm[r], krel, nwin, late, err)) continue;
-      const int j = sub * kTileRecords + r * kTileThreads + threadIdx.x;
-      f(j, base + (uint64_t)r * kTileThreads + threadIdx.x, key[r], krel, nwin);
-    }
+  for (int r = 0; r < kRecPerThread; ++r) {
+    uint64_t i = base + (uint64_t)r * kTileThreads + threadIdx.x;
+    if (i < b.n) wm_out[i] = wm[r];
   }
 }
 
+void launch_part_recwm(hipStream_t s, const Batch &b, const int64_t *tprefix, const DevScalars *sc, int64_t *wm) {
+  uint64_t tiles = (b.n + kTileRecords - 1) / kTileRecords;
+  if (tiles) hipLaunchKernelGGL(k_part_recwm, dim3((unsigned)tiles), dim3(kTileThreads), 0, s, b, tprefix, sc, wm);
+}
+
+// stream time source: the exchange's per-record times, else our own unless no
+// record can be late (then every window is accepted and none is needed)
+__device__ inline const int64_t *pick_wm(const int64_t *rec_wm, const int64_t *own, const DevScalars *sc) {
+  return rec_wm ? rec_wm : (sc->no_late ? nullptr : own);
+}
+
+// Walk the T records of one partition tile with NT threads (record (r, t) =
+// tile*T + r*NT + t); calls f(j, i, key, krel, nwin) for every record with
+// >= 1 accepted window (j = tile-local index, i = batch index). No barriers.
+template <int T, int NT, typename F>
+__device__ inline void walk_tile(const Batch &b, const TwParams &p, uint64_t tile, int64_t k_epoch,
+                                 const int64_t *__restrict__ wm, uint64_t &late, uint32_t &err, F f) {
+  const uint64_t base = tile * T;
+#pragma unroll 4
+  for (int r = 0; r < T / NT; ++r) {
+    const int j = r * NT + threadIdx.x;
+    const uint64_t i = base + j;
+    if (i >= b.n) break;
+    const uint32_t key = b.key[i];
+    const int64_t ts = b.ts[i];
+    const int64_t w = wm ? wm[i] : INT64_MIN;
+    uint32_t krel, nwin;
+    if (!part_record(p, k_epoch, key, ts, w, krel, nwin, late, err)) continue;
+    f(j, i, key, krel, nwin);
+  }
+}
+
+constexpr int kPNT = 512;  // threads of the partition passes
+
 template <int T>
-__global__ __launch_bounds__(kPartThreads) void k_part_hist(Batch b, TwParams p, PartParams pp,
-                                                            const int64_t *__restrict__ tprefix,
-                                                            const int64_t *__restrict__ rec_wm, PartBuffers pb,
-                                                            DevScalars *sc) {
+__global__ __launch_bounds__(kPNT) void k_part_hist(Batch b, TwParams p, PartParams pp,
+                                                    const int64_t *__restrict__ rec_wm,
+                                                    const int64_t *__restrict__ own_wm, PartBuffers pb,
+                                                    DevScalars *sc) {
   __shared__ uint32_t cnt[1 << kPartMaxLog2];
-  __shared__ uint64_t sred[kPartThreads / 64];
+  __shared__ uint64_t sred[kPNT / 64];
   const int nb = 1 << pp.np_log2;
   const uint64_t tile = xcd_tile(blockIdx.x, pp.tiles);
-  for (int i = threadIdx.x; i < nb; i += kPartThreads) cnt[i] = 0;
+  for (int i = threadIdx.x; i < nb; i += kPNT) cnt[i] = 0;
   __syncthreads();
   uint64_t late = 0;
   uint32_t err = 0;
-  walk_tile<T>(b, p, pp, tprefix, rec_wm, tile, sc->k_epoch, late, err,
-               [&](int, uint64_t, uint32_t key, uint32_t, uint32_t) { atomicAdd(&cnt[bucket_of(key, pp.np_log2)], 1u); },
-               sc->no_late != 0);
+  walk_tile<T, kPNT>(b, p, tile, sc->k_epoch, pick_wm(rec_wm, own_wm, sc), late, err,
+                     [&](int, uint64_t, uint32_t key, uint32_t, uint32_t) {
+                       atomicAdd(&cnt[bucket_of(key, pp.np_log2)], 1u);
+                     });
   __syncthreads();
-  for (int i = threadIdx.x; i < nb; i += kPartThreads) pb.hist[(uint64_t)i * pp.tiles + tile] = cnt[i];
+  for (int i = threadIdx.x; i < nb; i += kPNT) pb.hist[(uint64_t)i * pp.tiles + tile] = cnt[i];
   late = wave_sum_u64(late);
   if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = late;
   if (err) atomicOr(&sc->err, err);
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t l = 0;
-    for (int k = 0; k < kPartThreads / 64; ++k) l += sred[k];
+    for (int k = 0; k < kPNT / 64; ++k) l += sred[k];
     if (l) atomicAdd((unsigned long long *)&sc->late, (unsigned long long)l);
   }
 }
 
-template <int T, int WMAX>
-__global__ __launch_bounds__(kPartThreads) void k_part_scatter(Batch b, TwParams p, PartParams pp,
-                                                               const int64_t *__restrict__ tprefix,
-                                                               const int64_t *__restrict__ rec_wm,
-                                                               const int64_t *__restrict__ seq, PartBuffers pb,
-                                                               DevScalars *sc) {
-  __shared__ uint64_t stage[T * WMAX];
+// LDS holds only the tile's bucket sort (bucket, order, window run per record:
+// 12 B) plus per-bucket run starts, so two workgroups fit a CU; the record
+// words are gathered from the (L2-resident) input at write-out.
+template <int T>
+__global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, PartParams pp,
+                                                       const int64_t *__restrict__ rec_wm,
+                                                       const int64_t *__restrict__ own_wm,
+                                                       const int64_t *__restrict__ seq, PartBuffers pb,
+                                                       DevScalars *sc) {
   __shared__ uint16_t lbk[T];
   __shared__ uint16_t sidx[T];
+  __shared__ uint64_t lkn[T];  // krel | nwin << 32
   __shared__ uint32_t lstart[1 << kPartMaxLog2];
   __shared__ uint32_t cursor[1 << kPartMaxLog2];
-  __shared__ uint64_t goff[1 << kPartMaxLog2];
-  __shared__ uint32_t swave[kPartThreads / 64];
+  __shared__ uint32_t goff[1 << kPartMaxLog2];
+  __shared__ uint32_t swave[kPNT / 64];
   const int nb = 1 << pp.np_log2;
   const int W = pp.words;
   const int C = W - 2 - pp.has_seq;
   const uint64_t tile = xcd_tile(blockIdx.x, pp.tiles);
-  for (int i = threadIdx.x; i < nb; i += kPartThreads) cursor[i] = 0;
-  for (int j = threadIdx.x; j < T; j += kPartThreads) lbk[j] = kNoBucket;
+  for (int i = threadIdx.x; i < nb; i += kPNT) cursor[i] = 0;
+  for (int j = threadIdx.x; j < T; j += kPNT) lbk[j] = kNoBucket;
   __syncthreads();
-  // 1) records -> LDS in arrival order, bucket histogram
+  // 1) window runs and buckets of the tile's records, bucket histogram
   uint64_t late = 0;
   uint32_t err = 0;
-  walk_tile<T>(b, p, pp, tprefix, rec_wm, tile, sc->k_epoch, late, err,
-               [&](int j, uint64_t i, uint32_t key, uint32_t krel, uint32_t nwin) {
-                 const uint32_t bk = bucket_of(key, pp.np_log2);
-                 uint64_t vb = 0;
-                 uint64_t *w = &stage[j * WMAX];
-                 for (int c = 0; c < C; ++c) {
-                   w[2 + c] = (uint64_t)b.col[c][i];
-                   if (pp.has_valid && b.valid[c] && !b.valid[c][i]) continue;
-                   vb |= 1ull << c;
-                 }
-                 w[0] = (uint64_t)key | ((uint64_t)krel << 32);
-                 w[1] = (uint64_t)nwin | (vb << 32);
-                 if (pp.has_seq) w[2 + C] = (uint64_t)((seq ? seq[i] : (int64_t)(p.rec_base + i)) + 1);
-                 lbk[j] = (uint16_t)bk;
-                 atomicAdd(&cursor[bk], 1u);
-               },
-               sc->no_late != 0);
+  walk_tile<T, kPNT>(b, p, tile, sc->k_epoch, pick_wm(rec_wm, own_wm, sc), late, err,
+                     [&](int j, uint64_t, uint32_t key, uint32_t krel, uint32_t nwin) {
+                       const uint32_t bk = bucket_of(key, pp.np_log2);
+                       lkn[j] = (uint64_t)krel | ((uint64_t)nwin << 32);
+                       lbk[j] = (uint16_t)bk;
+                       atomicAdd(&cursor[bk], 1u);
+                     });
   __syncthreads();
   // 2) tile-local exclusive scan of the histogram; global run starts
-  const int per = (nb + kPartThreads - 1) / kPartThreads;
+  const int per = (nb + kPNT - 1) / kPNT;
   const int lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
   uint32_t loc = 0;
   for (int k = lo; k < hi; ++k) loc += cursor[k];
@@ -191,56 +204,59 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(Batch b, TwParams
     lstart[k] = run;
     run += cursor[k];
     cursor[k] = 0;
-    goff[k] = pb.off[(uint64_t)k * pp.tiles + tile];
+    goff[k] = (uint32_t)pb.off[(uint64_t)k * pp.tiles + tile];
   }
-  const uint32_t placed = swave[0] + swave[1] + swave[2] + swave[3];
+  uint32_t placed = 0;
+  for (int k = 0; k < kPNT / 64; ++k) placed += swave[k];
   __syncthreads();
-  // 3) bucket-sorted order of the staged records
-  for (int j = threadIdx.x; j < T; j += kPartThreads) {
+  // 3) bucket-sorted order of the tile's records
+  for (int j = threadIdx.x; j < T; j += kPNT) {
     const uint16_t bk = lbk[j];
     if (bk == kNoBucket) continue;
     sidx[lstart[bk] + atomicAdd(&cursor[bk], 1u)] = (uint16_t)j;
   }
   __syncthreads();
   // 4) coalesced write-out: consecutive lanes write consecutive words of a run
-  const uint32_t inv = (1u << 20) / (uint32_t)W + 1;  // t / W for t < 16384, W <= 64
+  const uint32_t inv = (1u << 20) / (uint32_t)W + 1;  // t / W for t < 2^16, W <= 16
   const uint32_t total = placed * (uint32_t)W;
-  for (uint32_t t = threadIdx.x; t < total; t += kPartThreads) {
+  const uint64_t base = tile * T;
+  for (uint32_t t = threadIdx.x; t < total; t += kPNT) {
     const uint32_t q = (uint32_t)(((uint64_t)t * inv) >> 20);
     const uint32_t w = t - q * (uint32_t)W;
     const uint16_t j = sidx[q];
     const uint16_t bk = lbk[j];
-    const uint64_t dest = goff[bk] + (q - lstart[bk]);
-    pb.rec[dest * W + w] = stage[j * WMAX + w];
+    const uint64_t i = base + j;
+    const uint64_t dest = (uint64_t)goff[bk] + (q - lstart[bk]);
+    uint64_t v;
+    if (w == 0) {
+      v = (uint64_t)b.key[i] | (lkn[j] << 32);
+    } else if (w == 1) {
+      uint64_t vb = 0;
+      for (int c = 0; c < C; ++c)
+        if (!(pp.has_valid && b.valid[c] && !b.valid[c][i])) vb |= 1ull << c;
+      v = (lkn[j] >> 32) | (vb << 32);
+    } else if ((int)w < 2 + C) {
+      v = (uint64_t)b.col[w - 2][i];
+    } else {
+      v = (uint64_t)((seq ? seq[i] : (int64_t)(p.rec_base + i)) + 1);
+    }
+    pb.rec[dest * W + w] = v;
   }
 }
 
-template <int T>
-static void hist_launch(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp, const int64_t *tprefix,
-                        const int64_t *rec_wm, const PartBuffers &pb, DevScalars *sc) {
-  hipLaunchKernelGGL(k_part_hist<T>, dim3((unsigned)pp.tiles), dim3(kPartThreads), 0, s, b, p, pp, tprefix, rec_wm,
+void launch_part_hist(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp, const int64_t *rec_wm,
+                      const int64_t *own_wm, const PartBuffers &pb, DevScalars *sc) {
+  if (!pp.tiles) return;
+  hipLaunchKernelGGL(k_part_hist<kPartTileRecs>, dim3((unsigned)pp.tiles), dim3(kPNT), 0, s, b, p, pp, rec_wm, own_wm,
                      pb, sc);
 }
 
-void launch_part_hist(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp,
-                      const int64_t *tprefix, const int64_t *rec_wm, const PartBuffers &pb, DevScalars *sc) {
-  if (!pp.tiles) return;
-  if (pp.tile == 4096) hist_launch<4096>(s, b, p, pp, tprefix, rec_wm, pb, sc);
-  else if (pp.tile == 2048) hist_launch<2048>(s, b, p, pp, tprefix, rec_wm, pb, sc);
-  else hist_launch<1024>(s, b, p, pp, tprefix, rec_wm, pb, sc);
-}
-
 void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp,
-                         const int64_t *tprefix, const int64_t *rec_wm, const int64_t *seq, const PartBuffers &pb,
+                         const int64_t *rec_wm, const int64_t *own_wm, const int64_t *seq, const PartBuffers &pb,
                          DevScalars *sc) {
   if (!pp.tiles) return;
-  const dim3 g((unsigned)pp.tiles), t(kPartThreads);
-  if (pp.tile == 4096)
-    hipLaunchKernelGGL((k_part_scatter<4096, 3>), g, t, 0, s, b, p, pp, tprefix, rec_wm, seq, pb, sc);
-  else if (pp.tile == 2048)
-    hipLaunchKernelGGL((k_part_scatter<2048, 7>), g, t, 0, s, b, p, pp, tprefix, rec_wm, seq, pb, sc);
-  else
-    hipLaunchKernelGGL((k_part_scatter<1024, 11>), g, t, 0, s, b, p, pp, tprefix, rec_wm, seq, pb, sc);
+  hipLaunchKernelGGL(k_part_scatter<kPartTileRecs>, dim3((unsigned)pp.tiles), dim3(kPNT), 0, s, b, p, pp, rec_wm,
+                     own_wm, seq, pb, sc);
 }
 
 // ---------------------------------------------------------------------------

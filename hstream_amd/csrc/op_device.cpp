@@ -80,7 +80,7 @@ int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog,
   };
   uint64_t o_hist = take(nh * 4), o_off = take((nh + 1) * 8), o_part = take((scan_partials_needed(nh) + 8) * 8);
   uint64_t o_rec = take(n * words * 8), o_chunk = take(((1ull << kPartMaxLog2) + 1) * 4);
-  uint64_t o_touch = take(d.cap * 4);
+  uint64_t o_touch = take(d.cap * 4), o_wm = take(n * 8);
   DTRY(hipMalloc(&d.part_mem, off));
   char *m = (char *)d.part_mem;
   pb.hist = (uint32_t *)(m + o_hist);
@@ -89,6 +89,7 @@ int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog,
   pb.rec = (uint64_t *)(m + o_rec);
   pb.chunk_start = (uint32_t *)(m + o_chunk);
   pb.touched = (uint32_t *)(m + o_touch);
+  pb.wm = (int64_t *)(m + o_wm);
   pb.n_cap = n;
   return HSG_OK;
 }
@@ -368,9 +369,10 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       pp.tile = part_tile_for(pp.words);
       pp.tiles = part_tiles(kb.n, pp.tile);
       const uint64_t nh = (1ull << pp.np_log2) * pp.tiles;
-      launch_part_hist(d.stream, kb, p, pp, d.tile_prefix, rec_wm, d.part, d.sc);
+      if (!rec_wm) launch_part_recwm(d.stream, kb, d.tile_prefix, d.sc, d.part.wm);
+      launch_part_hist(d.stream, kb, p, pp, rec_wm, d.part.wm, d.part, d.sc);
       scan_excl_u32(d.stream, d.part.hist, d.part.off, nh, d.part.partial, d.part.off + nh);
-      launch_part_scatter(d.stream, kb, p, pp, d.tile_prefix, rec_wm, seq, d.part, d.sc);
+      launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc);
       launch_part_agg(d.stream, prog, p, pp, d.tw, d.part, kb.n, d.sc);
     } else {
       launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, false);

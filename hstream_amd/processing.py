@@ -276,7 +276,7 @@ class Table:
             if a.kind != abi.HSG_COUNT_ALL and (a.field, a.is_float) not in fields:
                 fields.append((a.field, a.is_float))
         self.fields = fields
-        col_of = {f: i for i, (f, _) in enumerate(fields)}
+        col_of = {fk: i for i, fk in enumerate(fields)}
         spec.col_types = [abi.HSG_F64 if fl else abi.HSG_I64 for _, fl in fields]
         spec.aggs = [(a.kind, col_of[(a.field, a.is_float)] if a.kind != abi.HSG_COUNT_ALL else 0) for a in self.aggs]
         spec.state_capacity = materialized.state_capacity
