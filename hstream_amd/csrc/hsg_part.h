@@ -9,9 +9,9 @@ namespace hsg {
 
 constexpr int kPartThreads = 256;
 constexpr int kPartMaxLog2 = 11;                      // up to 2048 partitions
-constexpr int kAggThreads = 1024;
+constexpr int kAggThreads = 512;
 constexpr int kPartMaxWords = 11;                     // 2 + 8 columns + seq
-constexpr uint64_t kAggChunk = 16384;                 // records per aggregation workgroup
+constexpr uint64_t kAggChunk = 8192;                  // records per aggregation workgroup
 
 // A partitioned record is `words` 8-byte words:
 //   [key | krel << 32] [nwin | valid bits << 32] [col 0 .. C-1] [seq + 1]?
@@ -58,7 +58,7 @@ bool part_supported(const Program &prog);
 void launch_part_emit(hipStream_t s, const TwTable &t, const Program &prog, const TwParams &p, const PartBuffers &pb,
                       OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc);
 inline uint64_t part_lds_entries(const Program &prog) {
-  return prog.n_slots <= 2 ? 4096 : prog.n_slots <= 6 ? 2048 : 1024;
+  return prog.n_slots <= 2 ? 2048 : 1024;
 }
 
 }  // namespace hsg

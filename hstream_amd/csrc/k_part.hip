@@ -103,18 +103,25 @@ __device__ inline const int64_t *pick_wm(const int64_t *rec_wm, const int64_t *o
 template <int T, int NT, typename F>
 __device__ inline void walk_tile(const Batch &b, const TwParams &p, uint64_t tile, int64_t k_epoch,
                                  const int64_t *__restrict__ wm, uint64_t &late, uint32_t &err, F f) {
+  constexpr int R = T / NT;
   const uint64_t base = tile * T;
-#pragma unroll 4
-  for (int r = 0; r < T / NT; ++r) {
+  // every load of the tile is issued before the first record is processed
+  uint32_t key[R];
+  int64_t ts[R], w[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint64_t i = base + (uint64_t)r * NT + threadIdx.x;
+    const bool in = i < b.n;
+    key[r] = in ? b.key[i] : HSG_KEY_NONE;
+    ts[r] = in ? b.ts[i] : 0;
+    w[r] = in && wm ? wm[i] : INT64_MIN;
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
     const int j = r * NT + threadIdx.x;
-    const uint64_t i = base + j;
-    if (i >= b.n) break;
-    const uint32_t key = b.key[i];
-    const int64_t ts = b.ts[i];
-    const int64_t w = wm ? wm[i] : INT64_MIN;
     uint32_t krel, nwin;
-    if (!part_record(p, k_epoch, key, ts, w, krel, nwin, late, err)) continue;
-    f(j, i, key, krel, nwin);
+    if (!part_record(p, k_epoch, key[r], ts[r], w[r], krel, nwin, late, err)) continue;
+    f(j, base + j, key[r], krel, nwin);
   }
 }
 
@@ -170,6 +177,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
   const int W = pp.words;
   const int C = W - 2 - pp.has_seq;
   const uint64_t tile = xcd_tile(blockIdx.x, pp.tiles);
+  const uint64_t q0 = wall_clock64();
   for (int i = threadIdx.x; i < nb; i += kPNT) cursor[i] = 0;
   for (int j = threadIdx.x; j < T; j += kPNT) lbk[j] = kNoBucket;
   __syncthreads();
@@ -184,6 +192,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
                        atomicAdd(&cursor[bk], 1u);
                      });
   __syncthreads();
+  const uint64_t q1 = wall_clock64();
   // 2) tile-local exclusive scan of the histogram; global run starts
   const int per = (nb + kPNT - 1) / kPNT;
   const int lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
@@ -209,6 +218,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
   uint32_t placed = 0;
   for (int k = 0; k < kPNT / 64; ++k) placed += swave[k];
   __syncthreads();
+  const uint64_t q2 = wall_clock64();
   // 3) bucket-sorted order of the tile's records
   for (int j = threadIdx.x; j < T; j += kPNT) {
     const uint16_t bk = lbk[j];
@@ -216,10 +226,12 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
     sidx[lstart[bk] + atomicAdd(&cursor[bk], 1u)] = (uint16_t)j;
   }
   __syncthreads();
+  const uint64_t q3 = wall_clock64();
   // 4) coalesced write-out: consecutive lanes write consecutive words of a run
   const uint32_t inv = (1u << 20) / (uint32_t)W + 1;  // t / W for t < 2^16, W <= 16
   const uint32_t total = placed * (uint32_t)W;
   const uint64_t base = tile * T;
+#pragma unroll 4
   for (uint32_t t = threadIdx.x; t < total; t += kPNT) {
     const uint32_t q = (uint32_t)(((uint64_t)t * inv) >> 20);
     const uint32_t w = t - q * (uint32_t)W;
@@ -241,6 +253,15 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
       v = (uint64_t)((seq ? seq[i] : (int64_t)(p.rec_base + i)) + 1);
     }
     pb.rec[dest * W + w] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t q4 = wall_clock64();
+    atomicAdd((unsigned long long *)&sc->scratch[13], (unsigned long long)(q1 - q0));
+    atomicAdd((unsigned long long *)&sc->scratch[14], (unsigned long long)(q2 - q1));
+    atomicAdd((unsigned long long *)&sc->scratch[15], (unsigned long long)(q3 - q2));
+    atomicAdd((unsigned long long *)&sc->scratch[16], (unsigned long long)(q4 - q3));
+    atomicAdd((unsigned long long *)&sc->scratch[17], 1ull);
   }
 }
 
@@ -299,19 +320,27 @@ __global__ __launch_bounds__(1024) void k_part_chunks(const uint64_t *off, uint6
 // ---------------------------------------------------------------------------
 // LDS aggregation of one chunk
 // ---------------------------------------------------------------------------
-// One partitioned record: word 1 (window count + presence bits) in a register,
-// columns / sequence read from HBM (same cache line as words 0-1 mostly).
+// One partitioned record held in registers: [w0 w1 col 0..C-1 seq+1?]. Runtime
+// word selection is an unrolled compare chain, so the record never leaves VGPRs.
+template <int WMAX>
 struct PRec {
-  const uint64_t *w;
-  uint64_t w1;
+  uint64_t w[WMAX];
   int C;
-  __device__ bool present(int c) const { return (w1 >> (32 + c)) & 1ull; }
-  __device__ int64_t col(int c) const { return (int64_t)w[2 + c]; }
-  __device__ int64_t seq1() const { return (int64_t)w[2 + C]; }
+  __device__ bool present(int c) const { return (w[1] >> (32 + c)) & 1ull; }
+  __device__ int64_t word(int k) const {
+    int64_t v = 0;
+#pragma unroll
+    for (int q = 2; q < WMAX; ++q)
+      if (q == k) v = (int64_t)w[q];
+    return v;
+  }
+  __device__ int64_t col(int c) const { return word(2 + c); }
+  __device__ int64_t seq1() const { return word(2 + C); }
 };
 
 // contribution of the record to slot s (identity when absent)
-__device__ inline int64_t prec_elem(const Program &prog, int s, const PRec &r) {
+template <typename R>
+__device__ inline int64_t prec_elem(const Program &prog, int s, const R &r) {
   const int op = prog.slot_op[s];
   const int c = prog.slot_col[s];
   if (op == S_CNT_ALL) return 1;
@@ -330,8 +359,11 @@ __device__ inline int64_t prec_elem(const Program &prog, int s, const PRec &r) {
   }
 }
 
-__device__ inline void lds_apply(const Program &prog, int64_t *__restrict__ row, const PRec &r) {
-  for (int s = 0; s < prog.n_slots; ++s) {
+template <int MS, typename R>
+__device__ inline void lds_apply(const Program &prog, int64_t *__restrict__ row, const R &r) {
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    if (s >= prog.n_slots) break;
     const int op = prog.slot_op[s];
     if (op == S_LAST_VAL) continue;
     if (op != S_CNT_ALL && !r.present(prog.slot_col[s])) continue;
@@ -379,8 +411,8 @@ __device__ inline void flush_row(const Program &prog, int64_t *__restrict__ row,
   }
 }
 
-template <int MS, int E>
-__global__ __launch_bounds__(kAggThreads) void k_part_agg(Program prog, TwParams p, PartParams pp, TwTable t,
+template <int MS, int E, int WMAX, int KU>
+__global__ __launch_bounds__(kAggThreads, 4) void k_part_agg(Program prog, TwParams p, PartParams pp, TwTable t,
                                                           PartBuffers pb, DevScalars *sc) {
   __shared__ uint64_t lkey[E];
   __shared__ int64_t lagg[E * MS];
@@ -389,9 +421,12 @@ __global__ __launch_bounds__(kAggThreads) void k_part_agg(Program prog, TwParams
   __shared__ uint64_t sred[3][kAggThreads / 64];
   __shared__ uint32_t ltouch[E];  // slots this workgroup touched first in this batch
   __shared__ uint32_t ltn;
+  __shared__ uint16_t llive[E];   // live entries of the LDS table, compacted
+  __shared__ uint32_t lnl;
   __shared__ uint64_t lbase;
   const int nb = 1 << pp.np_log2;
   const uint32_t *chunk_start = pb.chunk_start;
+  const uint64_t t0 = wall_clock64();
   if (threadIdx.x == 0) {
     // find this workgroup's bucket: chunk_start[b] <= blockIdx.x < chunk_start[b + 1]
     uint32_t w = blockIdx.x;
@@ -406,6 +441,7 @@ __global__ __launch_bounds__(kAggThreads) void k_part_agg(Program prog, TwParams
     sc1 = chunk_start[lo + 1];
     lfill = 0;
     ltn = 0;
+    lnl = 0;
   }
   for (int e = threadIdx.x; e < E; e += kAggThreads) {
     lkey[e] = kEmpty;
@@ -422,25 +458,30 @@ __global__ __launch_bounds__(kAggThreads) void k_part_agg(Program prog, TwParams
   const uint32_t limit = (uint32_t)(E * 3 / 4);
   const int W = pp.words;
   const int C = W - 2 - pp.has_seq;
+  const uint64_t t1 = wall_clock64();
   uint64_t pairs = 0;
   uint32_t fresh = 0, err = 0;
-  constexpr int kU = 4;  // records loaded per thread before any is processed
-  for (uint64_t i0 = r0 + threadIdx.x; i0 < r1; i0 += (uint64_t)kAggThreads * kU) {
-    uint64_t b0[kU], b1[kU];
+  // KU records (whole, in registers) are loaded per thread before any is processed
+  for (uint64_t i0 = r0 + threadIdx.x; i0 < r1; i0 += (uint64_t)kAggThreads * KU) {
+    PRec<WMAX> rr[KU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < KU; ++u) {
       const uint64_t i = i0 + (uint64_t)u * kAggThreads;
-      b0[u] = i < r1 ? pb.rec[i * W] : 0;
-      b1[u] = i < r1 ? pb.rec[i * W + 1] : 0;
-    }
+      rr[u].C = C;
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-    const uint64_t i = i0 + (uint64_t)u * kAggThreads;
-    if (i >= r1) break;
-    const PRec r{pb.rec + i * W, b1[u], C};
-    const uint64_t w0 = b0[u];
+      for (int q = 0; q < WMAX; ++q) rr[u].w[q] = (i < r1 && q < W) ? pb.rec[i * W + q] : 0;
+    }
+    // one instance of the record body (a rolled loop over a shifting register
+    // queue): unrolling it KU times overflowed the instruction cache.
+    // Out-of-range records were loaded as zeros (no windows).
+#pragma unroll 1
+    for (int u = 0; u < KU; ++u) {
+    const PRec<WMAX> r = rr[0];
+#pragma unroll
+    for (int k = 0; k + 1 < KU; ++k) rr[k] = rr[k + 1];
+    const uint64_t w0 = r.w[0];
     const uint32_t key = (uint32_t)w0, krel = (uint32_t)(w0 >> 32);
-    const uint32_t nw = (uint32_t)b1[u];
+    const uint32_t nw = (uint32_t)r.w[1];
     pairs += nw;
     for (uint32_t j = 0; j < nw; ++j) {
       const uint64_t g = ((uint64_t)key << 32) | (uint64_t)(krel + j);
@@ -462,7 +503,7 @@ __global__ __launch_bounds__(kAggThreads) void k_part_agg(Program prog, TwParams
         h = (h + 1) & (E - 1);
       }
       if (e >= 0) {
-        lds_apply(prog, &lagg[e * MS], r);
+        lds_apply<MS>(prog, &lagg[e * MS], r);
       } else {
         // overflow: straight to the HBM table
         int64_t slot = tw_find_or_insert(t, g, fresh);
@@ -478,29 +519,57 @@ __global__ __launch_bounds__(kAggThreads) void k_part_agg(Program prog, TwParams
     }
   }
   __syncthreads();
-  // flush: one HBM update per group of the chunk
+  const uint64_t t2 = wall_clock64();
+  // flush: one HBM update per group of the chunk. Compact the live entries
+  // first so a thread carries about one group; every HBM access of a group is
+  // issued before any of its results is needed.
+  for (int e = threadIdx.x; e < E; e += kAggThreads)
+    if (lkey[e] != kEmpty) llive[atomicAdd(&lnl, 1u)] = (uint16_t)e;
+  __syncthreads();
+  const uint32_t nl = lnl;
   uint64_t groups = 0;
-  for (int e = threadIdx.x; e < E; e += kAggThreads) {
+  for (uint32_t q = threadIdx.x; q < nl; q += kAggThreads) {
+    const int e = llive[q];
     const uint64_t g = lkey[e];
-    if (g == kEmpty) continue;
     ++groups;
-    int64_t slot = tw_find_or_insert(t, g, fresh);
+    const uint32_t f0 = fresh;
+    const int64_t slot = tw_find_or_insert(t, g, fresh);
     if (slot < 0) { err |= ERR_OOM; continue; }
     int64_t v[MS];
 #pragma unroll
     for (int s = 0; s < MS; ++s) v[s] = lagg[e * MS + s];
-    flush_row(prog, t.aggs + (uint64_t)slot * prog.n_slots, v, exclusive);
-    // first touch of the group in this batch -> touched list (per-batch changelog)
+    int64_t *row = t.aggs + (uint64_t)slot * prog.n_slots;
     bool first;
-    if (exclusive) {
-      first = t.stamp[slot] != (uint32_t)p.batch_id;
+    if (exclusive && fresh != f0) {
+      // inserted just now by the group's only writer: the row holds identities
+#pragma unroll
+      for (int s = 0; s < MS; ++s)
+        if (s < prog.n_slots && prog.slot_op[s] != S_LAST_VAL) row[s] = v[s];
+      t.stamp[slot] = (uint32_t)p.batch_id;
+      first = true;
+    } else if (exclusive) {
+      int64_t cur[MS];
+#pragma unroll
+      for (int s = 0; s < MS; ++s) cur[s] = s < prog.n_slots ? row[s] : 0;
+      const uint32_t st = t.stamp[slot];
+#pragma unroll
+      for (int s = 0; s < MS; ++s) {
+        if (s >= prog.n_slots) break;
+        const int op = prog.slot_op[s];
+        if (op == S_LAST_VAL || v[s] == slot_identity_dev(op)) continue;
+        row[s] = op == S_LAST_SEQ ? ((uint64_t)v[s] > (uint64_t)cur[s] ? v[s] : cur[s]) : slot_combine(op, cur[s], v[s]);
+      }
+      first = st != (uint32_t)p.batch_id;
       if (first) t.stamp[slot] = (uint32_t)p.batch_id;
     } else {
+      flush_row(prog, row, v, false);
       first = atomicExch(&t.stamp[slot], (uint32_t)p.batch_id) != (uint32_t)p.batch_id;
     }
+    // first touch of the group in this batch -> touched list (per-batch changelog)
     if (first) ltouch[atomicAdd(&ltn, 1u)] = (uint32_t)slot;
   }
   __syncthreads();
+  const uint64_t t3 = wall_clock64();
   if (threadIdx.x == 0) lbase = ltn ? atomicAdd((unsigned long long *)&sc->scratch[1], (unsigned long long)ltn) : 0;
   __syncthreads();
   for (uint32_t q = threadIdx.x; q < ltn; q += kAggThreads) pb.touched[lbase + q] = ltouch[q];
@@ -524,6 +593,13 @@ __global__ __launch_bounds__(kAggThreads) void k_part_agg(Program prog, TwParams
     if (a) atomicAdd((unsigned long long *)&sc->pairs, (unsigned long long)a);
     if (f) atomicAdd((unsigned long long *)&sc->live, (unsigned long long)f);
     if (gr) atomicAdd((unsigned long long *)&sc->scratch[0], (unsigned long long)gr);
+    // phase clock (100 MHz wall clock) sums: init, records, flush, tail, workgroups
+    const uint64_t t4 = wall_clock64();
+    atomicAdd((unsigned long long *)&sc->scratch[8], (unsigned long long)(t1 - t0));
+    atomicAdd((unsigned long long *)&sc->scratch[9], (unsigned long long)(t2 - t1));
+    atomicAdd((unsigned long long *)&sc->scratch[10], (unsigned long long)(t3 - t2));
+    atomicAdd((unsigned long long *)&sc->scratch[11], (unsigned long long)(t4 - t3));
+    atomicAdd((unsigned long long *)&sc->scratch[12], 1ull);
   }
 }
 
@@ -564,17 +640,27 @@ void launch_part_emit(hipStream_t s, const TwTable &t, const Program &prog, cons
   hipLaunchKernelGGL(k_part_emit, dim3(2048), dim3(256), 0, s, t, prog, p, pb, out, out_base, out_cap, sc);
 }
 
+template <int MS, int E>
+static void agg_launch(hipStream_t s, dim3 g, int W, const Program &prog, const TwParams &p, const PartParams &pp,
+                       const TwTable &t, const PartBuffers &pb, DevScalars *sc) {
+  const dim3 th(kAggThreads);
+  constexpr int KU4 = MS >= 6 ? 6 : 8;  // records in flight per thread, within 128 VGPRs
+  if (W <= 4) hipLaunchKernelGGL((k_part_agg<MS, E, 4, KU4>), g, th, 0, s, prog, p, pp, t, pb, sc);
+  else if (W <= 6) hipLaunchKernelGGL((k_part_agg<MS, E, 6, 4>), g, th, 0, s, prog, p, pp, t, pb, sc);
+  else hipLaunchKernelGGL((k_part_agg<MS, E, kPartMaxWords, 2>), g, th, 0, s, prog, p, pp, t, pb, sc);
+}
+
 bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, const PartParams &pp, const TwTable &t,
                      const PartBuffers &pb, uint64_t n, DevScalars *sc) {
   if (!part_supported(prog)) return false;
   const uint64_t nb = 1ull << pp.np_log2;
   hipLaunchKernelGGL(k_part_chunks, dim3(1), dim3(1024), 0, s, pb.off, pp.tiles, pp.np_log2, pb.chunk_start);
-  const uint64_t grid = nb + n / kAggChunk + 1;
-  const dim3 g((unsigned)grid), th(kAggThreads);
-  if (prog.n_slots <= 2) hipLaunchKernelGGL((k_part_agg<2, 4096>), g, th, 0, s, prog, p, pp, t, pb, sc);
-  else if (prog.n_slots <= 4) hipLaunchKernelGGL((k_part_agg<4, 2048>), g, th, 0, s, prog, p, pp, t, pb, sc);
-  else if (prog.n_slots <= 6) hipLaunchKernelGGL((k_part_agg<6, 2048>), g, th, 0, s, prog, p, pp, t, pb, sc);
-  else hipLaunchKernelGGL((k_part_agg<8, 1024>), g, th, 0, s, prog, p, pp, t, pb, sc);
+  const dim3 g((unsigned)(nb + n / kAggChunk + 1));
+  const int W = pp.words;
+  if (prog.n_slots <= 2) agg_launch<2, 2048>(s, g, W, prog, p, pp, t, pb, sc);
+  else if (prog.n_slots <= 4) agg_launch<4, 1024>(s, g, W, prog, p, pp, t, pb, sc);
+  else if (prog.n_slots <= 6) agg_launch<6, 1024>(s, g, W, prog, p, pp, t, pb, sc);
+  else agg_launch<8, 1024>(s, g, W, prog, p, pp, t, pb, sc);
   return true;
 }
 

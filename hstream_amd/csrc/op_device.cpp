@@ -1,5 +1,7 @@
 // Host orchestration of one operator's batch on its HIP stream: staging, the
 // stream-time scan, the aggregation kernels, changelog bookkeeping, dumps.
+#include <cstdio>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -319,7 +321,7 @@ int clear_batch_scalars(OpDevice &d, std::string &err) {
   // err, pairs, late, out_rows, touched (offsets 20..55); wm/epoch/live persist
   DTRY(hipMemsetAsync((char *)d.sc + offsetof(DevScalars, err), 0,
                       offsetof(DevScalars, live) - offsetof(DevScalars, err), d.stream));
-  DTRY(hipMemsetAsync((char *)d.sc + offsetof(DevScalars, scratch), 0, 8 * sizeof(uint64_t), d.stream));
+  DTRY(hipMemsetAsync((char *)d.sc + offsetof(DevScalars, scratch), 0, 20 * sizeof(uint64_t), d.stream));
   return HSG_OK;
 }
 
@@ -339,6 +341,15 @@ int finish_batch(OpDevice &d, int64_t wm_in, uint64_t n, PushResult &r, std::str
   int rc = fetch_scalars(d, err);
   if (rc != HSG_OK) return rc;
   const DevScalars &s = *d.h_sc;
+  static const bool phases = getenv("HSG_PHASES") != nullptr;
+  if (phases && s.scratch[12])
+    fprintf(stderr, "[hsg phases] agg wg=%llu init=%.1fus records=%.1fus flush=%.1fus tail=%.1fus (per-wg avg)\n",
+            (unsigned long long)s.scratch[12], s.scratch[8] * 0.01 / s.scratch[12], s.scratch[9] * 0.01 / s.scratch[12],
+            s.scratch[10] * 0.01 / s.scratch[12], s.scratch[11] * 0.01 / s.scratch[12]);
+  if (phases && s.scratch[17])
+    fprintf(stderr, "[hsg phases] scatter wg=%llu walk=%.1fus scan=%.1fus place=%.1fus write=%.1fus (per-wg avg)\n",
+            (unsigned long long)s.scratch[17], s.scratch[13] * 0.01 / s.scratch[17], s.scratch[14] * 0.01 / s.scratch[17],
+            s.scratch[15] * 0.01 / s.scratch[17], s.scratch[16] * 0.01 / s.scratch[17]);
   r.wm_out = n ? s.wm_out : wm_in;
   r.pairs = s.pairs;
   r.late = s.late;
