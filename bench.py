@@ -74,8 +74,12 @@ def main():
     eng = Engine(device=local, rank=rank, nranks=world, comm_id=comm_id, batch_capacity=batch)
 
     # state sized for the config: distinct (key, window) groups over the whole run
-    windows = 3_600_000 // (cfg.advance_ms or cfg.size_ms or 60_000) + 2 if cfg.window_kind != abi.HSG_SESSION else 1
+    # the config's time density: cfg.n records per rank per hour of event time,
+    # also when fewer records are measured (--records)
+    span_ms = 3_600_000 * min(1.0, n_rank / cfg.n)
     wpr = -(-cfg.size_ms // cfg.advance_ms) if cfg.window_kind == abi.HSG_HOPPING else 1
+    windows = int(span_ms // (cfg.advance_ms or cfg.size_ms or 60_000)) + wpr + 2 \
+        if cfg.window_kind != abi.HSG_SESSION else 1
     groups = min(cfg.keys * windows, n_rank * world * wpr)
     if cfg.window_kind == abi.HSG_SESSION:
         groups = n_rank * world  # at most one session per record
@@ -87,7 +91,7 @@ def main():
     # every global batch = world consecutive pieces of `batch` records; rank r
     # ingests piece r of each (the C3 layout: a contiguous 1/G of every batch)
     pieces = [(s, min(batch, n_rank - s)) for s in range(0, n_rank, batch)]
-    parts = [datagen.generate_torch(cfg, m, device=dev, start=s * world + rank * m, total=n_rank * world)
+    parts = [datagen.generate_torch(cfg, m, device=dev, start=s * world + rank * m, total=cfg.n * world)
              for s, m in pieces]
     keys = torch.cat([p["key_id"] for p in parts])
     ts = torch.cat([p["ts"] for p in parts])

@@ -135,7 +135,9 @@ int session_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &pr
   DTRY(hipMalloc((void **)&t.list_len, d.cap * sizeof(uint32_t)));
   DTRY(hipMalloc((void **)&t.list_cap, d.cap * sizeof(uint32_t)));
   t.mask = d.cap - 1;
-  t.arena_cap = d.cap * kSessInline + rows;
+  // inline lists + a dynamic region for grown lists: growth doubles and
+  // abandons the old copy, so up to 2x the live sessions can be in use
+  t.arena_cap = d.cap * kSessInline + 2 * rows;
   DTRY(hipMalloc((void **)&t.a_start, t.arena_cap * sizeof(int64_t)));
   DTRY(hipMalloc((void **)&t.a_end, t.arena_cap * sizeof(int64_t)));
   DTRY(hipMalloc((void **)&t.a_stamp, t.arena_cap * sizeof(uint32_t)));

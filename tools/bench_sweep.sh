@@ -14,4 +14,5 @@ run c1 --config C1
 run c2f --config C2f
 run c5 --config C5 --records 33554432
 run c4 --config C4 --records 33554432
+run c3 --config C3 --records 100000000
 run c2_per_record --emit per_record --records 33554432
