@@ -93,7 +93,7 @@ struct DevScalars {
   uint64_t touched;
   uint64_t live;         // dump: rows found
   uint32_t no_late;      // this batch: no (record, window) can fail the grace check
-  uint32_t pad0;
+  uint32_t redo;         // optimistic partition path: the batch has late records, run it again carefully
   uint64_t scratch[23];  // [0] groups flushed (partition path), [1] touched-list length
 };
 static_assert(sizeof(DevScalars) == 256, "DevScalars layout");
@@ -118,13 +118,29 @@ struct Batch {
   const uint8_t *valid[kMaxCols];
 };
 
-// Time-window (tumbling / hopping / unwindowed) hash state in HBM.
+// Time-window (tumbling / hopping / unwindowed) hash state in HBM, one row per
+// (key, window) group, array-of-structs so a group is one cache line:
+//   word 0      group key = key_id << 32 | (k - k_epoch); kEmpty = free
+//   word 1      low 32 bits: id of the last batch that touched the group
+//   words 2..   aggregate slots (n_slots words)
+// Rows are `stride` words (a power of two up to 16, so a row never straddles a
+// 128-byte line). The home slot keeps the 8 windows of an aligned window block
+// of one key in 8 consecutive rows (see tw_home).
 struct TwTable {
-  uint64_t *keys;   // [cap] group key = key_id << 32 | (k - k_epoch); kEmpty = free
-  int64_t *aggs;    // [cap][n_slots]
-  uint32_t *stamp;  // [cap] id of the last batch that touched the group
+  uint64_t *rows;   // [cap][stride]
   uint64_t mask;    // cap - 1
+  uint32_t stride;  // words per row
+  uint32_t blocked; // window-block home slots, probe step 8 (windowed ops with >= 8 slots)
+  __host__ __device__ uint64_t *key(uint64_t s) const { return rows + s * stride; }
+  __host__ __device__ uint32_t *stamp(uint64_t s) const { return (uint32_t *)(rows + s * stride + 1); }
+  __host__ __device__ int64_t *aggs(uint64_t s) const { return (int64_t *)(rows + s * stride + 2); }
 };
+
+inline uint32_t tw_row_stride(int n_slots) {
+  uint32_t w = 2u + (uint32_t)n_slots, s = 4;
+  while (s < w && s < 16) s <<= 1;
+  return s >= w ? s : (w + 7u) & ~7u;
+}
 
 struct TwParams {
   int32_t kind;     // hsg_window_kind
@@ -167,8 +183,16 @@ inline int64_t slot_identity(int32_t op) {
 }
 
 // ---- kernel launchers (defined in the .hip files) --------------------------
+struct RowPtrs {
+  int64_t *p[kMaxAggs];
+};
+void launch_clear_scalars(hipStream_t s, DevScalars *sc);
+void launch_copy_rows(hipStream_t s, const OutCols &src, uint64_t from, uint64_t n, int n_aggs, uint32_t *key,
+                      int64_t *ws, int64_t *we, int64_t *si, const RowPtrs &aggs);
 void launch_fill_u64(hipStream_t s, uint64_t *p, uint64_t n, uint64_t v);
 void launch_fill_rows(hipStream_t s, int64_t *aggs, uint64_t rows, const Program &prog);
+// every row of a time-window table: key EMPTY, stamp 0, aggregate identities
+void launch_tw_reset(hipStream_t s, const TwTable &t, const Program &prog);
 void launch_fill_u32(hipStream_t s, uint32_t *p, uint64_t n, uint32_t v);
 
 // stream time: tile maxima -> exclusive tile prefix (+ epoch init)

@@ -57,6 +57,9 @@ struct OpDevice {
   void *part_mem = nullptr;
   bool use_part = false;
   int np_log2 = 10;             // partitions of the next batch (adapted per batch)
+  int rbits = 0;                // key-hash aggregation rounds of the next batch (log2)
+  int pane_S = 1;               // panes per window (0: one LDS entry per window)
+  bool agg_big = true;          // aggregation variant of the next batch (big LDS table)
   // sessions
   SessTable ss = {};
   uint64_t *arena_top = nullptr;  // device bump pointer

@@ -9,20 +9,28 @@ namespace hsg {
 
 constexpr int kPartThreads = 256;
 constexpr int kPartMaxLog2 = 11;                      // up to 2048 partitions
-constexpr int kAggThreads = 512;
 constexpr int kPartMaxWords = 11;                     // 2 + 8 columns + seq
-constexpr uint64_t kAggChunk = 8192;                  // records per aggregation workgroup
+constexpr uint64_t kTouchChunk = 4096;                // touched-list entries per emit workgroup
 
 // A partitioned record is `words` 8-byte words:
 //   [key | krel << 32] [nwin | valid bits << 32] [col 0 .. C-1] [seq + 1]?
 // krel = first accepted window relative to the epoch, nwin = accepted windows.
 struct PartBuffers {
-  uint32_t *hist;         // [np * tiles] bucket-major per-tile counts
-  uint64_t *off;          // [np * tiles + 1] exclusive prefix
+  uint32_t *hist;         // [tiles][np] tile-major per-tile bucket counts
+  uint32_t *offt;         // [tiles][np] tile-major bucket-major-order offsets of each (tile, bucket) run
+  uint32_t *segsum;       // [np][nseg] column sums over segments of kColSeg tiles
+  uint64_t *segoff;       // [np * nseg] exclusive prefix of segsum (bucket-major)
+  uint64_t *bstart;       // [np + 1] first record of each bucket; bstart[np] = records placed
   uint64_t *partial;      // scan partials
   uint64_t *rec;          // [n * words] partitioned records
   uint32_t *chunk_start;  // [np + 1] first aggregation workgroup of each bucket
-  uint32_t *touched;      // [table slots] groups first touched by this batch (length: sc->scratch[1])
+  uint32_t *chunk_bucket; // [workgroups] bucket of each aggregation workgroup
+  uint32_t *touched;      // [touched_cap] one entry per HBM window update: the slot on the group's first
+                          // update in the batch, else kTouchSkip (length: sc->scratch[1])
+  uint64_t touched_cap;   // records x windows per record: bounds the updates of one batch
+  uint32_t *tcnt;         // [touch_chunks] emit: non-skip entries per chunk
+  uint64_t *toff;         // [touch_chunks + 1] exclusive prefix
+  uint64_t *tpartial;     // scan partials
   int64_t *wm;            // [n] per-record stream time (written only when late records are possible)
   uint64_t n_cap;
 };
@@ -33,8 +41,12 @@ struct PartParams {
   int32_t has_seq;
   int32_t words;
   int32_t tile;       // records per partition-pass workgroup (1024, 2048 or 4096)
-  int32_t pad;
+  int32_t pane_S;     // aggregation: panes per window (size / advance), 0 = one LDS entry per window
+  int32_t rbits;      // aggregation: 2^rbits key-hash rounds per sub-chunk
+  int32_t big;        // aggregation variant: 1 = big LDS table, 1024 threads
+  int32_t exp;        // experiment knob (HSG_EXP, timing studies only): 1 = no LDS aggregate update, 2 = no LDS insert
   uint64_t tiles;     // partition-pass tiles of this batch
+  uint64_t chunk;     // records per aggregation workgroup
 };
 
 inline int part_words(int n_cols, bool has_seq) { return 2 + n_cols + (has_seq ? 1 : 0); }
@@ -45,8 +57,14 @@ inline uint64_t part_tiles(uint64_t n, int tile) { return (n + tile - 1) / tile;
 // per-record stream time into wm unless sc->no_late (decided by launch_tile_scan)
 void launch_part_recwm(hipStream_t s, const Batch &b, const int64_t *tprefix, const DevScalars *sc, int64_t *wm);
 // rec_wm: per-record stream time from a key exchange (else own_wm / none)
+// opt: optimistic pass (no record assumed late; also collects the batch's ts
+// extrema for launch_part_decide)
 void launch_part_hist(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp, const int64_t *rec_wm,
-                      const int64_t *own_wm, const PartBuffers &pb, DevScalars *sc);
+                      const int64_t *own_wm, const PartBuffers &pb, DevScalars *sc, bool opt);
+void launch_part_decide(hipStream_t s, DevScalars *sc, int64_t wm_in, int64_t grace);
+// bucket-major run offsets (offt, bstart) from the tile-major histogram
+void launch_part_offsets(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc);
+uint32_t part_nseg(uint64_t tiles);
 void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp,
                          const int64_t *rec_wm, const int64_t *own_wm, const int64_t *seq, const PartBuffers &pb,
                          DevScalars *sc);
@@ -57,8 +75,9 @@ bool part_supported(const Program &prog);
 // per-batch changelog rows of the groups in pb.touched
 void launch_part_emit(hipStream_t s, const TwTable &t, const Program &prog, const TwParams &p, const PartBuffers &pb,
                       OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc);
-inline uint64_t part_lds_entries(const Program &prog) {
-  return prog.n_slots <= 2 ? 2048 : 1024;
-}
+// LDS table entries of the small (2 workgroups per CU) / big (1 per CU) variant
+uint64_t part_lds_entries(const Program &prog, bool big);
+inline uint64_t touch_chunks(uint64_t cap) { return (cap + kTouchChunk - 1) / kTouchChunk; }
+constexpr uint64_t kAggChunk = 32768;                 // most records per aggregation workgroup
 
 }  // namespace hsg

@@ -19,6 +19,7 @@
 // the accepted windows of a record are one consecutive run).
 #include "hsg_dev.h"
 #include "hsg_part.h"
+#include "hsg_sort.h"
 #include "hsg_tw.h"
 
 namespace hsg {
@@ -100,9 +101,15 @@ __device__ inline const int64_t *pick_wm(const int64_t *rec_wm, const int64_t *o
 // Walk the T records of one partition tile with NT threads (record (r, t) =
 // tile*T + r*NT + t); calls f(j, i, key, krel, nwin) for every record with
 // >= 1 accepted window (j = tile-local index, i = batch index). No barriers.
+// Order-preserving u64 image of an i64 (max of images = image of the max).
+__device__ inline uint64_t i64_ord(int64_t v) { return (uint64_t)v ^ 0x8000000000000000ull; }
+
+// ext (optional): ext[0] = max image of every record's ts, ext[1] = max of
+// ~image of the ts of keyed records with ts >= 0 (i.e. their min); 0 = none.
 template <int T, int NT, typename F>
 __device__ inline void walk_tile(const Batch &b, const TwParams &p, uint64_t tile, int64_t k_epoch,
-                                 const int64_t *__restrict__ wm, uint64_t &late, uint32_t &err, F f) {
+                                 const int64_t *__restrict__ wm, uint64_t &late, uint32_t &err, F f,
+                                 uint64_t *ext = nullptr) {
   constexpr int R = T / NT;
   const uint64_t base = tile * T;
   // every load of the tile is issued before the first record is processed
@@ -115,6 +122,18 @@ __device__ inline void walk_tile(const Batch &b, const TwParams &p, uint64_t til
     key[r] = in ? b.key[i] : HSG_KEY_NONE;
     ts[r] = in ? b.ts[i] : 0;
     w[r] = in && wm ? wm[i] : INT64_MIN;
+  }
+  if (ext) {
+    uint64_t mx = 0, mn = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint64_t i = base + (uint64_t)r * NT + threadIdx.x;
+      const uint64_t o = i64_ord(ts[r]);
+      if (i < b.n) mx = o > mx ? o : mx;
+      if (key[r] != HSG_KEY_NONE && ts[r] >= 0) mn = ~o > mn ? ~o : mn;
+    }
+    ext[0] = mx;
+    ext[1] = mn;
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -131,21 +150,51 @@ template <int T>
 __global__ __launch_bounds__(kPNT) void k_part_hist(Batch b, TwParams p, PartParams pp,
                                                     const int64_t *__restrict__ rec_wm,
                                                     const int64_t *__restrict__ own_wm, PartBuffers pb,
-                                                    DevScalars *sc) {
+                                                    DevScalars *sc, int opt) {
   __shared__ uint32_t cnt[1 << kPartMaxLog2];
   __shared__ uint64_t sred[kPNT / 64];
+  __shared__ uint64_t sext[2][kPNT / 64];
   const int nb = 1 << pp.np_log2;
   const uint64_t tile = xcd_tile(blockIdx.x, pp.tiles);
   for (int i = threadIdx.x; i < nb; i += kPNT) cnt[i] = 0;
   __syncthreads();
   uint64_t late = 0;
   uint32_t err = 0;
-  walk_tile<T, kPNT>(b, p, tile, sc->k_epoch, pick_wm(rec_wm, own_wm, sc), late, err,
+  // optimistic pass: no record is assumed late (checked by k_part_decide); the
+  // stream-time inputs of the batch come out of the same walk: max ts of every
+  // record (Processor.hs:139), min ts of the keyed records (as k_tile_stats)
+  uint64_t ext[2] = {0, 0};
+  walk_tile<T, kPNT>(b, p, tile, sc->k_epoch, opt ? nullptr : pick_wm(rec_wm, own_wm, sc), late, err,
                      [&](int, uint64_t, uint32_t key, uint32_t, uint32_t) {
                        atomicAdd(&cnt[bucket_of(key, pp.np_log2)], 1u);
-                     });
+                     },
+                     opt ? ext : nullptr);
+  if (opt) {
+    uint64_t mx = ext[0], mn = ext[1];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t a = __shfl_xor(mx, o, 64), c = __shfl_xor(mn, o, 64);
+      mx = a > mx ? a : mx;
+      mn = c > mn ? c : mn;
+    }
+    if ((threadIdx.x & 63) == 0) {
+      sext[0][threadIdx.x >> 6] = mx;
+      sext[1][threadIdx.x >> 6] = mn;
+    }
+  }
   __syncthreads();
-  for (int i = threadIdx.x; i < nb; i += kPNT) pb.hist[(uint64_t)i * pp.tiles + tile] = cnt[i];
+  if (opt && threadIdx.x == 0) {
+    uint64_t mx = 0, mn = 0;
+    for (int k = 0; k < kPNT / 64; ++k) {
+      mx = sext[0][k] > mx ? sext[0][k] : mx;
+      mn = sext[1][k] > mn ? sext[1][k] : mn;
+    }
+    if (mx) atomicMax((unsigned long long *)&sc->scratch[21], (unsigned long long)mx);
+    if (mn) atomicMax((unsigned long long *)&sc->scratch[22], (unsigned long long)mn);
+  }
+  // tile-major counts: one contiguous row per tile (k_part_colsum / colscan
+  // turn them into bucket-major offsets)
+  for (int i = threadIdx.x; i < nb; i += kPNT) pb.hist[tile * (uint64_t)nb + i] = cnt[i];
   late = wave_sum_u64(late);
   if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = late;
   if (err) atomicOr(&sc->err, err);
@@ -173,6 +222,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
   __shared__ uint32_t cursor[1 << kPartMaxLog2];
   __shared__ uint32_t goff[1 << kPartMaxLog2];
   __shared__ uint32_t swave[kPNT / 64];
+  if (sc->redo) return;  // uniform: the optimistic pass found late records
   const int nb = 1 << pp.np_log2;
   const int W = pp.words;
   const int C = W - 2 - pp.has_seq;
@@ -213,7 +263,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
     lstart[k] = run;
     run += cursor[k];
     cursor[k] = 0;
-    goff[k] = (uint32_t)pb.off[(uint64_t)k * pp.tiles + tile];
+    goff[k] = pb.offt[tile * (uint64_t)nb + k];
   }
   uint32_t placed = 0;
   for (int k = 0; k < kPNT / 64; ++k) placed += swave[k];
@@ -266,10 +316,29 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
 }
 
 void launch_part_hist(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp, const int64_t *rec_wm,
-                      const int64_t *own_wm, const PartBuffers &pb, DevScalars *sc) {
+                      const int64_t *own_wm, const PartBuffers &pb, DevScalars *sc, bool opt) {
   if (!pp.tiles) return;
   hipLaunchKernelGGL(k_part_hist<kPartTileRecs>, dim3((unsigned)pp.tiles), dim3(kPNT), 0, s, b, p, pp, rec_wm, own_wm,
-                     pb, sc);
+                     pb, sc, opt ? 1 : 0);
+}
+
+// Optimistic path, after the histogram: stream time out, and whether the
+// no-late assumption held (same test as k_tile_scan); if not, every later
+// kernel of the batch exits and the host runs the batch again carefully.
+__global__ void k_part_decide(DevScalars *sc, int64_t wm_in, int64_t grace) {
+  if (threadIdx.x != 0) return;
+  const uint64_t mx = sc->scratch[21], mn = sc->scratch[22];
+  const int64_t bmax = mx ? (int64_t)(mx ^ 0x8000000000000000ull) : INT64_MIN;
+  const int64_t amin = mn ? (int64_t)(~mn ^ 0x8000000000000000ull) : INT64_MAX;
+  const int64_t all = bmax > wm_in ? bmax : wm_in;
+  sc->wm_out = all;
+  const bool ok = amin == INT64_MAX || amin > INT64_MAX - grace || all <= amin + grace;
+  sc->no_late = ok ? 1u : 0u;
+  sc->redo = ok ? 0u : 1u;
+}
+
+void launch_part_decide(hipStream_t s, DevScalars *sc, int64_t wm_in, int64_t grace) {
+  hipLaunchKernelGGL(k_part_decide, dim3(1), dim3(64), 0, s, sc, wm_in, grace);
 }
 
 void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp,
@@ -281,18 +350,84 @@ void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const
 }
 
 // ---------------------------------------------------------------------------
-// chunk map: chunk_start[b] = first aggregation workgroup of bucket b
+// bucket-major offsets from the tile-major counts hist[tile][bucket]:
+//   off(b, t) = sum_{b' < b} total(b') + sum_{t' < t} hist[t'][b]
+// colsum: per (64-bucket block, segment of kColSeg tiles) column sums, stored
+// bucket-major; a scan of those (nb x nseg entries) gives each segment's base;
+// colscan: the running column prefix inside a segment, written tile-major
+// (offt[t][b], what a scatter workgroup reads as one contiguous row), plus
+// the bucket starts bstart[b] (bstart[nb] = records placed).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_part_chunks(const uint64_t *off, uint64_t tiles, int np_log2,
-                                                      uint32_t *chunk_start) {
+constexpr uint64_t kColSeg = 256;
+
+uint32_t part_nseg(uint64_t tiles) { return (uint32_t)((tiles + kColSeg - 1) / kColSeg); }
+
+__global__ __launch_bounds__(256) void k_part_colsum(const uint32_t *__restrict__ hist, uint64_t tiles, int nb,
+                                                     uint32_t nseg, uint32_t *__restrict__ segsum, const DevScalars *sc) {
+  __shared__ uint32_t red[4][64];
+  if (sc->redo) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = blockIdx.x * 64 + lane;
+  const uint64_t t0 = (uint64_t)blockIdx.y * kColSeg, t1 = t0 + kColSeg < tiles ? t0 + kColSeg : tiles;
+  uint32_t sum = 0;
+  if (b < nb)
+    for (uint64_t t = t0 + w; t < t1; t += 4) sum += hist[t * nb + b];
+  red[w][lane] = sum;
+  __syncthreads();
+  if (w == 0 && b < nb) segsum[(uint64_t)b * nseg + blockIdx.y] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+}
+
+__global__ __launch_bounds__(256) void k_part_colscan(const uint32_t *__restrict__ hist, uint64_t tiles, int nb,
+                                                      uint32_t nseg, const uint64_t *__restrict__ segoff,
+                                                      uint32_t *__restrict__ offt, uint64_t *__restrict__ bstart,
+                                                      const DevScalars *sc) {
+  __shared__ uint32_t red[4][64];
+  if (sc->redo) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = blockIdx.x * 64 + lane;
+  const uint64_t t0 = (uint64_t)blockIdx.y * kColSeg, t1 = t0 + kColSeg < tiles ? t0 + kColSeg : tiles;
+  const uint64_t per = (t1 - t0 + 3) / 4;
+  const uint64_t r0 = t0 + w * per < t1 ? t0 + w * per : t1, r1 = r0 + per < t1 ? r0 + per : t1;
+  uint32_t sum = 0;
+  if (b < nb)
+    for (uint64_t t = r0; t < r1; ++t) sum += hist[t * nb + b];
+  red[w][lane] = sum;
+  __syncthreads();
+  if (b >= nb) return;
+  uint64_t run = segoff[(uint64_t)b * nseg + blockIdx.y];
+  for (int k = 0; k < w; ++k) run += red[k][lane];
+  for (uint64_t t = r0; t < r1; ++t) {
+    offt[t * nb + b] = (uint32_t)run;
+    run += hist[t * nb + b];
+  }
+  if (blockIdx.y == 0 && w == 0) bstart[b] = segoff[(uint64_t)b * nseg];
+}
+
+void launch_part_offsets(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc) {
+  if (!pp.tiles) return;
+  const int nb = 1 << pp.np_log2;
+  const uint32_t nseg = part_nseg(pp.tiles);
+  const dim3 g((unsigned)((nb + 63) / 64), nseg);
+  hipLaunchKernelGGL(k_part_colsum, g, dim3(256), 0, s, pb.hist, pp.tiles, nb, nseg, pb.segsum, sc);
+  scan_excl_u32(s, pb.segsum, pb.segoff, (uint64_t)nb * nseg, pb.partial, pb.bstart + nb);
+  hipLaunchKernelGGL(k_part_colscan, g, dim3(256), 0, s, pb.hist, pp.tiles, nb, nseg, pb.segoff, pb.offt, pb.bstart,
+                     sc);
+}
+
+// ---------------------------------------------------------------------------
+// chunk map: chunk_start[b] = first aggregation workgroup of bucket b
+// (a bucket of more than `chunk` records is split over several workgroups)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_part_chunks(const uint64_t *bstart, int np_log2, uint64_t chunk,
+                                                      uint32_t *chunk_start, uint32_t *chunk_bucket) {
   __shared__ uint32_t sw[16];
   const int nb = 1 << np_log2;
   const int per = (nb + 1023) / 1024;
   const int lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
   uint32_t loc = 0;
   for (int b = lo; b < hi; ++b) {
-    uint64_t sz = off[(uint64_t)(b + 1) * tiles] - off[(uint64_t)b * tiles];
-    loc += (uint32_t)((sz + kAggChunk - 1) / kAggChunk);
+    uint64_t sz = bstart[b + 1] - bstart[b];
+    loc += (uint32_t)((sz + chunk - 1) / chunk);
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t incl = loc;
@@ -307,8 +442,10 @@ __global__ __launch_bounds__(1024) void k_part_chunks(const uint64_t *off, uint6
   for (int k = 0; k < w; ++k) run += sw[k];
   for (int b = lo; b < hi; ++b) {
     chunk_start[b] = run;
-    uint64_t sz = off[(uint64_t)(b + 1) * tiles] - off[(uint64_t)b * tiles];
-    run += (uint32_t)((sz + kAggChunk - 1) / kAggChunk);
+    uint64_t sz = bstart[b + 1] - bstart[b];
+    const uint32_t k = (uint32_t)((sz + chunk - 1) / chunk);
+    for (uint32_t q = 0; q < k; ++q) chunk_bucket[run + q] = (uint32_t)b;
+    run += k;
   }
   if (threadIdx.x == 0) {
     uint32_t t = 0;
@@ -384,17 +521,27 @@ __device__ inline void lds_apply(const Program &prog, int64_t *__restrict__ row,
   }
 }
 
-// HBM-side combine of a finished row of partial aggregates (v) into `row`.
-__device__ inline void flush_row(const Program &prog, int64_t *__restrict__ row, const int64_t *v, bool exclusive) {
-  for (int s = 0; s < prog.n_slots; ++s) {
+// a <- a (+) x over the aggregate slots (LAST_SEQ = latest sequence)
+template <int MS>
+__device__ inline void acc_combine(const Program &prog, int64_t (&a)[MS], const int64_t *x) {
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    if (s >= prog.n_slots) break;
+    const int op = prog.slot_op[s];
+    if (op == S_LAST_VAL) continue;
+    a[s] = op == S_LAST_SEQ ? ((uint64_t)x[s] > (uint64_t)a[s] ? x[s] : a[s]) : slot_combine(op, a[s], x[s]);
+  }
+}
+
+// HBM-side atomic combine of a row of partial aggregates (v) into `row`.
+template <int MS>
+__device__ inline void flush_row_atomic(const Program &prog, int64_t *__restrict__ row, const int64_t (&v)[MS]) {
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    if (s >= prog.n_slots) break;
     const int op = prog.slot_op[s];
     const int64_t x = v[s];
-    if (op == S_LAST_VAL) continue;
-    if (x == slot_identity_dev(op)) continue;  // nothing to add
-    if (exclusive) {
-      row[s] = op == S_LAST_SEQ ? ((uint64_t)x > (uint64_t)row[s] ? x : row[s]) : slot_combine(op, row[s], x);
-      continue;
-    }
+    if (op == S_LAST_VAL || x == slot_identity_dev(op)) continue;  // nothing to add
     unsigned long long *u = (unsigned long long *)(row + s);
     switch (op) {
       case S_CNT_ALL:
@@ -411,216 +558,482 @@ __device__ inline void flush_row(const Program &prog, int64_t *__restrict__ row,
   }
 }
 
-template <int MS, int E, int WMAX, int KU>
-__global__ __launch_bounds__(kAggThreads, 4) void k_part_agg(Program prog, TwParams p, PartParams pp, TwTable t,
-                                                          PartBuffers pb, DevScalars *sc) {
-  __shared__ uint64_t lkey[E];
-  __shared__ int64_t lagg[E * MS];
-  __shared__ uint32_t lfill;
-  __shared__ uint32_t sb, sc0, sc1;
-  __shared__ uint64_t sred[3][kAggThreads / 64];
-  __shared__ uint32_t ltouch[E];  // slots this workgroup touched first in this batch
-  __shared__ uint32_t ltn;
-  __shared__ uint16_t llive[E];   // live entries of the LDS table, compacted
-  __shared__ uint32_t lnl;
-  __shared__ uint64_t lbase;
+constexpr uint32_t kTouchSkip = 0xFFFFFFFFu;
+
+// One HBM update of group g with the chunk's partial aggregate v. `exclusive`:
+// this workgroup is the only one updating the group in this launch, so a plain
+// read-modify-write suffices (agent-scope loads, served by L2 not L1: this
+// workgroup's own atomics may have updated the row). Returns the slot when this is the group's first update
+// in the batch (-> per-batch changelog), else kTouchSkip.
+template <int MS>
+__device__ inline uint32_t flush_window(const Program &prog, const TwParams &p, const TwTable &t, uint64_t g,
+                                        const int64_t (&v)[MS], bool exclusive, uint32_t &fresh, uint32_t &err) {
+  const uint32_t f0 = fresh;
+  const int64_t slot = tw_find_or_insert(t, g, fresh);
+  if (slot < 0) {
+    err |= ERR_OOM;
+    return kTouchSkip;
+  }
+  int64_t *row = t.aggs(slot);
+  uint32_t *stp = t.stamp(slot);
+  const uint32_t bid = (uint32_t)p.batch_id;
+  bool first;
+  if (exclusive && fresh != f0) {
+    // inserted just now by the group's only writer: the row holds identities
+#pragma unroll
+    for (int s = 0; s < MS; ++s)
+      if (s < prog.n_slots && prog.slot_op[s] != S_LAST_VAL) row[s] = v[s];
+    *stp = bid;
+    first = true;
+  } else if (exclusive) {
+    int64_t cur[MS];
+#pragma unroll
+    for (int s = 0; s < MS; ++s)
+      cur[s] = s < prog.n_slots ? __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    const uint32_t st = __hip_atomic_load(stp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int s = 0; s < MS; ++s) {
+      if (s >= prog.n_slots) break;
+      const int op = prog.slot_op[s];
+      if (op == S_LAST_VAL || v[s] == slot_identity_dev(op)) continue;
+      row[s] = op == S_LAST_SEQ ? ((uint64_t)v[s] > (uint64_t)cur[s] ? v[s] : cur[s]) : slot_combine(op, cur[s], v[s]);
+    }
+    first = st != bid;
+    if (first) *stp = bid;
+  } else {
+    flush_row_atomic<MS>(prog, row, v);
+    first = atomicExch(stp, bid) != bid;
+  }
+  return first ? (uint32_t)slot : kTouchSkip;
+}
+
+__device__ inline void touch_append(const PartBuffers &pb, DevScalars *sc, uint32_t slot, uint32_t &err) {
+  if (slot == kTouchSkip) return;
+  const uint64_t o = atomicAdd((unsigned long long *)&sc->scratch[1], 1ull);
+  if (o < pb.touched_cap) pb.touched[o] = slot;
+  else err |= ERR_OOM;
+}
+
+// Windows [w0, w1] of one record straight into the HBM table (records whose
+// earliest windows were rejected by grace, and LDS overflow in fan-out mode).
+template <int MS, typename R>
+__device__ inline void direct_windows(const Program &prog, const TwParams &p, const TwTable &t, const PartBuffers &pb,
+                                      DevScalars *sc, uint32_t key, uint32_t w0, uint32_t w1, const R &r,
+                                      uint32_t &fresh, uint32_t &err) {
+  int64_t v[MS];
+#pragma unroll
+  for (int s = 0; s < MS; ++s) v[s] = s < prog.n_slots ? prec_elem(prog, s, r) : 0;
+  for (uint32_t w = w0;; ++w) {
+    touch_append(pb, sc, flush_window<MS>(prog, p, t, ((uint64_t)key << 32) | w, v, false, fresh, err), err);
+    if (w == w1) break;
+  }
+}
+
+// find or insert g; -1 when g is absent and the table is at its fill limit
+template <int E>
+__device__ inline int lds_insert(uint64_t *lkey, uint32_t *lfill, uint32_t limit, uint64_t g) {
+  uint32_t h = (uint32_t)(mix64(g) & (E - 1));
+  for (int probe = 0; probe < E; ++probe) {
+    const uint64_t cur = lkey[h];
+    if (cur == g) return (int)h;
+    if (cur == kEmpty) {
+      if (*(volatile uint32_t *)lfill >= limit) return -1;
+      const uint64_t old = atomicCAS((unsigned long long *)&lkey[h], (unsigned long long)kEmpty, (unsigned long long)g);
+      if (old == kEmpty) {
+        atomicAdd(lfill, 1u);
+        return (int)h;
+      }
+      if (old == g) return (int)h;
+    }
+    h = (h + 1) & (E - 1);
+  }
+  return -1;
+}
+
+// sub-round of a key: the hash bits just below its bucket bits
+__device__ inline uint32_t key_round(uint32_t key, int np_log2, int rbits) {
+  if (!rbits) return 0;
+  const uint64_t h = mix64((uint64_t)key * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull);
+  return (uint32_t)(h >> (64 - np_log2 - rbits)) & ((1u << rbits) - 1u);
+}
+
+// Aggregation of one chunk of a bucket (buckets are disjoint key sets, so when
+// the bucket is one chunk this workgroup owns every group it updates).
+//
+// Pane mode (pp.pane_S = S >= 1, size = S * advance): a record of a full window
+// run only updates its pane (key, last window P) in the LDS table. At a flush
+// the live panes are sorted by (key, pane) in LDS; every pane P owns the
+// windows [a, P] that contain no earlier pane in the table, and window
+// w = combine(panes w .. w+S-1) gets one HBM update, with the panes summed
+// incrementally from the sorted neighbours (w+1 adds the panes up to w+S).
+// Tumbling is S = 1 (no sort). Fan-out mode (S = 0: size not a multiple of
+// advance) keeps one entry per window.
+//
+// The chunk is walked in register-resident sub-chunks of NT * RPT records and
+// the LDS table persists across them: it is flushed when full and at the end
+// of each of the 2^rbits key-hash rounds (host-sized from the previous batch so
+// that a round's panes fit), so a bucket's groups are normally flushed once.
+template <int MS, int E, int NT>
+struct AggLds {
+  uint64_t key[E];
+  int64_t agg[E * MS];
+  uint8_t nw[E];     // windows of the pane's records
+  uint8_t run[E];    // owned windows - 1
+  uint16_t live[E];  // compacted / sorted live entries
+  uint32_t fill, nl, b, c0, c1;
+  uint32_t wsum[NT / 64];
+  uint64_t base;
+  uint64_t red[2][NT / 64];
+};
+
+// Flush every live entry of the table as window updates, then clear it.
+// Block-wide: every thread calls. Returns the number of live entries.
+template <int MS, int E, int NT>
+__device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const Program &prog, const TwParams &p, const TwTable &t,
+                              const PartBuffers &pb, DevScalars *sc, int S, bool exclusive, uint32_t &fresh,
+                              uint32_t &err, uint64_t &t_sort) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t SW = S ? (uint32_t)S : 1u;
+  const uint64_t t0 = wall_clock64();
+  // compact the live entries (one LDS atomic per wave)
+  for (int e0 = 0; e0 < E; e0 += NT) {
+    const int e = e0 + threadIdx.x;
+    const bool on = L.key[e] != kEmpty;
+    const uint64_t m = __ballot(on);
+    uint32_t wb = 0;
+    if (lane == 0 && m) wb = atomicAdd(&L.nl, (uint32_t)__popcll(m));
+    wb = __shfl(wb, 0, 64);
+    if (on) L.live[wb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)e;
+  }
+  __syncthreads();
+  const uint32_t nl = L.nl;
+  if (S > 1 && nl > 1) {
+    // panes of one key become neighbours: bitonic sort of the live list by
+    // (key, pane), padded to a power of two with +inf
+    uint32_t M = 1;
+    while (M < nl) M <<= 1;
+    for (uint32_t q = nl + threadIdx.x; q < M; q += NT) L.live[q] = 0xFFFFu;
+    __syncthreads();
+    for (uint32_t k = 2; k <= M; k <<= 1) {
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        for (uint32_t i = threadIdx.x; i < M; i += NT) {
+          const uint32_t ixj = i ^ j;
+          if (ixj <= i) continue;
+          const uint16_t x = L.live[i], y = L.live[ixj];
+          const uint64_t kx = x == 0xFFFFu ? kEmpty : L.key[x];
+          const uint64_t ky = y == 0xFFFFu ? kEmpty : L.key[y];
+          if ((kx > ky) == ((i & k) == 0)) {
+            L.live[i] = y;
+            L.live[ixj] = x;
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  t_sort += wall_clock64() - t0;
+  // owned window run of every pane: [max(P - n + 1, previous pane + 1), P]
+  uint32_t cnt = 0;
+  for (uint32_t q = threadIdx.x; q < nl; q += NT) {
+    const int e = L.live[q];
+    const uint64_t g = L.key[e];
+    const uint32_t P = (uint32_t)g;
+    uint32_t a = P - (L.nw[e] - 1u);
+    if (S > 1 && q > 0) {
+      const uint64_t gp = L.key[L.live[q - 1]];
+      if ((gp >> 32) == (g >> 32) && (uint32_t)gp + 1u > a) a = (uint32_t)gp + 1u;
+    }
+    L.run[e] = (uint8_t)(P - a);
+    cnt += P - a + 1;
+  }
+  // block exclusive scan of the window counts -> changelog list positions
+  const uint64_t incl = wave_incl_sum((uint64_t)cnt);
+  if (lane == 63) L.wsum[wv] = (uint32_t)incl;
+  __syncthreads();
+  uint64_t o = incl - cnt, total = 0;
+  for (int k = 0; k < NT / 64; ++k) {
+    if (k < wv) o += L.wsum[k];
+    total += L.wsum[k];
+  }
+  if (threadIdx.x == 0) L.base = total ? atomicAdd((unsigned long long *)&sc->scratch[1], (unsigned long long)total) : 0;
+  __syncthreads();
+  o += L.base;
+  for (uint32_t q = threadIdx.x; q < nl; q += NT) {
+    const int e = L.live[q];
+    const uint64_t g = L.key[e];
+    const uint64_t kb = g & 0xFFFFFFFF00000000ull;
+    const uint32_t P = (uint32_t)g;
+    const uint32_t a = P - L.run[e];
+    int64_t acc[MS];
+#pragma unroll
+    for (int s = 0; s < MS; ++s) acc[s] = L.agg[e * MS + s];
+    // later panes of the key (sorted after q) that window w covers: pane <= w + SW - 1
+    uint32_t j = q + 1;
+    uint64_t top = (uint64_t)a + SW - 1;
+    for (uint32_t w = a;; ++w) {
+      while (S > 1 && j < nl) {
+        const int f = L.live[j];
+        const uint64_t gj = L.key[f];
+        if ((gj & 0xFFFFFFFF00000000ull) != kb || (uint64_t)(uint32_t)gj > top) break;
+        acc_combine<MS>(prog, acc, &L.agg[f * MS]);
+        ++j;
+      }
+      const uint32_t sl = flush_window<MS>(prog, p, t, kb | w, acc, exclusive, fresh, err);
+      if (o < pb.touched_cap) pb.touched[o] = sl;
+      else err |= ERR_OOM;
+      ++o;
+      if (w == P) break;
+      ++top;
+    }
+  }
+  __syncthreads();
+  // clear the table
+  for (uint32_t q = threadIdx.x; q < nl; q += NT) {
+    const int e = L.live[q];
+    L.key[e] = kEmpty;
+#pragma unroll
+    for (int s = 0; s < MS; ++s) L.agg[e * MS + s] = s < prog.n_slots ? slot_identity_dev(prog.slot_op[s]) : 0;
+  }
+  if (threadIdx.x == 0) {
+    L.fill = 0;
+    L.nl = 0;
+  }
+  __syncthreads();
+  return nl;
+}
+
+template <int MS, int E, int WMAX, int RPT, int NT, bool FAN>
+__global__ __launch_bounds__(NT, 1024 / NT) void k_part_agg(Program prog, TwParams p, PartParams pp, TwTable t,
+                                                            PartBuffers pb, DevScalars *sc) {
+  __shared__ AggLds<MS, E, NT> L;
+  if (sc->redo) return;  // uniform: the optimistic pass found late records
+  constexpr int SUB = NT * RPT;
   const int nb = 1 << pp.np_log2;
   const uint32_t *chunk_start = pb.chunk_start;
   const uint64_t t0 = wall_clock64();
   if (threadIdx.x == 0) {
-    // find this workgroup's bucket: chunk_start[b] <= blockIdx.x < chunk_start[b + 1]
-    uint32_t w = blockIdx.x;
-    int lo = 0, hi = nb;
-    while (lo < hi) {
-      int m = (lo + hi) >> 1;
-      if (chunk_start[m + 1] <= w) lo = m + 1;
-      else hi = m;
-    }
-    sb = (uint32_t)lo;
-    sc0 = chunk_start[lo];
-    sc1 = chunk_start[lo + 1];
-    lfill = 0;
-    ltn = 0;
-    lnl = 0;
+    // this workgroup's bucket: chunk_start[b] <= blockIdx.x < chunk_start[b + 1]
+    const uint32_t bk = blockIdx.x < chunk_start[nb] ? pb.chunk_bucket[blockIdx.x] : 0;
+    L.b = bk;
+    L.c0 = chunk_start[bk];
+    L.c1 = chunk_start[bk + 1];
+    L.fill = 0;
+    L.nl = 0;
   }
-  for (int e = threadIdx.x; e < E; e += kAggThreads) {
-    lkey[e] = kEmpty;
+  for (int e = threadIdx.x; e < E; e += NT) {
+    L.key[e] = kEmpty;
 #pragma unroll
-    for (int s = 0; s < MS; ++s) lagg[e * MS + s] = s < prog.n_slots ? slot_identity_dev(prog.slot_op[s]) : 0;
+    for (int s = 0; s < MS; ++s) L.agg[e * MS + s] = s < prog.n_slots ? slot_identity_dev(prog.slot_op[s]) : 0;
   }
   __syncthreads();
-  if (blockIdx.x >= chunk_start[nb]) return;  // uniform: grid is an upper bound
-  const uint32_t b = sb;
-  const uint64_t b0 = pb.off[(uint64_t)b * pp.tiles], b1 = pb.off[(uint64_t)(b + 1) * pp.tiles];
-  const uint64_t c = blockIdx.x - sc0;
-  const bool exclusive = (sc1 - sc0) == 1;
-  const uint64_t r0 = b0 + c * kAggChunk, r1 = r0 + kAggChunk < b1 ? r0 + kAggChunk : b1;
+  if (blockIdx.x >= chunk_start[nb]) return;  // uniform: the grid is an upper bound
+  const uint32_t b = L.b;
+  const uint64_t b0 = pb.bstart[b], b1 = pb.bstart[b + 1];
+  const uint64_t c = blockIdx.x - L.c0;
+  const bool exclusive = (L.c1 - L.c0) == 1;
+  const uint64_t r0 = b0 + c * pp.chunk, r1 = r0 + pp.chunk < b1 ? r0 + pp.chunk : b1;
   const uint32_t limit = (uint32_t)(E * 3 / 4);
   const int W = pp.words;
   const int C = W - 2 - pp.has_seq;
-  const uint64_t t1 = wall_clock64();
-  uint64_t pairs = 0;
+  const int S = pp.pane_S;
+  const int nrounds = 1 << pp.rbits;
+  const int64_t k_epoch = sc->k_epoch;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t pairs = 0, groups = 0, t_rec = 0, t_flush = 0, t_sort = 0, flushes = 0;
   uint32_t fresh = 0, err = 0;
-  // KU records (whole, in registers) are loaded per thread before any is processed
-  for (uint64_t i0 = r0 + threadIdx.x; i0 < r1; i0 += (uint64_t)kAggThreads * KU) {
-    PRec<WMAX> rr[KU];
+  const uint64_t t1 = wall_clock64();
+
+  for (int round = 0; round < nrounds; ++round) {
+    for (uint64_t s0 = r0; s0 < r1; s0 += SUB) {
+      uint64_t ta = wall_clock64();
+      PRec<WMAX> rr[RPT];
+      auto load = [&]() {
 #pragma unroll
-    for (int u = 0; u < KU; ++u) {
-      const uint64_t i = i0 + (uint64_t)u * kAggThreads;
-      rr[u].C = C;
+        for (int u = 0; u < RPT; ++u) {
+          const uint64_t i = s0 + (uint64_t)u * NT + threadIdx.x;
+          const bool in = i < r1;
+          rr[u].C = C;
 #pragma unroll
-      for (int q = 0; q < WMAX; ++q) rr[u].w[q] = (i < r1 && q < W) ? pb.rec[i * W + q] : 0;
-    }
-    // one instance of the record body (a rolled loop over a shifting register
-    // queue): unrolling it KU times overflowed the instruction cache.
-    // Out-of-range records were loaded as zeros (no windows).
-#pragma unroll 1
-    for (int u = 0; u < KU; ++u) {
-    const PRec<WMAX> r = rr[0];
-#pragma unroll
-    for (int k = 0; k + 1 < KU; ++k) rr[k] = rr[k + 1];
-    const uint64_t w0 = r.w[0];
-    const uint32_t key = (uint32_t)w0, krel = (uint32_t)(w0 >> 32);
-    const uint32_t nw = (uint32_t)r.w[1];
-    pairs += nw;
-    for (uint32_t j = 0; j < nw; ++j) {
-      const uint64_t g = ((uint64_t)key << 32) | (uint64_t)(krel + j);
-      uint32_t h = (uint32_t)(mix64(g) & (E - 1));
-      int e = -1;
-      for (int probe = 0; probe < 32; ++probe) {
-        uint64_t cur = lkey[h];
-        if (cur == g) { e = (int)h; break; }
-        if (cur == kEmpty) {
-          if (lfill >= limit) break;  // table nearly full: leave new groups to HBM
-          uint64_t old = atomicCAS((unsigned long long *)&lkey[h], (unsigned long long)kEmpty, (unsigned long long)g);
-          if (old == kEmpty) {
-            atomicAdd(&lfill, 1u);
-            e = (int)h;
-            break;
-          }
-          if (old == g) { e = (int)h; break; }
+          for (int q = 0; q < WMAX; ++q) rr[u].w[q] = (in && q < W) ? pb.rec[i * W + q] : 0;
         }
-        h = (h + 1) & (E - 1);
-      }
-      if (e >= 0) {
-        lds_apply<MS>(prog, &lagg[e * MS], r);
-      } else {
-        // overflow: straight to the HBM table
-        int64_t slot = tw_find_or_insert(t, g, fresh);
-        if (slot < 0) { err |= ERR_OOM; continue; }
-        int64_t v[MS];
+      };
+      load();
+      uint32_t pend = 0;
 #pragma unroll
-        for (int s = 0; s < MS; ++s) v[s] = s < prog.n_slots ? prec_elem(prog, s, r) : 0;
-        flush_row(prog, t.aggs + (uint64_t)slot * prog.n_slots, v, false);
-        if (atomicExch(&t.stamp[slot], (uint32_t)p.batch_id) != (uint32_t)p.batch_id)
-          pb.touched[atomicAdd((unsigned long long *)&sc->scratch[1], 1ull)] = (uint32_t)slot;
+      for (int u = 0; u < RPT; ++u) {
+        const uint64_t i = s0 + (uint64_t)u * NT + threadIdx.x;
+        if (i < r1 && (nrounds == 1 || key_round((uint32_t)rr[u].w[0], pp.np_log2, pp.rbits) == (uint32_t)round))
+          pend |= 1u << u;
+      }
+      uint32_t dpend = 0;  // records for the direct HBM path
+      for (;;) {
+        // one instance of the record body (a rolled loop over a rotating register
+        // queue, back in order after RPT steps): unrolling it overflowed the
+        // instruction cache
+#pragma unroll 1
+        for (int u = 0; u < RPT; ++u) {
+          const PRec<WMAX> r = rr[0];
+#pragma unroll
+          for (int k = 0; k + 1 < RPT; ++k) rr[k] = rr[k + 1];
+          rr[RPT - 1] = r;
+          if (!((pend >> u) & 1u)) continue;
+          const uint32_t key = (uint32_t)r.w[0], krel = (uint32_t)(r.w[0] >> 32);
+          const uint32_t nw = (uint32_t)r.w[1];
+          if (FAN) {
+            // fan-out: one entry per window, overflow straight to HBM
+            pairs += nw;
+            for (uint32_t j = 0; j < nw; ++j) {
+              const uint64_t g = ((uint64_t)key << 32) | (uint64_t)(krel + j);
+              const int e = lds_insert<E>(L.key, &L.fill, limit, g);
+              if (e >= 0) {
+                lds_apply<MS>(prog, &L.agg[e * MS], r);
+                L.nw[e] = 1;
+              } else {
+                direct_windows<MS>(prog, p, t, pb, sc, key, krel + j, krel + j, r, fresh, err);
+              }
+            }
+            pend &= ~(1u << u);
+            continue;
+          }
+          if (nw == 0) {  // never written by the scatter (cannot happen; keep loops bounded)
+            pend &= ~(1u << u);
+            continue;
+          }
+          const uint32_t P = krel + nw - 1;
+          const int64_t pabs = (int64_t)P + k_epoch;
+          const uint32_t full = pabs + 1 < (int64_t)S ? (uint32_t)(pabs + 1) : (uint32_t)S;
+          if (nw != full) {
+            // some earliest windows were rejected by grace: not a whole pane;
+            // straight to HBM after this loop
+            dpend |= 1u << u;
+            pend &= ~(1u << u);
+            continue;
+          }
+          if (pp.exp == 2) { pairs += nw; pend &= ~(1u << u); continue; }
+          const int e = lds_insert<E>(L.key, &L.fill, limit, ((uint64_t)key << 32) | P);
+          if (e < 0) continue;  // table full: after the next flush
+          pairs += nw;
+          if (pp.exp != 1) lds_apply<MS>(prog, &L.agg[e * MS], r);
+          L.nw[e] = (uint8_t)nw;
+          pend &= ~(1u << u);
+        }
+        const bool more = __syncthreads_or(pend != 0);
+        const uint64_t tb = wall_clock64();
+        t_rec += tb - ta;
+        if (!more) break;
+        // table full with records left: flush and go on (the records are
+        // loaded again afterwards, so they hold no registers across the flush)
+        groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, fresh, err, t_sort);
+        ++flushes;
+        load();
+        ta = wall_clock64();
+        t_flush += ta - tb;
+      }
+      if (!FAN && __syncthreads_or(dpend != 0)) {
+        load();
+#pragma unroll 1
+        for (int u = 0; u < RPT; ++u) {
+          const PRec<WMAX> r = rr[0];
+#pragma unroll
+          for (int k = 0; k + 1 < RPT; ++k) rr[k] = rr[k + 1];
+          rr[RPT - 1] = r;
+          if (!((dpend >> u) & 1u)) continue;
+          const uint32_t key = (uint32_t)r.w[0], krel = (uint32_t)(r.w[0] >> 32);
+          const uint32_t nw = (uint32_t)r.w[1];
+          pairs += nw;
+          direct_windows<MS>(prog, p, t, pb, sc, key, krel, krel + nw - 1, r, fresh, err);
+        }
       }
     }
-    }
+    const uint64_t tb = wall_clock64();
+    groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, fresh, err, t_sort);
+    ++flushes;
+    t_flush += wall_clock64() - tb;
   }
-  __syncthreads();
-  const uint64_t t2 = wall_clock64();
-  // flush: one HBM update per group of the chunk. Compact the live entries
-  // first so a thread carries about one group; every HBM access of a group is
-  // issued before any of its results is needed.
-  for (int e = threadIdx.x; e < E; e += kAggThreads)
-    if (lkey[e] != kEmpty) llive[atomicAdd(&lnl, 1u)] = (uint16_t)e;
-  __syncthreads();
-  const uint32_t nl = lnl;
-  uint64_t groups = 0;
-  for (uint32_t q = threadIdx.x; q < nl; q += kAggThreads) {
-    const int e = llive[q];
-    const uint64_t g = lkey[e];
-    ++groups;
-    const uint32_t f0 = fresh;
-    const int64_t slot = tw_find_or_insert(t, g, fresh);
-    if (slot < 0) { err |= ERR_OOM; continue; }
-    int64_t v[MS];
-#pragma unroll
-    for (int s = 0; s < MS; ++s) v[s] = lagg[e * MS + s];
-    int64_t *row = t.aggs + (uint64_t)slot * prog.n_slots;
-    bool first;
-    if (exclusive && fresh != f0) {
-      // inserted just now by the group's only writer: the row holds identities
-#pragma unroll
-      for (int s = 0; s < MS; ++s)
-        if (s < prog.n_slots && prog.slot_op[s] != S_LAST_VAL) row[s] = v[s];
-      t.stamp[slot] = (uint32_t)p.batch_id;
-      first = true;
-    } else if (exclusive) {
-      int64_t cur[MS];
-#pragma unroll
-      for (int s = 0; s < MS; ++s) cur[s] = s < prog.n_slots ? row[s] : 0;
-      const uint32_t st = t.stamp[slot];
-#pragma unroll
-      for (int s = 0; s < MS; ++s) {
-        if (s >= prog.n_slots) break;
-        const int op = prog.slot_op[s];
-        if (op == S_LAST_VAL || v[s] == slot_identity_dev(op)) continue;
-        row[s] = op == S_LAST_SEQ ? ((uint64_t)v[s] > (uint64_t)cur[s] ? v[s] : cur[s]) : slot_combine(op, cur[s], v[s]);
-      }
-      first = st != (uint32_t)p.batch_id;
-      if (first) t.stamp[slot] = (uint32_t)p.batch_id;
-    } else {
-      flush_row(prog, row, v, false);
-      first = atomicExch(&t.stamp[slot], (uint32_t)p.batch_id) != (uint32_t)p.batch_id;
-    }
-    // first touch of the group in this batch -> touched list (per-batch changelog)
-    if (first) ltouch[atomicAdd(&ltn, 1u)] = (uint32_t)slot;
-  }
-  __syncthreads();
   const uint64_t t3 = wall_clock64();
-  if (threadIdx.x == 0) lbase = ltn ? atomicAdd((unsigned long long *)&sc->scratch[1], (unsigned long long)ltn) : 0;
-  __syncthreads();
-  for (uint32_t q = threadIdx.x; q < ltn; q += kAggThreads) pb.touched[lbase + q] = ltouch[q];
   pairs = wave_sum_u64(pairs);
-  uint64_t fr = wave_sum_u64(fresh);
-  groups = wave_sum_u64(groups);
-  if ((threadIdx.x & 63) == 0) {
-    sred[0][threadIdx.x >> 6] = pairs;
-    sred[1][threadIdx.x >> 6] = fr;
-    sred[2][threadIdx.x >> 6] = groups;
+  const uint64_t fr = wave_sum_u64(fresh);
+  if (lane == 0) {
+    L.red[0][wv] = pairs;
+    L.red[1][wv] = fr;
   }
   if (err) atomicOr(&sc->err, err);
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint64_t a = 0, f = 0, gr = 0;
-    for (int k = 0; k < kAggThreads / 64; ++k) {
-      a += sred[0][k];
-      f += sred[1][k];
-      gr += sred[2][k];
+    uint64_t a = 0, f = 0;
+    for (int k = 0; k < NT / 64; ++k) {
+      a += L.red[0][k];
+      f += L.red[1][k];
     }
     if (a) atomicAdd((unsigned long long *)&sc->pairs, (unsigned long long)a);
     if (f) atomicAdd((unsigned long long *)&sc->live, (unsigned long long)f);
-    if (gr) atomicAdd((unsigned long long *)&sc->scratch[0], (unsigned long long)gr);
+    if (groups) atomicAdd((unsigned long long *)&sc->scratch[0], (unsigned long long)groups);
     // phase clock (100 MHz wall clock) sums: init, records, flush, tail, workgroups
     const uint64_t t4 = wall_clock64();
     atomicAdd((unsigned long long *)&sc->scratch[8], (unsigned long long)(t1 - t0));
-    atomicAdd((unsigned long long *)&sc->scratch[9], (unsigned long long)(t2 - t1));
-    atomicAdd((unsigned long long *)&sc->scratch[10], (unsigned long long)(t3 - t2));
+    atomicAdd((unsigned long long *)&sc->scratch[9], (unsigned long long)t_rec);
+    atomicAdd((unsigned long long *)&sc->scratch[10], (unsigned long long)t_flush);
     atomicAdd((unsigned long long *)&sc->scratch[11], (unsigned long long)(t4 - t3));
     atomicAdd((unsigned long long *)&sc->scratch[12], 1ull);
+    atomicAdd((unsigned long long *)&sc->scratch[18], (unsigned long long)t_sort);
+    atomicAdd((unsigned long long *)&sc->scratch[19], 0ull);
+    atomicAdd((unsigned long long *)&sc->scratch[20], (unsigned long long)flushes);
   }
 }
 
 bool part_supported(const Program &prog) { return prog.n_slots <= 8; }
 
-// per-batch changelog: one row per group in the touched list
-__global__ __launch_bounds__(256) void k_part_emit(TwTable t, Program prog, TwParams p, PartBuffers pb, OutCols out,
-                                                   uint64_t out_base, uint64_t out_cap, DevScalars *sc) {
-  const uint64_t n = sc->scratch[1];
+// ---------------------------------------------------------------------------
+// per-batch changelog: one row per first update of a group in the touched list
+// (entries of later updates are kTouchSkip); counts, scan, compacted rows.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_touch_count(const uint32_t *__restrict__ touched, const DevScalars *sc,
+                                                     uint64_t cap, uint32_t *__restrict__ cnt) {
+  __shared__ uint64_t sw[4];
+  uint64_t n = sc->scratch[1];
+  if (n > cap) n = cap;
+  const uint64_t c0 = (uint64_t)blockIdx.x * kTouchChunk;
+  uint64_t h = 0;
+  if (c0 < n)
+    for (uint64_t q = c0 + threadIdx.x; q < c0 + kTouchChunk && q < n; q += 256) h += touched[q] != kTouchSkip;
+  h = wave_sum_u64(h);
+  if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = (uint32_t)(sw[0] + sw[1] + sw[2] + sw[3]);
+}
+
+__global__ __launch_bounds__(256) void k_touch_emit(TwTable t, Program prog, TwParams p, const uint32_t *touched,
+                                                    uint64_t cap, const uint64_t *off, OutCols out, uint64_t out_base,
+                                                    uint64_t out_cap, DevScalars *sc) {
+  __shared__ uint64_t swave[4];
+  uint64_t n = sc->scratch[1];
+  if (n > cap) n = cap;
+  const uint64_t c0 = (uint64_t)blockIdx.x * kTouchChunk;
+  if (c0 >= n) return;  // uniform
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t k_epoch = sc->k_epoch;
   const bool unwin = p.kind == HSG_UNWINDOWED;
-  if (blockIdx.x == 0 && threadIdx.x == 0) sc->out_rows = n;
-  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < n; q += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t o = out_base + q;
+  uint64_t run = off[blockIdx.x];
+  for (uint64_t blk = c0; blk < c0 + kTouchChunk && blk < n; blk += 256) {
+    const uint64_t q = blk + threadIdx.x;
+    const uint32_t s = q < n ? touched[q] : kTouchSkip;
+    const bool hit = s != kTouchSkip;
+    const uint64_t f = hit ? 1 : 0;
+    const uint64_t incl = wave_incl_sum(f);
+    if (lane == 63) swave[w] = incl;
+    __syncthreads();
+    uint64_t o = run + incl - f;
+    for (int k = 0; k < w; ++k) o += swave[k];
+    run += swave[0] + swave[1] + swave[2] + swave[3];
+    __syncthreads();
+    if (!hit) continue;
+    o += out_base;
     if (o >= out_cap) {
       atomicOr(&sc->err, ERR_OOM);
-      break;
+      continue;
     }
-    const uint32_t s = pb.touched[q];
-    const uint64_t g = t.keys[s];
-    const int64_t *row = t.aggs + (uint64_t)s * prog.n_slots;
+    const uint64_t g = *t.key(s);
+    const int64_t *row = t.aggs(s);
     out.key[o] = (uint32_t)(g >> 32);
     int64_t ws = 0, we = 0;
     if (!unwin) {
@@ -637,30 +1050,56 @@ __global__ __launch_bounds__(256) void k_part_emit(TwTable t, Program prog, TwPa
 
 void launch_part_emit(hipStream_t s, const TwTable &t, const Program &prog, const TwParams &p, const PartBuffers &pb,
                       OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc) {
-  hipLaunchKernelGGL(k_part_emit, dim3(2048), dim3(256), 0, s, t, prog, p, pb, out, out_base, out_cap, sc);
+  const uint64_t nc = touch_chunks(pb.touched_cap);
+  hipLaunchKernelGGL(k_touch_count, dim3((unsigned)nc), dim3(256), 0, s, pb.touched, sc, pb.touched_cap, pb.tcnt);
+  scan_excl_u32(s, pb.tcnt, pb.toff, nc, pb.tpartial, &sc->out_rows);
+  hipLaunchKernelGGL(k_touch_emit, dim3((unsigned)nc), dim3(256), 0, s, t, prog, p, pb.touched, pb.touched_cap,
+                     pb.toff, out, out_base, out_cap, sc);
 }
 
-template <int MS, int E>
+// Aggregation variants: small = E_s entries and 512 threads (two workgroups per
+// CU), big = E_l entries and 1024 threads (one per CU). Records per thread
+// keep the record queue within 128 VGPRs.
+template <int MS, int E, int NT, int RPT4>
+static void agg_launch_v(hipStream_t s, dim3 g, int W, const Program &prog, const TwParams &p, const PartParams &pp,
+                         const TwTable &t, const PartBuffers &pb, DevScalars *sc) {
+  const dim3 th(NT);
+  constexpr int R6 = RPT4 / 2 > 0 ? RPT4 / 2 : 1, R11 = RPT4 / 4 > 0 ? RPT4 / 4 : 1;
+  if (pp.pane_S == 0) {
+    // fan-out (size not a multiple of advance): one generic-width variant
+    hipLaunchKernelGGL((k_part_agg<MS, E, kPartMaxWords, R11, NT, true>), g, th, 0, s, prog, p, pp, t, pb, sc);
+    return;
+  }
+  if (W <= 3) hipLaunchKernelGGL((k_part_agg<MS, E, 3, RPT4, NT, false>), g, th, 0, s, prog, p, pp, t, pb, sc);
+  else if (W <= 4) hipLaunchKernelGGL((k_part_agg<MS, E, 4, RPT4, NT, false>), g, th, 0, s, prog, p, pp, t, pb, sc);
+  else if (W <= 6) hipLaunchKernelGGL((k_part_agg<MS, E, 6, R6, NT, false>), g, th, 0, s, prog, p, pp, t, pb, sc);
+  else hipLaunchKernelGGL((k_part_agg<MS, E, kPartMaxWords, R11, NT, false>), g, th, 0, s, prog, p, pp, t, pb, sc);
+}
+
+template <int MS>
 static void agg_launch(hipStream_t s, dim3 g, int W, const Program &prog, const TwParams &p, const PartParams &pp,
                        const TwTable &t, const PartBuffers &pb, DevScalars *sc) {
-  const dim3 th(kAggThreads);
-  constexpr int KU4 = MS >= 6 ? 6 : 8;  // records in flight per thread, within 128 VGPRs
-  if (W <= 4) hipLaunchKernelGGL((k_part_agg<MS, E, 4, KU4>), g, th, 0, s, prog, p, pp, t, pb, sc);
-  else if (W <= 6) hipLaunchKernelGGL((k_part_agg<MS, E, 6, 4>), g, th, 0, s, prog, p, pp, t, pb, sc);
-  else hipLaunchKernelGGL((k_part_agg<MS, E, kPartMaxWords, 2>), g, th, 0, s, prog, p, pp, t, pb, sc);
+  constexpr int ES = MS <= 2 ? 2048 : 1024, EL = MS <= 2 ? 4096 : 2048;
+  if (pp.big) agg_launch_v<MS, EL, 1024, 8>(s, g, W, prog, p, pp, t, pb, sc);
+  else agg_launch_v<MS, ES, 512, 4>(s, g, W, prog, p, pp, t, pb, sc);
+}
+
+uint64_t part_lds_entries(const Program &prog, bool big) {
+  return prog.n_slots <= 2 ? (big ? 4096 : 2048) : (big ? 2048 : 1024);
 }
 
 bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, const PartParams &pp, const TwTable &t,
                      const PartBuffers &pb, uint64_t n, DevScalars *sc) {
   if (!part_supported(prog)) return false;
   const uint64_t nb = 1ull << pp.np_log2;
-  hipLaunchKernelGGL(k_part_chunks, dim3(1), dim3(1024), 0, s, pb.off, pp.tiles, pp.np_log2, pb.chunk_start);
-  const dim3 g((unsigned)(nb + n / kAggChunk + 1));
+  hipLaunchKernelGGL(k_part_chunks, dim3(1), dim3(1024), 0, s, pb.bstart, pp.np_log2, pp.chunk, pb.chunk_start,
+                     pb.chunk_bucket);
+  const dim3 g((unsigned)(nb + n / pp.chunk + 1));
   const int W = pp.words;
-  if (prog.n_slots <= 2) agg_launch<2, 2048>(s, g, W, prog, p, pp, t, pb, sc);
-  else if (prog.n_slots <= 4) agg_launch<4, 1024>(s, g, W, prog, p, pp, t, pb, sc);
-  else if (prog.n_slots <= 6) agg_launch<6, 1024>(s, g, W, prog, p, pp, t, pb, sc);
-  else agg_launch<8, 1024>(s, g, W, prog, p, pp, t, pb, sc);
+  if (prog.n_slots <= 2) agg_launch<2>(s, g, W, prog, p, pp, t, pb, sc);
+  else if (prog.n_slots <= 4) agg_launch<4>(s, g, W, prog, p, pp, t, pb, sc);
+  else if (prog.n_slots <= 6) agg_launch<6>(s, g, W, prog, p, pp, t, pb, sc);
+  else agg_launch<8>(s, g, W, prog, p, pp, t, pb, sc);
   return true;
 }
 

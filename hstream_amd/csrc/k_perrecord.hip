@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kTileThreads) void k_pr_pairs(Batch b, TwParams p, 
           int64_t slot = tw_find_or_insert(t, g, fresh);
           uint32_t s32;
           if (slot < 0) { err |= ERR_OOM; s32 = (uint32_t)(t.mask + 1); }
-          else { s32 = (uint32_t)slot; t.stamp[slot] = (uint32_t)p.batch_id; }
+          else { s32 = (uint32_t)slot; *t.stamp(slot) = (uint32_t)p.batch_id; }
           pb.pslot[o + c] = s32;
           pb.pidx[o + c] = (uint32_t)(o + c);
           pb.prec[o + c] = (uint32_t)i;
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_apply(Batch b, Program prog
     if (sl != cur_slot) {
       cur_slot = sl;
 #pragma unroll
-      for (int s = 0; s < MS; ++s) basev[s] = s < prog.n_slots ? t.aggs[(uint64_t)sl * prog.n_slots + s] : 0;
+      for (int s = 0; s < MS; ++s) basev[s] = s < prog.n_slots ? t.aggs(sl)[s] : 0;
     }
     int64_t R[MS];
 #pragma unroll
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_apply(Batch b, Program prog
     // changelog row at the pair's arrival position
     const uint64_t o = out_base + pi;
     const uint32_t rec = pb.prec[pi];
-    const uint64_t g = t.keys[sl];
+    const uint64_t g = *t.key(sl);
     out.key[o] = (uint32_t)(g >> 32);
     int64_t ws = 0, we = 0;
     if (!unwin) {
@@ -344,12 +344,12 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_apply(Batch b, Program prog
 
 // copy final rows of every segment end from the shadow table into the state
 __global__ void k_seg_commit(const uint32_t *slot, uint64_t P, uint64_t cap, int n_slots, const int64_t *shadow,
-                             int64_t *aggs) {
+                             TwTable t) {
   for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < P; q += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t sl = slot[q];
     if (sl >= cap) continue;
     if (q + 1 == P || slot[q + 1] != sl)
-      for (int s = 0; s < n_slots; ++s) aggs[(uint64_t)sl * n_slots + s] = shadow[(uint64_t)sl * n_slots + s];
+      for (int s = 0; s < n_slots; ++s) t.aggs(sl)[s] = shadow[(uint64_t)sl * n_slots + s];
   }
 }
 
@@ -366,7 +366,7 @@ static void seg_launch(hipStream_t s, const Batch &b, const Program &prog, const
   hipLaunchKernelGGL(k_seg_apply<MS>, dim3((unsigned)nb), dim3(kSegThreads), 0, s, b, prog, pb, p, t, slot, pidx, P,
                      seq, pb.carry, out, out_base, sc);
   hipLaunchKernelGGL(k_seg_commit, dim3(grid_for(P, 256)), dim3(256), 0, s, slot, P, t.mask + 1, prog.n_slots,
-                     pb.shadow, t.aggs);
+                     pb.shadow, t);
 }
 
 void launch_pr_segscan(hipStream_t s, const Batch &b, const Program &prog, const PrBuffers &pb, const TwParams &p,

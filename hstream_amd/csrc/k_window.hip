@@ -35,6 +35,50 @@ __global__ void k_fill_rows(int64_t *__restrict__ aggs, uint64_t rows, Program p
     aggs[i] = slot_identity_dev(prog.slot_op[i % prog.n_slots]);
 }
 
+__global__ void k_tw_reset(TwTable t, Program prog) {
+  const uint64_t cap = t.mask + 1, words = cap * t.stride;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < words; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t wi = (t.stride & (t.stride - 1)) ? (uint32_t)(i % t.stride) : (uint32_t)(i & (t.stride - 1));
+    uint64_t v = 0;
+    if (wi == 0) v = kEmpty;
+    else if (wi >= 2 && (int)(wi - 2) < prog.n_slots) v = (uint64_t)slot_identity_dev(prog.slot_op[wi - 2]);
+    t.rows[i] = v;
+  }
+}
+
+// per-batch scalars: err .. touched, redo and scratch (wm / epoch / live persist)
+__global__ void k_clear_scalars(DevScalars *sc) {
+  const int t = threadIdx.x;
+  if (t == 0) {
+    sc->err = 0;
+    sc->pairs = 0;
+    sc->late = 0;
+    sc->out_rows = 0;
+    sc->touched = 0;
+    sc->redo = 0;
+  }
+  if (t < 23) sc->scratch[t] = 0;
+}
+void launch_clear_scalars(hipStream_t s, DevScalars *sc) { hipLaunchKernelGGL(k_clear_scalars, dim3(1), dim3(64), 0, s, sc); }
+
+// changelog rows [from, from + n) of src into device columns (null = skip), one launch
+__global__ void k_copy_rows(OutCols src, uint64_t from, uint64_t n, int n_aggs, uint32_t *key, int64_t *ws, int64_t *we,
+                            int64_t *si, RowPtrs aggs) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t q = from + i;
+    if (key) key[i] = src.key[q];
+    if (ws) ws[i] = src.ws[q];
+    if (we) we[i] = src.we[q];
+    if (si) si[i] = src.src[q];
+    for (int j = 0; j < n_aggs; ++j)
+      if (aggs.p[j]) aggs.p[j][i] = src.agg[j][q];
+  }
+}
+void launch_copy_rows(hipStream_t s, const OutCols &src, uint64_t from, uint64_t n, int n_aggs, uint32_t *key,
+                      int64_t *ws, int64_t *we, int64_t *si, const RowPtrs &aggs) {
+  if (n) hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(n, 256)), dim3(256), 0, s, src, from, n, n_aggs, key, ws, we, si, aggs);
+}
+
 unsigned grid_for(uint64_t n, unsigned tpb) {
   uint64_t g = (n + tpb - 1) / tpb;
   if (g > 4096) g = 4096;
@@ -47,6 +91,9 @@ void launch_fill_u64(hipStream_t s, uint64_t *p, uint64_t n, uint64_t v) {
 }
 void launch_fill_u32(hipStream_t s, uint32_t *p, uint64_t n, uint32_t v) {
   if (n) hipLaunchKernelGGL(k_fill_u32, dim3(grid_for(n, 256)), dim3(256), 0, s, p, n, v);
+}
+void launch_tw_reset(hipStream_t s, const TwTable &t, const Program &prog) {
+  hipLaunchKernelGGL(k_tw_reset, dim3(4096), dim3(256), 0, s, t, prog);
 }
 void launch_fill_rows(hipStream_t s, int64_t *aggs, uint64_t rows, const Program &prog) {
   if (rows && prog.n_slots)
@@ -230,12 +277,12 @@ __global__ __launch_bounds__(kTileThreads) void k_tw_agg(Batch b, TwParams p, Tw
       if (PASS == 0) {
         int64_t slot = tw_find_or_insert(t, g, fresh);
         if (slot < 0) { err |= ERR_OOM; continue; }
-        apply_slots(prog, t.aggs + (uint64_t)slot * prog.n_slots, b, i, seq1);
-        t.stamp[slot] = (uint32_t)p.batch_id;
+        apply_slots(prog, t.aggs(slot), b, i, seq1);
+        *t.stamp(slot) = (uint32_t)p.batch_id;
         pairs += 1;
       } else {
         int64_t slot = tw_find(t, g);
-        if (slot >= 0) apply_last(prog, t.aggs + (uint64_t)slot * prog.n_slots, b, i, seq1);
+        if (slot >= 0) apply_last(prog, t.aggs(slot), b, i, seq1);
       }
     }
   }
@@ -277,9 +324,9 @@ void launch_tw_agg(hipStream_t s, const Batch &b, const TwParams &p, const TwTab
 // ---------------------------------------------------------------------------
 __device__ inline bool tw_hit(const TwTable &t, uint64_t s, uint64_t cap, int mode, uint32_t batch_id) {
   if (s >= cap) return false;
-  uint64_t g = t.keys[s];
+  uint64_t g = *t.key(s);
   if (g == kEmpty) return false;
-  return mode == 1 || t.stamp[s] == batch_id;
+  return mode == 1 || *t.stamp(s) == batch_id;
 }
 
 __global__ __launch_bounds__(256) void k_tw_emit_count(TwTable t, uint64_t cap, int mode, uint32_t batch_id,
@@ -320,8 +367,8 @@ __global__ __launch_bounds__(256) void k_tw_emit_rows(TwTable t, uint64_t cap, P
       atomicOr(&sc->err, ERR_OOM);
       continue;
     }
-    const uint64_t g = t.keys[s];
-    const int64_t *row = t.aggs + s * (uint64_t)prog.n_slots;
+    const uint64_t g = *t.key(s);
+    const int64_t *row = t.aggs(s);
     out.key[o] = (uint32_t)(g >> 32);
     int64_t ws = 0, we = 0;
     if (!unwin) {

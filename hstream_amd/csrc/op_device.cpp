@@ -80,47 +80,70 @@ int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog,
     off += bytes ? bytes : 1;
     return o;
   };
-  uint64_t o_hist = take(nh * 4), o_off = take((nh + 1) * 8), o_part = take((scan_partials_needed(nh) + 8) * 8);
+  const uint64_t ns = (1ull << kPartMaxLog2) * part_nseg(tiles);
+  uint64_t o_hist = take(nh * 4), o_offt = take(nh * 4), o_segsum = take(ns * 4), o_segoff = take((ns + 1) * 8);
+  uint64_t o_bstart = take(((1ull << kPartMaxLog2) + 1) * 8), o_part = take((scan_partials_needed(ns) + 8) * 8);
   uint64_t o_rec = take(n * words * 8), o_chunk = take(((1ull << kPartMaxLog2) + 1) * 4);
-  uint64_t o_touch = take(d.cap * 4), o_wm = take(n * 8);
+  uint64_t o_cbk = take(((1ull << kPartMaxLog2) + n / 1024 + 2) * 4);  // >= buckets + n / chunk + 1
+  const uint64_t tcap = n * (d.wpr ? d.wpr : 1), nc = touch_chunks(tcap);
+  uint64_t o_touch = take(tcap * 4), o_wm = take(n * 8);
+  uint64_t o_tcnt = take(nc * 4), o_toff = take((nc + 1) * 8), o_tpart = take((scan_partials_needed(nc) + 8) * 8);
   DTRY(hipMalloc(&d.part_mem, off));
   char *m = (char *)d.part_mem;
   pb.hist = (uint32_t *)(m + o_hist);
-  pb.off = (uint64_t *)(m + o_off);
+  pb.offt = (uint32_t *)(m + o_offt);
+  pb.segsum = (uint32_t *)(m + o_segsum);
+  pb.segoff = (uint64_t *)(m + o_segoff);
+  pb.bstart = (uint64_t *)(m + o_bstart);
   pb.partial = (uint64_t *)(m + o_part);
   pb.rec = (uint64_t *)(m + o_rec);
   pb.chunk_start = (uint32_t *)(m + o_chunk);
+  pb.chunk_bucket = (uint32_t *)(m + o_cbk);
   pb.touched = (uint32_t *)(m + o_touch);
+  pb.touched_cap = tcap;
+  pb.tcnt = (uint32_t *)(m + o_tcnt);
+  pb.toff = (uint64_t *)(m + o_toff);
+  pb.tpartial = (uint64_t *)(m + o_tpart);
   pb.wm = (int64_t *)(m + o_wm);
   pb.n_cap = n;
   return HSG_OK;
 }
 
-// Partitions for the next batch: about half an LDS table of groups per bucket,
-// and buckets of at least a few thousand records.
-static void adapt_partitions(OpDevice &d, const Program &prog, uint64_t groups, uint64_t n) {
-  const uint64_t per = part_lds_entries(prog) / 2;
-  uint64_t want = (groups + per - 1) / per;
-  // and buckets of about half a chunk, so nearly every bucket is owned by one
-  // workgroup (plain read-modify-write flush)
-  const uint64_t by_size = (2 * n + kAggChunk - 1) / kAggChunk;
-  if (by_size > want) want = by_size;
-  uint64_t cap_by_n = n / 2048 > 1 ? n / 2048 : 1;
-  if (want > cap_by_n) want = cap_by_n;
+// Partitions, aggregation variant and rounds for the next batch, from the
+// groups (LDS entries) the last batch flushed: buckets of at most half an LDS
+// table of groups, so a bucket is normally one workgroup's (plain
+// read-modify-write flushes) and its table is flushed once; the small table
+// (two workgroups per CU) when that needs at most 2^kPartMaxLog2 buckets;
+// fewer buckets mean longer coalesced runs in the scatter. When the bucket
+// count is at its maximum, key-hash rounds split a bucket's groups instead.
+static void adapt_partitions(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t groups, uint64_t n) {
+  const uint64_t by_size = (n + kAggChunk / 2 - 1) / (kAggChunk / 2);  // buckets of <= half a chunk on average
+  auto need = [&](bool big) {
+    const uint64_t per = part_lds_entries(prog, big) / 2;
+    uint64_t w = (groups + per - 1) / per;
+    return w > by_size ? w : by_size;
+  };
+  uint64_t want = need(false);
+  d.agg_big = want > (1ull << kPartMaxLog2);
+  if (d.agg_big) want = need(true);
   int l = 0;
   while ((1ull << l) < want && l < kPartMaxLog2) ++l;
   d.np_log2 = l < 4 ? 4 : l;
+  const uint64_t per_bucket = groups >> d.np_log2;
+  const uint64_t fit = part_lds_entries(prog, d.agg_big) * 6 / 10;
+  int rb = 0;
+  while ((fit << rb) < per_bucket && rb < 4) ++rb;
+  d.rbits = d.pane_S ? rb : 0;
 }
 
 int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err) {
   DTRY(hipMemsetAsync(d.sc, 0, sizeof(DevScalars), d.stream));
+  memset(d.h_sc, 0, sizeof(DevScalars));  // host mirror (epoch_set gates the optimistic path)
   if (cfg.window_kind == HSG_SESSION) {
     launch_ss_reset(d.stream, d.ss, d.cap);
     DTRY(hipMemsetAsync(d.arena_top, 0, sizeof(uint64_t), d.stream));
   } else {
-    launch_fill_u64(d.stream, d.tw.keys, d.cap, kEmpty);
-    launch_fill_rows(d.stream, d.tw.aggs, d.cap, prog);
-    DTRY(hipMemsetAsync(d.tw.stamp, 0, d.cap * sizeof(uint32_t), d.stream));
+    launch_tw_reset(d.stream, d.tw, prog);
     if (cfg.window_kind == HSG_UNWINDOWED) {
       // one implicit window: k = 0, epoch fixed at 0
       DevScalars init;
@@ -165,10 +188,10 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
     int rc = session_device_init(d, cfg, prog, rows, err);
     if (rc != HSG_OK) return rc;
   } else {
-    DTRY(dalloc(&d.tw.keys, d.cap));
-    DTRY(dalloc(&d.tw.aggs, d.cap * (uint64_t)prog.n_slots));
-    DTRY(dalloc(&d.tw.stamp, d.cap));
+    d.tw.stride = tw_row_stride(prog.n_slots);
+    DTRY(dalloc(&d.tw.rows, d.cap * (uint64_t)d.tw.stride));
     d.tw.mask = d.cap - 1;
+    d.tw.blocked = cfg.window_kind != HSG_UNWINDOWED && d.cap >= 64 ? 1u : 0u;
     uint64_t nb = emit_chunks(d.cap);
     DTRY(dalloc(&d.emit.cnt, nb));
     DTRY(dalloc(&d.emit.off, nb));
@@ -190,6 +213,10 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
     const char *env = getenv("HSG_AGG");
     d.use_part = !(env && strcmp(env, "atomic") == 0);
     if (d.use_part) {
+      // panes: size a multiple of advance (tumbling and unwindowed: one pane per window)
+      const int64_t adv = cfg.window_kind == HSG_HOPPING ? cfg.advance_ms : 0;
+      d.pane_S = 1;
+      if (adv > 0) d.pane_S = (cfg.size_ms % adv == 0 && cfg.size_ms / adv <= 64) ? (int)(cfg.size_ms / adv) : 0;
       rc = part_device_init(d, cfg, prog, err);
       if (rc != HSG_OK) return rc;
     }
@@ -218,9 +245,7 @@ void op_device_free(OpDevice &d) {
   }
   dfree(d.st_seq);
   dfree(d.st_wm);
-  dfree(d.tw.keys);
-  dfree(d.tw.aggs);
-  dfree(d.tw.stamp);
+  dfree(d.tw.rows);
   dfree(d.emit.cnt);
   dfree(d.emit.off);
   dfree(d.emit.partial);
@@ -318,10 +343,9 @@ int fetch_scalars(OpDevice &d, std::string &err) {
 }
 
 int clear_batch_scalars(OpDevice &d, std::string &err) {
-  // err, pairs, late, out_rows, touched (offsets 20..55); wm/epoch/live persist
-  DTRY(hipMemsetAsync((char *)d.sc + offsetof(DevScalars, err), 0,
-                      offsetof(DevScalars, live) - offsetof(DevScalars, err), d.stream));
-  DTRY(hipMemsetAsync((char *)d.sc + offsetof(DevScalars, scratch), 0, 20 * sizeof(uint64_t), d.stream));
+  // err, pairs, late, out_rows, touched, redo, scratch; wm/epoch/live persist
+  launch_clear_scalars(d.stream, d.sc);
+  DTRY(hipGetLastError());
   return HSG_OK;
 }
 
@@ -346,6 +370,10 @@ int finish_batch(OpDevice &d, int64_t wm_in, uint64_t n, PushResult &r, std::str
     fprintf(stderr, "[hsg phases] agg wg=%llu init=%.1fus records=%.1fus flush=%.1fus tail=%.1fus (per-wg avg)\n",
             (unsigned long long)s.scratch[12], s.scratch[8] * 0.01 / s.scratch[12], s.scratch[9] * 0.01 / s.scratch[12],
             s.scratch[10] * 0.01 / s.scratch[12], s.scratch[11] * 0.01 / s.scratch[12]);
+  if (phases && s.scratch[12])
+    fprintf(stderr, "[hsg phases] agg flush: sort=%.1fus runs=%.1fus rounds/wg=%.2f panes=%llu updates=%llu\n",
+            s.scratch[18] * 0.01 / s.scratch[12], s.scratch[19] * 0.01 / s.scratch[12],
+            (double)s.scratch[20] / s.scratch[12], (unsigned long long)s.scratch[0], (unsigned long long)s.scratch[1]);
   if (phases && s.scratch[17])
     fprintf(stderr, "[hsg phases] scatter wg=%llu walk=%.1fus scan=%.1fus place=%.1fus write=%.1fus (per-wg avg)\n",
             (unsigned long long)s.scratch[17], s.scratch[13] * 0.01 / s.scratch[17], s.scratch[14] * 0.01 / s.scratch[17],
@@ -363,12 +391,19 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
                             const Batch &kb, const int64_t *seq, const int64_t *rec_wm, PushResult &r,
                             std::string &err) {
   TwParams p = make_tw_params(cfg, a);
-  int rc = clear_batch_scalars(d, err);
-  if (rc != HSG_OK) return rc;
-  if (kb.n) {
+  // Optimistic partitioned path: assume no record of the batch is late, fold
+  // the stream-time inputs into the histogram pass and decide afterwards (one
+  // tiny kernel); a batch that does have late records is run again with the
+  // per-record stream time. Needs the window epoch (set by an earlier batch).
+  const bool opt = d.use_part && !rec_wm && !has_last(prog) && d.h_sc->epoch_set && cfg.grace_ms >= 0 &&
+                   cfg.window_kind != HSG_SESSION;
+  auto run = [&](bool optimistic) -> int {
+    int rc = clear_batch_scalars(d, err);
+    if (rc != HSG_OK) return rc;
+    if (!kb.n) return HSG_OK;
     // stream time (and the window epoch on the first batch); after a key exchange
     // the per-record stream time arrives in rec_wm and only the epoch is used
-    launch_stream_time(d, cfg, kb, a.wm_in, p.adv);
+    if (!optimistic) launch_stream_time(d, cfg, kb, a.wm_in, p.adv);
     DTRY(hipEventRecord(d.ev_a, d.stream));
     if (d.use_part) {
       PartParams pp;
@@ -379,10 +414,15 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       pp.words = part_words(cfg.n_cols, pp.has_seq);
       pp.tile = part_tile_for(pp.words);
       pp.tiles = part_tiles(kb.n, pp.tile);
-      const uint64_t nh = (1ull << pp.np_log2) * pp.tiles;
-      if (!rec_wm) launch_part_recwm(d.stream, kb, d.tile_prefix, d.sc, d.part.wm);
-      launch_part_hist(d.stream, kb, p, pp, rec_wm, d.part.wm, d.part, d.sc);
-      scan_excl_u32(d.stream, d.part.hist, d.part.off, nh, d.part.partial, d.part.off + nh);
+      pp.pane_S = d.pane_S;
+      { static const char *x = getenv("HSG_EXP"); pp.exp = x ? atoi(x) : 0; }
+      pp.rbits = d.rbits;
+      pp.chunk = kAggChunk;
+      pp.big = d.agg_big ? 1 : 0;
+      if (!rec_wm && !optimistic) launch_part_recwm(d.stream, kb, d.tile_prefix, d.sc, d.part.wm);
+      launch_part_hist(d.stream, kb, p, pp, rec_wm, d.part.wm, d.part, d.sc, optimistic);
+      if (optimistic) launch_part_decide(d.stream, d.sc, a.wm_in, cfg.grace_ms);
+      launch_part_offsets(d.stream, pp, d.part, d.sc);
       launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc);
       launch_part_agg(d.stream, prog, p, pp, d.tw, d.part, kb.n, d.sc);
     } else {
@@ -398,13 +438,21 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
                        (uint64_t *)&d.sc->out_rows);
     }
     DTRY(hipGetLastError());
-  }
+    return HSG_OK;
+  };
+  int rc = run(opt);
+  if (rc != HSG_OK) return rc;
   rc = finish_batch(d, a.wm_in, kb.n, r, err);
+  if (opt && kb.n && d.h_sc->redo) {
+    rc = run(false);
+    if (rc != HSG_OK) return rc;
+    rc = finish_batch(d, a.wm_in, kb.n, r, err);
+  }
   if (kb.n) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, d.ev_a, d.ev_b) == hipSuccess) r.agg_ms = ms;
     r.agg_launches = 1;
-    if (d.use_part) adapt_partitions(d, prog, d.h_sc->scratch[0], kb.n);
+    if (d.use_part) adapt_partitions(d, cfg, prog, d.h_sc->scratch[0], kb.n);
   }
   r.touched = cfg.emit_mode == HSG_EMIT_PER_BATCH ? r.out_rows : d.h_sc->scratch[0];
   return rc;
@@ -444,7 +492,18 @@ int push_local(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const
 int op_copy_rows(OpDevice &d, const OutCols &src, uint64_t from, uint64_t n, int n_aggs, const hsg_rows *out,
                  std::string &err) {
   if (n == 0) return HSG_OK;
-  hipMemcpyKind k = out->mem == HSG_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+  if (out->mem == HSG_MEM_DEVICE) {
+    // device-resident destination: every column in one launch
+    RowPtrs ap;
+    memset(&ap, 0, sizeof(ap));
+    for (int j = 0; j < n_aggs && out->aggs; ++j) ap.p[j] = (int64_t *)out->aggs[j];
+    launch_copy_rows(d.stream, src, from, n, n_aggs, (uint32_t *)out->key_id, out->win_start, out->win_end,
+                     out->src_index, ap);
+    DTRY(hipGetLastError());
+    DTRY(hipStreamSynchronize(d.stream));
+    return HSG_OK;
+  }
+  hipMemcpyKind k = hipMemcpyDeviceToHost;
   if (out->key_id) DTRY(hipMemcpyAsync(out->key_id, src.key + from, n * 4, k, d.stream));
   if (out->win_start) DTRY(hipMemcpyAsync(out->win_start, src.ws + from, n * 8, k, d.stream));
   if (out->win_end) DTRY(hipMemcpyAsync(out->win_end, src.we + from, n * 8, k, d.stream));

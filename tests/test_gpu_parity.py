@@ -128,6 +128,25 @@ def test_configs_reduced(eng, name):
     _drive(eng, spec, batches)
 
 
+@pytest.mark.parametrize("kind,kw", [(abi.HSG_HOPPING, dict(size_ms=60_000, advance_ms=5_000)),
+                                     (abi.HSG_TUMBLING, dict(size_ms=10_000)),
+                                     (abi.HSG_HOPPING, dict(size_ms=50_000, advance_ms=15_000))],
+                         ids=["hop-pane", "tumbling", "hop-fanout"])
+def test_dense_groups_rounds(eng, kind, kw):
+    """More panes per bucket than one LDS table holds: the aggregation's
+    key-hash rounds (sized from the previous batch) and overflow rounds; the
+    fan-out case spills windows straight to the HBM table."""
+    spec = OpSpec(kind, abi.HSG_EMIT_PER_BATCH, col_types=[abi.HSG_I64],
+                  aggs=[(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0)], state_capacity=1_000_000, **kw)
+    batches = []
+    for bi in range(2):
+        key, ts, cols, valid = gen_small(7000 + bi, 1 << 17, 12_000, span=60_000,
+                                         base=50_000_000 + bi * 60_000, very_late=False, none_frac=0.0,
+                                         neg_frac=0.0, absent_frac=0.0)
+        batches.append((key, ts, cols, None))
+    _drive(eng, spec, batches)
+
+
 def test_state_table_full_raises(eng):
     spec = OpSpec(abi.HSG_UNWINDOWED, abi.HSG_EMIT_NONE, aggs=[(abi.HSG_COUNT_ALL, 0)], state_capacity=16)
     g = eng.op(spec)
