@@ -1,0 +1,582 @@
+// The LDS aggregation kernel of the partitioned path (k_part_agg) and its
+// device helpers, included by the per-slot-count instantiation units
+// k_agg_s{2,4,6,8}.hip so the variants compile in parallel. Not ABI.
+#pragma once
+
+#include "hsg_dev.h"
+#include "hsg_part.h"
+#include "hsg_tw.h"
+
+namespace hsg {
+
+// ---------------------------------------------------------------------------
+// LDS aggregation of one chunk
+// ---------------------------------------------------------------------------
+// One partitioned record held in registers: [w0 w1 col 0..C-1 seq+1?]. Runtime
+// word selection is an unrolled compare chain, so the record never leaves VGPRs.
+// One partitioned record held in registers, in its memory layout (PK: packed,
+// see hsg_part.h). Runtime word selection is an unrolled compare chain, so
+// the record never leaves VGPRs.
+template <int WMAX, bool PK>
+struct PRec {
+  static constexpr int CB = PK ? 1 : 2;  // first column word
+  uint64_t w[WMAX];
+  int C;
+  __device__ uint32_t key() const { return (uint32_t)w[0]; }
+  __device__ uint32_t krel(uint32_t kbase) const {
+    return PK ? kbase + (uint32_t)((w[0] >> 32) & 0xFFFFull) : (uint32_t)(w[0] >> 32);
+  }
+  __device__ uint32_t nwin() const { return PK ? (uint32_t)((w[0] >> 48) & 0xFFull) : (uint32_t)w[1]; }
+  __device__ bool present(int c) const { return PK ? (w[0] >> (56 + c)) & 1ull : (w[1] >> (32 + c)) & 1ull; }
+  __device__ int64_t word(int k) const {
+    int64_t v = 0;
+#pragma unroll
+    for (int q = CB; q < WMAX; ++q)
+      if (q == k) v = (int64_t)w[q];
+    return v;
+  }
+  __device__ int64_t col(int c) const { return word(CB + c); }
+  __device__ int64_t seq1() const { return word(CB + C); }
+};
+
+// contribution of the record to slot s (identity when absent)
+template <typename R>
+__device__ inline int64_t prec_elem(const Program &prog, int s, const R &r) {
+  const int op = prog.slot_op[s];
+  const int c = prog.slot_col[s];
+  if (op == S_CNT_ALL) return 1;
+  if (op == S_LAST_VAL) return 0;
+  if (!r.present(c)) return slot_identity_dev(op);
+  switch (op) {
+    case S_CNT: return 1;
+    case S_SUM_I:
+    case S_SUM_F:
+    case S_MIN_I:
+    case S_MAX_I: return r.col(c);
+    case S_MIN_F:
+    case S_MAX_F: return (int64_t)f64_ord(__builtin_bit_cast(double, r.col(c)));
+    case S_LAST_SEQ: return r.seq1();
+    default: return 0;
+  }
+}
+
+template <int MS, typename R>
+__device__ inline void lds_apply(const Program &prog, int64_t *__restrict__ row, const R &r) {
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    if (s >= prog.n_slots) break;
+    const int op = prog.slot_op[s];
+    if (op == S_LAST_VAL) continue;
+    if (op != S_CNT_ALL && !r.present(prog.slot_col[s])) continue;
+    const int64_t x = prec_elem(prog, s, r);
+    unsigned long long *u = (unsigned long long *)(row + s);
+    switch (op) {
+      case S_CNT_ALL:
+      case S_CNT:
+      case S_SUM_I: atomicAdd(u, (unsigned long long)x); break;
+      case S_SUM_F: unsafeAtomicAdd((double *)(row + s), __builtin_bit_cast(double, x)); break;
+      case S_MIN_I: atomicMin((long long *)(row + s), (long long)x); break;
+      case S_MAX_I: atomicMax((long long *)(row + s), (long long)x); break;
+      case S_MIN_F: atomicMin(u, (unsigned long long)x); break;
+      case S_MAX_F:
+      case S_LAST_SEQ: atomicMax(u, (unsigned long long)x); break;
+      default: break;
+    }
+  }
+}
+
+// a <- a (+) x over the aggregate slots (LAST_SEQ = latest sequence)
+template <int MS>
+__device__ inline void acc_combine(const Program &prog, int64_t (&a)[MS], const int64_t *x) {
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    if (s >= prog.n_slots) break;
+    const int op = prog.slot_op[s];
+    if (op == S_LAST_VAL) continue;
+    a[s] = op == S_LAST_SEQ ? ((uint64_t)x[s] > (uint64_t)a[s] ? x[s] : a[s]) : slot_combine(op, a[s], x[s]);
+  }
+}
+
+// HBM-side atomic combine of a row of partial aggregates (v) into `row`.
+template <int MS>
+__device__ inline void flush_row_atomic(const Program &prog, int64_t *__restrict__ row, const int64_t (&v)[MS]) {
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    if (s >= prog.n_slots) break;
+    const int op = prog.slot_op[s];
+    const int64_t x = v[s];
+    if (op == S_LAST_VAL || x == slot_identity_dev(op)) continue;  // nothing to add
+    unsigned long long *u = (unsigned long long *)(row + s);
+    switch (op) {
+      case S_CNT_ALL:
+      case S_CNT:
+      case S_SUM_I: atomicAdd(u, (unsigned long long)x); break;
+      case S_SUM_F: unsafeAtomicAdd((double *)(row + s), __builtin_bit_cast(double, x)); break;
+      case S_MIN_I: atomicMin((long long *)(row + s), (long long)x); break;
+      case S_MAX_I: atomicMax((long long *)(row + s), (long long)x); break;
+      case S_MIN_F: atomicMin(u, (unsigned long long)x); break;
+      case S_MAX_F:
+      case S_LAST_SEQ: atomicMax(u, (unsigned long long)x); break;
+      default: break;
+    }
+  }
+}
+
+// One HBM update of group g with the chunk's partial aggregate v. `exclusive`:
+// this workgroup is the only one updating the group in this launch, so a plain
+// read-modify-write suffices (agent-scope loads, served by L2 not L1: this
+// workgroup's own atomics may have updated the row). Returns the slot when this is the group's first update
+// in the batch (-> per-batch changelog), else kTouchSkip.
+template <int MS>
+__device__ inline uint32_t flush_window(const Program &prog, const TwParams &p, const TwTable &t, uint64_t g,
+                                        const int64_t (&v)[MS], bool exclusive, uint32_t &fresh, uint32_t &err) {
+  const uint32_t f0 = fresh;
+  const int64_t slot = tw_find_or_insert(t, g, fresh);
+  if (slot < 0) {
+    err |= ERR_OOM;
+    return kTouchSkip;
+  }
+  int64_t *row = t.aggs(slot);
+  uint32_t *stp = t.stamp(slot);
+  const uint32_t bid = (uint32_t)p.batch_id;
+  bool first;
+  if (exclusive && fresh != f0) {
+    // inserted just now by the group's only writer: the row holds identities
+#pragma unroll
+    for (int s = 0; s < MS; ++s)
+      if (s < prog.n_slots && prog.slot_op[s] != S_LAST_VAL) row[s] = v[s];
+    *stp = bid;
+    first = true;
+  } else if (exclusive) {
+    int64_t cur[MS];
+#pragma unroll
+    for (int s = 0; s < MS; ++s)
+      cur[s] = s < prog.n_slots ? __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    const uint32_t st = __hip_atomic_load(stp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int s = 0; s < MS; ++s) {
+      if (s >= prog.n_slots) break;
+      const int op = prog.slot_op[s];
+      if (op == S_LAST_VAL || v[s] == slot_identity_dev(op)) continue;
+      row[s] = op == S_LAST_SEQ ? ((uint64_t)v[s] > (uint64_t)cur[s] ? v[s] : cur[s]) : slot_combine(op, cur[s], v[s]);
+    }
+    first = st != bid;
+    if (first) *stp = bid;
+  } else {
+    flush_row_atomic<MS>(prog, row, v);
+    first = atomicExch(stp, bid) != bid;
+  }
+  return first ? (uint32_t)slot : kTouchSkip;
+}
+
+__device__ inline void touch_append(const PartBuffers &pb, DevScalars *sc, uint32_t slot, uint32_t &err) {
+  if (slot == kTouchSkip) return;
+  const uint64_t o = atomicAdd((unsigned long long *)&sc->scratch[1], 1ull);
+  if (o < pb.touched_cap) pb.touched[o] = slot;
+  else err |= ERR_OOM;
+}
+
+// Windows [w0, w1] of one record straight into the HBM table (records whose
+// earliest windows were rejected by grace, and LDS overflow in fan-out mode).
+template <int MS, typename R>
+__device__ inline void direct_windows(const Program &prog, const TwParams &p, const TwTable &t, const PartBuffers &pb,
+                                      DevScalars *sc, uint32_t key, uint32_t w0, uint32_t w1, const R &r,
+                                      uint32_t &fresh, uint32_t &err) {
+  int64_t v[MS];
+#pragma unroll
+  for (int s = 0; s < MS; ++s) v[s] = s < prog.n_slots ? prec_elem(prog, s, r) : 0;
+  for (uint32_t w = w0;; ++w) {
+    touch_append(pb, sc, flush_window<MS>(prog, p, t, ((uint64_t)key << 32) | w, v, false, fresh, err), err);
+    if (w == w1) break;
+  }
+}
+
+// find or insert g; -1 when g is absent and the table is at its fill limit
+template <int E>
+__device__ inline int lds_insert(uint64_t *lkey, uint32_t *lfill, uint32_t limit, uint64_t g) {
+  uint32_t h = (uint32_t)(mix64(g) & (E - 1));
+  for (int probe = 0; probe < E; ++probe) {
+    const uint64_t cur = lkey[h];
+    if (cur == g) return (int)h;
+    if (cur == kEmpty) {
+      if (*(volatile uint32_t *)lfill >= limit) return -1;
+      const uint64_t old = atomicCAS((unsigned long long *)&lkey[h], (unsigned long long)kEmpty, (unsigned long long)g);
+      if (old == kEmpty) {
+        atomicAdd(lfill, 1u);
+        return (int)h;
+      }
+      if (old == g) return (int)h;
+    }
+    h = (h + 1) & (E - 1);
+  }
+  return -1;
+}
+
+// sub-round of a key: the hash bits just below its bucket bits
+__device__ inline uint32_t key_round(uint32_t key, int np_log2, int rbits) {
+  if (!rbits) return 0;
+  const uint64_t h = mix64((uint64_t)key * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull);
+  return (uint32_t)(h >> (64 - np_log2 - rbits)) & ((1u << rbits) - 1u);
+}
+
+// Aggregation of one chunk of a bucket (buckets are disjoint key sets, so when
+// the bucket is one chunk this workgroup owns every group it updates).
+//
+// Pane mode (pp.pane_S = S >= 1, size = S * advance): a record of a full window
+// run only updates its pane (key, last window P) in the LDS table. At a flush
+// the live panes are sorted by (key, pane) in LDS; every pane P owns the
+// windows [a, P] that contain no earlier pane in the table, and window
+// w = combine(panes w .. w+S-1) gets one HBM update, with the panes summed
+// incrementally from the sorted neighbours (w+1 adds the panes up to w+S).
+// Tumbling is S = 1 (no sort). Fan-out mode (S = 0: size not a multiple of
+// advance) keeps one entry per window.
+//
+// The chunk is walked in register-resident sub-chunks of NT * RPT records and
+// the LDS table persists across them: it is flushed when full and at the end
+// of each of the 2^rbits key-hash rounds (host-sized from the previous batch so
+// that a round's panes fit), so a bucket's groups are normally flushed once.
+template <int MS, int E, int NT>
+struct AggLds {
+  uint64_t key[E];
+  int64_t agg[E * MS];
+  uint8_t nw[E];     // windows of the pane's records
+  uint8_t run[E];    // owned windows - 1
+  uint16_t live[E];  // compacted / sorted live entries
+  uint32_t fill, nl, b, c0, c1;
+  uint32_t wsum[NT / 64];
+  uint64_t base;
+  uint64_t red[2][NT / 64];
+};
+
+// Flush every live entry of the table as window updates, then clear it.
+// Block-wide: every thread calls. Returns the number of live entries.
+template <int MS, int E, int NT>
+__device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const Program &prog, const TwParams &p, const TwTable &t,
+                              const PartBuffers &pb, DevScalars *sc, int S, bool exclusive, uint32_t &fresh,
+                              uint32_t &err, uint64_t &t_sort) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t SW = S ? (uint32_t)S : 1u;
+  const uint64_t t0 = wall_clock64();
+  // compact the live entries (one LDS atomic per wave)
+  for (int e0 = 0; e0 < E; e0 += NT) {
+    const int e = e0 + threadIdx.x;
+    const bool on = L.key[e] != kEmpty;
+    const uint64_t m = __ballot(on);
+    uint32_t wb = 0;
+    if (lane == 0 && m) wb = atomicAdd(&L.nl, (uint32_t)__popcll(m));
+    wb = __shfl(wb, 0, 64);
+    if (on) L.live[wb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)e;
+  }
+  __syncthreads();
+  const uint32_t nl = L.nl;
+  if (S > 1 && nl > 1) {
+    // panes of one key become neighbours: bitonic sort of the live list by
+    // (key, pane), padded to a power of two with +inf
+    uint32_t M = 1;
+    while (M < nl) M <<= 1;
+    for (uint32_t q = nl + threadIdx.x; q < M; q += NT) L.live[q] = 0xFFFFu;
+    __syncthreads();
+    for (uint32_t k = 2; k <= M; k <<= 1) {
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        for (uint32_t i = threadIdx.x; i < M; i += NT) {
+          const uint32_t ixj = i ^ j;
+          if (ixj <= i) continue;
+          const uint16_t x = L.live[i], y = L.live[ixj];
+          const uint64_t kx = x == 0xFFFFu ? kEmpty : L.key[x];
+          const uint64_t ky = y == 0xFFFFu ? kEmpty : L.key[y];
+          if ((kx > ky) == ((i & k) == 0)) {
+            L.live[i] = y;
+            L.live[ixj] = x;
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  t_sort += wall_clock64() - t0;
+  // owned window run of every pane: [max(P - n + 1, previous pane + 1), P]
+  uint32_t cnt = 0;
+  for (uint32_t q = threadIdx.x; q < nl; q += NT) {
+    const int e = L.live[q];
+    const uint64_t g = L.key[e];
+    const uint32_t P = (uint32_t)g;
+    uint32_t a = P - (L.nw[e] - 1u);
+    if (S > 1 && q > 0) {
+      const uint64_t gp = L.key[L.live[q - 1]];
+      if ((gp >> 32) == (g >> 32) && (uint32_t)gp + 1u > a) a = (uint32_t)gp + 1u;
+    }
+    L.run[e] = (uint8_t)(P - a);
+    cnt += P - a + 1;
+  }
+  // block exclusive scan of the window counts -> changelog list positions
+  const uint64_t incl = wave_incl_sum((uint64_t)cnt);
+  if (lane == 63) L.wsum[wv] = (uint32_t)incl;
+  __syncthreads();
+  uint64_t o = incl - cnt, total = 0;
+  for (int k = 0; k < NT / 64; ++k) {
+    if (k < wv) o += L.wsum[k];
+    total += L.wsum[k];
+  }
+  if (threadIdx.x == 0) L.base = total ? atomicAdd((unsigned long long *)&sc->scratch[1], (unsigned long long)total) : 0;
+  __syncthreads();
+  o += L.base;
+  for (uint32_t q = threadIdx.x; q < nl; q += NT) {
+    const int e = L.live[q];
+    const uint64_t g = L.key[e];
+    const uint64_t kb = g & 0xFFFFFFFF00000000ull;
+    const uint32_t P = (uint32_t)g;
+    const uint32_t a = P - L.run[e];
+    int64_t acc[MS];
+#pragma unroll
+    for (int s = 0; s < MS; ++s) acc[s] = L.agg[e * MS + s];
+    // later panes of the key (sorted after q) that window w covers: pane <= w + SW - 1
+    uint32_t j = q + 1;
+    uint64_t top = (uint64_t)a + SW - 1;
+    for (uint32_t w = a;; ++w) {
+      while (S > 1 && j < nl) {
+        const int f = L.live[j];
+        const uint64_t gj = L.key[f];
+        if ((gj & 0xFFFFFFFF00000000ull) != kb || (uint64_t)(uint32_t)gj > top) break;
+        acc_combine<MS>(prog, acc, &L.agg[f * MS]);
+        ++j;
+      }
+      const uint32_t sl = flush_window<MS>(prog, p, t, kb | w, acc, exclusive, fresh, err);
+      if (o < pb.touched_cap) pb.touched[o] = sl;
+      else err |= ERR_OOM;
+      ++o;
+      if (w == P) break;
+      ++top;
+    }
+  }
+  __syncthreads();
+  // clear the table
+  for (uint32_t q = threadIdx.x; q < nl; q += NT) {
+    const int e = L.live[q];
+    L.key[e] = kEmpty;
+#pragma unroll
+    for (int s = 0; s < MS; ++s) L.agg[e * MS + s] = s < prog.n_slots ? slot_identity_dev(prog.slot_op[s]) : 0;
+  }
+  if (threadIdx.x == 0) {
+    L.fill = 0;
+    L.nl = 0;
+  }
+  __syncthreads();
+  return nl;
+}
+
+// 4 waves per SIMD: two 512-thread or one 1024-thread workgroup per CU (<= 128 VGPRs)
+template <int MS, int E, int WMAX, int RPT, int NT, bool FAN, bool PK>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_part_agg(Program prog, TwParams p, PartParams pp, TwTable t,
+                                                            PartBuffers pb, DevScalars *sc) {
+  __shared__ AggLds<MS, E, NT> L;
+  if (sc->redo) return;  // uniform: the optimistic pass found late records
+  if ((sc->packed != 0) != PK) return;  // uniform: the other layout's variant runs
+  constexpr int SUB = NT * RPT;
+  const int nb = 1 << pp.np_log2;
+  const uint32_t *chunk_start = pb.chunk_start;
+  const uint64_t t0 = wall_clock64();
+  if (threadIdx.x == 0) {
+    // this workgroup's bucket: chunk_start[b] <= blockIdx.x < chunk_start[b + 1]
+    const uint32_t bk = blockIdx.x < chunk_start[nb] ? pb.chunk_bucket[blockIdx.x] : 0;
+    L.b = bk;
+    L.c0 = chunk_start[bk];
+    L.c1 = chunk_start[bk + 1];
+    L.fill = 0;
+    L.nl = 0;
+  }
+  for (int e = threadIdx.x; e < E; e += NT) {
+    L.key[e] = kEmpty;
+#pragma unroll
+    for (int s = 0; s < MS; ++s) L.agg[e * MS + s] = s < prog.n_slots ? slot_identity_dev(prog.slot_op[s]) : 0;
+  }
+  __syncthreads();
+  if (blockIdx.x >= chunk_start[nb]) return;  // uniform: the grid is an upper bound
+  const uint32_t b = L.b;
+  const uint64_t b0 = pb.bstart[b], b1 = pb.bstart[b + 1];
+  const uint64_t c = blockIdx.x - L.c0;
+  const bool exclusive = (L.c1 - L.c0) == 1;
+  const uint64_t r0 = b0 + c * pp.chunk, r1 = r0 + pp.chunk < b1 ? r0 + pp.chunk : b1;
+  const uint32_t limit = (uint32_t)(E * 3 / 4);
+  const int W = PK ? pp.words - 1 : pp.words;  // words per record in memory
+  const int C = pp.words - 2 - pp.has_seq;
+  const uint32_t kbase = (uint32_t)sc->kbase;
+  const int S = pp.pane_S;
+  const int nrounds = 1 << pp.rbits;
+  const int64_t k_epoch = sc->k_epoch;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t pairs = 0, groups = 0, t_rec = 0, t_flush = 0, t_sort = 0, flushes = 0;
+  uint32_t fresh = 0, err = 0;
+  const uint64_t t1 = wall_clock64();
+
+  for (int round = 0; round < nrounds; ++round) {
+    for (uint64_t s0 = r0; s0 < r1; s0 += SUB) {
+      uint64_t ta = wall_clock64();
+      PRec<WMAX, PK> rr[RPT];
+      auto load = [&]() {
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) {
+          const uint64_t i = s0 + (uint64_t)u * NT + threadIdx.x;
+          const bool in = i < r1;
+          rr[u].C = C;
+#pragma unroll
+          for (int q = 0; q < WMAX; ++q) rr[u].w[q] = (in && q < W) ? pb.rec[i * W + q] : 0;
+        }
+      };
+      load();
+      uint32_t pend = 0;
+#pragma unroll
+      for (int u = 0; u < RPT; ++u) {
+        const uint64_t i = s0 + (uint64_t)u * NT + threadIdx.x;
+        if (i < r1 && (nrounds == 1 || key_round(rr[u].key(), pp.np_log2, pp.rbits) == (uint32_t)round))
+          pend |= 1u << u;
+      }
+      uint32_t dpend = 0;  // records for the direct HBM path
+      for (;;) {
+        // one instance of the record body (a rolled loop over a rotating register
+        // queue, back in order after RPT steps): unrolling it overflowed the
+        // instruction cache
+#pragma unroll 1
+        for (int u = 0; u < RPT; ++u) {
+          const PRec<WMAX, PK> r = rr[0];
+#pragma unroll
+          for (int k = 0; k + 1 < RPT; ++k) rr[k] = rr[k + 1];
+          rr[RPT - 1] = r;
+          if (!((pend >> u) & 1u)) continue;
+          const uint32_t key = r.key(), krel = r.krel(kbase), nw = r.nwin();
+          if (FAN) {
+            // fan-out: one entry per window, overflow straight to HBM
+            pairs += nw;
+            for (uint32_t j = 0; j < nw; ++j) {
+              const uint64_t g = ((uint64_t)key << 32) | (uint64_t)(krel + j);
+              const int e = lds_insert<E>(L.key, &L.fill, limit, g);
+              if (e >= 0) {
+                lds_apply<MS>(prog, &L.agg[e * MS], r);
+                L.nw[e] = 1;
+              } else {
+                direct_windows<MS>(prog, p, t, pb, sc, key, krel + j, krel + j, r, fresh, err);
+              }
+            }
+            pend &= ~(1u << u);
+            continue;
+          }
+          if (nw == 0) {  // never written by the scatter (cannot happen; keep loops bounded)
+            pend &= ~(1u << u);
+            continue;
+          }
+          const uint32_t P = krel + nw - 1;
+          const int64_t pabs = (int64_t)P + k_epoch;
+          const uint32_t full = pabs + 1 < (int64_t)S ? (uint32_t)(pabs + 1) : (uint32_t)S;
+          if (nw != full) {
+            // some earliest windows were rejected by grace: not a whole pane;
+            // straight to HBM after this loop
+            dpend |= 1u << u;
+            pend &= ~(1u << u);
+            continue;
+          }
+          if (pp.exp == 2) { pairs += nw; pend &= ~(1u << u); continue; }
+          const int e = lds_insert<E>(L.key, &L.fill, limit, ((uint64_t)key << 32) | P);
+          if (e < 0) continue;  // table full: after the next flush
+          pairs += nw;
+          if (pp.exp != 1) lds_apply<MS>(prog, &L.agg[e * MS], r);
+          L.nw[e] = (uint8_t)nw;
+          pend &= ~(1u << u);
+        }
+        const bool more = __syncthreads_or(pend != 0);
+        const uint64_t tb = wall_clock64();
+        t_rec += tb - ta;
+        if (!more) break;
+        // table full with records left: flush and go on (the records are
+        // loaded again afterwards, so they hold no registers across the flush)
+        groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, fresh, err, t_sort);
+        ++flushes;
+        load();
+        ta = wall_clock64();
+        t_flush += ta - tb;
+      }
+      if (!FAN && __syncthreads_or(dpend != 0)) {
+        load();
+#pragma unroll 1
+        for (int u = 0; u < RPT; ++u) {
+          const PRec<WMAX, PK> r = rr[0];
+#pragma unroll
+          for (int k = 0; k + 1 < RPT; ++k) rr[k] = rr[k + 1];
+          rr[RPT - 1] = r;
+          if (!((dpend >> u) & 1u)) continue;
+          const uint32_t key = r.key(), krel = r.krel(kbase), nw = r.nwin();
+          pairs += nw;
+          direct_windows<MS>(prog, p, t, pb, sc, key, krel, krel + nw - 1, r, fresh, err);
+        }
+      }
+    }
+    const uint64_t tb = wall_clock64();
+    groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, fresh, err, t_sort);
+    ++flushes;
+    t_flush += wall_clock64() - tb;
+  }
+  const uint64_t t3 = wall_clock64();
+  pairs = wave_sum_u64(pairs);
+  const uint64_t fr = wave_sum_u64(fresh);
+  if (lane == 0) {
+    L.red[0][wv] = pairs;
+    L.red[1][wv] = fr;
+  }
+  if (err) atomicOr(&sc->err, err);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t a = 0, f = 0;
+    for (int k = 0; k < NT / 64; ++k) {
+      a += L.red[0][k];
+      f += L.red[1][k];
+    }
+    if (a) atomicAdd((unsigned long long *)&sc->pairs, (unsigned long long)a);
+    if (f) atomicAdd((unsigned long long *)&sc->live, (unsigned long long)f);
+    if (groups) atomicAdd((unsigned long long *)&sc->scratch[0], (unsigned long long)groups);
+    // phase clock (100 MHz wall clock) sums: init, records, flush, tail, workgroups
+    const uint64_t t4 = wall_clock64();
+    atomicAdd((unsigned long long *)&sc->scratch[8], (unsigned long long)(t1 - t0));
+    atomicAdd((unsigned long long *)&sc->scratch[9], (unsigned long long)t_rec);
+    atomicAdd((unsigned long long *)&sc->scratch[10], (unsigned long long)t_flush);
+    atomicAdd((unsigned long long *)&sc->scratch[11], (unsigned long long)(t4 - t3));
+    atomicAdd((unsigned long long *)&sc->scratch[12], 1ull);
+    atomicAdd((unsigned long long *)&sc->scratch[18], (unsigned long long)t_sort);
+    atomicAdd((unsigned long long *)&sc->scratch[19], 0ull);
+    atomicAdd((unsigned long long *)&sc->scratch[20], (unsigned long long)flushes);
+  }
+}
+
+// Aggregation variants: small = E_s entries and 512 threads (two workgroups per
+// CU), big = E_l entries and 1024 threads (one per CU). Records per thread
+// keep the record queue within 128 VGPRs.
+template <int MS, int E, int NT, int WM, int RPT, bool FAN>
+static void agg_launch_pk(hipStream_t s, dim3 g, bool maybe_packed, const Program &prog, const TwParams &p,
+                          const PartParams &pp, const TwTable &t, const PartBuffers &pb, DevScalars *sc) {
+  const dim3 th(NT);
+  hipLaunchKernelGGL((k_part_agg<MS, E, WM, RPT, NT, FAN, false>), g, th, 0, s, prog, p, pp, t, pb, sc);
+  if (maybe_packed)  // the layout is decided on the device: the variant not chosen exits at once
+    hipLaunchKernelGGL((k_part_agg<MS, E, WM - 1, RPT, NT, FAN, true>), g, th, 0, s, prog, p, pp, t, pb, sc);
+}
+
+template <int MS, int E, int NT, int RPT4>
+static void agg_launch_v(hipStream_t s, dim3 g, int W, bool mp, const Program &prog, const TwParams &p,
+                         const PartParams &pp, const TwTable &t, const PartBuffers &pb, DevScalars *sc) {
+  constexpr int R6 = RPT4 / 2 > 0 ? RPT4 / 2 : 1, R11 = RPT4 / 4 > 0 ? RPT4 / 4 : 1;
+  if (pp.pane_S == 0) {
+    // fan-out (size not a multiple of advance): one generic-width variant
+    agg_launch_pk<MS, E, NT, kPartMaxWords, R11, true>(s, g, mp, prog, p, pp, t, pb, sc);
+    return;
+  }
+  if (W <= 3) agg_launch_pk<MS, E, NT, 3, RPT4, false>(s, g, mp, prog, p, pp, t, pb, sc);
+  else if (W <= 4) agg_launch_pk<MS, E, NT, 4, RPT4, false>(s, g, mp, prog, p, pp, t, pb, sc);
+  else if (W <= 6) agg_launch_pk<MS, E, NT, 6, R6, false>(s, g, mp, prog, p, pp, t, pb, sc);
+  else agg_launch_pk<MS, E, NT, kPartMaxWords, R11, false>(s, g, mp, prog, p, pp, t, pb, sc);
+}
+
+template <int MS>
+static void agg_launch(hipStream_t s, dim3 g, int W, bool mp, const Program &prog, const TwParams &p,
+                       const PartParams &pp, const TwTable &t, const PartBuffers &pb, DevScalars *sc) {
+  constexpr int ES = MS <= 2 ? 2048 : 1024, EL = MS <= 2 ? 4096 : 2048;
+  if (pp.big) agg_launch_v<MS, EL, 1024, 8>(s, g, W, mp, prog, p, pp, t, pb, sc);
+  else agg_launch_v<MS, ES, 512, 4>(s, g, W, mp, prog, p, pp, t, pb, sc);
+}
+
+}  // namespace hsg

@@ -81,7 +81,7 @@ inline Divider make_divider(uint64_t d) {
   return v;
 }
 
-// Device-side per-op scalars (one 256-byte block, zeroed / set per batch).
+// Device-side per-op scalars (one 512-byte block, zeroed / set per batch).
 struct DevScalars {
   int64_t wm_out;        // watermark after the batch
   int64_t k_epoch;       // window index represented by k_rel = 0
@@ -94,9 +94,12 @@ struct DevScalars {
   uint64_t live;         // dump: rows found
   uint32_t no_late;      // this batch: no (record, window) can fail the grace check
   uint32_t redo;         // optimistic partition path: the batch has late records, run it again carefully
-  uint64_t scratch[23];  // [0] groups flushed (partition path), [1] touched-list length
+  uint64_t packed;       // partition path, this batch: records in the packed layout (hsg_part.h)
+  uint64_t kbase;        // packed layout: window (relative to the epoch) the 16-bit window offsets count from
+  uint64_t scratch[53];  // [0] groups flushed (partition path), [1] touched-list length, [8..20] phase clocks,
+                         // [21..22] optimistic pass ts extrema
 };
-static_assert(sizeof(DevScalars) == 256, "DevScalars layout");
+static_assert(sizeof(DevScalars) == 512, "DevScalars layout");
 
 constexpr uint32_t ERR_OOM = 1u;
 constexpr uint32_t ERR_RANGE = 2u;

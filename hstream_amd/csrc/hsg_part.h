@@ -11,10 +11,14 @@ constexpr int kPartThreads = 256;
 constexpr int kPartMaxLog2 = 11;                      // up to 2048 partitions
 constexpr int kPartMaxWords = 11;                     // 2 + 8 columns + seq
 constexpr uint64_t kTouchChunk = 4096;                // touched-list entries per emit workgroup
+constexpr uint32_t kTouchSkip = 0xFFFFFFFFu;           // touched-list entry of a later update of a group
 
-// A partitioned record is `words` 8-byte words:
+// A partitioned record is `words` 8-byte words (wide layout):
 //   [key | krel << 32] [nwin | valid bits << 32] [col 0 .. C-1] [seq + 1]?
 // krel = first accepted window relative to the epoch, nwin = accepted windows.
+// Packed layout (optimistic batches whose windows span < 2^16 advances, C <= 8,
+// nwin < 256): words - 1 words, the first one
+//   [key | (krel - kbase) << 32 | nwin << 48 | valid bits << 56]
 struct PartBuffers {
   uint32_t *hist;         // [tiles][np] tile-major per-tile bucket counts
   uint32_t *offt;         // [tiles][np] tile-major bucket-major-order offsets of each (tile, bucket) run
@@ -61,7 +65,8 @@ void launch_part_recwm(hipStream_t s, const Batch &b, const int64_t *tprefix, co
 // extrema for launch_part_decide)
 void launch_part_hist(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp, const int64_t *rec_wm,
                       const int64_t *own_wm, const PartBuffers &pb, DevScalars *sc, bool opt);
-void launch_part_decide(hipStream_t s, DevScalars *sc, int64_t wm_in, int64_t grace);
+void launch_part_decide(hipStream_t s, DevScalars *sc, const TwParams &p, int64_t wm_in, int64_t grace,
+                        bool can_pack);
 // bucket-major run offsets (offt, bstart) from the tile-major histogram
 void launch_part_offsets(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc);
 uint32_t part_nseg(uint64_t tiles);
@@ -69,8 +74,9 @@ void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const
                          const int64_t *rec_wm, const int64_t *own_wm, const int64_t *seq, const PartBuffers &pb,
                          DevScalars *sc);
 // returns false when the op's slot count has no LDS variant (caller falls back)
+// maybe_packed: the batch may be in the packed layout (launch both variants)
 bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, const PartParams &pp, const TwTable &t,
-                     const PartBuffers &pb, uint64_t n, DevScalars *sc);
+                     const PartBuffers &pb, uint64_t n, DevScalars *sc, bool maybe_packed);
 bool part_supported(const Program &prog);
 // per-batch changelog rows of the groups in pb.touched
 void launch_part_emit(hipStream_t s, const TwTable &t, const Program &prog, const TwParams &p, const PartBuffers &pb,

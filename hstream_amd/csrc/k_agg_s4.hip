@@ -1,0 +1,11 @@
+// k_part_agg instantiations for ops with <= 4 state slots (see hsg_agg.h).
+#include "hsg_agg.h"
+
+namespace hsg {
+
+void agg_launch_ms4(hipStream_t s, dim3 g, int W, bool maybe_packed, const Program &prog, const TwParams &p,
+                    const PartParams &pp, const TwTable &t, const PartBuffers &pb, DevScalars *sc) {
+  agg_launch<4>(s, g, W, maybe_packed, prog, p, pp, t, pb, sc);
+}
+
+}  // namespace hsg

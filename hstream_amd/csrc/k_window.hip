@@ -56,8 +56,10 @@ __global__ void k_clear_scalars(DevScalars *sc) {
     sc->out_rows = 0;
     sc->touched = 0;
     sc->redo = 0;
+    sc->packed = 0;
+    sc->kbase = 0;
   }
-  if (t < 23) sc->scratch[t] = 0;
+  if (t < 53) sc->scratch[t] = 0;
 }
 void launch_clear_scalars(hipStream_t s, DevScalars *sc) { hipLaunchKernelGGL(k_clear_scalars, dim3(1), dim3(64), 0, s, sc); }
 

@@ -375,7 +375,7 @@ int finish_batch(OpDevice &d, int64_t wm_in, uint64_t n, PushResult &r, std::str
             s.scratch[18] * 0.01 / s.scratch[12], s.scratch[19] * 0.01 / s.scratch[12],
             (double)s.scratch[20] / s.scratch[12], (unsigned long long)s.scratch[0], (unsigned long long)s.scratch[1]);
   if (phases && s.scratch[17])
-    fprintf(stderr, "[hsg phases] scatter wg=%llu walk=%.1fus scan=%.1fus place=%.1fus write=%.1fus (per-wg avg)\n",
+    fprintf(stderr, "[hsg phases] scatter wg=%llu walk=%.1fus -=%.1fus -=%.1fus write=%.1fus (per-wg avg)\n",
             (unsigned long long)s.scratch[17], s.scratch[13] * 0.01 / s.scratch[17], s.scratch[14] * 0.01 / s.scratch[17],
             s.scratch[15] * 0.01 / s.scratch[17], s.scratch[16] * 0.01 / s.scratch[17]);
   r.wm_out = n ? s.wm_out : wm_in;
@@ -421,10 +421,12 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       pp.big = d.agg_big ? 1 : 0;
       if (!rec_wm && !optimistic) launch_part_recwm(d.stream, kb, d.tile_prefix, d.sc, d.part.wm);
       launch_part_hist(d.stream, kb, p, pp, rec_wm, d.part.wm, d.part, d.sc, optimistic);
-      if (optimistic) launch_part_decide(d.stream, d.sc, a.wm_in, cfg.grace_ms);
+      static const bool nopack = getenv("HSG_NOPACK") != nullptr;  // timing studies
+      const bool can_pack = optimistic && !nopack && cfg.n_cols <= 8 && d.wpr < 256;
+      if (optimistic) launch_part_decide(d.stream, d.sc, p, a.wm_in, cfg.grace_ms, can_pack);
       launch_part_offsets(d.stream, pp, d.part, d.sc);
       launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc);
-      launch_part_agg(d.stream, prog, p, pp, d.tw, d.part, kb.n, d.sc);
+      launch_part_agg(d.stream, prog, p, pp, d.tw, d.part, kb.n, d.sc, can_pack);
     } else {
       launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, false);
     }
