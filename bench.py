@@ -36,6 +36,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget (0 = skip)")
     p.add_argument("--traffic-csv", default="", help="rocprofv3 --pmc counter CSV to fill roofline.traffic")
     p.add_argument("--force-exchange", action="store_true", help="N=1 through the RCCL exchange path")
+    p.add_argument("--copy-drain", action="store_true", help="drain by copy instead of the registered changelog")
     return p.parse_args()
 
 
@@ -105,7 +106,7 @@ def main():
         "src_index": torch.empty(out_cap, dtype=torch.int64, device=dev),
         "aggs": [torch.empty(out_cap, dtype=torch.float64 if f else torch.int64, device=dev) for f in f64],
     }
-    drain_dev = make_device_drain(op, outs, out_cap)
+    drain_dev = make_device_drain(op, outs, out_cap, zero_copy=not args.copy_drain)
 
     def step():
         op.reset()
@@ -224,7 +225,10 @@ def eng_out_capacity(op):
         -(-spec.size_ms // spec.advance_ms) if spec.window_kind == abi.HSG_HOPPING else 1)
 
 
-def make_device_drain(op, outs, cap):
+def make_device_drain(op, outs, cap, zero_copy=True):
+    """Drain each batch's changelog into HBM-resident columns: registered with
+    hsg_op_set_changelog (rows written in place, drain = count) or, with
+    --copy-drain, copied by hsg_drain from the op's own buffer."""
     import ctypes as C
     from hstream_amd import abi
     agg_ptrs = (C.c_void_p * max(1, len(outs["aggs"])))(*[t.data_ptr() for t in outs["aggs"]])
@@ -233,6 +237,17 @@ def make_device_drain(op, outs, cap):
                         win_end=outs["win_end"].data_ptr(), src_index=outs["src_index"].data_ptr(),
                         aggs=C.cast(agg_ptrs, C.POINTER(C.c_void_p)))
     got = C.c_uint64(0)
+    if zero_copy:
+        op.set_changelog(rows)
+
+        def drain_in_place():
+            rc = op._lib.hsg_drain(op._h, None, C.byref(got))
+            if rc != abi.HSG_OK:
+                raise abi.HStreamGpuError(rc, "hsg_drain")
+            return got.value
+
+        drain_in_place.keep = (agg_ptrs, rows, outs)
+        return drain_in_place
 
     def drain():
         rc = op._lib.hsg_drain(op._h, C.byref(rows), C.byref(got))

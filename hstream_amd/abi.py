@@ -149,6 +149,7 @@ EXPORTED_SYMBOLS = [
     "hsg_push_batch",
     "hsg_pending_rows",
     "hsg_drain",
+    "hsg_op_set_changelog",
     "hsg_state_rows",
     "hsg_dump_state",
     "hsg_op_stats",

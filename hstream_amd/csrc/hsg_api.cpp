@@ -365,16 +365,54 @@ static int check_rows(hsg_op *op, const hsg_rows *out) {
   return HSG_OK;
 }
 
+extern "C" int hsg_op_set_changelog(hsg_op *op, const hsg_rows *dst) {
+  try {
+    if (!op) return HSG_E_INVALID;
+    if (op->pending) return fail(op->err, HSG_E_INVALID, "set_changelog: drain the pending rows first");
+    OpDevice &d = op->dev;
+    if (!dst) {
+      d.out = d.own_out;
+      d.out_cap = d.own_out_cap;
+      d.ext_out = false;
+      return HSG_OK;
+    }
+    int rc = check_rows(op, dst);
+    if (rc != HSG_OK) return rc;
+    if (dst->mem != HSG_MEM_DEVICE) return fail(op->err, HSG_E_INVALID, "set_changelog: device columns only");
+    if (!dst->key_id || !dst->win_start || !dst->win_end || !dst->src_index || dst->capacity == 0 ||
+        (op->cfg.n_aggs && !dst->aggs))
+      return fail(op->err, HSG_E_INVALID, "set_changelog: every column is required");
+    OutCols o;
+    memset(&o, 0, sizeof(o));
+    o.key = dst->key_id;
+    o.ws = dst->win_start;
+    o.we = dst->win_end;
+    o.src = dst->src_index;
+    for (int j = 0; j < op->cfg.n_aggs; ++j) {
+      if (!dst->aggs[j]) return fail(op->err, HSG_E_INVALID, "set_changelog: every column is required");
+      o.agg[j] = (int64_t *)dst->aggs[j];
+    }
+    d.out = o;
+    d.out_cap = dst->capacity;
+    d.ext_out = true;
+    return HSG_OK;
+  } catch (...) {
+    return HSG_E_DEVICE;
+  }
+}
+
 extern "C" int hsg_drain(hsg_op *op, hsg_rows *out, uint64_t *n_out) {
   try {
     if (!op || !n_out) return HSG_E_INVALID;
-    int rc = check_rows(op, out);
+    int rc = op->dev.ext_out && !out ? HSG_OK : check_rows(op, out);
     if (rc != HSG_OK) return rc;
     *n_out = op->pending;
-    if (out->capacity < op->pending) return fail(op->err, HSG_E_CAPACITY, "drain: rows capacity < pending rows");
-    HIP_TRY(op, hipSetDevice(op->eng->device));
-    rc = op_copy_rows(op->dev, op->dev.out, 0, op->pending, op->cfg.n_aggs, out, op->err);
-    if (rc != HSG_OK) return rc;
+    if (!op->dev.ext_out) {
+      if (out->capacity < op->pending) return fail(op->err, HSG_E_CAPACITY, "drain: rows capacity < pending rows");
+      HIP_TRY(op, hipSetDevice(op->eng->device));
+      rc = op_copy_rows(op->dev, op->dev.out, 0, op->pending, op->cfg.n_aggs, out, op->err);
+      if (rc != HSG_OK) return rc;
+    }
     op->pending = 0;
     op->stats.pending_rows = 0;
     return HSG_OK;

@@ -37,6 +37,7 @@ struct OpDevice {
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr, ev_d = nullptr;
   DevScalars *sc = nullptr;     // device
   DevScalars *h_sc = nullptr;   // pinned host mirror
+  bool sc_clean = false;        // per-batch scalars already cleared on the stream
   uint64_t batch_cap = 0;       // records this op can take in one push (after exchange)
   uint64_t wpr = 1;             // max windows per record
   uint64_t n_tiles_cap = 0;
@@ -63,9 +64,13 @@ struct OpDevice {
   // sessions
   SessTable ss = {};
   uint64_t *arena_top = nullptr;  // device bump pointer
-  // changelog buffer
+  // changelog buffer: the op's own, or caller-owned device columns
+  // registered with hsg_op_set_changelog (rows land there directly)
   OutCols out = {};
   uint64_t out_cap = 0;
+  OutCols own_out = {};
+  uint64_t own_out_cap = 0;
+  bool ext_out = false;
   // per-record / session scratch (sort + scan)
   PrBuffers pr = {};
   void *scratch = nullptr;

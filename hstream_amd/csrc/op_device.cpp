@@ -139,6 +139,7 @@ static void adapt_partitions(OpDevice &d, const hsg_op_config &cfg, const Progra
 int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err) {
   DTRY(hipMemsetAsync(d.sc, 0, sizeof(DevScalars), d.stream));
   memset(d.h_sc, 0, sizeof(DevScalars));  // host mirror (epoch_set gates the optimistic path)
+  d.sc_clean = false;
   if (cfg.window_kind == HSG_SESSION) {
     launch_ss_reset(d.stream, d.ss, d.cap);
     DTRY(hipMemsetAsync(d.arena_top, 0, sizeof(uint64_t), d.stream));
@@ -205,6 +206,8 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
   }
   d.out_cap = oc;
   int rc = alloc_out(d.out, d.out_cap, cfg.n_aggs, err);
+  d.own_out = d.out;
+  d.own_out_cap = d.out_cap;
   if (rc != HSG_OK) return rc;
   if (cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.window_kind == HSG_SESSION) {
     rc = perrecord_device_init(d, cfg, prog, err);
@@ -258,7 +261,8 @@ void op_device_free(OpDevice &d) {
   dfree(d.ss.a_stamp);
   dfree(d.ss.a_aggs);
   dfree(d.arena_top);
-  free_out(d.out);
+  free_out(d.own_out);
+  d.out = d.own_out;
   if (d.scratch) hipFree(d.scratch);
   d.scratch = nullptr;
   if (d.part_mem) hipFree(d.part_mem);
@@ -335,15 +339,24 @@ void launch_stream_time(OpDevice &d, const hsg_op_config &cfg, const Batch &kb, 
                    tw ? (cfg.grace_ms >= 0 ? cfg.grace_ms : 0) : -1);
 }
 
+// Copies the scalars to the host mirror, then (same stream, before the host
+// waits) clears the per-batch ones for the next batch, so a push does not
+// start with a dependent launch.
 int fetch_scalars(OpDevice &d, std::string &err) {
   DTRY(hipMemcpyAsync(d.h_sc, d.sc, sizeof(DevScalars), hipMemcpyDeviceToHost, d.stream));
+  launch_clear_scalars(d.stream, d.sc);
   DTRY(hipStreamSynchronize(d.stream));
   DTRY(hipGetLastError());
+  d.sc_clean = true;
   return HSG_OK;
 }
 
 int clear_batch_scalars(OpDevice &d, std::string &err) {
   // err, pairs, late, out_rows, touched, redo, scratch; wm/epoch/live persist
+  if (d.sc_clean) {
+    d.sc_clean = false;
+    return HSG_OK;
+  }
   launch_clear_scalars(d.stream, d.sc);
   DTRY(hipGetLastError());
   return HSG_OK;

@@ -38,6 +38,8 @@ def load_library(path=LIB_PATH):
     L.hsg_op_create.restype = C.c_int
     L.hsg_op_stats.argtypes = [vp, P(abi.hsg_stats)]
     L.hsg_op_stats.restype = C.c_int
+    L.hsg_op_set_changelog.argtypes = [vp, P(abi.hsg_rows)]
+    L.hsg_op_set_changelog.restype = C.c_int
     declare_op_functions(L, "hsg")
     _lib = L
     return L
@@ -101,6 +103,21 @@ class GpuOp(OpHandle):
             raise abi.HStreamGpuError(rc, f"hsg_op_create: {msg.decode() if msg else ''}")
         self.engine = engine  # keep the engine alive while the op lives
         super().__init__(engine._lib, "hsg", h, spec)
+
+    def set_changelog(self, rows):
+        """Register caller-owned device columns (an abi.hsg_rows with mem =
+        HSG_MEM_DEVICE) as the changelog: pushes write rows there directly and
+        drain_count() reports how many (hsg_op_set_changelog). None restores
+        the op's own buffer."""
+        self._check(self._lib.hsg_op_set_changelog(self._h, C.byref(rows) if rows is not None else None),
+                    "op_set_changelog")
+        self._sink = rows
+
+    def drain_count(self) -> int:
+        """hsg_drain with a registered changelog: the rows are already in place."""
+        got = C.c_uint64(0)
+        self._check(self._lib.hsg_drain(self._h, None, C.byref(got)), "drain")
+        return got.value
 
     def stats(self) -> dict:
         s = abi.hsg_stats()

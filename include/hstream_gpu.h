@@ -198,6 +198,15 @@ int  hsg_pending_rows(const hsg_op *op, uint64_t *n);
  * pending and returns HSG_E_CAPACITY. */
 int  hsg_drain(hsg_op *op, hsg_rows *out, uint64_t *n_out);
 
+/* Zero-copy changelog: register caller-owned DEVICE columns (every column,
+ * capacity rows) that pushes then write their changelog rows into directly, at
+ * the pending offset; hsg_drain only reports and resets the pending count
+ * (rows are at [0, n) of the registered columns; `out` may be NULL). NULL
+ * restores the op's own buffer. Pending rows must be drained first. No
+ * counterpart in the reference, whose forward hands rows to the sink one by
+ * one (Processor.hs:221-266); here it saves a device copy per drain. */
+int  hsg_op_set_changelog(hsg_op *op, const hsg_rows *dst);
+
 int  hsg_state_rows(hsg_op *op, uint64_t *n);
 /* Copy every live state row (views). Same capacity rule as hsg_drain. */
 int  hsg_dump_state(hsg_op *op, hsg_rows *out, uint64_t *n_out);

@@ -6,7 +6,7 @@ import pytest
 
 import pyoracle
 from hstream_amd import abi, datagen
-from hstream_amd.columnar import OpSpec
+from hstream_amd.columnar import OpSpec, Rows
 from util import ALL_AGG_SETS, gen_small, load_kat, rows_equal, run_kat_case
 
 pytestmark = pytest.mark.gpu
@@ -145,6 +145,40 @@ def test_dense_groups_rounds(eng, kind, kw):
                                          neg_frac=0.0, absent_frac=0.0)
         batches.append((key, ts, cols, None))
     _drive(eng, spec, batches)
+
+
+def test_registered_changelog_zero_copy(eng):
+    """hsg_op_set_changelog: rows land in caller-owned device columns; drain only counts."""
+    import ctypes as C
+    import torch
+    spec = OpSpec(abi.HSG_HOPPING, abi.HSG_EMIT_PER_BATCH, size_ms=60_000, advance_ms=5_000,
+                  col_types=[abi.HSG_I64], aggs=datagen.C_AGGS_FULL)
+    g, o = _pair(eng, spec)
+    cap = 1 << 20
+    cols = {k: torch.empty(cap, dtype=t, device="cuda") for k, t in
+            (("key", torch.int32), ("ws", torch.int64), ("we", torch.int64), ("src", torch.int64))}
+    f64 = spec.agg_is_f64()
+    aggs = [torch.empty(cap, dtype=torch.float64 if f else torch.int64, device="cuda") for f in f64]
+    ap = (C.c_void_p * len(aggs))(*[a.data_ptr() for a in aggs])
+    rows = abi.hsg_rows(capacity=cap, mem=abi.HSG_MEM_DEVICE, n_aggs=len(aggs), key_id=cols["key"].data_ptr(),
+                        win_start=cols["ws"].data_ptr(), win_end=cols["we"].data_ptr(),
+                        src_index=cols["src"].data_ptr(), aggs=C.cast(ap, C.POINTER(C.c_void_p)))
+    g.set_changelog(rows)
+    wg = wo = -1
+    for bi in range(3):
+        key, ts, cv, valid = gen_small(300 + bi, 20_000, 500, span=120_000, base=9_000_000 + bi * 120_000)
+        wg = g.push(key, ts, cv, valid, watermark=wg)
+        wo = o.push(key, ts, cv, valid, watermark=wo)
+        assert wg == wo
+        n = g.drain_count()
+        torch.cuda.synchronize()
+        got = Rows(cols["key"][:n].cpu().numpy().view(np.uint32), cols["ws"][:n].cpu().numpy(),
+                   cols["we"][:n].cpu().numpy(), cols["src"][:n].cpu().numpy(), [a[:n].cpu().numpy() for a in aggs])
+        rows_equal(got, o.drain(), f64, what=f"zero-copy changelog batch {bi}")
+    g.set_changelog(None)
+    key, ts, cv, valid = gen_small(399, 5000, 500, span=60_000, base=9_400_000)
+    assert g.push(key, ts, cv, valid, watermark=wg) == o.push(key, ts, cv, valid, watermark=wo)
+    rows_equal(g.drain(), o.drain(), f64, what="own buffer again")
 
 
 def test_state_table_full_raises(eng):
