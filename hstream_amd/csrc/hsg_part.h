@@ -70,9 +70,10 @@ void launch_part_decide(hipStream_t s, DevScalars *sc, const TwParams &p, int64_
 // bucket-major run offsets (offt, bstart) from the tile-major histogram
 void launch_part_offsets(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc);
 uint32_t part_nseg(uint64_t tiles);
+// maybe_packed: the batch may be in the packed layout (staged variant too)
 void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp,
                          const int64_t *rec_wm, const int64_t *own_wm, const int64_t *seq, const PartBuffers &pb,
-                         DevScalars *sc);
+                         DevScalars *sc, bool maybe_packed);
 // returns false when the op's slot count has no LDS variant (caller falls back)
 // maybe_packed: the batch may be in the packed layout (launch both variants)
 bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, const PartParams &pp, const TwTable &t,

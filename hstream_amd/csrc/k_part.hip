@@ -221,7 +221,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
                                                        const int64_t *__restrict__ rec_wm,
                                                        const int64_t *__restrict__ own_wm,
                                                        const int64_t *__restrict__ seq, PartBuffers pb,
-                                                       DevScalars *sc) {
+                                                       DevScalars *sc, int staged) {
   __shared__ uint16_t lbk[T];
   __shared__ uint16_t sidx[T];
   __shared__ uint64_t lkn[T];  // krel | nwin << 32
@@ -230,6 +230,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
   __shared__ uint32_t goff[1 << kPartMaxLog2];
   __shared__ uint32_t swave[kPNT / 64];
   if (sc->redo) return;  // uniform: the optimistic pass found late records
+  if (staged && sc->packed) return;  // uniform: k_part_scatter_st wrote this batch
   const int nb = 1 << pp.np_log2;
   const int C = pp.words - 2 - pp.has_seq;
   const bool packed = sc->packed != 0;
@@ -374,12 +375,131 @@ void launch_part_decide(hipStream_t s, DevScalars *sc, const TwParams &p, int64_
   hipLaunchKernelGGL(k_part_decide, dim3(1), dim3(64), 0, s, sc, p, wm_in, grace, can_pack ? 1 : 0);
 }
 
+// Staged scatter for packed records of <= 2 words (<= 1 column, no LAST): the
+// walk reads every input column once, in arrival order; each record's packed
+// words go to its bucket-sorted slot of an LDS copy of the tile, written out
+// with consecutive lanes on consecutive records of a run (16-byte stores).
+// The gather scatter above re-read ~0.35 GB per 2^24-record batch from L2
+// misses (PMC) and waited on them. LDS: the tile (T x W words), two u16
+// counters per u32, u16 run starts: 72 KiB at W = 2, two workgroups per CU.
+// The bucket of a staged record is recomputed from its key at write-out.
+template <int T, int W>
+__global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, PartParams pp, PartBuffers pb,
+                                                          DevScalars *sc) {
+  __shared__ uint64_t stage[T * W];
+  __shared__ uint32_t cnt2[1 << (kPartMaxLog2 - 1)];
+  __shared__ uint16_t lstart[1 << kPartMaxLog2];
+  __shared__ uint32_t swave[kPNT / 64];
+  if (sc->redo || !sc->packed) return;  // uniform: the gather variant runs
+  constexpr int R = T / kPNT;
+  const int nb = 1 << pp.np_log2;
+  const uint32_t kbase = (uint32_t)sc->kbase;
+  const int64_t k_epoch = sc->k_epoch;
+  const uint64_t tile = xcd_tile(blockIdx.x, pp.tiles);
+  const uint64_t q0 = wall_clock64();
+  for (int i = threadIdx.x; i < (nb + 1) / 2; i += kPNT) cnt2[i] = 0;
+  const uint64_t base = tile * T;
+  uint32_t key[R];
+  int64_t ts[R];
+  uint64_t col[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint64_t i = base + (uint64_t)r * kPNT + threadIdx.x;
+    const bool in = i < b.n;
+    key[r] = in ? b.key[i] : HSG_KEY_NONE;
+    ts[r] = in ? b.ts[i] : 0;
+    col[r] = (W == 2 && in) ? (uint64_t)b.col[0][i] : 0;
+  }
+  __syncthreads();
+  uint64_t late = 0;
+  uint32_t err = 0;
+  uint32_t slot[R];  // bucket << 16 | slot in the tile's run of the bucket, ~0 = no window
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    uint32_t krel, nwin;
+    slot[r] = ~0u;
+    if (!part_record(p, k_epoch, key[r], ts[r], INT64_MIN, krel, nwin, late, err)) continue;
+    const uint32_t bk = bucket_of(key[r], pp.np_log2);
+    const uint32_t sh = (bk & 1u) * 16u;
+    const uint32_t pos = (atomicAdd(&cnt2[bk >> 1], 1u << sh) >> sh) & 0xFFFFu;
+    slot[r] = (bk << 16) | pos;
+    const uint64_t i = base + (uint64_t)r * kPNT + threadIdx.x;
+    uint64_t vb = 0;
+    if (W == 2 && !(pp.has_valid && b.valid[0] && !b.valid[0][i])) vb = 1;
+    ts[r] = (int64_t)((uint64_t)key[r] | ((uint64_t)((krel - kbase) & 0xFFFFu) << 32) | ((uint64_t)nwin << 48) |
+                      (vb << 56));  // the packed header word, kept in the ts register
+  }
+  __syncthreads();
+  // tile-local exclusive scan of the bucket counts -> run starts
+  const int per = (nb + kPNT - 1) / kPNT;
+  const int lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
+  uint32_t loc = 0;
+  for (int k = lo; k < hi; ++k) loc += (cnt2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t incl = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) swave[wv] = incl;
+  __syncthreads();
+  uint32_t run = incl - loc;
+  for (int k = 0; k < wv; ++k) run += swave[k];
+  for (int k = lo; k < hi; ++k) {
+    lstart[k] = (uint16_t)run;
+    run += (cnt2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+  }
+  uint32_t placed = 0;
+  for (int k = 0; k < kPNT / 64; ++k) placed += swave[k];
+  __syncthreads();
+  // place the packed records at their bucket-sorted positions
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (slot[r] == ~0u) continue;
+    const uint32_t q = lstart[slot[r] >> 16] + (slot[r] & 0xFFFFu);
+    stage[q * W] = (uint64_t)ts[r];
+    if (W == 2) stage[q * W + 1] = col[r];
+  }
+  __syncthreads();
+  const uint64_t q1 = wall_clock64();
+  // write-out: record q goes to offt[tile][bucket] + (q - run start)
+  const uint32_t *orow = pb.offt + tile * (uint64_t)nb;
+  for (uint32_t q = threadIdx.x; q < placed; q += kPNT) {
+    const uint64_t h = stage[q * W];
+    const uint32_t bk = bucket_of((uint32_t)h, pp.np_log2);
+    const uint64_t dest = (uint64_t)orow[bk] + (q - lstart[bk]);
+    if (W == 2) {
+      const uint64_t c = stage[q * W + 1];
+      *(ulonglong2 *)(pb.rec + dest * 2) = make_ulonglong2(h, c);
+    } else {
+      pb.rec[dest] = h;
+    }
+  }
+  late = wave_sum_u64(late);
+  if (err) atomicOr(&sc->err, err);
+  if (threadIdx.x == 0) {
+    const uint64_t q4 = wall_clock64();
+    atomicAdd((unsigned long long *)&sc->scratch[13], (unsigned long long)(q1 - q0));
+    atomicAdd((unsigned long long *)&sc->scratch[16], (unsigned long long)(q4 - q1));
+    atomicAdd((unsigned long long *)&sc->scratch[17], 1ull);
+  }
+}
+
 void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp,
                          const int64_t *rec_wm, const int64_t *own_wm, const int64_t *seq, const PartBuffers &pb,
-                         DevScalars *sc) {
+                         DevScalars *sc, bool maybe_packed) {
   if (!pp.tiles) return;
-  hipLaunchKernelGGL(k_part_scatter<kPartTileRecs>, dim3((unsigned)pp.tiles), dim3(kPNT), 0, s, b, p, pp, rec_wm,
-                     own_wm, seq, pb, sc);
+  const dim3 g((unsigned)pp.tiles);
+  const bool stage = maybe_packed && !pp.has_seq && pp.words - 1 <= 2;  // packed words <= 2
+  if (stage) {
+    if (pp.words - 1 == 2)
+      hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 2>), g, dim3(kPNT), 0, s, b, p, pp, pb, sc);
+    else
+      hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 1>), g, dim3(kPNT), 0, s, b, p, pp, pb, sc);
+  }
+  hipLaunchKernelGGL(k_part_scatter<kPartTileRecs>, g, dim3(kPNT), 0, s, b, p, pp, rec_wm, own_wm, seq, pb, sc,
+                     stage ? 1 : 0);
 }
 
 // ---------------------------------------------------------------------------

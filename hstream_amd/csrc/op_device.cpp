@@ -438,12 +438,11 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       const bool can_pack = optimistic && !nopack && cfg.n_cols <= 8 && d.wpr < 256;
       if (optimistic) launch_part_decide(d.stream, d.sc, p, a.wm_in, cfg.grace_ms, can_pack);
       launch_part_offsets(d.stream, pp, d.part, d.sc);
-      launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc);
+      launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc, can_pack);
       launch_part_agg(d.stream, prog, p, pp, d.tw, d.part, kb.n, d.sc, can_pack);
     } else {
       launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, false);
     }
-    DTRY(hipEventRecord(d.ev_b, d.stream));
     if (has_last(prog)) launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, true);
     if (cfg.emit_mode == HSG_EMIT_PER_BATCH) {
       if (d.use_part)
@@ -452,6 +451,8 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
         launch_tw_emit(d.stream, d.tw, d.cap, prog, p, 0, d.out, a.pending, d.out_cap, d.sc, d.emit,
                        (uint64_t *)&d.sc->out_rows);
     }
+    // ev_a .. ev_b: the batch's device pipeline (aggregation + changelog rows)
+    DTRY(hipEventRecord(d.ev_b, d.stream));
     DTRY(hipGetLastError());
     return HSG_OK;
   };
