@@ -140,22 +140,36 @@ def main():
     total_records = n_rank * world * args.steps
     value = total_records / elapsed
 
-    # roofline of the dominant kernel (window assignment + hash aggregation)
+    # roofline of the batch pipeline (one "launch" = one batch through the
+    # partition + aggregation + changelog kernels, timed by HIP events on the
+    # op's stream): SURVEY.md 8(d) algorithmic bytes
+    #   N*(4 + 8 + 8C) + 2*U*R + E*O
+    # N records, C value columns, U groups touched, R state row bytes (key +
+    # slots), E changelog rows, O row bytes (key 4, window 8 + 8, 8 per agg)
     launches = st1["agg_kernel_launches"] - st0["agg_kernel_launches"]
     agg_s = (st1["agg_kernel_ms"] - st0["agg_kernel_ms"]) / 1e3
     n_slots = len(spec_state_slots(spec))
     ncol = len(spec.col_types)
     rec_bytes = 4 + 8 + 8 * ncol
     row_bytes = 8 + 8 * n_slots
+    out_bytes = 4 + 8 + 8 + 8 * len(spec.aggs) if emit != abi.HSG_EMIT_NONE else 0
     touched = st1["touched_total"] - st0["touched_total"]
+    emitted = touched if emit == abi.HSG_EMIT_PER_BATCH else 0
     owned = (st1["records_owned"] - st0["records_owned"])
-    alg_bytes = owned * rec_bytes + 2 * touched * row_bytes
+    alg_bytes = owned * rec_bytes + 2 * touched * row_bytes + emitted * out_bytes
     achieved = (alg_bytes / agg_s / 1e9) if agg_s > 0 else 0.0
-    traffic = traffic_from_csv(args.traffic_csv, launches) if args.traffic_csv else None
+    traffic, tsrc = None, None
+    if args.traffic_csv:
+        traffic, tsrc = traffic_from_csv(args.traffic_csv, launches), args.traffic_csv
+    else:
+        traffic, tsrc = committed_traffic(args, world)
     roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-            "kernel": "k_tw_agg", "alg_bytes_per_launch": int(alg_bytes / max(1, launches)),
+            "kernel": "batch pipeline (k_part_hist, offsets, k_part_scatter[_st], k_part_agg, k_touch_emit)",
+            "alg_bytes_per_launch": int(alg_bytes / max(1, launches)),
             "avg_launch_ms": round(agg_s * 1e3 / max(1, launches), 4)}
+    if tsrc:
+        roof["traffic_source"] = tsrc
 
     xchg = None
     if world > 1 or args.force_exchange:
@@ -279,6 +293,23 @@ def spec_state_slots(spec):
             if s not in slots:
                 slots.append(s)
     return slots
+
+
+def committed_traffic(args, world):
+    """Per-batch HBM bytes of this configuration from the committed PMC summary
+    (tools/traffic.sh -> profiles/<round>/traffic_<config>.json), when the run
+    uses the configuration's default sizes; else None."""
+    if world != 1 or args.records or args.batch or args.emit != "per_batch" or args.force_exchange:
+        return None, None
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"traffic_{args.config.lower()}.json")))
+    if not paths:
+        return None, None
+    with open(paths[-1]) as f:
+        d = json.load(f)
+    if d.get("bench_args", "").strip() not in ("", f"--config {args.config}"):
+        return None, None
+    return int(d["hbm_bytes_per_batch"]), os.path.relpath(paths[-1], ROOT)
 
 
 def traffic_from_csv(path, launches):

@@ -60,23 +60,28 @@ __device__ inline int64_t prec_elem(const Program &prog, int s, const R &r) {
   }
 }
 
-template <int MS, typename R>
-__device__ inline void lds_apply(const Program &prog, int64_t *__restrict__ row, const R &r) {
+// LDS aggregates are slot-major: slot s of entry e at agg[s * ST + e] (ST = the
+// table's entry count), so the 64 lanes of one atomic instruction spread over
+// the banks (entry-major rows of 48 B hit a quarter of them). `skip`: slots not
+// updated in LDS (COUNT(col) of a batch without validity arrays = COUNT(*)).
+template <int MS, int ST, typename R>
+__device__ inline void lds_apply(const Program &prog, int64_t *__restrict__ row, const R &r, uint32_t skip) {
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
     if (s >= prog.n_slots) break;
     const int op = prog.slot_op[s];
-    if (op == S_LAST_VAL) continue;
+    if (op == S_LAST_VAL || ((skip >> s) & 1u)) continue;
     if (op != S_CNT_ALL && !r.present(prog.slot_col[s])) continue;
     const int64_t x = prec_elem(prog, s, r);
-    unsigned long long *u = (unsigned long long *)(row + s);
+    int64_t *a = row + s * ST;
+    unsigned long long *u = (unsigned long long *)a;
     switch (op) {
       case S_CNT_ALL:
       case S_CNT:
       case S_SUM_I: atomicAdd(u, (unsigned long long)x); break;
-      case S_SUM_F: unsafeAtomicAdd((double *)(row + s), __builtin_bit_cast(double, x)); break;
-      case S_MIN_I: atomicMin((long long *)(row + s), (long long)x); break;
-      case S_MAX_I: atomicMax((long long *)(row + s), (long long)x); break;
+      case S_SUM_F: unsafeAtomicAdd((double *)a, __builtin_bit_cast(double, x)); break;
+      case S_MIN_I: atomicMin((long long *)a, (long long)x); break;
+      case S_MAX_I: atomicMax((long long *)a, (long long)x); break;
       case S_MIN_F: atomicMin(u, (unsigned long long)x); break;
       case S_MAX_F:
       case S_LAST_SEQ: atomicMax(u, (unsigned long long)x); break;
@@ -85,15 +90,16 @@ __device__ inline void lds_apply(const Program &prog, int64_t *__restrict__ row,
   }
 }
 
-// a <- a (+) x over the aggregate slots (LAST_SEQ = latest sequence)
-template <int MS>
+// a <- a (+) x over the aggregate slots (LAST_SEQ = latest sequence); x strided by ST
+template <int MS, int ST>
 __device__ inline void acc_combine(const Program &prog, int64_t (&a)[MS], const int64_t *x) {
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
     if (s >= prog.n_slots) break;
     const int op = prog.slot_op[s];
     if (op == S_LAST_VAL) continue;
-    a[s] = op == S_LAST_SEQ ? ((uint64_t)x[s] > (uint64_t)a[s] ? x[s] : a[s]) : slot_combine(op, a[s], x[s]);
+    const int64_t v = x[s * ST];
+    a[s] = op == S_LAST_SEQ ? ((uint64_t)v > (uint64_t)a[s] ? v : a[s]) : slot_combine(op, a[s], v);
   }
 }
 
@@ -252,8 +258,8 @@ struct AggLds {
 // Block-wide: every thread calls. Returns the number of live entries.
 template <int MS, int E, int NT>
 __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const Program &prog, const TwParams &p, const TwTable &t,
-                              const PartBuffers &pb, DevScalars *sc, int S, bool exclusive, uint32_t &fresh,
-                              uint32_t &err, uint64_t &t_sort) {
+                              const PartBuffers &pb, DevScalars *sc, int S, bool exclusive, uint32_t skip,
+                              int cnt_all_slot, uint32_t &fresh, uint32_t &err, uint64_t &t_sort) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t SW = S ? (uint32_t)S : 1u;
   const uint64_t t0 = wall_clock64();
@@ -328,7 +334,7 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const Progra
     const uint32_t a = P - L.run[e];
     int64_t acc[MS];
 #pragma unroll
-    for (int s = 0; s < MS; ++s) acc[s] = L.agg[e * MS + s];
+    for (int s = 0; s < MS; ++s) acc[s] = L.agg[s * E + e];
     // later panes of the key (sorted after q) that window w covers: pane <= w + SW - 1
     uint32_t j = q + 1;
     uint64_t top = (uint64_t)a + SW - 1;
@@ -337,8 +343,14 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const Progra
         const int f = L.live[j];
         const uint64_t gj = L.key[f];
         if ((gj & 0xFFFFFFFF00000000ull) != kb || (uint64_t)(uint32_t)gj > top) break;
-        acc_combine<MS>(prog, acc, &L.agg[f * MS]);
+        acc_combine<MS, E>(prog, acc, &L.agg[f]);
         ++j;
+      }
+      if (skip) {
+        // COUNT(col) slots not kept in LDS: every record of the batch has the column
+#pragma unroll
+        for (int s = 0; s < MS; ++s)
+          if ((skip >> s) & 1u) acc[s] = acc[cnt_all_slot];
       }
       const uint32_t sl = flush_window<MS>(prog, p, t, kb | w, acc, exclusive, fresh, err);
       if (o < pb.touched_cap) pb.touched[o] = sl;
@@ -354,7 +366,7 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const Progra
     const int e = L.live[q];
     L.key[e] = kEmpty;
 #pragma unroll
-    for (int s = 0; s < MS; ++s) L.agg[e * MS + s] = s < prog.n_slots ? slot_identity_dev(prog.slot_op[s]) : 0;
+    for (int s = 0; s < MS; ++s) L.agg[s * E + e] = s < prog.n_slots ? slot_identity_dev(prog.slot_op[s]) : 0;
   }
   if (threadIdx.x == 0) {
     L.fill = 0;
@@ -387,7 +399,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   for (int e = threadIdx.x; e < E; e += NT) {
     L.key[e] = kEmpty;
 #pragma unroll
-    for (int s = 0; s < MS; ++s) L.agg[e * MS + s] = s < prog.n_slots ? slot_identity_dev(prog.slot_op[s]) : 0;
+    for (int s = 0; s < MS; ++s) L.agg[s * E + e] = s < prog.n_slots ? slot_identity_dev(prog.slot_op[s]) : 0;
   }
   __syncthreads();
   if (blockIdx.x >= chunk_start[nb]) return;  // uniform: the grid is an upper bound
@@ -402,6 +414,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const uint32_t kbase = (uint32_t)sc->kbase;
   const int S = pp.pane_S;
   const int nrounds = 1 << pp.rbits;
+  // without validity arrays COUNT(col) = COUNT(*): derive those slots at flush
+  int cnt_all_slot = -1;
+  uint32_t skip = 0;
+  for (int s = 0; s < prog.n_slots && s < MS; ++s)
+    if (prog.slot_op[s] == S_CNT_ALL && cnt_all_slot < 0) cnt_all_slot = s;
+  if (!pp.has_valid && cnt_all_slot >= 0)
+    for (int s = 0; s < prog.n_slots && s < MS; ++s)
+      if (prog.slot_op[s] == S_CNT) skip |= 1u << s;
   const int64_t k_epoch = sc->k_epoch;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint64_t pairs = 0, groups = 0, t_rec = 0, t_flush = 0, t_sort = 0, flushes = 0;
@@ -450,7 +470,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
               const uint64_t g = ((uint64_t)key << 32) | (uint64_t)(krel + j);
               const int e = lds_insert<E>(L.key, &L.fill, limit, g);
               if (e >= 0) {
-                lds_apply<MS>(prog, &L.agg[e * MS], r);
+                lds_apply<MS, E>(prog, &L.agg[e], r, skip);
                 L.nw[e] = 1;
               } else {
                 direct_windows<MS>(prog, p, t, pb, sc, key, krel + j, krel + j, r, fresh, err);
@@ -477,7 +497,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
           const int e = lds_insert<E>(L.key, &L.fill, limit, ((uint64_t)key << 32) | P);
           if (e < 0) continue;  // table full: after the next flush
           pairs += nw;
-          if (pp.exp != 1) lds_apply<MS>(prog, &L.agg[e * MS], r);
+          if (pp.exp != 1) lds_apply<MS, E>(prog, &L.agg[e], r, skip);
           L.nw[e] = (uint8_t)nw;
           pend &= ~(1u << u);
         }
@@ -487,7 +507,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         if (!more) break;
         // table full with records left: flush and go on (the records are
         // loaded again afterwards, so they hold no registers across the flush)
-        groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, fresh, err, t_sort);
+        groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, skip, cnt_all_slot, fresh, err, t_sort);
         ++flushes;
         load();
         ta = wall_clock64();
@@ -509,7 +529,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       }
     }
     const uint64_t tb = wall_clock64();
-    groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, fresh, err, t_sort);
+    groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, skip, cnt_all_slot, fresh, err, t_sort);
     ++flushes;
     t_flush += wall_clock64() - tb;
   }
