@@ -13,12 +13,14 @@
 //      (and stream times), so results equal one GPU fed the whole batch.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "hsg_exchange.h"
 #include "hsg_kernels.h"
+#include "hsg_part.h"
 #include "hsg_sort.h"
 
 namespace hsg {
@@ -76,6 +78,16 @@ int exchange_device_init(OpDevice &d, const hsg_op_config &cfg, uint64_t batch_c
   DTRY(hipMalloc((void **)&d.st_seq, (uint64_t)G * n * 8 + 8));
   DTRY(hipMalloc((void **)&d.st_wm, (uint64_t)G * n * 8 + 8));
   if (!d.h_tmp) DTRY(hipHostMalloc((void **)&d.h_tmp, 8 * sizeof(uint64_t), hipHostMallocDefault));
+  // owner partition of the fast exchange: log2(ranks) for a power-of-two rank
+  // count; HSG_XPART_LOG2 (tests) partitions a single rank finer, every
+  // region still going to rank 0
+  d.xpart_log2 = log2_exact((uint32_t)G);
+  if (const char *e = getenv("HSG_XPART_LOG2")) {
+    const int v = atoi(e);
+    if (G == 1 && v >= 0 && v <= 6) d.xpart_log2 = v;
+  }
+  d.bshift = d.xpart_log2 > 0 ? d.xpart_log2 : 0;
+  if (d.bshift + kPartMaxLog2 > 60) d.bshift = 0;
   return HSG_OK;
 }
 
@@ -98,8 +110,156 @@ void exchange_device_free(OpDevice &d) {
   d.x = nullptr;
 }
 
+// Fast path: no LAST / per-record changelog / sessions (record order and
+// global sequence irrelevant) and, decided after the all-gather, no late
+// record. Owner partition through the partition-offsets pipeline (owner = top
+// key-hash bits), columnar send buffers, one all-to-all-v per column; the
+// received columns are the owner's batch as they are (no unpack, no sort).
+// `fallback` = some record may be late: the caller runs the classic path.
+static int push_sharded_fast(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
+                             PushResult &r, std::string &err, bool &fallback) {
+  XBuffers &x = *d.x;
+  const int G = a.nranks, me = a.rank;
+  const int IW = info_words(G);
+  const int xl = d.xpart_log2;
+  ncclComm_t comm = a.comm->comm;
+  hipStream_t s = d.stream;
+  fallback = false;
+  if (a.batch->n > x.batch) {
+    err = "batch larger than batch_capacity";
+    return HSG_E_CAPACITY;
+  }
+  Batch kb;
+  int rc = stage_batch(d, a.batch, kb, err);
+  if (rc != HSG_OK) return rc;
+  bool has_valid = false;
+  for (int c = 0; c < cfg.n_cols; ++c) has_valid = has_valid || kb.valid[c] != nullptr;
+  const bool unwin = cfg.window_kind == HSG_UNWINDOWED;
+  const uint64_t n = kb.n;
+  DTRY(hipEventRecord(d.ev_c, s));
+  rc = clear_batch_scalars(d, err);
+  if (rc != HSG_OK) return rc;
+  // 1. owner counts per tile (+ ts extrema), owner-major run offsets, facts
+  launch_x_hist(s, kb, xl, unwin, d.part.hist, d.sc);
+  PartParams xp;
+  memset(&xp, 0, sizeof(xp));
+  xp.np_log2 = xl;
+  xp.tiles = x_tiles(n);
+  launch_part_offsets(s, xp, d.part, d.sc);
+  launch_x_info(s, d.sc, d.part.bstart, xl, (uint32_t)G, n, has_valid, x.info);
+  // 2. all-gather the per-rank facts
+  NTRY(ncclAllGather(x.info, x.info_all, IW, ncclInt64, comm, s));
+  DTRY(hipMemcpyAsync(x.h_info, x.info_all, (uint64_t)G * IW * 8, hipMemcpyDeviceToHost, s));
+  DTRY(hipStreamSynchronize(s));
+  const int64_t *H = x.h_info;
+  int64_t wm_global = a.wm_in, carry = a.wm_in, min_ts = INT64_MAX;
+  uint64_t total = 0;
+  bool any_valid = false;
+  for (int q = 0; q < G; ++q) {
+    const int64_t *I = H + (uint64_t)q * IW;
+    if (I[2] > 0) {
+      wm_global = I[0] > wm_global ? I[0] : wm_global;
+      if (q < me) carry = I[0] > carry ? I[0] : carry;
+      min_ts = I[1] < min_ts ? I[1] : min_ts;
+    }
+    total += (uint64_t)I[2];
+    any_valid = any_valid || I[3] != 0;
+  }
+  const bool time_win = cfg.window_kind == HSG_TUMBLING || cfg.window_kind == HSG_HOPPING;
+  if (time_win && min_ts != INT64_MAX && wm_global > (int64_t)((uint64_t)min_ts + (uint64_t)cfg.grace_ms)) {
+    fallback = true;  // some record may be late: per-record stream time in global order
+    return HSG_OK;
+  }
+  // 3. columnar scatter by owner, one all-to-all-v per column
+  std::vector<size_t> scount(G), sdispl(G), rcount(G), rdispl(G);
+  uint64_t so = 0, ro = 0;
+  for (int q = 0; q < G; ++q) {
+    scount[q] = (size_t)H[(uint64_t)me * IW + 4 + q];
+    sdispl[q] = so;
+    so += scount[q];
+    rcount[q] = (size_t)H[(uint64_t)q * IW + 4 + me];
+    rdispl[q] = ro;
+    ro += rcount[q];
+  }
+  if (ro > d.batch_cap) {
+    err = "received more records than the op's capacity";
+    return HSG_E_CAPACITY;
+  }
+  const int C = cfg.n_cols;
+  auto carve = [&](void *base, uint64_t cap) {
+    XCols c;
+    memset(&c, 0, sizeof(c));
+    char *p = (char *)base;
+    auto take = [&](uint64_t bytes) {
+      char *q = p;
+      p += (bytes + 255) & ~255ull;
+      return q;
+    };
+    c.ts = (int64_t *)take(cap * 8);
+    for (int k = 0; k < C; ++k) c.col[k] = (int64_t *)take(cap * 8);
+    c.key = (uint32_t *)take(cap * 4);
+    for (int k = 0; k < C; ++k) c.valid[k] = (uint8_t *)take(cap);
+    return c;
+  };
+  const XCols snd = carve(x.send, x.batch), rcv = carve(x.recv, (uint64_t)G * x.batch);
+  launch_x_scatter(s, kb, xl, unwin, any_valid, C, d.part.offt, snd);
+  NTRY(ncclGroupStart());
+  NTRY(ncclAllToAllv(snd.key, scount.data(), sdispl.data(), rcv.key, rcount.data(), rdispl.data(), ncclUint32, comm,
+                     s));
+  NTRY(ncclAllToAllv(snd.ts, scount.data(), sdispl.data(), rcv.ts, rcount.data(), rdispl.data(), ncclInt64, comm, s));
+  for (int k = 0; k < C; ++k) {
+    NTRY(ncclAllToAllv(snd.col[k], scount.data(), sdispl.data(), rcv.col[k], rcount.data(), rdispl.data(), ncclInt64,
+                       comm, s));
+    if (any_valid)
+      NTRY(ncclAllToAllv(snd.valid[k], scount.data(), sdispl.data(), rcv.valid[k], rcount.data(), rdispl.data(),
+                         ncclUint8, comm, s));
+  }
+  NTRY(ncclGroupEnd());
+  DTRY(hipEventRecord(d.ev_d, s));
+  DTRY(hipGetLastError());
+  // 4. aggregate the owned records (order irrelevant for these ops)
+  Batch rb;
+  memset(&rb, 0, sizeof(rb));
+  rb.n = ro;
+  rb.key = rcv.key;
+  rb.ts = rcv.ts;
+  for (int k = 0; k < C; ++k) {
+    rb.col[k] = rcv.col[k];
+    rb.valid[k] = any_valid ? rcv.valid[k] : nullptr;
+  }
+  PushArgs la = a;
+  la.wm_in = carry;  // any value <= the records' stream times keeps grace exact
+  rc = push_local(d, cfg, prog, la, rb, nullptr, nullptr, r, err);
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, d.ev_c, d.ev_d) == hipSuccess) r.exchange_ms = ms;
+  r.exchange_bytes = (uint64_t)(so - scount[me]) * (12 + 8 * C + (any_valid ? C : 0));
+  r.wm_out = wm_global;
+  r.owned = ro;
+  r.global_records = total;
+  return rc;
+}
+
+static int push_sharded_classic(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
+                                PushResult &r, std::string &err);
+
 int push_sharded(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, PushResult &r,
                  std::string &err) {
+  static const bool no_fast = [] {
+    const char *e = getenv("HSG_XFAST");
+    return e && strcmp(e, "0") == 0;
+  }();
+  bool need_seq = cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.window_kind == HSG_SESSION;
+  for (int q = 0; q < prog.n_slots; ++q) need_seq = need_seq || prog.slot_op[q] == S_LAST_SEQ;
+  if (!no_fast && d.use_part && d.xpart_log2 >= 0 && !need_seq) {
+    bool fallback = false;
+    int rc = push_sharded_fast(d, cfg, prog, a, r, err, fallback);
+    if (rc != HSG_OK || !fallback) return rc;
+  }
+  return push_sharded_classic(d, cfg, prog, a, r, err);
+}
+
+static int push_sharded_classic(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
+                                PushResult &r, std::string &err) {
   XBuffers &x = *d.x;
   const int G = a.nranks, me = a.rank;
   const int IW = info_words(G);

@@ -219,10 +219,9 @@ __device__ inline int lds_insert(uint64_t *lkey, uint32_t *lfill, uint32_t limit
 }
 
 // sub-round of a key: the hash bits just below its bucket bits
-__device__ inline uint32_t key_round(uint32_t key, int np_log2, int rbits) {
+__device__ inline uint32_t key_round(uint32_t key, int np_log2, int rbits, int bshift) {
   if (!rbits) return 0;
-  const uint64_t h = mix64((uint64_t)key * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull);
-  return (uint32_t)(h >> (64 - np_log2 - rbits)) & ((1u << rbits) - 1u);
+  return (uint32_t)((key_hash(key) << bshift) >> (64 - np_log2 - rbits)) & ((1u << rbits) - 1u);
 }
 
 // Aggregation of one chunk of a bucket (buckets are disjoint key sets, so when
@@ -447,7 +446,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
       for (int u = 0; u < RPT; ++u) {
         const uint64_t i = s0 + (uint64_t)u * NT + threadIdx.x;
-        if (i < r1 && (nrounds == 1 || key_round(rr[u].key(), pp.np_log2, pp.rbits) == (uint32_t)round))
+        if (i < r1 && (nrounds == 1 || key_round(rr[u].key(), pp.np_log2, pp.rbits, pp.bshift) == (uint32_t)round))
           pend |= 1u << u;
       }
       uint32_t dpend = 0;  // records for the direct HBM path

@@ -46,6 +46,22 @@ struct XBuffers {
   uint64_t batch;                    // per-rank push capacity
 };
 
+// columnar exchange buffers of the fast path
+struct XCols {
+  uint32_t *key;
+  int64_t *ts;
+  int64_t *col[kMaxCols];
+  uint8_t *valid[kMaxCols];
+};
+
+uint64_t x_tiles(uint64_t n);
+// xl = log2 of the owner partitions (ranks, or more when a test partitions finer)
+void launch_x_hist(hipStream_t s, const Batch &b, int xl, bool unwin, uint32_t *hist, DevScalars *sc);
+void launch_x_info(hipStream_t s, const DevScalars *sc, const uint64_t *bstart, int xl, uint32_t G, uint64_t n,
+                   bool has_valid, int64_t *info);
+void launch_x_scatter(hipStream_t s, const Batch &b, int xl, bool unwin, bool write_valid, int ncols,
+                      const uint32_t *offt, const XCols &send);
+
 void launch_x_minmax(hipStream_t s, const int64_t *tmax, const int64_t *tmin, uint64_t n_tiles, uint64_t n,
                      int has_valid, int64_t *info);
 void launch_x_owner(hipStream_t s, const Batch &b, uint32_t G, uint32_t *owner, uint32_t *idx, uint64_t *hist);

@@ -165,6 +165,18 @@ __device__ __host__ inline uint64_t mix64(uint64_t x) {
   return x;
 }
 
+// Hash of a group key: its top bits pick the owner GPU (power-of-two ranks),
+// the next bits the partition bucket, the bits below the aggregation round.
+__device__ __host__ inline uint64_t key_hash(uint32_t key) {
+  return mix64((uint64_t)key * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull);
+}
+__device__ __host__ inline int log2_exact(uint32_t g) {  // -1 unless g is a power of two
+  if (g == 0 || (g & (g - 1))) return -1;
+  int l = 0;
+  while ((1u << l) < g) ++l;
+  return l;
+}
+
 // Order-preserving map f64 -> u64 (total order on non-NaN values).
 __device__ __host__ inline uint64_t f64_ord(double d) {
   uint64_t u = __builtin_bit_cast(uint64_t, d);

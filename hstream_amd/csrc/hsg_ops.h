@@ -60,6 +60,8 @@ struct OpDevice {
   int np_log2 = 10;             // partitions of the next batch (adapted per batch)
   int rbits = 0;                // key-hash aggregation rounds of the next batch (log2)
   int pane_S = 1;               // panes per window (0: one LDS entry per window)
+  int bshift = 0;               // key-hash bits that pick the owner GPU (skipped by local buckets)
+  int xpart_log2 = -1;          // owner partition of the fast exchange: log2(ranks), -1 = not a power of two
   bool agg_big = true;          // aggregation variant of the next batch (big LDS table)
   // sessions
   SessTable ss = {};

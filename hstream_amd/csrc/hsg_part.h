@@ -40,7 +40,7 @@ struct PartBuffers {
 };
 
 struct PartParams {
-  int32_t np_log2;    // partitions = 1 << np_log2
+  int32_t np_log2;    // partitions = 1 << np_log2 (np_log2 + bshift <= 64)
   int32_t has_valid;
   int32_t has_seq;
   int32_t words;
@@ -48,6 +48,7 @@ struct PartParams {
   int32_t pane_S;     // aggregation: panes per window (size / advance), 0 = one LDS entry per window
   int32_t rbits;      // aggregation: 2^rbits key-hash rounds per sub-chunk
   int32_t big;        // aggregation variant: 1 = big LDS table, 1024 threads
+  int32_t bshift;     // owner bits above the bucket bits in the key hash (multi-GPU, power-of-two ranks)
   int32_t exp;        // experiment knob (HSG_EXP, timing studies only): 1 = no LDS aggregate update, 2 = no LDS insert
   uint64_t tiles;     // partition-pass tiles of this batch
   uint64_t chunk;     // records per aggregation workgroup

@@ -10,7 +10,11 @@
 
 namespace hsg {
 
-__device__ inline uint32_t owner_of(uint32_t key, uint32_t G) {
+// owner GPU of a key: the top log2(G) bits of key_hash for a power-of-two rank
+// count (the same bits the fast exchange partitions on; local buckets skip
+// them), hash mod G otherwise
+__device__ inline uint32_t owner_of(uint32_t key, uint32_t G, int lg) {
+  if (lg >= 0) return lg ? (uint32_t)(key_hash(key) >> (64 - lg)) : 0u;
   return (uint32_t)(mix64((uint64_t)key ^ 0x5bd1e9955bd1e995ull) % G);
 }
 
@@ -45,13 +49,13 @@ __global__ __launch_bounds__(1024) void k_x_minmax(const int64_t *tmax, const in
 
 // owner digit per record (G = dropped: HSG_KEY_NONE records only move stream
 // time, which the all-gathered maxima already carry) + histogram
-__global__ void k_x_owner(Batch b, uint32_t G, uint32_t *owner, uint32_t *idx, unsigned long long *hist) {
+__global__ void k_x_owner(Batch b, uint32_t G, int lg, uint32_t *owner, uint32_t *idx, unsigned long long *hist) {
   __shared__ unsigned int h[kMaxRanks + 1];
   if (threadIdx.x <= G) h[threadIdx.x] = 0;
   __syncthreads();
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < b.n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t key = b.key[i];
-    uint32_t o = key == HSG_KEY_NONE ? G : owner_of(key, G);
+    uint32_t o = key == HSG_KEY_NONE ? G : owner_of(key, G, lg);
     owner[i] = o;
     idx[i] = (uint32_t)i;
     atomicAdd(&h[o], 1u);
@@ -114,8 +118,125 @@ void launch_x_minmax(hipStream_t s, const int64_t *tmax, const int64_t *tmin, ui
 }
 void launch_x_owner(hipStream_t s, const Batch &b, uint32_t G, uint32_t *owner, uint32_t *idx, uint64_t *hist) {
   if (b.n)
-    hipLaunchKernelGGL(k_x_owner, dim3(grid_for(b.n, 256)), dim3(256), 0, s, b, G, owner, idx,
+    hipLaunchKernelGGL(k_x_owner, dim3(grid_for(b.n, 256)), dim3(256), 0, s, b, G, log2_exact(G), owner, idx,
                        (unsigned long long *)hist);
+}
+
+// ---------------------------------------------------------------------------
+// fast exchange (no LAST / per-record order / late records): owner partition
+// with the partition-offsets pipeline, columnar send buffers, one all-to-all-v
+// per column, the received columns are the owner's batch as they are
+// ---------------------------------------------------------------------------
+constexpr int kXT = 4096;   // records per tile
+constexpr int kXNT = 512;   // threads
+
+// a record travels iff it has a key and, for a time-window op, ts >= 0 (the
+// others only move stream time, which the all-gathered maxima carry)
+__device__ inline bool x_sends(const Batch &b, uint64_t i, bool unwin) {
+  return b.key[i] != HSG_KEY_NONE && (unwin || b.ts[i] >= 0);
+}
+
+// tile-major owner counts hist[tile][P] + the ts extrema (scratch[21..22] images)
+__global__ __launch_bounds__(kXNT) void k_x_hist(Batch b, int xl, int unwin, uint32_t *hist, uint64_t tiles,
+                                                 DevScalars *sc) {
+  __shared__ uint32_t cnt[kMaxRanks];
+  __shared__ uint64_t sext[2][kXNT / 64];
+  const uint32_t P = 1u << xl;
+  for (uint32_t o = threadIdx.x; o < P; o += kXNT) cnt[o] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * kXT;
+  uint64_t mx = 0, mn = 0;
+  for (int r = 0; r < kXT / kXNT; ++r) {
+    const uint64_t i = base + (uint64_t)r * kXNT + threadIdx.x;
+    if (i >= b.n) break;
+    const uint32_t key = b.key[i];
+    const int64_t ts = b.ts[i];
+    const uint64_t o = (uint64_t)ts ^ 0x8000000000000000ull;
+    mx = o > mx ? o : mx;
+    if (key != HSG_KEY_NONE && ts >= 0) mn = ~o > mn ? ~o : mn;
+    if (key != HSG_KEY_NONE && (unwin || ts >= 0)) atomicAdd(&cnt[owner_of(key, P, xl)], 1u);
+  }
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    const uint64_t a = __shfl_xor(mx, s, 64), c = __shfl_xor(mn, s, 64);
+    mx = a > mx ? a : mx;
+    mn = c > mn ? c : mn;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sext[0][threadIdx.x >> 6] = mx;
+    sext[1][threadIdx.x >> 6] = mn;
+  }
+  __syncthreads();
+  for (uint32_t o = threadIdx.x; o < P; o += kXNT) hist[blockIdx.x * (uint64_t)P + o] = cnt[o];
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < kXNT / 64; ++k) {
+      mx = sext[0][k] > mx ? sext[0][k] : mx;
+      mn = sext[1][k] > mn ? sext[1][k] : mn;
+    }
+    if (mx) atomicMax((unsigned long long *)&sc->scratch[21], (unsigned long long)mx);
+    if (mn) atomicMax((unsigned long long *)&sc->scratch[22], (unsigned long long)mn);
+  }
+}
+
+// this rank's facts for the all-gather: [max ts, min keyed ts, n, has_valid, per-rank counts]
+__global__ void k_x_info(const DevScalars *sc, const uint64_t *bstart, int xl, uint32_t G, uint64_t n, int has_valid,
+                         int64_t *info) {
+  if (threadIdx.x != 0) return;
+  const uint64_t mx = sc->scratch[21], mn = sc->scratch[22];
+  info[0] = mx ? (int64_t)(mx ^ 0x8000000000000000ull) : INT64_MIN;
+  info[1] = mn ? (int64_t)(~mn ^ 0x8000000000000000ull) : INT64_MAX;
+  info[2] = (int64_t)n;
+  info[3] = has_valid;
+  const uint32_t per = (1u << xl) / G;  // owner regions per rank (1 unless a test partitions finer)
+  for (uint32_t q = 0; q < G; ++q) info[4 + q] = (int64_t)(bstart[(q + 1) * per] - bstart[q * per]);
+}
+
+// every sent record at offt[tile][owner] + its slot in the tile's run, columnar
+__global__ __launch_bounds__(kXNT) void k_x_scatter(Batch b, int xl, int unwin, int write_valid, int ncols,
+                                                    const uint32_t *offt, XCols send) {
+  __shared__ uint32_t cnt[kMaxRanks];
+  __shared__ uint32_t goff[kMaxRanks];
+  const uint32_t P = 1u << xl;
+  for (uint32_t o = threadIdx.x; o < P; o += kXNT) {
+    cnt[o] = 0;
+    goff[o] = offt[blockIdx.x * (uint64_t)P + o];
+  }
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * kXT;
+  for (int r = 0; r < kXT / kXNT; ++r) {
+    const uint64_t i = base + (uint64_t)r * kXNT + threadIdx.x;
+    if (i >= b.n) break;
+    const uint32_t key = b.key[i];
+    const int64_t ts = b.ts[i];
+    if (key == HSG_KEY_NONE || (!unwin && ts < 0)) continue;
+    const uint32_t o = owner_of(key, P, xl);
+    const uint64_t d = (uint64_t)goff[o] + atomicAdd(&cnt[o], 1u);
+    send.key[d] = key;
+    send.ts[d] = ts;
+    for (int c = 0; c < ncols; ++c) {
+      send.col[c][d] = b.col[c][i];
+      if (write_valid) send.valid[c][d] = rec_present(b, c, i) ? 1 : 0;
+    }
+  }
+}
+
+uint64_t x_tiles(uint64_t n) { return (n + kXT - 1) / kXT; }
+
+void launch_x_hist(hipStream_t s, const Batch &b, int xl, bool unwin, uint32_t *hist, DevScalars *sc) {
+  const uint64_t tiles = x_tiles(b.n);
+  if (tiles)
+    hipLaunchKernelGGL(k_x_hist, dim3((unsigned)tiles), dim3(kXNT), 0, s, b, xl, unwin ? 1 : 0, hist, tiles, sc);
+}
+void launch_x_info(hipStream_t s, const DevScalars *sc, const uint64_t *bstart, int xl, uint32_t G, uint64_t n,
+                   bool has_valid, int64_t *info) {
+  hipLaunchKernelGGL(k_x_info, dim3(1), dim3(64), 0, s, sc, bstart, xl, G, n, has_valid ? 1 : 0, info);
+}
+void launch_x_scatter(hipStream_t s, const Batch &b, int xl, bool unwin, bool write_valid, int ncols,
+                      const uint32_t *offt, const XCols &send) {
+  const uint64_t tiles = x_tiles(b.n);
+  if (tiles)
+    hipLaunchKernelGGL(k_x_scatter, dim3((unsigned)tiles), dim3(kXNT), 0, s, b, xl, unwin ? 1 : 0,
+                       write_valid ? 1 : 0, ncols, offt, send);
 }
 void launch_x_recwm(hipStream_t s, const Batch &b, const int64_t *tprefix, int64_t *wm) {
   uint64_t tiles = (b.n + kTileRecords - 1) / kTileRecords;

@@ -26,9 +26,9 @@ namespace hsg {
 
 constexpr uint16_t kNoBucket = 0xFFFF;
 
-__device__ inline uint32_t bucket_of(uint32_t key, int np_log2) {
-  return np_log2 ? (uint32_t)(mix64((uint64_t)key * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull) >> (64 - np_log2))
-                 : 0u;
+// bucket = the np_log2 hash bits below the top `bshift` (owner) bits
+__device__ inline uint32_t bucket_of(uint32_t key, int np_log2, int bshift) {
+  return np_log2 ? (uint32_t)((key_hash(key) << bshift) >> (64 - np_log2)) : 0u;
 }
 
 // Accepted window run of one record: [krel, krel + nwin) relative to the epoch.
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(kPNT) void k_part_hist(Batch b, TwParams p, PartPar
   uint64_t ext[2] = {0, 0};
   walk_tile<T, kPNT>(b, p, tile, sc->k_epoch, opt ? nullptr : pick_wm(rec_wm, own_wm, sc), late, err,
                      [&](int, uint64_t, uint32_t key, uint32_t, uint32_t) {
-                       atomicAdd(&cnt[bucket_of(key, pp.np_log2)], 1u);
+                       atomicAdd(&cnt[bucket_of(key, pp.np_log2, pp.bshift)], 1u);
                      },
                      opt ? ext : nullptr);
   if (opt) {
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
   uint32_t err = 0;
   walk_tile<T, kPNT>(b, p, tile, sc->k_epoch, pick_wm(rec_wm, own_wm, sc), late, err,
                      [&](int j, uint64_t, uint32_t key, uint32_t krel, uint32_t nwin) {
-                       const uint32_t bk = bucket_of(key, pp.np_log2);
+                       const uint32_t bk = bucket_of(key, pp.np_log2, pp.bshift);
                        lkn[j] = (uint64_t)krel | ((uint64_t)nwin << 32);
                        lbk[j] = (uint16_t)bk;
                        atomicAdd(&cursor[bk], 1u);
@@ -419,7 +419,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
     uint32_t krel, nwin;
     slot[r] = ~0u;
     if (!part_record(p, k_epoch, key[r], ts[r], INT64_MIN, krel, nwin, late, err)) continue;
-    const uint32_t bk = bucket_of(key[r], pp.np_log2);
+    const uint32_t bk = bucket_of(key[r], pp.np_log2, pp.bshift);
     const uint32_t sh = (bk & 1u) * 16u;
     const uint32_t pos = (atomicAdd(&cnt2[bk >> 1], 1u << sh) >> sh) & 0xFFFFu;
     slot[r] = (bk << 16) | pos;
@@ -467,7 +467,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
   const uint32_t *orow = pb.offt + tile * (uint64_t)nb;
   for (uint32_t q = threadIdx.x; q < placed; q += kPNT) {
     const uint64_t h = stage[q * W];
-    const uint32_t bk = bucket_of((uint32_t)h, pp.np_log2);
+    const uint32_t bk = bucket_of((uint32_t)h, pp.np_log2, pp.bshift);
     const uint64_t dest = (uint64_t)orow[bk] + (q - lstart[bk]);
     if (W == 2) {
       const uint64_t c = stage[q * W + 1];

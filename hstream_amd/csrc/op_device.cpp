@@ -422,6 +422,7 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       PartParams pp;
       memset(&pp, 0, sizeof(pp));
       pp.np_log2 = d.np_log2;
+      pp.bshift = d.bshift;
       for (int c = 0; c < cfg.n_cols; ++c) pp.has_valid |= kb.valid[c] != nullptr;
       pp.has_seq = has_last(prog);
       pp.words = part_words(cfg.n_cols, pp.has_seq);

@@ -250,9 +250,15 @@ def _x_specs():
     return out
 
 
+@pytest.mark.parametrize("xpart", [None, "2"], ids=["xpart1", "xpart4"])
 @pytest.mark.parametrize("late", [False, True], ids=["no_late", "late"])
 @pytest.mark.parametrize("spec", _x_specs())
-def test_exchange_path_single_rank(xeng, spec, late):
+def test_exchange_path_single_rank(xeng, spec, late, xpart, monkeypatch):
+    """xpart4: the fast exchange partitions the single rank's records into 4
+    owner regions (HSG_XPART_LOG2=2), all sent to rank 0, so the multi-owner
+    offsets and scatter run with one GPU; late batches take the classic path."""
+    if xpart:
+        monkeypatch.setenv("HSG_XPART_LOG2", xpart)
     batches = []
     for bi in range(3):
         key, ts, cols, valid = gen_small(2000 + bi, 4000, 29, col_types=spec.col_types, span=60_000,
