@@ -206,6 +206,68 @@ __global__ __launch_bounds__(kPNT) void k_part_hist(Batch b, TwParams p, PartPar
   }
 }
 
+// Optimistic histogram (no record late): only the window range decides whether
+// a record is placed (as part_record with an unreachable stream time), plus
+// the batch's ts extrema for k_part_decide. Fewer live registers than the
+// general walk, so more workgroups per CU hide the HBM latency.
+template <int T>
+__global__ __launch_bounds__(kPNT) void k_part_hist_opt(Batch b, TwParams p, PartParams pp, PartBuffers pb,
+                                                        DevScalars *sc) {
+  __shared__ uint32_t cnt[1 << kPartMaxLog2];
+  __shared__ uint64_t sext[2][kPNT / 64];
+  constexpr int R = T / kPNT;
+  const int nb = 1 << pp.np_log2;
+  const uint64_t tile = xcd_tile(blockIdx.x, pp.tiles);
+  const int64_t k_epoch = sc->k_epoch;
+  for (int i = threadIdx.x; i < nb; i += kPNT) cnt[i] = 0;
+  const uint64_t base = tile * T;
+  uint32_t key[R];
+  int64_t ts[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint64_t i = base + (uint64_t)r * kPNT + threadIdx.x;
+    const bool in = i < b.n;
+    key[r] = in ? b.key[i] : HSG_KEY_NONE;
+    ts[r] = in ? b.ts[i] : INT64_MIN;
+  }
+  __syncthreads();
+  uint64_t mx = 0, mn = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint64_t o = i64_ord(ts[r]);
+    if (ts[r] != INT64_MIN || base + (uint64_t)r * kPNT + threadIdx.x < b.n) mx = o > mx ? o : mx;
+    if (key[r] == HSG_KEY_NONE) continue;
+    if (ts[r] >= 0) mn = ~o > mn ? ~o : mn;
+    uint64_t k_lo, k_hi;
+    if (!record_windows(p, ts[r], k_lo, k_hi)) continue;
+    int64_t a = (int64_t)k_lo - k_epoch, z = (int64_t)k_hi - k_epoch;
+    if (a < 0) a = 0;
+    if (z > 0xFFFFFFFFll) z = 0xFFFFFFFFll;
+    if (a > z) continue;
+    atomicAdd(&cnt[bucket_of(key[r], pp.np_log2, pp.bshift)], 1u);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t x = __shfl_xor(mx, o, 64), c = __shfl_xor(mn, o, 64);
+    mx = x > mx ? x : mx;
+    mn = c > mn ? c : mn;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sext[0][threadIdx.x >> 6] = mx;
+    sext[1][threadIdx.x >> 6] = mn;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nb; i += kPNT) pb.hist[tile * (uint64_t)nb + i] = cnt[i];
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < kPNT / 64; ++k) {
+      mx = sext[0][k] > mx ? sext[0][k] : mx;
+      mn = sext[1][k] > mn ? sext[1][k] : mn;
+    }
+    if (mx) atomicMax((unsigned long long *)&sc->scratch[21], (unsigned long long)mx);
+    if (mn) atomicMax((unsigned long long *)&sc->scratch[22], (unsigned long long)mn);
+  }
+}
+
 // LDS holds only the tile's bucket sort (bucket, order, window run per record:
 // 12 B) plus per-bucket run starts, so two workgroups fit a CU; the record
 // words are gathered from the (L2-resident) input at write-out, in bucket
@@ -335,8 +397,12 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
 void launch_part_hist(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp, const int64_t *rec_wm,
                       const int64_t *own_wm, const PartBuffers &pb, DevScalars *sc, bool opt) {
   if (!pp.tiles) return;
+  if (opt) {
+    hipLaunchKernelGGL(k_part_hist_opt<kPartTileRecs>, dim3((unsigned)pp.tiles), dim3(kPNT), 0, s, b, p, pp, pb, sc);
+    return;
+  }
   hipLaunchKernelGGL(k_part_hist<kPartTileRecs>, dim3((unsigned)pp.tiles), dim3(kPNT), 0, s, b, p, pp, rec_wm, own_wm,
-                     pb, sc, opt ? 1 : 0);
+                     pb, sc, 0);
 }
 
 // Optimistic path, after the histogram: stream time out, and whether the
