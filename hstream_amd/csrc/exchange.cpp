@@ -88,6 +88,7 @@ int exchange_device_init(OpDevice &d, const hsg_op_config &cfg, uint64_t batch_c
   }
   d.bshift = d.xpart_log2 > 0 ? d.xpart_log2 : 0;
   if (d.bshift + kPartMaxLog2 > 60) d.bshift = 0;
+  d.tw.bshift = d.bshift;  // table regions follow the local buckets
   return HSG_OK;
 }
 

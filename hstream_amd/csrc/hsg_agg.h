@@ -135,9 +135,10 @@ __device__ inline void flush_row_atomic(const Program &prog, int64_t *__restrict
 // in the batch (-> per-batch changelog), else kTouchSkip.
 template <int MS>
 __device__ inline uint32_t flush_window(const Program &prog, const TwParams &p, const TwTable &t, uint64_t g,
-                                        const int64_t (&v)[MS], bool exclusive, uint32_t &fresh, uint32_t &err) {
+                                        const int64_t (&v)[MS], bool exclusive, uint32_t &fresh, uint32_t &err,
+                                        bool plain_claim = false) {
   const uint32_t f0 = fresh;
-  const int64_t slot = tw_find_or_insert(t, g, fresh);
+  const int64_t slot = plain_claim ? tw_claim_exclusive(t, g, fresh) : tw_find_or_insert(t, g, fresh);
   if (slot < 0) {
     err |= ERR_OOM;
     return kTouchSkip;
@@ -257,8 +258,8 @@ struct AggLds {
 // Block-wide: every thread calls. Returns the number of live entries.
 template <int MS, int E, int NT>
 __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const Program &prog, const TwParams &p, const TwTable &t,
-                              const PartBuffers &pb, DevScalars *sc, int S, bool exclusive, uint32_t skip,
-                              int cnt_all_slot, uint32_t &fresh, uint32_t &err, uint64_t &t_sort) {
+                              const PartBuffers &pb, DevScalars *sc, int S, bool exclusive, bool plain_claim,
+                              uint32_t skip, int cnt_all_slot, uint32_t &fresh, uint32_t &err, uint64_t &t_sort) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t SW = S ? (uint32_t)S : 1u;
   const uint64_t t0 = wall_clock64();
@@ -351,7 +352,7 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const Progra
         for (int s = 0; s < MS; ++s)
           if ((skip >> s) & 1u) acc[s] = acc[cnt_all_slot];
       }
-      const uint32_t sl = flush_window<MS>(prog, p, t, kb | w, acc, exclusive, fresh, err);
+      const uint32_t sl = flush_window<MS>(prog, p, t, kb | w, acc, exclusive, fresh, err, plain_claim);
       if (o < pb.touched_cap) pb.touched[o] = sl;
       else err |= ERR_OOM;
       ++o;
@@ -406,6 +407,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const uint64_t b0 = pb.bstart[b], b1 = pb.bstart[b + 1];
   const uint64_t c = blockIdx.x - L.c0;
   const bool exclusive = (L.c1 - L.c0) == 1;
+  // the bucket's table regions are this workgroup's alone (hsg_tw.h)
+  const bool plain_claim = exclusive && pp.np_log2 <= t.rbits && pp.bshift == t.bshift;
   const uint64_t r0 = b0 + c * pp.chunk, r1 = r0 + pp.chunk < b1 ? r0 + pp.chunk : b1;
   const uint32_t limit = (uint32_t)(E * 3 / 4);
   const int W = PK ? pp.words - 1 : pp.words;  // words per record in memory
@@ -506,7 +509,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         if (!more) break;
         // table full with records left: flush and go on (the records are
         // loaded again afterwards, so they hold no registers across the flush)
-        groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, skip, cnt_all_slot, fresh, err, t_sort);
+        groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, plain_claim, skip, cnt_all_slot, fresh, err,
+                                   t_sort);
         ++flushes;
         load();
         ta = wall_clock64();
@@ -528,7 +532,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       }
     }
     const uint64_t tb = wall_clock64();
-    groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, skip, cnt_all_slot, fresh, err, t_sort);
+    groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, plain_claim, skip, cnt_all_slot, fresh, err,
+                                   t_sort);
     ++flushes;
     t_flush += wall_clock64() - tb;
   }

@@ -134,6 +134,9 @@ struct TwTable {
   uint64_t mask;    // cap - 1
   uint32_t stride;  // words per row
   uint32_t blocked; // window-block home slots, probe step 8 (windowed ops with >= 8 slots)
+  uint64_t rmask;   // slots per region - 1 (regions = 2^rbits, see hsg_tw.h)
+  int32_t rbits;    // region bits of the key hash (below the owner bits)
+  int32_t bshift;   // owner bits of the key hash (multi-GPU)
   __host__ __device__ uint64_t *key(uint64_t s) const { return rows + s * stride; }
   __host__ __device__ uint32_t *stamp(uint64_t s) const { return (uint32_t *)(rows + s * stride + 1); }
   __host__ __device__ int64_t *aggs(uint64_t s) const { return (int64_t *)(rows + s * stride + 2); }

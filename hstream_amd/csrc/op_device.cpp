@@ -13,6 +13,7 @@
 #include "hsg_kernels.h"
 #include "hsg_session.h"
 #include "hsg_sort.h"
+#include "hsg_part.h"
 
 namespace hsg {
 
@@ -193,6 +194,13 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
     DTRY(dalloc(&d.tw.rows, d.cap * (uint64_t)d.tw.stride));
     d.tw.mask = d.cap - 1;
     d.tw.blocked = cfg.window_kind != HSG_UNWINDOWED && d.cap >= 64 ? 1u : 0u;
+    // regions of >= 4096 slots (small spread of the per-region load), at
+    // most one per partition bucket
+    int cl = 0;
+    while ((1ull << cl) < d.cap) ++cl;
+    d.tw.rbits = cl - 12 < 0 ? 0 : (cl - 12 > kPartMaxLog2 ? kPartMaxLog2 : cl - 12);
+    d.tw.rmask = (d.cap >> d.tw.rbits) - 1;
+    d.tw.bshift = 0;  // set with the exchange (exchange_device_init)
     uint64_t nb = emit_chunks(d.cap);
     DTRY(dalloc(&d.emit.cnt, nb));
     DTRY(dalloc(&d.emit.off, nb));

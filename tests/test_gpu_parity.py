@@ -119,7 +119,8 @@ def test_configs_reduced(eng, name):
     """The BASELINE configs' window specs and aggregates at sizes the oracle finishes in seconds."""
     cfg = datagen.CONFIGS[name]
     n = {"C1": 1_000_000, "C2": 2_000_000, "C2f": 1_000_000, "C3": 300_000}[name]
-    spec = cfg.spec(abi.HSG_EMIT_PER_BATCH)
+    wpr = -(-cfg.size_ms // cfg.advance_ms) if cfg.window_kind == abi.HSG_HOPPING else 1
+    spec = cfg.spec(abi.HSG_EMIT_PER_BATCH, state_capacity=n * wpr)  # bound on the groups
     batches = []
     bsz = min(n, 1 << 20)
     for s in range(0, n, bsz):
