@@ -3,11 +3,57 @@
 // k_agg_s{2,4,6,8}.hip so the variants compile in parallel. Not ABI.
 #pragma once
 
+#include <initializer_list>
+#include <type_traits>
+
 #include "hsg_dev.h"
 #include "hsg_part.h"
 #include "hsg_tw.h"
 
 namespace hsg {
+
+// ---------------------------------------------------------------------------
+// Slot-program views
+// ---------------------------------------------------------------------------
+// The per-record LDS update dispatches on every slot's op. Read from the
+// runtime Program (ProgRT) that dispatch is a scalar branch chain per slot and
+// record; a program signature baked into the kernel (ProgSig<SIG>) folds it
+// to the slot's one LDS atomic. SIG packs 7 bits per slot, slot 0 lowest:
+// (op + 1) in the low 4 bits, the column in the high 3; 0 ends the program.
+struct ProgRT {
+  const Program &p;
+  __device__ explicit ProgRT(const Program &q) : p(q) {}
+  __device__ int n() const { return p.n_slots; }
+  __device__ int op(int s) const { return p.slot_op[s]; }
+  __device__ int col(int s) const { return p.slot_col[s]; }
+};
+
+template <uint64_t SIG>
+struct ProgSig {
+  static constexpr int count() {
+    int k = 0;
+    while (k < 8 && ((SIG >> (7 * k)) & 15u) != 0) ++k;
+    return k;
+  }
+  __device__ explicit ProgSig(const Program &) {}
+  __device__ constexpr int n() const { return count(); }
+  __device__ constexpr int op(int s) const { return (int)((SIG >> (7 * s)) & 15u) - 1; }
+  __device__ constexpr int col(int s) const { return (int)((SIG >> (7 * s + 4)) & 7u); }
+};
+
+template <uint64_t SIG>
+using ProgView = typename std::conditional<SIG == 0, ProgRT, ProgSig<SIG>>::type;
+
+// signature of a runtime program (0: not expressible)
+inline uint64_t program_sig(const Program &p) {
+  if (p.n_slots > 8) return 0;
+  uint64_t sig = 0;
+  for (int s = 0; s < p.n_slots; ++s) {
+    if (p.slot_op[s] < 0 || p.slot_op[s] > 14 || p.slot_col[s] < 0 || p.slot_col[s] > 7) return 0;
+    sig |= (uint64_t)((p.slot_op[s] + 1) | (p.slot_col[s] << 4)) << (7 * s);
+  }
+  return sig;
+}
 
 // ---------------------------------------------------------------------------
 // LDS aggregation of one chunk
@@ -40,10 +86,10 @@ struct PRec {
 };
 
 // contribution of the record to slot s (identity when absent)
-template <typename R>
-__device__ inline int64_t prec_elem(const Program &prog, int s, const R &r) {
-  const int op = prog.slot_op[s];
-  const int c = prog.slot_col[s];
+template <class PG, typename R>
+__device__ inline int64_t prec_elem(const PG &prog, int s, const R &r) {
+  const int op = prog.op(s);
+  const int c = prog.col(s);
   if (op == S_CNT_ALL) return 1;
   if (op == S_LAST_VAL) return 0;
   if (!r.present(c)) return slot_identity_dev(op);
@@ -64,14 +110,14 @@ __device__ inline int64_t prec_elem(const Program &prog, int s, const R &r) {
 // table's entry count), so the 64 lanes of one atomic instruction spread over
 // the banks (entry-major rows of 48 B hit a quarter of them). `skip`: slots not
 // updated in LDS (COUNT(col) of a batch without validity arrays = COUNT(*)).
-template <int MS, int ST, typename R>
-__device__ inline void lds_apply(const Program &prog, int64_t *__restrict__ row, const R &r, uint32_t skip) {
+template <int MS, int ST, typename R, class PG>
+__device__ inline void lds_apply(const PG &prog, int64_t *__restrict__ row, const R &r, uint32_t skip) {
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
-    if (s >= prog.n_slots) break;
-    const int op = prog.slot_op[s];
+    if (s >= prog.n()) break;
+    const int op = prog.op(s);
     if (op == S_LAST_VAL || ((skip >> s) & 1u)) continue;
-    if (op != S_CNT_ALL && !r.present(prog.slot_col[s])) continue;
+    if (op != S_CNT_ALL && !r.present(prog.col(s))) continue;
     const int64_t x = prec_elem(prog, s, r);
     int64_t *a = row + s * ST;
     unsigned long long *u = (unsigned long long *)a;
@@ -91,12 +137,12 @@ __device__ inline void lds_apply(const Program &prog, int64_t *__restrict__ row,
 }
 
 // a <- a (+) x over the aggregate slots (LAST_SEQ = latest sequence); x strided by ST
-template <int MS, int ST>
-__device__ inline void acc_combine(const Program &prog, int64_t (&a)[MS], const int64_t *x) {
+template <int MS, int ST, class PG>
+__device__ inline void acc_combine(const PG &prog, int64_t (&a)[MS], const int64_t *x) {
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
-    if (s >= prog.n_slots) break;
-    const int op = prog.slot_op[s];
+    if (s >= prog.n()) break;
+    const int op = prog.op(s);
     if (op == S_LAST_VAL) continue;
     const int64_t v = x[s * ST];
     a[s] = op == S_LAST_SEQ ? ((uint64_t)v > (uint64_t)a[s] ? v : a[s]) : slot_combine(op, a[s], v);
@@ -104,12 +150,12 @@ __device__ inline void acc_combine(const Program &prog, int64_t (&a)[MS], const 
 }
 
 // HBM-side atomic combine of a row of partial aggregates (v) into `row`.
-template <int MS>
-__device__ inline void flush_row_atomic(const Program &prog, int64_t *__restrict__ row, const int64_t (&v)[MS]) {
+template <int MS, class PG>
+__device__ inline void flush_row_atomic(const PG &prog, int64_t *__restrict__ row, const int64_t (&v)[MS]) {
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
-    if (s >= prog.n_slots) break;
-    const int op = prog.slot_op[s];
+    if (s >= prog.n()) break;
+    const int op = prog.op(s);
     const int64_t x = v[s];
     if (op == S_LAST_VAL || x == slot_identity_dev(op)) continue;  // nothing to add
     unsigned long long *u = (unsigned long long *)(row + s);
@@ -133,8 +179,8 @@ __device__ inline void flush_row_atomic(const Program &prog, int64_t *__restrict
 // read-modify-write suffices (agent-scope loads, served by L2 not L1: this
 // workgroup's own atomics may have updated the row). Returns the slot when this is the group's first update
 // in the batch (-> per-batch changelog), else kTouchSkip.
-template <int MS>
-__device__ inline uint32_t flush_window(const Program &prog, const TwParams &p, const TwTable &t, uint64_t g,
+template <int MS, class PG>
+__device__ inline uint32_t flush_window(const PG &prog, const TwParams &p, const TwTable &t, uint64_t g,
                                         const int64_t (&v)[MS], bool exclusive, uint32_t &fresh, uint32_t &err,
                                         bool plain_claim = false) {
   const uint32_t f0 = fresh;
@@ -151,19 +197,19 @@ __device__ inline uint32_t flush_window(const Program &prog, const TwParams &p, 
     // inserted just now by the group's only writer: the row holds identities
 #pragma unroll
     for (int s = 0; s < MS; ++s)
-      if (s < prog.n_slots && prog.slot_op[s] != S_LAST_VAL) row[s] = v[s];
+      if (s < prog.n() && prog.op(s) != S_LAST_VAL) row[s] = v[s];
     *stp = bid;
     first = true;
   } else if (exclusive) {
     int64_t cur[MS];
 #pragma unroll
     for (int s = 0; s < MS; ++s)
-      cur[s] = s < prog.n_slots ? __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+      cur[s] = s < prog.n() ? __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
     const uint32_t st = __hip_atomic_load(stp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int s = 0; s < MS; ++s) {
-      if (s >= prog.n_slots) break;
-      const int op = prog.slot_op[s];
+      if (s >= prog.n()) break;
+      const int op = prog.op(s);
       if (op == S_LAST_VAL || v[s] == slot_identity_dev(op)) continue;
       row[s] = op == S_LAST_SEQ ? ((uint64_t)v[s] > (uint64_t)cur[s] ? v[s] : cur[s]) : slot_combine(op, cur[s], v[s]);
     }
@@ -185,13 +231,13 @@ __device__ inline void touch_append(const PartBuffers &pb, DevScalars *sc, uint3
 
 // Windows [w0, w1] of one record straight into the HBM table (records whose
 // earliest windows were rejected by grace, and LDS overflow in fan-out mode).
-template <int MS, typename R>
-__device__ inline void direct_windows(const Program &prog, const TwParams &p, const TwTable &t, const PartBuffers &pb,
+template <int MS, typename R, class PG>
+__device__ inline void direct_windows(const PG &prog, const TwParams &p, const TwTable &t, const PartBuffers &pb,
                                       DevScalars *sc, uint32_t key, uint32_t w0, uint32_t w1, const R &r,
                                       uint32_t &fresh, uint32_t &err) {
   int64_t v[MS];
 #pragma unroll
-  for (int s = 0; s < MS; ++s) v[s] = s < prog.n_slots ? prec_elem(prog, s, r) : 0;
+  for (int s = 0; s < MS; ++s) v[s] = s < prog.n() ? prec_elem(prog, s, r) : 0;
   for (uint32_t w = w0;; ++w) {
     touch_append(pb, sc, flush_window<MS>(prog, p, t, ((uint64_t)key << 32) | w, v, false, fresh, err), err);
     if (w == w1) break;
@@ -256,8 +302,8 @@ struct AggLds {
 
 // Flush every live entry of the table as window updates, then clear it.
 // Block-wide: every thread calls. Returns the number of live entries.
-template <int MS, int E, int NT>
-__device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const Program &prog, const TwParams &p, const TwTable &t,
+template <int MS, int E, int NT, class PG>
+__device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const PG &prog, const TwParams &p, const TwTable &t,
                               const PartBuffers &pb, DevScalars *sc, int S, bool exclusive, bool plain_claim,
                               uint32_t skip, int cnt_all_slot, uint32_t &fresh, uint32_t &err, uint64_t &t_sort) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -366,7 +412,7 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const Progra
     const int e = L.live[q];
     L.key[e] = kEmpty;
 #pragma unroll
-    for (int s = 0; s < MS; ++s) L.agg[s * E + e] = s < prog.n_slots ? slot_identity_dev(prog.slot_op[s]) : 0;
+    for (int s = 0; s < MS; ++s) L.agg[s * E + e] = s < prog.n() ? slot_identity_dev(prog.op(s)) : 0;
   }
   if (threadIdx.x == 0) {
     L.fill = 0;
@@ -377,10 +423,11 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const Progra
 }
 
 // 4 waves per SIMD: two 512-thread or one 1024-thread workgroup per CU (<= 128 VGPRs)
-template <int MS, int E, int WMAX, int RPT, int NT, bool FAN, bool PK>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_part_agg(Program prog, TwParams p, PartParams pp, TwTable t,
+template <int MS, int E, int WMAX, int RPT, int NT, bool FAN, bool PK, uint64_t SIG>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_part_agg(Program prog_, TwParams p, PartParams pp, TwTable t,
                                                             PartBuffers pb, DevScalars *sc) {
   __shared__ AggLds<MS, E, NT> L;
+  const ProgView<SIG> prog(prog_);
   if (sc->redo) return;  // uniform: the optimistic pass found late records
   if ((sc->packed != 0) != PK) return;  // uniform: the other layout's variant runs
   constexpr int SUB = NT * RPT;
@@ -399,7 +446,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   for (int e = threadIdx.x; e < E; e += NT) {
     L.key[e] = kEmpty;
 #pragma unroll
-    for (int s = 0; s < MS; ++s) L.agg[s * E + e] = s < prog.n_slots ? slot_identity_dev(prog.slot_op[s]) : 0;
+    for (int s = 0; s < MS; ++s) L.agg[s * E + e] = s < prog.n() ? slot_identity_dev(prog.op(s)) : 0;
   }
   __syncthreads();
   if (blockIdx.x >= chunk_start[nb]) return;  // uniform: the grid is an upper bound
@@ -419,11 +466,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   // without validity arrays COUNT(col) = COUNT(*): derive those slots at flush
   int cnt_all_slot = -1;
   uint32_t skip = 0;
-  for (int s = 0; s < prog.n_slots && s < MS; ++s)
-    if (prog.slot_op[s] == S_CNT_ALL && cnt_all_slot < 0) cnt_all_slot = s;
+  for (int s = 0; s < prog.n() && s < MS; ++s)
+    if (prog.op(s) == S_CNT_ALL && cnt_all_slot < 0) cnt_all_slot = s;
   if (!pp.has_valid && cnt_all_slot >= 0)
-    for (int s = 0; s < prog.n_slots && s < MS; ++s)
-      if (prog.slot_op[s] == S_CNT) skip |= 1u << s;
+    for (int s = 0; s < prog.n() && s < MS; ++s)
+      if (prog.op(s) == S_CNT) skip |= 1u << s;
   const int64_t k_epoch = sc->k_epoch;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint64_t pairs = 0, groups = 0, t_rec = 0, t_flush = 0, t_sort = 0, flushes = 0;
@@ -571,13 +618,46 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // Aggregation variants: small = E_s entries and 512 threads (two workgroups per
 // CU), big = E_l entries and 1024 threads (one per CU). Records per thread
 // keep the record queue within 128 VGPRs.
-template <int MS, int E, int NT, int WM, int RPT, bool FAN>
+template <int MS, int E, int NT, int WM, int RPT, bool FAN, uint64_t SIG = 0>
 static void agg_launch_pk(hipStream_t s, dim3 g, bool maybe_packed, const Program &prog, const TwParams &p,
                           const PartParams &pp, const TwTable &t, const PartBuffers &pb, DevScalars *sc) {
   const dim3 th(NT);
-  hipLaunchKernelGGL((k_part_agg<MS, E, WM, RPT, NT, FAN, false>), g, th, 0, s, prog, p, pp, t, pb, sc);
+  hipLaunchKernelGGL((k_part_agg<MS, E, WM, RPT, NT, FAN, false, SIG>), g, th, 0, s, prog, p, pp, t, pb, sc);
   if (maybe_packed)  // the layout is decided on the device: the variant not chosen exits at once
-    hipLaunchKernelGGL((k_part_agg<MS, E, WM - 1, RPT, NT, FAN, true>), g, th, 0, s, prog, p, pp, t, pb, sc);
+    hipLaunchKernelGGL((k_part_agg<MS, E, WM - 1, RPT, NT, FAN, true, SIG>), g, th, 0, s, prog, p, pp, t, pb, sc);
+}
+
+// Aggregate sets with a kernel specialised on their slot program (ProgSig):
+// the SQL aggregates over one numeric column that a windowed GROUP BY most
+// often asks for. Every other program runs the runtime-program kernel.
+constexpr uint64_t sig_ops(std::initializer_list<int> ops) {
+  uint64_t sig = 0;
+  int k = 0;
+  for (int op : ops) sig |= (uint64_t)(op + 1) << (7 * k++);
+  return sig;
+}
+// COUNT(*), SUM, AVG, MIN, MAX of an i64 / f64 column
+constexpr uint64_t kSigAllI = sig_ops({S_CNT_ALL, S_SUM_I, S_CNT, S_MIN_I, S_MAX_I});
+constexpr uint64_t kSigAllF = sig_ops({S_CNT_ALL, S_SUM_F, S_CNT, S_MIN_F, S_MAX_F});
+// COUNT(*); COUNT(*), SUM; SUM, MAX
+constexpr uint64_t kSigCnt = sig_ops({S_CNT_ALL});
+constexpr uint64_t kSigCntSumI = sig_ops({S_CNT_ALL, S_SUM_I});
+constexpr uint64_t kSigCntSumF = sig_ops({S_CNT_ALL, S_SUM_F});
+constexpr uint64_t kSigSumMaxI = sig_ops({S_SUM_I, S_MAX_I});
+
+// the state-slot class (k_agg_s{2,4,6,8}.hip) a program of n slots runs in
+constexpr int ms_class(int n) { return n <= 2 ? 2 : n <= 4 ? 4 : n <= 6 ? 6 : 8; }
+
+template <int MS, int E, int NT, int RPT, uint64_t SIG>
+static bool agg_launch_sig(uint64_t sig, hipStream_t s, dim3 g, bool mp, const Program &prog, const TwParams &p,
+                           const PartParams &pp, const TwTable &t, const PartBuffers &pb, DevScalars *sc) {
+  if constexpr (ms_class(ProgSig<SIG>::count()) != MS) {
+    return false;
+  } else {
+    if (sig != SIG) return false;
+    agg_launch_pk<MS, E, NT, 3, RPT, false, SIG>(s, g, mp, prog, p, pp, t, pb, sc);
+    return true;
+  }
 }
 
 template <int MS, int E, int NT, int RPT4>
@@ -589,8 +669,18 @@ static void agg_launch_v(hipStream_t s, dim3 g, int W, bool mp, const Program &p
     agg_launch_pk<MS, E, NT, kPartMaxWords, R11, true>(s, g, mp, prog, p, pp, t, pb, sc);
     return;
   }
-  if (W <= 3) agg_launch_pk<MS, E, NT, 3, RPT4, false>(s, g, mp, prog, p, pp, t, pb, sc);
-  else if (W <= 4) agg_launch_pk<MS, E, NT, 4, RPT4, false>(s, g, mp, prog, p, pp, t, pb, sc);
+  if (W <= 3) {
+    // records of at most one column: a specialised slot program if there is one
+    const uint64_t sig = program_sig(prog);
+    if (agg_launch_sig<MS, E, NT, RPT4, kSigAllI>(sig, s, g, mp, prog, p, pp, t, pb, sc) ||
+        agg_launch_sig<MS, E, NT, RPT4, kSigAllF>(sig, s, g, mp, prog, p, pp, t, pb, sc) ||
+        agg_launch_sig<MS, E, NT, RPT4, kSigCnt>(sig, s, g, mp, prog, p, pp, t, pb, sc) ||
+        agg_launch_sig<MS, E, NT, RPT4, kSigCntSumI>(sig, s, g, mp, prog, p, pp, t, pb, sc) ||
+        agg_launch_sig<MS, E, NT, RPT4, kSigCntSumF>(sig, s, g, mp, prog, p, pp, t, pb, sc) ||
+        agg_launch_sig<MS, E, NT, RPT4, kSigSumMaxI>(sig, s, g, mp, prog, p, pp, t, pb, sc))
+      return;
+    agg_launch_pk<MS, E, NT, 3, RPT4, false>(s, g, mp, prog, p, pp, t, pb, sc);
+  } else if (W <= 4) agg_launch_pk<MS, E, NT, 4, RPT4, false>(s, g, mp, prog, p, pp, t, pb, sc);
   else if (W <= 6) agg_launch_pk<MS, E, NT, 6, R6, false>(s, g, mp, prog, p, pp, t, pb, sc);
   else agg_launch_pk<MS, E, NT, kPartMaxWords, R11, false>(s, g, mp, prog, p, pp, t, pb, sc);
 }
