@@ -91,8 +91,7 @@ int build_program(const hsg_op_config &cfg, const std::vector<int32_t> &col_type
         kind = isf ? O_AVG_F : O_AVG_I;
         break;
       case HSG_LAST: {
-        if (cfg.window_kind == HSG_SESSION)
-          return fail(err, HSG_E_INVALID, "HSG_LAST is not supported for session windows");
+        // sessions: merges keep the existing session's value (k_session.hip)
         int s = find_slot(S_LAST_SEQ, c);
         if (s < 0) {
           if (prog.n_slots + 2 > kMaxSlots) return fail(err, HSG_E_INVALID, "too many state slots");

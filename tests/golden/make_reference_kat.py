@@ -27,7 +27,7 @@ cases.append({
     "sql": "SELECT a, b, SUM(a) FROM s3 GROUP BY b, SESSION(INTERVAL 10 MINUTE) EMIT CHANGES;",
     "op": {"window_kind": SESSION, "emit_mode": PER_RECORD, "gap_ms": 600000,
            "col_types": [I64], "aggs": [[SUM, 0]]},
-    "note": "passthrough a/b columns are constant here; session passthrough is not modelled (HSG_LAST is time-window only)",
+    "note": "passthrough a/b columns are constant here; session passthrough (HSG_LAST, merge keeps the existing session value) is covered by the seeded session parity tests",
     "batch": {"key_id": [0, 0, 0, 0], "ts": [1000, 1250, 1500, 1750], "cols": [[1, 1, 1, 1]]},
     "expect_changelog_aggs": [[1], [2], [3], [4]],
 })

@@ -72,6 +72,20 @@ def test_time_windows_messy_batches(eng, spec):
     _drive(eng, spec, batches)
 
 
+@pytest.mark.parametrize("gap", [0, 700, 2_000])
+@pytest.mark.parametrize("mode", [abi.HSG_EMIT_PER_BATCH, abi.HSG_EMIT_NONE, abi.HSG_EMIT_PER_RECORD])
+def test_session_messy_batches(eng, mode, gap):
+    """Sessions with passthrough (LAST) columns: a point that merges into
+    existing sessions takes the last overlapped session's value
+    (aggregateMergeF _ _ o2, Codegen.hs:467; SessionWindowedStream.hs:99-115)."""
+    spec = OpSpec(abi.HSG_SESSION, mode, gap_ms=gap, col_types=[abi.HSG_I64, abi.HSG_F64], aggs=ALL_AGG_SETS["mixed"])
+    batches = []
+    for bi in range(3):
+        batches.append(gen_small(3000 + bi, 5000, 37, col_types=spec.col_types, span=100_000,
+                                 base=10_000_000 + bi * 60_000))
+    _drive(eng, spec, batches)
+
+
 @pytest.mark.parametrize("mode", [abi.HSG_EMIT_PER_BATCH, abi.HSG_EMIT_PER_RECORD])
 def test_edge_batches(eng, mode):
     spec = OpSpec(abi.HSG_HOPPING, mode, size_ms=7, advance_ms=3, col_types=[abi.HSG_I64],
@@ -244,7 +258,7 @@ def _x_specs():
     out = []
     for kind, kw in ((abi.HSG_TUMBLING, dict(size_ms=10_000)), (abi.HSG_HOPPING, dict(size_ms=10_000, advance_ms=3_000)),
                      (abi.HSG_UNWINDOWED, {}), (abi.HSG_SESSION, dict(gap_ms=2_000))):
-        aggs = [a for a in ALL_AGG_SETS["mixed"] if not (kind == abi.HSG_SESSION and a[0] == abi.HSG_LAST)]
+        aggs = ALL_AGG_SETS["mixed"]
         for mode in (abi.HSG_EMIT_PER_BATCH, abi.HSG_EMIT_PER_RECORD, abi.HSG_EMIT_NONE):
             out.append(pytest.param(OpSpec(kind, mode, col_types=[abi.HSG_I64, abi.HSG_F64], aggs=aggs, **kw),
                                     id=f"k{kind}-m{mode}"))

@@ -60,10 +60,7 @@ def _specs():
                          (abi.HSG_HOPPING, dict(size_ms=10_000, advance_ms=3_000)),
                          (abi.HSG_UNWINDOWED, {}),
                          (abi.HSG_SESSION, dict(gap_ms=2_000))):
-            if kind == abi.HSG_SESSION:
-                aggs_k = [a for a in aggs if a[0] != abi.HSG_LAST]
-            else:
-                aggs_k = aggs
+            aggs_k = aggs
             for mode in (abi.HSG_EMIT_PER_RECORD, abi.HSG_EMIT_PER_BATCH):
                 out.append(pytest.param(OpSpec(kind, mode, col_types=col_types, aggs=aggs_k, **kw),
                                         id=f"{aggname}-k{kind}-m{mode}"))

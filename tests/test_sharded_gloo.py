@@ -56,7 +56,7 @@ SPECS = {
     "tumbling_batch": OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=10_000,
                              col_types=[abi.HSG_I64, abi.HSG_F64], aggs=ALL_AGG_SETS["mixed"]),
     "session": OpSpec(abi.HSG_SESSION, abi.HSG_EMIT_PER_RECORD, gap_ms=2_000, col_types=[abi.HSG_I64, abi.HSG_F64],
-                      aggs=[a for a in ALL_AGG_SETS["mixed"] if a[0] != abi.HSG_LAST]),
+                      aggs=ALL_AGG_SETS["mixed"]),
 }
 
 
