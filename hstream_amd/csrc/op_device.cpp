@@ -416,15 +416,18 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
   // the stream-time inputs into the histogram pass and decide afterwards (one
   // tiny kernel); a batch that does have late records is run again with the
   // per-record stream time. Needs the window epoch (set by an earlier batch).
-  const bool opt = d.use_part && !rec_wm && !has_last(prog) && d.h_sc->epoch_set && cfg.grace_ms >= 0 &&
-                   cfg.window_kind != HSG_SESSION;
+  // The first batch after create/reset has no epoch yet: the stream-time pass
+  // sets it (device side) ahead of the optimistic kernels, which then run as on
+  // every later batch instead of the per-record stream-time path.
+  const bool opt = d.use_part && !rec_wm && !has_last(prog) && cfg.grace_ms >= 0 && cfg.window_kind != HSG_SESSION;
+  const bool need_epoch = !d.h_sc->epoch_set;
   auto run = [&](bool optimistic) -> int {
     int rc = clear_batch_scalars(d, err);
     if (rc != HSG_OK) return rc;
     if (!kb.n) return HSG_OK;
     // stream time (and the window epoch on the first batch); after a key exchange
     // the per-record stream time arrives in rec_wm and only the epoch is used
-    if (!optimistic) launch_stream_time(d, cfg, kb, a.wm_in, p.adv);
+    if (!optimistic || need_epoch) launch_stream_time(d, cfg, kb, a.wm_in, p.adv);
     DTRY(hipEventRecord(d.ev_a, d.stream));
     if (d.use_part) {
       PartParams pp;
