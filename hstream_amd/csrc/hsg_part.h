@@ -32,6 +32,7 @@ struct PartBuffers {
   uint32_t *touched;      // [touched_cap] one entry per HBM window update: the slot on the group's first
                           // update in the batch, else kTouchSkip (length: sc->scratch[1])
   uint64_t touched_cap;   // records x windows per record: bounds the updates of one batch
+  uint64_t *text;         // [2 * tiles] optimistic histogram: per-tile ts extrema images for the decide step
   uint32_t *tcnt;         // [touch_chunks] emit: non-skip entries per chunk
   uint64_t *toff;         // [touch_chunks + 1] exclusive prefix
   uint64_t *tpartial;     // scan partials
@@ -67,7 +68,7 @@ void launch_part_recwm(hipStream_t s, const Batch &b, const int64_t *tprefix, co
 void launch_part_hist(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp, const int64_t *rec_wm,
                       const int64_t *own_wm, const PartBuffers &pb, DevScalars *sc, bool opt);
 void launch_part_decide(hipStream_t s, DevScalars *sc, const TwParams &p, int64_t wm_in, int64_t grace,
-                        bool can_pack);
+                        bool can_pack, const PartBuffers &pb, uint64_t tiles);
 // bucket-major run offsets (offt, bstart) from the tile-major histogram
 void launch_part_offsets(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc);
 uint32_t part_nseg(uint64_t tiles);

@@ -189,8 +189,10 @@ __global__ __launch_bounds__(kPNT) void k_part_hist(Batch b, TwParams p, PartPar
       mx = sext[0][k] > mx ? sext[0][k] : mx;
       mn = sext[1][k] > mn ? sext[1][k] : mn;
     }
-    if (mx) atomicMax((unsigned long long *)&sc->scratch[21], (unsigned long long)mx);
-    if (mn) atomicMax((unsigned long long *)&sc->scratch[22], (unsigned long long)mn);
+    // per-tile slots, reduced by k_part_decide (one contended device-scope
+    // atomic per workgroup would serialise thousands of workgroups)
+    pb.text[2 * tile] = mx;
+    pb.text[2 * tile + 1] = mn;
   }
   // tile-major counts: one contiguous row per tile (k_part_colsum / colscan
   // turn them into bucket-major offsets)
@@ -286,8 +288,10 @@ __global__ __launch_bounds__(kPNT) void k_part_hist_opt(Batch b, TwParams p, Par
       mx = sext[0][k] > mx ? sext[0][k] : mx;
       mn = sext[1][k] > mn ? sext[1][k] : mn;
     }
-    if (mx) atomicMax((unsigned long long *)&sc->scratch[21], (unsigned long long)mx);
-    if (mn) atomicMax((unsigned long long *)&sc->scratch[22], (unsigned long long)mn);
+    // per-tile slots, reduced by k_part_decide (one contended device-scope
+    // atomic per workgroup would serialise thousands of workgroups)
+    pb.text[2 * tile] = mx;
+    pb.text[2 * tile + 1] = mn;
   }
 }
 
@@ -433,9 +437,34 @@ void launch_part_hist(hipStream_t s, const Batch &b, const TwParams &p, const Pa
 // kernel of the batch exits and the host runs the batch again carefully.
 // Also picks the packed record layout when every record's first window lies
 // within 2^16 windows of the batch's earliest (kbase).
-__global__ void k_part_decide(DevScalars *sc, TwParams p, int64_t wm_in, int64_t grace, int can_pack) {
+__global__ __launch_bounds__(256) void k_part_decide(DevScalars *sc, TwParams p, int64_t wm_in, int64_t grace,
+                                                    int can_pack, const uint64_t *__restrict__ text, uint64_t tiles) {
+  __shared__ uint64_t sred[2][4];
+  uint64_t tx = 0, tn = 0;
+  for (uint64_t t = threadIdx.x; t < tiles; t += 256) {
+    const uint64_t a = text[2 * t], c = text[2 * t + 1];
+    tx = a > tx ? a : tx;
+    tn = c > tn ? c : tn;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t a = __shfl_xor(tx, o, 64), c = __shfl_xor(tn, o, 64);
+    tx = a > tx ? a : tx;
+    tn = c > tn ? c : tn;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sred[0][threadIdx.x >> 6] = tx;
+    sred[1][threadIdx.x >> 6] = tn;
+  }
+  __syncthreads();
   if (threadIdx.x != 0) return;
-  const uint64_t mx = sc->scratch[21], mn = sc->scratch[22];
+  // scratch[21/22] may already hold extrema from an exchange step; the batch's
+  // tiles add theirs
+  uint64_t mx = sc->scratch[21], mn = sc->scratch[22];
+  for (int k = 0; k < 4; ++k) {
+    mx = sred[0][k] > mx ? sred[0][k] : mx;
+    mn = sred[1][k] > mn ? sred[1][k] : mn;
+  }
   const int64_t bmax = mx ? (int64_t)(mx ^ 0x8000000000000000ull) : INT64_MIN;
   const int64_t amin = mn ? (int64_t)(~mn ^ 0x8000000000000000ull) : INT64_MAX;
   const int64_t all = bmax > wm_in ? bmax : wm_in;
@@ -460,8 +489,8 @@ __global__ void k_part_decide(DevScalars *sc, TwParams p, int64_t wm_in, int64_t
 }
 
 void launch_part_decide(hipStream_t s, DevScalars *sc, const TwParams &p, int64_t wm_in, int64_t grace,
-                        bool can_pack) {
-  hipLaunchKernelGGL(k_part_decide, dim3(1), dim3(64), 0, s, sc, p, wm_in, grace, can_pack ? 1 : 0);
+                        bool can_pack, const PartBuffers &pb, uint64_t tiles) {
+  hipLaunchKernelGGL(k_part_decide, dim3(1), dim3(256), 0, s, sc, p, wm_in, grace, can_pack ? 1 : 0, pb.text, tiles);
 }
 
 // Staged scatter for packed records of <= 2 words (<= 1 column, no LAST): the

@@ -230,6 +230,10 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
       if (adv > 0) d.pane_S = (cfg.size_ms % adv == 0 && cfg.size_ms / adv <= 64) ? (int)(cfg.size_ms / adv) : 0;
       rc = part_device_init(d, cfg, prog, err);
       if (rc != HSG_OK) return rc;
+      // per-tile ts extrema of the optimistic histogram: 2 words per partition
+      // tile fit the stream-time tile maxima (4x as many tiles)
+      static_assert(kTileRecords * 2 <= kPartTileRecs, "tile extrema buffer");
+      d.part.text = (uint64_t *)d.tile_max;
     }
   }
   if (sharded) {
@@ -448,7 +452,7 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       launch_part_hist(d.stream, kb, p, pp, rec_wm, d.part.wm, d.part, d.sc, optimistic);
       static const bool nopack = getenv("HSG_NOPACK") != nullptr;  // timing studies
       const bool can_pack = optimistic && !nopack && cfg.n_cols <= 8 && d.wpr < 256;
-      if (optimistic) launch_part_decide(d.stream, d.sc, p, a.wm_in, cfg.grace_ms, can_pack);
+      if (optimistic) launch_part_decide(d.stream, d.sc, p, a.wm_in, cfg.grace_ms, can_pack, d.part, pp.tiles);
       launch_part_offsets(d.stream, pp, d.part, d.sc);
       launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc, can_pack);
       launch_part_agg(d.stream, prog, p, pp, d.tw, d.part, kb.n, d.sc, can_pack);
