@@ -141,13 +141,13 @@ static int push_sharded_fast(OpDevice &d, const hsg_op_config &cfg, const Progra
   rc = clear_batch_scalars(d, err);
   if (rc != HSG_OK) return rc;
   // 1. owner counts per tile (+ ts extrema), owner-major run offsets, facts
-  launch_x_hist(s, kb, xl, unwin, d.part.hist, d.sc);
+  launch_x_hist(s, kb, xl, unwin, d.part.hist, d.part.text, d.sc);
   PartParams xp;
   memset(&xp, 0, sizeof(xp));
   xp.np_log2 = xl;
   xp.tiles = x_tiles(n);
   launch_part_offsets(s, xp, d.part, d.sc);
-  launch_x_info(s, d.sc, d.part.bstart, xl, (uint32_t)G, n, has_valid, x.info);
+  launch_x_info(s, d.sc, d.part.bstart, xl, (uint32_t)G, n, has_valid, x.info, d.part.text, x_tiles(n));
   // 2. all-gather the per-rank facts
   NTRY(ncclAllGather(x.info, x.info_all, IW, ncclInt64, comm, s));
   DTRY(hipMemcpyAsync(x.h_info, x.info_all, (uint64_t)G * IW * 8, hipMemcpyDeviceToHost, s));

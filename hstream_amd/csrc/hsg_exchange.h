@@ -56,9 +56,9 @@ struct XCols {
 
 uint64_t x_tiles(uint64_t n);
 // xl = log2 of the owner partitions (ranks, or more when a test partitions finer)
-void launch_x_hist(hipStream_t s, const Batch &b, int xl, bool unwin, uint32_t *hist, DevScalars *sc);
-void launch_x_info(hipStream_t s, const DevScalars *sc, const uint64_t *bstart, int xl, uint32_t G, uint64_t n,
-                   bool has_valid, int64_t *info);
+void launch_x_hist(hipStream_t s, const Batch &b, int xl, bool unwin, uint32_t *hist, uint64_t *text, DevScalars *sc);
+void launch_x_info(hipStream_t s, DevScalars *sc, const uint64_t *bstart, int xl, uint32_t G, uint64_t n,
+                   bool has_valid, int64_t *info, const uint64_t *text, uint64_t tiles);
 void launch_x_scatter(hipStream_t s, const Batch &b, int xl, bool unwin, bool write_valid, int ncols,
                       const uint32_t *offt, const XCols &send);
 

@@ -138,7 +138,7 @@ __device__ inline bool x_sends(const Batch &b, uint64_t i, bool unwin) {
 
 // tile-major owner counts hist[tile][P] + the ts extrema (scratch[21..22] images)
 __global__ __launch_bounds__(kXNT) void k_x_hist(Batch b, int xl, int unwin, uint32_t *hist, uint64_t tiles,
-                                                 DevScalars *sc) {
+                                                 uint64_t *text) {
   __shared__ uint32_t cnt[kMaxRanks];
   __shared__ uint64_t sext[2][kXNT / 64];
   const uint32_t P = 1u << xl;
@@ -173,16 +173,33 @@ __global__ __launch_bounds__(kXNT) void k_x_hist(Batch b, int xl, int unwin, uin
       mx = sext[0][k] > mx ? sext[0][k] : mx;
       mn = sext[1][k] > mn ? sext[1][k] : mn;
     }
-    if (mx) atomicMax((unsigned long long *)&sc->scratch[21], (unsigned long long)mx);
-    if (mn) atomicMax((unsigned long long *)&sc->scratch[22], (unsigned long long)mn);
+    // per-tile slots, reduced by k_x_info (no contended device-scope atomics)
+    text[2 * blockIdx.x] = mx;
+    text[2 * blockIdx.x + 1] = mn;
   }
 }
 
 // this rank's facts for the all-gather: [max ts, min keyed ts, n, has_valid, per-rank counts]
-__global__ void k_x_info(const DevScalars *sc, const uint64_t *bstart, int xl, uint32_t G, uint64_t n, int has_valid,
-                         int64_t *info) {
+__global__ void k_x_info(DevScalars *sc, const uint64_t *bstart, int xl, uint32_t G, uint64_t n, int has_valid,
+                         int64_t *info, const uint64_t *__restrict__ text, uint64_t tiles) {
+  uint64_t tx = 0, tn = 0;
+  for (uint64_t t = threadIdx.x; t < tiles; t += 64) {
+    const uint64_t a = text[2 * t], c = text[2 * t + 1];
+    tx = a > tx ? a : tx;
+    tn = c > tn ? c : tn;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t a = __shfl_xor(tx, o, 64), c = __shfl_xor(tn, o, 64);
+    tx = a > tx ? a : tx;
+    tn = c > tn ? c : tn;
+  }
   if (threadIdx.x != 0) return;
-  const uint64_t mx = sc->scratch[21], mn = sc->scratch[22];
+  uint64_t mx = sc->scratch[21], mn = sc->scratch[22];
+  mx = tx > mx ? tx : mx;
+  mn = tn > mn ? tn : mn;
+  sc->scratch[21] = mx;  // as the per-workgroup atomics left them before
+  sc->scratch[22] = mn;
   info[0] = mx ? (int64_t)(mx ^ 0x8000000000000000ull) : INT64_MIN;
   info[1] = mn ? (int64_t)(~mn ^ 0x8000000000000000ull) : INT64_MAX;
   info[2] = (int64_t)n;
@@ -222,14 +239,14 @@ __global__ __launch_bounds__(kXNT) void k_x_scatter(Batch b, int xl, int unwin, 
 
 uint64_t x_tiles(uint64_t n) { return (n + kXT - 1) / kXT; }
 
-void launch_x_hist(hipStream_t s, const Batch &b, int xl, bool unwin, uint32_t *hist, DevScalars *sc) {
+void launch_x_hist(hipStream_t s, const Batch &b, int xl, bool unwin, uint32_t *hist, uint64_t *text, DevScalars *) {
   const uint64_t tiles = x_tiles(b.n);
   if (tiles)
-    hipLaunchKernelGGL(k_x_hist, dim3((unsigned)tiles), dim3(kXNT), 0, s, b, xl, unwin ? 1 : 0, hist, tiles, sc);
+    hipLaunchKernelGGL(k_x_hist, dim3((unsigned)tiles), dim3(kXNT), 0, s, b, xl, unwin ? 1 : 0, hist, tiles, text);
 }
-void launch_x_info(hipStream_t s, const DevScalars *sc, const uint64_t *bstart, int xl, uint32_t G, uint64_t n,
-                   bool has_valid, int64_t *info) {
-  hipLaunchKernelGGL(k_x_info, dim3(1), dim3(64), 0, s, sc, bstart, xl, G, n, has_valid ? 1 : 0, info);
+void launch_x_info(hipStream_t s, DevScalars *sc, const uint64_t *bstart, int xl, uint32_t G, uint64_t n,
+                   bool has_valid, int64_t *info, const uint64_t *text, uint64_t tiles) {
+  hipLaunchKernelGGL(k_x_info, dim3(1), dim3(64), 0, s, sc, bstart, xl, G, n, has_valid ? 1 : 0, info, text, tiles);
 }
 void launch_x_scatter(hipStream_t s, const Batch &b, int xl, bool unwin, bool write_valid, int ncols,
                       const uint32_t *offt, const XCols &send) {

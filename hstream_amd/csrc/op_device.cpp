@@ -178,6 +178,10 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
   DTRY(dalloc(&d.tile_max, d.n_tiles_cap));
   DTRY(dalloc(&d.tile_min, d.n_tiles_cap));
   DTRY(dalloc(&d.tile_prefix, d.n_tiles_cap));
+  // per-tile ts extrema of the optimistic and exchange histograms (4096-record
+  // tiles, 2 words each) share the stream-time tile maxima (1024-record tiles)
+  static_assert(kTileRecords * 2 <= kPartTileRecs, "tile extrema buffer");
+  d.part.text = (uint64_t *)d.tile_max;
   DTRY(dalloc(&d.st_key, d.batch_cap));
   DTRY(dalloc(&d.st_ts, d.batch_cap));
   for (int c = 0; c < cfg.n_cols; ++c) {
@@ -230,10 +234,6 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
       if (adv > 0) d.pane_S = (cfg.size_ms % adv == 0 && cfg.size_ms / adv <= 64) ? (int)(cfg.size_ms / adv) : 0;
       rc = part_device_init(d, cfg, prog, err);
       if (rc != HSG_OK) return rc;
-      // per-tile ts extrema of the optimistic histogram: 2 words per partition
-      // tile fit the stream-time tile maxima (4x as many tiles)
-      static_assert(kTileRecords * 2 <= kPartTileRecs, "tile extrema buffer");
-      d.part.text = (uint64_t *)d.tile_max;
     }
   }
   if (sharded) {
