@@ -97,6 +97,7 @@ class hsg_batch(C.Structure):
         ("ts", C.c_void_p),
         ("cols", C.POINTER(C.c_void_p)),
         ("valid", C.POINTER(C.c_void_p)),
+        ("ready_event", C.c_void_p),
     ]
 
 
@@ -130,6 +131,10 @@ class hsg_stats(C.Structure):
         ("exchange_bytes", C.c_uint64),
         ("pairs_total", C.c_uint64),
         ("touched_total", C.c_uint64),
+        ("state_slots", C.c_uint64),
+        ("state_row_bytes", C.c_uint64),
+        ("spilled_rows", C.c_uint64),
+        ("spill_events", C.c_uint64),
     ]
 
     def as_dict(self):
@@ -147,6 +152,8 @@ EXPORTED_SYMBOLS = [
     "hsg_op_reset",
     "hsg_last_error",
     "hsg_push_batch",
+    "hsg_push_batch_async",
+    "hsg_op_wait",
     "hsg_pending_rows",
     "hsg_drain",
     "hsg_op_set_changelog",
@@ -154,6 +161,10 @@ EXPORTED_SYMBOLS = [
     "hsg_dump_state",
     "hsg_op_stats",
 ]
+
+
+# void (*hsg_done_fn)(void *ctx, int rc)
+HSG_DONE_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int)
 
 
 class HStreamGpuError(RuntimeError):

@@ -37,6 +37,22 @@ int comm_create(const uint8_t *id_bytes, int rank, int nranks, int device, Comm 
   return HSG_OK;
 }
 
+// A communicator of the same ranks for one operator (collective over the
+// parent's ranks, so every rank calls it in the same op-creation order).
+int comm_split(const Comm *parent, Comm **out, std::string &err) {
+  Comm *c = new Comm();
+  c->rank = parent->rank;
+  c->nranks = parent->nranks;
+  ncclResult_t r = ncclCommSplit(parent->comm, 0, parent->rank, &c->comm, nullptr);
+  if (r != ncclSuccess) {
+    err = std::string("ncclCommSplit: ") + ncclGetErrorString(r);
+    delete c;
+    return HSG_E_COMM;
+  }
+  *out = c;
+  return HSG_OK;
+}
+
 void comm_destroy(Comm *c) {
   if (!c) return;
   if (c->comm) ncclCommDestroy(c->comm);

@@ -245,13 +245,9 @@ static int push_sharded_classic(OpDevice &d, const hsg_op_config &cfg, const Pro
 
 int push_sharded(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, PushResult &r,
                  std::string &err) {
-  static const bool no_fast = [] {
-    const char *e = getenv("HSG_XFAST");
-    return e && strcmp(e, "0") == 0;
-  }();
   bool need_seq = cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.window_kind == HSG_SESSION;
   for (int q = 0; q < prog.n_slots; ++q) need_seq = need_seq || prog.slot_op[q] == S_LAST_SEQ;
-  if (!no_fast && d.use_part && d.xpart_log2 >= 0 && !need_seq) {
+  if (d.use_part && d.xpart_log2 >= 0 && !need_seq) {
     bool fallback = false;
     int rc = push_sharded_fast(d, cfg, prog, a, r, err, fallback);
     if (rc != HSG_OK || !fallback) return rc;

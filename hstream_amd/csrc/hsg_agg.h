@@ -542,11 +542,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
             pend &= ~(1u << u);
             continue;
           }
-          if (pp.exp == 2) { pairs += nw; pend &= ~(1u << u); continue; }
           const int e = lds_insert<E>(L.key, &L.fill, limit, ((uint64_t)key << 32) | P);
           if (e < 0) continue;  // table full: after the next flush
           pairs += nw;
-          if (pp.exp != 1) lds_apply<MS, E>(prog, &L.agg[e], r, skip);
+          lds_apply<MS, E>(prog, &L.agg[e], r, skip);
           L.nw[e] = (uint8_t)nw;
           pend &= ~(1u << u);
         }

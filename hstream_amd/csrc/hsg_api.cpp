@@ -8,11 +8,14 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "hsg_internal.h"
@@ -126,7 +129,7 @@ struct hsg_engine {
   int nranks = 1;
   uint64_t batch_cap = 0;
   std::string err;
-  std::mutex mu;  // guards the communicator
+  std::mutex mu;  // guards the engine communicator (op creation splits it)
   Comm *comm = nullptr;
 };
 
@@ -185,6 +188,17 @@ extern "C" const char *hsg_engine_last_error(const hsg_engine *e) { return e ? e
 // ---------------------------------------------------------------------------
 // op
 // ---------------------------------------------------------------------------
+// One queued asynchronous push: the batch descriptor is copied (the caller's
+// struct may live on its stack); the arrays it points to are the caller's.
+struct AsyncJob {
+  hsg_batch b;
+  std::vector<const void *> cols;
+  std::vector<const uint8_t *> valid;
+  int64_t *wm = nullptr;
+  hsg_done_fn done = nullptr;
+  void *ctx = nullptr;
+};
+
 struct hsg_op {
   hsg_engine *eng = nullptr;
   hsg_op_config cfg;
@@ -192,13 +206,64 @@ struct hsg_op {
   std::vector<hsg_agg> aggs;
   Program prog;
   OpDevice dev;  // every HBM buffer + stream + events (hsg_ops.h)
+  // Sharded ops own a communicator split from the engine's at creation, so
+  // pushes of distinct ops never share RCCL call ordering (ranks may run their
+  // queries' pushes in any interleaving) and need no engine-wide lock.
+  Comm *comm = nullptr;
   std::string err;
   uint64_t pending = 0;
   uint64_t state_rows = 0;
   uint32_t batch_id = 0;
   uint64_t rec_base = 0;
   hsg_stats stats;
+  // asynchronous pushes (hsg_push_batch_async): one completion thread per op
+  std::mutex qmu;
+  std::condition_variable qcv;
+  std::deque<AsyncJob> queue;
+  bool busy = false;       // a job is running
+  bool stopping = false;
+  int async_rc = HSG_OK;   // first failure since the last hsg_op_wait
+  std::thread worker;
 };
+
+static int push_sync(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark);
+
+// Wait for the op's queued asynchronous pushes; returns (and clears) the first
+// failure among them.
+static int drain_async(hsg_op *op) {
+  std::unique_lock<std::mutex> lk(op->qmu);
+  op->qcv.wait(lk, [&] { return op->queue.empty() && !op->busy; });
+  int rc = op->async_rc;
+  op->async_rc = HSG_OK;
+  return rc;
+}
+
+// Same wait, keeping a failure for the next hsg_op_wait / hsg_push_batch.
+static void wait_idle(const hsg_op *cop) {
+  hsg_op *op = const_cast<hsg_op *>(cop);
+  std::unique_lock<std::mutex> lk(op->qmu);
+  op->qcv.wait(lk, [&] { return op->queue.empty() && !op->busy; });
+}
+
+static void async_loop(hsg_op *op) {
+  std::unique_lock<std::mutex> lk(op->qmu);
+  for (;;) {
+    op->qcv.wait(lk, [&] { return op->stopping || !op->queue.empty(); });
+    if (op->queue.empty()) return;  // stopping with nothing left
+    AsyncJob job = std::move(op->queue.front());
+    op->queue.pop_front();
+    op->busy = true;
+    lk.unlock();
+    job.b.cols = job.cols.empty() ? nullptr : job.cols.data();
+    job.b.valid = job.valid.empty() ? nullptr : job.valid.data();
+    const int rc = push_sync(op, &job.b, job.wm);
+    if (job.done) job.done(job.ctx, rc);
+    lk.lock();
+    if (rc != HSG_OK && op->async_rc == HSG_OK) op->async_rc = rc;
+    op->busy = false;
+    op->qcv.notify_all();
+  }
+}
 
 static int validate_config(const hsg_op_config *c, std::string &err) {
   if (!c) return fail(err, HSG_E_INVALID, "null config");
@@ -247,14 +312,24 @@ extern "C" int hsg_op_create(hsg_engine *eng, const hsg_op_config *cfg, hsg_op *
     rc = build_program(op->cfg, op->col_types, op->aggs, op->prog, eng->err);
     if (rc != HSG_OK) { delete op; return rc; }
     if (hipSetDevice(eng->device) != hipSuccess) { delete op; return HSG_E_DEVICE; }
-    rc = op_device_init(op->dev, op->cfg, op->prog, eng->batch_cap, eng->nranks, eng->comm != nullptr,
+    if (eng->comm) {
+      // collective over the engine's ranks: every rank creates its sharded ops
+      // in the same order (the same queries)
+      std::lock_guard<std::mutex> lk(eng->mu);
+      rc = comm_split(eng->comm, &op->comm, eng->err);
+      if (rc != HSG_OK) { delete op; return rc; }
+    }
+    rc = op_device_init(op->dev, op->cfg, op->prog, eng->batch_cap, eng->nranks, op->comm != nullptr,
                         hsg_windows_per_record(op->cfg),
                         eng->err);
     if (rc != HSG_OK) {
       op_device_free(op->dev);
+      comm_destroy(op->comm);
       delete op;
       return rc;
     }
+    op->stats.state_slots = (uint64_t)op->prog.n_slots;
+    op->stats.state_row_bytes = 8ull * (uint64_t)op->prog.n_slots + (cfg->window_kind == HSG_SESSION ? 16ull : 8ull);
     *out = op;
     return HSG_OK;
   } catch (const std::bad_alloc &) {
@@ -267,8 +342,15 @@ extern "C" int hsg_op_create(hsg_engine *eng, const hsg_op_config *cfg, hsg_op *
 extern "C" void hsg_op_destroy(hsg_op *op) {
   if (!op) return;
   try {
+    {
+      std::lock_guard<std::mutex> lk(op->qmu);
+      op->stopping = true;
+    }
+    op->qcv.notify_all();
+    if (op->worker.joinable()) op->worker.join();  // runs what is queued first
     hipSetDevice(op->eng->device);
     op_device_free(op->dev);
+    comm_destroy(op->comm);
   } catch (...) {
   }
   delete op;
@@ -279,6 +361,7 @@ extern "C" const char *hsg_last_error(const hsg_op *op) { return op ? op->err.c_
 extern "C" int hsg_op_reset(hsg_op *op) {
   try {
     if (!op) return HSG_E_INVALID;
+    wait_idle(op);
     HIP_TRY(op, hipSetDevice(op->eng->device));
     int rc = op_device_reset(op->dev, op->cfg, op->prog, op->err);
     if (rc != HSG_OK) return rc;
@@ -294,17 +377,22 @@ extern "C" int hsg_op_reset(hsg_op *op) {
   }
 }
 
-extern "C" int hsg_push_batch(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark) {
+static int validate_batch(hsg_op *op, const hsg_batch *b, const int64_t *inout_watermark) {
+  if (!b || !inout_watermark) return fail(op->err, HSG_E_INVALID, "null batch or watermark");
+  if (b->n_cols != op->cfg.n_cols) return fail(op->err, HSG_E_INVALID, "batch n_cols != op n_cols");
+  if (b->mem != HSG_MEM_HOST && b->mem != HSG_MEM_DEVICE) return fail(op->err, HSG_E_INVALID, "bad batch mem");
+  if (b->n > op->eng->batch_cap) return fail(op->err, HSG_E_CAPACITY, "batch larger than the engine's batch_capacity");
+  if (b->n && (!b->key_id || !b->ts)) return fail(op->err, HSG_E_INVALID, "null key_id / ts");
+  for (int c = 0; c < b->n_cols; ++c)
+    if (b->n && (!b->cols || !b->cols[c])) return fail(op->err, HSG_E_INVALID, "null value column");
+  return HSG_OK;
+}
+
+// The push itself (caller: hsg_push_batch, or the op's completion thread).
+static int push_sync(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark) {
   try {
-    if (!op) return HSG_E_INVALID;
-    if (!b || !inout_watermark) return fail(op->err, HSG_E_INVALID, "null batch or watermark");
-    if (b->n_cols != op->cfg.n_cols) return fail(op->err, HSG_E_INVALID, "batch n_cols != op n_cols");
-    if (b->mem != HSG_MEM_HOST && b->mem != HSG_MEM_DEVICE) return fail(op->err, HSG_E_INVALID, "bad batch mem");
-    if (b->n > op->eng->batch_cap)
-      return fail(op->err, HSG_E_CAPACITY, "batch larger than the engine's batch_capacity");
-    if (b->n && (!b->key_id || !b->ts)) return fail(op->err, HSG_E_INVALID, "null key_id / ts");
-    for (int c = 0; c < b->n_cols; ++c)
-      if (b->n && (!b->cols || !b->cols[c])) return fail(op->err, HSG_E_INVALID, "null value column");
+    int rc = validate_batch(op, b, inout_watermark);
+    if (rc != HSG_OK) return rc;
     HIP_TRY(op, hipSetDevice(op->eng->device));
     double t0 = now_ms();
     PushResult res;
@@ -314,13 +402,10 @@ extern "C" int hsg_push_batch(hsg_op *op, const hsg_batch *b, int64_t *inout_wat
     args.batch_id = ++op->batch_id;
     args.rec_base = op->rec_base;
     args.pending = op->pending;
-    args.comm = op->eng->comm;
+    args.comm = op->comm;
     args.rank = op->eng->rank;
     args.nranks = op->eng->nranks;
-    std::unique_lock<std::mutex> lk(op->eng->mu, std::defer_lock);
-    if (op->eng->comm) lk.lock();
-    int rc = op_push(op->dev, op->cfg, op->prog, args, res, op->err);
-    if (lk.owns_lock()) lk.unlock();
+    rc = op_push(op->dev, op->cfg, op->prog, args, res, op->err);
     if (rc != HSG_OK && rc != HSG_E_RANGE && rc != HSG_E_OOM) return rc;
     // state was mutated: account for what happened even on OOM / RANGE
     *inout_watermark = res.wm_out;
@@ -346,13 +431,52 @@ extern "C" int hsg_push_batch(hsg_op *op, const hsg_batch *b, int64_t *inout_wat
   } catch (const std::bad_alloc &) {
     return HSG_E_OOM;
   } catch (...) {
-    if (op) op->err = "unexpected exception";
+    op->err = "unexpected exception";
     return HSG_E_DEVICE;
   }
 }
 
+extern "C" int hsg_push_batch(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark) {
+  if (!op) return HSG_E_INVALID;
+  int rc = drain_async(op);
+  if (rc != HSG_OK) return rc;
+  return push_sync(op, b, inout_watermark);
+}
+
+extern "C" int hsg_push_batch_async(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark, hsg_done_fn done,
+                                    void *ctx) {
+  try {
+    if (!op) return HSG_E_INVALID;
+    int rc = validate_batch(op, b, inout_watermark);
+    if (rc != HSG_OK) return rc;
+    AsyncJob job;
+    job.b = *b;
+    if (b->cols) job.cols.assign(b->cols, b->cols + b->n_cols);
+    if (b->valid) job.valid.assign(b->valid, b->valid + b->n_cols);
+    job.wm = inout_watermark;
+    job.done = done;
+    job.ctx = ctx;
+    std::lock_guard<std::mutex> lk(op->qmu);
+    if (op->stopping) return fail(op->err, HSG_E_INVALID, "op is being destroyed");
+    if (!op->worker.joinable()) op->worker = std::thread(async_loop, op);
+    op->queue.push_back(std::move(job));
+    op->qcv.notify_all();
+    return HSG_OK;
+  } catch (const std::bad_alloc &) {
+    return HSG_E_OOM;
+  } catch (...) {
+    return HSG_E_DEVICE;
+  }
+}
+
+extern "C" int hsg_op_wait(hsg_op *op) {
+  if (!op) return HSG_E_INVALID;
+  return drain_async(op);
+}
+
 extern "C" int hsg_pending_rows(const hsg_op *op, uint64_t *n) {
   if (!op || !n) return HSG_E_INVALID;
+  wait_idle(op);
   *n = op->pending;
   return HSG_OK;
 }
@@ -367,6 +491,7 @@ static int check_rows(hsg_op *op, const hsg_rows *out) {
 extern "C" int hsg_op_set_changelog(hsg_op *op, const hsg_rows *dst) {
   try {
     if (!op) return HSG_E_INVALID;
+    wait_idle(op);
     if (op->pending) return fail(op->err, HSG_E_INVALID, "set_changelog: drain the pending rows first");
     OpDevice &d = op->dev;
     if (!dst) {
@@ -403,6 +528,7 @@ extern "C" int hsg_op_set_changelog(hsg_op *op, const hsg_rows *dst) {
 extern "C" int hsg_drain(hsg_op *op, hsg_rows *out, uint64_t *n_out) {
   try {
     if (!op || !n_out) return HSG_E_INVALID;
+    wait_idle(op);
     int rc = op->dev.ext_out && !out ? HSG_OK : check_rows(op, out);
     if (rc != HSG_OK) return rc;
     *n_out = op->pending;
@@ -422,6 +548,7 @@ extern "C" int hsg_drain(hsg_op *op, hsg_rows *out, uint64_t *n_out) {
 
 extern "C" int hsg_state_rows(hsg_op *op, uint64_t *n) {
   if (!op || !n) return HSG_E_INVALID;
+  wait_idle(op);
   *n = op->state_rows;
   return HSG_OK;
 }
@@ -429,6 +556,7 @@ extern "C" int hsg_state_rows(hsg_op *op, uint64_t *n) {
 extern "C" int hsg_dump_state(hsg_op *op, hsg_rows *out, uint64_t *n_out) {
   try {
     if (!op || !n_out) return HSG_E_INVALID;
+    wait_idle(op);
     int rc = check_rows(op, out);
     if (rc != HSG_OK) return rc;
     *n_out = op->state_rows;
@@ -445,6 +573,7 @@ extern "C" int hsg_dump_state(hsg_op *op, hsg_rows *out, uint64_t *n_out) {
 
 extern "C" int hsg_op_stats(const hsg_op *op, hsg_stats *out) {
   if (!op || !out) return HSG_E_INVALID;
+  wait_idle(op);
   *out = op->stats;
   return HSG_OK;
 }

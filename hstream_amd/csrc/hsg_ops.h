@@ -15,6 +15,7 @@ struct XBuffers;  // exchange scratch (hsg_exchange.h)
 
 int comm_unique_id(uint8_t *out);
 int comm_create(const uint8_t *id, int rank, int nranks, int device, Comm **out, std::string &err);
+int comm_split(const Comm *parent, Comm **out, std::string &err);
 void comm_destroy(Comm *c);
 
 // Session store in HBM (k_session.hip): per-key session lists in an arena.

@@ -50,7 +50,7 @@ struct PartParams {
   int32_t rbits;      // aggregation: 2^rbits key-hash rounds per sub-chunk
   int32_t big;        // aggregation variant: 1 = big LDS table, 1024 threads
   int32_t bshift;     // owner bits above the bucket bits in the key hash (multi-GPU, power-of-two ranks)
-  int32_t exp;        // experiment knob (HSG_EXP, timing studies only): 1 = no LDS aggregate update, 2 = no LDS insert
+  int32_t reserved;
   uint64_t tiles;     // partition-pass tiles of this batch
   uint64_t chunk;     // records per aggregation workgroup
 };

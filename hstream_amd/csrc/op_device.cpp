@@ -302,6 +302,8 @@ int stage_batch(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err) {
   kb.n = b->n;
   const uint64_t n = b->n;
   if (b->mem == HSG_MEM_DEVICE) {
+    // the producer's stream is not ordered with ours: wait on its event
+    if (b->ready_event) DTRY(hipStreamWaitEvent(d.stream, (hipEvent_t)b->ready_event, 0));
     kb.key = b->key_id;
     kb.ts = b->ts;
     for (int c = 0; c < b->n_cols; ++c) {
@@ -444,14 +446,12 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       pp.tile = part_tile_for(pp.words);
       pp.tiles = part_tiles(kb.n, pp.tile);
       pp.pane_S = d.pane_S;
-      { static const char *x = getenv("HSG_EXP"); pp.exp = x ? atoi(x) : 0; }
       pp.rbits = d.rbits;
       pp.chunk = kAggChunk;
       pp.big = d.agg_big ? 1 : 0;
       if (!rec_wm && !optimistic) launch_part_recwm(d.stream, kb, d.tile_prefix, d.sc, d.part.wm);
       launch_part_hist(d.stream, kb, p, pp, rec_wm, d.part.wm, d.part, d.sc, optimistic);
-      static const bool nopack = getenv("HSG_NOPACK") != nullptr;  // timing studies
-      const bool can_pack = optimistic && !nopack && cfg.n_cols <= 8 && d.wpr < 256;
+      const bool can_pack = optimistic && cfg.n_cols <= 8 && d.wpr < 256;
       if (optimistic) launch_part_decide(d.stream, d.sc, p, a.wm_in, cfg.grace_ms, can_pack, d.part, pp.tiles);
       launch_part_offsets(d.stream, pp, d.part, d.sc);
       launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc, can_pack);

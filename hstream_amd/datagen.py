@@ -43,6 +43,7 @@ class Config:
     zipf: float = 0.0       # > 0: Zipf(s) ranks over `keys` universe
     batch: int = 1 << 24
     seed: int = 0
+    span_ms: int = HOUR     # "span" mode: event time covered by the config's `total` records
 
     def spec(self, emit_mode=abi.HSG_EMIT_PER_BATCH, state_capacity=0, out_capacity=0) -> OpSpec:
         ncols = 0 if all(k == abi.HSG_COUNT_ALL for k, _ in self.aggs) else 1
@@ -97,7 +98,7 @@ def timestamps(cfg: Config, start: int, count: int, total: int, rng):
     if cfg.ts_mode == "step":
         base = TS0 + i
     else:
-        base = TS0 + (i * HOUR) // max(1, total)
+        base = TS0 + (i * cfg.span_ms) // max(1, total)
     return base + rng.integers(0, cfg.jitter, size=count, dtype=np.int64)
 
 
@@ -137,7 +138,7 @@ def generate_torch(cfg: Config, n, device="cuda", seed=None, start=0, total=None
     if cfg.ts_mode == "step":
         base = TS0 + i
     else:
-        base = TS0 + torch.div(i * HOUR, max(1, total), rounding_mode="floor")
+        base = TS0 + torch.div(i * cfg.span_ms, max(1, total), rounding_mode="floor")
     ts = base + torch.randint(0, cfg.jitter, (n,), device=device, generator=g, dtype=torch.int64)
     lo, hi = cfg.vrange
     if cfg.col_type == abi.HSG_F64:

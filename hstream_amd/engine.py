@@ -40,6 +40,10 @@ def load_library(path=LIB_PATH):
     L.hsg_op_stats.restype = C.c_int
     L.hsg_op_set_changelog.argtypes = [vp, P(abi.hsg_rows)]
     L.hsg_op_set_changelog.restype = C.c_int
+    L.hsg_push_batch_async.argtypes = [vp, P(abi.hsg_batch), P(C.c_int64), abi.HSG_DONE_FN, vp]
+    L.hsg_push_batch_async.restype = C.c_int
+    L.hsg_op_wait.argtypes = [vp]
+    L.hsg_op_wait.restype = C.c_int
     declare_op_functions(L, "hsg")
     _lib = L
     return L
@@ -118,6 +122,38 @@ class GpuOp(OpHandle):
         got = C.c_uint64(0)
         self._check(self._lib.hsg_drain(self._h, None, C.byref(got)), "drain")
         return got.value
+
+    def push_async(self, key_id, ts, cols=(), valid=None, watermark=None, done=None, mem=None):
+        """hsg_push_batch_async: queue the batch and return at once. `watermark`
+        is a ctypes.c_int64 shared by consecutive pushes (read when the batch
+        starts, written before `done(rc)` runs on the op's completion thread).
+        The arrays are kept alive until the completion has run."""
+        from .columnar import make_batch
+        b, keep = make_batch(key_id, ts, cols, valid, mem)
+        wm = watermark if watermark is not None else C.c_int64(-1)
+        entry = {}
+
+        def _cb(_ctx, rc):
+            try:
+                if done is not None:
+                    done(rc)
+            finally:
+                self._inflight.pop(id(entry), None)
+
+        cb = abi.HSG_DONE_FN(_cb)
+        entry.update(keep=keep, b=b, cb=cb, wm=wm)
+        if not hasattr(self, "_inflight"):
+            self._inflight = {}
+        self._inflight[id(entry)] = entry
+        rc = self._lib.hsg_push_batch_async(self._h, C.byref(b), C.byref(wm), cb, None)
+        if rc != abi.HSG_OK:
+            self._inflight.pop(id(entry), None)
+        self._check(rc, "push_batch_async")
+        return wm
+
+    def wait(self):
+        """hsg_op_wait: block until the queued pushes are done; raises the first failure."""
+        self._check(self._lib.hsg_op_wait(self._h), "op_wait")
 
     def stats(self) -> dict:
         s = abi.hsg_stats()

@@ -133,7 +133,15 @@ typedef struct {
   uint64_t out_capacity;   /* changelog rows buffered in HBM between drains; 0 = default */
 } hsg_op_config;
 
-/* One micro-batch in columnar form, records in arrival order. */
+/* One micro-batch in columnar form, records in arrival order.
+ *
+ * Device-resident batches (mem = HSG_MEM_DEVICE) are read on the op's own HIP
+ * stream, which is not ordered after the stream that produced them: either
+ * the producer's writes are complete when hsg_push_batch is called (e.g. the
+ * producer synchronised its stream), or ready_event names a hipEvent_t
+ * recorded on the producing stream after its last write, and the op's stream
+ * waits on it before reading. Host batches are copied to the device inside
+ * the call (sync) or before completion is signalled (async). */
 typedef struct {
   uint64_t n;
   int32_t mem;                  /* hsg_mem of every pointer below                        */
@@ -143,6 +151,8 @@ typedef struct {
   const void *const *cols;      /* n_cols arrays of int64_t or double                    */
   const uint8_t *const *valid;  /* n_cols presence arrays (1 byte/record, 0 = field absent);
                                    NULL or a NULL entry = all present                    */
+  void *ready_event;            /* optional hipEvent_t the op's stream waits on (device
+                                   batches); NULL = inputs already complete              */
 } hsg_batch;
 
 /* Columnar changelog / state rows. */
@@ -173,7 +183,19 @@ typedef struct {
   uint64_t exchange_bytes;    /* cumulative bytes this rank sent to peers               */
   uint64_t pairs_total;       /* cumulative accepted (record, window) updates           */
   uint64_t touched_total;     /* cumulative groups / sessions touched (summed per batch) */
+  uint64_t state_slots;       /* 8-byte aggregate words per state row (the op's program) */
+  uint64_t state_row_bytes;   /* algorithmic state row: group key 8 B + 8 B per slot
+                                 (sessions: start + end + slots)                        */
+  uint64_t spilled_rows;      /* rows evicted from HBM into the host spill store          */
+  uint64_t spill_events;      /* retention passes that moved rows to the host            */
 } hsg_stats;
+
+/* Completion callback of hsg_push_batch_async: rc is what hsg_push_batch
+ * would have returned. Runs on the op's completion thread; it must not call
+ * back into the same op. The Haskell binding passes a C shim that stores rc
+ * and calls hs_try_putmvar(cap, mvar), the pattern of
+ * hstream-store/cbits/logdevice/hs_writer.cpp:29-44. */
+typedef void (*hsg_done_fn)(void *ctx, int rc);
 
 /* ---- engine: one per process and GPU ---------------------------------------- */
 int  hsg_comm_unique_id(uint8_t *out, size_t len);
@@ -191,6 +213,20 @@ const char *hsg_last_error(const hsg_op *op);
  * Processor/Internal.hs:151); it is read as the value before the batch and
  * overwritten with the value after it (max over all ranks' records). */
 int  hsg_push_batch(hsg_op *op, const hsg_batch *batch, int64_t *inout_watermark);
+
+/* Asynchronous hsg_push_batch: validates and queues the batch, returns at
+ * once (HSG_OK = queued, or an argument error). Queued batches of one op run
+ * in call order on the op's completion thread; *inout_watermark is read when
+ * the batch starts (so consecutive pushes may share one watermark variable)
+ * and written before done(ctx, rc) is called. The batch's arrays (not the
+ * hsg_batch struct itself, which is copied) must stay valid until done runs.
+ * Any other call on the op first waits for the queue to drain. Bind as an
+ * unsafe ccall: it never blocks on the GPU. */
+int  hsg_push_batch_async(hsg_op *op, const hsg_batch *batch, int64_t *inout_watermark, hsg_done_fn done,
+                          void *ctx);
+/* Block until every queued asynchronous push of the op has completed; returns
+ * the first non-OK status among them (HSG_OK if none), and clears it. */
+int  hsg_op_wait(hsg_op *op);
 
 int  hsg_pending_rows(const hsg_op *op, uint64_t *n);
 /* Move up to out->capacity pending changelog rows into out (oldest first). If
