@@ -26,6 +26,8 @@ int push_time_perrecord(OpDevice &d, const hsg_op_config &cfg, const Program &pr
 
 // sessions (session.cpp / k_session.hip)
 int session_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t rows, std::string &err);
+int session_device_reset(OpDevice &d, std::string &err);
+void session_device_free(OpDevice &d);
 int push_session(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, const Batch &kb,
                  const int64_t *seq, PushResult &r, std::string &err);
 void launch_session_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, OutCols out, uint64_t cap,

@@ -18,19 +18,25 @@ int comm_create(const uint8_t *id, int rank, int nranks, int device, Comm **out,
 int comm_split(const Comm *parent, Comm **out, std::string &err);
 void comm_destroy(Comm *c);
 
-// Session store in HBM (k_session.hip): per-key session lists in an arena.
+// Session store in HBM (k_session.hip, hsg_session.h): a growable key table
+// (key -> slot) and per slot the key's sessions, sorted by start, in an arena.
+struct SessList {
+  uint64_t off;  // arena index of the first session
+  uint32_t len;
+  uint32_t cap;
+};
 struct SessTable {
-  uint32_t *keys;      // [cap] key id, kEmpty32 = free
-  uint64_t *list_off;  // [cap] arena offset (in sessions) of the key's list
-  uint32_t *list_len;  // [cap]
-  uint32_t *list_cap;  // [cap]
-  uint64_t mask;
+  uint32_t *keys;      // [kmask + 1] key id, kSessEmptyKey = free
+  SessList *lists;     // [kmask + 1]
+  uint64_t *emark;     // [kmask + 1] merge path: ~batch << 32 | lowest index the batch rewrote (~0 = none)
+  uint64_t kmask;
   // arena, structure of arrays: start, end, stamp and n_slots agg words per session
   int64_t *a_start;
   int64_t *a_end;
   uint32_t *a_stamp;
   int64_t *a_aggs;     // [arena_cap][n_slots]
   uint64_t arena_cap;
+  uint64_t *meta;      // [M_WORDS] device bookkeeping (hsg_session.h SessMeta)
 };
 
 struct OpDevice {
@@ -66,7 +72,11 @@ struct OpDevice {
   bool agg_big = true;          // aggregation variant of the next batch (big LDS table)
   // sessions
   SessTable ss = {};
-  uint64_t *arena_top = nullptr;  // device bump pointer
+  uint64_t *h_meta = nullptr;     // pinned mirror of ss.meta
+  uint64_t ss_keys = 0;           // live keys after the last batch (host mirror)
+  uint64_t ss_live_max = 0;       // sessions the arena was last compacted for
+  void *ss_part = nullptr;        // session partition scratch (tmax, progress)
+  bool ss_merge = false;          // sessions take the sort + runs + merge path (else replay)
   // changelog buffer: the op's own, or caller-owned device columns
   // registered with hsg_op_set_changelog (rows land there directly)
   OutCols out = {};

@@ -142,8 +142,8 @@ int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, 
   memset(d.h_sc, 0, sizeof(DevScalars));  // host mirror (epoch_set gates the optimistic path)
   d.sc_clean = false;
   if (cfg.window_kind == HSG_SESSION) {
-    launch_ss_reset(d.stream, d.ss, d.cap);
-    DTRY(hipMemsetAsync(d.arena_top, 0, sizeof(uint64_t), d.stream));
+    int rc = session_device_reset(d, err);
+    if (rc != HSG_OK) return rc;
   } else {
     launch_tw_reset(d.stream, d.tw, prog);
     if (cfg.window_kind == HSG_UNWINDOWED) {
@@ -221,7 +221,7 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
   d.own_out = d.out;
   d.own_out_cap = d.out_cap;
   if (rc != HSG_OK) return rc;
-  if (cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.window_kind == HSG_SESSION) {
+  if (cfg.emit_mode == HSG_EMIT_PER_RECORD || (cfg.window_kind == HSG_SESSION && !d.ss_merge)) {
     rc = perrecord_device_init(d, cfg, prog, err);
     if (rc != HSG_OK) return rc;
   } else if (part_supported(prog)) {
@@ -264,15 +264,7 @@ void op_device_free(OpDevice &d) {
   dfree(d.emit.cnt);
   dfree(d.emit.off);
   dfree(d.emit.partial);
-  dfree(d.ss.keys);
-  dfree(d.ss.list_off);
-  dfree(d.ss.list_len);
-  dfree(d.ss.list_cap);
-  dfree(d.ss.a_start);
-  dfree(d.ss.a_end);
-  dfree(d.ss.a_stamp);
-  dfree(d.ss.a_aggs);
-  dfree(d.arena_top);
+  session_device_free(d);
   free_out(d.own_out);
   d.out = d.own_out;
   if (d.scratch) hipFree(d.scratch);

@@ -1,0 +1,352 @@
+// Host orchestration of session windows (SessionWindowedStream.hs:74-118 over
+// Store.hs:139-272): store allocation and growth, and the two batch paths of
+// hsg_session.h (merge: partition + per-bucket sort / runs / sweep-merge;
+// replay: per-key arrival-order replay for the per-record changelog and LAST).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+
+#include "hsg_kernels.h"
+#include "hsg_part.h"
+#include "hsg_perrecord.h"
+#include "hsg_session.h"
+#include "hsg_sort.h"
+
+namespace hsg {
+
+#define DTRY(expr)                                                          \
+  do {                                                                      \
+    hipError_t _e = (expr);                                                 \
+    if (_e != hipSuccess) {                                                 \
+      err = std::string(#expr) + ": " + hipGetErrorString(_e);              \
+      return _e == hipErrorOutOfMemory ? HSG_E_OOM : HSG_E_DEVICE;          \
+    }                                                                       \
+  } while (0)
+
+static uint64_t pow2_at_least(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+static int log2u(uint64_t v) {
+  int l = 0;
+  while ((1ull << l) < v) ++l;
+  return l;
+}
+
+static bool has_last(const Program &prog) {
+  for (int s = 0; s < prog.n_slots; ++s)
+    if (prog.slot_op[s] == S_LAST_SEQ) return true;
+  return false;
+}
+
+static int alloc_keys(SessTable &t, uint64_t kcap, std::string &err) {
+  DTRY(hipMalloc((void **)&t.keys, kcap * sizeof(uint32_t)));
+  DTRY(hipMalloc((void **)&t.lists, kcap * sizeof(SessList)));
+  DTRY(hipMalloc((void **)&t.emark, kcap * sizeof(uint64_t)));
+  t.kmask = kcap - 1;
+  return HSG_OK;
+}
+
+static void free_keys(SessTable &t) {
+  if (t.keys) hipFree(t.keys);
+  if (t.lists) hipFree(t.lists);
+  if (t.emark) hipFree(t.emark);
+  t.keys = nullptr;
+  t.lists = nullptr;
+  t.emark = nullptr;
+}
+
+static int alloc_arena(SessTable &t, uint64_t cap, int ns, std::string &err) {
+  DTRY(hipMalloc((void **)&t.a_start, cap * sizeof(int64_t)));
+  DTRY(hipMalloc((void **)&t.a_end, cap * sizeof(int64_t)));
+  DTRY(hipMalloc((void **)&t.a_stamp, cap * sizeof(uint32_t)));
+  DTRY(hipMalloc((void **)&t.a_aggs, cap * (uint64_t)(ns ? ns : 1) * sizeof(int64_t)));
+  t.arena_cap = cap;
+  return HSG_OK;
+}
+
+static void free_arena(SessTable &t) {
+  if (t.a_start) hipFree(t.a_start);
+  if (t.a_end) hipFree(t.a_end);
+  if (t.a_stamp) hipFree(t.a_stamp);
+  if (t.a_aggs) hipFree(t.a_aggs);
+  t.a_start = t.a_end = nullptr;
+  t.a_stamp = nullptr;
+  t.a_aggs = nullptr;
+}
+
+// Session partition scratch: per-tile ts maxima and per-bucket progress.
+static SessPart sess_part(OpDevice &d) {
+  SessPart sp;
+  sp.hist = d.part.hist;
+  sp.offt = d.part.offt;
+  sp.bstart = d.part.bstart;
+  sp.rec = d.part.rec;
+  char *m = (char *)d.ss_part;
+  sp.tmax = (uint64_t *)m;
+  const uint64_t tiles = part_tiles(d.batch_cap, kPartTileRecs) + 1;
+  const uint64_t o_prog = (tiles * 8 + 255) & ~255ull;
+  sp.progress = (uint32_t *)(m + o_prog);
+  sp.touched = (uint32_t *)(m + o_prog + (((1ull << kPartMaxLog2) * 4 + 255) & ~255ull));
+  return sp;
+}
+
+int session_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t rows, std::string &err) {
+  SessTable &t = d.ss;
+  memset(&t, 0, sizeof(t));
+  // key table: keys <= sessions; grown by rehash as keys arrive (push_session)
+  uint64_t kc = rows < d.batch_cap ? rows : d.batch_cap;
+  const uint64_t kcap = pow2_at_least(2 * (kc > (1u << 14) ? kc : (1u << 14)));
+  int rc = alloc_keys(t, kcap, err);
+  if (rc != HSG_OK) return rc;
+  d.cap = kcap;
+  // arena: the expected live sessions, grown by compaction when a batch needs more
+  rc = alloc_arena(t, pow2_at_least(rows > (1u << 20) ? rows : (1u << 20)), prog.n_slots, err);
+  if (rc != HSG_OK) return rc;
+  DTRY(hipMalloc((void **)&t.meta, M_WORDS * sizeof(uint64_t)));
+  DTRY(hipHostMalloc((void **)&d.h_meta, M_WORDS * sizeof(uint64_t), hipHostMallocDefault));
+  d.ss_merge = cfg.emit_mode != HSG_EMIT_PER_RECORD && !has_last(prog) && prog.n_slots <= 8;
+  if (d.ss_merge) {
+    rc = part_device_init(d, cfg, prog, err);
+    if (rc != HSG_OK) return rc;
+    const uint64_t tiles = part_tiles(d.batch_cap, kPartTileRecs) + 1;
+    DTRY(hipMalloc(&d.ss_part, ((tiles * 8 + 255) & ~255ull) + (((1ull << kPartMaxLog2) * 4 + 255) & ~255ull) +
+                                   d.batch_cap * 4 + 256));
+  }
+  return HSG_OK;
+}
+
+int session_device_reset(OpDevice &d, std::string &err) {
+  launch_ss_reset(d.stream, d.ss);
+  DTRY(hipMemsetAsync(d.ss.meta, 0, M_WORDS * sizeof(uint64_t), d.stream));
+  d.ss_keys = 0;
+  return HSG_OK;
+}
+
+void session_device_free(OpDevice &d) {
+  free_keys(d.ss);
+  free_arena(d.ss);
+  if (d.ss.meta) hipFree(d.ss.meta);
+  d.ss.meta = nullptr;
+  if (d.h_meta) hipHostFree(d.h_meta);
+  d.h_meta = nullptr;
+  if (d.ss_part) hipFree(d.ss_part);
+  d.ss_part = nullptr;
+}
+
+// Key table with room for `incoming` more keys at load <= 1/2 (rehash).
+static int ensure_keys(OpDevice &d, uint64_t incoming, std::string &err) {
+  const uint64_t kcap = d.ss.kmask + 1;
+  if (2 * (d.ss_keys + incoming) <= kcap) return HSG_OK;
+  const uint64_t ncap = pow2_at_least(2 * (d.ss_keys + incoming) + 1);
+  SessTable to = d.ss;
+  to.keys = nullptr;
+  to.lists = nullptr;
+  to.emark = nullptr;
+  int rc = alloc_keys(to, ncap, err);
+  if (rc != HSG_OK) {
+    free_keys(to);
+    return rc;
+  }
+  launch_ss_rehash(d.stream, d.ss, to);
+  DTRY(hipGetLastError());
+  DTRY(hipStreamSynchronize(d.stream));
+  free_keys(d.ss);
+  d.ss.keys = to.keys;
+  d.ss.lists = to.lists;
+  d.ss.emark = to.emark;
+  d.ss.kmask = to.kmask;
+  d.cap = ncap;
+  return HSG_OK;
+}
+
+// Compact the arena into a fresh one with room for `extra` more sessions
+// beyond the compacted lists (at least twice what they use). Between batches or
+// between the passes of one batch: nothing is in flight on the stream.
+static int refill_arena(OpDevice &d, const Program &prog, uint64_t extra, std::string &err) {
+  SessTable &t = d.ss;
+  const uint64_t kcap = t.kmask + 1;
+  void *scratch = nullptr;
+  DTRY(hipMalloc(&scratch, ss_compact_scratch_bytes(kcap)));
+  uint64_t *total = d.h_meta + M_WORDS - 1;  // pinned word used as the landing slot
+  launch_ss_compact_plan(d.stream, t, scratch, t.meta + M_WORDS - 1);
+  hipMemcpyAsync(total, t.meta + M_WORDS - 1, 8, hipMemcpyDeviceToHost, d.stream);
+  hipError_t e = hipStreamSynchronize(d.stream);
+  if (e != hipSuccess) {
+    hipFree(scratch);
+    err = std::string("session compaction: ") + hipGetErrorString(e);
+    return HSG_E_DEVICE;
+  }
+  const uint64_t used = *total;
+  uint64_t cap = t.arena_cap;
+  while (cap < 2 * used + extra) cap <<= 1;
+  SessTable to = t;
+  to.a_start = to.a_end = nullptr;
+  to.a_stamp = nullptr;
+  to.a_aggs = nullptr;
+  int rc = alloc_arena(to, cap, prog.n_slots, err);
+  if (rc != HSG_OK) {
+    free_arena(to);
+    hipFree(scratch);
+    return rc;
+  }
+  launch_ss_compact_copy(d.stream, t, to, prog.n_slots, scratch);
+  hipMemcpyAsync(t.meta + M_TOP, t.meta + M_WORDS - 1, 8, hipMemcpyDeviceToDevice, d.stream);
+  e = hipStreamSynchronize(d.stream);
+  hipFree(scratch);
+  if (e != hipSuccess) {
+    free_arena(to);
+    err = std::string("session compaction: ") + hipGetErrorString(e);
+    return HSG_E_DEVICE;
+  }
+  free_arena(t);
+  t.a_start = to.a_start;
+  t.a_end = to.a_end;
+  t.a_stamp = to.a_stamp;
+  t.a_aggs = to.a_aggs;
+  t.arena_cap = to.arena_cap;
+  return HSG_OK;
+}
+
+static int finish_session_batch(OpDevice &d, int64_t wm_in, uint64_t n, PushResult &r, std::string &err) {
+  DTRY(hipMemcpyAsync(d.h_meta, d.ss.meta, M_WORDS * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
+  return finish_batch(d, wm_in, n, r, err);
+}
+
+static int clear_fail(OpDevice &d, std::string &err) {
+  DTRY(hipMemsetAsync(d.ss.meta + M_NEED, 0, 2 * sizeof(uint64_t), d.stream));  // M_NEED, M_FAIL
+  return HSG_OK;
+}
+
+// merge path: partition by key hash, then per bucket chunk: sort by (key, ts),
+// gap-delimited runs, sweep-merge per key with its resident sessions
+static int push_session_merge(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
+                              const Batch &kb, PushResult &r, std::string &err) {
+  const uint64_t n = kb.n;
+  SessParams sp;
+  sp.gap = cfg.gap_ms;
+  sp.rec_base = a.rec_base;
+  sp.batch_id = a.batch_id;
+  sp.emit_mode = cfg.emit_mode;
+  SessPart pt = sess_part(d);
+  const uint64_t tiles = part_tiles(n, kPartTileRecs);
+  // buckets of about one sort chunk (2048 records) each
+  int nl = log2u((n + 2047) / 2048);
+  nl = nl < 4 ? 4 : (nl > kPartMaxLog2 ? kPartMaxLog2 : nl);
+  bool has_valid = false;
+  for (int c = 0; c < cfg.n_cols; ++c) has_valid = has_valid || kb.valid[c] != nullptr;
+  const int words = 2 + cfg.n_cols;
+  PartParams pp;
+  memset(&pp, 0, sizeof(pp));
+  pp.np_log2 = nl;
+  pp.tiles = tiles;
+  DTRY(hipEventRecord(d.ev_a, d.stream));
+  DTRY(hipMemsetAsync(pt.progress, 0, (1ull << nl) * 4, d.stream));
+  launch_ss_phist(d.stream, kb, nl, tiles, pt);
+  launch_ss_wm(d.stream, pt, tiles, a.wm_in, d.sc);
+  launch_part_offsets(d.stream, pp, d.part, d.sc);
+  launch_ss_pscatter(d.stream, kb, nl, tiles, words, has_valid, pt);
+  launch_ss_merge(d.stream, sp, d.ss, prog, nl, words, pt, d.sc);
+  // the arena fill is only known on the host when a bucket could not reserve
+  // space: then it stopped at a chunk boundary; compact / grow and resume
+  DTRY(hipMemcpyAsync(d.h_meta, d.ss.meta, M_WORDS * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
+  DTRY(hipStreamSynchronize(d.stream));
+  DTRY(hipGetLastError());
+  while (d.h_meta[M_FAIL]) {
+    int rc = refill_arena(d, prog, 2 * n, err);
+    if (rc != HSG_OK) return rc;
+    rc = clear_fail(d, err);
+    if (rc != HSG_OK) return rc;
+    launch_ss_merge(d.stream, sp, d.ss, prog, nl, words, pt, d.sc);
+    DTRY(hipMemcpyAsync(d.h_meta, d.ss.meta, M_WORDS * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
+    DTRY(hipStreamSynchronize(d.stream));
+    DTRY(hipGetLastError());
+  }
+  launch_ss_emit(d.stream, d.ss, prog, pt, a.batch_id, cfg.emit_mode == HSG_EMIT_PER_BATCH ? 1 : 0, n, d.out,
+                 a.pending, d.sc);
+  DTRY(hipEventRecord(d.ev_b, d.stream));
+  DTRY(hipGetLastError());
+  int rc = finish_session_batch(d, a.wm_in, n, r, err);
+  if (cfg.emit_mode != HSG_EMIT_PER_BATCH) r.out_rows = 0;
+  return rc;
+}
+
+// replay path: stable sort by key slot, one thread per key replays its
+// records in arrival order
+static int push_session_replay(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
+                               const Batch &kb, const int64_t *seq, PushResult &r, std::string &err) {
+  PrBuffers &pb = d.pr;
+  const uint64_t n = kb.n;
+  const uint32_t cap = (uint32_t)(d.ss.kmask + 1);
+  SessParams sp;
+  sp.gap = cfg.gap_ms;
+  sp.rec_base = a.rec_base;
+  sp.batch_id = a.batch_id;
+  sp.emit_mode = cfg.emit_mode;
+  launch_stream_time(d, cfg, kb, a.wm_in, 1);
+  DTRY(hipEventRecord(d.ev_a, d.stream));
+  launch_ss_slot(d.stream, kb, d.ss, pb.pslot, pb.pidx, pb.cnt, d.sc);
+  scan_excl_u32(d.stream, pb.cnt, pb.off, n, pb.partial, pb.totals + 1);  // changelog positions, V
+  const int which = radix_sort_pairs(d.stream, pb.pslot, pb.pidx, pb.k1, pb.v1, n, log2u(cap) + 1, pb.sort_scratch);
+  const uint32_t *slot = which ? pb.k1 : pb.pslot;
+  const uint32_t *ridx = which ? pb.v1 : pb.pidx;
+  launch_ss_runs(d.stream, slot, n, cap, pb.flags, nullptr, nullptr, 0);
+  scan_excl_u8(d.stream, pb.flags, pb.runidx, n, pb.partial, pb.totals + 2);  // R
+  launch_ss_runs(d.stream, slot, n, cap, pb.flags, pb.runidx, pb.runs, 1);
+  DTRY(hipMemcpyAsync(d.h_tmp, pb.totals, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
+  DTRY(hipStreamSynchronize(d.stream));
+  const uint64_t V = d.h_tmp[1];
+  const uint64_t R = d.h_tmp[2];
+  // runs[R] = V closes the last run (valid records sort before HSG_KEY_NONE)
+  uint32_t *v32 = (uint32_t *)(d.h_tmp + 4);  // pinned
+  *v32 = (uint32_t)V;
+  DTRY(hipMemcpyAsync(pb.runs + R, v32, sizeof(uint32_t), hipMemcpyHostToDevice, d.stream));
+  int rc = HSG_OK;
+  for (int attempt = 0;; ++attempt) {
+    launch_ss_replay_need(d.stream, d.ss, slot, pb.runs, R);
+    launch_ss_process(d.stream, kb, sp, d.ss, prog, slot, ridx, pb.runs, R, pb.off, seq, d.out, a.pending, d.sc);
+    DTRY(hipEventRecord(d.ev_b, d.stream));
+    DTRY(hipGetLastError());
+    rc = finish_session_batch(d, a.wm_in, n, r, err);
+    if (rc != HSG_OK || !d.h_meta[M_FAIL] || attempt > 0) break;
+    // not enough arena for the lists that grow: compact / grow, then again
+    rc = refill_arena(d, prog, d.h_meta[M_NEED] + 2 * n, err);
+    if (rc != HSG_OK) return rc;
+    rc = clear_fail(d, err);
+    if (rc != HSG_OK) return rc;
+  }
+  if (rc == HSG_OK && d.h_meta[M_FAIL]) {
+    err = "session arena: no room after compaction";
+    return HSG_E_OOM;
+  }
+  if (cfg.emit_mode == HSG_EMIT_PER_RECORD) r.out_rows = V;
+  r.pairs = V;
+  return rc;
+}
+
+int push_session(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, const Batch &kb,
+                 const int64_t *seq, PushResult &r, std::string &err) {
+  int rc = clear_batch_scalars(d, err);
+  if (rc != HSG_OK) return rc;
+  if (!kb.n) return finish_batch(d, a.wm_in, 0, r, err);
+  rc = ensure_keys(d, kb.n, err);
+  if (rc != HSG_OK) return rc;
+  DTRY(hipMemsetAsync(d.ss.meta + M_NEED, 0, 3 * sizeof(uint64_t), d.stream));  // need, fail, touched list
+  rc = d.ss_merge ? push_session_merge(d, cfg, prog, a, kb, r, err) : push_session_replay(d, cfg, prog, a, kb, seq, r, err);
+  if (d.ss_merge) r.pairs = kb.n;  // keyed records (HSG_KEY_NONE are counted too; stats only)
+  d.ss_keys = d.h_meta[M_KEYS];
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, d.ev_a, d.ev_b) == hipSuccess) r.agg_ms = ms;
+  r.agg_launches = 1;
+  return rc;
+}
+
+void launch_session_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, OutCols out, uint64_t cap,
+                         uint64_t *counter) {
+  launch_ss_dump(d.stream, d.ss, prog, out, cap, counter);
+}
+
+}  // namespace hsg

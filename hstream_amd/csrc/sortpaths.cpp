@@ -1,5 +1,5 @@
-// Host orchestration of the sort-based paths: the exact per-record changelog
-// of time windows and session windows.
+// Host orchestration of the exact per-record changelog of time windows (and
+// the scratch it shares with the session replay path).
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -7,7 +7,6 @@
 
 #include "hsg_kernels.h"
 #include "hsg_perrecord.h"
-#include "hsg_session.h"
 #include "hsg_sort.h"
 
 namespace hsg {
@@ -123,81 +122,6 @@ int push_time_perrecord(OpDevice &d, const hsg_op_config &cfg, const Program &pr
     r.agg_launches = 1;
   }
   return rc;
-}
-
-// ---------------------------------------------------------------------------
-// sessions
-// ---------------------------------------------------------------------------
-int session_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t rows, std::string &err) {
-  SessTable &t = d.ss;
-  DTRY(hipMalloc((void **)&t.keys, d.cap * sizeof(uint32_t)));
-  DTRY(hipMalloc((void **)&t.list_off, d.cap * sizeof(uint64_t)));
-  DTRY(hipMalloc((void **)&t.list_len, d.cap * sizeof(uint32_t)));
-  DTRY(hipMalloc((void **)&t.list_cap, d.cap * sizeof(uint32_t)));
-  t.mask = d.cap - 1;
-  // inline lists + a dynamic region for grown lists: growth doubles and
-  // abandons the old copy, so up to 2x the live sessions can be in use
-  t.arena_cap = d.cap * kSessInline + 2 * rows;
-  DTRY(hipMalloc((void **)&t.a_start, t.arena_cap * sizeof(int64_t)));
-  DTRY(hipMalloc((void **)&t.a_end, t.arena_cap * sizeof(int64_t)));
-  DTRY(hipMalloc((void **)&t.a_stamp, t.arena_cap * sizeof(uint32_t)));
-  DTRY(hipMalloc((void **)&t.a_aggs, t.arena_cap * (uint64_t)(prog.n_slots ? prog.n_slots : 1) * sizeof(int64_t)));
-  DTRY(hipMalloc((void **)&d.arena_top, sizeof(uint64_t)));
-  return HSG_OK;
-}
-
-int push_session(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, const Batch &kb,
-                 const int64_t *seq, PushResult &r, std::string &err) {
-  int rc = clear_batch_scalars(d, err);
-  if (rc != HSG_OK) return rc;
-  uint64_t V = 0;
-  if (kb.n) {
-    PrBuffers &pb = d.pr;
-    const uint64_t n = kb.n;
-    const uint32_t cap = (uint32_t)d.cap;
-    SessParams sp;
-    sp.gap = cfg.gap_ms;
-    sp.rec_base = a.rec_base;
-    sp.dyn_base = d.cap * kSessInline;
-    sp.batch_id = a.batch_id;
-    sp.emit_mode = cfg.emit_mode;
-    launch_stream_time(d, cfg, kb, a.wm_in, 1);
-    DTRY(hipEventRecord(d.ev_a, d.stream));
-    launch_ss_slot(d.stream, kb, d.ss, pb.pslot, pb.pidx, pb.cnt, d.sc);
-    scan_excl_u32(d.stream, pb.cnt, pb.off, n, pb.partial, pb.totals + 1);  // changelog positions, V
-    int which = radix_sort_pairs(d.stream, pb.pslot, pb.pidx, pb.k1, pb.v1, n, log2u(d.cap) + 1, pb.sort_scratch);
-    const uint32_t *slot = which ? pb.k1 : pb.pslot;
-    const uint32_t *ridx = which ? pb.v1 : pb.pidx;
-    launch_ss_runs(d.stream, slot, n, cap, pb.flags, nullptr, nullptr, 0);
-    scan_excl_u8(d.stream, pb.flags, pb.runidx, n, pb.partial, pb.totals + 2);  // R
-    launch_ss_runs(d.stream, slot, n, cap, pb.flags, pb.runidx, pb.runs, 1);
-    DTRY(hipMemcpyAsync(d.h_tmp, pb.totals, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
-    DTRY(hipStreamSynchronize(d.stream));
-    V = d.h_tmp[1];
-    const uint64_t R = d.h_tmp[2];
-    // runs[R] = V closes the last run (valid records sort before HSG_KEY_NONE)
-    uint32_t *v32 = (uint32_t *)(d.h_tmp + 4);  // pinned
-    *v32 = (uint32_t)V;
-    DTRY(hipMemcpyAsync(pb.runs + R, v32, sizeof(uint32_t), hipMemcpyHostToDevice, d.stream));
-    launch_ss_process(d.stream, kb, sp, d.ss, prog, slot, ridx, pb.runs, R, pb.off, seq, d.out, a.pending,
-                      d.arena_top, d.sc);
-    DTRY(hipEventRecord(d.ev_b, d.stream));
-    DTRY(hipGetLastError());
-  }
-  rc = finish_batch(d, a.wm_in, kb.n, r, err);
-  if (cfg.emit_mode == HSG_EMIT_PER_RECORD) r.out_rows = V;
-  r.pairs = V;
-  if (kb.n) {
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, d.ev_a, d.ev_b) == hipSuccess) r.agg_ms = ms;
-    r.agg_launches = 1;
-  }
-  return rc;
-}
-
-void launch_session_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, OutCols out, uint64_t cap,
-                         uint64_t *counter) {
-  launch_ss_dump(d.stream, d.ss, d.cap, prog, out, cap, counter);
 }
 
 }  // namespace hsg
