@@ -128,6 +128,9 @@ def main():
                 drain_dev()
         return wm_c.value
 
+    # the synthetic columns were produced on torch's stream, which the op's
+    # stream is not ordered after (include/hstream_gpu.h, hsg_batch)
+    torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -158,10 +161,9 @@ def main():
     # slots), E changelog rows, O row bytes (key 4, window 8 + 8, 8 per agg)
     launches = st1["agg_kernel_launches"] - st0["agg_kernel_launches"]
     agg_s = (st1["agg_kernel_ms"] - st0["agg_kernel_ms"]) / 1e3
-    n_slots = len(spec_state_slots(spec))
     ncol = len(spec.col_types)
     rec_bytes = 4 + 8 + 8 * ncol
-    row_bytes = 8 + 8 * n_slots
+    row_bytes = st1["state_row_bytes"]  # R of the device's own slot program (hsg_op_stats)
     out_bytes = 4 + 8 + 8 + 8 * len(spec.aggs) if emit != abi.HSG_EMIT_NONE else 0
     touched = st1["touched_total"] - st0["touched_total"]
     emitted = touched if emit == abi.HSG_EMIT_PER_BATCH else 0
@@ -175,7 +177,8 @@ def main():
         traffic, tsrc = committed_traffic(args, world)
     roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-            "kernel": "batch pipeline (k_part_hist, offsets, k_part_scatter[_st], k_part_agg, k_touch_emit)",
+            "kernel": pipeline_name(cfg, args.emit),
+            "state_row_bytes": row_bytes,
             "alg_bytes_per_launch": int(alg_bytes / max(1, launches)),
             "avg_launch_ms": round(agg_s * 1e3 / max(1, launches), 4)}
     if tsrc:
@@ -283,26 +286,16 @@ def make_device_drain(op, outs, cap, zero_copy=True):
     return drain
 
 
-def spec_state_slots(spec):
-    """State words per group (mirrors build_program in csrc/hsg_api.cpp)."""
+def pipeline_name(cfg, emit):
+    """The kernels one bench "launch" (a batch, HIP events on the op's stream) covers."""
     from hstream_amd import abi
-    slots = []
-    for kind, col in spec.aggs:
-        isf = kind != abi.HSG_COUNT_ALL and spec.col_types[col] == abi.HSG_F64
-        if kind == abi.HSG_COUNT_ALL:
-            need = [("cnt_all", 0)]
-        elif kind == abi.HSG_COUNT:
-            need = [("cnt", col)]
-        elif kind == abi.HSG_AVG:
-            need = [("sum", col), ("cnt", col)]
-        elif kind == abi.HSG_LAST:
-            need = [("lseq", col), ("lval", col)]
-        else:
-            need = [({2: "sum", 3: "min", 4: "max"}[kind], col, isf)]
-        for s in need:
-            if s not in slots:
-                slots.append(s)
-    return slots
+    if cfg.window_kind == abi.HSG_SESSION:
+        if emit == "per_record":
+            return "session replay (k_ss_slot, radix sort, k_ss_process)"
+        return "session merge (k_ss_phist, offsets, k_ss_pscatter, k_ss_sort, k_ss_apply)"
+    if emit == "per_record":
+        return "per-record changelog (k_pr_count, k_pr_expand, radix sort, k_seg_*)"
+    return "batch pipeline (k_part_hist_opt, offsets, k_part_scatter_st, k_part_agg, k_touch_emit)"
 
 
 def committed_traffic(args, world):
@@ -343,29 +336,92 @@ def traffic_from_csv(path, launches):
     return int((2 * fetch + write) * 1024 / len(n))
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_threads():
+    """Host threads this process may use: its CPU affinity, at most 16 (the GPU
+    box's CPU share per GPU; os.cpu_count() there reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def cpu_baseline(cfg, spec, seconds):
-    """The oracle (sequential restatement, ordered-map store) on a bounded sample
-    of the same workload, single thread, on this host."""
+    """The oracle (sequential restatement of the reference path: ordered-map
+    store) on a bounded sample of the same workload on this host:
+    one thread, as the reference runs one query on one Haskell thread
+    (Processor.hs:128-144), and key-partitioned over cpu_threads() threads
+    (one oracle op per thread, records routed by key hash; each partition keeps
+    its own stream time), the stronger CPU baseline SURVEY.md 8d asks for."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
     import pyoracle
+    from concurrent.futures import ThreadPoolExecutor
     from hstream_amd import abi, datagen
-    o = pyoracle.OracleOp(spec, faithful_sessions=True)
     chunk = 1 << 18
-    done = 0
-    wm = -1
-    t_used = 0.0
-    while t_used < seconds and done < cfg.n:
-        h = datagen.generate(cfg, n=chunk, start=done, total=cfg.n)
-        t0 = time.perf_counter()
-        wm = o.push(h["key_id"], h["ts"], h["cols"] if spec.col_types else [], None, watermark=wm)
-        if spec.emit_mode != abi.HSG_EMIT_NONE:
-            o.drain()
-        t_used += time.perf_counter() - t0
-        done += chunk
-    o.close()
-    return {"value": round(done / t_used, 1), "unit": "records/s", "cores": 1, "kind": "port",
-            "sample": f"first {done} records of {cfg.name} (same generator), oracle/hsoracle.cpp ordered-map "
-                      f"restatement, 1 thread, {os.cpu_count()} host CPUs visible"}
+
+    def run_single(budget):
+        o = pyoracle.OracleOp(spec, faithful_sessions=True)
+        done, wm, used = 0, -1, 0.0
+        while used < budget and done < cfg.n:
+            h = datagen.generate(cfg, n=chunk, start=done, total=cfg.n)
+            t0 = time.perf_counter()
+            wm = o.push(h["key_id"], h["ts"], h["cols"] if spec.col_types else [], None, watermark=wm)
+            if spec.emit_mode != abi.HSG_EMIT_NONE:
+                o.drain()
+            used += time.perf_counter() - t0
+            done += chunk
+        o.close()
+        return done, used
+
+    def run_parallel(budget, T):
+        ops = [pyoracle.OracleOp(spec, faithful_sessions=True) for _ in range(T)]
+        wms = [-1] * T
+        done, used = 0, 0.0
+
+        def work(k, parts):
+            key, ts, cols = parts[k]
+            wms[k] = ops[k].push(key, ts, cols, None, watermark=wms[k])
+            if spec.emit_mode != abi.HSG_EMIT_NONE:
+                ops[k].drain()
+
+        with ThreadPoolExecutor(T) as ex:
+            while used < budget and done < cfg.n:
+                h = datagen.generate(cfg, n=chunk * T, start=done, total=cfg.n)
+                part = (h["key_id"].astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15) >> np.uint64(40)) % np.uint64(T)
+                parts = []
+                for k in range(T):
+                    sel = part == k
+                    parts.append((h["key_id"][sel], h["ts"][sel], [c[sel] for c in h["cols"]] if spec.col_types else []))
+                t0 = time.perf_counter()
+                list(ex.map(lambda k: work(k, parts), range(T)))
+                used += time.perf_counter() - t0
+                done += chunk * T
+        for o in ops:
+            o.close()
+        return done, used
+
+    n1, t1 = run_single(seconds)
+    T = cpu_threads()
+    nT, tT = run_parallel(seconds, T) if T > 1 else (n1, t1)
+    return {"value": round(n1 / t1, 1), "unit": "records/s", "cores": 1, "kind": "port",
+            "sample": f"first {n1} records of {cfg.name} (same generator), oracle/hsoracle.cpp ordered-map "
+                      f"restatement, 1 thread",
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "key_partitioned": {"value": round(nT / tT, 1), "unit": "records/s", "cores": T,
+                                "sample": f"first {nT} records, {T} oracle ops, records routed by key hash"}}
 
 
 if __name__ == "__main__":

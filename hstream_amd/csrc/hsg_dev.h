@@ -46,6 +46,16 @@ __device__ inline uint64_t wave_incl_sum(uint64_t v) {
   return v;
 }
 
+// Workgroup barrier that orders LDS only: __syncthreads() also waits for the
+// wave's outstanding global stores (its workgroup-scope release), which costs
+// microseconds after a burst of scattered stores that no one in the workgroup
+// reads back. Use where the only data crossing the barrier is in LDS.
+__device__ inline void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ inline int64_t slot_identity_dev(int32_t op) {
   switch (op) {
     case S_MIN_I: return INT64_MAX;

@@ -19,23 +19,25 @@ int comm_split(const Comm *parent, Comm **out, std::string &err);
 void comm_destroy(Comm *c);
 
 // Session store in HBM (k_session.hip, hsg_session.h): a growable key table
-// (key -> slot) and per slot the key's sessions, sorted by start, in an arena.
-struct SessList {
-  uint64_t off;  // arena index of the first session
-  uint32_t len;
-  uint32_t cap;
+// of 32-byte entries (key, the key's session list, the per-batch emit mark)
+// and the sessions, sorted by start per key, as array-of-struct rows
+// [start][end][stamp][aggs...] in an arena: a key's hot tail is one or two lines.
+struct SessKey {
+  uint32_t key;    // kSessEmptyKey = free
+  uint32_t len;    // sessions
+  uint64_t off;    // arena row of the first session
+  uint32_t cap;    // rows reserved at off
+  uint32_t pad;
+  uint64_t emark;  // merge path: ~batch << 32 | lowest index the batch rewrote (~0 = none)
 };
+static_assert(sizeof(SessKey) == 32, "SessKey");
 struct SessTable {
-  uint32_t *keys;      // [kmask + 1] key id, kSessEmptyKey = free
-  SessList *lists;     // [kmask + 1]
-  uint64_t *emark;     // [kmask + 1] merge path: ~batch << 32 | lowest index the batch rewrote (~0 = none)
+  SessKey *kt;         // [kmask + 1]
   uint64_t kmask;
-  // arena, structure of arrays: start, end, stamp and n_slots agg words per session
-  int64_t *a_start;
-  int64_t *a_end;
-  uint32_t *a_stamp;
-  int64_t *a_aggs;     // [arena_cap][n_slots]
-  uint64_t arena_cap;
+  uint64_t *rows;      // [arena_cap][stride]
+  uint32_t stride;     // 3 + n_slots words
+  uint32_t ns;         // n_slots
+  uint64_t arena_cap;  // rows
   uint64_t *meta;      // [M_WORDS] device bookkeeping (hsg_session.h SessMeta)
 };
 
@@ -73,6 +75,7 @@ struct OpDevice {
   // sessions
   SessTable ss = {};
   uint64_t *h_meta = nullptr;     // pinned mirror of ss.meta
+  uint64_t *h_regions = nullptr;  // pinned staging of the arena regions
   uint64_t ss_keys = 0;           // live keys after the last batch (host mirror)
   uint64_t ss_live_max = 0;       // sessions the arena was last compacted for
   void *ss_part = nullptr;        // session partition scratch (tmax, progress)

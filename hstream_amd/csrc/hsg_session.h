@@ -1,18 +1,24 @@
-// Session windows (k_session.hip, sortpaths.cpp). Not part of the ABI.
+// Session windows (k_session.hip, session.cpp). Not part of the ABI.
 //
-// State (SessTable, hsg_ops.h): a growable open-addressing key table
-// (key -> slot) and, per slot, the key's sessions as a list sorted by start in
-// an HBM arena (structure of arrays). Sessions of one key stay more than `gap`
-// apart (the closure of SessionWindowedStream.hs:84-118 over the findSessions
-// test of Store.hs:243-272), so a point or a batch run touches one contiguous
-// stretch of the list. Lists are bump-allocated; the host compacts (and grows)
-// the arena and rehashes the key table between batches, never mid-batch.
+// State (SessTable, hsg_ops.h): a growable open-addressing key table (32-byte
+// entries: key, the key's list, an emit mark) and, per key, its sessions as a
+// list of array-of-struct rows sorted by start in an HBM arena. Sessions of one
+// key stay more than `gap` apart (the closure of SessionWindowedStream.hs:84-118
+// over the findSessions test of Store.hs:243-272), so a point or a batch run
+// touches one contiguous stretch of the list. Lists are bump-allocated; the
+// host compacts (and grows) the arena and rehashes the key table between
+// kernel passes, never inside one.
 //
 // Batch paths:
-//   merge   (per-batch / state-only emission, no LAST): key-hash partition,
-//           then one workgroup per bucket: chunks sorted by (key, ts) in LDS,
-//           gap-delimited runs, and per key a sweep-merge of its runs with the
-//           key's resident sessions (order-free: COUNT/SUM/MIN/MAX commute).
+//   merge   (per-batch / state-only emission, no LAST): key-hash partition;
+//           per bucket (k_ss_sort) sub-buckets by further key-hash bits, each
+//           grouped by key in an LDS hash table and written out sorted by
+//           (key, ts), one group record per key; then one thread per key
+//           (k_ss_apply) sweep-merges its points with its resident sessions
+//           (points closer than the gap chain into one session).
+//           Buckets whose sub-buckets do not fit one sort (hot keys) are merged
+//           chunk by chunk by one workgroup (k_ss_merge_big). Order-free: the
+//           aggregates commute.
 //   replay  (per-record changelog or LAST, where arrival order matters):
 //           stable sort by key slot, then the key's records replayed in
 //           arrival order against its list, exactly as the reference's fold.
@@ -25,14 +31,25 @@ namespace hsg {
 
 constexpr uint32_t kSessEmptyKey = 0xFFFFFFFFu;
 
+// The arena's free rows are split into regions, each with its own bump
+// pointer, so thousands of workgroups reserving lists do not serialise on one
+// atomic; a workgroup allocates from region (block id mod kArenaRegions).
+constexpr int kArenaRegions = 64;
+constexpr int kRegionStride = 16;  // words between region pointers: one 128-byte line each
+
 // arena bookkeeping words (device, SessTable::meta)
 enum SessMeta : int {
-  M_TOP = 0,        // arena bump pointer (sessions)
   M_KEYS = 1,       // live keys in the key table
-  M_NEED = 2,       // replay path: arena sessions its growth needs this batch
-  M_FAIL = 3,       // a workgroup could not reserve arena space (host compacts, resumes)
+  M_FAIL = 3,       // a workgroup could not reserve arena rows (the host compacts, then resumes)
   M_TLEN = 4,       // merge path: touched-list entries this batch
-  M_WORDS = 8
+  M_GRP = 5,        // merge path: key groups written by k_ss_sort
+  M_RUNS = 6,       // merge path: runs written by k_ss_sort
+  M_BIG = 7,        // merge path: buckets left to k_ss_merge_big
+  M_SCRATCH = 15,   // device landing word (compaction total)
+  M_RNEED = 16,                              // [kArenaRegions] replay path: rows its list growth needs
+  M_RTOP = M_RNEED + kArenaRegions,          // [kArenaRegions x kRegionStride] region bump pointers
+  M_REND = M_RTOP + 1,                       //   and ends, interleaved
+  M_WORDS = M_RTOP + kArenaRegions * kRegionStride
 };
 
 struct SessParams {
@@ -46,13 +63,13 @@ struct SessParams {
 constexpr int kSessMaxWords = 2 + kMaxCols;
 
 void launch_ss_reset(hipStream_t s, const SessTable &t);
-// key table into a new table of new_cap slots (keys, list metadata)
+// key table into a larger one (keys, lists; emit marks start clear)
 void launch_ss_rehash(hipStream_t s, const SessTable &from, const SessTable &to);
 // arena compaction: plan (new caps = next pow2 of len + 1, >= 4; total ->
 // *total), then every list copied into `to`'s arena (same key table)
 uint64_t ss_compact_scratch_bytes(uint64_t kcap);
 void launch_ss_compact_plan(hipStream_t s, const SessTable &t, void *scratch, uint64_t *total);
-void launch_ss_compact_copy(hipStream_t s, const SessTable &from, const SessTable &to, int n_slots, void *scratch);
+void launch_ss_compact_copy(hipStream_t s, const SessTable &from, const SessTable &to, void *scratch);
 
 // replay path
 void launch_ss_slot(hipStream_t s, const Batch &b, const SessTable &t, uint32_t *rslot, uint32_t *ridx,
@@ -60,7 +77,7 @@ void launch_ss_slot(hipStream_t s, const Batch &b, const SessTable &t, uint32_t 
 // phase 0: head flags; phase 1: compact run starts using runidx = exclusive scan of flags
 void launch_ss_runs(hipStream_t s, const uint32_t *slot, uint64_t n, uint32_t cap, uint8_t *flag,
                     const uint64_t *runidx, uint32_t *runs, int phase);
-// arena sessions the replay's list growth needs (-> meta[M_NEED])
+// arena rows the replay's list growth needs (-> meta[M_NEED]) and the all-or-nothing check
 void launch_ss_replay_need(hipStream_t s, const SessTable &t, const uint32_t *slot, const uint32_t *runs, uint64_t R);
 void launch_ss_process(hipStream_t s, const Batch &b, const SessParams &p, const SessTable &t, const Program &prog,
                        const uint32_t *slot, const uint32_t *ridx, const uint32_t *runs, uint64_t R,
@@ -71,18 +88,31 @@ struct SessPart {
   uint32_t *hist;      // [tiles][nb]
   uint32_t *offt;      // [tiles][nb]
   uint64_t *bstart;    // [nb + 1]
-  uint64_t *rec;       // [n * words]
+  uint64_t *rec;       // [n * words] partitioned records
   uint64_t *tmax;      // [tiles] ts max image per tile (stream time)
-  uint32_t *progress;  // [nb] chunks of each bucket applied (resumable after an arena refill)
-  uint32_t *touched;   // [n] key slots a chunk rewrote (one entry per chunk and key)
+  uint32_t *progress;  // [nb] chunks of each big bucket applied (resumable after an arena refill)
+  uint32_t *touched;   // [n] key slots rewritten (a big bucket: one entry per chunk and key)
+  uint64_t *srec;      // [n][words] records sorted by (key, ts): ts, word 0, columns
+  uint32_t *groups;    // [n][4] key groups: key, first record in srec, records, -
+  uint8_t *done;       // [n / 256 + 1] apply blocks done (resumable)
+  uint64_t *bigmask;   // [nb] sub-buckets left to k_ss_merge_big
+  uint16_t *sidx;      // [n] per bucket: its record indices grouped by sub-bucket
+  uint32_t *gsparse;   // [n][4] group records at their sub-bucket's record positions
 };
-void launch_ss_phist(hipStream_t s, const Batch &b, int np_log2, uint64_t tiles, const SessPart &sp);
+// bshift: owner bits of the key hash above the bucket bits (multi-GPU)
+void launch_ss_phist(hipStream_t s, const Batch &b, int np_log2, int bshift, uint64_t tiles, const SessPart &sp);
 void launch_ss_wm(hipStream_t s, const SessPart &sp, uint64_t tiles, int64_t wm_in, DevScalars *sc);
-void launch_ss_pscatter(hipStream_t s, const Batch &b, int np_log2, uint64_t tiles, int words, bool has_valid,
-                        const SessPart &sp);
-void launch_ss_merge(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, int np_log2,
-                     int words, const SessPart &sp, DevScalars *sc);
-// per-batch changelog of the merge path (emit = 0: count the touched sessions only)
+void launch_ss_pscatter(hipStream_t s, const Batch &b, int np_log2, int bshift, uint64_t tiles, int words,
+                        bool has_valid, const SessPart &sp);
+void launch_ss_sort(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, int np_log2,
+                    int bshift, int words, const SessPart &sp, DevScalars *sc);
+// n_bound: records of the batch (an upper bound on the groups); writes the
+// changelog rows of its keys at out_base + sc->out_rows
+void launch_ss_apply(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, uint64_t n_bound,
+                     int words, const SessPart &sp, OutCols out, uint64_t out_base, DevScalars *sc);
+void launch_ss_merge_big(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, int np_log2,
+                         int bshift, int words, const SessPart &sp, DevScalars *sc);
+// per-batch changelog of the keys k_ss_merge_big touched (emit = 0: count only)
 void launch_ss_emit(hipStream_t s, const SessTable &t, const Program &prog, const SessPart &sp, uint32_t batch_id,
                     int emit, uint64_t n_bound, OutCols out, uint64_t out_base, DevScalars *sc);
 

@@ -8,15 +8,34 @@
 namespace hsg {
 
 // ---------------------------------------------------------------------------
-// key table
+// store helpers: key entries, session rows [start][end][stamp][aggs...]
 // ---------------------------------------------------------------------------
+__device__ inline uint64_t *ss_row(const SessTable &t, uint64_t i) { return t.rows + i * t.stride; }
+
+__device__ inline void ss_copy(const SessTable &dt, uint64_t dst, const SessTable &st, uint64_t src) {
+  const uint64_t *a = ss_row(st, src);
+  uint64_t *b = ss_row(dt, dst);
+  for (uint32_t w = 0; w < st.stride; ++w) b[w] = a[w];
+}
+
+// rows [base, base + n) from arena region r (bump); false when the region is
+// exhausted (the host then compacts the arena and re-partitions the regions)
+__device__ inline bool arena_take(const SessTable &t, uint32_t r, uint64_t n, uint64_t &base) {
+  base = atomicAdd((unsigned long long *)&t.meta[M_RTOP + r * kRegionStride], (unsigned long long)n);
+  return base + n <= t.meta[M_REND + r * kRegionStride];
+}
+__device__ inline uint32_t arena_region(uint32_t block) { return block % kArenaRegions; }
+
+__device__ inline uint32_t ss_grow_cap(uint64_t need) {
+  uint32_t c = 4;
+  while (c < need) c <<= 1;
+  return c;
+}
+
 __global__ void k_ss_reset(SessTable t) {
   const uint64_t cap = t.kmask + 1;
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap; s += (uint64_t)gridDim.x * blockDim.x) {
-    t.keys[s] = kSessEmptyKey;
-    t.lists[s] = SessList{0, 0, 0};
-    t.emark[s] = ~0ull;
-  }
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap; s += (uint64_t)gridDim.x * blockDim.x)
+    t.kt[s] = SessKey{kSessEmptyKey, 0, 0, 0, 0, ~0ull};
 }
 
 void launch_ss_reset(hipStream_t s, const SessTable &t) {
@@ -24,15 +43,15 @@ void launch_ss_reset(hipStream_t s, const SessTable &t) {
 }
 
 // find key's slot, inserting it if absent; -1 = table full. `inserted` is set
-// when this call claimed the slot.
+// when this call claimed the slot (its entry then still holds an empty list).
 __device__ inline int64_t ss_find_or_insert(const SessTable &t, uint32_t key, bool &inserted) {
   uint64_t s = mix64(key) & t.kmask;
   inserted = false;
   for (uint64_t probe = 0; probe <= t.kmask; ++probe) {
-    uint32_t cur = t.keys[s];
+    const uint32_t cur = t.kt[s].key;
     if (cur == key) return (int64_t)s;
     if (cur == kSessEmptyKey) {
-      uint32_t old = atomicCAS(&t.keys[s], kSessEmptyKey, key);
+      const uint32_t old = atomicCAS(&t.kt[s].key, kSessEmptyKey, key);
       if (old == kSessEmptyKey) {
         inserted = true;
         return (int64_t)s;
@@ -47,11 +66,11 @@ __device__ inline int64_t ss_find_or_insert(const SessTable &t, uint32_t key, bo
 __global__ void k_ss_rehash(SessTable from, SessTable to) {
   const uint64_t cap = from.kmask + 1;
   for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap; s += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t key = from.keys[s];
-    if (key == kSessEmptyKey) continue;
+    const SessKey e = from.kt[s];
+    if (e.key == kSessEmptyKey) continue;
     bool ins;
-    const int64_t d = ss_find_or_insert(to, key, ins);
-    if (d >= 0) to.lists[d] = from.lists[s];  // `to` is at most half full: d >= 0
+    const int64_t d = ss_find_or_insert(to, e.key, ins);  // `to` is at most half full: d >= 0
+    if (d >= 0) to.kt[d] = SessKey{e.key, e.len, e.off, e.cap, 0, ~0ull};
   }
 }
 
@@ -61,37 +80,26 @@ void launch_ss_rehash(hipStream_t s, const SessTable &from, const SessTable &to)
 }
 
 // ---------------------------------------------------------------------------
-// arena: session copies and compaction
+// arena compaction
 // ---------------------------------------------------------------------------
-__device__ inline void ss_copy(const SessTable &dt, uint64_t dst, const SessTable &st, uint64_t src, int ns) {
-  dt.a_start[dst] = st.a_start[src];
-  dt.a_end[dst] = st.a_end[src];
-  dt.a_stamp[dst] = st.a_stamp[src];
-  for (int s = 0; s < ns; ++s) dt.a_aggs[dst * ns + s] = st.a_aggs[src * ns + s];
-}
-
-__device__ inline uint32_t ss_grow_cap(uint64_t need) {
-  uint32_t c = 4;
-  while (c < need) c <<= 1;
-  return c;
-}
-
 __global__ void k_ss_ccount(SessTable t, uint32_t *newcap) {
   const uint64_t cap = t.kmask + 1;
   for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap; s += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t len = t.keys[s] == kSessEmptyKey ? 0u : t.lists[s].len;
+    const SessKey e = t.kt[s];
+    const uint32_t len = e.key == kSessEmptyKey ? 0u : e.len;
     newcap[s] = len ? ss_grow_cap((uint64_t)len + 1) : 0u;
   }
 }
 
-__global__ void k_ss_ccopy(SessTable from, SessTable to, int ns, const uint32_t *newcap, const uint64_t *newoff) {
+__global__ void k_ss_ccopy(SessTable from, SessTable to, const uint32_t *newcap, const uint64_t *newoff) {
   const uint64_t cap = from.kmask + 1;
   for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap; s += (uint64_t)gridDim.x * blockDim.x) {
-    if (from.keys[s] == kSessEmptyKey) continue;
-    const SessList L = from.lists[s];
+    const SessKey e = from.kt[s];
+    if (e.key == kSessEmptyKey) continue;
     const uint64_t o = newoff[s];
-    for (uint32_t k = 0; k < L.len; ++k) ss_copy(to, o + k, from, L.off + k, ns);
-    to.lists[s] = SessList{o, L.len, newcap[s]};
+    for (uint32_t k = 0; k < e.len; ++k) ss_copy(to, o + k, from, e.off + k);
+    to.kt[s].off = o;
+    to.kt[s].cap = newcap[s];
   }
 }
 
@@ -106,8 +114,6 @@ static void compact_views(void *scratch, uint64_t kcap, uint32_t *&newcap, uint6
   partial = (uint64_t *)((char *)newoff + (((kcap + 1) * 8 + 255) & ~255ull));
 }
 
-// new list capacities and their offsets; the total (the compacted arena's
-// top) -> *total (device)
 void launch_ss_compact_plan(hipStream_t s, const SessTable &t, void *scratch, uint64_t *total) {
   const uint64_t kcap = t.kmask + 1;
   uint32_t *newcap;
@@ -117,14 +123,12 @@ void launch_ss_compact_plan(hipStream_t s, const SessTable &t, void *scratch, ui
   scan_excl_u32(s, newcap, newoff, kcap, partial, total);
 }
 
-// every list copied into `to`'s arena (to shares the key table with from;
-// lists are rewritten in place)
-void launch_ss_compact_copy(hipStream_t s, const SessTable &from, const SessTable &to, int n_slots, void *scratch) {
+void launch_ss_compact_copy(hipStream_t s, const SessTable &from, const SessTable &to, void *scratch) {
   const uint64_t kcap = from.kmask + 1;
   uint32_t *newcap;
   uint64_t *newoff, *partial;
   compact_views(scratch, kcap, newcap, newoff, partial);
-  hipLaunchKernelGGL(k_ss_ccopy, dim3(grid_for(kcap, 256)), dim3(256), 0, s, from, to, n_slots, newcap, newoff);
+  hipLaunchKernelGGL(k_ss_ccopy, dim3(grid_for(kcap, 256)), dim3(256), 0, s, from, to, newcap, newoff);
 }
 
 // ---------------------------------------------------------------------------
@@ -138,10 +142,9 @@ __global__ void k_ss_slot(Batch b, SessTable t, uint32_t *rslot, uint32_t *ridx,
   for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < b.n; i0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t i = i0 + threadIdx.x;
     bool ins = false;
-    uint32_t sl = cap;
-    uint32_t key = HSG_KEY_NONE;
     if (i < b.n) {
-      key = b.key[i];
+      const uint32_t key = b.key[i];
+      uint32_t sl = cap;
       if (key != HSG_KEY_NONE) {
         const int64_t s = ss_find_or_insert(t, key, ins);
         if (s < 0) err |= ERR_OOM;
@@ -179,42 +182,50 @@ void launch_ss_runs(hipStream_t s, const uint32_t *slot, uint64_t n, uint32_t ca
   else hipLaunchKernelGGL(k_ss_runs, dim3(grid_for(n, 256)), dim3(256), 0, s, flag, runidx, n, runs);
 }
 
-// arena sessions the replay's list growth needs, then the all-or-nothing
-// decision (one workgroup, after every need has been added)
+// arena rows the replay's list growth needs, then the all-or-nothing decision
+// (one thread, after every need has been added)
+// (k_ss_process block q takes runs [256 q, 256 q + 256) and allocates from
+// region arena_region(q): the need is summed per region)
 __global__ __launch_bounds__(256) void k_ss_replay_need(SessTable t, const uint32_t *slot, const uint32_t *runs,
                                                         uint64_t R) {
+  const uint64_t r = blockIdx.x * 256ull + threadIdx.x;
   uint64_t need = 0;
-  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
-    const SessList L = t.lists[slot[runs[r]]];
-    const uint64_t want = (uint64_t)L.len + (runs[r + 1] - runs[r]);
-    if (want > L.cap) need += ss_grow_cap(want);
+  if (r < R) {
+    const SessKey e = t.kt[slot[runs[r]]];
+    const uint64_t want = (uint64_t)e.len + (runs[r + 1] - runs[r]);
+    if (want > e.cap) need = ss_grow_cap(want);
   }
   need = wave_sum_u64(need);
-  if ((threadIdx.x & 63) == 0 && need) atomicAdd((unsigned long long *)&t.meta[M_NEED], (unsigned long long)need);
+  if ((threadIdx.x & 63) == 0 && need)
+    atomicAdd((unsigned long long *)&t.meta[M_RNEED + arena_region(blockIdx.x)], (unsigned long long)need);
 }
 __global__ void k_ss_replay_check(SessTable t) {
-  if (t.meta[M_TOP] + t.meta[M_NEED] > t.arena_cap) t.meta[M_FAIL] = 1;
+  const int r = threadIdx.x;
+  if (r < kArenaRegions && t.meta[M_RTOP + r * kRegionStride] + t.meta[M_RNEED + r] > t.meta[M_REND + r * kRegionStride])
+    t.meta[M_FAIL] = 1;
 }
 
 void launch_ss_replay_need(hipStream_t s, const SessTable &t, const uint32_t *slot, const uint32_t *runs, uint64_t R) {
-  if (R) {
-    uint64_t blocks = (R + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(k_ss_replay_need, dim3((unsigned)blocks), dim3(256), 0, s, t, slot, runs, R);
-  }
-  hipLaunchKernelGGL(k_ss_replay_check, dim3(1), dim3(1), 0, s, t);
+  if (R) hipLaunchKernelGGL(k_ss_replay_need, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, t, slot, runs, R);
+  hipLaunchKernelGGL(k_ss_replay_check, dim3(1), dim3(kArenaRegions), 0, s, t);
 }
 
 template <int MS>
-__device__ inline void ss_load(const SessTable &t, int ns, uint64_t idx, int64_t (&a)[MS]) {
+__device__ inline void ss_load(const SessTable &t, uint64_t idx, int64_t (&a)[MS]) {
+  const uint64_t *r = ss_row(t, idx) + 3;
 #pragma unroll
-  for (int s = 0; s < MS; ++s) a[s] = s < ns ? t.a_aggs[idx * ns + s] : 0;
+  for (int s = 0; s < MS; ++s) a[s] = s < (int)t.ns ? (int64_t)r[s] : 0;
 }
 template <int MS>
-__device__ inline void ss_store(const SessTable &t, int ns, uint64_t idx, const int64_t (&a)[MS]) {
+__device__ inline void ss_store(const SessTable &t, uint64_t idx, int64_t st, int64_t en, uint32_t stamp,
+                                const int64_t (&a)[MS]) {
+  uint64_t *r = ss_row(t, idx);
+  r[0] = (uint64_t)st;
+  r[1] = (uint64_t)en;
+  r[2] = stamp;
 #pragma unroll
   for (int s = 0; s < MS; ++s)
-    if (s < ns) t.a_aggs[idx * ns + s] = a[s];
+    if (s < (int)t.ns) r[3 + s] = (uint64_t)a[s];
 }
 
 // One thread per touched key replays the key's records in arrival order
@@ -235,31 +246,32 @@ __global__ __launch_bounds__(256) void k_ss_process(Batch b, SessParams p, SessT
   const int ns = prog.n_slots;
   const bool active = r < R;
   uint64_t q0 = 0, q1 = 0;
-  uint32_t sl = 0, key = 0;
-  SessList L = {0, 0, 0};
+  uint32_t sl = 0;
+  SessKey e = {0, 0, 0, 0, 0, 0};
   int64_t live_delta = 0;
   if (active) {
     q0 = runs[r];
     q1 = runs[r + 1];
     sl = slot[q0];
-    key = t.keys[sl];
-    L = t.lists[sl];
+    e = t.kt[sl];
   }
+  const uint32_t key = e.key;
   // grow the key's list once for the whole run (each record adds <= 1
-  // session); one arena bump per wave, within what k_ss_replay_need reserved
-  const uint64_t want = (uint64_t)L.len + (q1 - q0);
-  const uint64_t new_cap = (active && want > L.cap) ? ss_grow_cap(want) : 0;
+  // session); one arena bump per wave, within what k_ss_replay_need checked
+  const uint64_t want = (uint64_t)e.len + (q1 - q0);
+  const uint64_t new_cap = (active && want > e.cap) ? ss_grow_cap(want) : 0;
   const uint64_t incl = wave_incl_sum(new_cap);
   const uint64_t wtot = __shfl(incl, 63, 64);
   uint64_t wbase = 0;
-  if (lane == 63 && wtot) wbase = atomicAdd((unsigned long long *)&t.meta[M_TOP], (unsigned long long)wtot);
+  if (lane == 63 && wtot) arena_take(t, arena_region(blockIdx.x), wtot, wbase);  // within the checked need
   wbase = __shfl(wbase, 63, 64);
-  uint64_t off = L.off, len = L.len;
+  uint64_t off = e.off, len = e.len;
+  uint32_t lcap = e.cap;
   if (new_cap) {
     const uint64_t noff = wbase + incl - new_cap;
-    for (uint64_t k = 0; k < len; ++k) ss_copy(t, noff + k, t, off + k, ns);
+    for (uint64_t k = 0; k < len; ++k) ss_copy(t, noff + k, t, off + k);
     off = noff;
-    L.cap = (uint32_t)new_cap;
+    lcap = (uint32_t)new_cap;
   }
   if (active) {
     for (uint64_t q = q0; q < q1; ++q) {
@@ -272,24 +284,25 @@ __global__ __launch_bounds__(256) void k_ss_process(Batch b, SessParams p, SessT
       uint64_t a = 0, z = len;
       while (a < z) {
         const uint64_t m = (a + z) >> 1;
-        if (t.a_end[off + m] < lo) a = m + 1;
+        if ((int64_t)ss_row(t, off + m)[1] < lo) a = m + 1;
         else z = m;
       }
       const uint64_t i0 = a;
       uint64_t i1 = i0;
-      while (i1 < len && t.a_start[off + i1] <= hi) ++i1;
+      while (i1 < len && (int64_t)ss_row(t, off + i1)[0] <= hi) ++i1;
       // aggF initialValue r, then mergeF acc cur over the overlapped sessions
-      int64_t acc[MS], e[MS];
+      int64_t acc[MS], ev[MS];
       identity_row<MS>(prog, acc);
-      elem_row<MS>(prog, e, b, i, seq1);
-      combine_row<MS>(prog, acc, e);
+      elem_row<MS>(prog, ev, b, i, seq1);
+      combine_row<MS>(prog, acc, ev);
       int64_t s0 = ts, e0 = ts;
       for (uint64_t k = i0; k < i1; ++k) {
-        const int64_t cs = t.a_start[off + k], ce = t.a_end[off + k];
+        const uint64_t *row = ss_row(t, off + k);
+        const int64_t cs = (int64_t)row[0], ce = (int64_t)row[1];
         s0 = cs < s0 ? cs : s0;
         e0 = ce > e0 ? ce : e0;
         int64_t cur[MS];
-        ss_load<MS>(t, ns, off + k, cur);
+        ss_load<MS>(t, off + k, cur);
         combine_row<MS>(prog, acc, cur);
         // passthrough columns: aggregateMergeF _ _ o2 keeps the existing
         // session's value (Codegen.hs:467), so after the fold the last
@@ -301,17 +314,14 @@ __global__ __launch_bounds__(256) void k_ss_process(Batch b, SessParams p, SessT
       const uint64_t c = i1 - i0;
       if (c == 0) {
         // insert at i0: near-sorted arrivals append (i0 == len), nothing moves
-        for (uint64_t k = len; k > i0; --k) ss_copy(t, off + k, t, off + k - 1, ns);
+        for (uint64_t k = len; k > i0; --k) ss_copy(t, off + k, t, off + k - 1);
         len += 1;
       } else if (c > 1) {
-        for (uint64_t k = i1; k < len; ++k) ss_copy(t, off + k - (c - 1), t, off + k, ns);
+        for (uint64_t k = i1; k < len; ++k) ss_copy(t, off + k - (c - 1), t, off + k);
         len -= c - 1;
       }
       live_delta += 1 - (int64_t)c;
-      t.a_start[off + i0] = s0;
-      t.a_end[off + i0] = e0;
-      t.a_stamp[off + i0] = p.batch_id;
-      ss_store<MS>(t, ns, off + i0, acc);
+      ss_store<MS>(t, off + i0, s0, e0, p.batch_id, acc);
       if (p.emit_mode == HSG_EMIT_PER_RECORD) {
         const uint64_t o = out_base + out_pos[i];
         out.key[o] = key;
@@ -321,12 +331,14 @@ __global__ __launch_bounds__(256) void k_ss_process(Batch b, SessParams p, SessT
         for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value_reg<MS>(prog, j, acc);
       }
     }
-    t.lists[sl] = SessList{off, (uint32_t)len, L.cap};
+    t.kt[sl].off = off;
+    t.kt[sl].len = (uint32_t)len;
+    t.kt[sl].cap = lcap;
   }
   // per-batch changelog: the key's sessions stamped by this batch
   uint64_t mine = 0;
   if (active && p.emit_mode == HSG_EMIT_PER_BATCH)
-    for (uint64_t k = 0; k < len; ++k) mine += t.a_stamp[off + k] == p.batch_id;
+    for (uint64_t k = 0; k < len; ++k) mine += (uint32_t)ss_row(t, off + k)[2] == p.batch_id;
   const uint64_t inc2 = wave_incl_sum(mine);
   if (lane == 63) swave[w] = inc2;
   __syncthreads();
@@ -340,13 +352,13 @@ __global__ __launch_bounds__(256) void k_ss_process(Batch b, SessParams p, SessT
     uint64_t o = out_base + sbase + inc2 - mine;
     for (int k = 0; k < w; ++k) o += swave[k];
     for (uint64_t k = 0; k < len; ++k) {
-      if (t.a_stamp[off + k] != p.batch_id) continue;
+      const uint64_t *row = ss_row(t, off + k);
+      if ((uint32_t)row[2] != p.batch_id) continue;
       out.key[o] = key;
-      out.ws[o] = t.a_start[off + k];
-      out.we[o] = t.a_end[off + k];
+      out.ws[o] = (int64_t)row[0];
+      out.we[o] = (int64_t)row[1];
       out.src[o] = -1;
-      const int64_t *row = t.a_aggs + (off + k) * ns;
-      for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, row);
+      for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, (const int64_t *)row + 3);
       ++o;
     }
   }
@@ -381,14 +393,16 @@ constexpr int kSsTile = 4096;     // records per partition tile (= kPartTileRecs
 constexpr int kSsPNT = 512;       // threads of the partition passes
 constexpr int kSsSub = 1024;      // records per scatter sub-tile (LDS staging)
 
-__device__ inline uint32_t ss_bucket(uint32_t key, int np_log2) {
-  return np_log2 ? (uint32_t)(key_hash(key) >> (64 - np_log2)) : 0u;
+// bucket = the np_log2 key-hash bits below the `bshift` owner bits (multi-GPU:
+// the owner of a key is the top log2(G) bits, so they carry no information here)
+__device__ inline uint32_t ss_bucket(uint32_t key, int np_log2, int bshift) {
+  return np_log2 ? (uint32_t)((key_hash(key) << bshift) >> (64 - np_log2)) : 0u;
 }
 __device__ inline uint64_t i64_img(int64_t v) { return (uint64_t)v ^ 0x8000000000000000ull; }
 
 // per-tile bucket counts of the keyed records, tile-major; per-tile max ts
 // image of EVERY record (stream time counts filtered records too)
-__global__ __launch_bounds__(kSsPNT) void k_ss_phist(Batch b, int np_log2, SessPart sp) {
+__global__ __launch_bounds__(kSsPNT) void k_ss_phist(Batch b, int np_log2, int bshift, SessPart sp) {
   __shared__ uint32_t cnt[1 << 11];
   __shared__ uint64_t smx[kSsPNT / 64];
   const int nb = 1 << np_log2;
@@ -404,7 +418,7 @@ __global__ __launch_bounds__(kSsPNT) void k_ss_phist(Batch b, int np_log2, SessP
     const uint32_t key = b.key[i];
     const uint64_t o = i64_img(b.ts[i]);
     mx = o > mx ? o : mx;
-    if (key != HSG_KEY_NONE) atomicAdd(&cnt[ss_bucket(key, np_log2)], 1u);
+    if (key != HSG_KEY_NONE) atomicAdd(&cnt[ss_bucket(key, np_log2, bshift)], 1u);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -420,8 +434,8 @@ __global__ __launch_bounds__(kSsPNT) void k_ss_phist(Batch b, int np_log2, SessP
   }
 }
 
-void launch_ss_phist(hipStream_t s, const Batch &b, int np_log2, uint64_t tiles, const SessPart &sp) {
-  if (tiles) hipLaunchKernelGGL(k_ss_phist, dim3((unsigned)tiles), dim3(kSsPNT), 0, s, b, np_log2, sp);
+void launch_ss_phist(hipStream_t s, const Batch &b, int np_log2, int bshift, uint64_t tiles, const SessPart &sp) {
+  if (tiles) hipLaunchKernelGGL(k_ss_phist, dim3((unsigned)tiles), dim3(kSsPNT), 0, s, b, np_log2, bshift, sp);
 }
 
 // stream time after the batch (Processor.hs:139: max over every polled record)
@@ -450,7 +464,7 @@ void launch_ss_wm(hipStream_t s, const SessPart &sp, uint64_t tiles, int64_t wm_
 // counting-sorted by bucket into an LDS copy and written out with consecutive
 // lanes on consecutive words of a run. Record: [key | valid bits << 32] [ts] [cols].
 template <int W>
-__global__ __launch_bounds__(kSsPNT) void k_ss_pscatter(Batch b, int np_log2, int has_valid, SessPart sp) {
+__global__ __launch_bounds__(kSsPNT) void k_ss_pscatter(Batch b, int np_log2, int bshift, int has_valid, SessPart sp) {
   __shared__ uint64_t stage[kSsSub * W];
   __shared__ uint32_t cursor[1 << 11];  // records of each bucket placed by earlier sub-tiles
   __shared__ uint32_t scnt[1 << 11];    // this sub-tile
@@ -474,7 +488,7 @@ __global__ __launch_bounds__(kSsPNT) void k_ss_pscatter(Batch b, int np_log2, in
     for (int r = 0; r < R; ++r) {
       const uint64_t i = base + (uint64_t)r * kSsPNT + threadIdx.x;
       key[r] = i < b.n ? b.key[i] : HSG_KEY_NONE;
-      pos[r] = key[r] != HSG_KEY_NONE ? atomicAdd(&scnt[ss_bucket(key[r], np_log2)], 1u) : ~0u;
+      pos[r] = key[r] != HSG_KEY_NONE ? atomicAdd(&scnt[ss_bucket(key[r], np_log2, bshift)], 1u) : ~0u;
     }
     __syncthreads();
     // sub-tile exclusive scan of the bucket counts -> LDS run starts
@@ -503,7 +517,7 @@ __global__ __launch_bounds__(kSsPNT) void k_ss_pscatter(Batch b, int np_log2, in
     for (int r = 0; r < R; ++r) {
       if (pos[r] == ~0u) continue;
       const uint64_t i = base + (uint64_t)r * kSsPNT + threadIdx.x;
-      const uint32_t bk = ss_bucket(key[r], np_log2);
+      const uint32_t bk = ss_bucket(key[r], np_log2, bshift);
       const uint32_t q = lstart[bk] + pos[r];
       uint64_t vb = 0;
 #pragma unroll
@@ -523,37 +537,33 @@ __global__ __launch_bounds__(kSsPNT) void k_ss_pscatter(Batch b, int np_log2, in
       const uint64_t dest = (uint64_t)orow[bk] + cursor[bk] + (q - lstart[bk]);
       sp.rec[dest * W + w] = stage[t];
     }
-    __syncthreads();
+    lds_barrier();  // the next sub-tile reuses the LDS stage only
     for (int i = threadIdx.x; i < nb; i += kSsPNT) cursor[i] += scnt[i];
   }
 }
 
-void launch_ss_pscatter(hipStream_t s, const Batch &b, int np_log2, uint64_t tiles, int words, bool has_valid,
-                        const SessPart &sp) {
+void launch_ss_pscatter(hipStream_t s, const Batch &b, int np_log2, int bshift, uint64_t tiles, int words,
+                        bool has_valid, const SessPart &sp) {
   if (!tiles) return;
   const dim3 g((unsigned)tiles), th(kSsPNT);
   const int hv = has_valid ? 1 : 0;
   switch (words) {
-    case 2: hipLaunchKernelGGL(k_ss_pscatter<2>, g, th, 0, s, b, np_log2, hv, sp); break;
-    case 3: hipLaunchKernelGGL(k_ss_pscatter<3>, g, th, 0, s, b, np_log2, hv, sp); break;
-    case 4: hipLaunchKernelGGL(k_ss_pscatter<4>, g, th, 0, s, b, np_log2, hv, sp); break;
-    case 5: hipLaunchKernelGGL(k_ss_pscatter<5>, g, th, 0, s, b, np_log2, hv, sp); break;
-    case 6: hipLaunchKernelGGL(k_ss_pscatter<6>, g, th, 0, s, b, np_log2, hv, sp); break;
-    case 7: hipLaunchKernelGGL(k_ss_pscatter<7>, g, th, 0, s, b, np_log2, hv, sp); break;
-    case 8: hipLaunchKernelGGL(k_ss_pscatter<8>, g, th, 0, s, b, np_log2, hv, sp); break;
-    case 9: hipLaunchKernelGGL(k_ss_pscatter<9>, g, th, 0, s, b, np_log2, hv, sp); break;
-    default: hipLaunchKernelGGL(k_ss_pscatter<10>, g, th, 0, s, b, np_log2, hv, sp); break;
+    case 2: hipLaunchKernelGGL(k_ss_pscatter<2>, g, th, 0, s, b, np_log2, bshift, hv, sp); break;
+    case 3: hipLaunchKernelGGL(k_ss_pscatter<3>, g, th, 0, s, b, np_log2, bshift, hv, sp); break;
+    case 4: hipLaunchKernelGGL(k_ss_pscatter<4>, g, th, 0, s, b, np_log2, bshift, hv, sp); break;
+    case 5: hipLaunchKernelGGL(k_ss_pscatter<5>, g, th, 0, s, b, np_log2, bshift, hv, sp); break;
+    case 6: hipLaunchKernelGGL(k_ss_pscatter<6>, g, th, 0, s, b, np_log2, bshift, hv, sp); break;
+    case 7: hipLaunchKernelGGL(k_ss_pscatter<7>, g, th, 0, s, b, np_log2, bshift, hv, sp); break;
+    case 8: hipLaunchKernelGGL(k_ss_pscatter<8>, g, th, 0, s, b, np_log2, bshift, hv, sp); break;
+    case 9: hipLaunchKernelGGL(k_ss_pscatter<9>, g, th, 0, s, b, np_log2, bshift, hv, sp); break;
+    default: hipLaunchKernelGGL(k_ss_pscatter<10>, g, th, 0, s, b, np_log2, bshift, hv, sp); break;
   }
 }
 
 // ---------------------------------------------------------------------------
-// merge path: per-bucket sort, gap-delimited runs, sweep-merge with the
-// resident sessions
+// merge path: runs and the sweep-merge of a key's runs with its sessions
 // ---------------------------------------------------------------------------
-constexpr int kMgNT = 512;               // threads
-constexpr int kMgCH = 2048;              // records per chunk
-constexpr int kMgPer = kMgCH / kMgNT;    // records / runs / groups per thread
-constexpr int kMgTail = 2;               // resident sessions a group may rewrite in place
+constexpr int kMgTail = 2;  // resident sessions a key may rewrite in place (held in registers)
 
 // contribution of one partitioned record to the slots (identity when absent)
 template <int MS>
@@ -589,23 +599,732 @@ __device__ inline void acc_row(const Program &prog, int64_t (&a)[MS], const int6
     if (s < prog.n_slots) a[s] = slot_combine(prog.slot_op[s], a[s], e[s]);
 }
 
+// One session of the sweep: start, end, aggregates, and whether a batch run
+// is in it (-> stamped with the batch, a changelog row)
+template <int MS>
+struct MgSess {
+  int64_t s, e;
+  int64_t a[MS];
+  uint32_t stamp;  // a resident's stamp (a session without a run is one resident, moved unchanged)
+  bool fresh;
+};
+
+// Changelog rows of the fresh sessions of one key (per-batch mode), written
+// by the sweep that produced them (k_ss_apply: every key once per batch).
+struct EmitSink {
+  OutCols out;
+  uint64_t pos;   // next row; ~0 = count only
+  uint32_t key;
+  uint32_t n;     // fresh sessions seen
+};
+
+template <int MS>
+__device__ inline void mg_emit(const Program &prog, EmitSink &k, const MgSess<MS> &c) {
+  if (k.pos != ~0ull) {
+    const uint64_t o = k.pos++;
+    k.out.key[o] = k.key;
+    k.out.ws[o] = c.s;
+    k.out.we[o] = c.e;
+    k.out.src[o] = -1;
+#pragma unroll
+    for (int j = 0; j < kMaxAggs; ++j)  // static indices: the column pointers stay in registers
+      if (j < prog.n_out) k.out.agg[j][o] = out_value_reg<MS>(prog, j, c.a);
+  }
+  ++k.n;
+}
+
+template <int MS>
+__device__ inline MgSess<MS> pick_tail(const MgSess<MS> (&tail)[kMgTail], uint64_t k) {
+  MgSess<MS> x = tail[0];
+  if (k == 1) x = tail[1];
+  return x;
+}
+
+// runs precomputed by k_ss_sort: rows [start][end][aggs]
+struct RunsGlobal {
+  const uint64_t *runs;
+  uint32_t rstride;
+  int ns;
+  __device__ int64_t start(uint32_t r) const { return (int64_t)runs[(uint64_t)r * rstride]; }
+  __device__ int64_t end(uint32_t r) const { return (int64_t)runs[(uint64_t)r * rstride + 1]; }
+  template <int MS>
+  __device__ void aggs(const Program &, uint32_t r, int64_t (&a)[MS]) const {
+    const uint64_t *q = runs + (uint64_t)r * rstride + 2;
+#pragma unroll
+    for (int s = 0; s < MS; ++s) a[s] = s < ns ? (int64_t)q[s] : 0;
+  }
+};
+
+// Sweep of one key: its resident sessions [i0, len) (in registers when
+// `tail_regs`: then len - i0 <= kMgTail) and its runs [r0, r1), in start
+// order; items closer than gap merge (next.start - running end <= gap). With
+// APPLY the merged sessions are written at dst + i0 + k, else only counted.
+template <int MS, bool APPLY, class RS>
+__device__ inline uint32_t mg_sweep(const Program &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t r0,
+                                    uint32_t r1, uint64_t off, uint64_t i0, uint64_t len, bool tail_regs,
+                                    const MgSess<MS> (&tail)[kMgTail], uint64_t dst, uint32_t batch_id,
+                                    EmitSink *sink = nullptr) {
+  const int ns = prog.n_slots;
+  uint64_t j = i0;   // next resident
+  uint32_t r = r0;   // next run
+  uint32_t k = 0;    // merged sessions so far
+  MgSess<MS> cur;
+  bool have = false;
+  for (;;) {
+    // next item in start order: resident j or run r (ties: resident first)
+    const bool has_res = j < len, has_run = r < r1;
+    if (!has_res && !has_run) break;
+    MgSess<MS> it;
+    bool take_res = false;
+    if (has_res) {
+      if (tail_regs) {
+        it = pick_tail<MS>(tail, j - i0);
+      } else {
+        const uint64_t *row = ss_row(t, off + j);
+        it.s = (int64_t)row[0];
+        it.e = (int64_t)row[1];
+        if (APPLY) {
+          it.stamp = (uint32_t)row[2];
+#pragma unroll
+          for (int s = 0; s < MS; ++s) it.a[s] = s < ns ? (int64_t)row[3 + s] : 0;
+        }
+      }
+      take_res = !has_run || it.s <= rs.start(r);
+    }
+    if (take_res) {
+      it.fresh = false;
+      ++j;
+    } else {
+      it.s = rs.start(r);
+      it.e = rs.end(r);
+      it.fresh = true;
+      it.stamp = batch_id;
+      if (APPLY) rs.template aggs<MS>(prog, r, it.a);
+      ++r;
+    }
+    if (have && (int64_t)((uint64_t)it.s - (uint64_t)cur.e) <= gap) {
+      cur.e = it.e > cur.e ? it.e : cur.e;
+      cur.fresh = cur.fresh || it.fresh;
+      if (APPLY) acc_row<MS>(prog, cur.a, it.a);
+    } else {
+      if (have) {
+        if (APPLY) ss_store<MS>(t, dst + i0 + k, cur.s, cur.e, cur.fresh ? batch_id : cur.stamp, cur.a);
+        if (sink && cur.fresh) mg_emit<MS>(prog, *sink, cur);
+        ++k;
+      }
+      cur = it;
+      have = true;
+    }
+  }
+  if (have) {
+    if (APPLY) ss_store<MS>(t, dst + i0 + k, cur.s, cur.e, cur.fresh ? batch_id : cur.stamp, cur.a);
+    if (sink && cur.fresh) mg_emit<MS>(prog, *sink, cur);
+    ++k;
+  }
+  return k;
+}
+
+// first resident session with end >= lo: galloping back from the end (near-
+// sorted arrivals touch the last session or none), then binary search
+__device__ inline uint64_t mg_first_end_ge(const SessTable &t, uint64_t off, uint64_t len, int64_t lo) {
+  uint64_t hi = len, step = 1;
+  while (hi > 0) {
+    const uint64_t probe = hi > step ? hi - step : 0;
+    if ((int64_t)ss_row(t, off + probe)[1] < lo) {
+      uint64_t a = probe + 1, z = hi;  // answer in (probe, hi]
+      while (a < z) {
+        const uint64_t m = (a + z) >> 1;
+        if ((int64_t)ss_row(t, off + m)[1] < lo) a = m + 1;
+        else z = m;
+      }
+      return a;
+    }
+    hi = probe;
+    step <<= 1;
+  }
+  return 0;
+}
+
+// Plan of one key against its list: the first resident its runs can reach,
+// the merged count, and the rows of a fresh list when it cannot stay in place.
+template <int MS, class RS>
+__device__ inline void mg_plan(const Program &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t ra,
+                               uint32_t rb, const SessKey &e, uint64_t &i0, uint32_t &M, uint32_t &newcap,
+                               uint32_t *fresh = nullptr) {
+  const int64_t lo = (int64_t)((uint64_t)rs.start(ra) - (uint64_t)gap);
+  i0 = mg_first_end_ge(t, e.off, e.len, lo);
+  MgSess<MS> dummy[kMgTail];
+  EmitSink cnt{OutCols{}, ~0ull, 0, 0};
+  M = mg_sweep<MS, false>(prog, t, gap, rs, ra, rb, e.off, i0, e.len, false, dummy, 0, 0, &cnt);
+  if (fresh) *fresh = cnt.n;
+  // in place when the merged list fits and the rewritten tail fits the
+  // registers, else a fresh list (prefix copied)
+  newcap = (i0 + M > e.cap || e.len - i0 > kMgTail) ? ss_grow_cap(i0 + M + 1) : 0u;
+}
+
+// Apply a planned key: the list at dst (fresh rows: the prefix copied first).
+template <int MS, class RS>
+__device__ inline void mg_apply(const Program &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t ra,
+                                uint32_t rb, const SessKey &e, uint64_t i0, uint64_t dst, bool reloc,
+                                uint32_t batch_id, EmitSink *sink = nullptr) {
+  const int ns = prog.n_slots;
+  if (reloc)
+    for (uint64_t k = 0; k < i0; ++k) ss_copy(t, dst + k, t, e.off + k);
+  MgSess<MS> tail[kMgTail];
+#pragma unroll
+  for (int k = 0; k < kMgTail; ++k) {
+    const uint64_t j = i0 + k;
+    tail[k].s = tail[k].e = 0;
+    tail[k].stamp = 0;
+    tail[k].fresh = false;
+#pragma unroll
+    for (int s = 0; s < MS; ++s) tail[k].a[s] = 0;
+    if (!reloc && j < e.len) {
+      const uint64_t *row = ss_row(t, e.off + j);
+      tail[k].s = (int64_t)row[0];
+      tail[k].e = (int64_t)row[1];
+      tail[k].stamp = (uint32_t)row[2];
+#pragma unroll
+      for (int s = 0; s < MS; ++s) tail[k].a[s] = s < ns ? (int64_t)row[3 + s] : 0;
+    }
+  }
+  mg_sweep<MS, true>(prog, t, gap, rs, ra, rb, e.off, i0, e.len, !reloc, tail, dst, batch_id, sink);
+}
+
+// ---------------------------------------------------------------------------
+// k_ss_sort: one workgroup per bucket, in sub-buckets (further key-hash bits)
+// of about half a sort chunk each. A sub-bucket's records are grouped by key
+// through an LDS hash table (count, scan, place with their values), each key's
+// few records are sorted by ts by its thread and walked into gap-delimited
+// runs (aggregates folded from the LDS copy) and one group record per key. A
+// sub-bucket with a key of more than kSoSmall records (hot keys), or more than
+// kSoCH records, is left to k_ss_merge_big (its bit in sp.bigmask).
+// ---------------------------------------------------------------------------
+constexpr int kSoNT = 512;
+constexpr int kSoCH = 1024;        // records per sub-bucket
+constexpr int kSoTab = 2048;       // LDS hash table entries
+constexpr int kSoMaxSubLog2 = 6;   // up to 64 sub-buckets (buckets of < 2^16 records)
+constexpr int kSoSmall = 32;       // a key's records sorted by its own thread
+
+template <int W>
+struct SortLds {
+  uint32_t tkey[kSoTab];
+  uint32_t tcnt[kSoTab];    // records of the key; after the scan the placement cursor
+  uint32_t tstart[kSoTab];  // first position of the key's segment
+  uint16_t tgid[kSoTab];    // group index of the key in the sub-bucket
+  int64_t ts[kSoCH];        // segments: ts and the record's other words (word 0, columns)
+  uint64_t vw[kSoCH * (W - 1)];
+  uint16_t qslot[kSoCH];    // table slot of the record at each segment position
+  uint32_t wsum[kSoNT / 64];
+  uint32_t subcnt[1 << kSoMaxSubLog2];
+  uint32_t suboff[1 << kSoMaxSubLog2];  // first entry of each sub-bucket in the bucket's index list
+  uint32_t subgrp[1 << kSoMaxSubLog2];  // key groups of each sub-bucket
+  uint32_t ngrp, nrun, maxseg;
+  uint64_t grpbase;
+};
+
+// sub-bucket of a key: the sl key-hash bits below the owner and bucket bits
+__device__ inline uint32_t ss_sub(uint32_t key, int hs, int sl) {
+  return sl ? (uint32_t)((key_hash(key) << hs) >> (64 - sl)) : 0u;
+}
+// sub-bucket bits for a bucket of m records: sub-buckets of about kSoCH / 2
+__device__ inline int ss_sub_log2(uint64_t m) {
+  int sl = 0;
+  while (((uint64_t)(kSoCH / 2) << sl) < m && sl < kSoMaxSubLog2) ++sl;
+  return sl;
+}
+
+__device__ inline int64_t ts_of(uint64_t img) { return (int64_t)(img ^ 0x8000000000000000ull); }
+
+// contribution of one record (word 0 and columns in `v`, as in the LDS copy:
+// v[0] = key | valid bits << 32, v[1 + c] = column c)
+template <int MS>
+__device__ inline void ss_vw_elem(const Program &prog, const uint64_t *v, int64_t (&e)[MS]) {
+  const uint64_t vb = v[0] >> 32;
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    e[s] = 0;
+    if (s >= prog.n_slots) continue;
+    const int op = prog.slot_op[s], c = prog.slot_col[s];
+    if (op == S_CNT_ALL) {
+      e[s] = 1;
+      continue;
+    }
+    if (!((vb >> c) & 1ull)) {
+      e[s] = slot_identity_dev(op);
+      continue;
+    }
+    const int64_t x = (int64_t)v[1 + c];
+    switch (op) {
+      case S_CNT: e[s] = 1; break;
+      case S_MIN_F:
+      case S_MAX_F: e[s] = (int64_t)f64_ord(__builtin_bit_cast(double, x)); break;
+      default: e[s] = x; break;
+    }
+  }
+}
+
+template <int MS, int W>
+__global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Program prog, int np_log2, int bshift,
+                                                   SessPart sp, DevScalars *sc) {
+  __shared__ SortLds<W> L;
+  const uint64_t c0 = wall_clock64();
+  uint64_t c_ins = 0, c_scan = 0, c_place = 0, c_key = 0, c1 = 0;
+  constexpr int B = 8;  // loads in flight per thread in the bucket passes
+  const uint32_t b = blockIdx.x;
+  const uint64_t r0 = sp.bstart[b], r1 = sp.bstart[b + 1];
+  const uint64_t m = r1 - r0;
+  if (m == 0) {
+    if (threadIdx.x == 0) sp.bigmask[b] = 0;
+    return;
+  }
+  const uint64_t *recs = sp.rec + r0 * W;
+  const int sl = ss_sub_log2(m), hs = bshift + np_log2;
+  const int nsub = 1 << sl;
+  // the bucket's record indices grouped by sub-bucket (sp.sidx, the bucket's
+  // own range): every later pass visits only its sub-bucket's records
+  uint16_t *sidx = sp.sidx + r0;
+  if (threadIdx.x < (1 << kSoMaxSubLog2)) {
+    L.subcnt[threadIdx.x] = 0;
+    L.subgrp[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  const bool indexable = m < 65536;
+  // (lanes of a wave with the same sub-bucket found by ballots: one LDS
+  // atomic per sub-bucket and wave instead of one per record)
+  const int lane0 = threadIdx.x & 63;
+  const uint64_t lt = lane0 ? (~0ull >> (64 - lane0)) : 0ull;
+  auto peers = [&](uint32_t q, bool in) {
+    uint64_t pm = __ballot(in);
+#pragma unroll
+    for (int bit = 0; bit < kSoMaxSubLog2; ++bit) {
+      if (bit >= sl) break;
+      const uint64_t bb = __ballot((q >> bit) & 1u);
+      pm &= ((q >> bit) & 1u) ? bb : ~bb;
+    }
+    return pm;
+  };
+  if (indexable)
+    for (uint64_t i0 = 0; i0 < m; i0 += (uint64_t)kSoNT * B) {
+      uint32_t q[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const uint64_t i = i0 + (uint64_t)u * kSoNT + threadIdx.x;
+        q[u] = i < m ? ss_sub((uint32_t)recs[i * W], hs, sl) : ~0u;
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const bool in = q[u] != ~0u;
+        const uint64_t pm = peers(q[u], in);
+        if (in && (pm & lt) == 0) atomicAdd(&L.subcnt[q[u]], (uint32_t)__popcll(pm));
+      }
+    }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t o = 0;
+    for (int q = 0; q < nsub; ++q) {
+      L.suboff[q] = o;
+      o += L.subcnt[q];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < (1 << kSoMaxSubLog2)) L.subcnt[threadIdx.x] = 0;
+  __syncthreads();
+  if (indexable)
+    for (uint64_t i0 = 0; i0 < m; i0 += (uint64_t)kSoNT * B) {
+      uint32_t q[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const uint64_t i = i0 + (uint64_t)u * kSoNT + threadIdx.x;
+        q[u] = i < m ? ss_sub((uint32_t)recs[i * W], hs, sl) : ~0u;
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const bool in = q[u] != ~0u;
+        const uint64_t pm = peers(q[u], in);
+        const uint32_t rk = (uint32_t)__popcll(pm & lt);
+        // the group's lowest lane reserves for the group; the others read its base
+        uint32_t base = 0;
+        if (in && rk == 0) base = atomicAdd(&L.subcnt[q[u]], (uint32_t)__popcll(pm));
+        const int leader = in ? __ffsll((long long)pm) - 1 : lane0;
+        base = __shfl(base, leader, 64);
+        if (in) sidx[L.suboff[q[u]] + base + rk] = (uint16_t)(i0 + (uint64_t)u * kSoNT + threadIdx.x);
+      }
+    }
+  __syncthreads();
+  uint64_t bigmask = indexable ? 0ull : ~0ull;  // a bucket that cannot be indexed goes to the big path whole
+  c1 = wall_clock64();
+  const uint32_t rstride = 2 + prog.n_slots;
+  constexpr int RP = kSoCH / kSoNT;  // records per thread in a sub-bucket pass
+  for (int sub = 0; indexable && sub < nsub; ++sub) {
+    const uint32_t m2 = L.subcnt[sub];
+    if (m2 == 0) continue;  // uniform
+    if (m2 > (uint32_t)kSoCH) {
+      bigmask |= 1ull << sub;
+      continue;
+    }
+    const uint16_t *lst = sidx + L.suboff[sub];
+    uint64_t ca = wall_clock64();
+    // 1. keys of the sub-bucket into the LDS table, records per key; the
+    // records' words stay in registers for the placement
+    for (int h = threadIdx.x; h < kSoTab; h += kSoNT) {
+      L.tkey[h] = 0xFFFFFFFFu;
+      L.tcnt[h] = 0;
+    }
+    if (threadIdx.x == 0) {
+      L.ngrp = 0;
+      L.nrun = 0;
+      L.maxseg = 0;
+    }
+    uint64_t rw[RP][W];
+#pragma unroll
+    for (int u = 0; u < RP; ++u) {
+      const uint32_t j = u * kSoNT + threadIdx.x;
+      const uint64_t i = j < m2 ? lst[j] : 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) rw[u][w] = j < m2 ? recs[i * W + w] : 0;
+    }
+    lds_barrier();
+    uint32_t hslot[RP];
+#pragma unroll
+    for (int u = 0; u < RP; ++u) {
+      hslot[u] = ~0u;
+      if (u * kSoNT + threadIdx.x >= m2) continue;
+      const uint32_t key = (uint32_t)rw[u][0];
+      uint32_t h = (uint32_t)mix64(key) & (kSoTab - 1);
+      for (;;) {
+        const uint32_t cur = L.tkey[h];
+        if (cur == key) break;
+        if (cur == 0xFFFFFFFFu) {
+          const uint32_t old = atomicCAS(&L.tkey[h], 0xFFFFFFFFu, key);
+          if (old == 0xFFFFFFFFu || old == key) break;
+        }
+        h = (h + 1) & (kSoTab - 1);
+      }
+      hslot[u] = h;
+      atomicAdd(&L.tcnt[h], 1u);
+    }
+    lds_barrier();
+    { const uint64_t cb = wall_clock64(); c_ins += cb - ca; ca = cb; }
+    // 2. segment starts: exclusive scan of the counts
+    // (records in the low 16 bits, occupied slots in the high: one scan gives
+    // each key its segment start and its group index)
+    constexpr int TP = kSoTab / kSoNT;
+    uint32_t loc = 0, mx = 0;
+#pragma unroll
+    for (int u = 0; u < TP; ++u) {
+      const uint32_t c = L.tcnt[threadIdx.x * TP + u];
+      loc += c + (c ? 0x10000u : 0u);
+      mx = c > mx ? c : mx;
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) L.wsum[wv] = incl;
+    if (mx > (uint32_t)kSoSmall) atomicMax(&L.maxseg, mx);
+    lds_barrier();
+    if (L.maxseg > (uint32_t)kSoSmall) {  // uniform: a hot key, the big path takes the sub-bucket
+      bigmask |= 1ull << sub;
+      lds_barrier();
+      continue;
+    }
+    uint32_t run = incl - loc, all = 0;
+    for (int k = 0; k < kSoNT / 64; ++k) {
+      if (k < wv) run += L.wsum[k];
+      all += L.wsum[k];
+    }
+#pragma unroll
+    for (int u = 0; u < TP; ++u) {
+      const int h = threadIdx.x * TP + u;
+      const uint32_t c = L.tcnt[h];
+      L.tstart[h] = run & 0xFFFFu;
+      L.tcnt[h] = run & 0xFFFFu;
+      L.tgid[h] = (uint16_t)(run >> 16);
+      run += c + (c ? 0x10000u : 0u);
+    }
+    if (threadIdx.x == 0) L.ngrp = all >> 16;
+    if (threadIdx.x == 0) L.subgrp[sub] = L.ngrp;
+    // a sub-bucket's sorted records and (sparse) group records live at its
+    // records' positions in the bucket
+    const uint64_t runbase = r0 + L.suboff[sub];
+    uint32_t *gsp = sp.gsparse + (r0 + L.suboff[sub]) * 4;
+    lds_barrier();
+    { const uint64_t cb = wall_clock64(); c_scan += cb - ca; ca = cb; }
+    // 3. place (ts, words) in the key's segment
+#pragma unroll
+    for (int u = 0; u < RP; ++u) {
+      if (hslot[u] == ~0u) continue;
+      const uint32_t q = atomicAdd(&L.tcnt[hslot[u]], 1u);
+      L.ts[q] = (int64_t)rw[u][1];
+      L.vw[q * (W - 1)] = rw[u][0];
+#pragma unroll
+      for (int w = 2; w < W; ++w) L.vw[q * (W - 1) + w - 1] = rw[u][w];
+      L.qslot[q] = (uint16_t)hslot[u];
+    }
+    lds_barrier();
+    { const uint64_t cb = wall_clock64(); c_place += cb - ca; ca = cb; }
+    // 4. every record ranked by ts within its key's segment (<= kSoSmall) and
+    // written out in (key, ts) order; one group record per key
+    for (uint32_t q = threadIdx.x; q < m2; q += kSoNT) {
+      const uint32_t h = L.qslot[q];
+      const uint32_t sa = L.tstart[h], se = L.tcnt[h];
+      const int64_t v = L.ts[q];
+      uint32_t rank = 0;
+      for (uint32_t j = sa; j < se; ++j) {
+        const int64_t tj = L.ts[j];
+        rank += (tj < v || (tj == v && j < q)) ? 1u : 0u;
+      }
+      uint64_t *row = sp.srec + (runbase + sa + rank) * W;
+      row[0] = (uint64_t)v;
+#pragma unroll
+      for (int w = 0; w < W - 1; ++w) row[1 + w] = L.vw[q * (W - 1) + w];
+    }
+    for (int h = threadIdx.x; h < kSoTab; h += kSoNT) {
+      const uint32_t key = L.tkey[h];
+      if (key == 0xFFFFFFFFu) continue;
+      const uint32_t sa = L.tstart[h];
+      *reinterpret_cast<uint4 *>(gsp + (uint64_t)L.tgid[h] * 4) =
+          make_uint4(key, (uint32_t)(runbase + sa), L.tcnt[h] - sa, 0u);
+    }
+    lds_barrier();
+    c_key += wall_clock64() - ca;
+  }
+  // the bucket's group records, dense: one reservation per bucket
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int q = 0; q < nsub; ++q) {
+      if (!indexable || ((bigmask >> q) & 1ull) || L.subcnt[q] == 0 || L.subcnt[q] > (uint32_t)kSoCH) L.subgrp[q] = 0;
+      tot += L.subgrp[q];
+    }
+    L.grpbase = tot ? atomicAdd((unsigned long long *)&t.meta[M_GRP], (unsigned long long)tot) : 0;
+    sp.bigmask[b] = bigmask;
+    if (bigmask) atomicAdd((unsigned long long *)&t.meta[M_BIG], 1ull);
+  }
+  __syncthreads();
+  uint64_t d = L.grpbase;
+  for (int q = 0; q < nsub; ++q) {
+    const uint32_t c = L.subgrp[q];
+    const uint4 *src = reinterpret_cast<const uint4 *>(sp.gsparse + (r0 + L.suboff[q]) * 4);
+    for (uint32_t j = threadIdx.x; j < c; j += kSoNT) reinterpret_cast<uint4 *>(sp.groups)[d + j] = src[j];
+    d += c;
+  }
+  if (threadIdx.x == 0) {  // phase clocks (100 MHz), HSG_PHASES
+    const uint64_t c2 = wall_clock64();
+    atomicAdd((unsigned long long *)&sc->scratch[24], (unsigned long long)(c1 - c0));
+    atomicAdd((unsigned long long *)&sc->scratch[25], (unsigned long long)c_ins);
+    atomicAdd((unsigned long long *)&sc->scratch[26], (unsigned long long)c_scan);
+    atomicAdd((unsigned long long *)&sc->scratch[27], (unsigned long long)c_place);
+    atomicAdd((unsigned long long *)&sc->scratch[28], (unsigned long long)c_key);
+    atomicAdd((unsigned long long *)&sc->scratch[29], (unsigned long long)(c2 - c0));
+    atomicAdd((unsigned long long *)&sc->scratch[30], 1ull);
+  }
+}
+
+template <int MS>
+static void sort_launch_w(hipStream_t s, int words, dim3 g, const SessParams &p, const SessTable &t,
+                          const Program &prog, int np_log2, int bshift, const SessPart &sp, DevScalars *sc) {
+  const dim3 th(kSoNT);
+  switch (words) {
+    case 2: hipLaunchKernelGGL((k_ss_sort<MS, 2>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+    case 3: hipLaunchKernelGGL((k_ss_sort<MS, 3>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+    case 4: hipLaunchKernelGGL((k_ss_sort<MS, 4>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+    case 5: hipLaunchKernelGGL((k_ss_sort<MS, 5>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+    case 6: hipLaunchKernelGGL((k_ss_sort<MS, 6>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+    default: hipLaunchKernelGGL((k_ss_sort<MS, kSessMaxWords>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+  }
+}
+
+void launch_ss_sort(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, int np_log2,
+                    int bshift, int words, const SessPart &sp, DevScalars *sc) {
+  const dim3 g(1u << np_log2);
+  if (prog.n_slots <= 2) sort_launch_w<2>(s, words, g, p, t, prog, np_log2, bshift, sp, sc);
+  else if (prog.n_slots <= 4) sort_launch_w<4>(s, words, g, p, t, prog, np_log2, bshift, sp, sc);
+  else sort_launch_w<8>(s, words, g, p, t, prog, np_log2, bshift, sp, sc);
+}
+
+// a key's batch records, sorted by ts (k_ss_sort), as sweep items: record r
+// is the point [ts, ts]; the sweep merges items closer than the gap, so
+// feeding points instead of pre-merged runs gives the same sessions
+template <int W>
+struct RecItems {
+  const uint64_t *rows;  // [n][W]: ts, word 0, columns
+  __device__ int64_t start(uint32_t r) const { return (int64_t)rows[(uint64_t)r * W]; }
+  __device__ int64_t end(uint32_t r) const { return (int64_t)rows[(uint64_t)r * W]; }
+  template <int MS>
+  __device__ void aggs(const Program &prog, uint32_t r, int64_t (&a)[MS]) const {
+    ss_vw_elem<MS>(prog, rows + (uint64_t)r * W + 1, a);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// k_ss_apply: one thread per key group (every key once per batch). Plan,
+// reserve the block's fresh lists in its arena region (all or nothing: a block
+// that cannot stays undone, the host compacts and runs the pass again), apply
+// and write the changelog rows of the fresh sessions.
+// ---------------------------------------------------------------------------
+constexpr int kApNT = 1024;  // large blocks: one arena / changelog reservation per 1024 keys
+
+template <int MS, int W>
+__global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, Program prog, SessPart sp,
+                                                    OutCols out, uint64_t out_base, DevScalars *sc) {
+  __shared__ uint64_t ws[kApNT / 64];
+  __shared__ uint64_t we[kApNT / 64];
+  __shared__ uint64_t sbase, sobase;
+  __shared__ int sfail;
+  const uint32_t blk = blockIdx.x;
+  if (sp.done[blk]) return;  // uniform: applied by an earlier pass of this batch
+  const uint64_t ng = t.meta[M_GRP];
+  const uint64_t g0 = (uint64_t)blk * kApNT;
+  if (g0 >= ng) return;  // uniform
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t g = g0 + threadIdx.x;
+  const bool act = g < ng;
+  const RecItems<W> rs{sp.srec};
+  uint32_t key = 0, ra = 0, nr = 0, newcap = 0, M = 0, fresh = 0;
+  uint64_t i0 = 0;
+  int64_t sl = -1;
+  bool ins = false;
+  SessKey e = {0, 0, 0, 0, 0, 0};
+  uint32_t err = 0;
+  if (act) {
+    const uint4 gr = *reinterpret_cast<const uint4 *>(sp.groups + g * 4);
+    key = gr.x;
+    ra = gr.y;
+    nr = gr.z;
+    sl = ss_find_or_insert(t, key, ins);
+    if (sl < 0) err |= ERR_OOM;
+    else {
+      if (!ins) e = t.kt[sl];
+      mg_plan<MS>(prog, t, p.gap, rs, ra, ra + nr, e, i0, M, newcap, &fresh);
+    }
+  }
+  const bool live = act && sl >= 0;
+  {
+    // keys inserted count now: a block that fails below finds them next pass
+    const uint64_t ksum = wave_sum_u64(ins ? 1ull : 0ull);
+    if (lane == 0 && ksum) atomicAdd((unsigned long long *)&t.meta[M_KEYS], (unsigned long long)ksum);
+    if (err) atomicOr(&sc->err, err);
+  }
+  // block exclusive scans of the fresh list rows and of the changelog rows
+  const uint64_t need = newcap, nem = live ? fresh : 0;
+  const uint64_t incl = wave_incl_sum(need), einc = wave_incl_sum(nem);
+  if (lane == 63) {
+    ws[wv] = incl;
+    we[wv] = einc;
+  }
+  __syncthreads();
+  uint64_t before = 0, total = 0, ebefore = 0, etotal = 0;
+  for (int k = 0; k < kApNT / 64; ++k) {
+    if (k < wv) {
+      before += ws[k];
+      ebefore += we[k];
+    }
+    total += ws[k];
+    etotal += we[k];
+  }
+  if (threadIdx.x == 0) {
+    uint64_t base = 0;
+    const int fail = total ? !arena_take(t, arena_region(blk), total, base) : 0;
+    sfail = fail;
+    sbase = base;
+    sobase = 0;
+    if (fail) atomicOr((unsigned int *)&t.meta[M_FAIL], 1u);
+    else if (etotal) {
+      // per-batch mode: touched = rows (the host takes it from out_rows)
+      if (p.emit_mode == HSG_EMIT_PER_BATCH) sobase = atomicAdd((unsigned long long *)&sc->out_rows, (unsigned long long)etotal);
+      else atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)etotal);
+    }
+  }
+  __syncthreads();
+  if (sfail) return;  // uniform: keys inserted above stay (idempotent); the block runs again
+  int64_t ld = 0;
+  if (live) {
+    const bool reloc = newcap != 0;
+    const uint64_t dst = reloc ? sbase + before + incl - need : e.off;
+    EmitSink sink{out, p.emit_mode == HSG_EMIT_PER_BATCH ? out_base + sobase + ebefore + einc - nem : ~0ull, key, 0};
+    mg_apply<MS>(prog, t, p.gap, rs, ra, ra + nr, e, i0, dst, reloc, p.batch_id, &sink);
+    SessKey &ke = t.kt[sl];
+    ke.off = dst;
+    ke.len = (uint32_t)(i0 + M);
+    if (reloc) ke.cap = newcap;
+    ld = (int64_t)M - (int64_t)(e.len - i0);
+  }
+  const uint64_t lsum = wave_sum_u64((uint64_t)ld);
+  if (lane == 0 && lsum) atomicAdd((unsigned long long *)&sc->live, (unsigned long long)lsum);
+  __syncthreads();
+  if (threadIdx.x == 0) sp.done[blk] = 1;
+}
+
+template <int MS>
+static void apply_launch_w(hipStream_t s, int words, dim3 g, const SessParams &p, const SessTable &t,
+                           const Program &prog, const SessPart &sp, OutCols out, uint64_t out_base, DevScalars *sc) {
+  const dim3 th(kApNT);
+  switch (words) {
+    case 2: hipLaunchKernelGGL((k_ss_apply<MS, 2>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 3: hipLaunchKernelGGL((k_ss_apply<MS, 3>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 4: hipLaunchKernelGGL((k_ss_apply<MS, 4>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 5: hipLaunchKernelGGL((k_ss_apply<MS, 5>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 6: hipLaunchKernelGGL((k_ss_apply<MS, 6>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    default: hipLaunchKernelGGL((k_ss_apply<MS, kSessMaxWords>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+  }
+}
+
+void launch_ss_apply(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, uint64_t n_bound,
+                     int words, const SessPart &sp, OutCols out, uint64_t out_base, DevScalars *sc) {
+  const dim3 g((unsigned)((n_bound + kApNT - 1) / kApNT + 1));
+  if (prog.n_slots <= 2) apply_launch_w<2>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  else if (prog.n_slots <= 4) apply_launch_w<4>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  else apply_launch_w<8>(s, words, g, p, t, prog, sp, out, out_base, sc);
+}
+
+// ---------------------------------------------------------------------------
+// k_ss_merge_big: a bucket too large for one sort (hot keys) is merged chunk
+// by chunk by one workgroup: each chunk sorted in LDS, its runs merged into the
+// resident sessions before the next chunk (the aggregates commute, so the
+// chunking does not change the result), one arena reservation per chunk.
+// ---------------------------------------------------------------------------
+constexpr int kMgNT = 512;
+constexpr int kMgCH = 2048;
+constexpr int kMgPer = kMgCH / kMgNT;
+
 struct MgLds {
-  uint32_t key[kMgCH];      // sort: key, ts image, record index in the chunk
+  uint32_t key[kMgCH];
   uint64_t tsu[kMgCH];
   uint16_t idx[kMgCH];
-  int64_t rs[kMgCH];        // runs: start, end (inclusive), first sorted position
+  int64_t rs[kMgCH];  // runs: start, end (inclusive), first sorted position
   int64_t re[kMgCH];
   uint16_t rbeg[kMgCH + 1];
-  uint16_t gfirst[kMgCH + 1];  // groups (keys): first run
+  uint16_t gfirst[kMgCH + 1];  // key groups: first run
   uint32_t wsum[kMgNT / 64];
   uint64_t red[kMgNT / 64];
-  uint32_t nrun, ngrp;
-  uint64_t base;            // arena reservation of this chunk
-  uint32_t tbase;           // touched-list entries of this chunk
+  uint64_t base;
+  uint32_t tbase;
+  uint32_t fill;
   int fail;
 };
 
-// block exclusive scan of one u32 per thread (kMgNT threads)
+// runs of the LDS-sorted chunk, aggregates folded from the member records
+template <int W>
+struct RunsLds {
+  const MgLds *L;
+  const uint64_t *recs;
+  __device__ int64_t start(uint32_t r) const { return L->rs[r]; }
+  __device__ int64_t end(uint32_t r) const { return L->re[r]; }
+  template <int MS>
+  __device__ void aggs(const Program &prog, uint32_t r, int64_t (&a)[MS]) const {
+    identity_row<MS>(prog, a);
+    for (uint32_t q = L->rbeg[r]; q < L->rbeg[r + 1]; ++q) {
+      int64_t e[MS];
+      ss_rec_elem<MS>(prog, recs + (uint64_t)L->idx[q] * W, e);
+      acc_row<MS>(prog, a, e);
+    }
+  }
+};
+
 __device__ inline uint32_t mg_scan(MgLds &L, uint32_t v, uint32_t &total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t incl = v;
@@ -626,7 +1345,6 @@ __device__ inline uint32_t mg_scan(MgLds &L, uint32_t v, uint32_t &total) {
   return before + incl - v;
 }
 
-// block exclusive scan of one u64 per thread; total -> *total
 __device__ inline uint64_t mg_scan64(MgLds &L, uint64_t v, uint64_t &total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint64_t incl = wave_incl_sum(v);
@@ -642,168 +1360,50 @@ __device__ inline uint64_t mg_scan64(MgLds &L, uint64_t v, uint64_t &total) {
   return before + incl - v;
 }
 
-__device__ inline uint64_t mg_sum64(MgLds &L, uint64_t v) {
-  v = wave_sum_u64(v);
-  if ((threadIdx.x & 63) == 0) L.red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  uint64_t t = 0;
-  for (int k = 0; k < kMgNT / 64; ++k) t += L.red[k];
-  __syncthreads();
-  return t;
-}
-
-// One session of the sweep: start, end, aggregates, and whether a batch run
-// is in it (-> changelog row, stamp)
-template <int MS>
-struct MgSess {
-  int64_t s, e;
-  int64_t a[MS];
-  uint32_t stamp;  // a resident session's stamp (sessions without a run are one resident, moved unchanged)
-  bool fresh;
-};
-
-// Sweep of one key: its resident sessions [i0, len) (the first kMgTail of them
-// in registers when `tail_regs`) and its runs, in start order; items closer
-// than gap merge (next.start - running end <= gap). With APPLY the merged
-// sessions are written at dst + i0 + k (a session with a run in it stamped
-// with the batch) and counted, else only counted.
-template <int MS, int W, bool APPLY>
-__device__ inline uint32_t mg_sweep(const MgLds &L, const Program &prog, const SessTable &t, int64_t gap,
-                                    const uint64_t *recs, uint32_t r0, uint32_t r1, uint64_t off, uint64_t i0,
-                                    uint64_t len, bool tail_regs, const MgSess<MS> (&tail)[kMgTail], uint64_t dst,
-                                    uint32_t batch_id) {
-  const int ns = prog.n_slots;
-  uint64_t j = i0;   // next resident
-  uint32_t r = r0;   // next run
-  uint32_t k = 0;    // merged sessions so far
-  MgSess<MS> cur;
-  bool have = false;
-  auto flush = [&]() {
-    if (APPLY) {
-      const uint64_t d = dst + i0 + k;
-      t.a_start[d] = cur.s;
-      t.a_end[d] = cur.e;
-      t.a_stamp[d] = cur.fresh ? batch_id : cur.stamp;
-#pragma unroll
-      for (int s = 0; s < MS; ++s)
-        if (s < ns) t.a_aggs[d * ns + s] = cur.a[s];
-    }
-    ++k;
-  };
-  for (;;) {
-    // next item in start order: resident j or run r (ties: resident first)
-    const bool has_res = j < len, has_run = r < r1;
-    if (!has_res && !has_run) break;
-    int64_t rs_ = 0, re_ = 0;
-    if (has_res) {
-      if (tail_regs && j - i0 < kMgTail) {
-        rs_ = tail[j - i0].s;
-        re_ = tail[j - i0].e;
-      } else {
-        rs_ = t.a_start[off + j];
-        re_ = t.a_end[off + j];
-      }
-    }
-    const bool take_res = has_res && (!has_run || rs_ <= L.rs[r]);
-    MgSess<MS> it;
-    if (take_res) {
-      it.s = rs_;
-      it.e = re_;
-      it.fresh = false;
-      it.stamp = 0;
-      if (APPLY) {
-        if (tail_regs && j - i0 < kMgTail) {
-          it.stamp = tail[j - i0].stamp;
-#pragma unroll
-          for (int s = 0; s < MS; ++s) it.a[s] = tail[j - i0].a[s];
-        } else {
-          it.stamp = t.a_stamp[off + j];
-#pragma unroll
-          for (int s = 0; s < MS; ++s) it.a[s] = s < ns ? t.a_aggs[(off + j) * ns + s] : 0;
-        }
-      }
-      ++j;
-    } else {
-      it.s = L.rs[r];
-      it.e = L.re[r];
-      it.fresh = true;
-      it.stamp = batch_id;
-      if (APPLY) {
-        identity_row<MS>(prog, it.a);
-        for (uint32_t q = L.rbeg[r]; q < L.rbeg[r + 1]; ++q) {
-          int64_t e[MS];
-          ss_rec_elem<MS>(prog, recs + (uint64_t)L.idx[q] * W, e);
-          acc_row<MS>(prog, it.a, e);
-        }
-      }
-      ++r;
-    }
-    if (have && (int64_t)((uint64_t)it.s - (uint64_t)cur.e) <= gap) {
-      cur.e = it.e > cur.e ? it.e : cur.e;
-      cur.fresh = cur.fresh || it.fresh;
-      if (APPLY) acc_row<MS>(prog, cur.a, it.a);
-    } else {
-      if (have) flush();
-      cur = it;
-      have = true;
-    }
-  }
-  if (have) flush();
-  return k;
-}
-
-// first resident session with end >= lo: galloping back from the end (near-
-// sorted arrivals touch the last session or none), then binary search
-__device__ inline uint64_t mg_first_end_ge(const SessTable &t, uint64_t off, uint64_t len, int64_t lo) {
-  uint64_t hi = len, step = 1;
-  while (hi > 0) {
-    const uint64_t probe = hi > step ? hi - step : 0;
-    if (t.a_end[off + probe] < lo) {
-      // answer in (probe, hi]
-      uint64_t a = probe + 1, z = hi;
-      while (a < z) {
-        const uint64_t m = (a + z) >> 1;
-        if (t.a_end[off + m] < lo) a = m + 1;
-        else z = m;
-      }
-      return a;
-    }
-    hi = probe;
-    step <<= 1;
-  }
-  return 0;
-}
-
 template <int MS, int W>
-__global__ __launch_bounds__(kMgNT) void k_ss_merge(SessParams p, SessTable t, Program prog, int np_log2,
-                                                    SessPart sp, DevScalars *sc) {
+__global__ __launch_bounds__(kMgNT) void k_ss_merge_big(SessParams p, SessTable t, Program prog, int np_log2,
+                                                        int bshift, SessPart sp, DevScalars *sc) {
   __shared__ MgLds L;
   const uint32_t b = blockIdx.x;
+  const uint64_t bigmask = sp.bigmask[b];
+  if (!bigmask) return;  // uniform
   const uint64_t r0 = sp.bstart[b], r1 = sp.bstart[b + 1];
   const uint32_t nch = (uint32_t)((r1 - r0 + kMgCH - 1) / kMgCH);
-  const int ns = prog.n_slots;
+  const int sl = ss_sub_log2(r1 - r0), hs = bshift + np_log2;
+  const int lane = threadIdx.x & 63;
   int64_t live_delta = 0;
   uint64_t keys_new = 0;
   uint32_t err = 0;
   for (uint32_t c = sp.progress[b]; c < nch; ++c) {
+    // window c of the bucket's records, restricted to the big sub-buckets
     const uint64_t q0 = r0 + (uint64_t)c * kMgCH;
-    const uint32_t m = (uint32_t)(r1 - q0 < kMgCH ? r1 - q0 : kMgCH);
+    const uint32_t mw = (uint32_t)(r1 - q0 < kMgCH ? r1 - q0 : kMgCH);
     const uint64_t *recs = sp.rec + q0 * W;
-    uint32_t N = 2;
-    while (N < m) N <<= 1;
-    // 1. load (key, ts) of the chunk; pad to N with +inf
-    for (uint32_t i = threadIdx.x; i < N; i += kMgNT) {
-      if (i < m) {
-        L.key[i] = (uint32_t)recs[(uint64_t)i * W];
-        L.tsu[i] = i64_img((int64_t)recs[(uint64_t)i * W + 1]);
-      } else {
-        L.key[i] = 0xFFFFFFFFu;
-        L.tsu[i] = ~0ull;
-      }
-      L.idx[i] = (uint16_t)i;
+    if (threadIdx.x == 0) L.fill = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < mw; i += kMgNT) {
+      const uint32_t key = (uint32_t)recs[(uint64_t)i * W];
+      if (!((bigmask >> ss_sub(key, hs, sl)) & 1ull)) continue;
+      const uint32_t q = atomicAdd(&L.fill, 1u);
+      L.key[q] = key;
+      L.tsu[q] = (uint64_t)recs[(uint64_t)i * W + 1] ^ 0x8000000000000000ull;
+      L.idx[q] = (uint16_t)i;
     }
     __syncthreads();
-    // 2. bitonic sort by (key, ts)
+    const uint32_t m = L.fill;
+    if (m == 0) {  // uniform
+      if (c + 1 == nch && threadIdx.x == 0) sp.progress[b] = nch;
+      __syncthreads();
+      continue;
+    }
+    uint32_t N = 2;
+    while (N < m) N <<= 1;
+    for (uint32_t i = m + threadIdx.x; i < N; i += kMgNT) {
+      L.key[i] = 0xFFFFFFFFu;
+      L.tsu[i] = ~0ull;
+      L.idx[i] = 0;
+    }
+    __syncthreads();
     for (uint32_t k = 2; k <= N; k <<= 1) {
       for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
         for (uint32_t i = threadIdx.x; i < N; i += kMgNT) {
@@ -825,18 +1425,14 @@ __global__ __launch_bounds__(kMgNT) void k_ss_merge(SessParams p, SessTable t, P
         __syncthreads();
       }
     }
-    // 3. gap-delimited runs: thread owns sorted positions [tid*kMgPer, +kMgPer)
+    // runs
     uint32_t heads = 0, hmask = 0;
 #pragma unroll
     for (int u = 0; u < kMgPer; ++u) {
       const uint32_t i = threadIdx.x * kMgPer + u;
       if (i >= m) break;
       bool h = i == 0 || L.key[i] != L.key[i - 1];
-      if (!h) {
-        const int64_t ta = (int64_t)(L.tsu[i - 1] ^ 0x8000000000000000ull);
-        const int64_t tb = (int64_t)(L.tsu[i] ^ 0x8000000000000000ull);
-        h = (int64_t)((uint64_t)tb - (uint64_t)ta) > p.gap;
-      }
+      if (!h) h = (int64_t)((uint64_t)ts_of(L.tsu[i]) - (uint64_t)ts_of(L.tsu[i - 1])) > p.gap;
       if (h) {
         hmask |= 1u << u;
         ++heads;
@@ -849,16 +1445,16 @@ __global__ __launch_bounds__(kMgNT) void k_ss_merge(SessParams p, SessTable t, P
       if (!((hmask >> u) & 1u)) continue;
       const uint32_t i = threadIdx.x * kMgPer + u;
       L.rbeg[rpos] = (uint16_t)i;
-      L.rs[rpos] = (int64_t)(L.tsu[i] ^ 0x8000000000000000ull);
-      if (rpos > 0) L.re[rpos - 1] = (int64_t)(L.tsu[i - 1] ^ 0x8000000000000000ull);
+      L.rs[rpos] = ts_of(L.tsu[i]);
+      if (rpos > 0) L.re[rpos - 1] = ts_of(L.tsu[i - 1]);
       ++rpos;
     }
     if (threadIdx.x == 0) {
       L.rbeg[nrun] = (uint16_t)m;
-      L.re[nrun - 1] = (int64_t)(L.tsu[m - 1] ^ 0x8000000000000000ull);
+      L.re[nrun - 1] = ts_of(L.tsu[m - 1]);
     }
     __syncthreads();
-    // 4. groups = runs of one key: thread owns runs [tid*kMgPer, +kMgPer)
+    // key groups
     uint32_t gh = 0, gmask = 0;
 #pragma unroll
     for (int u = 0; u < kMgPer; ++u) {
@@ -872,18 +1468,16 @@ __global__ __launch_bounds__(kMgNT) void k_ss_merge(SessParams p, SessTable t, P
     uint32_t ngrp;
     uint32_t gpos = mg_scan(L, gh, ngrp);
 #pragma unroll
-    for (int u = 0; u < kMgPer; ++u) {
-      if (!((gmask >> u) & 1u)) continue;
-      L.gfirst[gpos++] = (uint16_t)(threadIdx.x * kMgPer + u);
-    }
+    for (int u = 0; u < kMgPer; ++u)
+      if ((gmask >> u) & 1u) L.gfirst[gpos++] = (uint16_t)(threadIdx.x * kMgPer + u);
     if (threadIdx.x == 0) L.gfirst[ngrp] = (uint16_t)nrun;
     __syncthreads();
-    // 5. plan: per group (thread owns groups tid, tid + NT, ...): slot, the
-    // first resident session the runs can reach, merged count, relocation
+    // plan every group of the chunk (thread owns groups tid, tid + NT, ...)
+    const RunsLds<W> rsrc{&L, recs};
     int64_t gslot[kMgPer];
     uint64_t gi0[kMgPer];
     uint32_t gM[kMgPer], gcap[kMgPer];
-    SessList gl[kMgPer];
+    SessKey ge[kMgPer];
     uint64_t need = 0;
     uint32_t nt = 0;
 #pragma unroll
@@ -893,12 +1487,11 @@ __global__ __launch_bounds__(kMgNT) void k_ss_merge(SessParams p, SessTable t, P
       gcap[u] = 0;
       gM[u] = 0;
       gi0[u] = 0;
-      gl[u] = SessList{0, 0, 0};
+      ge[u] = SessKey{0, 0, 0, 0, 0, 0};
       if (g >= ngrp) continue;
       const uint32_t ra = L.gfirst[g], rb = L.gfirst[g + 1];
-      const uint32_t key = L.key[L.rbeg[ra]];
       bool ins;
-      const int64_t sl = ss_find_or_insert(t, key, ins);
+      const int64_t sl = ss_find_or_insert(t, L.key[L.rbeg[ra]], ins);
       if (sl < 0) {
         err |= ERR_OOM;
         continue;
@@ -906,21 +1499,10 @@ __global__ __launch_bounds__(kMgNT) void k_ss_merge(SessParams p, SessTable t, P
       keys_new += ins ? 1 : 0;
       gslot[u] = sl;
       ++nt;
-      const SessList Ls = ins ? SessList{0, 0, 0} : t.lists[sl];
-      gl[u] = Ls;
-      const int64_t lo = (int64_t)((uint64_t)L.rs[ra] - (uint64_t)p.gap);
-      const uint64_t i0 = mg_first_end_ge(t, Ls.off, Ls.len, lo);
-      gi0[u] = i0;
-      MgSess<MS> dummy[kMgTail];
-      const uint32_t M = mg_sweep<MS, W, false>(L, prog, t, p.gap, recs, ra, rb, Ls.off, i0, Ls.len, false, dummy, 0,
-                                                0);
-      gM[u] = M;
-      // in place when the merged list fits and the rewritten tail fits the
-      // registers, else a fresh list (prefix copied)
-      if (i0 + M > Ls.cap || Ls.len - i0 > kMgTail) gcap[u] = ss_grow_cap(i0 + M + 1);
+      if (!ins) ge[u] = t.kt[sl];
+      mg_plan<MS>(prog, t, p.gap, rsrc, ra, rb, ge[u], gi0[u], gM[u], gcap[u]);
       need += gcap[u];
     }
-    // 6. reserve the chunk's relocations in the arena (all or nothing)
     uint64_t tneed;
     const uint64_t npos = mg_scan64(L, need, tneed);
     uint32_t ttot;
@@ -929,32 +1511,21 @@ __global__ __launch_bounds__(kMgNT) void k_ss_merge(SessParams p, SessTable t, P
       L.fail = 0;
       L.base = 0;
       if (tneed) {
-        unsigned long long *top = (unsigned long long *)&t.meta[M_TOP];
-        unsigned long long old = __hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (;;) {
-          if (old + tneed > t.arena_cap) {
-            L.fail = 1;
-            break;
-          }
-          const unsigned long long seen = atomicCAS(top, old, old + tneed);
-          if (seen == old) break;
-          old = seen;
-        }
-        L.base = old;
+        uint64_t base = 0;
+        L.fail = !arena_take(t, arena_region(b), tneed, base);
+        L.base = base;
       }
       L.tbase = (!L.fail && ttot) ? (uint32_t)atomicAdd((unsigned long long *)&t.meta[M_TLEN], (unsigned long long)ttot) : 0;
     }
     __syncthreads();
     if (L.fail) {
-      // resumable: nothing of this chunk was applied (keys inserted stay, idempotent)
+      // resumable at this chunk: nothing of it was applied (inserted keys stay)
       if (threadIdx.x == 0) {
         sp.progress[b] = c;
         atomicOr((unsigned int *)&t.meta[M_FAIL], 1u);
       }
       break;
     }
-    // 7. apply; the touched list + per-slot mark (lowest index this batch
-    // rewrote) let k_ss_emit write each touched session once per batch
     uint64_t my_alloc = L.base + npos;
     uint32_t tp = L.tbase + tpos;
     const uint64_t bmark = (uint64_t)(~p.batch_id) << 32;
@@ -963,46 +1534,27 @@ __global__ __launch_bounds__(kMgNT) void k_ss_merge(SessParams p, SessTable t, P
       const uint32_t g = u * kMgNT + threadIdx.x;
       if (g >= ngrp || gslot[u] < 0) continue;
       const uint32_t ra = L.gfirst[g], rb = L.gfirst[g + 1];
-      const SessList Ls = gl[u];
-      const uint64_t i0 = gi0[u];
       const bool reloc = gcap[u] != 0;
-      uint64_t dst = Ls.off;
+      uint64_t dst = ge[u].off;
       if (reloc) {
         dst = my_alloc;
         my_alloc += gcap[u];
-        for (uint64_t k = 0; k < i0; ++k) ss_copy(t, dst + k, t, Ls.off + k, ns);
       }
-      MgSess<MS> tail[kMgTail];
-#pragma unroll
-      for (int k = 0; k < kMgTail; ++k) {
-        const uint64_t j = i0 + k;
-        if (!reloc && j < Ls.len) {
-          tail[k].s = t.a_start[Ls.off + j];
-          tail[k].e = t.a_end[Ls.off + j];
-          tail[k].stamp = t.a_stamp[Ls.off + j];
-#pragma unroll
-          for (int s = 0; s < MS; ++s) tail[k].a[s] = s < ns ? t.a_aggs[(Ls.off + j) * ns + s] : 0;
-        } else {
-          tail[k].s = tail[k].e = 0;
-          tail[k].stamp = 0;
-#pragma unroll
-          for (int s = 0; s < MS; ++s) tail[k].a[s] = 0;
-        }
-        tail[k].fresh = false;
-      }
-      mg_sweep<MS, W, true>(L, prog, t, p.gap, recs, ra, rb, Ls.off, i0, Ls.len, !reloc, tail, dst, p.batch_id);
-      t.lists[gslot[u]] = SessList{dst, (uint32_t)(i0 + gM[u]), reloc ? gcap[u] : Ls.cap};
-      live_delta += (int64_t)gM[u] - (int64_t)(Ls.len - i0);
-      atomicMin((unsigned long long *)&t.emark[gslot[u]], (unsigned long long)(bmark | i0));
+      mg_apply<MS>(prog, t, p.gap, rsrc, ra, rb, ge[u], gi0[u], dst, reloc, p.batch_id);
+      SessKey &ke = t.kt[gslot[u]];
+      ke.off = dst;
+      ke.len = (uint32_t)(gi0[u] + gM[u]);
+      if (reloc) ke.cap = gcap[u];
+      atomicMin((unsigned long long *)&ke.emark, (unsigned long long)(bmark | gi0[u]));
       sp.touched[tp++] = (uint32_t)gslot[u];
+      live_delta += (int64_t)gM[u] - (int64_t)(ge[u].len - gi0[u]);
     }
     __syncthreads();
     if (c + 1 == nch && threadIdx.x == 0) sp.progress[b] = nch;
   }
-  // live sessions, keys, touched rows, errors
-  const uint64_t ld = mg_sum64(L, (uint64_t)live_delta);
-  const uint64_t kn = mg_sum64(L, keys_new);
-  if (threadIdx.x == 0) {
+  const uint64_t ld = wave_sum_u64((uint64_t)live_delta);
+  const uint64_t kn = wave_sum_u64(keys_new);
+  if (lane == 0) {
     if (ld) atomicAdd((unsigned long long *)&sc->live, (unsigned long long)ld);
     if (kn) atomicAdd((unsigned long long *)&t.meta[M_KEYS], (unsigned long long)kn);
   }
@@ -1010,31 +1562,31 @@ __global__ __launch_bounds__(kMgNT) void k_ss_merge(SessParams p, SessTable t, P
 }
 
 template <int MS>
-static void merge_launch_w(hipStream_t s, int words, dim3 g, const SessParams &p, const SessTable &t,
-                           const Program &prog, int np_log2, const SessPart &sp, DevScalars *sc) {
+static void big_launch_w(hipStream_t s, int words, dim3 g, const SessParams &p, const SessTable &t,
+                         const Program &prog, int nl, int bs, const SessPart &sp, DevScalars *sc) {
   const dim3 th(kMgNT);
   switch (words) {
-    case 2: hipLaunchKernelGGL((k_ss_merge<MS, 2>), g, th, 0, s, p, t, prog, np_log2, sp, sc); break;
-    case 3: hipLaunchKernelGGL((k_ss_merge<MS, 3>), g, th, 0, s, p, t, prog, np_log2, sp, sc); break;
-    case 4: hipLaunchKernelGGL((k_ss_merge<MS, 4>), g, th, 0, s, p, t, prog, np_log2, sp, sc); break;
-    case 5: hipLaunchKernelGGL((k_ss_merge<MS, 5>), g, th, 0, s, p, t, prog, np_log2, sp, sc); break;
-    case 6: hipLaunchKernelGGL((k_ss_merge<MS, 6>), g, th, 0, s, p, t, prog, np_log2, sp, sc); break;
-    default: hipLaunchKernelGGL((k_ss_merge<MS, kSessMaxWords>), g, th, 0, s, p, t, prog, np_log2, sp, sc); break;
+    case 2: hipLaunchKernelGGL((k_ss_merge_big<MS, 2>), g, th, 0, s, p, t, prog, nl, bs, sp, sc); break;
+    case 3: hipLaunchKernelGGL((k_ss_merge_big<MS, 3>), g, th, 0, s, p, t, prog, nl, bs, sp, sc); break;
+    case 4: hipLaunchKernelGGL((k_ss_merge_big<MS, 4>), g, th, 0, s, p, t, prog, nl, bs, sp, sc); break;
+    default: hipLaunchKernelGGL((k_ss_merge_big<MS, kSessMaxWords>), g, th, 0, s, p, t, prog, nl, bs, sp, sc); break;
   }
 }
 
-void launch_ss_merge(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, int np_log2,
-                     int words, const SessPart &sp, DevScalars *sc) {
+void launch_ss_merge_big(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, int np_log2,
+                         int bshift, int words, const SessPart &sp, DevScalars *sc) {
   const dim3 g(1u << np_log2);
-  if (prog.n_slots <= 2) merge_launch_w<2>(s, words, g, p, t, prog, np_log2, sp, sc);
-  else if (prog.n_slots <= 4) merge_launch_w<4>(s, words, g, p, t, prog, np_log2, sp, sc);
-  else merge_launch_w<8>(s, words, g, p, t, prog, np_log2, sp, sc);
+  if (prog.n_slots <= 2) big_launch_w<2>(s, words, g, p, t, prog, np_log2, bshift, sp, sc);
+  else if (prog.n_slots <= 4) big_launch_w<4>(s, words, g, p, t, prog, np_log2, bshift, sp, sc);
+  else big_launch_w<8>(s, words, g, p, t, prog, np_log2, bshift, sp, sc);
 }
 
-// Per-batch changelog of the merge path: every session of a touched key at or
+// ---------------------------------------------------------------------------
+// per-batch changelog of the merge path: every session of a touched key at or
 // after the lowest index the batch rewrote, stamped by this batch. A key may
-// appear once per chunk in the touched list; the first entry to take the
-// slot's mark (resetting it) emits. emit = 0: count only (state-only ops).
+// be in the touched list more than once (a big bucket: once per chunk); the
+// entry that takes the key's mark (resetting it) emits. emit = 0: count only.
+// ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_ss_emit(SessTable t, Program prog, SessPart sp, uint32_t batch_id, int emit,
                                                  OutCols out, uint64_t out_base, DevScalars *sc) {
   __shared__ uint64_t swave[4];
@@ -1043,19 +1595,18 @@ __global__ __launch_bounds__(256) void k_ss_emit(SessTable t, Program prog, Sess
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (uint64_t blk = blockIdx.x * 256ull; blk < n; blk += (uint64_t)gridDim.x * 256ull) {
     const uint64_t q = blk + threadIdx.x;
-    uint64_t cnt = 0, i0 = 0;
-    SessList Ls = {0, 0, 0};
+    uint64_t cnt = 0, i0 = 0, off = 0, len = 0;
     uint32_t key = 0;
     if (q < n) {
       const uint32_t sl = sp.touched[q];
-      const uint64_t m = atomicExch((unsigned long long *)&t.emark[sl], ~0ull);
-      if ((uint32_t)(m >> 32) == ~batch_id) {
-        i0 = m & 0xFFFFFFFFull;
-        Ls = t.lists[sl];
-        key = t.keys[sl];
-        for (uint64_t k = i0; k < Ls.len; ++k) cnt += t.a_stamp[Ls.off + k] == batch_id;
-      } else {
-        Ls.len = 0;
+      const uint64_t mk = atomicExch((unsigned long long *)&t.kt[sl].emark, ~0ull);
+      if ((uint32_t)(mk >> 32) == ~batch_id) {
+        i0 = mk & 0xFFFFFFFFull;
+        const SessKey e = t.kt[sl];
+        key = e.key;
+        off = e.off;
+        len = e.len;
+        for (uint64_t k = i0; k < len; ++k) cnt += (uint32_t)ss_row(t, off + k)[2] == batch_id;
       }
     }
     const uint64_t incl = wave_incl_sum(cnt);
@@ -1070,15 +1621,14 @@ __global__ __launch_bounds__(256) void k_ss_emit(SessTable t, Program prog, Sess
     if (emit && cnt) {
       uint64_t o = out_base + sbase + incl - cnt;
       for (int k = 0; k < w; ++k) o += swave[k];
-      for (uint64_t k = i0; k < Ls.len; ++k) {
-        const uint64_t a = Ls.off + k;
-        if (t.a_stamp[a] != batch_id) continue;
+      for (uint64_t k = i0; k < len; ++k) {
+        const uint64_t *row = ss_row(t, off + k);
+        if ((uint32_t)row[2] != batch_id) continue;
         out.key[o] = key;
-        out.ws[o] = t.a_start[a];
-        out.we[o] = t.a_end[a];
+        out.ws[o] = (int64_t)row[0];
+        out.we[o] = (int64_t)row[1];
         out.src[o] = -1;
-        const int64_t *row = t.a_aggs + a * prog.n_slots;
-        for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, row);
+        for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, (const int64_t *)row + 3);
         ++o;
       }
     }
@@ -1109,11 +1659,11 @@ __global__ __launch_bounds__(256) void k_ss_dump(SessTable t, Program prog, OutC
     uint64_t len = 0, off = 0;
     uint32_t key = kSessEmptyKey;
     if (s < cap) {
-      key = t.keys[s];
+      const SessKey e = t.kt[s];
+      key = e.key;
       if (key != kSessEmptyKey) {
-        const SessList Ls = t.lists[s];
-        len = Ls.len;
-        off = Ls.off;
+        len = e.len;
+        off = e.off;
       }
     }
     const uint64_t incl = wave_incl_sum(len);
@@ -1127,12 +1677,12 @@ __global__ __launch_bounds__(256) void k_ss_dump(SessTable t, Program prog, OutC
     uint64_t o = sbase + incl - len;
     for (int k = 0; k < w; ++k) o += swave[k];
     for (uint64_t k = 0; k < len && o < out_cap; ++k, ++o) {
+      const uint64_t *row = ss_row(t, off + k);
       out.key[o] = key;
-      out.ws[o] = t.a_start[off + k];
-      out.we[o] = t.a_end[off + k];
+      out.ws[o] = (int64_t)row[0];
+      out.we[o] = (int64_t)row[1];
       out.src[o] = -1;
-      const int64_t *row = t.a_aggs + (off + k) * prog.n_slots;
-      for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, row);
+      for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, (const int64_t *)row + 3);
     }
     __syncthreads();
   }

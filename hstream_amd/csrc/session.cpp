@@ -4,6 +4,7 @@
 // replay: per-key arrival-order replay for the per-record changelog and LAST).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -43,78 +44,107 @@ static bool has_last(const Program &prog) {
 }
 
 static int alloc_keys(SessTable &t, uint64_t kcap, std::string &err) {
-  DTRY(hipMalloc((void **)&t.keys, kcap * sizeof(uint32_t)));
-  DTRY(hipMalloc((void **)&t.lists, kcap * sizeof(SessList)));
-  DTRY(hipMalloc((void **)&t.emark, kcap * sizeof(uint64_t)));
+  DTRY(hipMalloc((void **)&t.kt, kcap * sizeof(SessKey)));
   t.kmask = kcap - 1;
   return HSG_OK;
 }
 
 static void free_keys(SessTable &t) {
-  if (t.keys) hipFree(t.keys);
-  if (t.lists) hipFree(t.lists);
-  if (t.emark) hipFree(t.emark);
-  t.keys = nullptr;
-  t.lists = nullptr;
-  t.emark = nullptr;
+  if (t.kt) hipFree(t.kt);
+  t.kt = nullptr;
 }
 
-static int alloc_arena(SessTable &t, uint64_t cap, int ns, std::string &err) {
-  DTRY(hipMalloc((void **)&t.a_start, cap * sizeof(int64_t)));
-  DTRY(hipMalloc((void **)&t.a_end, cap * sizeof(int64_t)));
-  DTRY(hipMalloc((void **)&t.a_stamp, cap * sizeof(uint32_t)));
-  DTRY(hipMalloc((void **)&t.a_aggs, cap * (uint64_t)(ns ? ns : 1) * sizeof(int64_t)));
+static int alloc_arena(SessTable &t, uint64_t cap, std::string &err) {
+  DTRY(hipMalloc((void **)&t.rows, cap * t.stride * sizeof(uint64_t)));
   t.arena_cap = cap;
   return HSG_OK;
 }
 
 static void free_arena(SessTable &t) {
-  if (t.a_start) hipFree(t.a_start);
-  if (t.a_end) hipFree(t.a_end);
-  if (t.a_stamp) hipFree(t.a_stamp);
-  if (t.a_aggs) hipFree(t.a_aggs);
-  t.a_start = t.a_end = nullptr;
-  t.a_stamp = nullptr;
-  t.a_aggs = nullptr;
+  if (t.rows) hipFree(t.rows);
+  t.rows = nullptr;
 }
 
-// Session partition scratch: per-tile ts maxima and per-bucket progress.
-static SessPart sess_part(OpDevice &d) {
+// Arena regions over the free rows [used, arena_cap): bump pointers and ends
+// (hsg_session.h), written on the op's stream. The pinned staging words are
+// the op's own (d.h_regions), never reused while a copy may be pending: the
+// call synchronises the stream first.
+static int set_regions(OpDevice &d, uint64_t used, std::string &err) {
+  DTRY(hipStreamSynchronize(d.stream));
+  const uint64_t cap = d.ss.arena_cap, per = (cap - used) / kArenaRegions;
+  memset(d.h_regions, 0, kArenaRegions * kRegionStride * sizeof(uint64_t));
+  for (int r = 0; r < kArenaRegions; ++r) {
+    d.h_regions[r * kRegionStride] = used + (uint64_t)r * per;
+    d.h_regions[r * kRegionStride + 1] = r + 1 == kArenaRegions ? cap : used + (uint64_t)(r + 1) * per;
+  }
+  DTRY(hipMemcpyAsync(d.ss.meta + M_RTOP, d.h_regions, kArenaRegions * kRegionStride * sizeof(uint64_t),
+                      hipMemcpyHostToDevice, d.stream));
+  DTRY(hipStreamSynchronize(d.stream));
+  return HSG_OK;
+}
+
+// Session partition scratch (besides d.part's histogram, offsets and
+// records): per-tile ts maxima, per-bucket progress and big flags, the touched
+// list, the runs and key groups of k_ss_sort, the apply blocks' done flags.
+static uint64_t ss_part_layout(uint64_t n, int words, SessPart *sp, char *m) {
+  uint64_t off = 0;
+  auto take = [&](uint64_t bytes) {
+    off = (off + 255) & ~255ull;
+    const uint64_t o = off;
+    off += bytes ? bytes : 1;
+    return m ? m + o : nullptr;
+  };
+  const uint64_t tiles = part_tiles(n, kPartTileRecs) + 1, nb = 1ull << kPartMaxLog2;
+  SessPart x;
+  memset(&x, 0, sizeof(x));
+  x.tmax = (uint64_t *)take(tiles * 8);
+  x.progress = (uint32_t *)take(nb * 4);
+  x.bigmask = (uint64_t *)take(nb * 8);
+  x.touched = (uint32_t *)take(n * 4);
+  x.srec = (uint64_t *)take(n * (uint64_t)words * 8);
+  x.groups = (uint32_t *)take(n * 16);
+  x.done = (uint8_t *)take(n / 256 + 2);
+  x.sidx = (uint16_t *)take(n * 2);
+  x.gsparse = (uint32_t *)take(n * 16);
+  if (sp) *sp = x;
+  return off;
+}
+
+static SessPart sess_part(OpDevice &d, int words) {
   SessPart sp;
+  ss_part_layout(d.batch_cap, words, &sp, (char *)d.ss_part);
   sp.hist = d.part.hist;
   sp.offt = d.part.offt;
   sp.bstart = d.part.bstart;
   sp.rec = d.part.rec;
-  char *m = (char *)d.ss_part;
-  sp.tmax = (uint64_t *)m;
-  const uint64_t tiles = part_tiles(d.batch_cap, kPartTileRecs) + 1;
-  const uint64_t o_prog = (tiles * 8 + 255) & ~255ull;
-  sp.progress = (uint32_t *)(m + o_prog);
-  sp.touched = (uint32_t *)(m + o_prog + (((1ull << kPartMaxLog2) * 4 + 255) & ~255ull));
   return sp;
 }
 
 int session_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t rows, std::string &err) {
   SessTable &t = d.ss;
   memset(&t, 0, sizeof(t));
+  t.ns = (uint32_t)prog.n_slots;
+  t.stride = 3 + (uint32_t)prog.n_slots;
   // key table: keys <= sessions; grown by rehash as keys arrive (push_session)
   uint64_t kc = rows < d.batch_cap ? rows : d.batch_cap;
   const uint64_t kcap = pow2_at_least(2 * (kc > (1u << 14) ? kc : (1u << 14)));
   int rc = alloc_keys(t, kcap, err);
   if (rc != HSG_OK) return rc;
   d.cap = kcap;
-  // arena: the expected live sessions, grown by compaction when a batch needs more
-  rc = alloc_arena(t, pow2_at_least(rows > (1u << 20) ? rows : (1u << 20)), prog.n_slots, err);
+  // arena: the expected live sessions, grown by compaction when a batch needs
+  // more (HSG_SESS_ARENA_MIN: a smaller floor, so tests reach the refills)
+  uint64_t amin = 1u << 20;
+  if (const char *e = getenv("HSG_SESS_ARENA_MIN")) amin = strtoull(e, nullptr, 10) ? strtoull(e, nullptr, 10) : amin;
+  rc = alloc_arena(t, pow2_at_least(rows > amin ? rows : amin), err);
   if (rc != HSG_OK) return rc;
   DTRY(hipMalloc((void **)&t.meta, M_WORDS * sizeof(uint64_t)));
   DTRY(hipHostMalloc((void **)&d.h_meta, M_WORDS * sizeof(uint64_t), hipHostMallocDefault));
+  DTRY(hipHostMalloc((void **)&d.h_regions, kArenaRegions * kRegionStride * sizeof(uint64_t), hipHostMallocDefault));
   d.ss_merge = cfg.emit_mode != HSG_EMIT_PER_RECORD && !has_last(prog) && prog.n_slots <= 8;
   if (d.ss_merge) {
     rc = part_device_init(d, cfg, prog, err);
     if (rc != HSG_OK) return rc;
-    const uint64_t tiles = part_tiles(d.batch_cap, kPartTileRecs) + 1;
-    DTRY(hipMalloc(&d.ss_part, ((tiles * 8 + 255) & ~255ull) + (((1ull << kPartMaxLog2) * 4 + 255) & ~255ull) +
-                                   d.batch_cap * 4 + 256));
+    DTRY(hipMalloc(&d.ss_part, ss_part_layout(d.batch_cap, 2 + cfg.n_cols, nullptr, nullptr)));
   }
   return HSG_OK;
 }
@@ -123,7 +153,7 @@ int session_device_reset(OpDevice &d, std::string &err) {
   launch_ss_reset(d.stream, d.ss);
   DTRY(hipMemsetAsync(d.ss.meta, 0, M_WORDS * sizeof(uint64_t), d.stream));
   d.ss_keys = 0;
-  return HSG_OK;
+  return set_regions(d, 0, err);
 }
 
 void session_device_free(OpDevice &d) {
@@ -133,6 +163,8 @@ void session_device_free(OpDevice &d) {
   d.ss.meta = nullptr;
   if (d.h_meta) hipHostFree(d.h_meta);
   d.h_meta = nullptr;
+  if (d.h_regions) hipHostFree(d.h_regions);
+  d.h_regions = nullptr;
   if (d.ss_part) hipFree(d.ss_part);
   d.ss_part = nullptr;
 }
@@ -143,9 +175,7 @@ static int ensure_keys(OpDevice &d, uint64_t incoming, std::string &err) {
   if (2 * (d.ss_keys + incoming) <= kcap) return HSG_OK;
   const uint64_t ncap = pow2_at_least(2 * (d.ss_keys + incoming) + 1);
   SessTable to = d.ss;
-  to.keys = nullptr;
-  to.lists = nullptr;
-  to.emark = nullptr;
+  to.kt = nullptr;
   int rc = alloc_keys(to, ncap, err);
   if (rc != HSG_OK) {
     free_keys(to);
@@ -155,9 +185,7 @@ static int ensure_keys(OpDevice &d, uint64_t incoming, std::string &err) {
   DTRY(hipGetLastError());
   DTRY(hipStreamSynchronize(d.stream));
   free_keys(d.ss);
-  d.ss.keys = to.keys;
-  d.ss.lists = to.lists;
-  d.ss.emark = to.emark;
+  d.ss.kt = to.kt;
   d.ss.kmask = to.kmask;
   d.cap = ncap;
   return HSG_OK;
@@ -171,30 +199,26 @@ static int refill_arena(OpDevice &d, const Program &prog, uint64_t extra, std::s
   const uint64_t kcap = t.kmask + 1;
   void *scratch = nullptr;
   DTRY(hipMalloc(&scratch, ss_compact_scratch_bytes(kcap)));
-  uint64_t *total = d.h_meta + M_WORDS - 1;  // pinned word used as the landing slot
-  launch_ss_compact_plan(d.stream, t, scratch, t.meta + M_WORDS - 1);
-  hipMemcpyAsync(total, t.meta + M_WORDS - 1, 8, hipMemcpyDeviceToHost, d.stream);
+  launch_ss_compact_plan(d.stream, t, scratch, t.meta + M_SCRATCH);
+  hipMemcpyAsync(d.h_meta + M_SCRATCH, t.meta + M_SCRATCH, 8, hipMemcpyDeviceToHost, d.stream);
   hipError_t e = hipStreamSynchronize(d.stream);
   if (e != hipSuccess) {
     hipFree(scratch);
     err = std::string("session compaction: ") + hipGetErrorString(e);
     return HSG_E_DEVICE;
   }
-  const uint64_t used = *total;
+  const uint64_t used = d.h_meta[M_SCRATCH];
   uint64_t cap = t.arena_cap;
   while (cap < 2 * used + extra) cap <<= 1;
   SessTable to = t;
-  to.a_start = to.a_end = nullptr;
-  to.a_stamp = nullptr;
-  to.a_aggs = nullptr;
-  int rc = alloc_arena(to, cap, prog.n_slots, err);
+  to.rows = nullptr;
+  int rc = alloc_arena(to, cap, err);
   if (rc != HSG_OK) {
     free_arena(to);
     hipFree(scratch);
     return rc;
   }
-  launch_ss_compact_copy(d.stream, t, to, prog.n_slots, scratch);
-  hipMemcpyAsync(t.meta + M_TOP, t.meta + M_WORDS - 1, 8, hipMemcpyDeviceToDevice, d.stream);
+  launch_ss_compact_copy(d.stream, t, to, scratch);
   e = hipStreamSynchronize(d.stream);
   hipFree(scratch);
   if (e != hipSuccess) {
@@ -203,12 +227,9 @@ static int refill_arena(OpDevice &d, const Program &prog, uint64_t extra, std::s
     return HSG_E_DEVICE;
   }
   free_arena(t);
-  t.a_start = to.a_start;
-  t.a_end = to.a_end;
-  t.a_stamp = to.a_stamp;
-  t.a_aggs = to.a_aggs;
+  t.rows = to.rows;
   t.arena_cap = to.arena_cap;
-  return HSG_OK;
+  return set_regions(d, used, err);
 }
 
 static int finish_session_batch(OpDevice &d, int64_t wm_in, uint64_t n, PushResult &r, std::string &err) {
@@ -217,12 +238,13 @@ static int finish_session_batch(OpDevice &d, int64_t wm_in, uint64_t n, PushResu
 }
 
 static int clear_fail(OpDevice &d, std::string &err) {
-  DTRY(hipMemsetAsync(d.ss.meta + M_NEED, 0, 2 * sizeof(uint64_t), d.stream));  // M_NEED, M_FAIL
+  DTRY(hipMemsetAsync(d.ss.meta + M_FAIL, 0, sizeof(uint64_t), d.stream));
+  DTRY(hipMemsetAsync(d.ss.meta + M_RNEED, 0, kArenaRegions * sizeof(uint64_t), d.stream));
   return HSG_OK;
 }
 
-// merge path: partition by key hash, then per bucket chunk: sort by (key, ts),
-// gap-delimited runs, sweep-merge per key with its resident sessions
+// merge path: partition by key hash, per bucket sort / runs / key groups,
+// one thread per key merges its runs into its sessions
 static int push_session_merge(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
                               const Batch &kb, PushResult &r, std::string &err) {
   const uint64_t n = kb.n;
@@ -231,10 +253,10 @@ static int push_session_merge(OpDevice &d, const hsg_op_config &cfg, const Progr
   sp.rec_base = a.rec_base;
   sp.batch_id = a.batch_id;
   sp.emit_mode = cfg.emit_mode;
-  SessPart pt = sess_part(d);
+  SessPart pt = sess_part(d, 2 + cfg.n_cols);
   const uint64_t tiles = part_tiles(n, kPartTileRecs);
-  // buckets of about one sort chunk (2048 records) each
-  int nl = log2u((n + 2047) / 2048);
+  // buckets of about two sorts (k_ss_sort splits them in sub-buckets)
+  int nl = log2u((n + 4095) / 4096);
   nl = nl < 4 ? 4 : (nl > kPartMaxLog2 ? kPartMaxLog2 : nl);
   bool has_valid = false;
   for (int c = 0; c < cfg.n_cols; ++c) has_valid = has_valid || kb.valid[c] != nullptr;
@@ -245,32 +267,38 @@ static int push_session_merge(OpDevice &d, const hsg_op_config &cfg, const Progr
   pp.tiles = tiles;
   DTRY(hipEventRecord(d.ev_a, d.stream));
   DTRY(hipMemsetAsync(pt.progress, 0, (1ull << nl) * 4, d.stream));
-  launch_ss_phist(d.stream, kb, nl, tiles, pt);
+  DTRY(hipMemsetAsync(pt.done, 0, n / 256 + 2, d.stream));
+  launch_ss_phist(d.stream, kb, nl, d.bshift, tiles, pt);
   launch_ss_wm(d.stream, pt, tiles, a.wm_in, d.sc);
   launch_part_offsets(d.stream, pp, d.part, d.sc);
-  launch_ss_pscatter(d.stream, kb, nl, tiles, words, has_valid, pt);
-  launch_ss_merge(d.stream, sp, d.ss, prog, nl, words, pt, d.sc);
-  // the arena fill is only known on the host when a bucket could not reserve
-  // space: then it stopped at a chunk boundary; compact / grow and resume
-  DTRY(hipMemcpyAsync(d.h_meta, d.ss.meta, M_WORDS * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
-  DTRY(hipStreamSynchronize(d.stream));
-  DTRY(hipGetLastError());
-  while (d.h_meta[M_FAIL]) {
-    int rc = refill_arena(d, prog, 2 * n, err);
-    if (rc != HSG_OK) return rc;
-    rc = clear_fail(d, err);
-    if (rc != HSG_OK) return rc;
-    launch_ss_merge(d.stream, sp, d.ss, prog, nl, words, pt, d.sc);
+  launch_ss_pscatter(d.stream, kb, nl, d.bshift, tiles, words, has_valid, pt);
+  launch_ss_sort(d.stream, sp, d.ss, prog, nl, d.bshift, words, pt, d.sc);
+  // a pass stops short (M_FAIL) only where the arena could not take a key's
+  // fresh list: those apply blocks / big-bucket chunks were left untouched;
+  // compact / grow the arena, then run the pass again (done work is skipped)
+  for (int attempt = 0;; ++attempt) {
+    launch_ss_apply(d.stream, sp, d.ss, prog, n, words, pt, d.out, a.pending, d.sc);
+    launch_ss_merge_big(d.stream, sp, d.ss, prog, nl, d.bshift, words, pt, d.sc);
     DTRY(hipMemcpyAsync(d.h_meta, d.ss.meta, M_WORDS * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
     DTRY(hipStreamSynchronize(d.stream));
     DTRY(hipGetLastError());
+    if (!d.h_meta[M_FAIL]) break;
+    if (attempt >= 8) {
+      err = "session arena: no room after compaction";
+      return HSG_E_OOM;
+    }
+    int rc = refill_arena(d, prog, (2 * n) << attempt, err);
+    if (rc != HSG_OK) return rc;
+    rc = clear_fail(d, err);
+    if (rc != HSG_OK) return rc;
   }
   launch_ss_emit(d.stream, d.ss, prog, pt, a.batch_id, cfg.emit_mode == HSG_EMIT_PER_BATCH ? 1 : 0, n, d.out,
                  a.pending, d.sc);
   DTRY(hipEventRecord(d.ev_b, d.stream));
   DTRY(hipGetLastError());
   int rc = finish_session_batch(d, a.wm_in, n, r, err);
-  if (cfg.emit_mode != HSG_EMIT_PER_BATCH) r.out_rows = 0;
+  if (cfg.emit_mode == HSG_EMIT_PER_BATCH) r.touched = r.out_rows;
+  else r.out_rows = 0;
   return rc;
 }
 
@@ -313,7 +341,10 @@ static int push_session_replay(OpDevice &d, const hsg_op_config &cfg, const Prog
     rc = finish_session_batch(d, a.wm_in, n, r, err);
     if (rc != HSG_OK || !d.h_meta[M_FAIL] || attempt > 0) break;
     // not enough arena for the lists that grow: compact / grow, then again
-    rc = refill_arena(d, prog, d.h_meta[M_NEED] + 2 * n, err);
+    // regions are equal after compaction: room for the largest region's need in each
+    uint64_t need = 0;
+    for (int q = 0; q < kArenaRegions; ++q) need = d.h_meta[M_RNEED + q] > need ? d.h_meta[M_RNEED + q] : need;
+    rc = refill_arena(d, prog, kArenaRegions * need + 2 * n, err);
     if (rc != HSG_OK) return rc;
     rc = clear_fail(d, err);
     if (rc != HSG_OK) return rc;
@@ -334,7 +365,9 @@ int push_session(OpDevice &d, const hsg_op_config &cfg, const Program &prog, con
   if (!kb.n) return finish_batch(d, a.wm_in, 0, r, err);
   rc = ensure_keys(d, kb.n, err);
   if (rc != HSG_OK) return rc;
-  DTRY(hipMemsetAsync(d.ss.meta + M_NEED, 0, 3 * sizeof(uint64_t), d.stream));  // need, fail, touched list
+  // per-batch words: need, fail, touched list, groups, runs, big buckets
+  DTRY(hipMemsetAsync(d.ss.meta + M_FAIL, 0, (M_BIG - M_FAIL + 1) * sizeof(uint64_t), d.stream));
+  DTRY(hipMemsetAsync(d.ss.meta + M_RNEED, 0, kArenaRegions * sizeof(uint64_t), d.stream));
   rc = d.ss_merge ? push_session_merge(d, cfg, prog, a, kb, r, err) : push_session_replay(d, cfg, prog, a, kb, seq, r, err);
   if (d.ss_merge) r.pairs = kb.n;  // keyed records (HSG_KEY_NONE are counted too; stats only)
   d.ss_keys = d.h_meta[M_KEYS];

@@ -1,0 +1,94 @@
+"""GPU parity of the session store's less common paths against the oracle
+(SessionWindowedStream.hs:84-118, Store.hs:243-272): hot keys whose bucket
+is merged chunk by chunk (k_ss_merge_big), arena compaction / growth in the
+middle of a batch (merge and replay paths), key-table growth by rehash."""
+import numpy as np
+import pytest
+
+import pyoracle
+from hstream_amd import abi
+from hstream_amd.columnar import OpSpec
+from util import ALL_AGG_SETS, gen_small, rows_equal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need cuda:0"
+    from hstream_amd.engine import Engine
+    e = Engine(device=0, batch_capacity=1 << 20)
+    yield e
+    e.close()
+
+
+def _drive(eng, spec, batches, faithful=True):
+    g, o = eng.op(spec), pyoracle.OracleOp(spec, faithful_sessions=faithful)
+    f64 = spec.agg_is_f64()
+    wg = wo = -1
+    for bi, (key, ts, cols, valid) in enumerate(batches):
+        wg = g.push(key, ts, cols, valid, watermark=wg)
+        wo = o.push(key, ts, cols, valid, watermark=wo)
+        assert wg == wo
+        if spec.emit_mode != abi.HSG_EMIT_NONE:
+            rows_equal(g.drain(), o.drain(), f64, ordered=spec.emit_mode == abi.HSG_EMIT_PER_RECORD,
+                       what=f"changelog batch {bi}")
+    rows_equal(g.dump_state(), o.dump_state(), f64, what="state")
+    st = g.stats()
+    g.close()
+    o.close()
+    return st
+
+
+def _hot_batches(seed, n, nb=3, hot_frac=0.4):
+    out = []
+    for bi in range(nb):
+        key, ts, cols, valid = gen_small(seed + bi, n, 50_000, col_types=(abi.HSG_I64, abi.HSG_F64),
+                                         span=200_000, base=20_000_000 + bi * 150_000)
+        rng = np.random.default_rng(seed + 100 + bi)
+        hot = rng.random(n) < hot_frac
+        key = np.where(hot & (key != abi.HSG_KEY_NONE), rng.integers(0, 3, size=n).astype(np.uint32), key)
+        out.append((key.astype(np.uint32), ts, cols, valid))
+    return out
+
+
+@pytest.mark.parametrize("mode", [abi.HSG_EMIT_PER_BATCH, abi.HSG_EMIT_NONE], ids=["per_batch", "none"])
+@pytest.mark.parametrize("gap", [0, 500, 5_000])
+def test_hot_keys_big_buckets(eng, mode, gap):
+    """A few keys take 40 % of each batch: their buckets exceed one LDS sort
+    and are merged chunk by chunk (k_ss_merge_big), the rest by k_ss_apply."""
+    aggs = [(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0), (abi.HSG_MIN, 1), (abi.HSG_MAX, 0), (abi.HSG_AVG, 1),
+            (abi.HSG_COUNT, 1)]
+    spec = OpSpec(abi.HSG_SESSION, mode, gap_ms=gap, col_types=[abi.HSG_I64, abi.HSG_F64], aggs=aggs)
+    _drive(eng, spec, _hot_batches(11, 300_000), faithful=False)
+
+
+@pytest.mark.parametrize("mode", [abi.HSG_EMIT_PER_BATCH, abi.HSG_EMIT_PER_RECORD], ids=["merge", "replay"])
+def test_arena_refill_mid_batch(eng, mode, monkeypatch):
+    """A 1024-row arena floor: every batch outgrows it, so blocks / chunks that
+    cannot reserve their lists stop, the host compacts and grows the arena and
+    the batch resumes; the result is unchanged."""
+    monkeypatch.setenv("HSG_SESS_ARENA_MIN", "1024")
+    spec = OpSpec(abi.HSG_SESSION, mode, gap_ms=300, col_types=[abi.HSG_I64, abi.HSG_F64],
+                  aggs=ALL_AGG_SETS["mixed"] if mode == abi.HSG_EMIT_PER_RECORD else
+                  [(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0), (abi.HSG_SUM, 1)], state_capacity=16)
+    batches = [gen_small(500 + bi, 40_000, 3_000, col_types=spec.col_types, span=120_000,
+                         base=7_000_000 + bi * 100_000) for bi in range(4)]
+    batches += _hot_batches(77, 20_000, nb=2)
+    _drive(eng, spec, batches, faithful=False)
+
+
+def test_key_table_growth(eng):
+    """state_capacity 16: the key table starts at its floor and is rehashed
+    as 400K distinct keys arrive over the batches."""
+    spec = OpSpec(abi.HSG_SESSION, abi.HSG_EMIT_PER_BATCH, gap_ms=1_000, col_types=[abi.HSG_I64],
+                  aggs=[(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0)], state_capacity=16)
+    batches = []
+    for bi in range(4):
+        rng = np.random.default_rng(900 + bi)
+        n = 200_000
+        key = rng.integers(0, 400_000, size=n).astype(np.uint32)
+        ts = (30_000_000 + bi * 40_000 + np.arange(n) // 10 + rng.integers(0, 3_000, size=n)).astype(np.int64)
+        batches.append((key, ts, [rng.integers(-1000, 1000, size=n, dtype=np.int64)], None))
+    _drive(eng, spec, batches, faithful=False)
