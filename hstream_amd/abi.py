@@ -135,6 +135,8 @@ class hsg_stats(C.Structure):
         ("state_row_bytes", C.c_uint64),
         ("spilled_rows", C.c_uint64),
         ("spill_events", C.c_uint64),
+        ("table_slots", C.c_uint64),
+        ("grow_events", C.c_uint64),
     ]
 
     def as_dict(self):

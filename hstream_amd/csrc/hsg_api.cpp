@@ -330,6 +330,7 @@ extern "C" int hsg_op_create(hsg_engine *eng, const hsg_op_config *cfg, hsg_op *
     }
     op->stats.state_slots = (uint64_t)op->prog.n_slots;
     op->stats.state_row_bytes = 8ull * (uint64_t)op->prog.n_slots + (cfg->window_kind == HSG_SESSION ? 16ull : 8ull);
+    op->stats.table_slots = op->dev.cap;
     *out = op;
     return HSG_OK;
   } catch (const std::bad_alloc &) {
@@ -371,6 +372,7 @@ extern "C" int hsg_op_reset(hsg_op *op) {
     op->rec_base = 0;
     op->stats.state_rows = 0;
     op->stats.pending_rows = 0;
+    op->stats.spilled_rows = 0;
     return HSG_OK;
   } catch (...) {
     return HSG_E_DEVICE;
@@ -421,6 +423,10 @@ static int push_sync(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark) {
     op->stats.pairs_total += res.pairs;
     op->stats.touched_total += res.touched;
     op->stats.state_rows = op->state_rows;
+    op->stats.spilled_rows = op->dev.spilled_rows;
+    op->stats.spill_events = op->dev.spill_events;
+    op->stats.table_slots = op->dev.cap;
+    op->stats.grow_events = op->dev.grow_events;
     op->stats.pending_rows = op->pending;
     op->stats.last_batch_ms = now_ms() - t0;
     op->stats.agg_kernel_ms += res.agg_ms;

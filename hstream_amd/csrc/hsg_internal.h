@@ -238,6 +238,15 @@ uint64_t emit_chunks(uint64_t cap);
 void launch_tw_emit(hipStream_t s, const TwTable &t, uint64_t cap, const Program &prog, const TwParams &p, int mode,
                     OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc, const EmitScratch &es,
                     uint64_t *total);
+// retention (retention.cpp): rows closed at p.wm_in (end + grace <= stream
+// time). dst == nullptr: count them (*total, device; es.off = chunk offsets);
+// else copy them, raw row words in slot order, to dst (after the count).
+void launch_tw_closed(hipStream_t s, const TwTable &t, uint64_t cap, const TwParams &p, const DevScalars *sc,
+                      const EmitScratch &es, uint64_t *total, uint64_t *dst);
+// rows src[0, n) (stride = dst.stride words) into dst, skipping empty rows
+// and, with skip_closed, closed ones; *kept += rows inserted
+void launch_tw_reinsert(hipStream_t s, const uint64_t *src, uint64_t n, const TwTable &dst, const TwParams &p,
+                        DevScalars *sc, bool skip_closed, unsigned long long *kept);
 unsigned grid_for(uint64_t n, unsigned tpb);
 
 constexpr int kTileThreads = 256;

@@ -2,7 +2,9 @@
 // hsg_api.cpp. Not part of the ABI.
 #pragma once
 
+#include <cstdint>
 #include <string>
+#include <vector>
 
 #include "hsg_internal.h"
 #include "hsg_part.h"
@@ -80,6 +82,13 @@ struct OpDevice {
   uint64_t ss_live_max = 0;       // sessions the arena was last compacted for
   void *ss_part = nullptr;        // session partition scratch (tmax, progress)
   bool ss_merge = false;          // sessions take the sort + runs + merge path (else replay)
+  // retention (retention.cpp): closed windows moved out of HBM, raw rows of
+  // tw.stride words in host memory; hsg_dump_state appends them
+  std::vector<uint64_t> spill;
+  uint64_t spilled_rows = 0;
+  uint64_t spill_events = 0;
+  uint64_t grow_events = 0;
+  int64_t spill_wm = INT64_MIN;   // highest stream time a spill closed windows at
   // changelog buffer: the op's own, or caller-owned device columns
   // registered with hsg_op_set_changelog (rows land there directly)
   OutCols out = {};
@@ -136,8 +145,23 @@ void op_device_free(OpDevice &d);
 int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err);
 int op_push(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, PushResult &r,
             std::string &err);
+// rows [from, from + n) of src into out at row dst_off
 int op_copy_rows(OpDevice &d, const OutCols &src, uint64_t from, uint64_t n, int n_aggs, const hsg_rows *out,
-                 std::string &err);
+                 std::string &err, uint64_t dst_off = 0);
+
+// retention (retention.cpp)
+// table geometry for `cap` slots (stride and bshift kept)
+void tw_configure(TwTable &t, uint64_t cap, int window_kind);
+// Before a time-window batch of n_in records at stream time wm_in: when the
+// table could pass 3/4 load, move closed windows to the host and rebuild the
+// table (growing it until the open rows plus the batch's bound fit at 1/2).
+// A watermark below the last spill's brings every spilled row back first.
+int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t n_in, int64_t wm_in,
+                uint64_t pending, std::string &err);
+// append the spilled rows to a dump at row dst_off (*n_out = rows written)
+int tw_dump_spilled(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hsg_rows *out,
+                    uint64_t dst_off, uint64_t *n_out, std::string &err);
+void tw_retention_reset(OpDevice &d);
 int op_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hsg_rows *out, uint64_t *n_out,
             std::string &err);
 

@@ -387,6 +387,99 @@ __global__ __launch_bounds__(256) void k_tw_emit_rows(TwTable t, uint64_t cap, P
 
 uint64_t emit_chunks(uint64_t cap) { return (cap + kEmitChunk - 1) / kEmitChunk; }
 
+// ---------------------------------------------------------------------------
+// retention (retention.cpp): a window is closed once the stream time has
+// reached its end + grace, since stream time never decreases, no later record
+// passes the grace check of TimeWindowedStream.hs:92 for it. Closed rows are
+// copied out whole (raw row words) to be kept on the host; the table is
+// rebuilt from the rest, into the same or a larger capacity.
+// ---------------------------------------------------------------------------
+__device__ inline bool tw_row_closed(uint64_t g, int64_t k_epoch, const TwParams &p) {
+  if (g == kEmpty || p.kind == HSG_UNWINDOWED) return false;
+  const uint64_t k = (uint64_t)k_epoch + (g & 0xFFFFFFFFull);
+  return !window_accepted(p, k, p.wm_in);
+}
+
+__global__ __launch_bounds__(256) void k_tw_closed_count(TwTable t, uint64_t cap, TwParams p, const DevScalars *sc,
+                                                         uint32_t *cnt) {
+  __shared__ uint64_t sw[4];
+  const int64_t k_epoch = sc->k_epoch;
+  const uint64_t c0 = (uint64_t)blockIdx.x * kEmitChunk;
+  uint64_t h = 0;
+  for (uint64_t s = c0 + threadIdx.x; s < c0 + kEmitChunk && s < cap; s += 256) h += tw_row_closed(*t.key(s), k_epoch, p);
+  h = wave_sum_u64(h);
+  if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = (uint32_t)(sw[0] + sw[1] + sw[2] + sw[3]);
+}
+
+// closed rows, in slot order, to dst[row][stride] at the scanned chunk offsets
+__global__ __launch_bounds__(256) void k_tw_closed_copy(TwTable t, uint64_t cap, TwParams p, const DevScalars *sc,
+                                                        const uint64_t *off, uint64_t *__restrict__ dst) {
+  __shared__ uint64_t swave[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t k_epoch = sc->k_epoch;
+  const uint64_t c0 = (uint64_t)blockIdx.x * kEmitChunk;
+  uint64_t run = off[blockIdx.x];
+  for (uint64_t blk = c0; blk < c0 + kEmitChunk; blk += 256) {
+    const uint64_t s = blk + threadIdx.x;
+    const bool hit = s < cap && tw_row_closed(*t.key(s), k_epoch, p);
+    const uint64_t f = hit ? 1 : 0;
+    const uint64_t incl = wave_incl_sum(f);
+    if (lane == 63) swave[w] = incl;
+    __syncthreads();
+    uint64_t o = run + incl - f;
+    for (int k = 0; k < w; ++k) o += swave[k];
+    run += swave[0] + swave[1] + swave[2] + swave[3];
+    __syncthreads();
+    if (!hit) continue;
+    const uint64_t *src = t.key(s);
+    for (uint32_t q = 0; q < t.stride; ++q) dst[o * t.stride + q] = src[q];
+  }
+}
+
+// Rows src[0, n) (a table's slots or dense rows, `stride` words each) into
+// table dst: empty rows skipped, closed rows too when skip_closed; every row
+// is a distinct group, so an insert never meets a concurrent insert of its own
+// group. *kept counts the rows inserted.
+__global__ __launch_bounds__(256) void k_tw_reinsert(const uint64_t *__restrict__ src, uint64_t n, TwTable dst,
+                                                     TwParams p, DevScalars *sc, int skip_closed,
+                                                     unsigned long long *kept) {
+  const int64_t k_epoch = sc->k_epoch;
+  uint32_t fresh = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t *row = src + i * dst.stride;
+    const uint64_t g = row[0];
+    if (g == kEmpty || (skip_closed && tw_row_closed(g, k_epoch, p))) continue;
+    const int64_t s = tw_find_or_insert(dst, g, fresh);
+    if (s < 0) {
+      atomicOr(&sc->err, ERR_OOM);
+      continue;
+    }
+    uint64_t *d = dst.key((uint64_t)s);
+    for (uint32_t q = 1; q < dst.stride; ++q) d[q] = row[q];
+  }
+  const uint64_t tot = wave_sum_u64(fresh);
+  if ((threadIdx.x & 63) == 0 && tot) atomicAdd(kept, (unsigned long long)tot);
+}
+
+void launch_tw_closed(hipStream_t s, const TwTable &t, uint64_t cap, const TwParams &p, const DevScalars *sc,
+                      const EmitScratch &es, uint64_t *total, uint64_t *dst) {
+  const uint64_t nb = emit_chunks(cap);
+  if (!dst) {
+    hipLaunchKernelGGL(k_tw_closed_count, dim3((unsigned)nb), dim3(256), 0, s, t, cap, p, sc, es.cnt);
+    scan_excl_u32(s, es.cnt, es.off, nb, es.partial, total);
+  } else {
+    hipLaunchKernelGGL(k_tw_closed_copy, dim3((unsigned)nb), dim3(256), 0, s, t, cap, p, sc, es.off, dst);
+  }
+}
+
+void launch_tw_reinsert(hipStream_t s, const uint64_t *src, uint64_t n, const TwTable &dst, const TwParams &p,
+                        DevScalars *sc, bool skip_closed, unsigned long long *kept) {
+  if (n) hipLaunchKernelGGL(k_tw_reinsert, dim3(grid_for(n, 256)), dim3(256), 0, s, src, n, dst, p, sc,
+                            skip_closed ? 1 : 0, kept);
+}
+
 void launch_tw_emit(hipStream_t s, const TwTable &t, uint64_t cap, const Program &prog, const TwParams &p, int mode,
                     OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc, const EmitScratch &es,
                     uint64_t *total) {

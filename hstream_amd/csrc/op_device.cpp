@@ -146,6 +146,7 @@ int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, 
     if (rc != HSG_OK) return rc;
   } else {
     launch_tw_reset(d.stream, d.tw, prog);
+    tw_retention_reset(d);
     if (cfg.window_kind == HSG_UNWINDOWED) {
       // one implicit window: k = 0, epoch fixed at 0
       DevScalars init;
@@ -196,14 +197,7 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
   } else {
     d.tw.stride = tw_row_stride(prog.n_slots);
     DTRY(dalloc(&d.tw.rows, d.cap * (uint64_t)d.tw.stride));
-    d.tw.mask = d.cap - 1;
-    d.tw.blocked = cfg.window_kind != HSG_UNWINDOWED && d.cap >= 64 ? 1u : 0u;
-    // regions of >= 4096 slots (small spread of the per-region load), at
-    // most one per partition bucket
-    int cl = 0;
-    while ((1ull << cl) < d.cap) ++cl;
-    d.tw.rbits = cl - 12 < 0 ? 0 : (cl - 12 > kPartMaxLog2 ? kPartMaxLog2 : cl - 12);
-    d.tw.rmask = (d.cap >> d.tw.rbits) - 1;
+    tw_configure(d.tw, d.cap, cfg.window_kind);
     d.tw.bshift = 0;  // set with the exchange (exchange_device_init)
     uint64_t nb = emit_chunks(d.cap);
     DTRY(dalloc(&d.emit.cnt, nb));
@@ -408,7 +402,7 @@ int finish_batch(OpDevice &d, int64_t wm_in, uint64_t n, PushResult &r, std::str
   r.late = s.late;
   r.out_rows = s.out_rows;
   r.touched = s.touched;
-  r.state_rows = s.live;
+  r.state_rows = s.live + d.spilled_rows;
   return status_from_err(s.err, err);
 }
 
@@ -491,6 +485,12 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
 int op_push(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, PushResult &r,
             std::string &err) {
   const hsg_batch *b = a.batch;
+  // room in the table for the batch's worst case (sharded ops: in push_local,
+  // once the records this rank owns are known)
+  if (!a.comm) {
+    int rc = tw_maintain(d, cfg, prog, b->n, a.wm_in, a.pending, err);
+    if (rc != HSG_OK) return rc;
+  }
   // the changelog must have room for the worst case of this batch
   if (cfg.emit_mode != HSG_EMIT_NONE) {
     uint64_t bound = b->n * (uint64_t)a.nranks * d.wpr;
@@ -515,31 +515,39 @@ int op_push(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const Pu
 int push_local(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, const Batch &kb,
                const int64_t *seq, const int64_t *rec_wm, PushResult &r, std::string &err) {
   if (cfg.window_kind == HSG_SESSION) return push_session(d, cfg, prog, a, kb, seq, r, err);
+  if (a.comm) {
+    int rc = tw_maintain(d, cfg, prog, kb.n, a.wm_in, a.pending, err);
+    if (rc != HSG_OK) return rc;
+  }
   if (cfg.emit_mode == HSG_EMIT_PER_RECORD) return push_time_perrecord(d, cfg, prog, a, kb, seq, rec_wm, r, err);
   return push_time_atomic(d, cfg, prog, a, kb, seq, rec_wm, r, err);
 }
 
 int op_copy_rows(OpDevice &d, const OutCols &src, uint64_t from, uint64_t n, int n_aggs, const hsg_rows *out,
-                 std::string &err) {
+                 std::string &err, uint64_t dst_off) {
   if (n == 0) return HSG_OK;
+  const uint64_t o = dst_off;
+  uint32_t *key = out->key_id ? (uint32_t *)out->key_id + o : nullptr;
+  int64_t *ws = out->win_start ? out->win_start + o : nullptr;
+  int64_t *we = out->win_end ? out->win_end + o : nullptr;
+  int64_t *si = out->src_index ? out->src_index + o : nullptr;
+  RowPtrs ap;
+  memset(&ap, 0, sizeof(ap));
+  for (int j = 0; j < n_aggs && out->aggs; ++j) ap.p[j] = out->aggs[j] ? (int64_t *)out->aggs[j] + o : nullptr;
   if (out->mem == HSG_MEM_DEVICE) {
     // device-resident destination: every column in one launch
-    RowPtrs ap;
-    memset(&ap, 0, sizeof(ap));
-    for (int j = 0; j < n_aggs && out->aggs; ++j) ap.p[j] = (int64_t *)out->aggs[j];
-    launch_copy_rows(d.stream, src, from, n, n_aggs, (uint32_t *)out->key_id, out->win_start, out->win_end,
-                     out->src_index, ap);
+    launch_copy_rows(d.stream, src, from, n, n_aggs, key, ws, we, si, ap);
     DTRY(hipGetLastError());
     DTRY(hipStreamSynchronize(d.stream));
     return HSG_OK;
   }
   hipMemcpyKind k = hipMemcpyDeviceToHost;
-  if (out->key_id) DTRY(hipMemcpyAsync(out->key_id, src.key + from, n * 4, k, d.stream));
-  if (out->win_start) DTRY(hipMemcpyAsync(out->win_start, src.ws + from, n * 8, k, d.stream));
-  if (out->win_end) DTRY(hipMemcpyAsync(out->win_end, src.we + from, n * 8, k, d.stream));
-  if (out->src_index) DTRY(hipMemcpyAsync(out->src_index, src.src + from, n * 8, k, d.stream));
+  if (key) DTRY(hipMemcpyAsync(key, src.key + from, n * 4, k, d.stream));
+  if (ws) DTRY(hipMemcpyAsync(ws, src.ws + from, n * 8, k, d.stream));
+  if (we) DTRY(hipMemcpyAsync(we, src.we + from, n * 8, k, d.stream));
+  if (si) DTRY(hipMemcpyAsync(si, src.src + from, n * 8, k, d.stream));
   for (int j = 0; j < n_aggs; ++j)
-    if (out->aggs && out->aggs[j]) DTRY(hipMemcpyAsync(out->aggs[j], src.agg[j] + from, n * 8, k, d.stream));
+    if (ap.p[j]) DTRY(hipMemcpyAsync(ap.p[j], src.agg[j] + from, n * 8, k, d.stream));
   DTRY(hipStreamSynchronize(d.stream));
   return HSG_OK;
 }
@@ -550,7 +558,7 @@ int op_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hs
   if (rc != HSG_OK) return rc;
   uint64_t live = d.h_sc->live;
   *n_out = 0;
-  if (live == 0) return HSG_OK;
+  if (live == 0) return tw_dump_spilled(d, cfg, prog, out, 0, n_out, err);
   OutCols tmp;
   memset(&tmp, 0, sizeof(tmp));
   rc = alloc_out(tmp, live, cfg.n_aggs, err);
@@ -583,6 +591,12 @@ int op_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hs
     *n_out = got;
   }
   free_out(tmp);
+  if (rc == HSG_OK && cfg.window_kind != HSG_SESSION) {
+    // closed windows kept on the host (retention.cpp) follow the resident rows
+    uint64_t more = 0;
+    rc = tw_dump_spilled(d, cfg, prog, out, *n_out, &more, err);
+    *n_out += more;
+  }
   return rc;
 }
 

@@ -188,6 +188,7 @@ static int ensure_keys(OpDevice &d, uint64_t incoming, std::string &err) {
   d.ss.kt = to.kt;
   d.ss.kmask = to.kmask;
   d.cap = ncap;
+  d.grow_events += 1;
   return HSG_OK;
 }
 
@@ -273,11 +274,15 @@ static int push_session_merge(OpDevice &d, const hsg_op_config &cfg, const Progr
   launch_part_offsets(d.stream, pp, d.part, d.sc);
   launch_ss_pscatter(d.stream, kb, nl, d.bshift, tiles, words, has_valid, pt);
   launch_ss_sort(d.stream, sp, d.ss, prog, nl, d.bshift, words, pt, d.sc);
+  // the key groups k_ss_sort found size the apply grid
+  DTRY(hipMemcpyAsync(d.h_meta + M_GRP, d.ss.meta + M_GRP, sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
+  DTRY(hipStreamSynchronize(d.stream));
+  const uint64_t ngrp = d.h_meta[M_GRP];
   // a pass stops short (M_FAIL) only where the arena could not take a key's
   // fresh list: those apply blocks / big-bucket chunks were left untouched;
   // compact / grow the arena, then run the pass again (done work is skipped)
   for (int attempt = 0;; ++attempt) {
-    launch_ss_apply(d.stream, sp, d.ss, prog, n, words, pt, d.out, a.pending, d.sc);
+    launch_ss_apply(d.stream, sp, d.ss, prog, ngrp, words, pt, d.out, a.pending, d.sc);
     launch_ss_merge_big(d.stream, sp, d.ss, prog, nl, d.bshift, words, pt, d.sc);
     DTRY(hipMemcpyAsync(d.h_meta, d.ss.meta, M_WORDS * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
     DTRY(hipStreamSynchronize(d.stream));

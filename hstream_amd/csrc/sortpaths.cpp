@@ -81,7 +81,7 @@ int perrecord_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &
   d.scratch_bytes = probe.used;
   Carve real{(char *)d.scratch};
   carve_layout(real, d.pr, n, P, shadow);
-  DTRY(hipHostMalloc((void **)&d.h_tmp, 8 * sizeof(uint64_t), hipHostMallocDefault));
+  if (!d.h_tmp) DTRY(hipHostMalloc((void **)&d.h_tmp, 8 * sizeof(uint64_t), hipHostMallocDefault));
   return HSG_OK;
 }
 

@@ -186,8 +186,12 @@ typedef struct {
   uint64_t state_slots;       /* 8-byte aggregate words per state row (the op's program) */
   uint64_t state_row_bytes;   /* algorithmic state row: group key 8 B + 8 B per slot
                                  (sessions: start + end + slots)                        */
-  uint64_t spilled_rows;      /* rows evicted from HBM into the host spill store          */
-  uint64_t spill_events;      /* retention passes that moved rows to the host            */
+  uint64_t spilled_rows;      /* closed windows kept in host memory (counted in state_rows;
+                                 hsg_dump_state returns them after the HBM rows)        */
+  uint64_t spill_events;      /* retention passes that moved closed windows to the host */
+  uint64_t table_slots;       /* HBM hash-table slots (time windows) / key-table slots
+                                 (sessions) now                                          */
+  uint64_t grow_events;       /* times the HBM table was rebuilt larger                   */
 } hsg_stats;
 
 /* Completion callback of hsg_push_batch_async: rc is what hsg_push_batch

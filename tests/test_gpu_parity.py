@@ -196,13 +196,19 @@ def test_registered_changelog_zero_copy(eng):
     rows_equal(g.drain(), o.drain(), f64, what="own buffer again")
 
 
-def test_state_table_full_raises(eng):
+def test_state_table_grows_instead_of_failing(eng):
+    """A batch with more groups than the state capacity: the table is rebuilt
+    larger before the batch runs (retention.cpp), no HSG_E_OOM, exact counts."""
     spec = OpSpec(abi.HSG_UNWINDOWED, abi.HSG_EMIT_NONE, aggs=[(abi.HSG_COUNT_ALL, 0)], state_capacity=16)
     g = eng.op(spec)
     key = np.arange(1000, dtype=np.uint32)
-    with pytest.raises(abi.HStreamGpuError) as ei:
-        g.push(key, np.zeros(1000, np.int64), [], None)
-    assert ei.value.status == abi.HSG_E_OOM
+    g.push(np.concatenate([key, key[:10]]), np.zeros(1010, np.int64), [], None)
+    st = g.stats()
+    assert st["state_rows"] == 1000 and st["grow_events"] >= 1
+    d = g.dump_state()
+    cnt = dict(zip(d.key_id.tolist(), d.aggs[0].tolist()))
+    assert cnt == {k: (2 if k < 10 else 1) for k in range(1000)}
+    g.close()
 
 
 def test_changelog_must_be_drained(eng):
