@@ -165,6 +165,37 @@ EXPORTED_SYMBOLS = [
 ]
 
 
+# Every symbol include/hstream_ingest.h declares (host ingest, no GPU needed).
+INGEST_SYMBOLS = [
+    "hsg_keydict_create",
+    "hsg_keydict_destroy",
+    "hsg_keydict_size",
+    "hsg_keydict_encode",
+    "hsg_keydict_text",
+    "hsg_decoder_create",
+    "hsg_decoder_destroy",
+    "hsg_decode_json",
+]
+
+# hsg_decode_status
+HSG_DEC_OK = 0
+HSG_DEC_NOT_OBJECT = 1
+HSG_DEC_NO_KEY = 2
+HSG_DEC_TYPE = 3
+HSG_DEC_NOT_INTEGRAL = 4
+HSG_DEC_RANGE = 5
+
+
+class hsg_decoder_config(C.Structure):
+    _fields_ = [
+        ("key_field", C.c_char_p),
+        ("n_cols", C.c_int32),
+        ("col_fields", C.POINTER(C.c_char_p)),
+        ("col_types", C.POINTER(C.c_int32)),
+        ("col_numeric", C.POINTER(C.c_uint8)),
+    ]
+
+
 # void (*hsg_done_fn)(void *ctx, int rc)
 HSG_DONE_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int)
 

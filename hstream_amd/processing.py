@@ -277,6 +277,11 @@ class Table:
                 fields.append((a.field, a.is_float))
         self.fields = fields
         col_of = {fk: i for i, fk in enumerate(fields)}
+        # a column read only by COUNT(col) counts any present value (Codegen.hs:412-422);
+        # SUM / MIN / MAX / AVG / LAST need a Number (Codegen.hs:423-461)
+        self.numeric = [any(a.kind not in (abi.HSG_COUNT_ALL, abi.HSG_COUNT) and (a.field, a.is_float) == fk
+                            for a in self.aggs) for fk in fields]
+        self._decoder = None
         spec.col_types = [abi.HSG_F64 if fl else abi.HSG_I64 for _, fl in fields]
         spec.aggs = [(a.kind, col_of[(a.field, a.is_float)] if a.kind != abi.HSG_COUNT_ALL else 0) for a in self.aggs]
         spec.state_capacity = materialized.state_capacity
@@ -302,6 +307,8 @@ class Table:
                     valid[c][i] = 0  # HM.lookup ... Nothing -> the component leaves the acc alone
                     continue
                 v = value[f]
+                if not self.numeric[c]:
+                    continue  # COUNT(col): present is enough, whatever the value
                 if isinstance(v, bool) or not isinstance(v, (int, float, np.integer, np.floating)):
                     ok = False  # "Only columns with Int or Number type ..." aborts the record
                     break
@@ -319,6 +326,22 @@ class Table:
             else:
                 out.append((key, vals))
         return out
+
+    def process_json(self, buf: bytes, off, ts, watermark=-1, threads=0):
+        """One poll batch of raw JSON record values (SourceRecord srcValue) and
+        their timestamps, decoded by the native ingest (include/hstream_ingest.h)
+        straight into the op's columns; needs Materialized(keys=ingest.KeyDict())."""
+        from . import ingest
+        if not isinstance(self.mat.keys, ingest.KeyDict):
+            raise TypeError("process_json needs Materialized(keys=hstream_amd.ingest.KeyDict())")
+        if self._decoder is None:
+            self._decoder = ingest.Decoder(self.grouped.key_field,
+                                           [(f, abi.HSG_F64 if fl else abi.HSG_I64, num)
+                                            for (f, fl), num in zip(self.fields, self.numeric)])
+        keys, ts_out, cols, valid, _, _ = self._decoder.decode(self.mat.keys, buf, off, ts, threads)
+        wm = self.op.push(keys, ts_out, cols, valid, watermark=watermark)
+        rows = self.op.drain() if self.spec.emit_mode != abi.HSG_EMIT_NONE else None
+        return wm, ([] if rows is None else self._rows(rows))
 
     def process(self, records, watermark=-1):
         keys, ts, cols, valid = self.columns(records)

@@ -1,0 +1,93 @@
+/* libhstream_gpu — host ingest: poll batches of JSON records into the columnar
+ * hsg_batch of hstream_gpu.h, with the group key dictionary-encoded.
+ *
+ * Replaces, for the windowed GROUP BY path, the per-record work the reference
+ * does between the poll and the aggregate:
+ *   - value decode of every SourceRecord (buildSourceProcessor,
+ *     hstream-processing/src/HStream/Processing/Processor.hs:192-204: Aeson
+ *     decode to an Object),
+ *   - the GROUP BY key (hstream-sql/src/HStream/SQL/Codegen.hs:485-487:
+ *     HM.singleton col (getFieldByName value col)), whose identity in the
+ *     store is Aeson Value equality (Data.Scientific for numbers, so 1, 1.0,
+ *     10e-1 and 1E0 are one key; objects compare as maps),
+ *   - the field reads of the aggregate components (Codegen.hs:412-461:
+ *     HM.lookup of the column, absent = the accumulator is left alone, a
+ *     non-Number under SUM/MIN/MAX throws and the record is dropped by
+ *     runTask's catch, Processor.hs:140-143).
+ * A record that the reference would drop (undecodable value, missing GROUP BY
+ * field, wrong-typed aggregated field) gets key_id = HSG_KEY_NONE: it still
+ * moves stream time (Processor.hs:139), exactly as there.
+ *
+ * Where the GPU's fixed-width columns cannot hold what Scientific holds, the
+ * record is rejected with its own status instead of being rounded: a
+ * non-integral number, or one outside int64, in an HSG_I64 column (declare
+ * the column HSG_F64 for decimal data).
+ *
+ * Thread safety: one decoder / dictionary per operator; calls on one object
+ * are serialized by the caller (the operator's runTask loop), distinct objects
+ * are independent. Decoding itself fans out over n_threads host threads.
+ */
+#ifndef HSTREAM_INGEST_H
+#define HSTREAM_INGEST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* per-record decode status (status[] of hsg_decode_json) */
+enum hsg_decode_status {
+  HSG_DEC_OK = 0,
+  HSG_DEC_NOT_OBJECT = 1,   /* value is not a JSON object / malformed JSON        */
+  HSG_DEC_NO_KEY = 2,       /* GROUP BY field absent (getFieldByName throws)       */
+  HSG_DEC_TYPE = 3,         /* aggregated field present but not a Number           */
+  HSG_DEC_NOT_INTEGRAL = 4, /* non-integral Number in an HSG_I64 column            */
+  HSG_DEC_RANGE = 5         /* integral Number outside int64 in an HSG_I64 column   */
+};
+
+/* ---- key dictionary: Aeson Value -> dense u32 id (first-seen order) ------- */
+typedef struct hsg_keydict hsg_keydict;
+int  hsg_keydict_create(hsg_keydict **out);
+void hsg_keydict_destroy(hsg_keydict *d);
+uint64_t hsg_keydict_size(const hsg_keydict *d);
+/* Id of one JSON value (text), inserting it if new. HSG_E_INVALID for
+ * malformed JSON, HSG_E_CAPACITY when 2^32 - 1 keys exist. */
+int  hsg_keydict_encode(hsg_keydict *d, const char *json, size_t len, uint32_t *id);
+/* The key's JSON text as Aeson's encode prints the value (numbers in
+ * Scientific's shortest form: 1.0 -> 1, 0.001 -> 1.0e-3; object members in
+ * sorted order). *len = bytes needed; HSG_E_CAPACITY (nothing copied) when
+ * cap is smaller, HSG_E_INVALID for an unknown id. */
+int  hsg_keydict_text(const hsg_keydict *d, uint32_t id, char *buf, size_t cap, size_t *len);
+
+/* ---- record decoder --------------------------------------------------------- */
+typedef struct {
+  const char *key_field;          /* GROUP BY column name (composeColName stream field) */
+  int32_t n_cols;                 /* aggregated fields, in hsg_batch column order       */
+  const char *const *col_fields;
+  const int32_t *col_types;       /* hsg_col_type                                       */
+  const uint8_t *col_numeric;     /* 1: must be a Number (SUM/MIN/MAX/AVG/LAST);
+                                     0: presence only (COUNT(col): any value, null too) */
+} hsg_decoder_config;
+
+typedef struct hsg_decoder hsg_decoder;
+int  hsg_decoder_create(const hsg_decoder_config *cfg, hsg_decoder **out);
+void hsg_decoder_destroy(hsg_decoder *d);
+
+/* Decode n records into caller-owned host columns (an hsg_batch's arrays):
+ * record i is buf[off[i], off[i+1]) (off has n + 1 entries), its timestamp
+ * rec_ts[i] (SourceRecord srcTimestamp) is copied to ts[i]; key_id[i] from
+ * the dictionary (ids handed out in record order); cols[c][i] int64 or double;
+ * valid[c][i] = 1 when the field is present. status (optional) receives
+ * hsg_decode_status per record, *rejected (optional) the records passed as
+ * HSG_KEY_NONE. n_threads <= 0: one per hardware thread (at most 32). */
+int  hsg_decode_json(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, const char *buf, const uint64_t *off,
+                     const int64_t *rec_ts, uint32_t *key_id, int64_t *ts, void *const *cols,
+                     uint8_t *const *valid, uint8_t *status, uint64_t *rejected, int n_threads);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HSTREAM_INGEST_H */

@@ -3,6 +3,7 @@
 #include <stddef.h>
 #include <stdio.h>
 #include "../include/hstream_gpu.h"
+#include "../include/hstream_ingest.h"
 #define F(T, m) printf("%s.%s %zu\n", #T, #m, offsetof(T, m))
 #define S(T) printf("%s %zu\n", #T, sizeof(T))
 int main(void) {
@@ -13,5 +14,6 @@ int main(void) {
   S(hsg_batch); F(hsg_batch, key_id); F(hsg_batch, ts); F(hsg_batch, cols); F(hsg_batch, valid); F(hsg_batch, ready_event);
   S(hsg_rows); F(hsg_rows, key_id); F(hsg_rows, win_start); F(hsg_rows, src_index); F(hsg_rows, aggs);
   S(hsg_stats); F(hsg_stats, last_batch_ms); F(hsg_stats, exchange_bytes); F(hsg_stats, touched_total); F(hsg_stats, state_row_bytes); F(hsg_stats, spill_events); F(hsg_stats, grow_events);
+  S(hsg_decoder_config); F(hsg_decoder_config, n_cols); F(hsg_decoder_config, col_fields); F(hsg_decoder_config, col_numeric);
   return 0;
 }

@@ -11,12 +11,12 @@ import pytest
 from hstream_amd import abi, engine
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "hstream_gpu.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("hstream_gpu.h", "hstream_ingest.h")]
 
 
 def _header_functions():
-    src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*\*?\s*(hsg_\w+)\s*\(", src, re.M)))
+    src = "".join(open(h).read() for h in HEADERS)
+    return sorted(set(re.findall(r"^\s*(?:int|void|uint64_t|const char \*)\s*\*?\s*(hsg_\w+)\s*\(", src, re.M)))
 
 
 @pytest.fixture(scope="module")
@@ -28,7 +28,7 @@ def lib():
 
 
 def test_header_lists_every_abi_function():
-    assert _header_functions() == sorted(abi.EXPORTED_SYMBOLS)
+    assert _header_functions() == sorted(abi.EXPORTED_SYMBOLS + abi.INGEST_SYMBOLS)
 
 
 def test_library_exports_every_declared_symbol(lib):
@@ -56,7 +56,8 @@ def test_ctypes_layout_matches_c():
             k, v = ln.split()
             want[k] = int(v)
     types = {"hsg_engine_config": abi.hsg_engine_config, "hsg_agg": abi.hsg_agg, "hsg_op_config": abi.hsg_op_config,
-             "hsg_batch": abi.hsg_batch, "hsg_rows": abi.hsg_rows, "hsg_stats": abi.hsg_stats}
+             "hsg_batch": abi.hsg_batch, "hsg_rows": abi.hsg_rows, "hsg_stats": abi.hsg_stats,
+             "hsg_decoder_config": abi.hsg_decoder_config}
     for k, v in want.items():
         if "." in k:
             t, m = k.split(".")

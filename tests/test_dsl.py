@@ -117,3 +117,46 @@ def test_type_error_record_only_moves_stream_time(eng):
     assert wm == 900_000_000
     # the third record's window [0, 1000) is > 24 h behind stream time: skipped
     assert [v["SUM(v)"] for _, v in rows] == [2]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("window", ["tumbling", "session"])
+def test_json_poll_batch_through_native_ingest(eng, window):
+    """A poll batch of raw JSON values (SourceRecord srcValue) decoded by the
+    native ingest straight into the op: the changelog equals the same
+    records run through the Python columnariser into the oracle; the keys
+    come back as the values the records spelled (1 and 1.0 are one key)."""
+    import json
+    from hstream_amd import ingest
+    rng = np.random.default_rng(17)
+    vals, recs = [], []
+    for i in range(3000):
+        k = [1, 1.0, "a", "b", 7, {"x": 1}][int(rng.integers(0, 6))]
+        v = {"k": k, "v": int(rng.integers(-1000, 1000)), "pad": "z" * int(rng.integers(0, 20))}
+        if rng.random() < 0.05:
+            v["v"] = "oops"           # SUM over a string: the record only moves stream time
+        if rng.random() < 0.05:
+            del v["k"]                # no GROUP BY field
+        ts = 10_000 + 37 * i + int(rng.integers(0, 500))
+        vals.append(json.dumps(v).encode())
+        recs.append(_rec(ts, **v))
+    ts = np.array([r["timestamp"] for r in recs], np.int64)
+    buf, off = ingest.pack_records(vals)
+
+    def table(keys):
+        g = P.groupBy(eng, "k")
+        w = g.timeWindowedBy(P.mkTumblingWindow(2000)) if window == "tumbling" else \
+            g.sessionWindowedBy(P.mkSessionWindows(300))
+        return w.aggregate([P.COUNT_ALL("n"), P.SUM("v", "s"), P.MAX("v", "m")], P.Materialized(keys=keys))
+
+    tn = table(ingest.KeyDict())
+    wm_n, rows_n = tn.process_json(buf, off, ts, threads=4)
+    tp = table(P.KeyDict())
+    wm_p, rows_p = tp.process(recs)
+    assert wm_n == wm_p == int(ts.max())
+    assert len(rows_n) == len(rows_p)
+    for (kn, vn), (kp, vp) in zip(rows_n, rows_p):
+        assert kn.twkWindow == kp.twkWindow and vn == vp
+        assert P._canon(kn.twkKey) == P._canon(kp.twkKey)
+    tn.close()
+    tp.close()
