@@ -115,9 +115,9 @@ def test_device_dump_with_spilled_rows(eng):
     rows at the right offsets."""
     import ctypes as C
     import torch
-    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_NONE, size_ms=1000, grace_ms=0, col_types=[abi.HSG_I64],
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_NONE, size_ms=1000, grace_ms=3000, col_types=[abi.HSG_I64],
                   aggs=[(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0)], state_capacity=512)
-    bs = _stream(51, 6, 20_000, 300, 20_000)
+    bs = _stream(51, 10, 20_000, 300, 20_000)
     g = eng.op(spec)
     o = pyoracle.OracleOp(spec)
     wg = wo = -1
