@@ -196,6 +196,34 @@ class hsg_decoder_config(C.Structure):
     ]
 
 
+class hsg_sink_config(C.Structure):
+    _fields_ = [
+        ("windowed", C.c_int32),
+        ("n_members", C.c_int32),
+        ("key_field", C.c_char_p),
+        ("aliases", C.POINTER(C.c_char_p)),
+        ("agg_index", C.POINTER(C.c_int32)),
+    ]
+
+
+class hsg_sink_records(C.Structure):
+    _fields_ = [
+        ("mem", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("key_capacity", C.c_uint64),
+        ("value_capacity", C.c_uint64),
+        ("key_bytes", C.c_void_p),
+        ("key_off", C.c_void_p),
+        ("value_bytes", C.c_void_p),
+        ("value_off", C.c_void_p),
+    ]
+
+
+
+# Every symbol include/hstream_sink.h declares.
+SINK_SYMBOLS = ["hsg_sink_create", "hsg_sink_destroy", "hsg_sink_encode", "hsg_format_number"]
+
+
 # void (*hsg_done_fn)(void *ctx, int rc)
 HSG_DONE_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int)
 

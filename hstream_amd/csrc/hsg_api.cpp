@@ -583,3 +583,18 @@ extern "C" int hsg_op_stats(const hsg_op *op, hsg_stats *out) {
   *out = op->stats;
   return HSG_OK;
 }
+
+namespace hsg {
+// For the sink encoder (sink.cpp): the op's device and which changelog
+// aggregate columns hold f64 bits.
+int op_sink_info(const hsg_op *op, int *device, int *n_aggs, uint32_t *f64_mask) {
+  if (!op) return HSG_E_INVALID;
+  *device = op->eng->device;
+  *n_aggs = op->prog.n_out;
+  uint32_t m = 0;
+  for (int j = 0; j < op->prog.n_out; ++j)
+    if (op->prog.out_kind[j] != O_I64) m |= 1u << j;
+  *f64_mask = m;
+  return HSG_OK;
+}
+}  // namespace hsg

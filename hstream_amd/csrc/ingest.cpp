@@ -932,3 +932,12 @@ extern "C" int hsg_decode_json(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, 
     return HSG_E_INVALID;
   }
 }
+
+namespace hsg {
+// For the sink encoder (sink.cpp): the key texts, id after id.
+void keydict_texts(const hsg_keydict *d, const char **text, const uint64_t **off, uint64_t *n) {
+  *text = d->text.data();
+  *off = d->toff.data();
+  *n = d->size();
+}
+}  // namespace hsg

@@ -4,6 +4,7 @@
 #include <stdio.h>
 #include "../include/hstream_gpu.h"
 #include "../include/hstream_ingest.h"
+#include "../include/hstream_sink.h"
 #define F(T, m) printf("%s.%s %zu\n", #T, #m, offsetof(T, m))
 #define S(T) printf("%s %zu\n", #T, sizeof(T))
 int main(void) {
@@ -15,5 +16,7 @@ int main(void) {
   S(hsg_rows); F(hsg_rows, key_id); F(hsg_rows, win_start); F(hsg_rows, src_index); F(hsg_rows, aggs);
   S(hsg_stats); F(hsg_stats, last_batch_ms); F(hsg_stats, exchange_bytes); F(hsg_stats, touched_total); F(hsg_stats, state_row_bytes); F(hsg_stats, spill_events); F(hsg_stats, grow_events);
   S(hsg_decoder_config); F(hsg_decoder_config, n_cols); F(hsg_decoder_config, col_fields); F(hsg_decoder_config, col_numeric);
+  S(hsg_sink_config); F(hsg_sink_config, key_field); F(hsg_sink_config, agg_index);
+  S(hsg_sink_records); F(hsg_sink_records, key_capacity); F(hsg_sink_records, key_bytes); F(hsg_sink_records, value_off);
   return 0;
 }
