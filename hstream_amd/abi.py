@@ -224,6 +224,40 @@ class hsg_sink_records(C.Structure):
 SINK_SYMBOLS = ["hsg_sink_create", "hsg_sink_destroy", "hsg_sink_encode", "hsg_format_number"]
 
 
+class hsg_join_config(C.Structure):
+    _fields_ = [("before_ms", C.c_int64), ("after_ms", C.c_int64), ("batch_capacity", C.c_uint64)]
+
+
+class hsg_join_batch(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint64),
+        ("mem", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("side", C.c_void_p),
+        ("key_id", C.c_void_p),
+        ("join_key", C.c_void_p),
+        ("ts", C.c_void_p),
+        ("handle", C.c_void_p),
+    ]
+
+
+class hsg_join_rows(C.Structure):
+    _fields_ = [
+        ("capacity", C.c_uint64),
+        ("mem", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("this_handle", C.c_void_p),
+        ("other_handle", C.c_void_p),
+        ("join_key", C.c_void_p),
+        ("ts", C.c_void_p),
+    ]
+
+
+# Every symbol include/hstream_join.h declares.
+JOIN_SYMBOLS = ["hsg_join_create", "hsg_join_destroy", "hsg_join_last_error", "hsg_join_push", "hsg_join_pending",
+                "hsg_join_drain", "hsg_join_state_rows"]
+
+
 # void (*hsg_done_fn)(void *ctx, int rc)
 HSG_DONE_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int)
 

@@ -598,3 +598,8 @@ int op_sink_info(const hsg_op *op, int *device, int *n_aggs, uint32_t *f64_mask)
   return HSG_OK;
 }
 }  // namespace hsg
+
+namespace hsg {
+// For the join (join.cpp): the engine's device.
+int engine_device(const hsg_engine *e) { return e ? e->device : 0; }
+}  // namespace hsg

@@ -5,6 +5,7 @@
 #include "../include/hstream_gpu.h"
 #include "../include/hstream_ingest.h"
 #include "../include/hstream_sink.h"
+#include "../include/hstream_join.h"
 #define F(T, m) printf("%s.%s %zu\n", #T, #m, offsetof(T, m))
 #define S(T) printf("%s %zu\n", #T, sizeof(T))
 int main(void) {
@@ -18,5 +19,8 @@ int main(void) {
   S(hsg_decoder_config); F(hsg_decoder_config, n_cols); F(hsg_decoder_config, col_fields); F(hsg_decoder_config, col_numeric);
   S(hsg_sink_config); F(hsg_sink_config, key_field); F(hsg_sink_config, agg_index);
   S(hsg_sink_records); F(hsg_sink_records, key_capacity); F(hsg_sink_records, key_bytes); F(hsg_sink_records, value_off);
+  S(hsg_join_config); F(hsg_join_config, batch_capacity);
+  S(hsg_join_batch); F(hsg_join_batch, side); F(hsg_join_batch, handle);
+  S(hsg_join_rows); F(hsg_join_rows, this_handle); F(hsg_join_rows, ts);
   return 0;
 }

@@ -11,7 +11,7 @@ import pytest
 from hstream_amd import abi, engine
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("hstream_gpu.h", "hstream_ingest.h", "hstream_sink.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("hstream_gpu.h", "hstream_ingest.h", "hstream_sink.h", "hstream_join.h")]
 
 
 def _header_functions():
@@ -28,7 +28,7 @@ def lib():
 
 
 def test_header_lists_every_abi_function():
-    assert _header_functions() == sorted(abi.EXPORTED_SYMBOLS + abi.INGEST_SYMBOLS + abi.SINK_SYMBOLS)
+    assert _header_functions() == sorted(abi.EXPORTED_SYMBOLS + abi.INGEST_SYMBOLS + abi.SINK_SYMBOLS + abi.JOIN_SYMBOLS)
 
 
 def test_library_exports_every_declared_symbol(lib):
@@ -58,7 +58,9 @@ def test_ctypes_layout_matches_c():
     types = {"hsg_engine_config": abi.hsg_engine_config, "hsg_agg": abi.hsg_agg, "hsg_op_config": abi.hsg_op_config,
              "hsg_batch": abi.hsg_batch, "hsg_rows": abi.hsg_rows, "hsg_stats": abi.hsg_stats,
              "hsg_decoder_config": abi.hsg_decoder_config,
-             "hsg_sink_config": abi.hsg_sink_config, "hsg_sink_records": abi.hsg_sink_records}
+             "hsg_sink_config": abi.hsg_sink_config, "hsg_sink_records": abi.hsg_sink_records,
+             "hsg_join_config": abi.hsg_join_config, "hsg_join_batch": abi.hsg_join_batch,
+             "hsg_join_rows": abi.hsg_join_rows}
     for k, v in want.items():
         if "." in k:
             t, m = k.split(".")
