@@ -121,16 +121,27 @@ __device__ inline void lds_apply(const PG &prog, int64_t *__restrict__ row, cons
     const int64_t x = prec_elem(prog, s, r);
     int64_t *a = row + s * ST;
     unsigned long long *u = (unsigned long long *)a;
+    // min / max: a plain read first; the atomic only when x would change the
+    // value (a stale read costs an atomic that changes nothing, never a wrong
+    // result), so a group's later records mostly skip the LDS atomic unit
     switch (op) {
       case S_CNT_ALL:
       case S_CNT:
       case S_SUM_I: atomicAdd(u, (unsigned long long)x); break;
       case S_SUM_F: unsafeAtomicAdd((double *)a, __builtin_bit_cast(double, x)); break;
-      case S_MIN_I: atomicMin((long long *)a, (long long)x); break;
-      case S_MAX_I: atomicMax((long long *)a, (long long)x); break;
-      case S_MIN_F: atomicMin(u, (unsigned long long)x); break;
+      case S_MIN_I:
+        if (x < *(volatile int64_t *)a) atomicMin((long long *)a, (long long)x);
+        break;
+      case S_MAX_I:
+        if (x > *(volatile int64_t *)a) atomicMax((long long *)a, (long long)x);
+        break;
+      case S_MIN_F:
+        if ((uint64_t)x < *(volatile uint64_t *)a) atomicMin(u, (unsigned long long)x);
+        break;
       case S_MAX_F:
-      case S_LAST_SEQ: atomicMax(u, (unsigned long long)x); break;
+      case S_LAST_SEQ:
+        if ((uint64_t)x > *(volatile uint64_t *)a) atomicMax(u, (unsigned long long)x);
+        break;
       default: break;
     }
   }
@@ -265,6 +276,19 @@ __device__ inline int lds_insert(uint64_t *lkey, uint32_t *lfill, uint32_t limit
   return -1;
 }
 
+// slot of g in the LDS table, -1 when absent
+template <int E>
+__device__ inline int lds_find(const uint64_t *lkey, uint64_t g) {
+  uint32_t h = (uint32_t)(mix64(g) & (E - 1));
+  for (int probe = 0; probe < E; ++probe) {
+    const uint64_t cur = lkey[h];
+    if (cur == g) return (int)h;
+    if (cur == kEmpty) return -1;
+    h = (h + 1) & (E - 1);
+  }
+  return -1;
+}
+
 // sub-round of a key: the hash bits just below its bucket bits
 __device__ inline uint32_t key_round(uint32_t key, int np_log2, int rbits, int bshift) {
   if (!rbits) return 0;
@@ -287,18 +311,118 @@ __device__ inline uint32_t key_round(uint32_t key, int np_log2, int rbits, int b
 // the LDS table persists across them: it is flushed when full and at the end
 // of each of the 2^rbits key-hash rounds (host-sized from the previous batch so
 // that a round's panes fit), so a bucket's groups are normally flushed once.
+// Pane grouping at a flush: a counting sort of the live panes by key hash
+// (LDS counters per hash bucket) and an insertion sort of each bucket by
+// (key, pane) puts every key's panes next to each other in pane order, which
+// is all the window pass needs (the key order itself is irrelevant). Tables
+// whose counters do not fit next to the aggregates (8-slot programs) sort
+// the whole list (bitonic) instead, as do flushes with an oversized bucket.
+template <int MS, int E>
+struct PaneGroup {
+  static constexpr bool kCount = MS <= 6;
+  uint32_t cnt[kCount ? E : 1];     // per hash bucket: count, then end offset
+  uint16_t order[kCount ? E : 1];   // live entries grouped by key
+};
+
 template <int MS, int E, int NT>
 struct AggLds {
   uint64_t key[E];
   int64_t agg[E * MS];
   uint8_t nw[E];     // windows of the pane's records
   uint8_t run[E];    // owned windows - 1
-  uint16_t live[E];  // compacted / sorted live entries
-  uint32_t fill, nl, b, c0, c1;
+  uint16_t live[E];  // compacted / key-grouped live entries
+  uint32_t fill, nl, b, c0, c1, maxb;
   uint32_t wsum[NT / 64];
   uint64_t base;
   uint64_t red[2][NT / 64];
+  PaneGroup<MS, E> pg;
 };
+
+// Bitonic sort of the live list by (key, pane), padded to a power of two.
+template <int MS, int E, int NT>
+__device__ inline void sort_live_bitonic(AggLds<MS, E, NT> &L, uint32_t nl) {
+  uint32_t M = 1;
+  while (M < nl) M <<= 1;
+  for (uint32_t q = nl + threadIdx.x; q < M; q += NT) L.live[q] = 0xFFFFu;
+  __syncthreads();
+  for (uint32_t k = 2; k <= M; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < M; i += NT) {
+        const uint32_t ixj = i ^ j;
+        if (ixj <= i) continue;
+        const uint16_t x = L.live[i], y = L.live[ixj];
+        const uint64_t kx = x == 0xFFFFu ? kEmpty : L.key[x];
+        const uint64_t ky = y == 0xFFFFu ? kEmpty : L.key[y];
+        if ((kx > ky) == ((i & k) == 0)) {
+          L.live[i] = y;
+          L.live[ixj] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Group the live list by key, panes ascending within a key (see PaneGroup).
+template <int MS, int E, int NT>
+__device__ inline void group_live(AggLds<MS, E, NT> &L, uint32_t nl) {
+  if constexpr (!PaneGroup<MS, E>::kCount) {
+    sort_live_bitonic<MS, E, NT>(L, nl);
+  } else {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr uint32_t PER = E / NT;  // buckets per thread
+    for (uint32_t h = threadIdx.x; h < E; h += NT) L.pg.cnt[h] = 0;
+    if (threadIdx.x == 0) L.maxb = 0;
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < nl; q += NT) {
+      const uint32_t h = (uint32_t)(mix64(L.key[L.live[q]] >> 32) & (E - 1));
+      const uint32_t c = atomicAdd(&L.pg.cnt[h], 1u) + 1u;
+      atomicMax(&L.maxb, c);
+    }
+    __syncthreads();
+    if (L.maxb > 48) {  // a hot key: one long bucket would make the insertion sort quadratic
+      sort_live_bitonic<MS, E, NT>(L, nl);
+      return;
+    }
+    // exclusive scan of the bucket counts (PER consecutive buckets per thread)
+    uint32_t local = 0;
+    for (uint32_t k = 0; k < PER; ++k) local += L.pg.cnt[threadIdx.x * PER + k];
+    const uint64_t incl = wave_incl_sum((uint64_t)local);
+    if (lane == 63) L.wsum[wv] = (uint32_t)incl;
+    __syncthreads();
+    uint32_t run = (uint32_t)(incl - local);
+    for (int k = 0; k < wv; ++k) run += L.wsum[k];
+    for (uint32_t k = 0; k < PER; ++k) {
+      const uint32_t h = threadIdx.x * PER + k, c = L.pg.cnt[h];
+      L.pg.cnt[h] = run;  // start, advanced to the end by the scatter
+      run += c;
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < nl; q += NT) {
+      const uint16_t e = L.live[q];
+      const uint32_t h = (uint32_t)(mix64(L.key[e] >> 32) & (E - 1));
+      L.pg.order[atomicAdd(&L.pg.cnt[h], 1u)] = e;
+    }
+    __syncthreads();
+    // each bucket by (key, pane): a handful of entries, one thread per bucket
+    for (uint32_t h = threadIdx.x; h < E; h += NT) {
+      const uint32_t end = L.pg.cnt[h], start = h ? L.pg.cnt[h - 1] : 0u;
+      for (uint32_t i = start + 1; i < end; ++i) {
+        const uint16_t x = L.pg.order[i];
+        const uint64_t kx = L.key[x];
+        uint32_t j = i;
+        while (j > start && L.key[L.pg.order[j - 1]] > kx) {
+          L.pg.order[j] = L.pg.order[j - 1];
+          --j;
+        }
+        L.pg.order[j] = x;
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < nl; q += NT) L.live[q] = L.pg.order[q];
+    __syncthreads();
+  }
+}
 
 // Flush every live entry of the table as window updates, then clear it.
 // Block-wide: every thread calls. Returns the number of live entries.
@@ -321,30 +445,8 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const PG &pr
   }
   __syncthreads();
   const uint32_t nl = L.nl;
-  if (S > 1 && nl > 1) {
-    // panes of one key become neighbours: bitonic sort of the live list by
-    // (key, pane), padded to a power of two with +inf
-    uint32_t M = 1;
-    while (M < nl) M <<= 1;
-    for (uint32_t q = nl + threadIdx.x; q < M; q += NT) L.live[q] = 0xFFFFu;
-    __syncthreads();
-    for (uint32_t k = 2; k <= M; k <<= 1) {
-      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-        for (uint32_t i = threadIdx.x; i < M; i += NT) {
-          const uint32_t ixj = i ^ j;
-          if (ixj <= i) continue;
-          const uint16_t x = L.live[i], y = L.live[ixj];
-          const uint64_t kx = x == 0xFFFFu ? kEmpty : L.key[x];
-          const uint64_t ky = y == 0xFFFFu ? kEmpty : L.key[y];
-          if ((kx > ky) == ((i & k) == 0)) {
-            L.live[i] = y;
-            L.live[ixj] = x;
-          }
-        }
-        __syncthreads();
-      }
-    }
-  }
+  // pane mode: a key's panes become neighbours in pane order
+  if (S > 1 && nl > 1) group_live<MS, E, NT>(L, nl);
   t_sort += wall_clock64() - t0;
   // owned window run of every pane: [max(P - n + 1, previous pane + 1), P]
   uint32_t cnt = 0;
@@ -381,7 +483,7 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const PG &pr
     int64_t acc[MS];
 #pragma unroll
     for (int s = 0; s < MS; ++s) acc[s] = L.agg[s * E + e];
-    // later panes of the key (sorted after q) that window w covers: pane <= w + SW - 1
+    // later panes of the key (after q) that window w covers: pane <= w + SW - 1
     uint32_t j = q + 1;
     uint64_t top = (uint64_t)a + SW - 1;
     for (uint32_t w = a;; ++w) {
@@ -392,13 +494,16 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const PG &pr
         acc_combine<MS, E>(prog, acc, &L.agg[f]);
         ++j;
       }
+      int64_t v[MS];
+#pragma unroll
+      for (int s = 0; s < MS; ++s) v[s] = acc[s];
       if (skip) {
         // COUNT(col) slots not kept in LDS: every record of the batch has the column
 #pragma unroll
         for (int s = 0; s < MS; ++s)
-          if ((skip >> s) & 1u) acc[s] = acc[cnt_all_slot];
+          if ((skip >> s) & 1u) v[s] = v[cnt_all_slot];
       }
-      const uint32_t sl = flush_window<MS>(prog, p, t, kb | w, acc, exclusive, fresh, err, plain_claim);
+      const uint32_t sl = flush_window<MS>(prog, p, t, kb | w, v, exclusive, fresh, err, plain_claim);
       if (o < pb.touched_cap) pb.touched[o] = sl;
       else err |= ERR_OOM;
       ++o;

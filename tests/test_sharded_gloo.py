@@ -6,7 +6,12 @@ Protocol per global batch (rank r ingests slice r; slices are in rank order):
   all-gather (max ts, min keyed ts, n) -> global watermark, stream-time carry
   of rank r = max(wm_in, max ts of ranks < r), sequence base = sum of n of
   ranks < r, and whether any record may be late (stream time > min ts + grace);
-  owner = hash(key) mod G; all-to-all of (key, ts, cols, valid, seq[, wm]);
+  owner = the top log2(G) bits of key_hash(key) (power-of-two G, the bits the
+  local partition skips; hash mod G otherwise);
+  fast path (no LAST, no per-record changelog, no sessions, and no record can
+  be late): one all-to-all per column of (key, ts, col..., valid...) of the
+  keyed records with ts >= 0, aggregated in any order at stream time = carry;
+  classic path otherwise: all-to-all of (key, ts, cols, valid, seq[, wm]),
   each rank aggregates its owned records in global order.
 The per-rank aggregation here is the oracle, so this checks the protocol's
 claims (exact stream time and sequence numbers after the exchange, disjoint
@@ -38,7 +43,19 @@ def mix64(x):
     return x
 
 
+def key_hash(key):
+    """hsg_internal.h key_hash: mix64(key * golden + c)"""
+    with np.errstate(over="ignore"):
+        return mix64(np.asarray(key, np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(0x632BE59BD9B4E019))
+
+
 def owner_of(key, G):
+    """k_exchange.hip owner_of"""
+    lg = G.bit_length() - 1
+    if (1 << lg) == G:
+        if lg == 0:
+            return np.zeros(len(key), np.int64)
+        return (key_hash(key) >> np.uint64(64 - lg)).astype(np.int64)
     return (mix64(np.asarray(key, np.uint64) ^ np.uint64(0x5BD1E9955BD1E995)) % np.uint64(G)).astype(np.int64)
 
 
@@ -57,7 +74,27 @@ SPECS = {
                              col_types=[abi.HSG_I64, abi.HSG_F64], aggs=ALL_AGG_SETS["mixed"]),
     "session": OpSpec(abi.HSG_SESSION, abi.HSG_EMIT_PER_RECORD, gap_ms=2_000, col_types=[abi.HSG_I64, abi.HSG_F64],
                       aggs=ALL_AGG_SETS["mixed"]),
+    # no LAST: the fast exchange when no record can be late
+    "tumbling_fast": OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=10_000,
+                            col_types=[abi.HSG_I64, abi.HSG_F64],
+                            aggs=[a for a in ALL_AGG_SETS["mixed"] if a[0] != abi.HSG_LAST]),
+    "hopping_fast": OpSpec(abi.HSG_HOPPING, abi.HSG_EMIT_NONE, size_ms=9_000, advance_ms=3_000,
+                           col_types=[abi.HSG_I64, abi.HSG_F64],
+                           aggs=[a for a in ALL_AGG_SETS["mixed"] if a[0] != abi.HSG_LAST]),
+    # no LAST but a short grace: batches whose records may be late fall back to the classic exchange
+    "tumbling_fast_grace": OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=10_000, grace_ms=5_000,
+                                  col_types=[abi.HSG_I64, abi.HSG_F64],
+                                  aggs=[a for a in ALL_AGG_SETS["mixed"] if a[0] != abi.HSG_LAST]),
 }
+# the exchange each spec takes on these batches (very late records have ts < 0: never windowed)
+PATHS = {"hopping": "classic", "tumbling_batch": "classic", "session": "classic", "tumbling_fast": "fast",
+         "hopping_fast": "fast", "tumbling_fast_grace": "classic"}
+
+
+def fast_eligible(spec):
+    """exchange.cpp push_sharded: no LAST, per-record changelog or sessions"""
+    return (spec.emit_mode != abi.HSG_EMIT_PER_RECORD and spec.window_kind != abi.HSG_SESSION
+            and all(k != abi.HSG_LAST for k, _ in spec.aggs))
 
 
 def _batches(G, late):
@@ -81,6 +118,7 @@ def _worker(rank, G, port, spec_name, late, q):
     wm = -1
     rec_base = 0
     results = []
+    paths = []
     for slices in _batches(G, late):
         key, ts, cols, valid = slices[rank]
         keyed = key != abi.HSG_KEY_NONE
@@ -96,36 +134,61 @@ def _worker(rank, G, port, spec_name, late, q):
         total = sum(f[2] for f in allf)
         time_win = spec.window_kind in (abi.HSG_TUMBLING, abi.HSG_HOPPING)
         may_be_late = time_win and wm_global > min_ts + spec.grace_ms
-        rec_wm = np.maximum.accumulate(np.concatenate([[carry], ts]))[1:]
-        seq = seq_base + np.arange(len(ts), dtype=np.int64)
-        own = np.where(keyed, owner_of(key, G), G)
-        # stable partition by owner, drop HSG_KEY_NONE
-        order = np.argsort(own, kind="stable")
-        order = order[own[order] < G]
-        counts = np.bincount(own[own < G], minlength=G)
-        rows = np.stack([key.astype(np.int64), ts, cols[0], cols[1].view(np.int64), valid[0].astype(np.int64),
-                         valid[1].astype(np.int64), seq, rec_wm], axis=1)[order]
-        send = torch.from_numpy(np.ascontiguousarray(rows)).reshape(-1)
-        cnt_t = torch.from_numpy(counts.astype(np.int64))
-        rcnt = torch.zeros(G, dtype=torch.int64)
-        dist.all_to_all_single(rcnt, cnt_t)
-        recv = torch.zeros(int(rcnt.sum()) * 8, dtype=torch.int64)
-        dist.all_to_all_single(recv, send, [int(c) * 8 for c in rcnt], [int(c) * 8 for c in counts])
-        got = recv.reshape(-1, 8).numpy()
-        r_key = got[:, 0].astype(np.uint32)
-        r_cols = [got[:, 2].copy(), got[:, 3].copy().view(np.float64)]
-        r_valid = [got[:, 4].astype(np.uint8), got[:, 5].astype(np.uint8)]
-        op.push_ex(r_key, got[:, 1].copy(), r_cols, r_valid, watermark=carry,
-                   rec_wm=got[:, 7].copy() if may_be_late else None, seq=got[:, 6].copy())
+        if fast_eligible(spec) and not may_be_late:
+            # fast path: keyed records with ts >= 0 (any ts for unwindowed), one all-to-all per column
+            sel = keyed & ((ts >= 0) | (spec.window_kind == abi.HSG_UNWINDOWED))
+            own = np.where(sel, owner_of(key, G), G)
+            order = np.argsort(own, kind="stable")
+            order = order[own[order] < G]
+            counts = np.bincount(own[own < G], minlength=G)
+            rcnt = torch.zeros(G, dtype=torch.int64)
+            dist.all_to_all_single(rcnt, torch.from_numpy(counts.astype(np.int64)))
+            cols_in = [key.astype(np.int64), ts, cols[0], cols[1].view(np.int64), valid[0].astype(np.int64),
+                       valid[1].astype(np.int64)]
+            cols_out = []
+            for col in cols_in:
+                send = torch.from_numpy(np.ascontiguousarray(col[order]))
+                recv = torch.zeros(int(rcnt.sum()), dtype=torch.int64)
+                dist.all_to_all_single(recv, send, [int(c) for c in rcnt], [int(c) for c in counts])
+                cols_out.append(recv.numpy())
+            op.push_ex(cols_out[0].astype(np.uint32), cols_out[1].copy(),
+                       [cols_out[2].copy(), cols_out[3].copy().view(np.float64)],
+                       [cols_out[4].astype(np.uint8), cols_out[5].astype(np.uint8)], watermark=carry)
+            paths.append("fast")
+        else:
+            rec_wm = np.maximum.accumulate(np.concatenate([[carry], ts]))[1:]
+            seq = seq_base + np.arange(len(ts), dtype=np.int64)
+            own = np.where(keyed, owner_of(key, G), G)
+            # stable partition by owner, drop HSG_KEY_NONE
+            order = np.argsort(own, kind="stable")
+            order = order[own[order] < G]
+            counts = np.bincount(own[own < G], minlength=G)
+            rows = np.stack([key.astype(np.int64), ts, cols[0], cols[1].view(np.int64), valid[0].astype(np.int64),
+                             valid[1].astype(np.int64), seq, rec_wm], axis=1)[order]
+            send = torch.from_numpy(np.ascontiguousarray(rows)).reshape(-1)
+            cnt_t = torch.from_numpy(counts.astype(np.int64))
+            rcnt = torch.zeros(G, dtype=torch.int64)
+            dist.all_to_all_single(rcnt, cnt_t)
+            recv = torch.zeros(int(rcnt.sum()) * 8, dtype=torch.int64)
+            dist.all_to_all_single(recv, send, [int(c) * 8 for c in rcnt], [int(c) * 8 for c in counts])
+            got = recv.reshape(-1, 8).numpy()
+            r_key = got[:, 0].astype(np.uint32)
+            r_cols = [got[:, 2].copy(), got[:, 3].copy().view(np.float64)]
+            r_valid = [got[:, 4].astype(np.uint8), got[:, 5].astype(np.uint8)]
+            op.push_ex(r_key, got[:, 1].copy(), r_cols, r_valid, watermark=carry,
+                       rec_wm=got[:, 7].copy() if may_be_late else None, seq=got[:, 6].copy())
+            paths.append("classic")
         wm = wm_global
         rec_base += total
         rows_out = op.drain() if spec.emit_mode != abi.HSG_EMIT_NONE else None
+        if rows_out is not None and spec.emit_mode == abi.HSG_EMIT_PER_BATCH:
+            rows_out.src_index[:] = -1  # per-batch rows carry no producing record
         results.append(None if rows_out is None else rows_out.tuples_with_src() if hasattr(rows_out, "tuples_with_src")
                        else [(int(rows_out.key_id[i]), int(rows_out.win_start[i]), int(rows_out.win_end[i]),
                               int(rows_out.src_index[i]), tuple(a[i].item() for a in rows_out.aggs))
                              for i in range(len(rows_out))])
     state = op.dump_state().tuples()
-    q.put((rank, wm, results, state))
+    q.put((rank, wm, results, state, paths))
     dist.destroy_process_group()
 
 
@@ -141,7 +204,12 @@ def _single(spec_name, G, late):
         cols = [np.concatenate([s[2][c] for s in slices]) for c in range(2)]
         valid = [np.concatenate([s[3][c] for s in slices]) for c in range(2)]
         wm = op.push(key, ts, cols, valid, watermark=wm)
+        if spec.emit_mode == abi.HSG_EMIT_NONE:
+            results.append(None)
+            continue
         r = op.drain()
+        if spec.emit_mode == abi.HSG_EMIT_PER_BATCH:
+            r.src_index[:] = -1
         results.append([(int(r.key_id[i]), int(r.win_start[i]), int(r.win_end[i]), int(r.src_index[i]),
                          tuple(a[i].item() for a in r.aggs)) for i in range(len(r))])
     return wm, results, op.dump_state().tuples()
@@ -174,6 +242,9 @@ def test_two_rank_protocol_equals_single_stream(spec_name, late):
     outs.sort()
     wm1, res1, st1 = _single(spec_name, G, late)
     assert all(o[1] == wm1 for o in outs)
+    # which exchange ran: the fast one when eligible and no record can be late
+    for o in outs:
+        assert set(o[4]) == {PATHS[spec_name]}, o[4]
     # union of the ranks' state = the single-stream state, keys disjoint
     keys = [set(k for k, *_ in o[3]) for o in outs]
     assert not (keys[0] & keys[1])
@@ -183,6 +254,8 @@ def test_two_rank_protocol_equals_single_stream(spec_name, late):
         assert a[:3] == b[:3] and _close(a[3], b[3]), (a, b)
     # changelogs: per-record rows carry the global sequence; merged by (src, start)
     for bi in range(len(res1)):
+        if res1[bi] is None:
+            continue
         rows = sorted(outs[0][2][bi] + outs[1][2][bi], key=lambda t: (t[3], t[1], t[0], t[2]))
         ref = sorted(res1[bi], key=lambda t: (t[3], t[1], t[0], t[2]))
         assert len(rows) == len(ref)
