@@ -2,9 +2,9 @@
 
 bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950 FETCH_SIZE counts
 half of the bytes of wide streaming reads (MI355X_MICROARCH.md, HBM section),
-WRITE_SIZE is exact for 16-byte stores. A batch = one k_part_hist dispatch (the
-first kernel of the partitioned pipeline); the warmup step is dropped by
-keeping the last half of the dispatches.
+WRITE_SIZE is exact for 16-byte stores. A batch = one dispatch of the first
+kernel of the pipeline (k_part_hist for time windows, k_ss_phist for
+sessions); the warmup step is dropped by keeping the last half of them.
 """
 import collections
 import csv
@@ -25,7 +25,8 @@ def load(path):
 fetch, names = load(sys.argv[1])
 write, _ = load(sys.argv[2])
 disp = sorted(names)
-starts = [d for d in disp if "k_part_hist" in names[d]]
+first = "k_ss_phist" if any("k_ss_phist" in names[d] for d in disp) else "k_part_hist"
+starts = [d for d in disp if first in names[d]]
 half = starts[len(starts) // 2:]  # the timed step (warmup step first)
 batches = []
 for i, s in enumerate(half):
@@ -34,8 +35,6 @@ for i, s in enumerate(half):
     kib = sum(2 * fetch.get(d, 0.0) + write.get(d, 0.0) for d in ks)
     batches.append(kib * 1024)
 by_kernel = collections.defaultdict(float)
-for s in half:
-    pass
 for d in disp:
     if half and d >= half[0]:
         by_kernel[names[d].split("(")[0][:60]] += (2 * fetch.get(d, 0.0) + write.get(d, 0.0)) * 1024 / max(1, len(half))

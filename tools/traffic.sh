@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 name=$1; shift
 mkdir -p gpurun_out/pmc
 for ctr in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "hsg::" -d gpurun_out/pmc -o ${name}_$ctr \
+  timeout -s KILL 300 rocprofv3 --pmc $ctr --kernel-include-regex "hsg::" -d gpurun_out/pmc -o ${name}_$ctr \
     --output-format csv -- python3 bench.py --steps 1 --warmup 1 --cpu-seconds 0 "$@" > gpurun_out/pmc/${name}_$ctr.log 2>&1
   rc=$?; echo "== $name $ctr rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
