@@ -35,6 +35,7 @@ struct ProgSig {
     while (k < 8 && ((SIG >> (7 * k)) & 15u) != 0) ++k;
     return k;
   }
+  __device__ ProgSig() {}
   __device__ explicit ProgSig(const Program &) {}
   __device__ constexpr int n() const { return count(); }
   __device__ constexpr int op(int s) const { return (int)((SIG >> (7 * s)) & 15u) - 1; }

@@ -96,9 +96,12 @@ struct DevScalars {
   uint32_t redo;         // optimistic partition path: the batch has late records, run it again carefully
   uint64_t packed;       // partition path, this batch: records in the packed layout (hsg_part.h)
   uint64_t kbase;        // packed layout: window (relative to the epoch) the 16-bit window offsets count from
-  uint64_t scratch[53];  // [0] groups flushed (partition path), [1] touched-list length, [8..20] phase clocks,
+  uint64_t scratch[45];  // [0] groups flushed (partition path), [1] touched-list length, [8..20] phase clocks,
                          // [21..22] optimistic pass ts extrema
+  uint64_t live_x[8];    // more rows found, one shard per XCD (blockIdx & 7) for kernels whose every
+                         // workgroup adds; the host folds them into `live` when it fetches the scalars
 };
+constexpr int kScratchWords = 45;
 static_assert(sizeof(DevScalars) == 512, "DevScalars layout");
 
 constexpr uint32_t ERR_OOM = 1u;

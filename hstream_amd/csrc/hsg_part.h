@@ -37,6 +37,9 @@ struct PartBuffers {
   uint64_t *toff;         // [touch_chunks + 1] exclusive prefix
   uint64_t *tpartial;     // scan partials
   int64_t *wm;            // [n] per-record stream time (written only when late records are possible)
+  uint64_t *pane;         // lean aggregation: [n][pane_words] group partials [g][slot 0 .. n_slots-1], each
+                          // workgroup's entries at its chunk's record range
+  uint64_t *pane_info;    // [workgroups][2]: first entry, entry count | overflow flag << 32
   uint64_t n_cap;
 };
 
@@ -81,6 +84,12 @@ void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const
 bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, const PartParams &pp, const TwTable &t,
                      const PartBuffers &pb, uint64_t n, DevScalars *sc, bool maybe_packed);
 bool part_supported(const Program &prog);
+// Lean aggregation of packed tumbling / unwindowed batches (pane_S = 1, no key
+// rounds, a specialised slot program): records -> LDS table -> group partials
+// in pb.pane, applied to the HBM table by a separate launch (k_agg_lean.hip).
+// Returns false when the batch's shape has no lean variant.
+bool launch_part_agg_lean(hipStream_t s, dim3 g, const Program &prog, const TwParams &p, const PartParams &pp,
+                          const TwTable &t, const PartBuffers &pb, DevScalars *sc);
 // per-batch changelog rows of the groups in pb.touched
 void launch_part_emit(hipStream_t s, const TwTable &t, const Program &prog, const TwParams &p, const PartBuffers &pb,
                       OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc);

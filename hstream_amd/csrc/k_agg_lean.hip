@@ -1,0 +1,367 @@
+// Lean aggregation of packed one-window-per-record batches (tumbling and
+// unwindowed ops, the BASELINE C2 / C5 shape), in two launches:
+//
+//   k_agg_lean   one workgroup per bucket chunk: the chunk's packed records
+//                (register double-buffered, no barrier per record block) into
+//                an LDS hash table keyed by a 32-bit multiplicative hash of
+//                (key, window); at the end the live entries are written as
+//                group partials [g][slot 0 .. n-1] to the chunk's own range of
+//                pb.pane (coalesced stores, nothing waited on). A record whose
+//                LDS probe sequence finds no room becomes a one-record partial
+//                of its own (rare: buckets are sized to half a table).
+//   k_pane_apply one workgroup per aggregation workgroup: its partials into
+//                the HBM (key, window) table -- claim / read-modify-write as
+//                the general kernel's flush (hsg_agg.h flush_window), touched
+//                list for the per-batch changelog.
+//
+// Splitting the HBM updates out of the aggregation workgroup takes their
+// dependent HBM round trips (claim load, CAS, row read) off the LDS-resident
+// workgroup: many apply workgroups per CU hide them instead.
+//
+// Semantics are those of k_part_agg with pane_S = 1 (TimeWindowedStream.hs:
+// 86-103 per (key, window) group, commutative SQL aggregates of Codegen.hs:
+// 399-469): every record updates exactly one group.
+#include "hsg_agg.h"
+
+namespace hsg {
+
+constexpr int kLeanProbe = 32;  // LDS probes before a record becomes its own partial
+
+// 32-bit hash of (key, relative window) for the LDS table (top bits used)
+__device__ inline uint32_t lean_hash(uint32_t key, uint32_t w) {
+  uint32_t h = key * 0x9E3779B1u + w * 0x85EBCA77u;
+  return h ^ (h >> 16) * 0x7FEB352Du;
+}
+
+template <int E>
+__device__ inline uint32_t lean_home(uint32_t key, uint32_t w) {
+  constexpr int LOG2E = __builtin_ctz(E);
+  return lean_hash(key, w) >> (32 - LOG2E);
+}
+
+// value of slot s for one packed record (COUNT(col) slots of batches without
+// validity arrays are filled from COUNT(*) at write-out)
+template <int NS, uint64_t SIG, int W>
+__device__ inline void lean_elems(const PRec<W, true> &r, int64_t (&v)[NS]) {
+  const ProgSig<SIG> prog;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) v[s] = prec_elem(prog, s, r);
+}
+
+// chunk of this workgroup: records [r0, r1) of bucket b; false past the chunks
+__device__ inline bool lean_chunk(const PartParams &pp, const PartBuffers &pb, uint32_t &b, uint64_t &r0,
+                                  uint64_t &r1, bool &exclusive) {
+  const int nb = 1 << pp.np_log2;
+  if (blockIdx.x >= pb.chunk_start[nb]) return false;
+  b = pb.chunk_bucket[blockIdx.x];
+  const uint32_t c0 = pb.chunk_start[b], c1 = pb.chunk_start[b + 1];
+  const uint64_t b0 = pb.bstart[b], b1 = pb.bstart[b + 1];
+  r0 = b0 + (uint64_t)(blockIdx.x - c0) * pp.chunk;
+  r1 = r0 + pp.chunk < b1 ? r0 + pp.chunk : b1;
+  exclusive = c1 - c0 == 1;
+  return true;
+}
+
+template <int E, int NT, int W, uint64_t SIG>
+__global__ __launch_bounds__(NT) void k_agg_lean(PartParams pp, PartBuffers pb, DevScalars *sc) {
+  constexpr int NS = ProgSig<SIG>::count();
+  constexpr int PW = 1 + NS;  // pane entry words
+  constexpr int RB = 4;       // records per thread per block (one block in flight beside it)
+  __shared__ uint64_t lkey[E];
+  __shared__ int64_t lagg[NS * E];
+  __shared__ uint32_t s_cnt, s_ovf;
+  if (sc->redo || !sc->packed) return;  // uniform: the careful path / wide variant runs
+  uint32_t b;
+  uint64_t r0, r1;
+  bool exclusive;
+  if (!lean_chunk(pp, pb, b, r0, r1, exclusive)) return;  // uniform
+  const ProgSig<SIG> prog;
+  const uint32_t kbase = (uint32_t)sc->kbase;
+  // without validity arrays COUNT(col) = COUNT(*): not kept in LDS
+  int cnt_all_slot = -1;
+  uint32_t skip = 0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (prog.op(s) == S_CNT_ALL && cnt_all_slot < 0) cnt_all_slot = s;
+  if (!pp.has_valid && cnt_all_slot >= 0) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      if (prog.op(s) == S_CNT) skip |= 1u << s;
+  }
+  for (int e = threadIdx.x; e < E; e += NT) {
+    lkey[e] = kEmpty;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) lagg[s * E + e] = slot_identity_dev(prog.op(s));
+  }
+  if (threadIdx.x == 0) {
+    s_cnt = 0;
+    s_ovf = 0;
+  }
+  uint64_t *const pane = pb.pane + r0 * PW;
+  __syncthreads();
+
+  // records: block k holds records r0 + k*RB*NT + u*NT + tid; the next block's
+  // loads are issued before the current one is processed
+  PRec<W, true> cur[RB], nxt[RB];
+  auto load = [&](uint64_t s0, PRec<W, true>(&d)[RB]) {
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const uint64_t i = s0 + (uint64_t)u * NT + threadIdx.x;
+      d[u].C = W - 1;
+      if (i < r1) {
+        if constexpr (W == 2) {
+          const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(pb.rec + i * 2);
+          d[u].w[0] = x.x;
+          d[u].w[1] = x.y;
+        } else {
+          d[u].w[0] = pb.rec[i];
+        }
+      } else {
+        d[u].w[0] = kEmpty;  // no record (a real header has nwin = 1 in bits 48..55)
+        if constexpr (W == 2) d[u].w[1] = 0;
+      }
+    }
+  };
+  load(r0, cur);
+  for (uint64_t s0 = r0; s0 < r1; s0 += (uint64_t)RB * NT) {
+    if (s0 + (uint64_t)RB * NT < r1) load(s0 + (uint64_t)RB * NT, nxt);
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const PRec<W, true> &r = cur[u];
+      if (r.w[0] == kEmpty) continue;
+      const uint32_t key = r.key(), kw = r.krel(kbase);
+      const uint64_t g = ((uint64_t)key << 32) | kw;
+      uint32_t h = lean_home<E>(key, kw);
+      int e = -1;
+      for (int probe = 0; probe < kLeanProbe; ++probe) {
+        const uint64_t c = lkey[h];
+        if (c == g) {
+          e = (int)h;
+          break;
+        }
+        if (c == kEmpty) {
+          const uint64_t old =
+              atomicCAS((unsigned long long *)&lkey[h], (unsigned long long)kEmpty, (unsigned long long)g);
+          if (old == kEmpty || old == g) {
+            e = (int)h;
+            break;
+          }
+        }
+        h = (h + 1) & (E - 1);
+      }
+      if (e >= 0) {
+        lds_apply<NS, E>(prog, &lagg[e], r, skip);
+      } else {
+        // no room: this record is a partial of its own
+        int64_t v[NS];
+        lean_elems<NS, SIG, W>(r, v);
+        if (skip) {
+#pragma unroll
+          for (int s = 0; s < NS; ++s)
+            if ((skip >> s) & 1u) v[s] = 1;
+        }
+        const uint32_t q = atomicAdd(&s_cnt, 1u);
+        uint64_t *o = pane + (uint64_t)q * PW;
+        o[0] = g;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) o[1 + s] = (uint64_t)v[s];
+        s_ovf = 1;
+      }
+    }
+    if (s0 + (uint64_t)RB * NT < r1) {
+#pragma unroll
+      for (int u = 0; u < RB; ++u) cur[u] = nxt[u];
+    }
+  }
+  __syncthreads();
+
+  // live entries -> partials (one LDS atomic per wave for the positions)
+  const int lane = threadIdx.x & 63;
+  for (int e0 = 0; e0 < E; e0 += NT) {
+    const int e = e0 + threadIdx.x;
+    const uint64_t g = lkey[e];
+    const bool on = g != kEmpty;
+    const uint64_t m = __ballot(on);
+    uint32_t wb = 0;
+    if (lane == 0 && m) wb = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
+    wb = __shfl(wb, 0, 64);
+    if (!on) continue;
+    const uint32_t q = wb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    uint64_t *o = pane + (uint64_t)q * PW;
+    o[0] = g;
+    const int64_t call = cnt_all_slot >= 0 ? lagg[cnt_all_slot * E + e] : 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) o[1 + s] = (uint64_t)(((skip >> s) & 1u) ? call : lagg[s * E + e]);
+  }
+  __syncthreads();
+  // the batch totals (pairs = records placed, groups = partials) are set by
+  // the last apply workgroup: no per-workgroup atomic on a shared counter
+  if (threadIdx.x == 0) {
+    pb.pane_info[2 * blockIdx.x] = r0;
+    pb.pane_info[2 * blockIdx.x + 1] = (uint64_t)s_cnt | ((uint64_t)s_ovf << 32);
+  }
+}
+
+// One workgroup per aggregation workgroup: its partials into the HBM table.
+// exclusive (the bucket is one chunk): no other workgroup updates these groups
+// in this batch; without overflow partials each group appears once, so a plain
+// read-modify-write (plain stores into a row claimed just now) suffices; with
+// them, workgroup-scope atomics (this workgroup's XCD L2). Split buckets use
+// device-scope atomics, as the general kernel.
+template <uint64_t SIG>
+__global__ __launch_bounds__(256) void k_pane_apply(TwParams p, PartParams pp, TwTable t, PartBuffers pb,
+                                                    DevScalars *sc) {
+  constexpr int NS = ProgSig<SIG>::count();
+  constexpr int PW = 1 + NS;
+  __shared__ uint64_t s_red[4];
+  if (sc->redo || !sc->packed) return;  // uniform
+  uint32_t b;
+  uint64_t r0, r1;
+  bool exclusive;
+  if (!lean_chunk(pp, pb, b, r0, r1, exclusive)) return;  // uniform
+  const ProgSig<SIG> prog;
+  const uint64_t base = pb.pane_info[2 * blockIdx.x], ci = pb.pane_info[2 * blockIdx.x + 1];
+  const uint32_t cnt = (uint32_t)ci;
+  const bool ovf = (ci >> 32) != 0;
+  const bool plain_claim = exclusive && pp.np_log2 <= t.rbits && pp.bshift == t.bshift;
+  const bool plain_rmw = exclusive && !ovf;
+  // touched-list position: the partials of the workgroups before this one
+  // (a few L2-resident loads per thread instead of a returning atomic on one
+  // counter from every workgroup)
+  uint64_t before = 0;
+  for (uint32_t k = threadIdx.x; k < blockIdx.x; k += 256) before += (uint32_t)pb.pane_info[2 * k + 1];
+  before = wave_sum_u64(before);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = before;
+  __syncthreads();
+  const uint64_t tb = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+  const int nb = 1 << pp.np_log2;
+  if (threadIdx.x == 0 && blockIdx.x + 1 == pb.chunk_start[nb]) {
+    // last workgroup: batch totals (every placed record updates one group)
+    sc->scratch[1] = tb + cnt;
+    sc->scratch[0] = tb + cnt;
+    sc->pairs = pb.bstart[nb];
+  }
+  __syncthreads();
+  const uint64_t *pane = pb.pane + base * PW;
+  const uint32_t bid = (uint32_t)p.batch_id;
+  uint32_t fresh = 0, err = 0;
+  for (uint32_t q = threadIdx.x; q < cnt; q += 256) {
+    const uint64_t *ent = pane + (uint64_t)q * PW;
+    const uint64_t g = ent[0];
+    int64_t v[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) v[s] = (int64_t)ent[1 + s];
+    const uint32_t f0 = fresh;
+    const int64_t slot = plain_claim ? tw_claim_exclusive(t, g, fresh) : tw_find_or_insert(t, g, fresh);
+    uint32_t tl = kTouchSkip;
+    if (slot < 0) {
+      err |= ERR_OOM;
+    } else {
+      int64_t *row = t.aggs(slot);
+      uint32_t *stp = t.stamp(slot);
+      bool first;
+      if (plain_rmw && fresh != f0) {
+        // claimed just now by the group's only writer: the row holds identities
+#pragma unroll
+        for (int s = 0; s < NS; ++s) row[s] = v[s];
+        *stp = bid;
+        first = true;
+      } else if (plain_rmw) {
+        int64_t c[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) c[s] = __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t st = __hip_atomic_load(stp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          if (v[s] != slot_identity_dev(prog.op(s))) row[s] = slot_combine(prog.op(s), c[s], v[s]);
+        first = st != bid;
+        if (first) *stp = bid;
+      } else if (exclusive) {
+        // overflow partials: the same group may appear twice in this segment
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const int op = prog.op(s);
+          const int64_t x = v[s];
+          if (x == slot_identity_dev(op)) continue;
+          switch (op) {
+            case S_CNT_ALL:
+            case S_CNT:
+            case S_SUM_I:
+              __hip_atomic_fetch_add((unsigned long long *)(row + s), (unsigned long long)x, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+              break;
+            case S_SUM_F:
+              __hip_atomic_fetch_add((double *)(row + s), __builtin_bit_cast(double, x), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+              break;
+            case S_MIN_I:
+              __hip_atomic_fetch_min((long long *)(row + s), (long long)x, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+              break;
+            case S_MAX_I:
+              __hip_atomic_fetch_max((long long *)(row + s), (long long)x, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+              break;
+            case S_MIN_F:
+              __hip_atomic_fetch_min((unsigned long long *)(row + s), (unsigned long long)x, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+              break;
+            case S_MAX_F:
+              __hip_atomic_fetch_max((unsigned long long *)(row + s), (unsigned long long)x, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+              break;
+            default: break;
+          }
+        }
+        first = __hip_atomic_exchange(stp, bid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != bid;
+      } else {
+        flush_row_atomic<NS>(prog, row, v);
+        first = atomicExch(stp, bid) != bid;
+      }
+      if (first) tl = (uint32_t)slot;
+    }
+    const uint64_t o = tb + q;
+    if (o < pb.touched_cap) pb.touched[o] = tl;
+    else err |= ERR_OOM;
+  }
+  if (err) atomicOr(&sc->err, err);
+  const uint64_t fr = wave_sum_u64(fresh);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = fr;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t f = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+    if (f) atomicAdd((unsigned long long *)&sc->live_x[blockIdx.x & 7], (unsigned long long)f);
+  }
+}
+
+template <int W, uint64_t SIG>
+static bool lean_launch(uint64_t sig, hipStream_t s, dim3 g, bool big, const TwParams &p, const PartParams &pp,
+                        const TwTable &t, const PartBuffers &pb, DevScalars *sc) {
+  if (sig != SIG) return false;
+  constexpr int NS = ProgSig<SIG>::count();
+  constexpr int ES = NS <= 2 ? 2048 : 1024, EL = NS <= 2 ? 4096 : 2048;  // part_lds_entries
+  if (big)
+    hipLaunchKernelGGL((k_agg_lean<EL, 1024, W, SIG>), g, dim3(1024), 0, s, pp, pb, sc);
+  else
+    hipLaunchKernelGGL((k_agg_lean<ES, 512, W, SIG>), g, dim3(512), 0, s, pp, pb, sc);
+  hipLaunchKernelGGL((k_pane_apply<SIG>), g, dim3(256), 0, s, p, pp, t, pb, sc);
+  return true;
+}
+
+bool launch_part_agg_lean(hipStream_t s, dim3 g, const Program &prog, const TwParams &p, const PartParams &pp,
+                          const TwTable &t, const PartBuffers &pb, DevScalars *sc) {
+  if (pp.pane_S != 1 || pp.rbits != 0 || pp.has_seq) return false;
+  const int W = pp.words - 1;  // packed words
+  const uint64_t sig = program_sig(prog);
+  const bool big = pp.big != 0;
+  if (W == 1) return lean_launch<1, kSigCnt>(sig, s, g, big, p, pp, t, pb, sc);
+  if (W != 2) return false;
+  return lean_launch<2, kSigAllI>(sig, s, g, big, p, pp, t, pb, sc) ||
+         lean_launch<2, kSigAllF>(sig, s, g, big, p, pp, t, pb, sc) ||
+         lean_launch<2, kSigCnt>(sig, s, g, big, p, pp, t, pb, sc) ||
+         lean_launch<2, kSigCntSumI>(sig, s, g, big, p, pp, t, pb, sc) ||
+         lean_launch<2, kSigCntSumF>(sig, s, g, big, p, pp, t, pb, sc) ||
+         lean_launch<2, kSigSumMaxI>(sig, s, g, big, p, pp, t, pb, sc);
+}
+
+}  // namespace hsg

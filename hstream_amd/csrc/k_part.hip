@@ -822,6 +822,9 @@ bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, cons
   hipLaunchKernelGGL(k_part_chunks, dim3(1), dim3(1024), 0, s, pb.bstart, pp.np_log2, pp.chunk, pb.chunk_start,
                      pb.chunk_bucket);
   const dim3 g((unsigned)(nb + n / pp.chunk + 1));
+  // packed one-window batches of the common slot programs: the lean kernels
+  // (k_agg_lean.hip); the general kernel below then only covers the wide layout
+  if (maybe_packed && launch_part_agg_lean(s, g, prog, p, pp, t, pb, sc)) maybe_packed = false;
   const int W = pp.words;
   if (prog.n_slots <= 2) agg_launch_ms2(s, g, W, maybe_packed, prog, p, pp, t, pb, sc);
   else if (prog.n_slots <= 4) agg_launch_ms4(s, g, W, maybe_packed, prog, p, pp, t, pb, sc);

@@ -35,14 +35,24 @@ __global__ void k_fill_rows(int64_t *__restrict__ aggs, uint64_t rows, Program p
     aggs[i] = slot_identity_dev(prog.slot_op[i % prog.n_slots]);
 }
 
-__global__ void k_tw_reset(TwTable t, Program prog) {
-  const uint64_t cap = t.mask + 1, words = cap * t.stride;
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < words; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t wi = (t.stride & (t.stride - 1)) ? (uint32_t)(i % t.stride) : (uint32_t)(i & (t.stride - 1));
-    uint64_t v = 0;
-    if (wi == 0) v = kEmpty;
-    else if (wi >= 2 && (int)(wi - 2) < prog.n_slots) v = (uint64_t)slot_identity_dev(prog.slot_op[wi - 2]);
-    t.rows[i] = v;
+// word wi of an empty row: key EMPTY, stamp 0, slot identities, padding 0
+__device__ inline uint64_t tw_empty_word(const Program &prog, uint32_t wi) {
+  if (wi == 0) return kEmpty;
+  if (wi >= 2 && (int)(wi - 2) < prog.n_slots) return (uint64_t)slot_identity_dev(prog.slot_op[wi - 2]);
+  return 0;
+}
+
+// Rows are an even number of words (tw_row_stride), so every 16-byte pair lies
+// in one row: one 16-byte store per lane and iteration (the table is sized for
+// the whole run, so this is a streaming write of hundreds of MB).
+__global__ __launch_bounds__(256) void k_tw_reset(TwTable t, Program prog) {
+  const uint64_t pairs = (t.mask + 1) * (uint64_t)t.stride / 2;
+  const uint32_t sp = t.stride / 2;
+  const bool pow2 = (sp & (sp - 1)) == 0;
+  ulonglong2 *rows = reinterpret_cast<ulonglong2 *>(t.rows);
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < pairs; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t wi = 2u * (pow2 ? (uint32_t)(i & (sp - 1)) : (uint32_t)(i % sp));
+    rows[i] = make_ulonglong2(tw_empty_word(prog, wi), tw_empty_word(prog, wi + 1));
   }
 }
 
@@ -59,7 +69,7 @@ __global__ void k_clear_scalars(DevScalars *sc) {
     sc->packed = 0;
     sc->kbase = 0;
   }
-  if (t < 53) sc->scratch[t] = 0;
+  if (t < kScratchWords) sc->scratch[t] = 0;
 }
 void launch_clear_scalars(hipStream_t s, DevScalars *sc) { hipLaunchKernelGGL(k_clear_scalars, dim3(1), dim3(64), 0, s, sc); }
 

@@ -89,6 +89,9 @@ int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog,
   const uint64_t tcap = n * (d.wpr ? d.wpr : 1), nc = touch_chunks(tcap);
   uint64_t o_touch = take(tcap * 4), o_wm = take(n * 8);
   uint64_t o_tcnt = take(nc * 4), o_toff = take((nc + 1) * 8), o_tpart = take((scan_partials_needed(nc) + 8) * 8);
+  // lean aggregation: one pane entry per record at most, [g][slots]
+  uint64_t o_pane = take(n * (1 + (uint64_t)prog.n_slots) * 8);
+  uint64_t o_pinfo = take(((1ull << kPartMaxLog2) + n / 1024 + 2) * 16);
   DTRY(hipMalloc(&d.part_mem, off));
   char *m = (char *)d.part_mem;
   pb.hist = (uint32_t *)(m + o_hist);
@@ -106,6 +109,8 @@ int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog,
   pb.toff = (uint64_t *)(m + o_toff);
   pb.tpartial = (uint64_t *)(m + o_tpart);
   pb.wm = (int64_t *)(m + o_wm);
+  pb.pane = (uint64_t *)(m + o_pane);
+  pb.pane_info = (uint64_t *)(m + o_pinfo);
   pb.n_cap = n;
   return HSG_OK;
 }
@@ -347,6 +352,7 @@ int fetch_scalars(OpDevice &d, std::string &err) {
   launch_clear_scalars(d.stream, d.sc);
   DTRY(hipStreamSynchronize(d.stream));
   DTRY(hipGetLastError());
+  for (int k = 0; k < 8; ++k) d.h_sc->live += d.h_sc->live_x[k];  // device: live + shards
   d.sc_clean = true;
   return HSG_OK;
 }

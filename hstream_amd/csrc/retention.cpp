@@ -200,6 +200,7 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
   if (back) tw_retention_reset(d);
   d.h_sc->live = keep;
   DTRY(hipMemcpyAsync(&d.sc->live, &d.h_sc->live, 8, hipMemcpyHostToDevice, d.stream));
+  DTRY(hipMemsetAsync(d.sc->live_x, 0, sizeof(d.sc->live_x), d.stream));
   if (ncap != d.cap) {
     d.grow_events += 1;
     // emit / dump scratch for the larger table
