@@ -40,6 +40,7 @@ struct PartBuffers {
   uint64_t *pane;         // lean aggregation: [n][pane_words] group partials [g][slot 0 .. n_slots-1], each
                           // workgroup's entries at its chunk's record range
   uint64_t *pane_info;    // [workgroups][2]: first entry, entry count | overflow flag << 32
+  uint32_t *pane_cnt;     // [workgroups] entry counts, dense (the apply's touched-list prefix)
   uint64_t n_cap;
 };
 

@@ -3,8 +3,8 @@
 //
 //   k_agg_lean   one workgroup per bucket chunk: the chunk's packed records
 //                (register double-buffered, no barrier per record block) into
-//                an LDS hash table keyed by a 32-bit multiplicative hash of
-//                (key, window); at the end the live entries are written as
+//                an LDS hash table at a 32-bit multiplicative hash of the key
+//                plus the window; at the end the live entries are written as
 //                group partials [g][slot 0 .. n-1] to the chunk's own range of
 //                pb.pane (coalesced stores, nothing waited on). A record whose
 //                LDS probe sequence finds no room becomes a one-record partial
@@ -27,16 +27,27 @@ namespace hsg {
 
 constexpr int kLeanProbe = 32;  // LDS probes before a record becomes its own partial
 
-// 32-bit hash of (key, relative window) for the LDS table (top bits used)
-__device__ inline uint32_t lean_hash(uint32_t key, uint32_t w) {
-  uint32_t h = key * 0x9E3779B1u + w * 0x85EBCA77u;
-  return h ^ (h >> 16) * 0x7FEB352Du;
-}
-
+// LDS home of (key, window): a 32-bit multiplicative hash (top bits),
+// linear probing
 template <int E>
 __device__ inline uint32_t lean_home(uint32_t key, uint32_t w) {
   constexpr int LOG2E = __builtin_ctz(E);
-  return lean_hash(key, w) >> (32 - LOG2E);
+  uint32_t h = key * 0x9E3779B1u + w * 0x85EBCA77u;
+  h ^= (h >> 16) * 0x7FEB352Du;
+  return h >> (32 - LOG2E);
+}
+
+// Sort key of a partial for the write-out: its HBM home row within the slot
+// range the bucket's groups can occupy, in kLeanSortBins bins, so that the
+// apply's neighbouring lanes update neighbouring rows (shared lines, no
+// line touched by two wave-instructions of one workgroup more than needed).
+constexpr int kLeanSortBins = 1024;
+__device__ inline uint32_t lean_sort_bin(const TwTable &t, const PartParams &pp, uint64_t g) {
+  const uint64_t slot = tw_region_base(t, g) + tw_home_in(t, g);
+  const int cl = 64 - __builtin_clzll(t.mask);  // log2(cap)
+  const int span = pp.np_log2 <= t.rbits ? cl - pp.np_log2 : cl - t.rbits;  // log2 of the bucket's slot range
+  const uint64_t local = slot & ((1ull << span) - 1);
+  return span > 10 ? (uint32_t)(local >> (span - 10)) : (uint32_t)local;
 }
 
 // value of slot s for one packed record (COUNT(col) slots of batches without
@@ -63,13 +74,15 @@ __device__ inline bool lean_chunk(const PartParams &pp, const PartBuffers &pb, u
 }
 
 template <int E, int NT, int W, uint64_t SIG>
-__global__ __launch_bounds__(NT) void k_agg_lean(PartParams pp, PartBuffers pb, DevScalars *sc) {
+__global__ __launch_bounds__(NT) void k_agg_lean(PartParams pp, TwTable t, PartBuffers pb, DevScalars *sc) {
   constexpr int NS = ProgSig<SIG>::count();
   constexpr int PW = 1 + NS;  // pane entry words
   constexpr int RB = 4;       // records per thread per block (one block in flight beside it)
   __shared__ uint64_t lkey[E];
   __shared__ int64_t lagg[NS * E];
   __shared__ uint32_t s_cnt, s_ovf;
+  __shared__ uint32_t s_bin[kLeanSortBins];
+  __shared__ uint32_t s_wsum[NT / 64];
   if (sc->redo || !sc->packed) return;  // uniform: the careful path / wide variant runs
   uint32_t b;
   uint64_t r0, r1;
@@ -88,6 +101,7 @@ __global__ __launch_bounds__(NT) void k_agg_lean(PartParams pp, PartBuffers pb, 
     for (int s = 0; s < NS; ++s)
       if (prog.op(s) == S_CNT) skip |= 1u << s;
   }
+  for (int k = threadIdx.x; k < kLeanSortBins; k += NT) s_bin[k] = 0;
   for (int e = threadIdx.x; e < E; e += NT) {
     lkey[e] = kEmpty;
 #pragma unroll
@@ -175,31 +189,95 @@ __global__ __launch_bounds__(NT) void k_agg_lean(PartParams pp, PartBuffers pb, 
   }
   __syncthreads();
 
-  // live entries -> partials (one LDS atomic per wave for the positions)
-  const int lane = threadIdx.x & 63;
-  for (int e0 = 0; e0 < E; e0 += NT) {
-    const int e = e0 + threadIdx.x;
-    const uint64_t g = lkey[e];
-    const bool on = g != kEmpty;
-    const uint64_t m = __ballot(on);
-    uint32_t wb = 0;
-    if (lane == 0 && m) wb = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
-    wb = __shfl(wb, 0, 64);
-    if (!on) continue;
-    const uint32_t q = wb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  // live entries -> partials, in the order of their HBM home rows (counting
+  // sort over kLeanSortBins bins), after the overflow partials
+  constexpr int PER = E / NT;
+  uint32_t bin[PER], rank[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const uint64_t g = lkey[k * NT + threadIdx.x];
+    bin[k] = g != kEmpty ? lean_sort_bin(t, pp, g) : ~0u;
+    rank[k] = g != kEmpty ? atomicAdd(&s_bin[bin[k]], 1u) : 0u;
+  }
+  __syncthreads();
+  // exclusive scan of the bins (kLeanSortBins / NT consecutive bins per thread)
+  constexpr int BPT = kLeanSortBins / NT > 0 ? kLeanSortBins / NT : 1;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t loc = 0;
+  if (threadIdx.x * BPT < kLeanSortBins) {
+#pragma unroll
+    for (int k = 0; k < BPT; ++k) loc += s_bin[threadIdx.x * BPT + k];
+  }
+  const uint32_t incl = (uint32_t)wave_incl_sum((uint64_t)loc);
+  if (lane == 63) s_wsum[wv] = incl;
+  __syncthreads();
+  uint32_t run = incl - loc + s_cnt;  // overflow partials first
+  for (int k = 0; k < wv; ++k) run += s_wsum[k];
+  uint32_t total = 0;
+  for (int k = 0; k < NT / 64; ++k) total += s_wsum[k];
+  __syncthreads();
+  if (threadIdx.x * BPT < kLeanSortBins) {
+#pragma unroll
+    for (int k = 0; k < BPT; ++k) {
+      const uint32_t c = s_bin[threadIdx.x * BPT + k];
+      s_bin[threadIdx.x * BPT + k] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (bin[k] == ~0u) continue;
+    const int e = k * NT + threadIdx.x;
+    const uint32_t q = s_bin[bin[k]] + rank[k];
     uint64_t *o = pane + (uint64_t)q * PW;
-    o[0] = g;
+    o[0] = lkey[e];
     const int64_t call = cnt_all_slot >= 0 ? lagg[cnt_all_slot * E + e] : 0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) o[1 + s] = (uint64_t)(((skip >> s) & 1u) ? call : lagg[s * E + e]);
   }
+  if (threadIdx.x == 0) s_cnt += total;
   __syncthreads();
   // the batch totals (pairs = records placed, groups = partials) are set by
   // the last apply workgroup: no per-workgroup atomic on a shared counter
   if (threadIdx.x == 0) {
     pb.pane_info[2 * blockIdx.x] = r0;
     pb.pane_info[2 * blockIdx.x + 1] = (uint64_t)s_cnt | ((uint64_t)s_ovf << 32);
+    pb.pane_cnt[blockIdx.x] = s_cnt;
   }
+}
+
+// Claim or find g in a table region only this workgroup writes, without a
+// global atomic: the plain load of a slot is only a hint (it may show EMPTY
+// for a slot another thread of this workgroup has just claimed); the LDS set
+// of slots claimed in this launch decides, so a slot is claimed once.
+constexpr int kClaimSet = 4096;  // LDS slots (u32 slot + 1); <= kClaimSet / 2 claims per workgroup
+__device__ inline bool claim_set_insert(uint32_t *cset, uint32_t slot) {
+  uint32_t h = (slot * 0x9E3779B1u) >> (32 - 12);
+  for (int probe = 0; probe < kClaimSet; ++probe) {
+    const uint32_t old = atomicCAS(&cset[h], 0u, slot + 1u);
+    if (old == 0u) return true;
+    if (old == slot + 1u) return false;
+    h = (h + 1) & (kClaimSet - 1);
+  }
+  return false;
+}
+
+__device__ inline int64_t tw_claim_lds(const TwTable &t, uint64_t g, uint32_t *cset, uint32_t &fresh) {
+  const uint64_t base = tw_region_base(t, g);
+  uint64_t s = tw_home_in(t, g);
+  const uint64_t step = tw_step(t), n = (t.rmask + 1) / step;
+  for (uint64_t probe = 0; probe < n && probe < kMaxProbes; ++probe) {
+    const uint64_t cur = *t.key(base + s);
+    if (cur == g) return (int64_t)(base + s);
+    if (cur == kEmpty && claim_set_insert(cset, (uint32_t)(base + s))) {
+      *t.key(base + s) = g;
+      fresh += 1;
+      return (int64_t)(base + s);
+    }
+    s = (s + step) & t.rmask;
+  }
+  return -1;
 }
 
 // One workgroup per aggregation workgroup: its partials into the HBM table.
@@ -214,6 +292,7 @@ __global__ __launch_bounds__(256) void k_pane_apply(TwParams p, PartParams pp, T
   constexpr int NS = ProgSig<SIG>::count();
   constexpr int PW = 1 + NS;
   __shared__ uint64_t s_red[4];
+  __shared__ uint32_t cset[kClaimSet];
   if (sc->redo || !sc->packed) return;  // uniform
   uint32_t b;
   uint64_t r0, r1;
@@ -225,11 +304,21 @@ __global__ __launch_bounds__(256) void k_pane_apply(TwParams p, PartParams pp, T
   const bool ovf = (ci >> 32) != 0;
   const bool plain_claim = exclusive && pp.np_log2 <= t.rbits && pp.bshift == t.bshift;
   const bool plain_rmw = exclusive && !ovf;
+  // claims arbitrated in LDS: region owned, every group once, slots < 2^32
+  const bool lds_claim = plain_claim && plain_rmw && cnt <= kClaimSet / 2 && t.mask < 0xFFFFFFFFull;
+  if (lds_claim)
+    for (int k = threadIdx.x; k < kClaimSet; k += 256) cset[k] = 0;
   // touched-list position: the partials of the workgroups before this one
   // (a few L2-resident loads per thread instead of a returning atomic on one
   // counter from every workgroup)
   uint64_t before = 0;
-  for (uint32_t k = threadIdx.x; k < blockIdx.x; k += 256) before += (uint32_t)pb.pane_info[2 * k + 1];
+  const uint32_t w4 = blockIdx.x >> 2;  // whole uint4 groups of counts before this workgroup
+#pragma unroll 4
+  for (uint32_t k = threadIdx.x; k <= w4; k += 256) {
+    const uint4 c = reinterpret_cast<const uint4 *>(pb.pane_cnt)[k];
+    const uint32_t lim = blockIdx.x - 4 * k;  // counts of this group that precede us
+    before += (lim > 0 ? c.x : 0u) + (lim > 1 ? c.y : 0u) + (lim > 2 ? c.z : 0u) + (lim > 3 ? c.w : 0u);
+  }
   before = wave_sum_u64(before);
   if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = before;
   __syncthreads();
@@ -252,7 +341,9 @@ __global__ __launch_bounds__(256) void k_pane_apply(TwParams p, PartParams pp, T
 #pragma unroll
     for (int s = 0; s < NS; ++s) v[s] = (int64_t)ent[1 + s];
     const uint32_t f0 = fresh;
-    const int64_t slot = plain_claim ? tw_claim_exclusive(t, g, fresh) : tw_find_or_insert(t, g, fresh);
+    const int64_t slot = lds_claim     ? tw_claim_lds(t, g, cset, fresh)
+                         : plain_claim ? tw_claim_exclusive(t, g, fresh)
+                                       : tw_find_or_insert(t, g, fresh);
     uint32_t tl = kTouchSkip;
     if (slot < 0) {
       err |= ERR_OOM;
@@ -341,9 +432,9 @@ static bool lean_launch(uint64_t sig, hipStream_t s, dim3 g, bool big, const TwP
   constexpr int NS = ProgSig<SIG>::count();
   constexpr int ES = NS <= 2 ? 2048 : 1024, EL = NS <= 2 ? 4096 : 2048;  // part_lds_entries
   if (big)
-    hipLaunchKernelGGL((k_agg_lean<EL, 1024, W, SIG>), g, dim3(1024), 0, s, pp, pb, sc);
+    hipLaunchKernelGGL((k_agg_lean<EL, 1024, W, SIG>), g, dim3(1024), 0, s, pp, t, pb, sc);
   else
-    hipLaunchKernelGGL((k_agg_lean<ES, 512, W, SIG>), g, dim3(512), 0, s, pp, pb, sc);
+    hipLaunchKernelGGL((k_agg_lean<ES, 512, W, SIG>), g, dim3(512), 0, s, pp, t, pb, sc);
   hipLaunchKernelGGL((k_pane_apply<SIG>), g, dim3(256), 0, s, p, pp, t, pb, sc);
   return true;
 }

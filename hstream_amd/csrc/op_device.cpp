@@ -92,6 +92,7 @@ int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog,
   // lean aggregation: one pane entry per record at most, [g][slots]
   uint64_t o_pane = take(n * (1 + (uint64_t)prog.n_slots) * 8);
   uint64_t o_pinfo = take(((1ull << kPartMaxLog2) + n / 1024 + 2) * 16);
+  uint64_t o_pcnt = take(((1ull << kPartMaxLog2) + n / 1024 + 2 + 4) * 4);
   DTRY(hipMalloc(&d.part_mem, off));
   char *m = (char *)d.part_mem;
   pb.hist = (uint32_t *)(m + o_hist);
@@ -111,6 +112,7 @@ int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog,
   pb.wm = (int64_t *)(m + o_wm);
   pb.pane = (uint64_t *)(m + o_pane);
   pb.pane_info = (uint64_t *)(m + o_pinfo);
+  pb.pane_cnt = (uint32_t *)(m + o_pcnt);
   pb.n_cap = n;
   return HSG_OK;
 }
