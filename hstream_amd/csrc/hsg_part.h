@@ -82,15 +82,21 @@ void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const
                          DevScalars *sc, bool maybe_packed);
 // returns false when the op's slot count has no LDS variant (caller falls back)
 // maybe_packed: the batch may be in the packed layout (launch both variants)
+// out (per-batch changelog, else null): the lean path may write the rows itself
 bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, const PartParams &pp, const TwTable &t,
-                     const PartBuffers &pb, uint64_t n, DevScalars *sc, bool maybe_packed);
+                     const PartBuffers &pb, uint64_t n, DevScalars *sc, bool maybe_packed, const OutCols *out,
+                     uint64_t out_base, uint64_t out_cap);
 bool part_supported(const Program &prog);
 // Lean aggregation of packed tumbling / unwindowed batches (pane_S = 1, no key
 // rounds, a specialised slot program): records -> LDS table -> group partials
 // in pb.pane, applied to the HBM table by a separate launch (k_agg_lean.hip).
-// Returns false when the batch's shape has no lean variant.
+// When every group of the batch gets exactly one partial (no bucket split over
+// workgroups, no overflow partial) and out is given, the apply writes the
+// per-batch changelog rows itself (count in sc->scratch[3]) and leaves the
+// touched list empty. Returns false when the batch's shape has no lean variant.
 bool launch_part_agg_lean(hipStream_t s, dim3 g, const Program &prog, const TwParams &p, const PartParams &pp,
-                          const TwTable &t, const PartBuffers &pb, DevScalars *sc);
+                          const TwTable &t, const PartBuffers &pb, DevScalars *sc, const OutCols *out,
+                          uint64_t out_base, uint64_t out_cap);
 // per-batch changelog rows of the groups in pb.touched
 void launch_part_emit(hipStream_t s, const TwTable &t, const Program &prog, const TwParams &p, const PartBuffers &pb,
                       OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc);

@@ -21,6 +21,8 @@
 // Semantics are those of k_part_agg with pane_S = 1 (TimeWindowedStream.hs:
 // 86-103 per (key, window) group, commutative SQL aggregates of Codegen.hs:
 // 399-469): every record updates exactly one group.
+#include <cstring>
+
 #include "hsg_agg.h"
 
 namespace hsg {
@@ -243,7 +245,7 @@ __global__ __launch_bounds__(NT) void k_agg_lean(PartParams pp, TwTable t, PartB
   if (threadIdx.x == 0) {
     pb.pane_info[2 * blockIdx.x] = r0;
     pb.pane_info[2 * blockIdx.x + 1] = (uint64_t)s_cnt | ((uint64_t)s_ovf << 32);
-    pb.pane_cnt[blockIdx.x] = s_cnt;
+    pb.pane_cnt[blockIdx.x] = s_cnt | (s_ovf << 31);
   }
 }
 
@@ -286,12 +288,21 @@ __device__ inline int64_t tw_claim_lds(const TwTable &t, uint64_t g, uint32_t *c
 // read-modify-write (plain stores into a row claimed just now) suffices; with
 // them, workgroup-scope atomics (this workgroup's XCD L2). Split buckets use
 // device-scope atomics, as the general kernel.
+//
+// Direct changelog (out.key != null, no bucket split, no overflow partial in
+// the batch): every group of the batch has exactly one partial, so the row
+// this thread leaves is the group's final state for the batch -- its
+// per-batch changelog row (k_touch_emit's row) is written here, at the
+// partial's position, and the touched list stays empty.
 template <uint64_t SIG>
-__global__ __launch_bounds__(256) void k_pane_apply(TwParams p, PartParams pp, TwTable t, PartBuffers pb,
+__global__ __launch_bounds__(256) void k_pane_apply(Program rprog, TwParams p, PartParams pp, TwTable t,
+                                                    PartBuffers pb, OutCols out, uint64_t out_base, uint64_t out_cap,
                                                     DevScalars *sc) {
   constexpr int NS = ProgSig<SIG>::count();
   constexpr int PW = 1 + NS;
   __shared__ uint64_t s_red[4];
+  __shared__ uint64_t s_tot[4];
+  __shared__ uint32_t s_ovf[4];
   __shared__ uint32_t cset[kClaimSet];
   if (sc->redo || !sc->packed) return;  // uniform
   uint32_t b;
@@ -308,28 +319,46 @@ __global__ __launch_bounds__(256) void k_pane_apply(TwParams p, PartParams pp, T
   const bool lds_claim = plain_claim && plain_rmw && cnt <= kClaimSet / 2 && t.mask < 0xFFFFFFFFull;
   if (lds_claim)
     for (int k = threadIdx.x; k < kClaimSet; k += 256) cset[k] = 0;
-  // touched-list position: the partials of the workgroups before this one
-  // (a few L2-resident loads per thread instead of a returning atomic on one
-  // counter from every workgroup)
-  uint64_t before = 0;
-  const uint32_t w4 = blockIdx.x >> 2;  // whole uint4 groups of counts before this workgroup
-#pragma unroll 4
-  for (uint32_t k = threadIdx.x; k <= w4; k += 256) {
-    const uint4 c = reinterpret_cast<const uint4 *>(pb.pane_cnt)[k];
-    const uint32_t lim = blockIdx.x - 4 * k;  // counts of this group that precede us
-    before += (lim > 0 ? c.x : 0u) + (lim > 1 ? c.y : 0u) + (lim > 2 ? c.z : 0u) + (lim > 3 ? c.w : 0u);
+  // every workgroup's partial count (a few L2-resident loads per thread instead
+  // of a returning atomic on one counter from every workgroup): this one's
+  // position, the batch total, and whether any workgroup wrote overflow partials
+  const int nb = 1 << pp.np_log2;
+  const uint32_t nch = pb.chunk_start[nb];
+  uint64_t before = 0, total = 0;
+  uint32_t anyovf = 0;
+  for (uint32_t k = threadIdx.x; 4 * k < nch; k += 256) {
+    const uint4 c4 = reinterpret_cast<const uint4 *>(pb.pane_cnt)[k];
+    const uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t w = 4 * k + j;
+      if (w >= nch) break;
+      const uint32_t n = c[j] & 0x7FFFFFFFu;
+      anyovf |= c[j] >> 31;
+      total += n;
+      if (w < blockIdx.x) before += n;
+    }
   }
   before = wave_sum_u64(before);
-  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = before;
+  total = wave_sum_u64(total);
+  anyovf = __ballot(anyovf != 0) != 0;
+  if ((threadIdx.x & 63) == 0) {
+    s_red[threadIdx.x >> 6] = before;
+    s_tot[threadIdx.x >> 6] = total;
+    s_ovf[threadIdx.x >> 6] = anyovf;
+  }
   __syncthreads();
   const uint64_t tb = s_red[0] + s_red[1] + s_red[2] + s_red[3];
-  const int nb = 1 << pp.np_log2;
-  if (threadIdx.x == 0 && blockIdx.x + 1 == pb.chunk_start[nb]) {
+  total = s_tot[0] + s_tot[1] + s_tot[2] + s_tot[3];
+  const bool direct = out.key != nullptr && pb.chunk_start[nb + 1] == 0 && !(s_ovf[0] | s_ovf[1] | s_ovf[2] | s_ovf[3]);
+  if (threadIdx.x == 0 && blockIdx.x + 1 == nch) {
     // last workgroup: batch totals (every placed record updates one group)
-    sc->scratch[1] = tb + cnt;
-    sc->scratch[0] = tb + cnt;
+    sc->scratch[1] = direct ? 0 : total;
+    sc->scratch[3] = direct ? total : 0;
+    sc->scratch[0] = total;
     sc->pairs = pb.bstart[nb];
   }
+  const int64_t k_epoch = sc->k_epoch;
   __syncthreads();
   const uint64_t *pane = pb.pane + base * PW;
   const uint32_t bid = (uint32_t)p.batch_id;
@@ -351,22 +380,43 @@ __global__ __launch_bounds__(256) void k_pane_apply(TwParams p, PartParams pp, T
       int64_t *row = t.aggs(slot);
       uint32_t *stp = t.stamp(slot);
       bool first;
-      if (plain_rmw && fresh != f0) {
-        // claimed just now by the group's only writer: the row holds identities
+      if (plain_rmw) {
+        if (fresh == f0) {
+          // an existing group (its earlier windows' batches): combine
+          int64_t c[NS];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) c[s] = __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint32_t st = __hip_atomic_load(stp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+          for (int s = 0; s < NS; ++s)
+            if (v[s] != slot_identity_dev(prog.op(s))) v[s] = slot_combine(prog.op(s), c[s], v[s]);
+          first = st != bid;
+        } else {
+          first = true;  // claimed just now by the group's only writer: the row holds identities
+        }
 #pragma unroll
         for (int s = 0; s < NS; ++s) row[s] = v[s];
-        *stp = bid;
-        first = true;
-      } else if (plain_rmw) {
-        int64_t c[NS];
-#pragma unroll
-        for (int s = 0; s < NS; ++s) c[s] = __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t st = __hip_atomic_load(stp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-          if (v[s] != slot_identity_dev(prog.op(s))) row[s] = slot_combine(prog.op(s), c[s], v[s]);
-        first = st != bid;
         if (first) *stp = bid;
+        if (direct) {
+          // v is the group's state after this batch: its changelog row
+          const uint64_t o = out_base + tb + q;
+          if (o < out_cap) {
+            out.key[o] = (uint32_t)(g >> 32);
+            int64_t ws = 0, we = 0;
+            if (p.kind != HSG_UNWINDOWED) {
+              const int64_t k = k_epoch + (int64_t)(g & 0xFFFFFFFFull);
+              ws = (int64_t)((uint64_t)k * (uint64_t)p.adv);
+              we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
+            }
+            out.ws[o] = ws;
+            out.we[o] = we;
+            out.src[o] = -1;
+            for (int j = 0; j < rprog.n_out; ++j) out.agg[j][o] = out_value_reg<NS>(rprog, j, v);
+          } else {
+            err |= ERR_OOM;
+          }
+          continue;
+        }
       } else if (exclusive) {
         // overflow partials: the same group may appear twice in this segment
 #pragma unroll
@@ -426,8 +476,9 @@ __global__ __launch_bounds__(256) void k_pane_apply(TwParams p, PartParams pp, T
 }
 
 template <int W, uint64_t SIG>
-static bool lean_launch(uint64_t sig, hipStream_t s, dim3 g, bool big, const TwParams &p, const PartParams &pp,
-                        const TwTable &t, const PartBuffers &pb, DevScalars *sc) {
+static bool lean_launch(uint64_t sig, hipStream_t s, dim3 g, bool big, const Program &prog, const TwParams &p,
+                        const PartParams &pp, const TwTable &t, const PartBuffers &pb, DevScalars *sc,
+                        const OutCols &out, uint64_t out_base, uint64_t out_cap) {
   if (sig != SIG) return false;
   constexpr int NS = ProgSig<SIG>::count();
   constexpr int ES = NS <= 2 ? 2048 : 1024, EL = NS <= 2 ? 4096 : 2048;  // part_lds_entries
@@ -435,24 +486,28 @@ static bool lean_launch(uint64_t sig, hipStream_t s, dim3 g, bool big, const TwP
     hipLaunchKernelGGL((k_agg_lean<EL, 1024, W, SIG>), g, dim3(1024), 0, s, pp, t, pb, sc);
   else
     hipLaunchKernelGGL((k_agg_lean<ES, 512, W, SIG>), g, dim3(512), 0, s, pp, t, pb, sc);
-  hipLaunchKernelGGL((k_pane_apply<SIG>), g, dim3(256), 0, s, p, pp, t, pb, sc);
+  hipLaunchKernelGGL((k_pane_apply<SIG>), g, dim3(256), 0, s, prog, p, pp, t, pb, out, out_base, out_cap, sc);
   return true;
 }
 
 bool launch_part_agg_lean(hipStream_t s, dim3 g, const Program &prog, const TwParams &p, const PartParams &pp,
-                          const TwTable &t, const PartBuffers &pb, DevScalars *sc) {
+                          const TwTable &t, const PartBuffers &pb, DevScalars *sc, const OutCols *out,
+                          uint64_t out_base, uint64_t out_cap) {
+  OutCols oc;
+  memset(&oc, 0, sizeof(oc));
+  if (out) oc = *out;
   if (pp.pane_S != 1 || pp.rbits != 0 || pp.has_seq) return false;
   const int W = pp.words - 1;  // packed words
   const uint64_t sig = program_sig(prog);
   const bool big = pp.big != 0;
-  if (W == 1) return lean_launch<1, kSigCnt>(sig, s, g, big, p, pp, t, pb, sc);
+  if (W == 1) return lean_launch<1, kSigCnt>(sig, s, g, big, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
   if (W != 2) return false;
-  return lean_launch<2, kSigAllI>(sig, s, g, big, p, pp, t, pb, sc) ||
-         lean_launch<2, kSigAllF>(sig, s, g, big, p, pp, t, pb, sc) ||
-         lean_launch<2, kSigCnt>(sig, s, g, big, p, pp, t, pb, sc) ||
-         lean_launch<2, kSigCntSumI>(sig, s, g, big, p, pp, t, pb, sc) ||
-         lean_launch<2, kSigCntSumF>(sig, s, g, big, p, pp, t, pb, sc) ||
-         lean_launch<2, kSigSumMaxI>(sig, s, g, big, p, pp, t, pb, sc);
+  return lean_launch<2, kSigAllI>(sig, s, g, big, prog, p, pp, t, pb, sc, oc, out_base, out_cap) ||
+         lean_launch<2, kSigAllF>(sig, s, g, big, prog, p, pp, t, pb, sc, oc, out_base, out_cap) ||
+         lean_launch<2, kSigCnt>(sig, s, g, big, prog, p, pp, t, pb, sc, oc, out_base, out_cap) ||
+         lean_launch<2, kSigCntSumI>(sig, s, g, big, prog, p, pp, t, pb, sc, oc, out_base, out_cap) ||
+         lean_launch<2, kSigCntSumF>(sig, s, g, big, prog, p, pp, t, pb, sc, oc, out_base, out_cap) ||
+         lean_launch<2, kSigSumMaxI>(sig, s, g, big, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
 }
 
 }  // namespace hsg

@@ -723,6 +723,11 @@ __global__ __launch_bounds__(1024) void k_part_chunks(const uint64_t *bstart, in
     for (int k = 0; k < 16; ++k) t += sw[k];
     chunk_start[nb] = t;
   }
+  // chunk_start[nb + 1]: some bucket is split over several workgroups
+  uint32_t split = 0;
+  for (int b = lo; b < hi; ++b) split |= (bstart[b + 1] - bstart[b]) > chunk;
+  split = __syncthreads_or(split);
+  if (threadIdx.x == 0) chunk_start[nb + 1] = split;
 }
 
 bool part_supported(const Program &prog) { return prog.n_slots <= 8; }
@@ -816,7 +821,8 @@ uint64_t part_lds_entries(const Program &prog, bool big) {
 }
 
 bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, const PartParams &pp, const TwTable &t,
-                     const PartBuffers &pb, uint64_t n, DevScalars *sc, bool maybe_packed) {
+                     const PartBuffers &pb, uint64_t n, DevScalars *sc, bool maybe_packed, const OutCols *out,
+                     uint64_t out_base, uint64_t out_cap) {
   if (!part_supported(prog)) return false;
   const uint64_t nb = 1ull << pp.np_log2;
   hipLaunchKernelGGL(k_part_chunks, dim3(1), dim3(1024), 0, s, pb.bstart, pp.np_log2, pp.chunk, pb.chunk_start,
@@ -824,7 +830,7 @@ bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, cons
   const dim3 g((unsigned)(nb + n / pp.chunk + 1));
   // packed one-window batches of the common slot programs: the lean kernels
   // (k_agg_lean.hip); the general kernel below then only covers the wide layout
-  if (maybe_packed && launch_part_agg_lean(s, g, prog, p, pp, t, pb, sc)) maybe_packed = false;
+  if (maybe_packed && launch_part_agg_lean(s, g, prog, p, pp, t, pb, sc, out, out_base, out_cap)) maybe_packed = false;
   const int W = pp.words;
   if (prog.n_slots <= 2) agg_launch_ms2(s, g, W, maybe_packed, prog, p, pp, t, pb, sc);
   else if (prog.n_slots <= 4) agg_launch_ms4(s, g, W, maybe_packed, prog, p, pp, t, pb, sc);

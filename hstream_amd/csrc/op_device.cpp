@@ -84,7 +84,7 @@ int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog,
   const uint64_t ns = (1ull << kPartMaxLog2) * part_nseg(tiles);
   uint64_t o_hist = take(nh * 4), o_offt = take(nh * 4), o_segsum = take(ns * 4), o_segoff = take((ns + 1) * 8);
   uint64_t o_bstart = take(((1ull << kPartMaxLog2) + 1) * 8), o_part = take((scan_partials_needed(ns) + 8) * 8);
-  uint64_t o_rec = take(n * words * 8), o_chunk = take(((1ull << kPartMaxLog2) + 1) * 4);
+  uint64_t o_rec = take(n * words * 8), o_chunk = take(((1ull << kPartMaxLog2) + 2) * 4);
   uint64_t o_cbk = take(((1ull << kPartMaxLog2) + n / 1024 + 2) * 4);  // >= buckets + n / chunk + 1
   const uint64_t tcap = n * (d.wpr ? d.wpr : 1), nc = touch_chunks(tcap);
   uint64_t o_touch = take(tcap * 4), o_wm = take(n * 8);
@@ -408,7 +408,7 @@ int finish_batch(OpDevice &d, int64_t wm_in, uint64_t n, PushResult &r, std::str
   r.wm_out = n ? s.wm_out : wm_in;
   r.pairs = s.pairs;
   r.late = s.late;
-  r.out_rows = s.out_rows;
+  r.out_rows = s.out_rows + s.scratch[3];  // touched-list emit, or rows the lean apply wrote itself
   r.touched = s.touched;
   r.state_rows = s.live + d.spilled_rows;
   return status_from_err(s.err, err);
@@ -455,7 +455,9 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       if (optimistic) launch_part_decide(d.stream, d.sc, p, a.wm_in, cfg.grace_ms, can_pack, d.part, pp.tiles);
       launch_part_offsets(d.stream, pp, d.part, d.sc);
       launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc, can_pack);
-      launch_part_agg(d.stream, prog, p, pp, d.tw, d.part, kb.n, d.sc, can_pack);
+      const bool emit_batch = cfg.emit_mode == HSG_EMIT_PER_BATCH;
+      launch_part_agg(d.stream, prog, p, pp, d.tw, d.part, kb.n, d.sc, can_pack, emit_batch ? &d.out : nullptr,
+                      a.pending, d.out_cap);
     } else {
       launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, false);
     }
