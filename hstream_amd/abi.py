@@ -137,6 +137,9 @@ class hsg_stats(C.Structure):
         ("spill_events", C.c_uint64),
         ("table_slots", C.c_uint64),
         ("grow_events", C.c_uint64),
+        ("lean_batches", C.c_uint64),
+        ("direct_batches", C.c_uint64),
+        ("replays", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -427,6 +427,9 @@ static int push_sync(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark) {
     op->stats.spill_events = op->dev.spill_events;
     op->stats.table_slots = op->dev.cap;
     op->stats.grow_events = op->dev.grow_events;
+    op->stats.lean_batches = op->dev.lean_batches;
+    op->stats.direct_batches = op->dev.direct_batches;
+    op->stats.replays = op->dev.replays;
     op->stats.pending_rows = op->pending;
     op->stats.last_batch_ms = now_ms() - t0;
     op->stats.agg_kernel_ms += res.agg_ms;

@@ -74,6 +74,9 @@ struct OpDevice {
   int bshift = 0;               // key-hash bits that pick the owner GPU (skipped by local buckets)
   int xpart_log2 = -1;          // owner partition of the fast exchange: log2(ranks), -1 = not a power of two
   bool agg_big = true;          // aggregation variant of the next batch (big LDS table)
+  bool pred_packed = false;     // launch prediction: the last batch was packed (wide variants not launched)
+  bool pred_direct = false;     // launch prediction: the last batch's changelog came from the lean apply
+  uint64_t lean_batches = 0, direct_batches = 0, replays = 0;  // hsg_stats
   // sessions
   SessTable ss = {};
   uint64_t *h_meta = nullptr;     // pinned mirror of ss.meta

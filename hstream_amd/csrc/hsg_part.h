@@ -77,15 +77,16 @@ void launch_part_decide(hipStream_t s, DevScalars *sc, const TwParams &p, int64_
 void launch_part_offsets(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc);
 uint32_t part_nseg(uint64_t tiles);
 // maybe_packed: the batch may be in the packed layout (staged variant too)
+// wide = false: the wide-layout variant is not launched (predicted packed)
 void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp,
                          const int64_t *rec_wm, const int64_t *own_wm, const int64_t *seq, const PartBuffers &pb,
-                         DevScalars *sc, bool maybe_packed);
+                         DevScalars *sc, bool maybe_packed, bool wide = true);
 // returns false when the op's slot count has no LDS variant (caller falls back)
 // maybe_packed: the batch may be in the packed layout (launch both variants)
 // out (per-batch changelog, else null): the lean path may write the rows itself
 bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, const PartParams &pp, const TwTable &t,
                      const PartBuffers &pb, uint64_t n, DevScalars *sc, bool maybe_packed, const OutCols *out,
-                     uint64_t out_base, uint64_t out_cap);
+                     uint64_t out_base, uint64_t out_cap, bool wide = true, bool *lean = nullptr);
 bool part_supported(const Program &prog);
 // Lean aggregation of packed tumbling / unwindowed batches (pane_S = 1, no key
 // rounds, a specialised slot program): records -> LDS table -> group partials
@@ -93,7 +94,9 @@ bool part_supported(const Program &prog);
 // When every group of the batch gets exactly one partial (no bucket split over
 // workgroups, no overflow partial) and out is given, the apply writes the
 // per-batch changelog rows itself (count in sc->scratch[3]) and leaves the
-// touched list empty. Returns false when the batch's shape has no lean variant.
+// touched list empty (sc->scratch[2] = 1; 2 when it filled the touched list
+// instead). Returns false when the batch's shape has no lean variant.
+bool part_lean_eligible(const Program &prog, const PartParams &pp);
 bool launch_part_agg_lean(hipStream_t s, dim3 g, const Program &prog, const TwParams &p, const PartParams &pp,
                           const TwTable &t, const PartBuffers &pb, DevScalars *sc, const OutCols *out,
                           uint64_t out_base, uint64_t out_cap);

@@ -27,7 +27,9 @@
 
 namespace hsg {
 
-constexpr int kLeanProbe = 32;  // LDS probes before a record becomes its own partial
+// The LDS table takes new groups up to 7/8 of its entries (probe sequences
+// stay short: buckets are sized to half a table); past that a record of a new
+// group becomes a partial of its own, so a probe sequence always ends.
 
 // LDS home of (key, window): a 32-bit multiplicative hash (top bits),
 // linear probing
@@ -82,7 +84,7 @@ __global__ __launch_bounds__(NT) void k_agg_lean(PartParams pp, TwTable t, PartB
   constexpr int RB = 4;       // records per thread per block (one block in flight beside it)
   __shared__ uint64_t lkey[E];
   __shared__ int64_t lagg[NS * E];
-  __shared__ uint32_t s_cnt, s_ovf;
+  __shared__ uint32_t s_cnt, s_ovf, s_fill;
   __shared__ uint32_t s_bin[kLeanSortBins];
   __shared__ uint32_t s_wsum[NT / 64];
   if (sc->redo || !sc->packed) return;  // uniform: the careful path / wide variant runs
@@ -111,6 +113,7 @@ __global__ __launch_bounds__(NT) void k_agg_lean(PartParams pp, TwTable t, PartB
   }
   if (threadIdx.x == 0) {
     s_cnt = 0;
+    s_fill = 0;
     s_ovf = 0;
   }
   uint64_t *const pane = pb.pane + r0 * PW;
@@ -149,15 +152,17 @@ __global__ __launch_bounds__(NT) void k_agg_lean(PartParams pp, TwTable t, PartB
       const uint64_t g = ((uint64_t)key << 32) | kw;
       uint32_t h = lean_home<E>(key, kw);
       int e = -1;
-      for (int probe = 0; probe < kLeanProbe; ++probe) {
+      for (int probe = 0; probe < E; ++probe) {
         const uint64_t c = lkey[h];
         if (c == g) {
           e = (int)h;
           break;
         }
         if (c == kEmpty) {
+          if (*(volatile uint32_t *)&s_fill >= (uint32_t)(E - E / 8)) break;  // full: g is not in the table
           const uint64_t old =
               atomicCAS((unsigned long long *)&lkey[h], (unsigned long long)kEmpty, (unsigned long long)g);
+          if (old == kEmpty) atomicAdd(&s_fill, 1u);
           if (old == kEmpty || old == g) {
             e = (int)h;
             break;
@@ -355,6 +360,7 @@ __global__ __launch_bounds__(256) void k_pane_apply(Program rprog, TwParams p, P
     // last workgroup: batch totals (every placed record updates one group)
     sc->scratch[1] = direct ? 0 : total;
     sc->scratch[3] = direct ? total : 0;
+    sc->scratch[2] = direct ? 1 : 2;
     sc->scratch[0] = total;
     sc->pairs = pb.bstart[nb];
   }
@@ -490,13 +496,22 @@ static bool lean_launch(uint64_t sig, hipStream_t s, dim3 g, bool big, const Pro
   return true;
 }
 
+bool part_lean_eligible(const Program &prog, const PartParams &pp) {
+  if (pp.pane_S != 1 || pp.rbits != 0 || pp.has_seq) return false;
+  const uint64_t sig = program_sig(prog);
+  const int W = pp.words - 1;
+  if (W == 1) return sig == kSigCnt;
+  return W == 2 && (sig == kSigAllI || sig == kSigAllF || sig == kSigCnt || sig == kSigCntSumI ||
+                    sig == kSigCntSumF || sig == kSigSumMaxI);
+}
+
 bool launch_part_agg_lean(hipStream_t s, dim3 g, const Program &prog, const TwParams &p, const PartParams &pp,
                           const TwTable &t, const PartBuffers &pb, DevScalars *sc, const OutCols *out,
                           uint64_t out_base, uint64_t out_cap) {
   OutCols oc;
   memset(&oc, 0, sizeof(oc));
   if (out) oc = *out;
-  if (pp.pane_S != 1 || pp.rbits != 0 || pp.has_seq) return false;
+  if (!part_lean_eligible(prog, pp)) return false;
   const int W = pp.words - 1;  // packed words
   const uint64_t sig = program_sig(prog);
   const bool big = pp.big != 0;

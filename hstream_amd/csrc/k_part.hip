@@ -606,7 +606,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
 
 void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const PartParams &pp,
                          const int64_t *rec_wm, const int64_t *own_wm, const int64_t *seq, const PartBuffers &pb,
-                         DevScalars *sc, bool maybe_packed) {
+                         DevScalars *sc, bool maybe_packed, bool wide) {
   if (!pp.tiles) return;
   const dim3 g((unsigned)pp.tiles);
   const bool stage = maybe_packed && !pp.has_seq && pp.words - 1 <= 2;  // packed words <= 2
@@ -616,8 +616,9 @@ void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const
     else
       hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 1>), g, dim3(kPNT), 0, s, b, p, pp, pb, sc);
   }
-  hipLaunchKernelGGL(k_part_scatter<kPartTileRecs>, g, dim3(kPNT), 0, s, b, p, pp, rec_wm, own_wm, seq, pb, sc,
-                     stage ? 1 : 0);
+  if (wide || !stage)
+    hipLaunchKernelGGL(k_part_scatter<kPartTileRecs>, g, dim3(kPNT), 0, s, b, p, pp, rec_wm, own_wm, seq, pb, sc,
+                       stage ? 1 : 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -822,7 +823,8 @@ uint64_t part_lds_entries(const Program &prog, bool big) {
 
 bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, const PartParams &pp, const TwTable &t,
                      const PartBuffers &pb, uint64_t n, DevScalars *sc, bool maybe_packed, const OutCols *out,
-                     uint64_t out_base, uint64_t out_cap) {
+                     uint64_t out_base, uint64_t out_cap, bool wide, bool *lean) {
+  if (lean) *lean = false;
   if (!part_supported(prog)) return false;
   const uint64_t nb = 1ull << pp.np_log2;
   hipLaunchKernelGGL(k_part_chunks, dim3(1), dim3(1024), 0, s, pb.bstart, pp.np_log2, pp.chunk, pb.chunk_start,
@@ -830,7 +832,11 @@ bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, cons
   const dim3 g((unsigned)(nb + n / pp.chunk + 1));
   // packed one-window batches of the common slot programs: the lean kernels
   // (k_agg_lean.hip); the general kernel below then only covers the wide layout
-  if (maybe_packed && launch_part_agg_lean(s, g, prog, p, pp, t, pb, sc, out, out_base, out_cap)) maybe_packed = false;
+  if (maybe_packed && launch_part_agg_lean(s, g, prog, p, pp, t, pb, sc, out, out_base, out_cap)) {
+    maybe_packed = false;
+    if (lean) *lean = true;
+    if (!wide) return true;  // predicted packed: the wide variant is not launched
+  }
   const int W = pp.words;
   if (prog.n_slots <= 2) agg_launch_ms2(s, g, W, maybe_packed, prog, p, pp, t, pb, sc);
   else if (prog.n_slots <= 4) agg_launch_ms4(s, g, W, maybe_packed, prog, p, pp, t, pb, sc);

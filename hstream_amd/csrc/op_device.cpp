@@ -427,6 +427,14 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
   // every later batch instead of the per-record stream-time path.
   const bool opt = d.use_part && !rec_wm && !has_last(prog) && cfg.grace_ms >= 0 && cfg.window_kind != HSG_SESSION;
   const bool need_epoch = !d.h_sc->epoch_set;
+  // Launch prediction (speed only): the variants a batch does not take exit at
+  // once on the device, but each costs a launch. After a packed batch whose
+  // changelog the lean apply wrote itself, the next batch's wide-layout
+  // variants and touched-list emit chain are not launched; a batch that turns
+  // out otherwise is completed after the fetch (wide: run again -- the packed
+  // kernels exited without touching the state; emit: the chain runs on the
+  // touched list the apply left).
+  bool skipped_wide = false, skipped_emit = false;
   auto run = [&](bool optimistic) -> int {
     int rc = clear_batch_scalars(d, err);
     if (rc != HSG_OK) return rc;
@@ -454,20 +462,25 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       const bool can_pack = optimistic && cfg.n_cols <= 8 && d.wpr < 256;
       if (optimistic) launch_part_decide(d.stream, d.sc, p, a.wm_in, cfg.grace_ms, can_pack, d.part, pp.tiles);
       launch_part_offsets(d.stream, pp, d.part, d.sc);
-      launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc, can_pack);
+      skipped_wide = can_pack && d.pred_packed && part_lean_eligible(prog, pp);
+      launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc, can_pack, !skipped_wide);
       const bool emit_batch = cfg.emit_mode == HSG_EMIT_PER_BATCH;
+      bool lean = false;
       launch_part_agg(d.stream, prog, p, pp, d.tw, d.part, kb.n, d.sc, can_pack, emit_batch ? &d.out : nullptr,
-                      a.pending, d.out_cap);
+                      a.pending, d.out_cap, !skipped_wide, &lean);
+      if (!lean) skipped_wide = false;  // the general kernel ran both layouts
+      skipped_emit = emit_batch && lean && d.pred_direct;
     } else {
       launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, false);
     }
     if (has_last(prog)) launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, true);
     if (cfg.emit_mode == HSG_EMIT_PER_BATCH) {
-      if (d.use_part)
-        launch_part_emit(d.stream, d.tw, prog, p, d.part, d.out, a.pending, d.out_cap, d.sc);
-      else
+      if (d.use_part) {
+        if (!skipped_emit) launch_part_emit(d.stream, d.tw, prog, p, d.part, d.out, a.pending, d.out_cap, d.sc);
+      } else {
         launch_tw_emit(d.stream, d.tw, d.cap, prog, p, 0, d.out, a.pending, d.out_cap, d.sc, d.emit,
                        (uint64_t *)&d.sc->out_rows);
+      }
     }
     // ev_a .. ev_b: the batch's device pipeline (aggregation + changelog rows)
     DTRY(hipEventRecord(d.ev_b, d.stream));
@@ -481,12 +494,37 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     rc = run(false);
     if (rc != HSG_OK) return rc;
     rc = finish_batch(d, a.wm_in, kb.n, r, err);
+  } else if (kb.n && skipped_wide && !d.h_sc->packed) {
+    d.pred_packed = false;  // a wide batch: nothing was aggregated, run it with every variant
+    d.replays += 1;
+    rc = run(opt);
+    if (rc != HSG_OK) return rc;
+    rc = finish_batch(d, a.wm_in, kb.n, r, err);
+  }
+  const uint64_t groups = d.h_sc->scratch[0];
+  if (kb.n && d.use_part) {
+    d.pred_packed = d.h_sc->packed != 0;
+    d.pred_direct = d.h_sc->scratch[2] == 1;
+    d.lean_batches += d.h_sc->scratch[2] != 0;
+    d.direct_batches += d.h_sc->scratch[2] == 1;
+  }
+  if (rc == HSG_OK && kb.n && skipped_emit && d.h_sc->scratch[2] != 1 && d.h_sc->scratch[1] != 0) {
+    // the apply filled the touched list: the emit chain that was not launched
+    d.replays += 1;
+    PushResult r1 = r;
+    DTRY(hipMemcpyAsync(&d.sc->scratch[1], &d.h_sc->scratch[1], 8, hipMemcpyHostToDevice, d.stream));
+    d.sc_clean = false;
+    launch_part_emit(d.stream, d.tw, prog, p, d.part, d.out, a.pending, d.out_cap, d.sc);
+    DTRY(hipEventRecord(d.ev_b, d.stream));
+    rc = finish_batch(d, a.wm_in, kb.n, r1, err);
+    r.out_rows = r1.out_rows;
+    if (rc != HSG_OK) return rc;
   }
   if (kb.n) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, d.ev_a, d.ev_b) == hipSuccess) r.agg_ms = ms;
     r.agg_launches = 1;
-    if (d.use_part) adapt_partitions(d, cfg, prog, d.h_sc->scratch[0], kb.n);
+    if (d.use_part) adapt_partitions(d, cfg, prog, groups, kb.n);
   }
   r.touched = cfg.emit_mode == HSG_EMIT_PER_BATCH ? r.out_rows : d.h_sc->scratch[0];
   return rc;

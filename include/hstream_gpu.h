@@ -192,6 +192,10 @@ typedef struct {
   uint64_t table_slots;       /* HBM hash-table slots (time windows) / key-table slots
                                  (sessions) now                                          */
   uint64_t grow_events;       /* times the HBM table was rebuilt larger                   */
+  uint64_t lean_batches;      /* batches aggregated by the lean one-window path            */
+  uint64_t direct_batches;    /* ... whose changelog rows the lean apply wrote itself      */
+  uint64_t replays;           /* batches completed after the fetch because the predicted
+                                 kernel variants did not match the batch (speed only)     */
 } hsg_stats;
 
 /* Completion callback of hsg_push_batch_async: rc is what hsg_push_batch

@@ -1,0 +1,101 @@
+"""GPU parity of the lean one-window path (k_agg_lean.hip) across batch-shape
+transitions: the host predicts from the previous batch which kernel variants
+to launch (packed layout, changelog written by the apply), and a batch that
+turns out otherwise is completed after the fetch. Each batch's changelog and
+the final state are compared with the CPU oracle (TimeWindowedStream.hs:86-103
+per (key, window) group)."""
+import numpy as np
+import pytest
+
+import pyoracle
+from hstream_amd import abi, datagen
+from hstream_amd.columnar import OpSpec
+from util import rows_equal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need cuda:0"
+    from hstream_amd.engine import Engine
+    e = Engine(device=0, batch_capacity=1 << 22)
+    yield e
+    e.close()
+
+
+def _uniform(rng, n, nkeys, t0, span):
+    key = rng.integers(0, nkeys, size=n).astype(np.uint32)
+    ts = (t0 + np.sort(rng.integers(0, span, size=n))).astype(np.int64)
+    return key, ts, [rng.integers(-10**9, 10**9, size=n, dtype=np.int64)]
+
+
+def _batches(seed):
+    """uniform (direct changelog) -> hot key (a bucket split over workgroups:
+    touched list) -> a span of > 2^16 windows (wide layout) -> uniform ->
+    many fresh groups at once (LDS overflow partials) -> uniform."""
+    rng = np.random.default_rng(seed)
+    out = []
+    t = 10_000_000
+    out.append(_uniform(rng, 300_000, 2_000, t, 600_000))
+    t += 600_000
+    k, ts, c = _uniform(rng, 200_000, 2_000, t, 600_000)
+    k[rng.random(len(k)) < 0.8] = 7  # ~160K records of one key: its bucket exceeds a workgroup's chunk
+    out.append((k, ts, c))
+    t += 600_000
+    out.append(_uniform(rng, 100_000, 500, t, 2_000_000_000))  # 10 s windows over 23 days
+    t += 2_000_000_000
+    out.append(_uniform(rng, 300_000, 2_000, t, 600_000))
+    t += 600_000
+    out.append(_uniform(rng, 400_000, 400_000, t, 6_000_000))  # ~10x the groups the sizing expects
+    t += 6_000_000
+    out.append(_uniform(rng, 300_000, 2_000, t, 600_000))
+    return out
+
+
+@pytest.mark.parametrize("aggs", [datagen.C_AGGS_FULL, [(abi.HSG_SUM, 0), (abi.HSG_MAX, 0)]],
+                         ids=["count_sum_avg_min_max", "sum_max"])
+def test_lean_shape_transitions(eng, aggs):
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=10_000, col_types=[abi.HSG_I64], aggs=aggs,
+                  state_capacity=1 << 20)
+    g, o = eng.op(spec), pyoracle.OracleOp(spec)
+    f64 = spec.agg_is_f64()
+    wg = wo = -1
+    for bi, (key, ts, cols) in enumerate(_batches(5)):
+        wg = g.push(key, ts, cols, None, watermark=wg)
+        wo = o.push(key, ts, cols, None, watermark=wo)
+        assert wg == wo, f"batch {bi}: watermark {wg} != {wo}"
+        rows_equal(g.drain(), o.drain(), f64, what=f"changelog batch {bi}")
+    rows_equal(g.dump_state(), o.dump_state(), f64, what="state dump")
+    st = g.stats()
+    # the transitions took the paths they are meant to: lean batches, direct
+    # changelogs, and replays of the emit chain (the hot-key and the
+    # overflowing batch, each after a direct one)
+    assert st["lean_batches"] >= 4 and st["direct_batches"] >= 3, st
+    assert st["replays"] >= 2, st
+    g.close()
+    o.close()
+
+
+def test_lean_late_batch_after_prediction(eng):
+    """A batch with records beyond the grace (careful path) between lean
+    batches: the prediction must not skip kernels the careful path needs."""
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=10_000, col_types=[abi.HSG_I64],
+                  aggs=datagen.C_AGGS_FULL, state_capacity=1 << 20)
+    rng = np.random.default_rng(9)
+    g, o = eng.op(spec), pyoracle.OracleOp(spec)
+    wg = wo = -1
+    t = 50_000_000
+    for bi in range(5):
+        key, ts, cols = _uniform(rng, 200_000, 3_000, t, 300_000)
+        if bi == 3:
+            ts[::50] -= abi.HSG_DEFAULT_GRACE_MS + 400_000  # late by more than the grace
+        t += 300_000
+        wg = g.push(key, ts, cols, None, watermark=wg)
+        wo = o.push(key, ts, cols, None, watermark=wo)
+        assert wg == wo
+        rows_equal(g.drain(), o.drain(), spec.agg_is_f64(), what=f"changelog batch {bi}")
+    rows_equal(g.dump_state(), o.dump_state(), spec.agg_is_f64(), what="state dump")
+    g.close()
+    o.close()
