@@ -295,7 +295,10 @@ def pipeline_name(cfg, emit):
         return "session merge (k_ss_phist, offsets, k_ss_pscatter, k_ss_sort, k_ss_apply)"
     if emit == "per_record":
         return "per-record changelog (k_pr_count, k_pr_expand, radix sort, k_seg_*)"
-    return "batch pipeline (k_part_hist_opt, offsets, k_part_scatter_st, k_part_agg, k_touch_emit)"
+    if cfg.window_kind in (abi.HSG_TUMBLING, abi.HSG_UNWINDOWED):
+        return ("batch pipeline (k_part_hist_opt, offsets + decide, k_part_scatter_st, k_agg_lean, "
+                "k_pane_apply writing the changelog rows)")
+    return "batch pipeline (k_part_hist_opt, offsets + decide, k_part_scatter_st, k_part_agg, k_touch_emit)"
 
 
 def committed_traffic(args, world):

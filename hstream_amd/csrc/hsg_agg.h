@@ -250,6 +250,7 @@ __device__ inline void direct_windows(const PG &prog, const TwParams &p, const T
   int64_t v[MS];
 #pragma unroll
   for (int s = 0; s < MS; ++s) v[s] = s < prog.n() ? prec_elem(prog, s, r) : 0;
+  atomicOr((unsigned int *)&sc->scratch[5], 1u);  // updated in-kernel: the batch is not clean
   for (uint32_t w = w0;; ++w) {
     touch_append(pb, sc, flush_window<MS>(prog, p, t, ((uint64_t)key << 32) | w, v, false, fresh, err), err);
     if (w == w1) break;
@@ -335,6 +336,9 @@ struct AggLds {
   uint32_t fill, nl, b, c0, c1, maxb;
   uint32_t wsum[NT / 64];
   uint64_t base;
+  uint64_t pbase;        // deferred flush: first pane entry of this flush
+  uint32_t nseg, dnow;   // deferred segments so far; this flush is deferred
+  uint32_t pcnt;         // deferred entries of this workgroup
   uint64_t red[2][NT / 64];
   PaneGroup<MS, E> pg;
 };
@@ -430,7 +434,8 @@ __device__ inline void group_live(AggLds<MS, E, NT> &L, uint32_t nl) {
 template <int MS, int E, int NT, class PG>
 __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const PG &prog, const TwParams &p, const TwTable &t,
                               const PartBuffers &pb, DevScalars *sc, int S, bool exclusive, bool plain_claim,
-                              uint32_t skip, int cnt_all_slot, uint32_t &fresh, uint32_t &err, uint64_t &t_sort) {
+                              uint32_t skip, int cnt_all_slot, uint32_t &fresh, uint32_t &err, uint64_t &t_sort,
+                              bool defer) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t SW = S ? (uint32_t)S : 1u;
   const uint64_t t0 = wall_clock64();
@@ -472,9 +477,30 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const PG &pr
     if (k < wv) o += L.wsum[k];
     total += L.wsum[k];
   }
-  if (threadIdx.x == 0) L.base = total ? atomicAdd((unsigned long long *)&sc->scratch[1], (unsigned long long)total) : 0;
+  if (threadIdx.x == 0) {
+    // deferred to k_seg_apply when this workgroup owns the bucket and the
+    // segment fits; else updated here, with touched-list entries
+    uint32_t df = 0;
+    uint64_t pb0 = 0;
+    if (defer && total && L.nseg < (uint32_t)kMaxSeg) {
+      pb0 = atomicAdd((unsigned long long *)&sc->scratch[4], (unsigned long long)total);
+      df = pb0 + total <= pb.pane_cap;
+    }
+    if (df) {
+      pb.seg[((uint64_t)blockIdx.x * kMaxSeg + L.nseg) * 2] = pb0;
+      pb.seg[((uint64_t)blockIdx.x * kMaxSeg + L.nseg) * 2 + 1] = total;
+      L.nseg += 1;
+      L.pcnt += (uint32_t)total;
+    } else if (total) {
+      atomicOr((unsigned int *)&sc->scratch[5], 1u);  // updated in-kernel: the batch is not clean
+    }
+    L.dnow = df;
+    L.pbase = pb0;
+    L.base = total && !df ? atomicAdd((unsigned long long *)&sc->scratch[1], (unsigned long long)total) : 0;
+  }
   __syncthreads();
-  o += L.base;
+  const bool dnow = L.dnow != 0;
+  const uint64_t pw = 1 + (uint64_t)prog.n();  // pane entry words
   for (uint32_t q = threadIdx.x; q < nl; q += NT) {
     const int e = L.live[q];
     const uint64_t g = L.key[e];
@@ -504,9 +530,18 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const PG &pr
         for (int s = 0; s < MS; ++s)
           if ((skip >> s) & 1u) v[s] = v[cnt_all_slot];
       }
-      const uint32_t sl = flush_window<MS>(prog, p, t, kb | w, v, exclusive, fresh, err, plain_claim);
-      if (o < pb.touched_cap) pb.touched[o] = sl;
-      else err |= ERR_OOM;
+      if (dnow) {
+        // the window's update for k_seg_apply: [g][slot 0 .. n-1]
+        uint64_t *ent = pb.pane + (L.pbase + o) * pw;
+        ent[0] = kb | w;
+#pragma unroll
+        for (int s = 0; s < MS; ++s)
+          if (s < prog.n()) ent[1 + s] = (uint64_t)v[s];
+      } else {
+        const uint32_t sl = flush_window<MS>(prog, p, t, kb | w, v, exclusive, fresh, err, plain_claim);
+        if (L.base + o < pb.touched_cap) pb.touched[L.base + o] = sl;
+        else err |= ERR_OOM;
+      }
       ++o;
       if (w == P) break;
       ++top;
@@ -548,6 +583,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     L.c1 = chunk_start[bk + 1];
     L.fill = 0;
     L.nl = 0;
+    L.nseg = 0;
+    L.pcnt = 0;
   }
   for (int e = threadIdx.x; e < E; e += NT) {
     L.key[e] = kEmpty;
@@ -563,6 +600,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   // the bucket's table regions are this workgroup's alone (hsg_tw.h)
   const bool plain_claim = exclusive && pp.np_log2 <= t.rbits && pp.bshift == t.bshift;
   const uint64_t r0 = b0 + c * pp.chunk, r1 = r0 + pp.chunk < b1 ? r0 + pp.chunk : b1;
+  // window updates of a bucket this workgroup owns go to k_seg_apply
+  const bool defer = pp.defer && exclusive;
   const uint32_t limit = (uint32_t)(E * 3 / 4);
   const int W = PK ? pp.words - 1 : pp.words;  // words per record in memory
   const int C = pp.words - 2 - pp.has_seq;
@@ -662,7 +701,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         // table full with records left: flush and go on (the records are
         // loaded again afterwards, so they hold no registers across the flush)
         groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, plain_claim, skip, cnt_all_slot, fresh, err,
-                                   t_sort);
+                                   t_sort, defer);
+        // a mid-round flush: a group may be updated again later in the batch
+        if (threadIdx.x == 0) atomicOr((unsigned int *)&sc->scratch[5], 1u);
         ++flushes;
         load();
         ta = wall_clock64();
@@ -685,7 +726,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
     const uint64_t tb = wall_clock64();
     groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, plain_claim, skip, cnt_all_slot, fresh, err,
-                                   t_sort);
+                                   t_sort, defer);
     ++flushes;
     t_flush += wall_clock64() - tb;
   }
@@ -699,6 +740,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   if (err) atomicOr(&sc->err, err);
   __syncthreads();
   if (threadIdx.x == 0) {
+    // the deferred segments of this workgroup (k_seg_apply)
+    pb.pane_info[2 * blockIdx.x] = L.nseg;
+    pb.pane_cnt[blockIdx.x] = L.pcnt;
     uint64_t a = 0, f = 0;
     for (int k = 0; k < NT / 64; ++k) {
       a += L.red[0][k];

@@ -12,6 +12,7 @@ constexpr int kPartMaxLog2 = 11;                      // up to 2048 partitions
 constexpr int kPartMaxWords = 11;                     // 2 + 8 columns + seq
 constexpr uint64_t kTouchChunk = 4096;                // touched-list entries per emit workgroup
 constexpr uint32_t kTouchSkip = 0xFFFFFFFFu;           // touched-list entry of a later update of a group
+constexpr int kMaxSeg = 8;                            // deferred flush segments per aggregation workgroup
 
 // A partitioned record is `words` 8-byte words (wide layout):
 //   [key | krel << 32] [nwin | valid bits << 32] [col 0 .. C-1] [seq + 1]?
@@ -41,6 +42,8 @@ struct PartBuffers {
                           // workgroup's entries at its chunk's record range
   uint64_t *pane_info;    // [workgroups][2]: first entry, entry count | overflow flag << 32
   uint32_t *pane_cnt;     // [workgroups] entry counts, dense (the apply's touched-list prefix)
+  uint64_t *seg;          // [workgroups][kMaxSeg][2] general kernel: deferred flush segments (first entry, count)
+  uint64_t pane_cap;      // entries pb.pane holds
   uint64_t n_cap;
 };
 
@@ -54,7 +57,7 @@ struct PartParams {
   int32_t rbits;      // aggregation: 2^rbits key-hash rounds per sub-chunk
   int32_t big;        // aggregation variant: 1 = big LDS table, 1024 threads
   int32_t bshift;     // owner bits above the bucket bits in the key hash (multi-GPU, power-of-two ranks)
-  int32_t reserved;
+  int32_t defer;      // aggregation: window updates of exclusive buckets go to pb.pane segments (k_seg_apply)
   uint64_t tiles;     // partition-pass tiles of this batch
   uint64_t chunk;     // records per aggregation workgroup
 };
@@ -75,6 +78,9 @@ void launch_part_decide(hipStream_t s, DevScalars *sc, const TwParams &p, int64_
                         bool can_pack, const PartBuffers &pb, uint64_t tiles);
 // bucket-major run offsets (offt, bstart) from the tile-major histogram
 void launch_part_offsets(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc);
+// launch_part_decide + launch_part_offsets in the launches of the offsets
+void launch_part_decide_offsets(hipStream_t s, DevScalars *sc, const TwParams &p, int64_t wm_in, int64_t grace,
+                                bool can_pack, const PartParams &pp, const PartBuffers &pb);
 uint32_t part_nseg(uint64_t tiles);
 // maybe_packed: the batch may be in the packed layout (staged variant too)
 // wide = false: the wide-layout variant is not launched (predicted packed)
@@ -95,8 +101,15 @@ bool part_supported(const Program &prog);
 // workgroups, no overflow partial) and out is given, the apply writes the
 // per-batch changelog rows itself (count in sc->scratch[3]) and leaves the
 // touched list empty (sc->scratch[2] = 1; 2 when it filled the touched list
-// instead). Returns false when the batch's shape has no lean variant.
+// instead; k_seg_apply: 3 / 4). Returns false when the batch's shape has no lean variant.
 bool part_lean_eligible(const Program &prog, const PartParams &pp);
+// After the general aggregation kernel with pp.defer: its deferred window
+// updates into the HBM table (one workgroup per aggregation workgroup, its
+// segments in order), per-batch changelog rows written directly when the
+// batch is clean (every window updated once, no split bucket).
+void launch_seg_apply(hipStream_t s, dim3 g, const Program &prog, const TwParams &p, const PartParams &pp,
+                      const TwTable &t, const PartBuffers &pb, DevScalars *sc, const OutCols *out, uint64_t out_base,
+                      uint64_t out_cap, bool lean);
 bool launch_part_agg_lean(hipStream_t s, dim3 g, const Program &prog, const TwParams &p, const PartParams &pp,
                           const TwTable &t, const PartBuffers &pb, DevScalars *sc, const OutCols *out,
                           uint64_t out_base, uint64_t out_cap);

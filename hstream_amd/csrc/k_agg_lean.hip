@@ -481,6 +481,199 @@ __global__ __launch_bounds__(256) void k_pane_apply(Program rprog, TwParams p, P
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_seg_apply: the general kernel's deferred window updates (hsg_agg.h
+// agg_flush with pp.defer), one workgroup per aggregation workgroup, its
+// segments in flush order. Only a bucket's own workgroup defers, so the
+// groups are this workgroup's alone: plain read-modify-write; a later segment
+// may update a group an earlier one did (a mid-round flush), hence the
+// barrier between segments and L2-served (agent-scope) key and row loads.
+// Touched-list entries go after the ones the aggregation kernel appended
+// itself (sc->scratch[1]); the list length is left in sc->scratch[6]. A clean
+// batch (every window updated once: no split bucket, no in-kernel update, no
+// mid-round flush, no LAST) gets its changelog rows here instead.
+// ---------------------------------------------------------------------------
+constexpr int kSegClaimSet = 16384;  // claims per workgroup up to half of it (else workgroup-scope CAS)
+__device__ inline bool seg_claim_insert(uint32_t *cset, uint32_t slot) {
+  uint32_t h = (slot * 0x9E3779B1u) >> (32 - 14);
+  for (int probe = 0; probe < kSegClaimSet; ++probe) {
+    const uint32_t old = atomicCAS(&cset[h], 0u, slot + 1u);
+    if (old == 0u) return true;
+    if (old == slot + 1u) return false;
+    h = (h + 1) & (kSegClaimSet - 1);
+  }
+  return false;
+}
+
+__device__ inline int64_t tw_claim_seg(const TwTable &t, uint64_t g, uint32_t *cset, uint32_t &fresh) {
+  const uint64_t base = tw_region_base(t, g);
+  uint64_t s = tw_home_in(t, g);
+  const uint64_t step = tw_step(t), n = (t.rmask + 1) / step;
+  for (uint64_t probe = 0; probe < n && probe < kMaxProbes; ++probe) {
+    const uint64_t cur = __hip_atomic_load(t.key(base + s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == g) return (int64_t)(base + s);
+    if (cur == kEmpty && seg_claim_insert(cset, (uint32_t)(base + s))) {
+      *t.key(base + s) = g;
+      fresh += 1;
+      return (int64_t)(base + s);
+    }
+    s = (s + step) & t.rmask;
+  }
+  return -1;
+}
+
+template <int MS>
+__global__ __launch_bounds__(1024) void k_seg_apply(Program prog, TwParams p, PartParams pp, TwTable t, PartBuffers pb,
+                                                    OutCols out, uint64_t out_base, uint64_t out_cap, int lean,
+                                                    DevScalars *sc) {
+  constexpr int NT = 1024;
+  __shared__ uint64_t s_red[NT / 64], s_tot[NT / 64];
+  __shared__ uint32_t cset[kSegClaimSet];
+  if (sc->redo || (lean && sc->packed)) return;  // uniform: late batch / the lean kernels took it
+  uint32_t b;
+  uint64_t r0, r1;
+  bool exclusive;
+  if (!lean_chunk(pp, pb, b, r0, r1, exclusive)) return;  // uniform
+  const ProgRT pg(prog);
+  const int ns = prog.n_slots;
+  const uint64_t pw = 1 + (uint64_t)ns;
+  const uint32_t nseg = (uint32_t)pb.pane_info[2 * blockIdx.x];
+  const uint32_t mine = pb.pane_cnt[blockIdx.x];
+  const bool plain_claim = pp.np_log2 <= t.rbits && pp.bshift == t.bshift;
+  const bool lds_claim = plain_claim && mine <= kSegClaimSet / 2 && t.mask < 0xFFFFFFFFull;
+  if (lds_claim)
+    for (int k = threadIdx.x; k < kSegClaimSet; k += NT) cset[k] = 0;
+  // every workgroup's deferred count: this one's position and the total
+  const int nb = 1 << pp.np_log2;
+  const uint32_t nch = pb.chunk_start[nb];
+  uint64_t before = 0, total = 0;
+  for (uint32_t k = threadIdx.x; k < nch; k += NT) {
+    const uint64_t c = pb.pane_cnt[k];
+    total += c;
+    if (k < blockIdx.x) before += c;
+  }
+  before = wave_sum_u64(before);
+  total = wave_sum_u64(total);
+  if ((threadIdx.x & 63) == 0) {
+    s_red[threadIdx.x >> 6] = before;
+    s_tot[threadIdx.x >> 6] = total;
+  }
+  __syncthreads();
+  before = total = 0;
+  for (int k = 0; k < NT / 64; ++k) {
+    before += s_red[k];
+    total += s_tot[k];
+  }
+  bool has_last = false;
+  for (int s = 0; s < ns; ++s) has_last |= prog.slot_op[s] == S_LAST_SEQ;
+  const bool direct = out.key != nullptr && pb.chunk_start[nb + 1] == 0 && sc->scratch[5] == 0 && !has_last;
+  const uint64_t t0 = sc->scratch[1];  // touched entries the aggregation kernel appended itself
+  if (threadIdx.x == 0 && blockIdx.x + 1 == nch) {
+    sc->scratch[6] = direct ? 0 : t0 + total;
+    if (direct) sc->scratch[3] = total;
+    sc->scratch[2] = direct ? 3 : 4;
+  }
+  const uint32_t bid = (uint32_t)p.batch_id;
+  const int64_t k_epoch = sc->k_epoch;
+  uint32_t fresh = 0, err = 0;
+  uint64_t run = before;
+  for (uint32_t sg = 0; sg < nseg; ++sg) {
+    const uint64_t base = pb.seg[((uint64_t)blockIdx.x * kMaxSeg + sg) * 2];
+    const uint64_t cnt = pb.seg[((uint64_t)blockIdx.x * kMaxSeg + sg) * 2 + 1];
+    for (uint64_t q = threadIdx.x; q < cnt; q += NT) {
+      const uint64_t *ent = pb.pane + (base + q) * pw;
+      const uint64_t g = ent[0];
+      int64_t v[MS];
+#pragma unroll
+      for (int s = 0; s < MS; ++s) v[s] = s < ns ? (int64_t)ent[1 + s] : 0;
+      const uint32_t f0 = fresh;
+      const int64_t slot = lds_claim     ? tw_claim_seg(t, g, cset, fresh)
+                           : plain_claim ? tw_claim_exclusive(t, g, fresh)
+                                         : tw_find_or_insert(t, g, fresh);
+      uint32_t tl = kTouchSkip;
+      if (slot < 0) {
+        err |= ERR_OOM;
+      } else {
+        int64_t *row = t.aggs(slot);
+        uint32_t *stp = t.stamp(slot);
+        bool first = true;
+        if (fresh == f0) {
+          int64_t c[MS];
+#pragma unroll
+          for (int s = 0; s < MS; ++s)
+            c[s] = s < ns ? __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+          const uint32_t st = __hip_atomic_load(stp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+          for (int s = 0; s < MS; ++s) {
+            if (s >= ns) break;
+            const int op = pg.op(s);
+            if (op == S_LAST_VAL) continue;
+            v[s] = op == S_LAST_SEQ ? ((uint64_t)v[s] > (uint64_t)c[s] ? v[s] : c[s]) : slot_combine(op, c[s], v[s]);
+          }
+          first = st != bid;
+        }
+#pragma unroll
+        for (int s = 0; s < MS; ++s)
+          if (s < ns && pg.op(s) != S_LAST_VAL) row[s] = v[s];
+        if (first) *stp = bid;
+        if (direct) {
+          const uint64_t o = out_base + run + q;
+          if (o < out_cap) {
+            out.key[o] = (uint32_t)(g >> 32);
+            int64_t ws = 0, we = 0;
+            if (p.kind != HSG_UNWINDOWED) {
+              const int64_t k = k_epoch + (int64_t)(g & 0xFFFFFFFFull);
+              ws = (int64_t)((uint64_t)k * (uint64_t)p.adv);
+              we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
+            }
+            out.ws[o] = ws;
+            out.we[o] = we;
+            out.src[o] = -1;
+            for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value_reg<MS>(prog, j, v);
+          } else {
+            err |= ERR_OOM;
+          }
+          continue;
+        }
+        if (first) tl = (uint32_t)slot;
+      }
+      if (!direct) {
+        const uint64_t o = t0 + run + q;
+        if (o < pb.touched_cap) pb.touched[o] = tl;
+        else err |= ERR_OOM;
+      }
+    }
+    run += cnt;
+    __syncthreads();  // the next segment may update this one's groups
+  }
+  if (err) atomicOr(&sc->err, err);
+  const uint64_t fr = wave_sum_u64(fresh);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = fr;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t f = 0;
+    for (int k = 0; k < NT / 64; ++k) f += s_red[k];
+    if (f) atomicAdd((unsigned long long *)&sc->live_x[blockIdx.x & 7], (unsigned long long)f);
+  }
+}
+
+void launch_seg_apply(hipStream_t s, dim3 g, const Program &prog, const TwParams &p, const PartParams &pp,
+                      const TwTable &t, const PartBuffers &pb, DevScalars *sc, const OutCols *out, uint64_t out_base,
+                      uint64_t out_cap, bool lean) {
+  OutCols oc;
+  memset(&oc, 0, sizeof(oc));
+  if (out) oc = *out;
+  const int l = lean ? 1 : 0;
+  if (prog.n_slots <= 2)
+    hipLaunchKernelGGL((k_seg_apply<2>), g, dim3(1024), 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
+  else if (prog.n_slots <= 4)
+    hipLaunchKernelGGL((k_seg_apply<4>), g, dim3(1024), 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
+  else if (prog.n_slots <= 6)
+    hipLaunchKernelGGL((k_seg_apply<6>), g, dim3(1024), 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
+  else
+    hipLaunchKernelGGL((k_seg_apply<8>), g, dim3(1024), 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
+}
+
 template <int W, uint64_t SIG>
 static bool lean_launch(uint64_t sig, hipStream_t s, dim3 g, bool big, const Program &prog, const TwParams &p,
                         const PartParams &pp, const TwTable &t, const PartBuffers &pb, DevScalars *sc,

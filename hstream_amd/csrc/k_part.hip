@@ -17,6 +17,8 @@
 // Window assignment and grace follow TimeWindowedStream.hs:86-103 / :105-117
 // exactly as in k_window.hip (rejected windows are always the earliest ones, so
 // the accepted windows of a record are one consecutive run).
+#include <cstring>
+
 #include "hsg_dev.h"
 #include "hsg_part.h"
 #include "hsg_sort.h"
@@ -437,8 +439,17 @@ void launch_part_hist(hipStream_t s, const Batch &b, const TwParams &p, const Pa
 // kernel of the batch exits and the host runs the batch again carefully.
 // Also picks the packed record layout when every record's first window lies
 // within 2^16 windows of the batch's earliest (kbase).
-__global__ __launch_bounds__(256) void k_part_decide(DevScalars *sc, TwParams p, int64_t wm_in, int64_t grace,
-                                                    int can_pack, const uint64_t *__restrict__ text, uint64_t tiles) {
+struct DecideArgs {
+  TwParams p;
+  int64_t wm_in, grace;
+  int can_pack, on;
+  const uint64_t *text;
+  uint64_t tiles;
+};
+
+// 256 threads of one workgroup
+__device__ inline void part_decide_body(DevScalars *sc, const TwParams &p, int64_t wm_in, int64_t grace, int can_pack,
+                                        const uint64_t *__restrict__ text, uint64_t tiles) {
   __shared__ uint64_t sred[2][4];
   uint64_t tx = 0, tn = 0;
   for (uint64_t t = threadIdx.x; t < tiles; t += 256) {
@@ -488,9 +499,38 @@ __global__ __launch_bounds__(256) void k_part_decide(DevScalars *sc, TwParams p,
   sc->kbase = kb;
 }
 
+__global__ __launch_bounds__(256) void k_part_decide(DevScalars *sc, DecideArgs a) {
+  part_decide_body(sc, a.p, a.wm_in, a.grace, a.can_pack, a.text, a.tiles);
+}
+
+static DecideArgs decide_args(const TwParams &p, int64_t wm_in, int64_t grace, bool can_pack, const PartBuffers &pb,
+                              uint64_t tiles) {
+  DecideArgs a;
+  memset(&a, 0, sizeof(a));
+  a.p = p;
+  a.wm_in = wm_in;
+  a.grace = grace;
+  a.can_pack = can_pack ? 1 : 0;
+  a.on = 1;
+  a.text = pb.text;
+  a.tiles = tiles;
+  return a;
+}
+
 void launch_part_decide(hipStream_t s, DevScalars *sc, const TwParams &p, int64_t wm_in, int64_t grace,
                         bool can_pack, const PartBuffers &pb, uint64_t tiles) {
-  hipLaunchKernelGGL(k_part_decide, dim3(1), dim3(256), 0, s, sc, p, wm_in, grace, can_pack ? 1 : 0, pb.text, tiles);
+  hipLaunchKernelGGL(k_part_decide, dim3(1), dim3(256), 0, s, sc, decide_args(p, wm_in, grace, can_pack, pb, tiles));
+}
+
+void launch_part_offsets(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc,
+                         const DecideArgs *da);
+void launch_part_offsets(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc) {
+  launch_part_offsets(s, pp, pb, sc, nullptr);
+}
+void launch_part_decide_offsets(hipStream_t s, DevScalars *sc, const TwParams &p, int64_t wm_in, int64_t grace,
+                                bool can_pack, const PartParams &pp, const PartBuffers &pb) {
+  const DecideArgs a = decide_args(p, wm_in, grace, can_pack, pb, pp.tiles);
+  launch_part_offsets(s, pp, pb, sc, &a);
 }
 
 // Staged scatter for packed records of <= 2 words (<= 1 column, no LAST): the
@@ -634,10 +674,17 @@ constexpr uint64_t kColSeg = 256;
 
 uint32_t part_nseg(uint64_t tiles) { return (uint32_t)((tiles + kColSeg - 1) / kColSeg); }
 
+// The extra column of workgroups (blockIdx.x == gridDim.x - 1) is the decide
+// step of an optimistic batch (one launch fewer); the column sums do not
+// depend on it (a batch found late is run again from the start).
 __global__ __launch_bounds__(256) void k_part_colsum(const uint32_t *__restrict__ hist, uint64_t tiles, int nb,
-                                                     uint32_t nseg, uint32_t *__restrict__ segsum, const DevScalars *sc) {
+                                                     uint32_t nseg, uint32_t *__restrict__ segsum, DevScalars *sc,
+                                                     DecideArgs da) {
   __shared__ uint32_t red[4][64];
-  if (sc->redo) return;
+  if (blockIdx.x == gridDim.x - 1) {
+    if (da.on && blockIdx.y == 0) part_decide_body(sc, da.p, da.wm_in, da.grace, da.can_pack, da.text, da.tiles);
+    return;
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int b = blockIdx.x * 64 + lane;
   const uint64_t t0 = (uint64_t)blockIdx.y * kColSeg, t1 = t0 + kColSeg < tiles ? t0 + kColSeg : tiles;
@@ -675,12 +722,16 @@ __global__ __launch_bounds__(256) void k_part_colscan(const uint32_t *__restrict
   if (blockIdx.y == 0 && w == 0) bstart[b] = segoff[(uint64_t)b * nseg];
 }
 
-void launch_part_offsets(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc) {
+void launch_part_offsets(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc,
+                         const DecideArgs *da) {
   if (!pp.tiles) return;
   const int nb = 1 << pp.np_log2;
   const uint32_t nseg = part_nseg(pp.tiles);
   const dim3 g((unsigned)((nb + 63) / 64), nseg);
-  hipLaunchKernelGGL(k_part_colsum, g, dim3(256), 0, s, pb.hist, pp.tiles, nb, nseg, pb.segsum, sc);
+  DecideArgs off;
+  memset(&off, 0, sizeof(off));
+  hipLaunchKernelGGL(k_part_colsum, dim3(g.x + 1, g.y), dim3(256), 0, s, pb.hist, pp.tiles, nb, nseg, pb.segsum, sc,
+                     da ? *da : off);
   scan_excl_u32(s, pb.segsum, pb.segoff, (uint64_t)nb * nseg, pb.partial, pb.bstart + nb);
   hipLaunchKernelGGL(k_part_colscan, g, dim3(256), 0, s, pb.hist, pp.tiles, nb, nseg, pb.segoff, pb.offt, pb.bstart,
                      sc);
@@ -691,14 +742,18 @@ void launch_part_offsets(hipStream_t s, const PartParams &pp, const PartBuffers 
 // (a bucket of more than `chunk` records is split over several workgroups)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_part_chunks(const uint64_t *bstart, int np_log2, uint64_t chunk,
-                                                      uint32_t *chunk_start, uint32_t *chunk_bucket) {
+                                                      uint32_t *chunk_start, uint32_t *chunk_bucket,
+                                                      const DevScalars *sc) {
   __shared__ uint32_t sw[16];
+  // a batch found late (the optimistic decide) has no fresh bucket starts:
+  // every aggregation kernel exits too
+  if (sc->redo) return;
   const int nb = 1 << np_log2;
   const int per = (nb + 1023) / 1024;
   const int lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
   uint32_t loc = 0;
   for (int b = lo; b < hi; ++b) {
-    uint64_t sz = bstart[b + 1] - bstart[b];
+    const uint64_t sz = bstart[b + 1] > bstart[b] ? bstart[b + 1] - bstart[b] : 0;
     loc += (uint32_t)((sz + chunk - 1) / chunk);
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -714,7 +769,7 @@ __global__ __launch_bounds__(1024) void k_part_chunks(const uint64_t *bstart, in
   for (int k = 0; k < w; ++k) run += sw[k];
   for (int b = lo; b < hi; ++b) {
     chunk_start[b] = run;
-    uint64_t sz = bstart[b + 1] - bstart[b];
+    const uint64_t sz = bstart[b + 1] > bstart[b] ? bstart[b + 1] - bstart[b] : 0;
     const uint32_t k = (uint32_t)((sz + chunk - 1) / chunk);
     for (uint32_t q = 0; q < k; ++q) chunk_bucket[run + q] = (uint32_t)b;
     run += k;
@@ -726,7 +781,7 @@ __global__ __launch_bounds__(1024) void k_part_chunks(const uint64_t *bstart, in
   }
   // chunk_start[nb + 1]: some bucket is split over several workgroups
   uint32_t split = 0;
-  for (int b = lo; b < hi; ++b) split |= (bstart[b + 1] - bstart[b]) > chunk;
+  for (int b = lo; b < hi; ++b) split |= bstart[b + 1] > bstart[b] + chunk;
   split = __syncthreads_or(split);
   if (threadIdx.x == 0) chunk_start[nb + 1] = split;
 }
@@ -740,7 +795,7 @@ bool part_supported(const Program &prog) { return prog.n_slots <= 8; }
 __global__ __launch_bounds__(256) void k_touch_count(const uint32_t *__restrict__ touched, const DevScalars *sc,
                                                      uint64_t cap, uint32_t *__restrict__ cnt) {
   __shared__ uint64_t sw[4];
-  uint64_t n = sc->scratch[1];
+  uint64_t n = sc->scratch[6] ? sc->scratch[6] : sc->scratch[1];  // after k_seg_apply: [6]
   if (n > cap) n = cap;
   const uint64_t c0 = (uint64_t)blockIdx.x * kTouchChunk;
   uint64_t h = 0;
@@ -756,7 +811,7 @@ __global__ __launch_bounds__(256) void k_touch_emit(TwTable t, Program prog, TwP
                                                     uint64_t cap, const uint64_t *off, OutCols out, uint64_t out_base,
                                                     uint64_t out_cap, DevScalars *sc) {
   __shared__ uint64_t swave[4];
-  uint64_t n = sc->scratch[1];
+  uint64_t n = sc->scratch[6] ? sc->scratch[6] : sc->scratch[1];  // after k_seg_apply: [6]
   if (n > cap) n = cap;
   const uint64_t c0 = (uint64_t)blockIdx.x * kTouchChunk;
   if (c0 >= n) return;  // uniform
@@ -824,16 +879,18 @@ uint64_t part_lds_entries(const Program &prog, bool big) {
 bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, const PartParams &pp, const TwTable &t,
                      const PartBuffers &pb, uint64_t n, DevScalars *sc, bool maybe_packed, const OutCols *out,
                      uint64_t out_base, uint64_t out_cap, bool wide, bool *lean) {
+  bool took_lean = false;
   if (lean) *lean = false;
   if (!part_supported(prog)) return false;
   const uint64_t nb = 1ull << pp.np_log2;
   hipLaunchKernelGGL(k_part_chunks, dim3(1), dim3(1024), 0, s, pb.bstart, pp.np_log2, pp.chunk, pb.chunk_start,
-                     pb.chunk_bucket);
+                     pb.chunk_bucket, sc);
   const dim3 g((unsigned)(nb + n / pp.chunk + 1));
   // packed one-window batches of the common slot programs: the lean kernels
   // (k_agg_lean.hip); the general kernel below then only covers the wide layout
   if (maybe_packed && launch_part_agg_lean(s, g, prog, p, pp, t, pb, sc, out, out_base, out_cap)) {
     maybe_packed = false;
+    took_lean = true;
     if (lean) *lean = true;
     if (!wide) return true;  // predicted packed: the wide variant is not launched
   }
@@ -842,6 +899,7 @@ bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, cons
   else if (prog.n_slots <= 4) agg_launch_ms4(s, g, W, maybe_packed, prog, p, pp, t, pb, sc);
   else if (prog.n_slots <= 6) agg_launch_ms6(s, g, W, maybe_packed, prog, p, pp, t, pb, sc);
   else agg_launch_ms8(s, g, W, maybe_packed, prog, p, pp, t, pb, sc);
+  if (pp.defer) launch_seg_apply(s, g, prog, p, pp, t, pb, sc, out, out_base, out_cap, took_lean);
   return true;
 }
 

@@ -112,6 +112,40 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const T *in, uint64
   }
 }
 
+// One workgroup for short inputs (n <= kScanSmall): each of 1024 threads owns
+// kScanSmallPer consecutive elements, all loaded before the scan; one launch
+// instead of three.
+constexpr int kScanSmallPer = 8;
+constexpr uint64_t kScanSmall = 1024 * kScanSmallPer;
+template <typename T, typename U>
+__global__ __launch_bounds__(1024) void k_scan_small(const T *in, uint64_t n, U *out, uint64_t *__restrict__ total) {
+  __shared__ uint64_t sw[16];
+  const uint64_t lo = (uint64_t)threadIdx.x * kScanSmallPer;
+  uint64_t v[kScanSmallPer];
+  uint64_t loc = 0;
+#pragma unroll
+  for (int r = 0; r < kScanSmallPer; ++r) {
+    v[r] = lo + r < n ? (uint64_t)in[lo + r] : 0;  // in and out may alias: every read before any write
+    loc += v[r];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t incl = wave_incl_sum64(loc);
+  if (lane == 63) sw[w] = incl;
+  __syncthreads();
+  uint64_t run = incl - loc;
+  for (int k = 0; k < w; ++k) run += sw[k];
+#pragma unroll
+  for (int r = 0; r < kScanSmallPer; ++r) {
+    if (lo + r < n) out[lo + r] = (U)run;
+    run += v[r];
+  }
+  if (threadIdx.x == 0 && total) {
+    uint64_t t = 0;
+    for (int k = 0; k < 16; ++k) t += sw[k];
+    *total = t;
+  }
+}
+
 uint64_t scan_partials_needed(uint64_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
 
 template <typename T, typename U>
@@ -119,6 +153,10 @@ static void scan_excl_impl(hipStream_t s, const T *in, U *out, uint64_t n, uint6
   uint64_t blocks = (n + kScanTile - 1) / kScanTile;
   if (blocks == 0) {
     hipMemsetAsync(total, 0, 8, s);
+    return;
+  }
+  if (n <= kScanSmall) {
+    hipLaunchKernelGGL((k_scan_small<T, U>), dim3(1), dim3(1024), 0, s, in, n, out, total);
     return;
   }
   hipLaunchKernelGGL((k_scan_reduce<T>), dim3((unsigned)blocks), dim3(kScanThreads), 0, s, in, n, partial);

@@ -89,8 +89,12 @@ int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog,
   const uint64_t tcap = n * (d.wpr ? d.wpr : 1), nc = touch_chunks(tcap);
   uint64_t o_touch = take(tcap * 4), o_wm = take(n * 8);
   uint64_t o_tcnt = take(nc * 4), o_toff = take((nc + 1) * 8), o_tpart = take((scan_partials_needed(nc) + 8) * 8);
-  // lean aggregation: one pane entry per record at most, [g][slots]
-  uint64_t o_pane = take(n * (1 + (uint64_t)prog.n_slots) * 8);
+  // lean aggregation: one pane entry per record at most, [g][slots]; the
+  // general kernel's deferred window updates: up to 2 per record, more fall
+  // back to in-kernel updates
+  const uint64_t pcap = n * (d.wpr > 1 ? 2 : 1);
+  uint64_t o_pane = take(pcap * (1 + (uint64_t)prog.n_slots) * 8);
+  uint64_t o_seg = take(((1ull << kPartMaxLog2) + n / 1024 + 2) * kMaxSeg * 16);
   uint64_t o_pinfo = take(((1ull << kPartMaxLog2) + n / 1024 + 2) * 16);
   uint64_t o_pcnt = take(((1ull << kPartMaxLog2) + n / 1024 + 2 + 4) * 4);
   DTRY(hipMalloc(&d.part_mem, off));
@@ -113,6 +117,8 @@ int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog,
   pb.pane = (uint64_t *)(m + o_pane);
   pb.pane_info = (uint64_t *)(m + o_pinfo);
   pb.pane_cnt = (uint32_t *)(m + o_pcnt);
+  pb.seg = (uint64_t *)(m + o_seg);
+  pb.pane_cap = pcap;
   pb.n_cap = n;
   return HSG_OK;
 }
@@ -457,11 +463,14 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       pp.rbits = d.rbits;
       pp.chunk = kAggChunk;
       pp.big = d.agg_big ? 1 : 0;
+      pp.defer = 1;
       if (!rec_wm && !optimistic) launch_part_recwm(d.stream, kb, d.tile_prefix, d.sc, d.part.wm);
       launch_part_hist(d.stream, kb, p, pp, rec_wm, d.part.wm, d.part, d.sc, optimistic);
       const bool can_pack = optimistic && cfg.n_cols <= 8 && d.wpr < 256;
-      if (optimistic) launch_part_decide(d.stream, d.sc, p, a.wm_in, cfg.grace_ms, can_pack, d.part, pp.tiles);
-      launch_part_offsets(d.stream, pp, d.part, d.sc);
+      if (optimistic)
+        launch_part_decide_offsets(d.stream, d.sc, p, a.wm_in, cfg.grace_ms, can_pack, pp, d.part);
+      else
+        launch_part_offsets(d.stream, pp, d.part, d.sc);
       skipped_wide = can_pack && d.pred_packed && part_lean_eligible(prog, pp);
       launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc, can_pack, !skipped_wide);
       const bool emit_batch = cfg.emit_mode == HSG_EMIT_PER_BATCH;
@@ -469,7 +478,7 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       launch_part_agg(d.stream, prog, p, pp, d.tw, d.part, kb.n, d.sc, can_pack, emit_batch ? &d.out : nullptr,
                       a.pending, d.out_cap, !skipped_wide, &lean);
       if (!lean) skipped_wide = false;  // the general kernel ran both layouts
-      skipped_emit = emit_batch && lean && d.pred_direct;
+      skipped_emit = emit_batch && d.pred_direct;  // the lean or the deferred (k_seg_apply) path
     } else {
       launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, false);
     }
@@ -504,15 +513,18 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
   const uint64_t groups = d.h_sc->scratch[0];
   if (kb.n && d.use_part) {
     d.pred_packed = d.h_sc->packed != 0;
-    d.pred_direct = d.h_sc->scratch[2] == 1;
-    d.lean_batches += d.h_sc->scratch[2] != 0;
-    d.direct_batches += d.h_sc->scratch[2] == 1;
+    const uint64_t how = d.h_sc->scratch[2];  // 1/2 lean, 3/4 deferred; odd: changelog written directly
+    d.pred_direct = how == 1 || how == 3;
+    d.lean_batches += how == 1 || how == 2;
+    d.direct_batches += how == 1 || how == 3;
   }
-  if (rc == HSG_OK && kb.n && skipped_emit && d.h_sc->scratch[2] != 1 && d.h_sc->scratch[1] != 0) {
-    // the apply filled the touched list: the emit chain that was not launched
+  const uint64_t how = d.h_sc->scratch[2];
+  if (rc == HSG_OK && kb.n && skipped_emit && how != 1 && how != 3 && (d.h_sc->scratch[1] | d.h_sc->scratch[6])) {
+    // the touched list was filled: the emit chain that was not launched runs on
+    // it (its lengths, scratch[1] / [6], back on the device)
     d.replays += 1;
     PushResult r1 = r;
-    DTRY(hipMemcpyAsync(&d.sc->scratch[1], &d.h_sc->scratch[1], 8, hipMemcpyHostToDevice, d.stream));
+    DTRY(hipMemcpyAsync(&d.sc->scratch[1], &d.h_sc->scratch[1], 6 * 8, hipMemcpyHostToDevice, d.stream));
     d.sc_clean = false;
     launch_part_emit(d.stream, d.tw, prog, p, d.part, d.out, a.pending, d.out_cap, d.sc);
     DTRY(hipEventRecord(d.ev_b, d.stream));
