@@ -409,22 +409,19 @@ __device__ inline void group_live(AggLds<MS, E, NT> &L, uint32_t nl) {
       L.pg.order[atomicAdd(&L.pg.cnt[h], 1u)] = e;
     }
     __syncthreads();
-    // each bucket by (key, pane): a handful of entries, one thread per bucket
-    for (uint32_t h = threadIdx.x; h < E; h += NT) {
+    // each bucket by (key, pane): every entry counts the entries of its
+    // bucket that sort before it (one thread per entry; a bucket holds a key's
+    // panes, ~size / advance of them, so a serial sort per bucket would keep
+    // one thread busy for the whole bucket)
+    for (uint32_t q = threadIdx.x; q < nl; q += NT) {
+      const uint16_t x = L.pg.order[q];
+      const uint64_t kx = L.key[x];
+      const uint32_t h = (uint32_t)(mix64(kx >> 32) & (E - 1));
       const uint32_t end = L.pg.cnt[h], start = h ? L.pg.cnt[h - 1] : 0u;
-      for (uint32_t i = start + 1; i < end; ++i) {
-        const uint16_t x = L.pg.order[i];
-        const uint64_t kx = L.key[x];
-        uint32_t j = i;
-        while (j > start && L.key[L.pg.order[j - 1]] > kx) {
-          L.pg.order[j] = L.pg.order[j - 1];
-          --j;
-        }
-        L.pg.order[j] = x;
-      }
+      uint32_t rank = 0;
+      for (uint32_t j = start; j < end; ++j) rank += L.key[L.pg.order[j]] < kx;
+      L.live[start + rank] = x;
     }
-    __syncthreads();
-    for (uint32_t q = threadIdx.x; q < nl; q += NT) L.live[q] = L.pg.order[q];
     __syncthreads();
   }
 }

@@ -689,8 +689,10 @@ __global__ __launch_bounds__(256) void k_part_colsum(const uint32_t *__restrict_
   const int b = blockIdx.x * 64 + lane;
   const uint64_t t0 = (uint64_t)blockIdx.y * kColSeg, t1 = t0 + kColSeg < tiles ? t0 + kColSeg : tiles;
   uint32_t sum = 0;
-  if (b < nb)
+  if (b < nb) {
+#pragma unroll 16
     for (uint64_t t = t0 + w; t < t1; t += 4) sum += hist[t * nb + b];
+  }
   red[w][lane] = sum;
   __syncthreads();
   if (w == 0 && b < nb) segsum[(uint64_t)b * nseg + blockIdx.y] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
@@ -705,19 +707,28 @@ __global__ __launch_bounds__(256) void k_part_colscan(const uint32_t *__restrict
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int b = blockIdx.x * 64 + lane;
   const uint64_t t0 = (uint64_t)blockIdx.y * kColSeg, t1 = t0 + kColSeg < tiles ? t0 + kColSeg : tiles;
-  const uint64_t per = (t1 - t0 + 3) / 4;
-  const uint64_t r0 = t0 + w * per < t1 ? t0 + w * per : t1, r1 = r0 + per < t1 ? r0 + per : t1;
+  // each wave a quarter of the segment's tiles: their sum, then the running
+  // prefix (the second read is served by L2); loads unrolled so that many
+  // are in flight
+  constexpr int PER = kColSeg / 4;
+  const uint64_t r0 = t0 + (uint64_t)w * PER;
+  const uint32_t *hp = hist + r0 * nb + b;
+  const int cnt = r0 < t1 ? (int)(t1 - r0 < (uint64_t)PER ? t1 - r0 : PER) : 0;
   uint32_t sum = 0;
-  if (b < nb)
-    for (uint64_t t = r0; t < r1; ++t) sum += hist[t * nb + b];
+  if (b < nb) {
+#pragma unroll 16
+    for (int k = 0; k < cnt; ++k) sum += hp[(uint64_t)k * nb];
+  }
   red[w][lane] = sum;
   __syncthreads();
   if (b >= nb) return;
   uint64_t run = segoff[(uint64_t)b * nseg + blockIdx.y];
   for (int k = 0; k < w; ++k) run += red[k][lane];
-  for (uint64_t t = r0; t < r1; ++t) {
-    offt[t * nb + b] = (uint32_t)run;
-    run += hist[t * nb + b];
+  uint32_t *op = offt + r0 * nb + b;
+#pragma unroll 16
+  for (int k = 0; k < cnt; ++k) {
+    op[(uint64_t)k * nb] = (uint32_t)run;
+    run += hp[(uint64_t)k * nb];
   }
   if (blockIdx.y == 0 && w == 0) bstart[b] = segoff[(uint64_t)b * nseg];
 }
