@@ -74,17 +74,12 @@ def main():
         comm_id = comm_unique_id()  # 1-rank communicator: the exchange path with itself
     eng = Engine(device=local, rank=rank, nranks=world, comm_id=comm_id, batch_capacity=batch)
 
-    # state sized for the config: distinct (key, window) groups over the whole run
-    # the config's time density: cfg.n records per rank per hour of event time,
-    # also when fewer records are measured (--records)
-    span_ms = 3_600_000 * min(1.0, n_rank / cfg.n)
-    wpr = -(-cfg.size_ms // cfg.advance_ms) if cfg.window_kind == abi.HSG_HOPPING else 1
-    windows = int(span_ms // (cfg.advance_ms or cfg.size_ms or 60_000)) + wpr + 2 \
-        if cfg.window_kind != abi.HSG_SESSION else 1
-    groups = min(cfg.keys * windows, n_rank * world * wpr)
-    if cfg.window_kind == abi.HSG_SESSION:
-        groups = n_rank * world  # at most one session per record
-    spec = cfg.spec(emit, state_capacity=max(1 << 16, groups))
+    # time-window state: the engine sizes its HBM table itself (default, then
+    # growth before any batch that could pass 3/4 load: hsg_op_config
+    # state_capacity = 0), as a query with no cardinality hint; sessions: an
+    # arena for at most one session per record
+    groups = n_rank * world if cfg.window_kind == abi.HSG_SESSION else 0
+    spec = cfg.spec(emit, state_capacity=groups)
     op = eng.op(spec)
     f64 = spec.agg_is_f64()
 

@@ -115,7 +115,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const T *in, uint64
 // One workgroup for short inputs (n <= kScanSmall): each of 1024 threads owns
 // kScanSmallPer consecutive elements, all loaded before the scan; one launch
 // instead of three.
-constexpr int kScanSmallPer = 32;
+constexpr int kScanSmallPer = 8;
 constexpr uint64_t kScanSmall = 1024 * kScanSmallPer;
 template <typename T, typename U>
 __global__ __launch_bounds__(1024) void k_scan_small(const T *in, uint64_t n, U *out, uint64_t *__restrict__ total) {
