@@ -58,7 +58,9 @@ struct PartParams {
   int32_t big;        // aggregation variant: 1 = big LDS table, 1024 threads
   int32_t bshift;     // owner bits above the bucket bits in the key hash (multi-GPU, power-of-two ranks)
   int32_t defer;      // aggregation: window updates of exclusive buckets go to pb.pane segments (k_seg_apply)
-  uint64_t tiles;     // partition-pass tiles of this batch
+  int32_t sub;        // partition passes: kPartTileRecs-record sub-tiles per offsets row (one workgroup per row)
+  int32_t pad;
+  uint64_t tiles;     // offsets rows of this batch     // partition-pass tiles of this batch
   uint64_t chunk;     // records per aggregation workgroup
 };
 
@@ -66,6 +68,12 @@ inline int part_words(int n_cols, bool has_seq) { return 2 + n_cols + (has_seq ?
 constexpr int kPartTileRecs = 4096;                   // records per partition-pass workgroup
 inline int part_tile_for(int) { return kPartTileRecs; }
 inline uint64_t part_tiles(uint64_t n, int tile) { return (n + tile - 1) / tile; }
+// Sub-tiles per offsets row of the optimistic pipeline (the partition
+// kernels walk a row's sub-tiles in order). Rows of 2 or 8 tiles shrink the
+// (row, bucket) offsets matrix 2x / 8x but measured slower overall on C2
+// (staged scatter 184 -> 228 / 249 us: half / an eighth of the workgroups,
+// each waiting on its sub-tiles' loads in turn), so one tile per row.
+constexpr int kRowSub = 1;
 
 // per-record stream time into wm unless sc->no_late (decided by launch_tile_scan)
 void launch_part_recwm(hipStream_t s, const Batch &b, const int64_t *tprefix, const DevScalars *sc, int64_t *wm);

@@ -166,11 +166,16 @@ __global__ __launch_bounds__(kPNT) void k_part_hist(Batch b, TwParams p, PartPar
   // stream-time inputs of the batch come out of the same walk: max ts of every
   // record (Processor.hs:139), min ts of the keyed records (as k_tile_stats)
   uint64_t ext[2] = {0, 0};
-  walk_tile<T, kPNT>(b, p, tile, sc->k_epoch, opt ? nullptr : pick_wm(rec_wm, own_wm, sc), late, err,
-                     [&](int, uint64_t, uint32_t key, uint32_t, uint32_t) {
-                       atomicAdd(&cnt[bucket_of(key, pp.np_log2, pp.bshift)], 1u);
-                     },
-                     opt ? ext : nullptr);
+  for (int st = 0; st < pp.sub; ++st) {
+    uint64_t e2[2] = {0, 0};
+    walk_tile<T, kPNT>(b, p, tile * pp.sub + st, sc->k_epoch, opt ? nullptr : pick_wm(rec_wm, own_wm, sc), late, err,
+                       [&](int, uint64_t, uint32_t key, uint32_t, uint32_t) {
+                         atomicAdd(&cnt[bucket_of(key, pp.np_log2, pp.bshift)], 1u);
+                       },
+                       opt ? e2 : nullptr);
+    ext[0] = e2[0] > ext[0] ? e2[0] : ext[0];
+    ext[1] = e2[1] > ext[1] ? e2[1] : ext[1];
+  }
   if (opt) {
     uint64_t mx = ext[0], mn = ext[1];
 #pragma unroll
@@ -221,10 +226,14 @@ __global__ __launch_bounds__(kPNT) void k_part_hist_opt(Batch b, TwParams p, Par
   __shared__ uint64_t sext[2][kPNT / 64];
   constexpr int R = T / kPNT;
   const int nb = 1 << pp.np_log2;
-  const uint64_t tile = xcd_tile(blockIdx.x, pp.tiles);
+  const uint64_t tile = xcd_tile(blockIdx.x, pp.tiles);  // offsets row
   const int64_t k_epoch = sc->k_epoch;
   for (int i = threadIdx.x; i < nb; i += kPNT) cnt[i] = 0;
-  const uint64_t base = tile * T;
+  __syncthreads();
+  uint64_t mx = 0, mn = 0;
+  for (int st = 0; st < pp.sub; ++st) {
+  const uint64_t base = (tile * pp.sub + st) * T;
+  if (base >= b.n) break;  // uniform
   uint32_t key[R];
   int64_t ts[R];
   // the counts are per tile, so which thread reads which record of the tile is
@@ -257,8 +266,6 @@ __global__ __launch_bounds__(kPNT) void k_part_hist_opt(Batch b, TwParams p, Par
       ts[r] = in ? b.ts[i] : INT64_MIN;
     }
   }
-  __syncthreads();
-  uint64_t mx = 0, mn = 0;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const uint64_t o = i64_ord(ts[r]);
@@ -273,6 +280,7 @@ __global__ __launch_bounds__(kPNT) void k_part_hist_opt(Batch b, TwParams p, Par
     if (a > z) continue;
     atomicAdd(&cnt[bucket_of(key[r], pp.np_log2, pp.bshift)], 1u);
   }
+  }  // sub-tiles
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const uint64_t x = __shfl_xor(mx, o, 64), c = __shfl_xor(mn, o, 64);
@@ -318,7 +326,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
   __shared__ uint64_t lkn[T];  // krel | nwin << 32
   __shared__ uint32_t lstart[1 << kPartMaxLog2];
   __shared__ uint32_t cursor[1 << kPartMaxLog2];
-  __shared__ uint32_t goff[1 << kPartMaxLog2];
+  __shared__ uint32_t goff[1 << kPartMaxLog2];  // the row's next output slot per bucket
   __shared__ uint32_t swave[kPNT / 64];
   if (sc->redo) return;  // uniform: the optimistic pass found late records
   if (staged && sc->packed) return;  // uniform: k_part_scatter_st wrote this batch
@@ -327,92 +335,109 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
   const bool packed = sc->packed != 0;
   const int W = packed ? pp.words - 1 : pp.words;
   const uint32_t kbase = (uint32_t)sc->kbase;
-  const uint64_t tile = xcd_tile(blockIdx.x, pp.tiles);
+  const uint64_t row = xcd_tile(blockIdx.x, pp.tiles);
   const uint64_t q0 = wall_clock64();
-  for (int i = threadIdx.x; i < nb; i += kPNT) cursor[i] = 0;
-  for (int j = threadIdx.x; j < T; j += kPNT) lbk[j] = kNoBucket;
-  __syncthreads();
-  // 1) window runs and buckets of the tile's records, bucket histogram
-  uint64_t late = 0;
-  uint32_t err = 0;
-  walk_tile<T, kPNT>(b, p, tile, sc->k_epoch, pick_wm(rec_wm, own_wm, sc), late, err,
-                     [&](int j, uint64_t, uint32_t key, uint32_t krel, uint32_t nwin) {
-                       const uint32_t bk = bucket_of(key, pp.np_log2, pp.bshift);
-                       lkn[j] = (uint64_t)krel | ((uint64_t)nwin << 32);
-                       lbk[j] = (uint16_t)bk;
-                       atomicAdd(&cursor[bk], 1u);
-                     });
-  __syncthreads();
-  const uint64_t q1 = wall_clock64();
-  // 2) tile-local exclusive scan of the histogram; global run starts
+  for (int i = threadIdx.x; i < nb; i += kPNT) {
+    cursor[i] = 0;
+    goff[i] = pb.offt[row * (uint64_t)nb + i];
+  }
   const int per = (nb + kPNT - 1) / kPNT;
   const int lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
-  uint32_t loc = 0;
-  for (int k = lo; k < hi; ++k) loc += cursor[k];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t incl = loc;
+  uint64_t late = 0;
+  uint32_t err = 0;
+  uint64_t q1 = q0, q2 = q0, q3 = q0;
+  // the row's sub-tiles in order: a bucket's runs of consecutive sub-tiles
+  // are adjacent in the output
+  for (int st = 0; st < pp.sub; ++st) {
+    const uint64_t tile = row * pp.sub + st;
+    if (tile * T >= b.n) break;  // uniform
+    for (int j = threadIdx.x; j < T; j += kPNT) lbk[j] = kNoBucket;
+    __syncthreads();
+    // 1) window runs and buckets of the sub-tile's records, bucket histogram
+    walk_tile<T, kPNT>(b, p, tile, sc->k_epoch, pick_wm(rec_wm, own_wm, sc), late, err,
+                       [&](int j, uint64_t, uint32_t key, uint32_t krel, uint32_t nwin) {
+                         const uint32_t bk = bucket_of(key, pp.np_log2, pp.bshift);
+                         lkn[j] = (uint64_t)krel | ((uint64_t)nwin << 32);
+                         lbk[j] = (uint16_t)bk;
+                         atomicAdd(&cursor[bk], 1u);
+                       });
+    __syncthreads();
+    q1 = wall_clock64();
+    // 2) sub-tile-local exclusive scan of the histogram
+    uint32_t loc = 0;
+    for (int k = lo; k < hi; ++k) loc += cursor[k];
+    uint32_t incl = loc;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t u = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += u;
-  }
-  if (lane == 63) swave[wv] = incl;
-  __syncthreads();
-  uint32_t run = incl - loc;
-  for (int k = 0; k < wv; ++k) run += swave[k];
-  for (int k = lo; k < hi; ++k) {
-    lstart[k] = run;
-    run += cursor[k];
-    cursor[k] = 0;
-    goff[k] = pb.offt[tile * (uint64_t)nb + k];
-  }
-  uint32_t placed = 0;
-  for (int k = 0; k < kPNT / 64; ++k) placed += swave[k];
-  __syncthreads();
-  const uint64_t q2 = wall_clock64();
-  // 3) bucket-sorted order of the tile's records
-  for (int j = threadIdx.x; j < T; j += kPNT) {
-    const uint16_t bk = lbk[j];
-    if (bk == kNoBucket) continue;
-    sidx[lstart[bk] + atomicAdd(&cursor[bk], 1u)] = (uint16_t)j;
-  }
-  __syncthreads();
-  const uint64_t q3 = wall_clock64();
-  // 4) coalesced write-out: consecutive lanes write consecutive words of a run
-  const uint32_t inv = (1u << 20) / (uint32_t)W + 1;  // t / W for t < 2^16, W <= 16
-  const uint32_t total = placed * (uint32_t)W;
-  const uint64_t base = tile * T;
-#pragma unroll 4
-  for (uint32_t t = threadIdx.x; t < total; t += kPNT) {
-    const uint32_t q = (uint32_t)(((uint64_t)t * inv) >> 20);
-    const uint32_t w = t - q * (uint32_t)W;
-    const uint16_t j = sidx[q];
-    const uint16_t bk = lbk[j];
-    const uint64_t i = base + j;
-    const uint64_t dest = (uint64_t)goff[bk] + (q - lstart[bk]);
-    uint64_t v;
-    const uint32_t wc = packed ? w + 1 : w;  // word index in the wide layout (packed: 0 is both headers)
-    if (w == 0 && packed) {
-      uint64_t vb = 0;
-      for (int c = 0; c < C; ++c)
-        if (!(pp.has_valid && b.valid[c] && !b.valid[c][i])) vb |= 1ull << c;
-      const uint64_t kn = lkn[j];
-      v = (uint64_t)b.key[i] | ((uint64_t)(((uint32_t)kn - kbase) & 0xFFFFu) << 32) | ((kn >> 32) << 48) | (vb << 56);
-    } else if (w == 0) {
-      v = (uint64_t)b.key[i] | (lkn[j] << 32);
-    } else if (wc == 1) {
-      uint64_t vb = 0;
-      for (int c = 0; c < C; ++c)
-        if (!(pp.has_valid && b.valid[c] && !b.valid[c][i])) vb |= 1ull << c;
-      v = (lkn[j] >> 32) | (vb << 32);
-    } else if ((int)wc < 2 + C) {
-      v = (uint64_t)b.col[wc - 2][i];
-    } else {
-      v = (uint64_t)((seq ? seq[i] : (int64_t)(p.rec_base + i)) + 1);
+    for (int o = 1; o < 64; o <<= 1) {
+      uint32_t u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
     }
-    pb.rec[dest * W + w] = v;
+    if (lane == 63) swave[wv] = incl;
+    __syncthreads();
+    uint32_t run = incl - loc;
+    for (int k = 0; k < wv; ++k) run += swave[k];
+    for (int k = lo; k < hi; ++k) {
+      lstart[k] = run;
+      run += cursor[k];
+      cursor[k] = 0;
+    }
+    uint32_t placed = 0;
+    for (int k = 0; k < kPNT / 64; ++k) placed += swave[k];
+    __syncthreads();
+    q2 = wall_clock64();
+    // 3) bucket-sorted order of the sub-tile's records
+    for (int j = threadIdx.x; j < T; j += kPNT) {
+      const uint16_t bk = lbk[j];
+      if (bk == kNoBucket) continue;
+      sidx[lstart[bk] + atomicAdd(&cursor[bk], 1u)] = (uint16_t)j;
+    }
+    __syncthreads();
+    q3 = wall_clock64();
+    // 4) coalesced write-out: consecutive lanes write consecutive words of a run
+    const uint32_t inv = (1u << 20) / (uint32_t)W + 1;  // t / W for t < 2^16, W <= 16
+    const uint32_t total = placed * (uint32_t)W;
+    const uint64_t base = tile * T;
+#pragma unroll 4
+    for (uint32_t t = threadIdx.x; t < total; t += kPNT) {
+      const uint32_t q = (uint32_t)(((uint64_t)t * inv) >> 20);
+      const uint32_t w = t - q * (uint32_t)W;
+      const uint16_t j = sidx[q];
+      const uint16_t bk = lbk[j];
+      const uint64_t i = base + j;
+      const uint64_t dest = (uint64_t)goff[bk] + (q - lstart[bk]);
+      uint64_t v;
+      const uint32_t wc = packed ? w + 1 : w;  // word index in the wide layout (packed: 0 is both headers)
+      if (w == 0 && packed) {
+        uint64_t vb = 0;
+        for (int c = 0; c < C; ++c)
+          if (!(pp.has_valid && b.valid[c] && !b.valid[c][i])) vb |= 1ull << c;
+        const uint64_t kn = lkn[j];
+        v = (uint64_t)b.key[i] | ((uint64_t)(((uint32_t)kn - kbase) & 0xFFFFu) << 32) | ((kn >> 32) << 48) | (vb << 56);
+      } else if (w == 0) {
+        v = (uint64_t)b.key[i] | (lkn[j] << 32);
+      } else if (wc == 1) {
+        uint64_t vb = 0;
+        for (int c = 0; c < C; ++c)
+          if (!(pp.has_valid && b.valid[c] && !b.valid[c][i])) vb |= 1ull << c;
+        v = (lkn[j] >> 32) | (vb << 32);
+      } else if ((int)wc < 2 + C) {
+        v = (uint64_t)b.col[wc - 2][i];
+      } else {
+        v = (uint64_t)((seq ? seq[i] : (int64_t)(p.rec_base + i)) + 1);
+      }
+      pb.rec[dest * W + w] = v;
+    }
+    __syncthreads();
+    // 5) the row's next slots: past this sub-tile's runs
+    for (int k = lo; k < hi; ++k) {
+      goff[k] += cursor[k];
+      cursor[k] = 0;
+    }
+    __syncthreads();
   }
-  __syncthreads();
+  late = wave_sum_u64(late);
+  if (err) atomicOr(&sc->err, err);
   if (threadIdx.x == 0) {
     const uint64_t q4 = wall_clock64();
     atomicAdd((unsigned long long *)&sc->scratch[13], (unsigned long long)(q1 - q0));
@@ -545,96 +570,108 @@ template <int T, int W>
 __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, PartParams pp, PartBuffers pb,
                                                           DevScalars *sc) {
   __shared__ uint64_t stage[T * W];
-  __shared__ uint32_t cnt2[1 << (kPartMaxLog2 - 1)];
-  __shared__ uint16_t lstart[1 << kPartMaxLog2];
+  __shared__ uint32_t cnt2[1 << (kPartMaxLog2 - 1)];  // two u16 counts per word, then the u16 run starts
+  __shared__ uint32_t cursor[1 << kPartMaxLog2];      // the row's next output slot per bucket
   __shared__ uint32_t swave[kPNT / 64];
   if (sc->redo || !sc->packed) return;  // uniform: the gather variant runs
   constexpr int R = T / kPNT;
   const int nb = 1 << pp.np_log2;
   const uint32_t kbase = (uint32_t)sc->kbase;
   const int64_t k_epoch = sc->k_epoch;
-  const uint64_t tile = xcd_tile(blockIdx.x, pp.tiles);
+  const uint64_t row = xcd_tile(blockIdx.x, pp.tiles);
   const uint64_t q0 = wall_clock64();
+  uint16_t *lstart = reinterpret_cast<uint16_t *>(cnt2);
   for (int i = threadIdx.x; i < (nb + 1) / 2; i += kPNT) cnt2[i] = 0;
-  const uint64_t base = tile * T;
-  uint32_t key[R];
-  int64_t ts[R];
-  uint64_t col[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint64_t i = base + (uint64_t)r * kPNT + threadIdx.x;
-    const bool in = i < b.n;
-    key[r] = in ? b.key[i] : HSG_KEY_NONE;
-    ts[r] = in ? b.ts[i] : 0;
-    col[r] = (W == 2 && in) ? (uint64_t)b.col[0][i] : 0;
-  }
-  __syncthreads();
-  uint64_t late = 0;
-  uint32_t err = 0;
-  uint32_t slot[R];  // bucket << 16 | slot in the tile's run of the bucket, ~0 = no window
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    uint32_t krel, nwin;
-    slot[r] = ~0u;
-    if (!part_record(p, k_epoch, key[r], ts[r], INT64_MIN, krel, nwin, late, err)) continue;
-    const uint32_t bk = bucket_of(key[r], pp.np_log2, pp.bshift);
-    const uint32_t sh = (bk & 1u) * 16u;
-    const uint32_t pos = (atomicAdd(&cnt2[bk >> 1], 1u << sh) >> sh) & 0xFFFFu;
-    slot[r] = (bk << 16) | pos;
-    const uint64_t i = base + (uint64_t)r * kPNT + threadIdx.x;
-    uint64_t vb = 0;
-    if (W == 2 && !(pp.has_valid && b.valid[0] && !b.valid[0][i])) vb = 1;
-    ts[r] = (int64_t)((uint64_t)key[r] | ((uint64_t)((krel - kbase) & 0xFFFFu) << 32) | ((uint64_t)nwin << 48) |
-                      (vb << 56));  // the packed header word, kept in the ts register
-  }
-  __syncthreads();
-  // tile-local exclusive scan of the bucket counts -> run starts
+  for (int i = threadIdx.x; i < nb; i += kPNT) cursor[i] = pb.offt[row * (uint64_t)nb + i];
+  // buckets [lo, hi) of this thread: whole words of cnt2 (scan, run starts)
   const int per = (nb + kPNT - 1) / kPNT;
   const int lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
-  uint32_t loc = 0;
-  for (int k = lo; k < hi; ++k) loc += (cnt2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t incl = loc;
+  uint64_t late = 0, q1 = q0;
+  uint32_t err = 0;
+  for (int st = 0; st < pp.sub; ++st) {
+    const uint64_t base = (row * pp.sub + st) * T;
+    if (base >= b.n) break;  // uniform
+    uint32_t key[R];
+    int64_t ts[R];
+    uint64_t col[R];
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t u = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += u;
-  }
-  if (lane == 63) swave[wv] = incl;
-  __syncthreads();
-  uint32_t run = incl - loc;
-  for (int k = 0; k < wv; ++k) run += swave[k];
-  for (int k = lo; k < hi; ++k) {
-    lstart[k] = (uint16_t)run;
-    run += (cnt2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
-  }
-  uint32_t placed = 0;
-  for (int k = 0; k < kPNT / 64; ++k) placed += swave[k];
-  __syncthreads();
-  // place the packed records at their bucket-sorted positions
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    if (slot[r] == ~0u) continue;
-    const uint32_t q = lstart[slot[r] >> 16] + (slot[r] & 0xFFFFu);
-    stage[q * W] = (uint64_t)ts[r];
-    if (W == 2) stage[q * W + 1] = col[r];
-  }
-  __syncthreads();
-  const uint64_t q1 = wall_clock64();
-  // write-out: record q goes to offt[tile][bucket] + (q - run start)
-  const uint32_t *orow = pb.offt + tile * (uint64_t)nb;
-  for (uint32_t q = threadIdx.x; q < placed; q += kPNT) {
-    const uint64_t h = stage[q * W];
-    const uint32_t bk = bucket_of((uint32_t)h, pp.np_log2, pp.bshift);
-    const uint64_t dest = (uint64_t)orow[bk] + (q - lstart[bk]);
-    if (W == 2) {
-      const uint64_t c = stage[q * W + 1];
-      *(ulonglong2 *)(pb.rec + dest * 2) = make_ulonglong2(h, c);
-    } else {
-      pb.rec[dest] = h;
+    for (int r = 0; r < R; ++r) {
+      const uint64_t i = base + (uint64_t)r * kPNT + threadIdx.x;
+      const bool in = i < b.n;
+      key[r] = in ? b.key[i] : HSG_KEY_NONE;
+      ts[r] = in ? b.ts[i] : 0;
+      col[r] = (W == 2 && in) ? (uint64_t)b.col[0][i] : 0;
     }
+    __syncthreads();  // counters clear
+    uint32_t slot[R];  // bucket << 16 | slot in the sub-tile's run of the bucket, ~0 = no window
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      uint32_t krel, nwin;
+      slot[r] = ~0u;
+      if (!part_record(p, k_epoch, key[r], ts[r], INT64_MIN, krel, nwin, late, err)) continue;
+      const uint32_t bk = bucket_of(key[r], pp.np_log2, pp.bshift);
+      const uint32_t sh = (bk & 1u) * 16u;
+      const uint32_t pos = (atomicAdd(&cnt2[bk >> 1], 1u << sh) >> sh) & 0xFFFFu;
+      slot[r] = (bk << 16) | pos;
+      const uint64_t i = base + (uint64_t)r * kPNT + threadIdx.x;
+      uint64_t vb = 0;
+      if (W == 2 && !(pp.has_valid && b.valid[0] && !b.valid[0][i])) vb = 1;
+      ts[r] = (int64_t)((uint64_t)key[r] | ((uint64_t)((krel - kbase) & 0xFFFFu) << 32) | ((uint64_t)nwin << 48) |
+                        (vb << 56));  // the packed header word, kept in the ts register
+    }
+    __syncthreads();
+    // sub-tile-local exclusive scan of the bucket counts -> run starts (in place)
+    uint32_t c[4] = {0, 0, 0, 0};  // per <= 4 (2048 buckets / 512 threads)
+    uint32_t loc = 0;
+    for (int k = lo; k < hi; ++k) {
+      c[k - lo] = (cnt2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+      loc += c[k - lo];
+    }
+    uint32_t incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) swave[wv] = incl;
+    __syncthreads();
+    uint32_t run = incl - loc;
+    for (int k = 0; k < wv; ++k) run += swave[k];
+    for (int k = lo; k < hi; ++k) {
+      lstart[k] = (uint16_t)run;
+      run += c[k - lo];
+    }
+    uint32_t placed = 0;
+    for (int k = 0; k < kPNT / 64; ++k) placed += swave[k];
+    __syncthreads();
+    // place the packed records at their bucket-sorted positions
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (slot[r] == ~0u) continue;
+      const uint32_t q = lstart[slot[r] >> 16] + (slot[r] & 0xFFFFu);
+      stage[q * W] = (uint64_t)ts[r];
+      if (W == 2) stage[q * W + 1] = col[r];
+    }
+    __syncthreads();
+    q1 = wall_clock64();
+    // write-out: record q goes to the row's slot for its bucket + (q - run start)
+    for (uint32_t q = threadIdx.x; q < placed; q += kPNT) {
+      const uint64_t h = stage[q * W];
+      const uint32_t bk = bucket_of((uint32_t)h, pp.np_log2, pp.bshift);
+      const uint64_t dest = (uint64_t)cursor[bk] + (q - lstart[bk]);
+      if (W == 2) {
+        const uint64_t cc = stage[q * W + 1];
+        *(ulonglong2 *)(pb.rec + dest * 2) = make_ulonglong2(h, cc);
+      } else {
+        pb.rec[dest] = h;
+      }
+    }
+    __syncthreads();
+    // the row's next slots, past this sub-tile's runs; counters cleared
+    for (int k = lo; k < hi; ++k) cursor[k] += c[k - lo];
+    for (int k = lo; k < hi; k += 2) cnt2[k >> 1] = 0;
   }
-  late = wave_sum_u64(late);
   if (err) atomicOr(&sc->err, err);
   if (threadIdx.x == 0) {
     const uint64_t q4 = wall_clock64();

@@ -458,7 +458,8 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       pp.has_seq = has_last(prog);
       pp.words = part_words(cfg.n_cols, pp.has_seq);
       pp.tile = part_tile_for(pp.words);
-      pp.tiles = part_tiles(kb.n, pp.tile);
+      pp.sub = optimistic ? kRowSub : 1;  // offsets rows of kRowSub tiles (the careful path: one)
+      pp.tiles = part_tiles(kb.n, pp.tile * pp.sub);
       pp.pane_S = d.pane_S;
       pp.rbits = d.rbits;
       pp.chunk = kAggChunk;
