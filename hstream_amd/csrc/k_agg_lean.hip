@@ -250,7 +250,9 @@ __global__ __launch_bounds__(NT) void k_agg_lean(PartParams pp, TwTable t, PartB
   if (threadIdx.x == 0) {
     pb.pane_info[2 * blockIdx.x] = r0;
     pb.pane_info[2 * blockIdx.x + 1] = (uint64_t)s_cnt | ((uint64_t)s_ovf << 32);
-    pb.pane_cnt[blockIdx.x] = s_cnt | (s_ovf << 31);
+    // count | overflow << 31 | split bucket << 30: the apply writes the
+    // changelog rows of workgroups with neither itself
+    pb.pane_cnt[blockIdx.x] = s_cnt | (s_ovf << 31) | ((exclusive ? 0u : 1u) << 30);
   }
 }
 
@@ -305,9 +307,7 @@ __global__ __launch_bounds__(256) void k_pane_apply(Program rprog, TwParams p, P
                                                     DevScalars *sc) {
   constexpr int NS = ProgSig<SIG>::count();
   constexpr int PW = 1 + NS;
-  __shared__ uint64_t s_red[4];
-  __shared__ uint64_t s_tot[4];
-  __shared__ uint32_t s_ovf[4];
+  __shared__ uint64_t s_red[4], s_tot[4], s_d[4], s_t[4];
   __shared__ uint32_t cset[kClaimSet];
   if (sc->redo || !sc->packed) return;  // uniform
   uint32_t b;
@@ -325,12 +325,16 @@ __global__ __launch_bounds__(256) void k_pane_apply(Program rprog, TwParams p, P
   if (lds_claim)
     for (int k = threadIdx.x; k < kClaimSet; k += 256) cset[k] = 0;
   // every workgroup's partial count (a few L2-resident loads per thread instead
-  // of a returning atomic on one counter from every workgroup): this one's
-  // position, the batch total, and whether any workgroup wrote overflow partials
+  // of a returning atomic on one counter from every workgroup). A workgroup
+  // whose bucket is its own and that wrote no overflow partial has every group
+  // of its partials exactly once in the batch: its rows go straight to the
+  // changelog (positions after the direct rows of the workgroups before it);
+  // the others' partials leave touched-list entries for the emit pass, whose
+  // rows follow every direct row (sc->scratch[3]).
   const int nb = 1 << pp.np_log2;
   const uint32_t nch = pb.chunk_start[nb];
-  uint64_t before = 0, total = 0;
-  uint32_t anyovf = 0;
+  const bool has_out = out.key != nullptr;
+  uint64_t bd = 0, bt = 0, td = 0, tt = 0;  // before / total, direct / touched
   for (uint32_t k = threadIdx.x; 4 * k < nch; k += 256) {
     const uint4 c4 = reinterpret_cast<const uint4 *>(pb.pane_cnt)[k];
     const uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
@@ -338,30 +342,35 @@ __global__ __launch_bounds__(256) void k_pane_apply(Program rprog, TwParams p, P
     for (int j = 0; j < 4; ++j) {
       const uint32_t w = 4 * k + j;
       if (w >= nch) break;
-      const uint32_t n = c[j] & 0x7FFFFFFFu;
-      anyovf |= c[j] >> 31;
-      total += n;
-      if (w < blockIdx.x) before += n;
+      const uint32_t n = c[j] & 0x3FFFFFFFu;
+      const bool d = has_out && (c[j] >> 30) == 0;
+      (d ? td : tt) += n;
+      if (w < blockIdx.x) (d ? bd : bt) += n;
     }
   }
-  before = wave_sum_u64(before);
-  total = wave_sum_u64(total);
-  anyovf = __ballot(anyovf != 0) != 0;
+  bd = wave_sum_u64(bd);
+  bt = wave_sum_u64(bt);
+  td = wave_sum_u64(td);
+  tt = wave_sum_u64(tt);
   if ((threadIdx.x & 63) == 0) {
-    s_red[threadIdx.x >> 6] = before;
-    s_tot[threadIdx.x >> 6] = total;
-    s_ovf[threadIdx.x >> 6] = anyovf;
+    s_red[threadIdx.x >> 6] = bd;
+    s_tot[threadIdx.x >> 6] = bt;
+    s_d[threadIdx.x >> 6] = td;
+    s_t[threadIdx.x >> 6] = tt;
   }
   __syncthreads();
-  const uint64_t tb = s_red[0] + s_red[1] + s_red[2] + s_red[3];
-  total = s_tot[0] + s_tot[1] + s_tot[2] + s_tot[3];
-  const bool direct = out.key != nullptr && pb.chunk_start[nb + 1] == 0 && !(s_ovf[0] | s_ovf[1] | s_ovf[2] | s_ovf[3]);
+  bd = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+  bt = s_tot[0] + s_tot[1] + s_tot[2] + s_tot[3];
+  td = s_d[0] + s_d[1] + s_d[2] + s_d[3];
+  tt = s_t[0] + s_t[1] + s_t[2] + s_t[3];
+  const bool direct = has_out && exclusive && !ovf;
+  const uint64_t tb = direct ? bd : bt;
   if (threadIdx.x == 0 && blockIdx.x + 1 == nch) {
     // last workgroup: batch totals (every placed record updates one group)
-    sc->scratch[1] = direct ? 0 : total;
-    sc->scratch[3] = direct ? total : 0;
-    sc->scratch[2] = direct ? 1 : 2;
-    sc->scratch[0] = total;
+    sc->scratch[1] = tt;
+    sc->scratch[3] = td;
+    sc->scratch[2] = tt == 0 ? 1 : 2;
+    sc->scratch[0] = td + tt;
     sc->pairs = pb.bstart[nb];
   }
   const int64_t k_epoch = sc->k_epoch;

@@ -880,7 +880,7 @@ __global__ __launch_bounds__(256) void k_touch_emit(TwTable t, Program prog, TwP
     run += swave[0] + swave[1] + swave[2] + swave[3];
     __syncthreads();
     if (!hit) continue;
-    o += out_base;
+    o += out_base + sc->scratch[3];  // after the rows the lean apply wrote itself
     if (o >= out_cap) {
       atomicOr(&sc->err, ERR_OOM);
       continue;
