@@ -201,10 +201,14 @@ __device__ inline bool record_windows(const TwParams &p, int64_t ts, uint64_t &k
     return true;
   }
   if (ts < 0) return false;
+  k_hi = udiv(p.div, (uint64_t)ts);
+  if (p.size == p.adv) {  // tumbling: the one window (uniform branch)
+    k_lo = k_hi;
+    return true;
+  }
   int64_t t0 = (int64_t)((uint64_t)ts - (uint64_t)p.size + (uint64_t)p.adv);
   if (t0 < 0) t0 = 0;
   k_lo = udiv(p.div, (uint64_t)t0);
-  k_hi = udiv(p.div, (uint64_t)ts);
   return true;
 }
 

@@ -173,8 +173,22 @@ __device__ __host__ inline uint64_t mix64(uint64_t x) {
 
 // Hash of a group key: its top bits pick the owner GPU (power-of-two ranks),
 // the next bits the partition bucket, the bits below the aggregation round.
+// Key hash whose TOP bits pick the owner GPU, the partition bucket, the table
+// region and the key-hash rounds (every user takes bits from the top, at most
+// 32 of them): a 32-bit finaliser (murmur3 fmix32) in the high word -- 32-bit
+// multiplies only, it runs for every record in the histogram and scatter
+// passes -- and a cheaper second mix in the low word.
+__device__ __host__ inline uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
 __device__ __host__ inline uint64_t key_hash(uint32_t key) {
-  return mix64((uint64_t)key * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull);
+  const uint32_t h = fmix32(key * 0x9E3779B1u + 0x632BE59Bu);
+  return ((uint64_t)h << 32) | (uint32_t)((h * 0x27D4EB2Fu) ^ key);
 }
 __device__ __host__ inline int log2_exact(uint32_t g) {  // -1 unless g is a power of two
   if (g == 0 || (g & (g - 1))) return -1;

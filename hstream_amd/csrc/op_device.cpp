@@ -5,8 +5,10 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "hsg_internal.h"
 #include "hsg_ops.h"
@@ -613,6 +615,65 @@ int op_copy_rows(OpDevice &d, const OutCols &src, uint64_t from, uint64_t n, int
   return HSG_OK;
 }
 
+// A dump lists the rows in (key, window start, window end) order, the order of
+// the reference's ordered stores (ksDump / ssDump over Data.Map, Store.hs:81,
+// 238-241), independent of where the rows sit in the HBM table. Host-side
+// permutation of the caller's columns (views are read back rarely; the rows
+// of a device-memory dump make one round trip).
+static int sort_dump_rows(OpDevice &d, const hsg_rows *out, uint64_t n, int n_aggs, std::string &err) {
+  if (n < 2) return HSG_OK;
+  const bool dev = out->mem == HSG_MEM_DEVICE;
+  const hipMemcpyKind d2h = hipMemcpyDeviceToHost, h2d = hipMemcpyHostToDevice;
+  std::vector<uint32_t> key(n);
+  std::vector<int64_t> ws(n), we(n);
+  std::vector<std::vector<int64_t>> cols;  // src + aggs, 8-byte words
+  std::vector<int64_t *> ptrs;
+  if (out->src_index) ptrs.push_back(out->src_index);
+  for (int j = 0; j < n_aggs && out->aggs; ++j)
+    if (out->aggs[j]) ptrs.push_back((int64_t *)out->aggs[j]);
+  auto fetch = [&](void *dst, const void *src, uint64_t bytes) -> int {
+    if (dev) DTRY(hipMemcpy(dst, src, bytes, d2h));
+    else memcpy(dst, src, bytes);
+    return HSG_OK;
+  };
+  auto store = [&](void *dst, const void *src, uint64_t bytes) -> int {
+    if (dev) DTRY(hipMemcpy(dst, src, bytes, h2d));
+    else memcpy(dst, src, bytes);
+    return HSG_OK;
+  };
+  if (!out->key_id || !out->win_start || !out->win_end) return HSG_OK;  // nothing to order by
+  int rc = fetch(key.data(), out->key_id, n * 4);
+  if (rc == HSG_OK) rc = fetch(ws.data(), out->win_start, n * 8);
+  if (rc == HSG_OK) rc = fetch(we.data(), out->win_end, n * 8);
+  cols.resize(ptrs.size());
+  for (size_t c = 0; rc == HSG_OK && c < ptrs.size(); ++c) {
+    cols[c].resize(n);
+    rc = fetch(cols[c].data(), ptrs[c], n * 8);
+  }
+  if (rc != HSG_OK) return rc;
+  std::vector<uint64_t> ord(n);
+  for (uint64_t i = 0; i < n; ++i) ord[i] = i;
+  std::stable_sort(ord.begin(), ord.end(), [&](uint64_t a, uint64_t b) {
+    if (key[a] != key[b]) return key[a] < key[b];
+    if (ws[a] != ws[b]) return ws[a] < ws[b];
+    return we[a] < we[b];
+  });
+  auto permute = [&](auto &v) {
+    auto tmp = v;
+    for (uint64_t i = 0; i < n; ++i) v[i] = tmp[ord[i]];
+  };
+  permute(key);
+  permute(ws);
+  permute(we);
+  for (auto &c : cols) permute(c);
+  rc = store(out->key_id, key.data(), n * 4);
+  if (rc == HSG_OK) rc = store(out->win_start, ws.data(), n * 8);
+  if (rc == HSG_OK) rc = store(out->win_end, we.data(), n * 8);
+  for (size_t c = 0; rc == HSG_OK && c < ptrs.size(); ++c) rc = store(ptrs[c], cols[c].data(), n * 8);
+  (void)d;
+  return rc;
+}
+
 int op_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hsg_rows *out, uint64_t *n_out,
             std::string &err) {
   int rc = fetch_scalars(d, err);
@@ -658,6 +719,7 @@ int op_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hs
     rc = tw_dump_spilled(d, cfg, prog, out, *n_out, &more, err);
     *n_out += more;
   }
+  if (rc == HSG_OK) rc = sort_dump_rows(d, out, *n_out, cfg.n_aggs, err);
   return rc;
 }
 

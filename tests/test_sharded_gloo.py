@@ -43,10 +43,26 @@ def mix64(x):
     return x
 
 
-def key_hash(key):
-    """hsg_internal.h key_hash: mix64(key * golden + c)"""
+def fmix32(h):
+    """hsg_internal.h fmix32 (murmur3's 32-bit finaliser)"""
+    h = np.asarray(h, np.uint32)
     with np.errstate(over="ignore"):
-        return mix64(np.asarray(key, np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(0x632BE59BD9B4E019))
+        h = h ^ (h >> np.uint32(16))
+        h = h * np.uint32(0x85EBCA6B)
+        h = h ^ (h >> np.uint32(13))
+        h = h * np.uint32(0xC2B2AE35)
+        h = h ^ (h >> np.uint32(16))
+    return h
+
+
+def key_hash(key):
+    """hsg_internal.h key_hash: fmix32(key * golden32 + c) in the high word, a
+    second mix in the low word"""
+    k = np.asarray(key, np.uint32)
+    with np.errstate(over="ignore"):
+        h = fmix32(k * np.uint32(0x9E3779B1) + np.uint32(0x632BE59B))
+        lo = (h * np.uint32(0x27D4EB2F)) ^ k
+    return (h.astype(np.uint64) << np.uint64(32)) | lo.astype(np.uint64)
 
 
 def owner_of(key, G):
