@@ -46,6 +46,12 @@ struct SessTable {
 struct OpDevice {
   hipStream_t stream = nullptr;
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr, ev_d = nullptr;
+  // the time-window table is cleared on a side stream by hsg_op_reset, so the
+  // next batch's partition passes (which do not touch it) overlap the clear;
+  // the first kernel that touches the table waits for it (wait_table_reset)
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_reset = nullptr, ev_pre = nullptr;
+  bool reset_pending = false;
   DevScalars *sc = nullptr;     // device
   DevScalars *h_sc = nullptr;   // pinned host mirror
   bool sc_clean = false;        // per-batch scalars already cleared on the stream
@@ -165,6 +171,8 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
 int tw_dump_spilled(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hsg_rows *out,
                     uint64_t dst_off, uint64_t *n_out, std::string &err);
 void tw_retention_reset(OpDevice &d);
+// order the op's stream after a pending table clear (no-op when none)
+void wait_table_reset(OpDevice &d);
 int op_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hsg_rows *out, uint64_t *n_out,
             std::string &err);
 

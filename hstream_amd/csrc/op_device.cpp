@@ -152,6 +152,12 @@ static void adapt_partitions(OpDevice &d, const hsg_op_config &cfg, const Progra
   d.rbits = d.pane_S ? rb : 0;
 }
 
+void wait_table_reset(OpDevice &d) {
+  if (!d.reset_pending) return;
+  hipStreamWaitEvent(d.stream, d.ev_reset, 0);
+  d.reset_pending = false;
+}
+
 int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err) {
   DTRY(hipMemsetAsync(d.sc, 0, sizeof(DevScalars), d.stream));
   memset(d.h_sc, 0, sizeof(DevScalars));  // host mirror (epoch_set gates the optimistic path)
@@ -160,7 +166,13 @@ int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, 
     int rc = session_device_reset(d, err);
     if (rc != HSG_OK) return rc;
   } else {
-    launch_tw_reset(d.stream, d.tw, prog);
+    // the clear runs on the side stream after everything queued on the op's
+    // stream; kernels that touch the table wait for it (wait_table_reset)
+    DTRY(hipEventRecord(d.ev_pre, d.stream));
+    DTRY(hipStreamWaitEvent(d.aux, d.ev_pre, 0));
+    launch_tw_reset(d.aux, d.tw, prog);
+    DTRY(hipEventRecord(d.ev_reset, d.aux));
+    d.reset_pending = true;
     tw_retention_reset(d);
     if (cfg.window_kind == HSG_UNWINDOWED) {
       // one implicit window: k = 0, epoch fixed at 0
@@ -184,6 +196,9 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
   // after a key exchange a rank can receive up to nranks * batch_cap records
   d.batch_cap = batch_cap * (uint64_t)nranks;
   DTRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  DTRY(hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
+  DTRY(hipEventCreateWithFlags(&d.ev_reset, hipEventDisableTiming));
+  DTRY(hipEventCreateWithFlags(&d.ev_pre, hipEventDisableTiming));
   DTRY(hipEventCreate(&d.ev_a));
   DTRY(hipEventCreate(&d.ev_b));
   DTRY(hipEventCreate(&d.ev_c));
@@ -253,6 +268,7 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
 }
 
 void op_device_free(OpDevice &d) {
+  if (d.aux) hipStreamSynchronize(d.aux);
   if (d.stream) hipStreamSynchronize(d.stream);
   exchange_device_free(d);
   dfree(d.sc);
@@ -295,6 +311,12 @@ void op_device_free(OpDevice &d) {
   d.ev_a = d.ev_b = d.ev_c = d.ev_d = nullptr;
   if (d.stream) hipStreamDestroy(d.stream);
   d.stream = nullptr;
+  if (d.aux) hipStreamDestroy(d.aux);
+  d.aux = nullptr;
+  if (d.ev_reset) hipEventDestroy(d.ev_reset);
+  if (d.ev_pre) hipEventDestroy(d.ev_pre);
+  d.ev_reset = d.ev_pre = nullptr;
+  d.reset_pending = false;
 }
 
 // Resolve the batch into device pointers, copying host arrays into staging.
@@ -478,11 +500,13 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc, can_pack, !skipped_wide);
       const bool emit_batch = cfg.emit_mode == HSG_EMIT_PER_BATCH;
       bool lean = false;
+      wait_table_reset(d);  // the partition passes above do not touch the table
       launch_part_agg(d.stream, prog, p, pp, d.tw, d.part, kb.n, d.sc, can_pack, emit_batch ? &d.out : nullptr,
                       a.pending, d.out_cap, !skipped_wide, &lean);
       if (!lean) skipped_wide = false;  // the general kernel ran both layouts
       skipped_emit = emit_batch && d.pred_direct;  // the lean or the deferred (k_seg_apply) path
     } else {
+      wait_table_reset(d);
       launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, false);
     }
     if (has_last(prog)) launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, true);
@@ -676,6 +700,7 @@ static int sort_dump_rows(OpDevice &d, const hsg_rows *out, uint64_t n, int n_ag
 
 int op_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hsg_rows *out, uint64_t *n_out,
             std::string &err) {
+  wait_table_reset(d);
   int rc = fetch_scalars(d, err);
   if (rc != HSG_OK) return rc;
   uint64_t live = d.h_sc->live;

@@ -118,6 +118,7 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
   const uint64_t live = d.h_sc->live;
   const uint64_t bound = n_in * d.wpr;
   if (!reopen && 4 * (live + bound) <= 3 * d.cap) return HSG_OK;
+  wait_table_reset(d);
   const TwParams p = retention_params(cfg, wm_in);
   // small pinned block for the counters read back here
   uint64_t *h = nullptr;

@@ -87,6 +87,7 @@ int perrecord_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &
 
 int push_time_perrecord(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
                         const Batch &kb, const int64_t *seq, const int64_t *rec_wm, PushResult &r, std::string &err) {
+  wait_table_reset(d);
   TwParams p = make_tw_params(cfg, a);
   int rc = clear_batch_scalars(d, err);
   if (rc != HSG_OK) return rc;
