@@ -451,9 +451,14 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const PG &pr
   // pane mode: a key's panes become neighbours in pane order
   if (S > 1 && nl > 1) group_live<MS, E, NT>(L, nl);
   t_sort += wall_clock64() - t0;
-  // owned window run of every pane: [max(P - n + 1, previous pane + 1), P]
+  // owned window run of every pane: [max(P - n + 1, previous pane + 1), P];
+  // each thread takes a contiguous range of the (key-grouped) live list, so
+  // the window positions below follow pane order
+  const uint32_t per = (nl + NT - 1) / NT;
+  const uint32_t q0 = threadIdx.x * per < nl ? threadIdx.x * per : nl;
+  const uint32_t q1 = q0 + per < nl ? q0 + per : nl;
   uint32_t cnt = 0;
-  for (uint32_t q = threadIdx.x; q < nl; q += NT) {
+  for (uint32_t q = q0; q < q1; ++q) {
     const int e = L.live[q];
     const uint64_t g = L.key[e];
     const uint32_t P = (uint32_t)g;
@@ -465,7 +470,7 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const PG &pr
     L.run[e] = (uint8_t)(P - a);
     cnt += P - a + 1;
   }
-  // block exclusive scan of the window counts -> changelog list positions
+  // block exclusive scan of the window counts -> positions in the flush
   const uint64_t incl = wave_incl_sum((uint64_t)cnt);
   if (lane == 63) L.wsum[wv] = (uint32_t)incl;
   __syncthreads();
@@ -473,6 +478,17 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const PG &pr
   for (int k = 0; k < NT / 64; ++k) {
     if (k < wv) o += L.wsum[k];
     total += L.wsum[k];
+  }
+  // first window position of every pane (reusing the grouping counters), so
+  // that the windows can be spread one per thread: a key's first pane in the
+  // batch owns up to size / advance windows, the others one each
+  constexpr bool kSpread = PaneGroup<MS, E>::kCount;
+  if constexpr (kSpread) {
+    uint32_t run = (uint32_t)o;
+    for (uint32_t q = q0; q < q1; ++q) {
+      L.pg.cnt[q] = run;
+      run += L.run[L.live[q]] + 1u;
+    }
   }
   if (threadIdx.x == 0) {
     // deferred to k_seg_apply when this workgroup owns the bucket and the
@@ -498,50 +514,62 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const PG &pr
   __syncthreads();
   const bool dnow = L.dnow != 0;
   const uint64_t pw = 1 + (uint64_t)prog.n();  // pane entry words
-  for (uint32_t q = threadIdx.x; q < nl; q += NT) {
+  // window w of the key of pane q (w in q's run): pane q plus the key's later
+  // panes up to w + SW - 1, then its update at position `at`
+  auto emit_window = [&](uint32_t q, uint32_t w, uint64_t at) {
     const int e = L.live[q];
     const uint64_t g = L.key[e];
     const uint64_t kb = g & 0xFFFFFFFF00000000ull;
-    const uint32_t P = (uint32_t)g;
-    const uint32_t a = P - L.run[e];
-    int64_t acc[MS];
+    int64_t v[MS];
 #pragma unroll
-    for (int s = 0; s < MS; ++s) acc[s] = L.agg[s * E + e];
-    // later panes of the key (after q) that window w covers: pane <= w + SW - 1
-    uint32_t j = q + 1;
-    uint64_t top = (uint64_t)a + SW - 1;
-    for (uint32_t w = a;; ++w) {
-      while (S > 1 && j < nl) {
-        const int f = L.live[j];
-        const uint64_t gj = L.key[f];
-        if ((gj & 0xFFFFFFFF00000000ull) != kb || (uint64_t)(uint32_t)gj > top) break;
-        acc_combine<MS, E>(prog, acc, &L.agg[f]);
-        ++j;
+    for (int s = 0; s < MS; ++s) v[s] = L.agg[s * E + e];
+    const uint64_t top = (uint64_t)w + SW - 1;
+    for (uint32_t j = q + 1; S > 1 && j < nl; ++j) {
+      const int f = L.live[j];
+      const uint64_t gj = L.key[f];
+      if ((gj & 0xFFFFFFFF00000000ull) != kb || (uint64_t)(uint32_t)gj > top) break;
+      acc_combine<MS, E>(prog, v, &L.agg[f]);
+    }
+    if (skip) {
+      // COUNT(col) slots not kept in LDS: every record of the batch has the column
+#pragma unroll
+      for (int s = 0; s < MS; ++s)
+        if ((skip >> s) & 1u) v[s] = v[cnt_all_slot];
+    }
+    if (dnow) {
+      // the window's update for k_seg_apply: [g][slot 0 .. n-1]
+      uint64_t *ent = pb.pane + (L.pbase + at) * pw;
+      ent[0] = kb | w;
+#pragma unroll
+      for (int s = 0; s < MS; ++s)
+        if (s < prog.n()) ent[1 + s] = (uint64_t)v[s];
+    } else {
+      const uint32_t sl = flush_window<MS>(prog, p, t, kb | w, v, exclusive, fresh, err, plain_claim);
+      if (L.base + at < pb.touched_cap) pb.touched[L.base + at] = sl;
+      else err |= ERR_OOM;
+    }
+  };
+  if constexpr (kSpread) {
+    // one thread per window: its pane by binary search over the positions
+    for (uint32_t at = threadIdx.x; at < total; at += NT) {
+      uint32_t lo = 0, hi = nl;  // last pane whose first position is <= at
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (L.pg.cnt[mid] <= at) lo = mid;
+        else hi = mid;
       }
-      int64_t v[MS];
-#pragma unroll
-      for (int s = 0; s < MS; ++s) v[s] = acc[s];
-      if (skip) {
-        // COUNT(col) slots not kept in LDS: every record of the batch has the column
-#pragma unroll
-        for (int s = 0; s < MS; ++s)
-          if ((skip >> s) & 1u) v[s] = v[cnt_all_slot];
+      const int e = L.live[lo];
+      const uint32_t P = (uint32_t)L.key[e];
+      emit_window(lo, P - L.run[e] + (at - L.pg.cnt[lo]), at);
+    }
+  } else {
+    for (uint32_t q = q0; q < q1; ++q) {
+      const int e = L.live[q];
+      const uint32_t P = (uint32_t)L.key[e];
+      for (uint32_t w = P - L.run[e];; ++w) {
+        emit_window(q, w, o++);
+        if (w == P) break;
       }
-      if (dnow) {
-        // the window's update for k_seg_apply: [g][slot 0 .. n-1]
-        uint64_t *ent = pb.pane + (L.pbase + o) * pw;
-        ent[0] = kb | w;
-#pragma unroll
-        for (int s = 0; s < MS; ++s)
-          if (s < prog.n()) ent[1 + s] = (uint64_t)v[s];
-      } else {
-        const uint32_t sl = flush_window<MS>(prog, p, t, kb | w, v, exclusive, fresh, err, plain_claim);
-        if (L.base + o < pb.touched_cap) pb.touched[L.base + o] = sl;
-        else err |= ERR_OOM;
-      }
-      ++o;
-      if (w == P) break;
-      ++top;
     }
   }
   __syncthreads();
