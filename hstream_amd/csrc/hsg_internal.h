@@ -140,7 +140,12 @@ struct TwTable {
   uint64_t rmask;   // slots per region - 1 (regions = 2^rbits, see hsg_tw.h)
   int32_t rbits;    // region bits of the key hash (below the owner bits)
   int32_t bshift;   // owner bits of the key hash (multi-GPU)
+  uint8_t *dirty;   // [cap / 8]: 8-slot blocks claimed since the last clear (null: not kept)
   __host__ __device__ uint64_t *key(uint64_t s) const { return rows + s * stride; }
+  // every claim marks its block, so a clear rewrites only the claimed blocks
+  __device__ void mark(uint64_t s) const {
+    if (dirty) dirty[s >> 3] = 1;
+  }
   __host__ __device__ uint32_t *stamp(uint64_t s) const { return (uint32_t *)(rows + s * stride + 1); }
   __host__ __device__ int64_t *aggs(uint64_t s) const { return (int64_t *)(rows + s * stride + 2); }
 };
@@ -227,7 +232,13 @@ void launch_copy_rows(hipStream_t s, const OutCols &src, uint64_t from, uint64_t
 void launch_fill_u64(hipStream_t s, uint64_t *p, uint64_t n, uint64_t v);
 void launch_fill_rows(hipStream_t s, int64_t *aggs, uint64_t rows, const Program &prog);
 // every row of a time-window table: key EMPTY, stamp 0, aggregate identities
+// whole table (and its dirty map, when kept)
 void launch_tw_reset(hipStream_t s, const TwTable &t, const Program &prog);
+// only the blocks the dirty map marks (the map must cover every claim since
+// the last launch_tw_reset); *cnt (device) <- the dirty blocks counted
+void launch_tw_reset_dirty(hipStream_t s, const TwTable &t, const Program &prog, uint64_t *cnt);
+// one byte per 8-slot block, padded to 16 bytes
+inline uint64_t tw_dirty_bytes(uint64_t cap) { return ((cap >> 3) + 16) & ~15ull; }
 void launch_fill_u32(hipStream_t s, uint32_t *p, uint64_t n, uint32_t v);
 
 // stream time: tile maxima -> exclusive tile prefix (+ epoch init)

@@ -52,6 +52,14 @@ struct OpDevice {
   hipStream_t aux = nullptr;
   hipEvent_t ev_reset = nullptr, ev_pre = nullptr;
   bool reset_pending = false;
+  // dirty-block map of the table (hsg_internal.h TwTable::dirty): tw.dirty is
+  // the map while claims mark it, null once a clear found most blocks dirty
+  // (marking then costs more than it saves; whole-table clears from then on)
+  bool tw_map_valid = false;  // tw.dirty covers every claim since the last whole-table clear
+  uint8_t *tw_dirty_mem = nullptr;
+  uint64_t *tw_cnt = nullptr;    // device: dirty blocks the last clear counted
+  uint64_t *h_tw_cnt = nullptr;  // pinned copy (read at the next reset)
+  bool tw_cnt_pending = false;
   DevScalars *sc = nullptr;     // device
   DevScalars *h_sc = nullptr;   // pinned host mirror
   bool sc_clean = false;        // per-batch scalars already cleared on the stream

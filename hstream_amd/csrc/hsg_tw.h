@@ -49,6 +49,7 @@ __device__ inline int64_t tw_find_or_insert(const TwTable &t, uint64_t g, uint32
       uint64_t old =
           atomicCAS((unsigned long long *)t.key(base + s), (unsigned long long)kEmpty, (unsigned long long)g);
       if (old == kEmpty) {
+        t.mark(base + s);
         fresh += 1;
         return (int64_t)(base + s);
       }
@@ -74,6 +75,7 @@ __device__ inline int64_t tw_claim_exclusive(const TwTable &t, uint64_t g, uint3
       uint64_t expected = kEmpty;
       if (__hip_atomic_compare_exchange_strong(t.key(base + s), &expected, g, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        t.mark(base + s);
         fresh += 1;
         return (int64_t)(base + s);
       }

@@ -281,6 +281,7 @@ __device__ inline int64_t tw_claim_lds(const TwTable &t, uint64_t g, uint32_t *c
     if (cur == g) return (int64_t)(base + s);
     if (cur == kEmpty && claim_set_insert(cset, (uint32_t)(base + s))) {
       *t.key(base + s) = g;
+      t.mark(base + s);
       fresh += 1;
       return (int64_t)(base + s);
     }
@@ -523,6 +524,7 @@ __device__ inline int64_t tw_claim_seg(const TwTable &t, uint64_t g, uint32_t *c
     if (cur == g) return (int64_t)(base + s);
     if (cur == kEmpty && seg_claim_insert(cset, (uint32_t)(base + s))) {
       *t.key(base + s) = g;
+      t.mark(base + s);
       fresh += 1;
       return (int64_t)(base + s);
     }

@@ -56,6 +56,62 @@ __global__ __launch_bounds__(256) void k_tw_reset(TwTable t, Program prog) {
   }
 }
 
+// Clear of the claimed blocks only (t.dirty): a table sized for the worst
+// batch holds few groups at a reset (C2: 4.3M of 32M slots, in ~1/8 of the
+// blocks since a key's windows share a block), so this rewrites the rows of
+// the claimed blocks instead of streaming the whole table. k_tw_dirty_count
+// counts them first; when more than half the blocks are dirty (one-window
+// keys spread over the table, C5) the whole table is streamed as by
+// k_tw_reset. A lane per map byte; a dirty block's 8 rows are written by its
+// wave, 16 bytes per lane and store, one block after another (ballot order).
+__global__ __launch_bounds__(256) void k_tw_dirty_count(TwTable t, uint64_t nblk, unsigned long long *cnt) {
+  uint64_t c = 0;
+  const uint4 *m = reinterpret_cast<const uint4 *>(t.dirty);
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; 16 * i < nblk; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint4 v = m[i];  // the map is padded to 16 bytes (tw_dirty_bytes); bytes past nblk stay 0
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      c += ((w[k] & 0xFFu) != 0) + ((w[k] & 0xFF00u) != 0) + ((w[k] & 0xFF0000u) != 0) + ((w[k] >> 24) != 0);
+  }
+  c = wave_sum_u64(c);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, (unsigned long long)c);
+}
+
+__global__ __launch_bounds__(256) void k_tw_reset_dirty(TwTable t, Program prog, uint64_t nblk, const uint64_t *cnt) {
+  if (2 * *cnt > nblk) {  // uniform: most blocks dirty, stream the table and the map
+    const uint64_t pairs = (t.mask + 1) * (uint64_t)t.stride / 2;
+    const uint32_t sp = t.stride / 2;
+    ulonglong2 *rows = reinterpret_cast<ulonglong2 *>(t.rows);
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < pairs; i += step) {
+      const uint32_t wi = 2u * (uint32_t)(i % sp);
+      rows[i] = make_ulonglong2(tw_empty_word(prog, wi), tw_empty_word(prog, wi + 1));
+    }
+    uint4 *m = reinterpret_cast<uint4 *>(t.dirty);
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; 16 * i < nblk; i += step) m[i] = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const uint32_t bw = 8u * t.stride;  // words of a block
+  const uint64_t waves = (uint64_t)gridDim.x * 4, w0 = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  for (uint64_t i0 = w0 * 64; i0 < nblk; i0 += waves * 64) {
+    const uint64_t i = i0 + lane;
+    const bool d = i < nblk && t.dirty[i] != 0;
+    uint64_t m = __ballot(d);
+    if (d) t.dirty[i] = 0;
+    while (m) {
+      const int j = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      ulonglong2 *rows = reinterpret_cast<ulonglong2 *>(t.rows + (i0 + j) * bw);
+      for (uint32_t q = lane; 2 * q < bw; q += 64) {
+        const uint32_t wi = (2u * q) % t.stride;
+        rows[q] = make_ulonglong2(tw_empty_word(prog, wi), tw_empty_word(prog, wi + 1));
+      }
+    }
+  }
+}
+
 // per-batch scalars: err .. touched, redo and scratch (wm / epoch / live persist)
 __global__ void k_clear_scalars(DevScalars *sc) {
   const int t = threadIdx.x;
@@ -106,6 +162,15 @@ void launch_fill_u32(hipStream_t s, uint32_t *p, uint64_t n, uint32_t v) {
 }
 void launch_tw_reset(hipStream_t s, const TwTable &t, const Program &prog) {
   hipLaunchKernelGGL(k_tw_reset, dim3(4096), dim3(256), 0, s, t, prog);
+  if (t.dirty) hipMemsetAsync(t.dirty, 0, tw_dirty_bytes(t.mask + 1), s);
+}
+void launch_tw_reset_dirty(hipStream_t s, const TwTable &t, const Program &prog, uint64_t *cnt) {
+  const uint64_t nblk = (t.mask + 1) >> 3;
+  if (!nblk) return launch_tw_reset(s, t, prog);
+  hipMemsetAsync(cnt, 0, 8, s);
+  hipLaunchKernelGGL(k_tw_dirty_count, dim3(grid_for(nblk / 16 + 1, 256)), dim3(256), 0, s, t, nblk,
+                     (unsigned long long *)cnt);
+  hipLaunchKernelGGL(k_tw_reset_dirty, dim3(4096), dim3(256), 0, s, t, prog, nblk, (const uint64_t *)cnt);
 }
 void launch_fill_rows(hipStream_t s, int64_t *aggs, uint64_t rows, const Program &prog) {
   if (rows && prog.n_slots)

@@ -170,7 +170,25 @@ int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, 
     // stream; kernels that touch the table wait for it (wait_table_reset)
     DTRY(hipEventRecord(d.ev_pre, d.stream));
     DTRY(hipStreamWaitEvent(d.aux, d.ev_pre, 0));
-    launch_tw_reset(d.aux, d.tw, prog);
+    // (only the blocks claimed since the last clear, once the dirty map is
+    // valid; HSG_TW_FULL_RESET: always the whole table)
+    static const bool full = getenv("HSG_TW_FULL_RESET") != nullptr;
+    if (d.tw_cnt_pending) {  // the previous clear's count (long finished)
+      DTRY(hipEventSynchronize(d.ev_reset));
+      d.tw_cnt_pending = false;
+      if (2 * *d.h_tw_cnt > ((d.tw.mask + 1) >> 3)) {
+        d.tw.dirty = nullptr;
+        d.tw_map_valid = false;
+      }
+    }
+    if (d.tw_map_valid && !full) {
+      launch_tw_reset_dirty(d.aux, d.tw, prog, d.tw_cnt);
+      DTRY(hipMemcpyAsync(d.h_tw_cnt, d.tw_cnt, 8, hipMemcpyDeviceToHost, d.aux));
+      d.tw_cnt_pending = true;
+    } else {
+      launch_tw_reset(d.aux, d.tw, prog);
+    }
+    d.tw_map_valid = d.tw.dirty != nullptr;
     DTRY(hipEventRecord(d.ev_reset, d.aux));
     d.reset_pending = true;
     tw_retention_reset(d);
@@ -227,6 +245,10 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
   } else {
     d.tw.stride = tw_row_stride(prog.n_slots);
     DTRY(dalloc(&d.tw.rows, d.cap * (uint64_t)d.tw.stride));
+    DTRY(dalloc(&d.tw_dirty_mem, tw_dirty_bytes(d.cap)));
+    d.tw.dirty = d.tw_dirty_mem;
+    DTRY(dalloc(&d.tw_cnt, 1));
+    DTRY(hipHostMalloc((void **)&d.h_tw_cnt, 8, hipHostMallocDefault));
     tw_configure(d.tw, d.cap, cfg.window_kind);
     d.tw.bshift = 0;  // set with the exchange (exchange_device_init)
     uint64_t nb = emit_chunks(d.cap);
@@ -286,6 +308,10 @@ void op_device_free(OpDevice &d) {
   dfree(d.st_seq);
   dfree(d.st_wm);
   dfree(d.tw.rows);
+  dfree(d.tw_dirty_mem);
+  dfree(d.tw_cnt);
+  if (d.h_tw_cnt) hipHostFree(d.h_tw_cnt);
+  d.h_tw_cnt = nullptr;
   dfree(d.emit.cnt);
   dfree(d.emit.off);
   dfree(d.emit.partial);

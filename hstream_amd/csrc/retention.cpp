@@ -133,7 +133,7 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
       if (p) hipFree(p);
     }
   };
-  DevFree dw, dense, up, fresh;
+  DevFree dw, dense, up, fresh, fresh_map;
   uint64_t *dwords = nullptr;  // [0] closed total, [1] rows kept by the rebuild
   DTRY(hipMalloc((void **)&dwords, 2 * sizeof(uint64_t)));
   dw.p = dwords;
@@ -159,6 +159,11 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
   nt.rows = nullptr;
   DTRY(hipMalloc((void **)&nt.rows, ncap * (uint64_t)nt.stride * 8));
   fresh.p = nt.rows;
+  if (d.tw.dirty) {  // claims still mark: a map for the new table
+    nt.dirty = nullptr;
+    DTRY(hipMalloc((void **)&nt.dirty, tw_dirty_bytes(ncap)));
+    fresh_map.p = nt.dirty;
+  }
   tw_configure(nt, ncap, cfg.window_kind);
   if (closed) DTRY(hipMalloc(&dense.p, closed * d.tw.stride * 8));
   if (back) DTRY(hipMalloc(&up.p, back * d.tw.stride * 8));
@@ -191,8 +196,13 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
   if (((uint32_t)h[2] & ERR_OOM) || h[1] != keep) return undo("table rebuild: rows lost (internal)", HSG_E_DEVICE);
   // commit
   fresh.p = nullptr;
+  fresh_map.p = nullptr;
   hipFree(d.tw.rows);
-  d.tw = nt;
+  if (nt.dirty) {
+    hipFree(d.tw_dirty_mem);
+    d.tw_dirty_mem = nt.dirty;
+  }
+  d.tw = nt;  // its dirty map: cleared with it, then marked by the reinsert
   if (closed) {
     d.spilled_rows += closed;
     d.spill_events += 1;
