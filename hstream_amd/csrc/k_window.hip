@@ -62,8 +62,7 @@ __global__ __launch_bounds__(256) void k_tw_reset(TwTable t, Program prog) {
 // the claimed blocks instead of streaming the whole table. k_tw_dirty_count
 // counts them first; when more than half the blocks are dirty (one-window
 // keys spread over the table, C5) the whole table is streamed as by
-// k_tw_reset. A lane per map byte; a dirty block's 8 rows are written by its
-// wave, 16 bytes per lane and store, one block after another (ballot order).
+// k_tw_reset.
 __global__ __launch_bounds__(256) void k_tw_dirty_count(TwTable t, uint64_t nblk, unsigned long long *cnt) {
   uint64_t c = 0;
   const uint4 *m = reinterpret_cast<const uint4 *>(t.dirty);
@@ -78,36 +77,52 @@ __global__ __launch_bounds__(256) void k_tw_dirty_count(TwTable t, uint64_t nblk
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, (unsigned long long)c);
 }
 
+// position of the r-th set bit of m (r < popcount(m)): binary search on
+// popcounts of the low halves
+__device__ inline uint32_t kth_set_bit(uint64_t m, uint32_t r) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t w = 32; w; w >>= 1) {
+    const uint32_t c = (uint32_t)__popcll((m >> pos) & ((1ull << w) - 1));
+    if (c <= r) {
+      r -= c;
+      pos += w;
+    }
+  }
+  return pos;
+}
+
 __global__ __launch_bounds__(256) void k_tw_reset_dirty(TwTable t, Program prog, uint64_t nblk, const uint64_t *cnt) {
+  const uint32_t sp = t.stride / 2;
+  const bool pow2 = (sp & (sp - 1)) == 0;
+  ulonglong2 *rows = reinterpret_cast<ulonglong2 *>(t.rows);
   if (2 * *cnt > nblk) {  // uniform: most blocks dirty, stream the table and the map
-    const uint64_t pairs = (t.mask + 1) * (uint64_t)t.stride / 2;
-    const uint32_t sp = t.stride / 2;
-    ulonglong2 *rows = reinterpret_cast<ulonglong2 *>(t.rows);
+    const uint64_t pairs = (t.mask + 1) * (uint64_t)sp;
     const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < pairs; i += step) {
-      const uint32_t wi = 2u * (uint32_t)(i % sp);
+      const uint32_t wi = 2u * (pow2 ? (uint32_t)(i & (sp - 1)) : (uint32_t)(i % sp));
       rows[i] = make_ulonglong2(tw_empty_word(prog, wi), tw_empty_word(prog, wi + 1));
     }
     uint4 *m = reinterpret_cast<uint4 *>(t.dirty);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; 16 * i < nblk; i += step) m[i] = make_uint4(0, 0, 0, 0);
     return;
   }
+  // a wave per 64 map bytes; the dirty blocks' 16-byte pairs spread over
+  // all 64 lanes (pair q: the (q / ppb)-th dirty block of the ballot)
   const int lane = threadIdx.x & 63;
-  const uint32_t bw = 8u * t.stride;  // words of a block
+  const uint32_t ppb = 8u * sp;  // pairs per block
   const uint64_t waves = (uint64_t)gridDim.x * 4, w0 = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   for (uint64_t i0 = w0 * 64; i0 < nblk; i0 += waves * 64) {
     const uint64_t i = i0 + lane;
     const bool d = i < nblk && t.dirty[i] != 0;
-    uint64_t m = __ballot(d);
+    const uint64_t m = __ballot(d);
     if (d) t.dirty[i] = 0;
-    while (m) {
-      const int j = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      ulonglong2 *rows = reinterpret_cast<ulonglong2 *>(t.rows + (i0 + j) * bw);
-      for (uint32_t q = lane; 2 * q < bw; q += 64) {
-        const uint32_t wi = (2u * q) % t.stride;
-        rows[q] = make_ulonglong2(tw_empty_word(prog, wi), tw_empty_word(prog, wi + 1));
-      }
+    const uint32_t total = (uint32_t)__popcll(m) * ppb;
+    for (uint32_t q = lane; q < total; q += 64) {
+      const uint32_t k = q / ppb, pr = q - k * ppb;
+      const uint64_t blk = i0 + kth_set_bit(m, k);
+      const uint32_t wi = 2u * (pow2 ? (pr & (sp - 1)) : (pr % sp));
+      rows[blk * ppb + pr] = make_ulonglong2(tw_empty_word(prog, wi), tw_empty_word(prog, wi + 1));
     }
   }
 }
