@@ -244,6 +244,9 @@ void launch_fill_u32(hipStream_t s, uint32_t *p, uint64_t n, uint32_t v);
 // stream time: tile maxima -> exclusive tile prefix (+ epoch init)
 void launch_tile_stats(hipStream_t s, const Batch &b, int64_t *tile_max, int64_t *tile_min, uint64_t n_tiles);
 // grace >= 0: also decide sc->no_late for a time-window op
+// window epoch from the first keyed record (ts >= 0) of the batch, when not
+// yet set: optimistic batches need no stream-time pass for it
+void launch_epoch_first(hipStream_t s, const Batch &b, int64_t adv, DevScalars *sc);
 void launch_tile_scan(hipStream_t s, const int64_t *tile_max, const int64_t *tile_min, int64_t *tile_prefix,
                       uint64_t n_tiles, int64_t wm_in, int64_t adv, bool set_epoch, DevScalars *sc,
                       int64_t grace = -1);

@@ -277,6 +277,36 @@ __global__ __launch_bounds__(1024) void k_tile_scan(const int64_t *__restrict__ 
   }
 }
 
+// One wave: the first keyed record with ts >= 0 (4 records per lane and
+// step; usually record 0) sets the epoch 2^31 windows below its window, so
+// the batch's windows fit 32 bits unless they span 2^31 windows. No keyed
+// record: the epoch stays unset, as with k_tile_scan.
+__global__ __launch_bounds__(64) void k_epoch_first(Batch b, int64_t adv, DevScalars *sc) {
+  if (sc->epoch_set) return;
+  const int lane = threadIdx.x;
+  for (uint64_t base = 0; base < b.n; base += 256) {
+    int64_t first = -1;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint64_t i = base + (uint64_t)u * 64 + lane;
+      const bool ok = i < b.n && b.key[i] != HSG_KEY_NONE && b.ts[i] >= 0;
+      const uint64_t m = __ballot(ok);
+      if (m && first < 0) first = (int64_t)(base + (uint64_t)u * 64 + (__ffsll((long long)m) - 1));
+    }
+    if (first >= 0) {  // uniform
+      if (lane == 0) {
+        const int64_t k0 = b.ts[first] / adv - (int64_t)(1ll << 31);
+        sc->k_epoch = k0 > 0 ? k0 : 0;
+        sc->epoch_set = 1;
+      }
+      return;
+    }
+  }
+}
+void launch_epoch_first(hipStream_t s, const Batch &b, int64_t adv, DevScalars *sc) {
+  hipLaunchKernelGGL(k_epoch_first, dim3(1), dim3(64), 0, s, b, adv, sc);
+}
+
 void launch_tile_stats(hipStream_t s, const Batch &b, int64_t *tile_max, int64_t *tile_min, uint64_t n_tiles) {
   if (n_tiles) hipLaunchKernelGGL(k_tile_stats, dim3((unsigned)n_tiles), dim3(kTileThreads), 0, s, b, tile_max, tile_min);
 }

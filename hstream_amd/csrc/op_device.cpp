@@ -478,9 +478,9 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
   // the stream-time inputs into the histogram pass and decide afterwards (one
   // tiny kernel); a batch that does have late records is run again with the
   // per-record stream time. Needs the window epoch (set by an earlier batch).
-  // The first batch after create/reset has no epoch yet: the stream-time pass
-  // sets it (device side) ahead of the optimistic kernels, which then run as on
-  // every later batch instead of the per-record stream-time path.
+  // The first batch after create/reset has no epoch yet: k_epoch_first sets it
+  // (device side) from the batch's first keyed record ahead of the optimistic
+  // kernels, which then run as on every later batch.
   const bool opt = d.use_part && !rec_wm && !has_last(prog) && cfg.grace_ms >= 0 && cfg.window_kind != HSG_SESSION;
   const bool need_epoch = !d.h_sc->epoch_set;
   // Launch prediction (speed only): the variants a batch does not take exit at
@@ -497,7 +497,10 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     if (!kb.n) return HSG_OK;
     // stream time (and the window epoch on the first batch); after a key exchange
     // the per-record stream time arrives in rec_wm and only the epoch is used
-    if (!optimistic || need_epoch) launch_stream_time(d, cfg, kb, a.wm_in, p.adv);
+    // the optimistic kernels fold stream time into the histogram; the first
+    // batch after create/reset takes its epoch from its first keyed record
+    if (!optimistic) launch_stream_time(d, cfg, kb, a.wm_in, p.adv);
+    else if (need_epoch) launch_epoch_first(d.stream, kb, p.adv, d.sc);
     DTRY(hipEventRecord(d.ev_a, d.stream));
     if (d.use_part) {
       PartParams pp;
