@@ -2,10 +2,21 @@
 """Benchmark: windowed GROUP BY records/s on MI355X (BASELINE.json metric).
 
 One step = one pass of the hot path over the configured workload: reset the
-operator's HBM state, push every batch of the (HBM-resident, synthetic) input
-through libhstream_gpu and drain each batch's changelog into HBM. Default
-workload = BASELINE config C2 (tumbling 60 s COUNT/SUM/AVG/MIN/MAX, 100M
-records, 64K uniform keys, batches of 2^24), which fits one GPU.
+operator's HBM state, push every batch of the synthetic input through
+libhstream_gpu and drain each batch's changelog into HBM. Default workload =
+BASELINE config C2 (tumbling 60 s COUNT/SUM/AVG/MIN/MAX, 100M records, 64K
+uniform keys, batches of 2^24), which fits one GPU.
+
+`value` is the harness contract's number: input resident in HBM when the
+timed region starts. The same JSON line also carries, at one rank:
+  host_input  BASELINE.md's reporting formula ("kernels plus H2D of the
+              input"): the same step with the batches handed over as pinned
+              host buffers through hsg_push_batch_async, whose H2D copies run
+              on the op's copy stream, overlapped with the previous batch's
+              kernels (PCIe fraction of the 63 GB/s host link);
+  per_record  the EMIT CHANGES changelog the drop-in wires:
+              one row per (record, window) in arrival order, its B_alg with
+              the E*O changelog bytes.
 
 Multi-GPU: launched by torch.distributed.run, one process per GPU; every rank
 ingests its own C2-sized slice (weak scaling) and the library exchanges
@@ -22,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+PCIE_PEAK_GBS = 63.0   # host link, PCIe Gen5 x16 (MI355X_MICROARCH.md, chip-level parameters)
 
 
 def parse():
@@ -37,6 +49,9 @@ def parse():
     p.add_argument("--traffic-csv", default="", help="rocprofv3 --pmc counter CSV to fill roofline.traffic")
     p.add_argument("--force-exchange", action="store_true", help="N=1 through the RCCL exchange path")
     p.add_argument("--copy-drain", action="store_true", help="drain by copy instead of the registered changelog")
+    p.add_argument("--no-host-input", action="store_true", help="skip the pinned-host-input (H2D) block")
+    p.add_argument("--no-per-record", action="store_true", help="skip the per-record (EMIT CHANGES) block")
+    p.add_argument("--extra-steps", type=int, default=3, help="timed steps of the host_input / per_record blocks")
     return p.parse_args()
 
 
@@ -148,36 +163,18 @@ def main():
     total_records = n_rank * world * args.steps
     value = total_records / elapsed
 
-    # roofline of the batch pipeline (one "launch" = one batch through the
-    # partition + aggregation + changelog kernels, timed by HIP events on the
-    # op's stream): SURVEY.md 8(d) algorithmic bytes
-    #   N*(4 + 8 + 8C) + 2*U*R + E*O
-    # N records, C value columns, U groups touched, R state row bytes (key +
-    # slots), E changelog rows, O row bytes (key 4, window 8 + 8, 8 per agg)
-    launches = st1["agg_kernel_launches"] - st0["agg_kernel_launches"]
-    agg_s = (st1["agg_kernel_ms"] - st0["agg_kernel_ms"]) / 1e3
-    ncol = len(spec.col_types)
-    rec_bytes = 4 + 8 + 8 * ncol
-    row_bytes = st1["state_row_bytes"]  # R of the device's own slot program (hsg_op_stats)
-    out_bytes = 4 + 8 + 8 + 8 * len(spec.aggs) if emit != abi.HSG_EMIT_NONE else 0
-    touched = st1["touched_total"] - st0["touched_total"]
-    emitted = touched if emit == abi.HSG_EMIT_PER_BATCH else 0
-    owned = (st1["records_owned"] - st0["records_owned"])
-    alg_bytes = owned * rec_bytes + 2 * touched * row_bytes + emitted * out_bytes
-    achieved = (alg_bytes / agg_s / 1e9) if agg_s > 0 else 0.0
+    roof = roofline(st0, st1, spec, emit)
     traffic, tsrc = None, None
     if args.traffic_csv:
-        traffic, tsrc = traffic_from_csv(args.traffic_csv, launches), args.traffic_csv
+        traffic, tsrc = traffic_from_csv(args.traffic_csv, cfg, args.emit), args.traffic_csv
     else:
         traffic, tsrc = committed_traffic(args, world)
-    roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-            "kernel": pipeline_name(cfg, args.emit),
-            "state_row_bytes": row_bytes,
-            "alg_bytes_per_launch": int(alg_bytes / max(1, launches)),
-            "avg_launch_ms": round(agg_s * 1e3 / max(1, launches), 4)}
+    roof["traffic"] = traffic
+    roof["kernel"] = pipeline_name(cfg, args.emit)
     if tsrc:
         roof["traffic_source"] = tsrc
+    agg_s = (st1["agg_kernel_ms"] - st0["agg_kernel_ms"]) / 1e3
+    touched = st1["touched_total"] - st0["touched_total"]
 
     xchg = None
     if world > 1 or args.force_exchange:
@@ -191,6 +188,17 @@ def main():
         xchg = {"bytes_per_step": int(xb_all / args.steps), "device_ms_per_step_per_rank":
                 round(xs_sum * 1e3 / args.steps / world, 3),
                 "xgmi_frac": round(xb_all / elapsed / links, 6) if world > 1 else None}
+
+    host_in = per_rec = None
+    if world == 1 and not args.force_exchange:
+        if not args.no_host_input:
+            host_in = host_input_block(op, keys, ts, cols, pieces, spec, emit, args, value)
+        del descs
+        op.close()
+        op = None
+        if (not args.no_per_record and cfg.window_kind in (abi.HSG_TUMBLING, abi.HSG_UNWINDOWED)
+                and emit != abi.HSG_EMIT_PER_RECORD):
+            per_rec = per_record_block(eng, cfg, keys, ts, cols, pieces, args)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -215,16 +223,171 @@ def main():
                        "parallelism": f"key-hash sharded x{world}" if world > 1 else "single GPU"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "host_input": host_in,
+            "per_record": per_rec,
             "exchange": xchg,
             "agg_kernel_share": round(agg_s / elapsed, 4) if elapsed > 0 else None,
             "pairs_per_step": int((st1["pairs_total"] - st0["pairs_total"]) / max(1, args.steps)),
             "touched_per_step": int(touched / max(1, args.steps)),
         }
         print(json.dumps(line), flush=True)
-    op.close()
+    if op is not None:
+        op.close()
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def roofline(st0, st1, spec, emit):
+    """Roofline of the batch pipeline: one "launch" = one batch through the
+    partition + aggregation + changelog kernels, timed by HIP events on the
+    op's stream (hsg_stats agg_kernel_ms). SURVEY.md 8(d) algorithmic bytes
+      N*(4 + 8 + 8C) + 2*U*R + E*O
+    N records, C value columns, U groups touched, R state row bytes (group key
+    + slots, from the device's own slot program), E changelog rows, O row
+    bytes (key 4, window 8 + 8, 8 per aggregate)."""
+    from hstream_amd import abi
+    launches = st1["agg_kernel_launches"] - st0["agg_kernel_launches"]
+    agg_s = (st1["agg_kernel_ms"] - st0["agg_kernel_ms"]) / 1e3
+    ncol = len(spec.col_types)
+    rec_bytes = 4 + 8 + 8 * ncol
+    row_bytes = st1["state_row_bytes"]
+    out_bytes = 4 + 8 + 8 + 8 * len(spec.aggs) if emit != abi.HSG_EMIT_NONE else 0
+    touched = st1["touched_total"] - st0["touched_total"]
+    pairs = st1["pairs_total"] - st0["pairs_total"]
+    emitted = {abi.HSG_EMIT_PER_BATCH: touched, abi.HSG_EMIT_PER_RECORD: pairs}.get(emit, 0)
+    owned = st1["records_owned"] - st0["records_owned"]
+    alg_bytes = owned * rec_bytes + 2 * touched * row_bytes + emitted * out_bytes
+    achieved = (alg_bytes / agg_s / 1e9) if agg_s > 0 else 0.0
+    return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+            "state_row_bytes": row_bytes, "out_row_bytes": out_bytes,
+            "alg_bytes_per_launch": int(alg_bytes / max(1, launches)),
+            "rows_emitted_per_launch": int(emitted / max(1, launches)),
+            "avg_launch_ms": round(agg_s * 1e3 / max(1, launches), 4)}
+
+
+def host_input_block(op, keys, ts, cols, pieces, spec, emit, args, hbm_value):
+    """BASELINE.md's reporting formula: the same steps with every batch handed
+    over as pinned host buffers (what a poll loop holds) through
+    hsg_push_batch_async. The library queues each batch's H2D copies on the
+    op's copy stream while the batch before it computes (op_prestage), so a
+    step costs max(PCIe, kernels) rather than their sum. The step's changelog
+    goes into device columns registered for the whole step, drained once."""
+    import ctypes as C
+    import torch
+    from hstream_amd import abi
+    from hstream_amd.columnar import make_batch
+    kh = keys.cpu().pin_memory()
+    th = ts.cpu().pin_memory()
+    chs = [c.cpu().pin_memory() for c in cols]
+    descs = [make_batch(kh[s:s + m], th[s:s + m], [c[s:s + m] for c in chs], None, abi.HSG_MEM_HOST)
+             for s, m in pieces]
+    wpr = -(-spec.size_ms // spec.advance_ms) if spec.window_kind == abi.HSG_HOPPING else 1
+    n_rank = sum(m for _, m in pieces)
+    cap = max(1, n_rank * wpr) if emit != abi.HSG_EMIT_NONE else 1
+    dev = keys.device
+    outs = {"key_id": torch.empty(cap, dtype=torch.int32, device=dev),
+            "win_start": torch.empty(cap, dtype=torch.int64, device=dev),
+            "win_end": torch.empty(cap, dtype=torch.int64, device=dev),
+            "src_index": torch.empty(cap, dtype=torch.int64, device=dev),
+            "aggs": [torch.empty(cap, dtype=torch.float64 if f else torch.int64, device=dev) for f in spec.agg_is_f64()]}
+    drain = make_device_drain(op, outs, cap, zero_copy=True)
+    lib = op._lib
+    wm = C.c_int64(-1)
+    no_cb = C.cast(None, abi.HSG_DONE_FN)  # no completion callback: hsg_op_wait below
+
+    def step():
+        op.reset()
+        wm.value = -1
+        for b, _keep in descs:
+            rc = lib.hsg_push_batch_async(op._h, C.byref(b), C.byref(wm), no_cb, None)
+            if rc != abi.HSG_OK:
+                op._check(rc, "push_batch_async")
+        rc = lib.hsg_op_wait(op._h)
+        if rc != abi.HSG_OK:
+            op._check(rc, "op_wait")
+        if emit != abi.HSG_EMIT_NONE:
+            drain()
+
+    torch.cuda.synchronize()
+    step()
+    torch.cuda.synchronize()
+    k = max(1, args.extra_steps)
+    t0 = time.perf_counter()
+    for _ in range(k):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    op.set_changelog(None)
+    rec_bytes = 4 + 8 + 8 * len(spec.col_types)
+    h2d = n_rank * rec_bytes * k
+    out = {"value": round(n_rank * k / el, 1), "unit": "records/s", "steps": k,
+           "ms_per_step": round(el * 1e3 / k, 3),
+           "input": "pinned host buffers, one hsg_push_batch_async per batch (H2D in the timed region)",
+           "h2d_bytes_per_step": n_rank * rec_bytes,
+           "pcie": {"achieved": round(h2d / el / 1e9, 3), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(h2d / el / 1e9 / PCIE_PEAK_GBS, 4)},
+           "vs_hbm_resident": round(n_rank * k / el / hbm_value, 4) if hbm_value else None}
+    del descs, kh, th, chs, outs
+    torch.cuda.empty_cache()
+    return out
+
+
+def per_record_block(eng, cfg, keys, ts, cols, pieces, args):
+    """The EMIT CHANGES changelog (HSG_EMIT_PER_RECORD: one row per accepted
+    (record, window) in arrival order, TimeWindowedStream.hs:89-103) over the
+    same HBM-resident input; its B_alg counts the E*O changelog bytes."""
+    import ctypes as C
+    import torch
+    from hstream_amd import abi
+    from hstream_amd.columnar import make_batch
+    emit = abi.HSG_EMIT_PER_RECORD
+    spec = cfg.spec(emit)
+    op = eng.op(spec)
+    dev = keys.device
+    cap = max(1, eng_out_capacity(op))
+    outs = {"key_id": torch.empty(cap, dtype=torch.int32, device=dev),
+            "win_start": torch.empty(cap, dtype=torch.int64, device=dev),
+            "win_end": torch.empty(cap, dtype=torch.int64, device=dev),
+            "src_index": torch.empty(cap, dtype=torch.int64, device=dev),
+            "aggs": [torch.empty(cap, dtype=torch.float64 if f else torch.int64, device=dev) for f in spec.agg_is_f64()]}
+    drain = make_device_drain(op, outs, cap, zero_copy=True)
+    descs = [make_batch(keys[s:s + m], ts[s:s + m], [c[s:s + m] for c in cols], None, abi.HSG_MEM_DEVICE)
+             for s, m in pieces]
+    push_fn = op._lib.hsg_push_batch
+    wm = C.c_int64(-1)
+
+    def step():
+        op.reset()
+        wm.value = -1
+        for b, _keep in descs:
+            rc = push_fn(op._h, C.byref(b), C.byref(wm))
+            if rc != abi.HSG_OK:
+                op._check(rc, "push_batch")
+            drain()
+
+    torch.cuda.synchronize()
+    step()
+    torch.cuda.synchronize()
+    k = max(1, args.extra_steps)
+    st0 = op.stats()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    st1 = op.stats()
+    n_rank = sum(m for _, m in pieces)
+    roof = roofline(st0, st1, spec, emit)
+    roof["kernel"] = pipeline_name(cfg, "per_record")
+    out = {"value": round(n_rank * k / el, 1), "unit": "records/s", "steps": k,
+           "ms_per_step": round(el * 1e3 / k, 3), "emit": "per_record",
+           "rows_per_step": int((st1["pairs_total"] - st0["pairs_total"]) / k), "roofline": roof}
+    op.close()
+    del descs, outs
+    torch.cuda.empty_cache()
+    return out
 
 
 def workload_text(cfg):
@@ -313,25 +476,33 @@ def committed_traffic(args, world):
     return int(d["hbm_bytes_per_batch"]), os.path.relpath(paths[-1], ROOT)
 
 
-def traffic_from_csv(path, launches):
-    """Sum FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE over k_tw_agg rows of a
-    rocprofv3 --pmc counter_collection.csv, per launch, in bytes."""
+def traffic_from_csv(path, cfg, emit):
+    """HBM bytes per batch from a rocprofv3 --pmc counter_collection.csv that
+    holds FETCH_SIZE and / or WRITE_SIZE rows: 2 x FETCH_SIZE (the gfx950
+    correction for wide streaming reads, MI355X_MICROARCH.md) + WRITE_SIZE,
+    over every hsg:: kernel, divided by the batches (dispatches of the
+    pipeline's first kernel); KiB -> bytes."""
     import csv
+    from hstream_amd import abi
+    first = "k_ss_phist" if cfg.window_kind == abi.HSG_SESSION else (
+        "k_pr_" if emit == "per_record" else "k_part_hist")
     fetch = write = 0.0
-    n = set()
+    batches = set()
     with open(path) as f:
         for r in csv.DictReader(f):
-            if "k_tw_agg" not in r.get("Kernel_Name", ""):
+            name = r.get("Kernel_Name", "")
+            if "hsg::" not in name:
                 continue
-            n.add(r.get("Dispatch_Id"))
-            name, val = r.get("Counter_Name"), float(r.get("Counter_Value", 0))
-            if name == "FETCH_SIZE":
+            if first in name:
+                batches.add(r.get("Dispatch_Id"))
+            cn, val = r.get("Counter_Name"), float(r.get("Counter_Value", 0))
+            if cn == "FETCH_SIZE":
                 fetch += val
-            elif name == "WRITE_SIZE":
+            elif cn == "WRITE_SIZE":
                 write += val
-    if not n:
+    if not batches:
         return None
-    return int((2 * fetch + write) * 1024 / len(n))
+    return int((2 * fetch + write) * 1024 / len(batches))
 
 
 def cpu_model():

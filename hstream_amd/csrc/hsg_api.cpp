@@ -197,6 +197,7 @@ struct AsyncJob {
   int64_t *wm = nullptr;
   hsg_done_fn done = nullptr;
   void *ctx = nullptr;
+  int staged_set = -1;  // host arrays already queued for H2D (op_prestage)
 };
 
 struct hsg_op {
@@ -224,9 +225,32 @@ struct hsg_op {
   bool stopping = false;
   int async_rc = HSG_OK;   // first failure since the last hsg_op_wait
   std::thread worker;
+  int next_set = 0;        // staging set of the next prestaged batch
 };
 
-static int push_sync(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark);
+static int push_sync(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark, int staged_set = -1);
+
+// Queue the H2D copies of a queued host batch (single-GPU ops) so that they
+// overlap the batch before it; the sets alternate, so the set a prestage
+// fills was last read by a push that has completed (pushes are synchronous on
+// the op's completion thread). Failure only means the push stages itself.
+static void prestage_job(hsg_op *op, AsyncJob &job) {
+  if (job.staged_set >= 0 || op->comm || job.b.mem != HSG_MEM_HOST || job.b.n == 0) return;
+  if (job.b.n > op->eng->batch_cap || job.b.n_cols != op->cfg.n_cols || !job.b.key_id || !job.b.ts)
+    return;  // push_sync reports it
+  hsg_batch b = job.b;
+  b.cols = job.cols.empty() ? nullptr : job.cols.data();
+  b.valid = job.valid.empty() ? nullptr : job.valid.data();
+  for (int c = 0; c < b.n_cols; ++c)
+    if (!b.cols || !b.cols[c]) return;
+  if (hipSetDevice(op->eng->device) != hipSuccess) return;
+  std::string err;
+  const int set = op->next_set;
+  if (op_prestage(op->dev, &b, set, err) == HSG_OK) {
+    job.staged_set = set;
+    op->next_set ^= 1;
+  }
+}
 
 // Wait for the op's queued asynchronous pushes; returns (and clears) the first
 // failure among them.
@@ -253,10 +277,15 @@ static void async_loop(hsg_op *op) {
     AsyncJob job = std::move(op->queue.front());
     op->queue.pop_front();
     op->busy = true;
+    // the next queued job stays in the deque (only this thread pops it, and
+    // push_back keeps references to elements valid)
+    AsyncJob *next = op->queue.empty() ? nullptr : &op->queue.front();
     lk.unlock();
+    prestage_job(op, job);
+    if (next) prestage_job(op, *next);
     job.b.cols = job.cols.empty() ? nullptr : job.cols.data();
     job.b.valid = job.valid.empty() ? nullptr : job.valid.data();
-    const int rc = push_sync(op, &job.b, job.wm);
+    const int rc = push_sync(op, &job.b, job.wm, job.staged_set);
     if (job.done) job.done(job.ctx, rc);
     lk.lock();
     if (rc != HSG_OK && op->async_rc == HSG_OK) op->async_rc = rc;
@@ -391,7 +420,7 @@ static int validate_batch(hsg_op *op, const hsg_batch *b, const int64_t *inout_w
 }
 
 // The push itself (caller: hsg_push_batch, or the op's completion thread).
-static int push_sync(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark) {
+static int push_sync(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark, int staged_set) {
   try {
     int rc = validate_batch(op, b, inout_watermark);
     if (rc != HSG_OK) return rc;
@@ -407,6 +436,7 @@ static int push_sync(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark) {
     args.comm = op->comm;
     args.rank = op->eng->rank;
     args.nranks = op->eng->nranks;
+    args.staged_set = staged_set;
     rc = op_push(op->dev, op->cfg, op->prog, args, res, op->err);
     if (rc != HSG_OK && rc != HSG_E_RANGE && rc != HSG_E_OOM) return rc;
     // state was mutated: account for what happened even on OOM / RANGE

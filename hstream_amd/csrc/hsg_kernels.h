@@ -9,7 +9,7 @@
 namespace hsg {
 
 // op_device.cpp
-int stage_batch(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err);
+int stage_batch(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err, int staged_set = -1);
 TwParams make_tw_params(const hsg_op_config &cfg, const PushArgs &a);
 void launch_stream_time(OpDevice &d, const hsg_op_config &cfg, const Batch &kb, int64_t wm_in, int64_t adv);
 int fetch_scalars(OpDevice &d, std::string &err);

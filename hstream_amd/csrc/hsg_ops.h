@@ -74,6 +74,18 @@ struct OpDevice {
   uint8_t *st_valid[kMaxCols] = {};
   int64_t *st_seq = nullptr;    // global record seq of received records (multi-GPU)
   int64_t *st_wm = nullptr;     // per-record watermark of received records (multi-GPU)
+  // prestaged host batches of asynchronous pushes (single-GPU ops): the H2D
+  // copies of the next queued batch run on their own stream, into the other
+  // of two staging sets, while the current batch computes (op_prestage)
+  struct Staging {
+    uint32_t *key = nullptr;
+    int64_t *ts = nullptr;
+    int64_t *col[kMaxCols] = {};
+    uint8_t *valid[kMaxCols] = {};
+  };
+  Staging pre[2];
+  hipStream_t h2d = nullptr;
+  hipEvent_t ev_h2d[2] = {nullptr, nullptr};
   // time windows
   TwTable tw = {};
   uint64_t cap = 0;             // table slots
@@ -139,6 +151,7 @@ struct PushArgs {
   Comm *comm = nullptr;
   int rank = 0;
   int nranks = 1;
+  int staged_set = -1;    // host batch already copied into OpDevice::pre[staged_set] (op_prestage)
 };
 
 struct PushResult {
@@ -162,6 +175,11 @@ void op_device_free(OpDevice &d);
 int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err);
 int op_push(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, PushResult &r,
             std::string &err);
+// Queue the H2D copies of a host batch (single-GPU ops) into staging set
+// `set` on the op's copy stream; the push that names the set (PushArgs::
+// staged_set) waits for them on the op's stream. The set must not be in use
+// by a push still running.
+int op_prestage(OpDevice &d, const hsg_batch *b, int set, std::string &err);
 // rows [from, from + n) of src into out at row dst_off
 int op_copy_rows(OpDevice &d, const OutCols &src, uint64_t from, uint64_t n, int n_aggs, const hsg_rows *out,
                  std::string &err, uint64_t dst_off = 0);

@@ -307,6 +307,21 @@ void op_device_free(OpDevice &d) {
   }
   dfree(d.st_seq);
   dfree(d.st_wm);
+  if (d.h2d) hipStreamSynchronize(d.h2d);
+  for (auto &s : d.pre) {
+    dfree(s.key);
+    dfree(s.ts);
+    for (int c = 0; c < kMaxCols; ++c) {
+      dfree(s.col[c]);
+      dfree(s.valid[c]);
+    }
+  }
+  for (auto &e : d.ev_h2d) {
+    if (e) hipEventDestroy(e);
+    e = nullptr;
+  }
+  if (d.h2d) hipStreamDestroy(d.h2d);
+  d.h2d = nullptr;
   dfree(d.tw.rows);
   dfree(d.tw_dirty_mem);
   dfree(d.tw_cnt);
@@ -345,11 +360,56 @@ void op_device_free(OpDevice &d) {
   d.reset_pending = false;
 }
 
-// Resolve the batch into device pointers, copying host arrays into staging.
-int stage_batch(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err) {
+int op_prestage(OpDevice &d, const hsg_batch *b, int set, std::string &err) {
+  if (b->mem != HSG_MEM_HOST || set < 0 || set > 1 || b->n > d.batch_cap || b->n_cols != d.n_cols) {
+    err = "prestage: not a host batch of this op";
+    return HSG_E_INVALID;
+  }
+  if (!d.h2d) {
+    DTRY(hipStreamCreateWithFlags(&d.h2d, hipStreamNonBlocking));
+    DTRY(hipEventCreateWithFlags(&d.ev_h2d[0], hipEventDisableTiming));
+    DTRY(hipEventCreateWithFlags(&d.ev_h2d[1], hipEventDisableTiming));
+  }
+  OpDevice::Staging &s = d.pre[set];
+  if (!s.key) {
+    DTRY(dalloc(&s.key, d.batch_cap));
+    DTRY(dalloc(&s.ts, d.batch_cap));
+    for (int c = 0; c < d.n_cols; ++c) {
+      DTRY(dalloc(&s.col[c], d.batch_cap));
+      DTRY(dalloc(&s.valid[c], d.batch_cap));
+    }
+  }
+  const uint64_t n = b->n;
+  const hipMemcpyKind k = hipMemcpyHostToDevice;
+  if (n) {
+    DTRY(hipMemcpyAsync(s.key, b->key_id, n * 4, k, d.h2d));
+    DTRY(hipMemcpyAsync(s.ts, b->ts, n * 8, k, d.h2d));
+    for (int c = 0; c < b->n_cols; ++c) {
+      DTRY(hipMemcpyAsync(s.col[c], b->cols[c], n * 8, k, d.h2d));
+      if (b->valid && b->valid[c]) DTRY(hipMemcpyAsync(s.valid[c], b->valid[c], n, k, d.h2d));
+    }
+  }
+  DTRY(hipEventRecord(d.ev_h2d[set], d.h2d));
+  return HSG_OK;
+}
+
+// Resolve the batch into device pointers, copying host arrays into staging
+// (or taking the ones op_prestage queued for it).
+int stage_batch(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err, int staged_set) {
   memset(&kb, 0, sizeof(kb));
   kb.n = b->n;
   const uint64_t n = b->n;
+  if (staged_set >= 0 && b->mem == HSG_MEM_HOST) {
+    const OpDevice::Staging &s = d.pre[staged_set];
+    DTRY(hipStreamWaitEvent(d.stream, d.ev_h2d[staged_set], 0));
+    kb.key = s.key;
+    kb.ts = s.ts;
+    for (int c = 0; c < b->n_cols; ++c) {
+      kb.col[c] = s.col[c];
+      kb.valid[c] = (b->valid && b->valid[c]) ? s.valid[c] : nullptr;
+    }
+    return HSG_OK;
+  }
   if (b->mem == HSG_MEM_DEVICE) {
     // the producer's stream is not ordered with ours: wait on its event
     if (b->ready_event) DTRY(hipStreamWaitEvent(d.stream, (hipEvent_t)b->ready_event, 0));
@@ -618,7 +678,7 @@ int op_push(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const Pu
   }
   if (a.comm) return push_sharded(d, cfg, prog, a, r, err);
   Batch kb;
-  int rc = stage_batch(d, b, kb, err);
+  int rc = stage_batch(d, b, kb, err, a.staged_set);
   if (rc != HSG_OK) return rc;
   r.owned = kb.n;
   r.global_records = kb.n;
