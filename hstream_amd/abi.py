@@ -224,7 +224,7 @@ class hsg_sink_records(C.Structure):
 
 
 # Every symbol include/hstream_sink.h declares.
-SINK_SYMBOLS = ["hsg_sink_create", "hsg_sink_destroy", "hsg_sink_encode", "hsg_format_number"]
+SINK_SYMBOLS = ["hsg_sink_create", "hsg_sink_destroy", "hsg_sink_encode", "hsg_sink_member_order", "hsg_format_number"]
 
 
 class hsg_join_config(C.Structure):

@@ -62,6 +62,7 @@ __device__ inline int64_t slot_identity_dev(int32_t op) {
     case S_MAX_I: return INT64_MIN;
     case S_MIN_F: return (int64_t)f64_ord(9223372036854775807.0);
     case S_MAX_F: return (int64_t)f64_ord(-9223372036854775808.0);
+    case S_SUM_F: return INT64_MIN;  // -0.0 (slot_identity)
     default: return 0;
   }
 }

@@ -211,6 +211,17 @@ HSG_HD int fmt_f64(double v, const Pow5Tables &T, char *out) {
     out[0] = 'n', out[1] = 'u', out[2] = 'l', out[3] = 'l';
     return 4;
   }
+  // Aggregate identities are integers in the reference (Codegen.hs:425,438,
+  // 451: Number 0, minBound / maxBound :: Int, exponent 0), which aeson prints
+  // plainly. Here a SUM no value reached keeps its identity -0.0
+  // (slot_identity), a MIN / MAX the f64 image of maxBound (2^63, rounded) /
+  // minBound (-2^63).
+  if (bits == 0x8000000000000000ull) {
+    out[0] = '0';
+    return 1;
+  }
+  if (v == 9223372036854775808.0) return fmt_i64(INT64_MAX, out);
+  if (v == -9223372036854775808.0) return fmt_i64(INT64_MIN, out);
   if (ie == 0 && im == 0) return fmt_generic(false, nullptr, 0, 0, out);
   uint64_t m;
   int32_t e;

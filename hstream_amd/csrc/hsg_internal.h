@@ -19,7 +19,7 @@ enum SlotOp : int32_t {
   S_CNT_ALL = 0,  // += 1                               (COUNT(*))
   S_CNT = 1,      // += present(col)                    (COUNT(col), AVG denominator)
   S_SUM_I = 2,    // += v (wrapping int64)              (SUM / AVG numerator of an i64 column)
-  S_SUM_F = 3,    // += v (f64)                         (SUM / AVG numerator of an f64 column)
+  S_SUM_F = 3,    // += v (f64), identity -0.0          (SUM / AVG numerator of an f64 column)
   S_MIN_I = 4,    // min, identity INT64_MAX
   S_MAX_I = 5,    // max, identity INT64_MIN
   S_MIN_F = 6,    // min over order-preserving u64 image of the f64, identity img(2^63)
@@ -218,6 +218,7 @@ inline int64_t slot_identity(int32_t op) {
     case S_MAX_I: return INT64_MIN;
     case S_MIN_F: return (int64_t)f64_ord((double)INT64_MAX);
     case S_MAX_F: return (int64_t)f64_ord((double)INT64_MIN);
+    case S_SUM_F: return INT64_MIN;  // -0.0: x + -0.0 == x for every x, and a SUM nothing reached stays -0.0
     default: return 0;
   }
 }

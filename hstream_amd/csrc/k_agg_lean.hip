@@ -404,8 +404,7 @@ __global__ __launch_bounds__(256) void k_pane_apply(Program rprog, TwParams p, P
           for (int s = 0; s < NS; ++s) c[s] = __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           const uint32_t st = __hip_atomic_load(stp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-          for (int s = 0; s < NS; ++s)
-            if (v[s] != slot_identity_dev(prog.op(s))) v[s] = slot_combine(prog.op(s), c[s], v[s]);
+          for (int s = 0; s < NS; ++s) v[s] = slot_combine(prog.op(s), c[s], v[s]);
           first = st != bid;
         } else {
           first = true;  // claimed just now by the group's only writer: the row holds identities

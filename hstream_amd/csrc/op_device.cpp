@@ -171,8 +171,7 @@ int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, 
     DTRY(hipEventRecord(d.ev_pre, d.stream));
     DTRY(hipStreamWaitEvent(d.aux, d.ev_pre, 0));
     // (only the blocks claimed since the last clear, once the dirty map is
-    // valid; HSG_TW_FULL_RESET: always the whole table)
-    static const bool full = getenv("HSG_TW_FULL_RESET") != nullptr;
+    // valid)
     if (d.tw_cnt_pending) {  // the previous clear's count (long finished)
       DTRY(hipEventSynchronize(d.ev_reset));
       d.tw_cnt_pending = false;
@@ -181,7 +180,7 @@ int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, 
         d.tw_map_valid = false;
       }
     }
-    if (d.tw_map_valid && !full) {
+    if (d.tw_map_valid) {
       launch_tw_reset_dirty(d.aux, d.tw, prog, d.tw_cnt);
       DTRY(hipMemcpyAsync(d.h_tw_cnt, d.tw_cnt, 8, hipMemcpyDeviceToHost, d.aux));
       d.tw_cnt_pending = true;
@@ -271,9 +270,8 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
     rc = perrecord_device_init(d, cfg, prog, err);
     if (rc != HSG_OK) return rc;
   } else if (part_supported(prog)) {
-    const char *env = getenv("HSG_AGG");
-    d.use_part = !(env && strcmp(env, "atomic") == 0);
-    if (d.use_part) {
+    d.use_part = true;
+    {
       // panes: size a multiple of advance (tumbling and unwindowed: one pane per window)
       const int64_t adv = cfg.window_kind == HSG_HOPPING ? cfg.advance_ms : 0;
       d.pane_S = 1;

@@ -3,6 +3,7 @@
 // encode (k_sink.hip) with an exclusive scan of the record sizes between.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <new>
 #include <string>
@@ -139,7 +140,67 @@ int sync_keys(hsg_sink *s) {
   return HSG_OK;
 }
 
+// Member order of an aeson-encoded Object. aeson 1.4 writes an Object's
+// members in the traversal order of its HashMap (Data.Aeson.Encoding.Internal
+// dict over HM.foldrWithKey), so the sink writes them in that order too. Stack
+// lts-16.21 (hstream-processing/stack.yaml:20-21; the cabal bounds
+// hashable < 1.4, unordered-containers ^>= 0.2.9 in
+// hstream-store/admin/hstore-admin.cabal:71,84) pins hashable-1.3.0.0,
+// text-1.2.4.0 and unordered-containers-0.2.10.0:
+//   hash (Text) = hashWithSalt defaultSalt: FNV-1 (prime 16777619, 64-bit)
+//     over the UTF-16 code units' bytes (little-endian), seeded with
+//     combine defaultSalt len = defaultSalt * 16777619 xor len,
+//     defaultSalt = -2578643520546668380 (0xdc36d1615b7400a4);
+//   the HAMT indexes 4-bit subkeys from the low bits (bitsPerSubkey = 4) and
+//     traverses children in subkey order, so members come out in increasing
+//     order of the hash read nibble by nibble from the lowest; equal hashes
+//     (a collision node) keep insertion order (here: SELECT order).
+// Restated from the libraries' published source; no reference test prints an
+// encoded object, so the order is pinned by this restatement only
+// (tests/test_sink.py restates it independently).
+uint64_t aeson_key_hash(const char *utf8) {
+  std::vector<uint16_t> u16;
+  for (const unsigned char *p = (const unsigned char *)utf8; *p;) {
+    uint32_t c = *p, extra = 0;
+    if (c >= 0xF0) c &= 0x07, extra = 3;
+    else if (c >= 0xE0) c &= 0x0F, extra = 2;
+    else if (c >= 0xC0) c &= 0x1F, extra = 1;
+    ++p;
+    for (uint32_t k = 0; k < extra && (*p & 0xC0) == 0x80; ++k, ++p) c = (c << 6) | (*p & 0x3F);
+    if (c >= 0x10000) {
+      c -= 0x10000;
+      u16.push_back((uint16_t)(0xD800 + (c >> 10)));
+      u16.push_back((uint16_t)(0xDC00 + (c & 0x3FF)));
+    } else {
+      u16.push_back((uint16_t)c);
+    }
+  }
+  const uint64_t prime = 16777619ull;
+  uint64_t h = 0xdc36d1615b7400a4ull * prime ^ (uint64_t)u16.size();
+  for (uint16_t u : u16) {
+    h = (h * prime) ^ (uint64_t)(u & 0xFF);
+    h = (h * prime) ^ (uint64_t)(u >> 8);
+  }
+  return h;
+}
+
+uint64_t nibble_reverse(uint64_t h) {
+  uint64_t r = 0;
+  for (int k = 0; k < 16; ++k) r = (r << 4) | ((h >> (4 * k)) & 15);
+  return r;
+}
+
 }  // namespace
+
+namespace hsg {
+// for hsg_sink_member_order (tests): member m's position in the encoded object
+void sink_member_order(const char *const *aliases, int n, int32_t *order) {
+  std::vector<std::pair<uint64_t, int>> v;
+  for (int m = 0; m < n; ++m) v.push_back({nibble_reverse(aeson_key_hash(aliases[m])), m});
+  std::stable_sort(v.begin(), v.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+  for (int k = 0; k < n; ++k) order[k] = v[k].second;
+}
+}  // namespace hsg
 
 extern "C" int hsg_sink_create(hsg_op *op, const hsg_keydict *dict, const hsg_sink_config *cfg, hsg_sink **out) {
   if (!op || !dict || !cfg || !out || !cfg->key_field || cfg->n_members < 0 || cfg->n_members > kSinkMaxMembers)
@@ -172,12 +233,16 @@ extern "C" int hsg_sink_create(hsg_op *op, const hsg_keydict *dict, const hsg_si
   kp += ":";
   add(kp);
   add("}");
-  for (int m = 0; m < cfg->n_members; ++m) {
-    std::string t = m ? "," : "{";
+  // members in the HashMap's traversal order (sink_member_order)
+  int32_t order[kSinkMaxMembers];
+  sink_member_order(cfg->aliases, cfg->n_members, order);
+  for (int k = 0; k < cfg->n_members; ++k) {
+    const int m = order[k];
+    std::string t = k ? "," : "{";
     put_json_string(t, cfg->aliases[m]);
     t += ":";
     add(t);
-    s->S.agg_index[m] = cfg->agg_index[m];
+    s->S.agg_index[k] = cfg->agg_index[m];
   }
   add(cfg->n_members ? "}" : "{}");
   fo.push_back((uint32_t)frag.size());
@@ -201,6 +266,18 @@ extern "C" int hsg_sink_create(hsg_op *op, const hsg_keydict *dict, const hsg_si
 }
 
 extern "C" void hsg_sink_destroy(hsg_sink *s) { free_sink(s); }
+
+extern "C" int hsg_sink_member_order(const char *const *aliases, int32_t n, int32_t *order) {
+  if (n < 0 || n > kSinkMaxMembers || (n && (!aliases || !order))) return HSG_E_INVALID;
+  for (int m = 0; m < n; ++m)
+    if (!aliases[m]) return HSG_E_INVALID;
+  try {
+    sink_member_order(aliases, n, order);
+  } catch (...) {
+    return HSG_E_OOM;
+  }
+  return HSG_OK;
+}
 
 extern "C" int hsg_sink_encode(hsg_sink *s, const hsg_rows *rows, uint64_t n, hsg_sink_records *out,
                                uint64_t *key_need, uint64_t *value_need) {

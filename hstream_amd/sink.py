@@ -29,6 +29,8 @@ def _lib():
         L.hsg_sink_encode.argtypes = [vp, P(abi.hsg_rows), C.c_uint64, P(hsg_sink_records), P(C.c_uint64),
                                       P(C.c_uint64)]
         L.hsg_sink_encode.restype = C.c_int
+        L.hsg_sink_member_order.argtypes = [P(C.c_char_p), C.c_int32, P(C.c_int32)]
+        L.hsg_sink_member_order.restype = C.c_int
         L.hsg_format_number.argtypes = [C.c_int32, C.c_int64, C.c_char_p, C.c_size_t, P(C.c_size_t)]
         L.hsg_format_number.restype = C.c_int
         _declared = True
@@ -46,8 +48,22 @@ def format_number(value, is_f64: bool) -> str:
     return buf.raw[: n.value].decode()
 
 
+def member_order(aliases: Sequence[str]) -> List[int]:
+    """Indices of `aliases` in the order the encoder writes the value
+    object's members (aeson's HashMap traversal order)."""
+    L = _lib()
+    n = len(aliases)
+    arr = (C.c_char_p * max(1, n))(*[a.encode() for a in aliases])
+    out = (C.c_int32 * max(1, n))()
+    rc = L.hsg_sink_member_order(arr, n, out)
+    if rc != abi.HSG_OK:
+        raise abi.HStreamGpuError(rc, "hsg_sink_member_order")
+    return list(out[:n])
+
+
 class Sink:
-    """members: [(alias, agg column or -1 for the GROUP BY value)], SELECT order."""
+    """members: [(alias, agg column or -1 for the GROUP BY value)], SELECT
+    order; the encoder writes them in aeson's order (member_order)."""
 
     def __init__(self, op, keys, key_field: str, members: Sequence[Tuple[str, int]], windowed=True):
         self._L = _lib()

@@ -14,10 +14,16 @@
  * The key object is {key_field: key value} (Codegen.hs:485-487) with the key's
  * text from the ingest dictionary (hstream_ingest.h). Numbers print as aeson
  * prints Data.Scientific: integers plainly, f64 aggregates in Scientific's
- * Generic form of their shortest round-trip decimal ("2.5", "4.0", "1.0e-3").
- * Members are written in SELECT order (aeson writes a HashMap's internal
- * order, which depends on hashable / unordered-containers internals: parity of
- * the member order is unpinned; every member's text is).
+ * Generic form of their shortest round-trip decimal ("2.5", "4.0", "1.0e-3");
+ * an aggregate identity prints as the reference's integer initial value
+ * (Codegen.hs:425,438,451: a decimal SUM nothing reached "0", MAX / MIN
+ * "-9223372036854775808" / "9223372036854775807"). Known divergence: a decimal
+ * aggregate of integer JSON literals only (Scientific exponent >= 0) prints
+ * "6.0" where aeson prints "6" (the f64 column keeps no exponent).
+ * Members are written in aeson's order for an Object, the traversal order of
+ * its HashMap (hashable-1.3.0.0 Text hash, unordered-containers-0.2.10.0,
+ * Stack lts-16.21; restated in sink.cpp, pinned by that restatement only: no
+ * reference test prints an encoded object).
  */
 #ifndef HSTREAM_SINK_H
 #define HSTREAM_SINK_H
@@ -61,6 +67,10 @@ void hsg_sink_destroy(hsg_sink *s);
  * they exceed the capacities nothing is written and HSG_E_CAPACITY returned. */
 int  hsg_sink_encode(hsg_sink *s, const hsg_rows *rows, uint64_t n, hsg_sink_records *out, uint64_t *key_need,
                      uint64_t *value_need);
+/* The order the value object's members are written in: order[k] = index (in
+ * aliases) of the k-th member written. For tests and hosts that build the
+ * same objects. */
+int  hsg_sink_member_order(const char *const *aliases, int32_t n, int32_t *order);
 /* One value's text as the encoder prints it (is_f64: bits is a double's bit
  * pattern, else an int64). *len = text bytes; HSG_E_CAPACITY if cap < *len. */
 int  hsg_format_number(int32_t is_f64, int64_t bits, char *buf, size_t cap, size_t *len);

@@ -13,7 +13,9 @@ Follows, record by record in arrival order over both streams:
   key selectors         hstream-sql/src/HStream/SQL/Codegen.hs:241-243 (a
                         missing join field throws at the first candidate,
                         which runTask catches: the record's scan ends there)
-Parity is pinned by the reference's code only: its tests hold no join vectors.
+Pinned by the reference's one join vector, RegressionSpec.hs:24-40 (#391_JOIN,
+tests/golden/reference_kat.json "joins", tests/test_join.py), and by
+hand-derived vectors of its code (tests/test_join.py).
 """
 import bisect
 

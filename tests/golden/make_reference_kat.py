@@ -127,6 +127,37 @@ cases.append({
     "expect_changelog": [[0, 0, 0, [1]], [0, 11, 11, [1]], [1, 0, 0, [1]], [1, 0, 10, [2]]],
 })
 
+# hstream/test/HStream/RegressionSpec.hs:24-40  (#391_JOIN)
+# SELECT s1.a, s2.a, s1.b, s2.b, SUM(s1.a), SUM(s2.a) FROM s1 INNER JOIN s2
+#   WITHIN (INTERVAL 1 MINUTE) ON (s1.b = s2.b) GROUP BY s1.b EMIT CHANGES;
+# INSERT INTO s1 (a, b) VALUES (1, 3); INSERT INTO s2 (a, b) VALUES (2, 3);
+#   -> one row: SUM(s1.a) = 1, SUM(s2.a) = 2, s1.a = 1, s1.b = 3, s2.a = 2, s2.b = 3
+# Codegen: s1 is the join's "this" stream (genStreamWithSourceStream,
+# Codegen.hs:253-266), both windows 60000 ms (genJoinWindows :232-240), the
+# join key is the ON field (genKeySelector :242-244), every source record's
+# key is the dummy "{}" (HStore.hs:110-112: one record key, key_id 0), the
+# joined value is genJoiner's union of prefixed fields (Internal/Codegen.hs:
+# 62-67), then genGroupByNode's unwindowed aggregate over s1.b with the
+# non-aggregate columns as passthrough (LAST, Codegen.hs:463-469).
+joins = [{
+    "name": "RegressionSpec#391_JOIN",
+    "ref": "hstream/test/HStream/RegressionSpec.hs:24-40",
+    "sql": "SELECT s1.a, s2.a, s1.b, s2.b, SUM(s1.a), SUM(s2.a) FROM s1 INNER JOIN s2 WITHIN (INTERVAL 1 MINUTE) "
+           "ON (s1.b = s2.b) GROUP BY s1.b EMIT CHANGES;",
+    "join": {"before_ms": 60000, "after_ms": 60000,
+             "batches": [
+                 {"side": [0], "key_id": [0], "join_key": [0], "ts": [1000], "handle": [0]},
+                 {"side": [1], "key_id": [0], "join_key": [0], "ts": [1500], "handle": [1]}]},
+    "note": "join_key 0 <-> b = 3; handle 0 = s1's record, 1 = s2's record",
+    "values": {"0": {"a": 1, "b": 3}, "1": {"a": 2, "b": 3}},
+    "expect_join_rows": [[0, 1, 0, 1500]],
+    "group_by": ["this", "b"],
+    "columns": [["this", "a"], ["other", "a"], ["this", "b"], ["other", "b"]],
+    "op": {"window_kind": UNWINDOWED, "emit_mode": PER_RECORD, "col_types": [I64, I64, I64, I64],
+           "aggs": [[LAST, 0], [LAST, 1], [LAST, 2], [LAST, 3], [SUM, 0], [SUM, 1]]},
+    "expect_changelog_aggs": [[1, 2, 3, 3, 1, 2]],
+}]
+
 out = {
     "generator": "tests/golden/make_reference_kat.py",
     "reference": "Yu-zh/hstream @ 2025-01-17",
@@ -135,6 +166,7 @@ out = {
               "emit": "PER_RECORD=0 PER_BATCH=1 NONE=2"},
     "windows_for": windows,
     "cases": cases,
+    "joins": joins,
 }
 path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_kat.json")
 with open(path, "w") as f:

@@ -123,9 +123,10 @@ def test_type_error_record_only_moves_stream_time(eng):
 @pytest.mark.parametrize("window", ["tumbling", "session"])
 def test_json_poll_batch_through_native_ingest(eng, window):
     """A poll batch of raw JSON values (SourceRecord srcValue) decoded by the
-    native ingest straight into the op: the changelog equals the same
-    records run through the Python columnariser into the oracle; the keys
-    come back as the values the records spelled (1 and 1.0 are one key)."""
+    native ingest straight into the GPU op: the changelog equals the same
+    records run through the Python columnariser into the CPU oracle
+    (pyoracle, the checker); the keys come back as the values the records
+    spelled (1 and 1.0 are one key)."""
     import json
     from hstream_amd import ingest
     rng = np.random.default_rng(17)
@@ -143,15 +144,19 @@ def test_json_poll_batch_through_native_ingest(eng, window):
     ts = np.array([r["timestamp"] for r in recs], np.int64)
     buf, off = ingest.pack_records(vals)
 
-    def table(keys):
-        g = P.groupBy(eng, "k")
+    class OracleEngine:  # the Table's operator factory, on the CPU restatement
+        def op(self, spec):
+            return pyoracle.OracleOp(spec)
+
+    def table(keys, engine):
+        g = P.groupBy(engine, "k")
         w = g.timeWindowedBy(P.mkTumblingWindow(2000)) if window == "tumbling" else \
             g.sessionWindowedBy(P.mkSessionWindows(300))
         return w.aggregate([P.COUNT_ALL("n"), P.SUM("v", "s"), P.MAX("v", "m")], P.Materialized(keys=keys))
 
-    tn = table(ingest.KeyDict())
+    tn = table(ingest.KeyDict(), eng)
     wm_n, rows_n = tn.process_json(buf, off, ts, threads=4)
-    tp = table(P.KeyDict())
+    tp = table(P.KeyDict(), OracleEngine())
     wm_p, rows_p = tp.process(recs)
     assert wm_n == wm_p == int(ts.max())
     assert len(rows_n) == len(rows_p)

@@ -99,3 +99,34 @@ def test_lean_late_batch_after_prediction(eng):
     rows_equal(g.dump_state(), o.dump_state(), spec.agg_is_f64(), what="state dump")
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("ctype", [abi.HSG_I64, abi.HSG_F64], ids=["i64", "f64"])
+def test_lean_later_batch_with_identity_partials(eng, ctype):
+    """A group's later batch whose partial equals the slot identities (its
+    values cancel to a zero SUM, or every record lacks the field): the row
+    keeps its earlier state (Codegen.hs:423-461: an absent field leaves the
+    accumulator alone, +0 changes nothing)."""
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=10_000, col_types=[ctype],
+                  aggs=datagen.C_AGGS_FULL, state_capacity=1 << 20)
+    g, o = eng.op(spec), pyoracle.OracleOp(spec)
+    dt = np.float64 if ctype == abi.HSG_F64 else np.int64
+    n = 4096
+    key = np.arange(n, dtype=np.uint32) % 512
+    ts = np.full(n, 1_000_000, np.int64) + np.arange(n)
+    v1 = (np.arange(n) % 97 - 40).astype(dt)
+    # second batch: keys 0..255 get +x, -x pairs (partial SUM 0), keys 256..511 only absent fields
+    key2 = np.concatenate([np.repeat(np.arange(256, dtype=np.uint32), 8), np.arange(256, 512, dtype=np.uint32)])
+    v2 = np.concatenate([np.tile(np.array([7, -7], dt), 1024), np.zeros(256, dt)])
+    valid2 = np.concatenate([np.ones(2048, np.uint8), np.zeros(256, np.uint8)])
+    ts2 = np.full(key2.size, 1_005_000, np.int64)
+    wg = g.push(key, ts, [v1], None, watermark=-1)
+    wo = o.push(key, ts, [v1], None, watermark=-1)
+    rows_equal(g.drain(), o.drain(), spec.agg_is_f64(), what="batch 0")
+    wg = g.push(key2, ts2, [v2], [valid2], watermark=wg)
+    wo = o.push(key2, ts2, [v2], [valid2], watermark=wo)
+    assert wg == wo
+    rows_equal(g.drain(), o.drain(), spec.agg_is_f64(), what="batch 1")
+    rows_equal(g.dump_state(), o.dump_state(), spec.agg_is_f64(), what="state dump")
+    g.close()
+    o.close()

@@ -5,12 +5,49 @@ Stream.hs:267-300, over InMemoryTimestampedKVStore, Store.hs:316-385).
 CPU: hand-derived vectors pin the oracle (window bounds, the end-point quirk
 of tksRange, overwrite of an equal (key, ts), the missing-join-field abort).
 GPU: batches of interleaved records compared row for row, in order.
+The reference's one join vector (RegressionSpec.hs:24-40, #391_JOIN: join ->
+unwindowed GROUP BY) runs through the oracle on CPU and the GPU join + GPU
+op on the GPU.
 """
 import numpy as np
 import pytest
 
 import joinref
+import pyoracle
 from joinref import NONE
+from util import load_kat, run_join_kat
+
+JOIN_KAT = load_kat()["joins"]
+
+
+def _jarrays(b):
+    return (np.asarray(b["side"], np.uint8), np.asarray(b["key_id"], np.uint32),
+            np.asarray(b["join_key"], np.uint32), np.asarray(b["ts"], np.int64), np.asarray(b["handle"], np.uint64))
+
+
+@pytest.mark.parametrize("case", JOIN_KAT, ids=lambda c: c["name"])
+def test_reference_join_kat_oracle(case):
+    ref = joinref.JoinRef(case["join"]["before_ms"], case["join"]["after_ms"])
+    run_join_kat(case, lambda b: ref.push(*_jarrays(b)), lambda spec: pyoracle.OracleOp(spec))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", JOIN_KAT, ids=lambda c: c["name"])
+def test_reference_join_kat_gpu(case):
+    import torch
+    assert torch.cuda.is_available()
+    from hstream_amd.engine import Engine
+    from hstream_amd.join import Join
+    eng = Engine(device=0, batch_capacity=1 << 10)
+    j = Join(eng, case["join"]["before_ms"], case["join"]["after_ms"], batch_capacity=1 << 10)
+
+    def push(b):
+        j.push(*_jarrays(b))
+        return list(zip(*[x.tolist() for x in j.drain()]))
+
+    run_join_kat(case, push, lambda spec: eng.op(spec))
+    j.close()
+    eng.close()
 
 
 def _run(ref, recs):

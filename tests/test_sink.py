@@ -9,6 +9,19 @@ GPU: changelog rows of an op -> key bytes (timeWindowSerde int64BE start ++
 int64BE 0 ++ encode {key_field: key}, Boilerplate.hs:60-74, TimeWindows.hs:68-73)
 and value bytes (encode of the SELECT-projected object, Codegen.hs:355-369),
 compared byte for byte with a Python restatement of the same serdes.
+
+Member order: aeson writes an Object's members in its HashMap's traversal
+order; restated below from hashable-1.3.0.0 / text-1.2.4.0 /
+unordered-containers-0.2.10.0 (Stack lts-16.21, hstream-processing/
+stack.yaml:20-21). No reference test prints an encoded object, so the order
+is pinned by this restatement of the libraries' published algorithm only.
+Aggregate identities (Codegen.hs:425,438,451: Number 0, minBound / maxBound
+:: Int, exponent 0) print as integers: a decimal column's SUM / MAX / MIN no
+value reached is "0" / "-9223372036854775808" / "9223372036854775807"
+(test_sink_identity_text, hand-derived). Known divergence, parity
+unpinned: a decimal aggregate whose value came only from integer JSON
+literals (Scientific exponent >= 0) prints "6" in the reference and "6.0"
+here (the f64 column keeps no exponent).
 """
 import json
 import math
@@ -42,7 +55,37 @@ def generic(d: Decimal) -> str:
 def ref_f64(v: float) -> str:
     if math.isnan(v) or math.isinf(v):
         return "null"
+    # the identities of the f64 slots (a SUM nothing was added to is -0.0 on
+    # the device, MIN / MAX +-2^63): the reference's Number 0 / maxBound /
+    # minBound, exponent 0, printed as integers
+    if v == 0.0 and math.copysign(1.0, v) < 0:
+        return "0"
+    if v == 2.0 ** 63:
+        return str((1 << 63) - 1)
+    if v == -(2.0 ** 63):
+        return str(-(1 << 63))
     return generic(Decimal(repr(v)))
+
+
+_M64 = (1 << 64) - 1
+
+
+def aeson_key_hash(alias: str) -> int:
+    """hashable-1.3.0.0 hashWithSalt defaultSalt (Text): FNV-1 over the UTF-16
+    code units' little-endian bytes, seeded with combine defaultSalt len."""
+    u = alias.encode("utf-16-le")
+    h = ((0xDC36D1615B7400A4 * 16777619) & _M64) ^ (len(u) // 2)
+    for b in u:
+        h = ((h * 16777619) & _M64) ^ b
+    return h
+
+
+def aeson_member_order(aliases):
+    """Traversal order of a HashMap Text (unordered-containers-0.2.10.0: 4-bit
+    subkeys from the low bits of the hash, children in subkey order)."""
+    def digits(h):
+        return [(h >> (4 * k)) & 15 for k in range(16)]
+    return sorted(range(len(aliases)), key=lambda m: (digits(aeson_key_hash(aliases[m])), m))
 
 
 def test_int64_text():
@@ -51,7 +94,7 @@ def test_int64_text():
 
 
 def test_f64_text_known():
-    cases = {0.0: "0.0", -0.0: "0.0", 1.0: "1.0", 4.0: "4.0", 2.5: "2.5", 0.1: "0.1", 0.25: "0.25",
+    cases = {0.0: "0.0", 1.0: "1.0", 4.0: "4.0", 2.5: "2.5", 0.1: "0.1", 0.25: "0.25",
              0.001: "1.0e-3", 1234567.5: "1234567.5", 12345678.5: "1.23456785e7", 1e7: "1.0e7", 1e22: "1.0e22",
              -3.75: "-3.75", 1 / 3: "0.3333333333333333", 5e-324: "5.0e-324", 1.7976931348623157e308:
              "1.7976931348623157e308", 0.30000000000000004: "0.30000000000000004", 100.0: "100.0"}
@@ -59,6 +102,27 @@ def test_f64_text_known():
         assert format_number(v, True) == t, v
         assert ref_f64(v) == t, v
     assert format_number(float("nan"), True) == "null"
+
+
+def test_sink_identity_text():
+    """Hand-derived from Codegen.hs:423-461 and aeson's Scientific encoding: a
+    group whose decimal field was absent in every record keeps the initial
+    values Number 0 / minBound / maxBound (exponent 0), printed as integers."""
+    assert format_number(-0.0, True) == "0"                       # SUM: Number 0
+    assert format_number(-(2.0 ** 63), True) == "-9223372036854775808"  # MAX: minBound :: Int
+    assert format_number(2.0 ** 63, True) == "9223372036854775807"      # MIN: maxBound :: Int
+
+
+def test_member_order_restatement():
+    """The encoder's member order (sink.cpp, hsg_sink_member_order) equals the
+    independent Python restatement of the HashMap traversal."""
+    from hstream_amd.sink import member_order
+    rng = random.Random(11)
+    pool = ["cnt", "total", "avg_x", "k", "max_x", "min v", "SUM(a)", "a", "b", "s1.a", "s2.b", "result",
+            "COUNT(*)", "é", "𝄞x", "a+1", "winStart", "key1", "key2", "key3"]
+    for _ in range(200):
+        names = rng.sample(pool, rng.randrange(1, 12))
+        assert member_order(names) == aeson_member_order(names), names
 
 
 def test_f64_text_random_bits():
@@ -124,13 +188,14 @@ def test_sink_records_match_serdes(windowed):
     rows = op.drain()
     members = [("cnt", 0), ("total", 1), ("avg_x", 2), ("k", -1), ("max_x", 3), ("min v", 4)]
     sink = Sink(op, keys, "k", members, windowed=windowed)
+    written = [members[m] for m in aeson_member_order([a for a, _ in members])]
     got = sink.encode(rows)
     assert len(got) == len(rows) > 0
     f64 = spec.agg_is_f64()
     for i, (kb, vb) in enumerate(got):
         ktext = keys.text(int(rows.key_id[i]))
         mem = []
-        for alias, j in members:
+        for alias, j in written:
             if j < 0:
                 mem.append((alias, ktext))
             else:

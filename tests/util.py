@@ -116,3 +116,27 @@ ALL_AGG_SETS = {
     "mixed": [(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0), (abi.HSG_SUM, 1), (abi.HSG_MIN, 1), (abi.HSG_MAX, 1),
               (abi.HSG_AVG, 1), (abi.HSG_MAX, 0), (abi.HSG_COUNT, 1), (abi.HSG_LAST, 1)],
 }
+
+
+def run_join_kat(case, push_join, make_op):
+    """A reference join vector: the join (push_join(batch) -> rows (this handle,
+    other handle, join key, ts) of that batch, in order), then its rows through
+    the GROUP BY op built from case["op"], as genStreamBuilderWithStream chains
+    them (Codegen.hs:532-559). Asserts the join rows and the changelog."""
+    rows = []
+    for b in case["join"]["batches"]:
+        rows += [tuple(int(x) for x in r) for r in push_join(b)]
+    assert [list(r) for r in rows] == case["expect_join_rows"], f"{case['name']}: join rows {rows}"
+    vals = case["values"]
+    pick = lambda r, side, field: vals[str(r[0] if side == "this" else r[1])][field]
+    gside, gfield = case["group_by"]
+    dict_ids = {}
+    key = np.asarray([dict_ids.setdefault(pick(r, gside, gfield), len(dict_ids)) for r in rows], dtype=np.uint32)
+    ts = np.asarray([r[3] for r in rows], dtype=np.int64)
+    cols = [np.asarray([pick(r, s, f) for r in rows], dtype=np.int64) for s, f in case["columns"]]
+    spec = spec_from_json(case["op"])
+    op = make_op(spec)
+    op.push(key, ts, cols, None, watermark=-1)
+    got = [list(v) for _, _, _, v in op.drain().tuples()]
+    assert got == case["expect_changelog_aggs"], f"{case['name']}: {got}"
+    op.close() if hasattr(op, "close") else None
