@@ -21,6 +21,8 @@ int push_local(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const
 // per-record changelog for time windows (perrecord.cpp / k_perrecord.hip)
 int perrecord_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err);
 int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err);
+bool perrecord_part_eligible(const Program &prog, uint64_t wpr);
+int perrecord_part_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err);
 int push_time_perrecord(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
                         const Batch &kb, const int64_t *seq, const int64_t *rec_wm, PushResult &r, std::string &err);
 

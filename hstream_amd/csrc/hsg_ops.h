@@ -127,6 +127,8 @@ struct OpDevice {
   bool ext_out = false;
   // per-record / session scratch (sort + scan)
   PrBuffers pr = {};
+  PrPart prp = {};              // per-record changelog on the partitioned pipeline (k_prpart.hip)
+  bool pr_part = false;
   void *scratch = nullptr;
   uint64_t scratch_bytes = 0;
   // exchange buffers (multi-GPU)

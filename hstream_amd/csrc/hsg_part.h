@@ -45,6 +45,10 @@ struct PartBuffers {
   uint64_t *seg;          // [workgroups][kMaxSeg][2] general kernel: deferred flush segments (first entry, count)
   uint64_t pane_cap;      // entries pb.pane holds
   uint64_t n_cap;
+  uint32_t *tpairs;       // per-record changelog only (else null): [tiles] accepted (record, window)
+                          // pairs of each tile, written by the histogram pass
+  uint32_t *pos;          // per-record changelog only (else null): [n] partitioned index of each
+                          // arrival-order record, written by the scatter
 };
 
 struct PartParams {
@@ -102,6 +106,8 @@ bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, cons
                      const PartBuffers &pb, uint64_t n, DevScalars *sc, bool maybe_packed, const OutCols *out,
                      uint64_t out_base, uint64_t out_cap, bool wide = true, bool *lean = nullptr);
 bool part_supported(const Program &prog);
+// chunk map of the aggregation workgroups (buckets split into pp.chunk records)
+void launch_part_chunks(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc);
 // Lean aggregation of packed tumbling / unwindowed batches (pane_S = 1, no key
 // rounds, a specialised slot program): records -> LDS table -> group partials
 // in pb.pane, applied to the HBM table by a separate launch (k_agg_lean.hip).

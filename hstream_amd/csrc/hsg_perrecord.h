@@ -26,6 +26,24 @@ struct PrBuffers {
   uint64_t max_pairs;
 };
 
+// Per-record changelog of time windows on the partitioned pipeline
+// (k_prpart.hip). Pairs = (record, accepted window); "bucket-major pair
+// position" = the record's index in the partitioned array x wpr + window.
+constexpr int kPrPairs = 2048;         // pairs per k_pr_local chunk (its LDS sort)
+constexpr int kPrEmitRecs = 16384;     // arrival-order records per k_pr_emit workgroup (4 partition tiles)
+struct PrPart {
+  uint32_t *tpairs;   // [tiles] accepted pairs of each partition tile (the histogram pass)
+  uint64_t *tpoff;    // [tiles] exclusive prefix of tpairs: the tile's first changelog row
+  uint32_t *pos;      // [n] partitioned (bucket-major) index of each arrival-order record (the scatter)
+  uint64_t *inter;    // [n * wpr][1 + ns] per pair: its partial's index, its inclusive prefix in the chunk
+  uint64_t *gkey;     // [n * wpr] group key of each partial
+  int64_t *part;      // [n * wpr][ns] each partial's chunk total, then its carry (the row before the chunk)
+  uint32_t *cbase;    // [chunks] first partial of each k_pr_local chunk
+  uint32_t *ccnt;     // [chunks] partials of each chunk
+  uint64_t *counter;  // partials allocated in this batch
+  uint64_t *partial;  // scan partials
+};
+
 void launch_pr_count(hipStream_t s, const Batch &b, const TwParams &p, const TwTable &t, const int64_t *tprefix,
                      const int64_t *rec_wm, const PrBuffers &pb, DevScalars *sc);
 void launch_pr_expand(hipStream_t s, const Batch &b, const TwParams &p, const TwTable &t, const int64_t *tprefix,
@@ -34,5 +52,11 @@ void launch_pr_segscan(hipStream_t s, const Batch &b, const Program &prog, const
                        const TwTable &t, const uint32_t *slot, const uint32_t *pidx, uint64_t P, const int64_t *seq,
                        OutCols out, uint64_t out_base, DevScalars *sc);
 uint64_t seg_tiles(uint64_t P);
+struct PartParams;
+struct PartBuffers;
+// k_pr_local + k_pr_carry + k_pr_emit over a partitioned batch (chunks mapped)
+void launch_pr_part(hipStream_t s, const Batch &b, const Program &prog, const TwParams &p, const PartParams &pp,
+                    const TwTable &t, const PartBuffers &pb, const PrPart &pr, uint32_t wpr, const int64_t *rec_wm,
+                    const int64_t *seq, const OutCols &out, uint64_t out_base, uint64_t out_cap, DevScalars *sc);
 
 }  // namespace hsg

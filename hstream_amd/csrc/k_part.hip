@@ -156,6 +156,7 @@ __global__ __launch_bounds__(kPNT) void k_part_hist(Batch b, TwParams p, PartPar
   __shared__ uint32_t cnt[1 << kPartMaxLog2];
   __shared__ uint64_t sred[kPNT / 64];
   __shared__ uint64_t sext[2][kPNT / 64];
+  __shared__ uint64_t spairs[kPNT / 64];
   const int nb = 1 << pp.np_log2;
   const uint64_t tile = xcd_tile(blockIdx.x, pp.tiles);
   for (int i = threadIdx.x; i < nb; i += kPNT) cnt[i] = 0;
@@ -166,11 +167,13 @@ __global__ __launch_bounds__(kPNT) void k_part_hist(Batch b, TwParams p, PartPar
   // stream-time inputs of the batch come out of the same walk: max ts of every
   // record (Processor.hs:139), min ts of the keyed records (as k_tile_stats)
   uint64_t ext[2] = {0, 0};
+  uint64_t npairs = 0;
   for (int st = 0; st < pp.sub; ++st) {
     uint64_t e2[2] = {0, 0};
     walk_tile<T, kPNT>(b, p, tile * pp.sub + st, sc->k_epoch, opt ? nullptr : pick_wm(rec_wm, own_wm, sc), late, err,
-                       [&](int, uint64_t, uint32_t key, uint32_t, uint32_t) {
+                       [&](int, uint64_t, uint32_t key, uint32_t, uint32_t nwin) {
                          atomicAdd(&cnt[bucket_of(key, pp.np_log2, pp.bshift)], 1u);
+                         npairs += nwin;
                        },
                        opt ? e2 : nullptr);
     ext[0] = e2[0] > ext[0] ? e2[0] : ext[0];
@@ -205,9 +208,18 @@ __global__ __launch_bounds__(kPNT) void k_part_hist(Batch b, TwParams p, PartPar
   // turn them into bucket-major offsets)
   for (int i = threadIdx.x; i < nb; i += kPNT) pb.hist[tile * (uint64_t)nb + i] = cnt[i];
   late = wave_sum_u64(late);
-  if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = late;
+  npairs = wave_sum_u64(npairs);
+  if ((threadIdx.x & 63) == 0) {
+    sred[threadIdx.x >> 6] = late;
+    spairs[threadIdx.x >> 6] = npairs;
+  }
   if (err) atomicOr(&sc->err, err);
   __syncthreads();
+  if (threadIdx.x == 0 && pb.tpairs) {
+    uint64_t tp = 0;
+    for (int k = 0; k < kPNT / 64; ++k) tp += spairs[k];
+    pb.tpairs[tile] = (uint32_t)tp;
+  }
   if (threadIdx.x == 0) {
     uint64_t l = 0;
     for (int k = 0; k < kPNT / 64; ++k) l += sred[k];
@@ -224,6 +236,7 @@ __global__ __launch_bounds__(kPNT) void k_part_hist_opt(Batch b, TwParams p, Par
                                                         DevScalars *sc) {
   __shared__ uint32_t cnt[1 << kPartMaxLog2];
   __shared__ uint64_t sext[2][kPNT / 64];
+  __shared__ uint32_t spairs[kPNT / 64];
   constexpr int R = T / kPNT;
   const int nb = 1 << pp.np_log2;
   const uint64_t tile = xcd_tile(blockIdx.x, pp.tiles);  // offsets row
@@ -231,6 +244,7 @@ __global__ __launch_bounds__(kPNT) void k_part_hist_opt(Batch b, TwParams p, Par
   for (int i = threadIdx.x; i < nb; i += kPNT) cnt[i] = 0;
   __syncthreads();
   uint64_t mx = 0, mn = 0;
+  uint32_t npairs = 0;
   for (int st = 0; st < pp.sub; ++st) {
   const uint64_t base = (tile * pp.sub + st) * T;
   if (base >= b.n) break;  // uniform
@@ -279,8 +293,10 @@ __global__ __launch_bounds__(kPNT) void k_part_hist_opt(Batch b, TwParams p, Par
     if (z > 0xFFFFFFFFll) z = 0xFFFFFFFFll;
     if (a > z) continue;
     atomicAdd(&cnt[bucket_of(key[r], pp.np_log2, pp.bshift)], 1u);
+    npairs += (uint32_t)(z - a + 1);
   }
   }  // sub-tiles
+  npairs = (uint32_t)wave_sum_u64(npairs);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const uint64_t x = __shfl_xor(mx, o, 64), c = __shfl_xor(mn, o, 64);
@@ -290,9 +306,15 @@ __global__ __launch_bounds__(kPNT) void k_part_hist_opt(Batch b, TwParams p, Par
   if ((threadIdx.x & 63) == 0) {
     sext[0][threadIdx.x >> 6] = mx;
     sext[1][threadIdx.x >> 6] = mn;
+    spairs[threadIdx.x >> 6] = npairs;
   }
   __syncthreads();
   for (int i = threadIdx.x; i < nb; i += kPNT) pb.hist[tile * (uint64_t)nb + i] = cnt[i];
+  if (threadIdx.x == 0 && pb.tpairs) {
+    uint32_t tp = 0;
+    for (int k = 0; k < kPNT / 64; ++k) tp += spairs[k];
+    pb.tpairs[tile] = tp;  // accepted pairs of the tile (no record late: every window of the range)
+  }
   if (threadIdx.x == 0) {
     for (int k = 0; k < kPNT / 64; ++k) {
       mx = sext[0][k] > mx ? sext[0][k] : mx;
@@ -407,6 +429,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
       const uint64_t i = base + j;
       const uint64_t dest = (uint64_t)goff[bk] + (q - lstart[bk]);
       uint64_t v;
+      if (w == 0 && pb.pos) pb.pos[i] = (uint32_t)dest;
       const uint32_t wc = packed ? w + 1 : w;  // word index in the wide layout (packed: 0 is both headers)
       if (w == 0 && packed) {
         uint64_t vb = 0;
@@ -649,6 +672,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (slot[r] == ~0u) continue;
+      if (pb.pos) pb.pos[base + (uint64_t)r * kPNT + threadIdx.x] = cursor[slot[r] >> 16] + (slot[r] & 0xFFFFu);
       const uint32_t q = lstart[slot[r] >> 16] + (slot[r] & 0xFFFFu);
       stage[q * W] = (uint64_t)ts[r];
       if (W == 2) stage[q * W + 1] = col[r];
@@ -835,6 +859,11 @@ __global__ __launch_bounds__(1024) void k_part_chunks(const uint64_t *bstart, in
 }
 
 bool part_supported(const Program &prog) { return prog.n_slots <= 8; }
+
+void launch_part_chunks(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc) {
+  hipLaunchKernelGGL(k_part_chunks, dim3(1), dim3(1024), 0, s, pb.bstart, pp.np_log2, pp.chunk, pb.chunk_start,
+                     pb.chunk_bucket, sc);
+}
 
 // ---------------------------------------------------------------------------
 // per-batch changelog: one row per first update of a group in the touched list

@@ -266,7 +266,10 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
   d.own_out = d.out;
   d.own_out_cap = d.out_cap;
   if (rc != HSG_OK) return rc;
-  if (cfg.emit_mode == HSG_EMIT_PER_RECORD || (cfg.window_kind == HSG_SESSION && !d.ss_merge)) {
+  if (cfg.emit_mode == HSG_EMIT_PER_RECORD && cfg.window_kind != HSG_SESSION && perrecord_part_eligible(prog, wpr)) {
+    rc = perrecord_part_init(d, cfg, prog, err);
+    if (rc != HSG_OK) return rc;
+  } else if (cfg.emit_mode == HSG_EMIT_PER_RECORD || (cfg.window_kind == HSG_SESSION && !d.ss_merge)) {
     rc = perrecord_device_init(d, cfg, prog, err);
     if (rc != HSG_OK) return rc;
   } else if (part_supported(prog)) {

@@ -6,6 +6,7 @@
 #include <string>
 
 #include "hsg_kernels.h"
+#include "hsg_part.h"
 #include "hsg_perrecord.h"
 #include "hsg_sort.h"
 
@@ -85,8 +86,131 @@ int perrecord_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &
   return HSG_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Per-record changelog on the partitioned pipeline (k_prpart.hip): ops with
+// <= 8 state slots and < 256 windows per record. Others: the sort path below.
+// ---------------------------------------------------------------------------
+static bool has_last_slot(const Program &prog) {
+  for (int s = 0; s < prog.n_slots; ++s)
+    if (prog.slot_op[s] == S_LAST_SEQ) return true;
+  return false;
+}
+
+bool perrecord_part_eligible(const Program &prog, uint64_t wpr) { return part_supported(prog) && wpr < 256; }
+
+int perrecord_part_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err) {
+  int rc = part_device_init(d, cfg, prog, err);
+  if (rc != HSG_OK) return rc;
+  const uint64_t n = d.batch_cap, wpr = d.wpr ? d.wpr : 1, P = n * wpr, ns = (uint64_t)prog.n_slots;
+  if (P >= 0xFFFFFFFFull) {
+    err = "batch_capacity x windows per record must be < 2^32 for the per-record changelog";
+    return HSG_E_INVALID;
+  }
+  const uint64_t tiles = part_tiles(n, kPartTileRecs) + 2;
+  const uint64_t chunks = (1ull << kPartMaxLog2) + n / (kPrPairs / wpr) + 2;
+  auto layout = [&](Carve &c, PrPart &x) {
+    x.tpairs = c.take<uint32_t>(tiles);
+    x.tpoff = c.take<uint64_t>(tiles + 1);
+    x.pos = c.take<uint32_t>(n);
+    x.inter = c.take<uint64_t>(P * (1 + ns));
+    x.gkey = c.take<uint64_t>(P);
+    x.part = c.take<int64_t>(P * ns);
+    x.cbase = c.take<uint32_t>(chunks);
+    x.ccnt = c.take<uint32_t>(chunks);
+    x.counter = c.take<uint64_t>(8);
+    x.partial = c.take<uint64_t>(scan_partials_needed(tiles) + 8);
+  };
+  Carve probe{nullptr};
+  PrPart tmp;
+  layout(probe, tmp);
+  DTRY(hipMalloc(&d.scratch, probe.used));
+  d.scratch_bytes = probe.used;
+  Carve real{(char *)d.scratch};
+  layout(real, d.prp);
+  d.part.tpairs = d.prp.tpairs;
+  d.part.pos = d.prp.pos;
+  d.pr_part = true;
+  return HSG_OK;
+}
+
+// buckets of about four chunks: k_pr_carry walks a bucket's chunks in order,
+// and k_pr_emit's gathers read runs of (records per emit tile / buckets)
+static int pr_buckets_log2(uint64_t n, uint64_t chunk) {
+  const uint64_t want = n / (4 * chunk);
+  int l = 0;
+  while ((1ull << l) < want && l < kPartMaxLog2) ++l;
+  return l < 4 ? 4 : l;
+}
+
+static int push_time_perrecord_part(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
+                                    const Batch &kb, const int64_t *seq, const int64_t *rec_wm, PushResult &r,
+                                    std::string &err) {
+  TwParams p = make_tw_params(cfg, a);
+  const uint32_t wpr = (uint32_t)(d.wpr ? d.wpr : 1);
+  // optimistic: the histogram assumes no record is late and the decide step
+  // checks it on the device (as the per-batch pipeline, op_device.cpp); a
+  // batch with late records runs again with per-record stream time
+  const bool opt = !rec_wm && cfg.grace_ms >= 0;
+  const bool need_epoch = !d.h_sc->epoch_set;
+  const bool last = has_last_slot(prog);
+  auto run = [&](bool optimistic) -> int {
+    int rc = clear_batch_scalars(d, err);
+    if (rc != HSG_OK) return rc;
+    if (!kb.n) return HSG_OK;
+    if (!optimistic) launch_stream_time(d, cfg, kb, a.wm_in, p.adv);
+    else if (need_epoch) launch_epoch_first(d.stream, kb, p.adv, d.sc);
+    DTRY(hipEventRecord(d.ev_a, d.stream));
+    PartParams pp;
+    memset(&pp, 0, sizeof(pp));
+    pp.chunk = kPrPairs / wpr;
+    pp.np_log2 = pr_buckets_log2(kb.n, pp.chunk);
+    pp.bshift = d.bshift;
+    for (int c = 0; c < cfg.n_cols; ++c) pp.has_valid |= kb.valid[c] != nullptr;
+    pp.has_seq = last ? 1 : 0;
+    pp.words = part_words(cfg.n_cols, last);
+    pp.tile = part_tile_for(pp.words);
+    pp.sub = 1;
+    pp.tiles = part_tiles(kb.n, pp.tile);
+    pp.pane_S = 1;
+    if (!rec_wm && !optimistic) launch_part_recwm(d.stream, kb, d.tile_prefix, d.sc, d.part.wm);
+    launch_part_hist(d.stream, kb, p, pp, rec_wm, d.part.wm, d.part, d.sc, optimistic);
+    const bool can_pack = optimistic && cfg.n_cols <= 8 && wpr < 256;
+    if (optimistic)
+      launch_part_decide_offsets(d.stream, d.sc, p, a.wm_in, cfg.grace_ms, can_pack, pp, d.part);
+    else
+      launch_part_offsets(d.stream, pp, d.part, d.sc);
+    // each tile's first changelog row; the batch's rows in sc->out_rows
+    scan_excl_u32(d.stream, d.prp.tpairs, d.prp.tpoff, pp.tiles, d.prp.partial, &d.sc->out_rows);
+    launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc, can_pack, true);
+    wait_table_reset(d);  // the passes above do not touch the table
+    DTRY(hipMemsetAsync(d.prp.counter, 0, 8, d.stream));
+    launch_part_chunks(d.stream, pp, d.part, d.sc);
+    launch_pr_part(d.stream, kb, prog, p, pp, d.tw, d.part, d.prp, wpr, rec_wm, seq, d.out, a.pending, d.out_cap,
+                   d.sc);
+    DTRY(hipEventRecord(d.ev_b, d.stream));
+    DTRY(hipGetLastError());
+    return HSG_OK;
+  };
+  int rc = run(opt);
+  if (rc != HSG_OK) return rc;
+  rc = finish_batch(d, a.wm_in, kb.n, r, err);
+  if (opt && kb.n && d.h_sc->redo) {
+    rc = run(false);
+    if (rc != HSG_OK) return rc;
+    rc = finish_batch(d, a.wm_in, kb.n, r, err);
+  }
+  r.pairs = r.out_rows;
+  if (kb.n) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, d.ev_a, d.ev_b) == hipSuccess) r.agg_ms = ms;
+    r.agg_launches = 1;
+  }
+  return rc;
+}
+
 int push_time_perrecord(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
                         const Batch &kb, const int64_t *seq, const int64_t *rec_wm, PushResult &r, std::string &err) {
+  if (d.pr_part) return push_time_perrecord_part(d, cfg, prog, a, kb, seq, rec_wm, r, err);
   wait_table_reset(d);
   TwParams p = make_tw_params(cfg, a);
   int rc = clear_batch_scalars(d, err);

@@ -299,3 +299,36 @@ def test_exchange_path_single_rank(xeng, spec, late, xpart, monkeypatch):
     rows_equal(g.dump_state(), o.dump_state(), f64, what="state")
     st = g.stats()
     assert st["records_owned"] == sum(int((b[0] != abi.HSG_KEY_NONE).sum()) for b in batches)
+
+
+@pytest.mark.parametrize("kind,kw", [(abi.HSG_TUMBLING, dict(size_ms=10_000)),
+                                     (abi.HSG_HOPPING, dict(size_ms=10_000, advance_ms=3_000)),
+                                     (abi.HSG_UNWINDOWED, {})], ids=["tumbling", "hopping", "unwindowed"])
+@pytest.mark.parametrize("late", [False, True], ids=["in_time", "late"])
+def test_per_record_groups_span_chunks(eng, kind, kw, late):
+    """EMIT CHANGES (TimeWindowedStream.hs:89-103) where a few keys carry
+    whole batches: each group's records span many k_pr_local chunks of its
+    bucket, which k_pr_carry applies in arrival order; rows in arrival x
+    window order, bit-exact against the oracle (LAST included)."""
+    spec = OpSpec(kind, abi.HSG_EMIT_PER_RECORD, col_types=[abi.HSG_I64], aggs=ALL_AGG_SETS["full_i64"], **kw)
+    batches = []
+    for bi in range(3):
+        key, ts, cols, valid = gen_small(77 + bi, 60_000, 3, span=40_000, base=5_000_000 + bi * 40_000,
+                                         very_late=late)
+        batches.append((key, ts, cols, valid))
+    _drive(eng, spec, batches)
+
+
+@pytest.mark.parametrize("name", ["C2", "C2f", "C5"])
+def test_per_record_configs_reduced(eng, name):
+    """The per-record changelog on the C2 / C2f / C5 workloads at reduced size
+    (2 batches of 2^18 records), ordered rows against the oracle."""
+    from hstream_amd import datagen
+    cfg = datagen.CONFIGS[name]
+    spec = cfg.spec(abi.HSG_EMIT_PER_RECORD)
+    n, batch = 1 << 19, 1 << 18
+    batches = []
+    for s in range(0, n, batch):
+        h = datagen.generate(cfg, n=batch, start=s, total=n)
+        batches.append((h["key_id"], h["ts"], h["cols"], None))
+    _drive(eng, spec, batches)
