@@ -103,6 +103,39 @@ __device__ inline const int64_t *pick_wm(const int64_t *rec_wm, const int64_t *o
 // Order-preserving u64 image of an i64 (max of images = image of the max).
 __device__ inline uint64_t i64_ord(int64_t v) { return (uint64_t)v ^ 0x8000000000000000ull; }
 
+// Stable ranking for the per-record changelog, which needs a bucket's records
+// in arrival order (k_prpart.hip): a tile's records are ranked in rounds of
+// kPNT consecutive records (record = round * kPNT + thread), so within a
+// round the lanes of earlier waves and lower lanes come first. Lanes of one
+// wave with the same bucket find each other with one ballot per bucket bit;
+// wcnt[w][b] holds wave w's count of bucket b in this round (cleared again by
+// its writer before the next round). Returns this record's rank among its
+// bucket's records of the round (earlier rounds are the caller's base).
+constexpr int kPNT = 512;  // threads of the partition passes
+constexpr int kPW = kPNT / 64;
+__device__ inline uint32_t stable_round_rank(uint32_t bk, bool ok, int nbits, uint8_t (*wcnt)[1 << kPartMaxLog2],
+                                             uint64_t &peers) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t m = __ballot(ok);
+  for (int bit = 0; bit < nbits; ++bit) {
+    const bool x = (bk >> bit) & 1u;
+    const uint64_t bb = __ballot(x);
+    m &= x ? bb : ~bb;
+  }
+  peers = m;
+  const bool leader = ok && (m >> lane) == 1ull;
+  if (leader) wcnt[wv][bk] = (uint8_t)__popcll(m);
+  lds_barrier();
+  uint32_t before = 0;
+  if (ok)
+    for (int w = 0; w < wv; ++w) before += wcnt[w][bk];
+  return before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+__device__ inline void stable_round_done(uint32_t bk, bool ok, uint64_t peers, uint8_t (*wcnt)[1 << kPartMaxLog2]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (ok && (peers >> lane) == 1ull) wcnt[wv][bk] = 0;
+}
+
 // Walk the T records of one partition tile with NT threads (record (r, t) =
 // tile*T + r*NT + t); calls f(j, i, key, krel, nwin) for every record with
 // >= 1 accepted window (j = tile-local index, i = batch index). No barriers.
@@ -146,7 +179,6 @@ __device__ inline void walk_tile(const Batch &b, const TwParams &p, uint64_t til
   }
 }
 
-constexpr int kPNT = 512;  // threads of the partition passes
 
 template <int T>
 __global__ __launch_bounds__(kPNT) void k_part_hist(Batch b, TwParams p, PartParams pp,
@@ -337,12 +369,13 @@ __global__ __launch_bounds__(kPNT) void k_part_hist_opt(Batch b, TwParams p, Par
 // Record layouts (sc->packed, decided per batch on the device):
 //   wide   [key | krel << 32] [nwin | valid bits << 32] [col 0 .. C-1] [seq + 1]?
 //   packed [key | (krel - kbase) << 32 | nwin << 48 | valid bits << 56] [cols] [seq + 1]?
-template <int T>
+template <int T, bool STABLE>
 __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, PartParams pp,
                                                        const int64_t *__restrict__ rec_wm,
                                                        const int64_t *__restrict__ own_wm,
                                                        const int64_t *__restrict__ seq, PartBuffers pb,
                                                        DevScalars *sc, int staged) {
+  __shared__ uint8_t wcnt[STABLE ? kPW : 1][1 << kPartMaxLog2];
   __shared__ uint16_t lbk[T];
   __shared__ uint16_t sidx[T];
   __shared__ uint64_t lkn[T];  // krel | nwin << 32
@@ -363,6 +396,8 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
     cursor[i] = 0;
     goff[i] = pb.offt[row * (uint64_t)nb + i];
   }
+  if constexpr (STABLE)
+    for (int i = threadIdx.x; i < kPW * nb; i += kPNT) wcnt[i / nb][i % nb] = 0;
   const int per = (nb + kPNT - 1) / kPNT;
   const int lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -408,11 +443,28 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
     for (int k = 0; k < kPNT / 64; ++k) placed += swave[k];
     __syncthreads();
     q2 = wall_clock64();
-    // 3) bucket-sorted order of the sub-tile's records
-    for (int j = threadIdx.x; j < T; j += kPNT) {
-      const uint16_t bk = lbk[j];
-      if (bk == kNoBucket) continue;
-      sidx[lstart[bk] + atomicAdd(&cursor[bk], 1u)] = (uint16_t)j;
+    // 3) bucket-sorted order of the sub-tile's records (STABLE: in arrival
+    // order inside each bucket's run)
+    if constexpr (STABLE) {
+      for (int j = threadIdx.x; j < T; j += kPNT) {  // uniform trip count (T % kPNT == 0)
+        const uint16_t bk = lbk[j];
+        const bool ok = bk != kNoBucket;
+        uint64_t peers;
+        const uint32_t rk = stable_round_rank(ok ? bk : 0u, ok, pp.np_log2, wcnt, peers);
+        const uint32_t base_rk = ok ? cursor[bk] : 0u;
+        lds_barrier();  // every rank read before the counts move
+        if (ok) {
+          sidx[lstart[bk] + base_rk + rk] = (uint16_t)j;
+          if ((peers >> (threadIdx.x & 63)) == 1ull) atomicAdd(&cursor[bk], (uint32_t)__popcll(peers));
+        }
+        stable_round_done(ok ? bk : 0u, ok, peers, wcnt);
+      }
+    } else {
+      for (int j = threadIdx.x; j < T; j += kPNT) {
+        const uint16_t bk = lbk[j];
+        if (bk == kNoBucket) continue;
+        sidx[lstart[bk] + atomicAdd(&cursor[bk], 1u)] = (uint16_t)j;
+      }
     }
     __syncthreads();
     q3 = wall_clock64();
@@ -589,9 +641,10 @@ void launch_part_decide_offsets(hipStream_t s, DevScalars *sc, const TwParams &p
 // misses (PMC) and waited on them. LDS: the tile (T x W words), two u16
 // counters per u32, u16 run starts: 72 KiB at W = 2, two workgroups per CU.
 // The bucket of a staged record is recomputed from its key at write-out.
-template <int T, int W>
+template <int T, int W, bool STABLE>
 __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, PartParams pp, PartBuffers pb,
                                                           DevScalars *sc) {
+  __shared__ uint8_t wcnt[STABLE ? kPW : 1][1 << kPartMaxLog2];
   __shared__ uint64_t stage[T * W];
   __shared__ uint32_t cnt2[1 << (kPartMaxLog2 - 1)];  // two u16 counts per word, then the u16 run starts
   __shared__ uint32_t cursor[1 << kPartMaxLog2];      // the row's next output slot per bucket
@@ -606,6 +659,8 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
   uint16_t *lstart = reinterpret_cast<uint16_t *>(cnt2);
   for (int i = threadIdx.x; i < (nb + 1) / 2; i += kPNT) cnt2[i] = 0;
   for (int i = threadIdx.x; i < nb; i += kPNT) cursor[i] = pb.offt[row * (uint64_t)nb + i];
+  if constexpr (STABLE)
+    for (int i = threadIdx.x; i < kPW * nb; i += kPNT) wcnt[i / nb][i % nb] = 0;
   // buckets [lo, hi) of this thread: whole words of cnt2 (scan, run starts)
   const int per = (nb + kPNT - 1) / kPNT;
   const int lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
@@ -630,12 +685,25 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
     uint32_t slot[R];  // bucket << 16 | slot in the sub-tile's run of the bucket, ~0 = no window
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      uint32_t krel, nwin;
+      uint32_t krel = 0, nwin = 0;
       slot[r] = ~0u;
-      if (!part_record(p, k_epoch, key[r], ts[r], INT64_MIN, krel, nwin, late, err)) continue;
-      const uint32_t bk = bucket_of(key[r], pp.np_log2, pp.bshift);
+      const bool ok = part_record(p, k_epoch, key[r], ts[r], INT64_MIN, krel, nwin, late, err);
+      const uint32_t bk = ok ? bucket_of(key[r], pp.np_log2, pp.bshift) : 0u;
       const uint32_t sh = (bk & 1u) * 16u;
-      const uint32_t pos = (atomicAdd(&cnt2[bk >> 1], 1u << sh) >> sh) & 0xFFFFu;
+      uint32_t pos;
+      if constexpr (STABLE) {
+        // rank in arrival order: earlier rounds (cnt2) + this round's earlier lanes
+        uint64_t peers;
+        const uint32_t rk = stable_round_rank(bk, ok, pp.np_log2, wcnt, peers);
+        pos = ok ? ((cnt2[bk >> 1] >> sh) & 0xFFFFu) + rk : 0u;
+        lds_barrier();
+        if (ok && (peers >> (threadIdx.x & 63)) == 1ull) atomicAdd(&cnt2[bk >> 1], (uint32_t)__popcll(peers) << sh);
+        stable_round_done(bk, ok, peers, wcnt);
+        if (!ok) continue;
+      } else {
+        if (!ok) continue;
+        pos = (atomicAdd(&cnt2[bk >> 1], 1u << sh) >> sh) & 0xFFFFu;
+      }
       slot[r] = (bk << 16) | pos;
       const uint64_t i = base + (uint64_t)r * kPNT + threadIdx.x;
       uint64_t vb = 0;
@@ -711,15 +779,25 @@ void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const
   if (!pp.tiles) return;
   const dim3 g((unsigned)pp.tiles);
   const bool stage = maybe_packed && !pp.has_seq && pp.words - 1 <= 2;  // packed words <= 2
+  // the per-record changelog (pb.pos) needs arrival order inside a bucket's runs
+  const bool stable = pb.pos != nullptr;
   if (stage) {
-    if (pp.words - 1 == 2)
-      hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 2>), g, dim3(kPNT), 0, s, b, p, pp, pb, sc);
-    else
-      hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 1>), g, dim3(kPNT), 0, s, b, p, pp, pb, sc);
+    if (pp.words - 1 == 2) {
+      if (stable) hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 2, true>), g, dim3(kPNT), 0, s, b, p, pp, pb, sc);
+      else hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 2, false>), g, dim3(kPNT), 0, s, b, p, pp, pb, sc);
+    } else {
+      if (stable) hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 1, true>), g, dim3(kPNT), 0, s, b, p, pp, pb, sc);
+      else hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 1, false>), g, dim3(kPNT), 0, s, b, p, pp, pb, sc);
+    }
   }
-  if (wide || !stage)
-    hipLaunchKernelGGL(k_part_scatter<kPartTileRecs>, g, dim3(kPNT), 0, s, b, p, pp, rec_wm, own_wm, seq, pb, sc,
-                       stage ? 1 : 0);
+  if (wide || !stage) {
+    if (stable)
+      hipLaunchKernelGGL((k_part_scatter<kPartTileRecs, true>), g, dim3(kPNT), 0, s, b, p, pp, rec_wm, own_wm, seq, pb,
+                         sc, stage ? 1 : 0);
+    else
+      hipLaunchKernelGGL((k_part_scatter<kPartTileRecs, false>), g, dim3(kPNT), 0, s, b, p, pp, rec_wm, own_wm, seq,
+                         pb, sc, stage ? 1 : 0);
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -550,9 +550,18 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit(Batch bt, Program pr
     const uint64_t i = i0 + r;
     const uint64_t pos = pr.pos[i];
     const int64_t src = seq ? seq[i] : (int64_t)(p.rec_base + i);
+    if (pos >= pb.n_cap) {  // cannot happen: the scatter placed every record with a window
+      err |= ERR_OOM;
+      o += nwin[r];
+      continue;
+    }
     for (uint32_t j = 0; j < nwin[r]; ++j, ++o) {
       const uint64_t *it = pr.inter + (pos * wpr + j) * rw;
       const uint32_t gi = (uint32_t)it[0];
+      if ((uint64_t)gi >= pb.n_cap * wpr) {
+        err |= ERR_OOM;
+        continue;
+      }
       int64_t R[MS];
 #pragma unroll
       for (int s = 0; s < MS; ++s) R[s] = s < ns ? pr.part[(uint64_t)gi * ns + s] : 0;

@@ -86,19 +86,25 @@ int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog,
   const uint64_t ns = (1ull << kPartMaxLog2) * part_nseg(tiles);
   uint64_t o_hist = take(nh * 4), o_offt = take(nh * 4), o_segsum = take(ns * 4), o_segoff = take((ns + 1) * 8);
   uint64_t o_bstart = take(((1ull << kPartMaxLog2) + 1) * 8), o_part = take((scan_partials_needed(ns) + 8) * 8);
+  // records per aggregation workgroup: >= 1024 (kAggChunk / 32 at least), the
+  // per-record changelog's chunks of kPrPairs pairs (k_prpart.hip) fewer
+  const bool per_record = cfg.emit_mode == HSG_EMIT_PER_RECORD;
+  const uint64_t min_chunk = per_record ? (uint64_t)kPrPairs / (d.wpr ? d.wpr : 1) : 1024;
+  const uint64_t nwg = (1ull << kPartMaxLog2) + n / (min_chunk ? min_chunk : 1) + 2;
   uint64_t o_rec = take(n * words * 8), o_chunk = take(((1ull << kPartMaxLog2) + 2) * 4);
-  uint64_t o_cbk = take(((1ull << kPartMaxLog2) + n / 1024 + 2) * 4);  // >= buckets + n / chunk + 1
+  uint64_t o_cbk = take(nwg * 4);  // >= buckets + n / chunk + 1
   const uint64_t tcap = n * (d.wpr ? d.wpr : 1), nc = touch_chunks(tcap);
   uint64_t o_touch = take(tcap * 4), o_wm = take(n * 8);
   uint64_t o_tcnt = take(nc * 4), o_toff = take((nc + 1) * 8), o_tpart = take((scan_partials_needed(nc) + 8) * 8);
   // lean aggregation: one pane entry per record at most, [g][slots]; the
   // general kernel's deferred window updates: up to 2 per record, more fall
   // back to in-kernel updates
-  const uint64_t pcap = n * (d.wpr > 1 ? 2 : 1);
+  // (the per-record changelog uses none of them)
+  const uint64_t pcap = per_record ? 1 : n * (d.wpr > 1 ? 2 : 1);
   uint64_t o_pane = take(pcap * (1 + (uint64_t)prog.n_slots) * 8);
-  uint64_t o_seg = take(((1ull << kPartMaxLog2) + n / 1024 + 2) * kMaxSeg * 16);
-  uint64_t o_pinfo = take(((1ull << kPartMaxLog2) + n / 1024 + 2) * 16);
-  uint64_t o_pcnt = take(((1ull << kPartMaxLog2) + n / 1024 + 2 + 4) * 4);
+  uint64_t o_seg = take(nwg * kMaxSeg * 16);
+  uint64_t o_pinfo = take(nwg * 16);
+  uint64_t o_pcnt = take((nwg + 4) * 4);
   DTRY(hipMalloc(&d.part_mem, off));
   char *m = (char *)d.part_mem;
   pb.hist = (uint32_t *)(m + o_hist);

@@ -227,8 +227,9 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
       DTRY(hipMalloc((void **)&d.emit.partial, (scan_partials_needed(nb) + 8) * 8));
     }
     d.cap = ncap;
-    // the per-record path keeps a [slots][n_slots] shadow table
-    if (cfg.emit_mode == HSG_EMIT_PER_RECORD) {
+    // the sort-based per-record path keeps a [slots][n_slots] shadow table
+    // (the partitioned one, d.pr_part, keeps nothing sized by the table)
+    if (cfg.emit_mode == HSG_EMIT_PER_RECORD && !d.pr_part) {
       DTRY(hipStreamSynchronize(d.stream));
       hipFree(d.scratch);
       d.scratch = nullptr;

@@ -332,3 +332,20 @@ def test_per_record_configs_reduced(eng, name):
         h = datagen.generate(cfg, n=batch, start=s, total=n)
         batches.append((h["key_id"], h["ts"], h["cols"], None))
     _drive(eng, spec, batches)
+
+
+def test_per_record_table_grows(eng):
+    """The per-record changelog with a state table far smaller than the groups:
+    the table grows between batches (retention.cpp) and the changelog stays
+    exact (the per-record scratch is not sized by the table)."""
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_RECORD, size_ms=10_000, col_types=[abi.HSG_I64],
+                  aggs=ALL_AGG_SETS["full_i64"], state_capacity=256)
+    batches = []
+    for bi in range(3):
+        key, ts, cols, valid = gen_small(300 + bi, 40_000, 5_000, span=30_000, base=2_000_000 + bi * 30_000,
+                                         very_late=False)
+        batches.append((key, ts, cols, valid))
+    g, o = _drive(eng, spec, batches)
+    assert g.stats()["grow_events"] >= 1
+    g.close()
+    o.close()
