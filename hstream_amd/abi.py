@@ -24,6 +24,8 @@ STATUS_NAMES = {
 }
 
 HSG_KEY_NONE = 0xFFFFFFFF
+HSG_TRANSPORT_RCCL = 0
+HSG_TRANSPORT_HOST = 1
 HSG_COMM_ID_BYTES = 128
 HSG_DEFAULT_GRACE_MS = 86400000
 
@@ -61,7 +63,7 @@ class hsg_engine_config(C.Structure):
         ("device", C.c_int32),
         ("rank", C.c_int32),
         ("nranks", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("transport", C.c_int32),
         ("comm_id", C.POINTER(C.c_uint8)),
         ("batch_capacity", C.c_uint64),
     ]

@@ -123,7 +123,7 @@ static int push_sharded_fast(OpDevice &d, const hsg_op_config &cfg, const Progra
   const int G = a.nranks, me = a.rank;
   const int IW = info_words(G);
   const int xl = d.xpart_log2;
-  ncclComm_t comm = a.comm->comm;
+  Comm *comm = a.comm;
   hipStream_t s = d.stream;
   fallback = false;
   if (a.batch->n > x.batch) {
@@ -149,7 +149,8 @@ static int push_sharded_fast(OpDevice &d, const hsg_op_config &cfg, const Progra
   launch_part_offsets(s, xp, d.part, d.sc);
   launch_x_info(s, d.sc, d.part.bstart, xl, (uint32_t)G, n, has_valid, x.info, d.part.text, x_tiles(n));
   // 2. all-gather the per-rank facts
-  NTRY(ncclAllGather(x.info, x.info_all, IW, ncclInt64, comm, s));
+  rc = comm_allgather(comm, x.info, x.info_all, IW, ncclInt64, 8, s, err);
+  if (rc != HSG_OK) return rc;
   DTRY(hipMemcpyAsync(x.h_info, x.info_all, (uint64_t)G * IW * 8, hipMemcpyDeviceToHost, s));
   DTRY(hipStreamSynchronize(s));
   const int64_t *H = x.h_info;
@@ -204,18 +205,21 @@ static int push_sharded_fast(OpDevice &d, const hsg_op_config &cfg, const Progra
   };
   const XCols snd = carve(x.send, x.batch), rcv = carve(x.recv, (uint64_t)G * x.batch);
   launch_x_scatter(s, kb, xl, unwin, any_valid, C, d.part.offt, snd);
-  NTRY(ncclGroupStart());
-  NTRY(ncclAllToAllv(snd.key, scount.data(), sdispl.data(), rcv.key, rcount.data(), rdispl.data(), ncclUint32, comm,
-                     s));
-  NTRY(ncclAllToAllv(snd.ts, scount.data(), sdispl.data(), rcv.ts, rcount.data(), rdispl.data(), ncclInt64, comm, s));
+#define XA2A(buf, dt, el)                                                                              \
+  do {                                                                                                  \
+    rc = comm_alltoallv(comm, snd.buf, scount.data(), sdispl.data(), rcv.buf, rcount.data(), rdispl.data(), \
+                        dt, el, s, err);                                                                \
+    if (rc != HSG_OK) return rc;                                                                        \
+  } while (0)
+  if ((rc = comm_group_start(comm, err)) != HSG_OK) return rc;
+  XA2A(key, ncclUint32, 4);
+  XA2A(ts, ncclInt64, 8);
   for (int k = 0; k < C; ++k) {
-    NTRY(ncclAllToAllv(snd.col[k], scount.data(), sdispl.data(), rcv.col[k], rcount.data(), rdispl.data(), ncclInt64,
-                       comm, s));
-    if (any_valid)
-      NTRY(ncclAllToAllv(snd.valid[k], scount.data(), sdispl.data(), rcv.valid[k], rcount.data(), rdispl.data(),
-                         ncclUint8, comm, s));
+    XA2A(col[k], ncclInt64, 8);
+    if (any_valid) XA2A(valid[k], ncclUint8, 1);
   }
-  NTRY(ncclGroupEnd());
+  if ((rc = comm_group_end(comm, err)) != HSG_OK) return rc;
+#undef XA2A
   DTRY(hipEventRecord(d.ev_d, s));
   DTRY(hipGetLastError());
   // 4. aggregate the owned records (order irrelevant for these ops)
@@ -260,7 +264,7 @@ static int push_sharded_classic(OpDevice &d, const hsg_op_config &cfg, const Pro
   XBuffers &x = *d.x;
   const int G = a.nranks, me = a.rank;
   const int IW = info_words(G);
-  ncclComm_t comm = a.comm->comm;
+  Comm *comm = a.comm;
   hipStream_t s = d.stream;
   if (a.batch->n > x.batch) {
     err = "batch larger than batch_capacity";
@@ -284,7 +288,8 @@ static int push_sharded_classic(OpDevice &d, const hsg_op_config &cfg, const Pro
   int which = radix_sort_pairs(s, x.owner, x.idx, x.k1, x.v1, n, 8, x.sort_scratch);
   const uint32_t *sidx = which ? x.v1 : x.idx;
   // 2. all-gather the per-rank facts
-  NTRY(ncclAllGather(x.info, x.info_all, IW, ncclInt64, comm, s));
+  rc = comm_allgather(comm, x.info, x.info_all, IW, ncclInt64, 8, s, err);
+  if (rc != HSG_OK) return rc;
   DTRY(hipMemcpyAsync(x.h_info, x.info_all, (uint64_t)G * IW * 8, hipMemcpyDeviceToHost, s));
   DTRY(hipStreamSynchronize(s));
   const int64_t *H = x.h_info;
@@ -336,8 +341,9 @@ static int push_sharded_classic(OpDevice &d, const hsg_op_config &cfg, const Pro
     return HSG_E_CAPACITY;
   }
   launch_x_pack(s, kb, L, sidx, m_send, seq_base, x.wm_local, x.send);
-  NTRY(ncclAllToAllv(x.send, scount.data(), sdispl.data(), x.recv, rcount.data(), rdispl.data(), ncclUint64, comm,
-                     s));
+  rc = comm_alltoallv(comm, x.send, scount.data(), sdispl.data(), x.recv, rcount.data(), rdispl.data(), ncclUint64, 8,
+                      s, err);
+  if (rc != HSG_OK) return rc;
   XStaging st;
   memset(&st, 0, sizeof(st));
   // received records reuse the op's staging arrays (the local slice is packed already)

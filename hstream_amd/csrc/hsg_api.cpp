@@ -162,8 +162,10 @@ extern "C" int hsg_engine_create(const hsg_engine_config *cfg, hsg_engine **out)
     e->rank = cfg->rank;
     e->nranks = cfg->nranks;
     e->batch_cap = cfg->batch_capacity;
+    if (cfg->transport != HSG_TRANSPORT_RCCL && cfg->transport != HSG_TRANSPORT_HOST) { delete e; return HSG_E_INVALID; }
     if (cfg->nranks > 1 || cfg->comm_id) {
-      int rc = comm_create(cfg->comm_id, cfg->rank, cfg->nranks, dev, &e->comm, e->err);
+      int rc = comm_create(cfg->comm_id, cfg->rank, cfg->nranks, dev, cfg->transport, cfg->batch_capacity, &e->comm,
+                           e->err);
       if (rc != HSG_OK) { delete e; return rc; }
     }
     *out = e;

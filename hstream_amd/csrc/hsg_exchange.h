@@ -10,11 +10,24 @@ namespace hsg {
 
 constexpr int kMaxRanks = 64;
 
+struct HostComm;  // shared-memory transport (comm.cpp)
+
 struct Comm {
-  ncclComm_t comm = nullptr;
+  ncclComm_t comm = nullptr;   // RCCL
+  HostComm *host = nullptr;    // HSG_TRANSPORT_HOST (tests: several ranks on one GPU)
+  uint64_t slot_bytes = 0;
   int rank = 0;
   int nranks = 1;
 };
+
+// collectives over either transport (RCCL calls, or the host copies)
+int comm_group_start(Comm *c, std::string &err);
+int comm_group_end(Comm *c, std::string &err);
+int comm_allgather(Comm *c, const void *send, void *recv, size_t count, ncclDataType_t dt, size_t elem,
+                   hipStream_t s, std::string &err);
+int comm_alltoallv(Comm *c, const void *send, const size_t *scount, const size_t *sdispl, void *recv,
+                   const size_t *rcount, const size_t *rdispl, ncclDataType_t dt, size_t elem, hipStream_t s,
+                   std::string &err);
 
 struct XLayout {
   int32_t words;     // 8-byte words per record

@@ -16,8 +16,9 @@ struct Comm;      // RCCL communicator wrapper (hsg_exchange.h)
 struct XBuffers;  // exchange scratch (hsg_exchange.h)
 
 int comm_unique_id(uint8_t *out);
-int comm_create(const uint8_t *id, int rank, int nranks, int device, Comm **out, std::string &err);
-int comm_split(const Comm *parent, Comm **out, std::string &err);
+int comm_create(const uint8_t *id, int rank, int nranks, int device, int transport, uint64_t batch_cap, Comm **out,
+                std::string &err);
+int comm_split(Comm *parent, Comm **out, std::string &err);
 void comm_destroy(Comm *c);
 
 // Session store in HBM (k_session.hip, hsg_session.h): a growable key table

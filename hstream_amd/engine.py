@@ -61,12 +61,20 @@ def comm_unique_id() -> bytes:
 class Engine:
     """One per process and GPU (hsg_engine_create)."""
 
-    def __init__(self, device=0, rank=0, nranks=1, comm_id=None, batch_capacity=1 << 24):
+    def __init__(self, device=0, rank=0, nranks=1, comm_id=None, batch_capacity=1 << 24,
+                 transport=abi.HSG_TRANSPORT_RCCL):
+        """comm_id: RCCL id bytes (comm_unique_id() on rank 0) or, with
+        transport=HSG_TRANSPORT_HOST, a segment name (str / bytes) shared by
+        the ranks of one host."""
         L = load_library()
         self._lib = L
         self._id_buf = None
-        cfg = abi.hsg_engine_config(device=device, rank=rank, nranks=nranks, reserved0=0,
+        cfg = abi.hsg_engine_config(device=device, rank=rank, nranks=nranks, transport=transport,
                                     comm_id=None, batch_capacity=batch_capacity)
+        if isinstance(comm_id, str):
+            comm_id = comm_id.encode()
+        if comm_id is not None and transport == abi.HSG_TRANSPORT_HOST:
+            comm_id = comm_id[: abi.HSG_COMM_ID_BYTES - 1].ljust(abi.HSG_COMM_ID_BYTES, b"\0")
         if comm_id is not None:
             self._id_buf = (C.c_uint8 * abi.HSG_COMM_ID_BYTES)(*comm_id[: abi.HSG_COMM_ID_BYTES])
             cfg.comm_id = C.cast(self._id_buf, P_u8)

@@ -103,13 +103,19 @@ enum hsg_mem { HSG_MEM_HOST = 0, HSG_MEM_DEVICE = 1 };
 typedef struct hsg_engine hsg_engine;
 typedef struct hsg_op hsg_op;
 
+/* transports of the key exchange */
+#define HSG_TRANSPORT_RCCL 0  /* one process per GPU over RCCL (xGMI)                       */
+#define HSG_TRANSPORT_HOST 1  /* ranks of one host through shared memory (several ranks may
+                                 share one GPU): for testing the multi-rank sequencing    */
+
 typedef struct {
   int32_t device;          /* HIP device ordinal; -1 = the calling thread's current device */
   int32_t rank;            /* this process's rank in the key-sharded group                */
   int32_t nranks;          /* 1 = single GPU, no communicator                              */
-  int32_t reserved0;
-  const uint8_t *comm_id;  /* HSG_COMM_ID_BYTES from hsg_comm_unique_id() on rank 0, shared
-                              out of band; NULL when nranks == 1                            */
+  int32_t transport;       /* HSG_TRANSPORT_RCCL (0) or HSG_TRANSPORT_HOST                  */
+  const uint8_t *comm_id;  /* RCCL: HSG_COMM_ID_BYTES from hsg_comm_unique_id() on rank 0,
+                              shared out of band; HOST: a NUL-terminated segment name (the
+                              same on every rank, no '/'); NULL when nranks == 1           */
   uint64_t batch_capacity; /* max records per hsg_push_batch on this rank                   */
 } hsg_engine_config;
 

@@ -1,0 +1,121 @@
+"""GPU, two ranks: the real multi-rank C++ exchange (hstream_amd/csrc/
+exchange.cpp) -- all-gather of the per-rank facts, stream-time carry,
+sequence bases, fast-vs-classic decision, owner partition, all-to-all-v,
+per-rank aggregation -- driven by two processes that share cuda:0 over the
+host transport (HSG_TRANSPORT_HOST: the same collectives through shared
+memory instead of RCCL, which needs one GPU per rank). Each rank pushes its
+slice of every global batch; the union of the ranks' changelogs and state
+must equal one oracle fed the whole stream (keys shard by hash,
+each GPU owns its key range, results equal one GPU fed everything).
+
+tests/test_sharded_gloo.py restates the same protocol in Python on the CPU;
+this runs the library itself."""
+import os
+import uuid
+
+import numpy as np
+import pytest
+
+from hstream_amd import abi
+from hstream_amd.columnar import OpSpec
+from test_sharded_gloo import SPECS, _batches, _close
+from util import ALL_AGG_SETS
+
+pytestmark = pytest.mark.gpu
+
+GPU_SPECS = dict(SPECS)
+# the per-record changelog on the partitioned pipeline (<= 8 slots, with LAST)
+GPU_SPECS["hopping_pr_part"] = OpSpec(abi.HSG_HOPPING, abi.HSG_EMIT_PER_RECORD, size_ms=10_000, advance_ms=3_000,
+                                      col_types=[abi.HSG_I64, abi.HSG_F64], aggs=ALL_AGG_SETS["full_i64"])
+GPU_SPECS["tumbling_pr_part"] = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_RECORD, size_ms=10_000,
+                                       col_types=[abi.HSG_I64, abi.HSG_F64],
+                                       aggs=[(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0), (abi.HSG_MAX, 1)])
+# sessions on the merge path (per-batch changelog)
+GPU_SPECS["session_merge"] = OpSpec(abi.HSG_SESSION, abi.HSG_EMIT_PER_BATCH, gap_ms=2_000,
+                                    col_types=[abi.HSG_I64, abi.HSG_F64],
+                                    aggs=[(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0), (abi.HSG_MIN, 1)])
+
+
+def _rows(spec, r):
+    if spec.emit_mode == abi.HSG_EMIT_PER_BATCH:
+        r.src_index[:] = -1
+    return [(int(r.key_id[i]), int(r.win_start[i]), int(r.win_end[i]), int(r.src_index[i]),
+             tuple(a[i].item() for a in r.aggs)) for i in range(len(r))]
+
+
+def _gpu_worker(rank, G, name, spec_name, late, q):
+    try:
+        from hstream_amd.engine import Engine
+        eng = Engine(device=0, rank=rank, nranks=G, comm_id=name, batch_capacity=1 << 13,
+                     transport=abi.HSG_TRANSPORT_HOST)
+        spec = GPU_SPECS[spec_name]
+        op = eng.op(spec)
+        wm, results = -1, []
+        for slices in _batches(G, late):
+            key, ts, cols, valid = slices[rank]
+            wm = op.push(key, ts, cols, valid, watermark=wm)
+            results.append(None if spec.emit_mode == abi.HSG_EMIT_NONE else _rows(spec, op.drain()))
+        state = op.dump_state().tuples()
+        op.close()
+        eng.close()
+        q.put((rank, wm, results, state))
+    except Exception as e:  # reported to the parent, which fails the test
+        q.put((rank, "error", repr(e), None))
+
+
+def _single(spec_name, G, late):
+    import pyoracle
+    spec = GPU_SPECS[spec_name]
+    op = pyoracle.OracleOp(spec)
+    wm, results = -1, []
+    for slices in _batches(G, late):
+        key = np.concatenate([s[0] for s in slices])
+        ts = np.concatenate([s[1] for s in slices])
+        cols = [np.concatenate([s[2][c] for s in slices]) for c in range(2)]
+        valid = [np.concatenate([s[3][c] for s in slices]) for c in range(2)]
+        wm = op.push(key, ts, cols, valid, watermark=wm)
+        results.append(None if spec.emit_mode == abi.HSG_EMIT_NONE else _rows(spec, op.drain()))
+    return wm, results, op.dump_state().tuples()
+
+
+@pytest.mark.parametrize("late", [False, True], ids=["no_late", "late"])
+@pytest.mark.parametrize("spec_name", list(GPU_SPECS))
+def test_two_ranks_equal_single_stream(spec_name, late):
+    import multiprocessing as mp
+    G = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = f"hsgt-{os.getpid()}-{uuid.uuid4().hex[:12]}"
+    procs = [ctx.Process(target=_gpu_worker, args=(r, G, name, spec_name, late, q)) for r in range(G)]
+    for p in procs:
+        p.start()
+    try:
+        outs = [q.get(timeout=100) for _ in range(G)]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    errs = [o for o in outs if o[1] == "error"]
+    assert not errs, errs
+    for p in procs:
+        assert p.exitcode == 0
+    outs.sort(key=lambda o: o[0])
+    wm1, res1, st1 = _single(spec_name, G, late)
+    assert all(o[1] == wm1 for o in outs), ([o[1] for o in outs], wm1)
+    # union of the ranks' state = the single-stream state, keys disjoint
+    keys = [set(k for k, *_ in o[3]) for o in outs]
+    assert not (keys[0] & keys[1])
+    merged = sorted(outs[0][3] + outs[1][3])
+    assert len(merged) == len(st1)
+    for a, b in zip(merged, sorted(st1)):
+        assert a[:3] == b[:3] and _close(a[3], b[3]), (a, b)
+    # changelogs: per-record rows carry the global sequence; merged by (src, start)
+    for bi in range(len(res1)):
+        if res1[bi] is None:
+            continue
+        rows = sorted(outs[0][2][bi] + outs[1][2][bi], key=lambda t: (t[3], t[1], t[0], t[2], t[4]))
+        ref = sorted(res1[bi], key=lambda t: (t[3], t[1], t[0], t[2], t[4]))
+        assert len(rows) == len(ref), (bi, len(rows), len(ref))
+        for a, b in zip(rows, ref):
+            assert a[:4] == b[:4] and _close(a[4], b[4]), (bi, a, b)
