@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "hsg_exchange.h"
 #include "hsg_kernels.h"
@@ -241,6 +242,43 @@ int comm_allgather(Comm *c, const void *send, void *recv, size_t count, ncclData
   for (int q = 0; q < h->nranks; ++q)
     CHTRY(hipMemcpy((char *)recv + (size_t)q * bytes, slot(h, q) + kSlotHdr, bytes, hipMemcpyHostToDevice));
   return host_barrier(h, err);
+}
+
+// Every rank's status of a collective step (op creation): one all-gather of
+// an int64 per rank. Returns the first failing rank's code (HSG_OK when all
+// succeeded), or the transport's own error.
+int comm_agree(Comm *c, int rc_local, std::string &err) {
+  hipStream_t s = nullptr;
+  int64_t *buf = nullptr;
+  CHTRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  std::vector<int64_t> h((size_t)c->nranks + 1, 0);
+  h[0] = rc_local;
+  int rc = HSG_OK;
+  hipError_t e = hipMalloc((void **)&buf, ((size_t)c->nranks + 1) * sizeof(int64_t));
+  if (e == hipSuccess) e = hipMemcpyAsync(buf, h.data(), sizeof(int64_t), hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) {
+    err = std::string("comm_agree: ") + hipGetErrorString(e);
+    rc = HSG_E_DEVICE;
+  }
+  if (rc == HSG_OK) rc = comm_allgather(c, buf, buf + 1, 1, ncclInt64, sizeof(int64_t), s, err);
+  if (rc == HSG_OK) {
+    e = hipMemcpyAsync(h.data() + 1, buf + 1, (size_t)c->nranks * sizeof(int64_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+      err = std::string("comm_agree: ") + hipGetErrorString(e);
+      rc = HSG_E_DEVICE;
+    }
+  }
+  if (rc == HSG_OK)
+    for (int q = 0; q < c->nranks; ++q)
+      if (h[1 + q] != HSG_OK) {
+        if (rc_local == HSG_OK) err = "rank " + std::to_string(q) + " failed to create its shard of the operator";
+        rc = (int)h[1 + q];
+        break;
+      }
+  if (buf) hipFree(buf);
+  hipStreamDestroy(s);
+  return rc;
 }
 
 int comm_alltoallv(Comm *c, const void *send, const size_t *scount, const size_t *sdispl, void *recv,

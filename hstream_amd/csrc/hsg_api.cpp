@@ -353,6 +353,17 @@ extern "C" int hsg_op_create(hsg_engine *eng, const hsg_op_config *cfg, hsg_op *
     rc = op_device_init(op->dev, op->cfg, op->prog, eng->batch_cap, eng->nranks, op->comm != nullptr,
                         hsg_windows_per_record(op->cfg),
                         eng->err);
+    if (op->comm) {
+      // the ranks agree on the creation: a rank whose shard failed (e.g. out
+      // of memory) takes every rank's shard down with it, so no rank keeps an
+      // op whose first exchange would wait forever on the missing one
+      std::string aerr;
+      const int arc = comm_agree(op->comm, rc, aerr);
+      if (rc == HSG_OK && arc != HSG_OK) {
+        rc = arc;
+        eng->err = aerr;
+      }
+    }
     if (rc != HSG_OK) {
       op_device_free(op->dev);
       comm_destroy(op->comm);

@@ -19,6 +19,8 @@ int comm_unique_id(uint8_t *out);
 int comm_create(const uint8_t *id, int rank, int nranks, int device, int transport, uint64_t batch_cap, Comm **out,
                 std::string &err);
 int comm_split(Comm *parent, Comm **out, std::string &err);
+// every rank's status of a collective step: the first failing rank's code, else HSG_OK
+int comm_agree(Comm *c, int rc_local, std::string &err);
 void comm_destroy(Comm *c);
 
 // Session store in HBM (k_session.hip, hsg_session.h): a growable key table

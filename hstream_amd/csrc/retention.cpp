@@ -198,10 +198,14 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
   fresh.p = nullptr;
   fresh_map.p = nullptr;
   hipFree(d.tw.rows);
-  if (nt.dirty) {
+  if (nt.dirty || ncap != d.cap) {
+    // the old-size map goes: the new table's map, or none once claims stopped
+    // marking (they never mark again: whole-table clears from then on)
     hipFree(d.tw_dirty_mem);
     d.tw_dirty_mem = nt.dirty;
   }
+  // a clear's pending count of dirty blocks describes the old table
+  if (ncap != d.cap) d.tw_cnt_pending = false;
   d.tw = nt;  // its dirty map: cleared with it, then marked by the reinsert
   if (closed) {
     d.spilled_rows += closed;
