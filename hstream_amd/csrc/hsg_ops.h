@@ -24,18 +24,23 @@ int comm_agree(Comm *c, int rc_local, std::string &err);
 void comm_destroy(Comm *c);
 
 // Session store in HBM (k_session.hip, hsg_session.h): a growable key table
-// of 32-byte entries (key, the key's session list, the per-batch emit mark)
-// and the sessions, sorted by start per key, as array-of-struct rows
-// [start][end][stamp][aggs...] in an arena: a key's hot tail is one or two lines.
+// of 64-byte entries (key, the key's session list, the per-batch emit mark, a
+// mirror of the list's last session) and the sessions, sorted by start per
+// key, as array-of-struct rows [start][end][stamp][aggs...] in an arena. The
+// home slot of a key is the top bits of its key hash below the owner bits, so
+// the keys of one partition bucket live in one contiguous stretch of entries.
 struct SessKey {
   uint32_t key;    // kSessEmptyKey = free
   uint32_t len;    // sessions
   uint64_t off;    // arena row of the first session
   uint32_t cap;    // rows reserved at off
-  uint32_t pad;
+  uint32_t mvalid; // merge path, <= 2 state slots: ms / me / ma mirror session len - 1
   uint64_t emark;  // merge path: ~batch << 32 | lowest index the batch rewrote (~0 = none)
+  int64_t ms, me;  // mirror of the last session: start, end
+  int64_t ma[2];   // and its state slots
 };
-static_assert(sizeof(SessKey) == 32, "SessKey");
+static_assert(sizeof(SessKey) == 64, "SessKey");
+constexpr int kSessMirrorSlots = 2;
 struct SessTable {
   SessKey *kt;         // [kmask + 1]
   uint64_t kmask;
@@ -44,6 +49,8 @@ struct SessTable {
   uint32_t ns;         // n_slots
   uint64_t arena_cap;  // rows
   uint64_t *meta;      // [M_WORDS] device bookkeeping (hsg_session.h SessMeta)
+  int32_t kbits;       // log2(kmask + 1)
+  int32_t hshift;      // key-hash owner bits skipped by the home slot (multi-GPU)
 };
 
 struct OpDevice {

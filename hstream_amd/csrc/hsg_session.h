@@ -1,7 +1,8 @@
 // Session windows (k_session.hip, session.cpp). Not part of the ABI.
 //
-// State (SessTable, hsg_ops.h): a growable open-addressing key table (32-byte
-// entries: key, the key's list, an emit mark) and, per key, its sessions as a
+// State (SessTable, hsg_ops.h): a growable open-addressing key table (64-byte
+// entries: key, the key's list, an emit mark, a mirror of its last session)
+// and, per key, its sessions as a
 // list of array-of-struct rows sorted by start in an HBM arena. Sessions of one
 // key stay more than `gap` apart (the closure of SessionWindowedStream.hs:84-118
 // over the findSessions test of Store.hs:243-272), so a point or a batch run

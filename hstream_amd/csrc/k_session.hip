@@ -32,10 +32,23 @@ __device__ inline uint32_t ss_grow_cap(uint64_t need) {
   return c;
 }
 
+__device__ inline SessKey ss_blank(uint32_t key) {
+  SessKey e;
+  e.key = key;
+  e.len = 0;
+  e.off = 0;
+  e.cap = 0;
+  e.mvalid = 0;
+  e.emark = ~0ull;
+  e.ms = e.me = 0;
+  e.ma[0] = e.ma[1] = 0;
+  return e;
+}
+
 __global__ void k_ss_reset(SessTable t) {
   const uint64_t cap = t.kmask + 1;
   for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap; s += (uint64_t)gridDim.x * blockDim.x)
-    t.kt[s] = SessKey{kSessEmptyKey, 0, 0, 0, 0, ~0ull};
+    t.kt[s] = ss_blank(kSessEmptyKey);
 }
 
 void launch_ss_reset(hipStream_t s, const SessTable &t) {
@@ -44,8 +57,16 @@ void launch_ss_reset(hipStream_t s, const SessTable &t) {
 
 // find key's slot, inserting it if absent; -1 = table full. `inserted` is set
 // when this call claimed the slot (its entry then still holds an empty list).
+// Home slot: the top key-hash bits below the owner bits, the same bits that
+// pick the key's partition bucket (and sub-bucket), so the keys of a bucket
+// occupy one stretch of the table and the merge path, which walks a bucket's
+// keys in hash order, touches neighbouring entries from neighbouring lanes.
+__device__ inline uint64_t ss_home(const SessTable &t, uint32_t key) {
+  return t.kbits ? (uint64_t)((key_hash(key) << t.hshift) >> (64 - t.kbits)) : 0ull;
+}
+
 __device__ inline int64_t ss_find_or_insert(const SessTable &t, uint32_t key, bool &inserted) {
-  uint64_t s = mix64(key) & t.kmask;
+  uint64_t s = ss_home(t, key);
   inserted = false;
   for (uint64_t probe = 0; probe <= t.kmask; ++probe) {
     const uint32_t cur = t.kt[s].key;
@@ -70,7 +91,11 @@ __global__ void k_ss_rehash(SessTable from, SessTable to) {
     if (e.key == kSessEmptyKey) continue;
     bool ins;
     const int64_t d = ss_find_or_insert(to, e.key, ins);  // `to` is at most half full: d >= 0
-    if (d >= 0) to.kt[d] = SessKey{e.key, e.len, e.off, e.cap, 0, ~0ull};
+    if (d >= 0) {
+      SessKey x = e;
+      x.emark = ~0ull;
+      to.kt[d] = x;
+    }
   }
 }
 
@@ -247,7 +272,7 @@ __global__ __launch_bounds__(256) void k_ss_process(Batch b, SessParams p, SessT
   const bool active = r < R;
   uint64_t q0 = 0, q1 = 0;
   uint32_t sl = 0;
-  SessKey e = {0, 0, 0, 0, 0, 0};
+  SessKey e = ss_blank(0);
   int64_t live_delta = 0;
   if (active) {
     q0 = runs[r];
@@ -334,6 +359,7 @@ __global__ __launch_bounds__(256) void k_ss_process(Batch b, SessParams p, SessT
     t.kt[sl].off = off;
     t.kt[sl].len = (uint32_t)len;
     t.kt[sl].cap = lcap;
+    t.kt[sl].mvalid = 0;  // the replay path keeps no mirror of the last session
   }
   // per-batch changelog: the key's sessions stamped by this batch
   uint64_t mine = 0;
@@ -663,7 +689,7 @@ template <int MS, bool APPLY, class RS>
 __device__ inline uint32_t mg_sweep(const Program &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t r0,
                                     uint32_t r1, uint64_t off, uint64_t i0, uint64_t len, bool tail_regs,
                                     const MgSess<MS> (&tail)[kMgTail], uint64_t dst, uint32_t batch_id,
-                                    EmitSink *sink = nullptr) {
+                                    EmitSink *sink = nullptr, MgSess<MS> *lastp = nullptr) {
   const int ns = prog.n_slots;
   uint64_t j = i0;   // next resident
   uint32_t r = r0;   // next run
@@ -720,6 +746,7 @@ __device__ inline uint32_t mg_sweep(const Program &prog, const SessTable &t, int
     if (APPLY) ss_store<MS>(t, dst + i0 + k, cur.s, cur.e, cur.fresh ? batch_id : cur.stamp, cur.a);
     if (sink && cur.fresh) mg_emit<MS>(prog, *sink, cur);
     ++k;
+    if (lastp) *lastp = cur;  // the list's new last session (the sweep runs to its end)
   }
   return k;
 }
@@ -762,11 +789,79 @@ __device__ inline void mg_plan(const Program &prog, const SessTable &t, int64_t 
   newcap = (i0 + M > e.cap || e.len - i0 > kMgTail) ? ss_grow_cap(i0 + M + 1) : 0u;
 }
 
+// The key's last session from its entry's mirror (valid when e.mvalid).
+template <int MS>
+__device__ inline void mg_mirror_tail(const Program &prog, const SessKey &e, uint32_t batch_id,
+                                      MgSess<MS> (&tail)[kMgTail]) {
+#pragma unroll
+  for (int k = 0; k < kMgTail; ++k) {
+    tail[k].s = tail[k].e = 0;
+    tail[k].stamp = batch_id;  // a fast-path resident always merges with a run: rewritten as fresh
+    tail[k].fresh = false;
+#pragma unroll
+    for (int s = 0; s < MS; ++s) tail[k].a[s] = 0;
+  }
+  tail[0].s = e.ms;
+  tail[0].e = e.me;
+#pragma unroll
+  for (int s = 0; s < MS; ++s) tail[0].a[s] = (s < kSessMirrorSlots && s < prog.n_slots) ? e.ma[s] : 0;
+}
+
+// Fast plan from the mirror, no list read: the batch's first run starts at or
+// after the last session's start, so no resident but the last can be reached
+// (the one before ends more than gap before the last starts); the last is
+// touched iff the first run comes within gap of its end.
+template <int MS, class RS>
+__device__ inline bool mg_plan_fast(const Program &prog, int64_t gap, const RS &rs, uint32_t ra, uint32_t rb,
+                                    const SessKey &e, uint32_t batch_id, uint64_t &i0, uint32_t &M, uint32_t &newcap,
+                                    uint32_t *fresh) {
+  if (!e.mvalid || e.len == 0 || rs.start(ra) < e.ms) return false;
+  const int64_t lo = (int64_t)((uint64_t)rs.start(ra) - (uint64_t)gap);
+  i0 = e.me >= lo ? e.len - 1 : e.len;
+  MgSess<MS> tail[kMgTail];
+  mg_mirror_tail<MS>(prog, e, batch_id, tail);
+  EmitSink cnt{OutCols{}, ~0ull, 0, 0};
+  SessTable none = {};
+  M = mg_sweep<MS, false>(prog, none, gap, rs, ra, rb, 0, i0, e.len, true, tail, 0, 0, &cnt);
+  if (fresh) *fresh = cnt.n;
+  newcap = (i0 + M > e.cap) ? ss_grow_cap(i0 + M + 1) : 0u;
+  return true;
+}
+
+// Apply a fast-planned key: residents [i0, len) come from the mirror.
+template <int MS, class RS>
+__device__ inline void mg_apply_fast(const Program &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t ra,
+                                     uint32_t rb, const SessKey &e, uint64_t i0, uint64_t dst, bool reloc,
+                                     uint32_t batch_id, EmitSink *sink, MgSess<MS> *lastp) {
+  if (reloc)
+    for (uint64_t k = 0; k < i0; ++k) ss_copy(t, dst + k, t, e.off + k);
+  MgSess<MS> tail[kMgTail];
+  mg_mirror_tail<MS>(prog, e, batch_id, tail);
+  mg_sweep<MS, true>(prog, t, gap, rs, ra, rb, e.off, i0, e.len, true, tail, dst, batch_id, sink, lastp);
+}
+
+// The entry after a merge: list position, capacity and the last-session mirror.
+template <int MS>
+__device__ inline void ss_entry_commit(const Program &prog, SessKey &ke, uint64_t off, uint32_t len, uint32_t newcap,
+                                       const MgSess<MS> &last) {
+  ke.off = off;
+  ke.len = len;
+  if (newcap) ke.cap = newcap;
+  const bool mirror = prog.n_slots <= kSessMirrorSlots && len > 0;
+  if (mirror) {
+    ke.ms = last.s;
+    ke.me = last.e;
+#pragma unroll
+    for (int s = 0; s < kSessMirrorSlots; ++s) ke.ma[s] = s < MS ? last.a[s] : 0;
+  }
+  ke.mvalid = mirror ? 1u : 0u;
+}
+
 // Apply a planned key: the list at dst (fresh rows: the prefix copied first).
 template <int MS, class RS>
 __device__ inline void mg_apply(const Program &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t ra,
                                 uint32_t rb, const SessKey &e, uint64_t i0, uint64_t dst, bool reloc,
-                                uint32_t batch_id, EmitSink *sink = nullptr) {
+                                uint32_t batch_id, EmitSink *sink = nullptr, MgSess<MS> *lastp = nullptr) {
   const int ns = prog.n_slots;
   if (reloc)
     for (uint64_t k = 0; k < i0; ++k) ss_copy(t, dst + k, t, e.off + k);
@@ -788,7 +883,7 @@ __device__ inline void mg_apply(const Program &prog, const SessTable &t, int64_t
       for (int s = 0; s < MS; ++s) tail[k].a[s] = s < ns ? (int64_t)row[3 + s] : 0;
     }
   }
-  mg_sweep<MS, true>(prog, t, gap, rs, ra, rb, e.off, i0, e.len, !reloc, tail, dst, batch_id, sink);
+  mg_sweep<MS, true>(prog, t, gap, rs, ra, rb, e.off, i0, e.len, !reloc, tail, dst, batch_id, sink, lastp);
 }
 
 // ---------------------------------------------------------------------------
@@ -802,7 +897,8 @@ __device__ inline void mg_apply(const Program &prog, const SessTable &t, int64_t
 // ---------------------------------------------------------------------------
 constexpr int kSoNT = 512;
 constexpr int kSoCH = 1024;        // records per sub-bucket
-constexpr int kSoTab = 2048;       // LDS hash table entries
+constexpr int kSoTabLog2 = 11;
+constexpr int kSoTab = 1 << kSoTabLog2;  // LDS hash table entries
 constexpr int kSoMaxSubLog2 = 6;   // up to 64 sub-buckets (buckets of < 2^16 records)
 constexpr int kSoSmall = 32;       // a key's records sorted by its own thread
 
@@ -991,7 +1087,10 @@ __global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Pr
       hslot[u] = ~0u;
       if (u * kSoNT + threadIdx.x >= m2) continue;
       const uint32_t key = (uint32_t)rw[u][0];
-      uint32_t h = (uint32_t)mix64(key) & (kSoTab - 1);
+      // the key-hash bits below the bucket and sub-bucket bits: the groups
+      // come out in key-table home order (ss_home), so k_ss_apply's
+      // neighbouring lanes touch neighbouring key entries
+      uint32_t h = (uint32_t)((key_hash(key) << (hs + sl)) >> (64 - kSoTabLog2));
       for (;;) {
         const uint32_t cur = L.tkey[h];
         if (cur == key) break;
@@ -1187,8 +1286,8 @@ __global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, P
   uint32_t key = 0, ra = 0, nr = 0, newcap = 0, M = 0, fresh = 0;
   uint64_t i0 = 0;
   int64_t sl = -1;
-  bool ins = false;
-  SessKey e = {0, 0, 0, 0, 0, 0};
+  bool ins = false, fast = false;
+  SessKey e = ss_blank(0);
   uint32_t err = 0;
   if (act) {
     const uint4 gr = *reinterpret_cast<const uint4 *>(sp.groups + g * 4);
@@ -1199,7 +1298,9 @@ __global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, P
     if (sl < 0) err |= ERR_OOM;
     else {
       if (!ins) e = t.kt[sl];
-      mg_plan<MS>(prog, t, p.gap, rs, ra, ra + nr, e, i0, M, newcap, &fresh);
+      // near-sorted arrivals: planned from the entry's mirror, no list read
+      fast = mg_plan_fast<MS>(prog, p.gap, rs, ra, ra + nr, e, p.batch_id, i0, M, newcap, &fresh);
+      if (!fast) mg_plan<MS>(prog, t, p.gap, rs, ra, ra + nr, e, i0, M, newcap, &fresh);
     }
   }
   const bool live = act && sl >= 0;
@@ -1246,11 +1347,10 @@ __global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, P
     const bool reloc = newcap != 0;
     const uint64_t dst = reloc ? sbase + before + incl - need : e.off;
     EmitSink sink{out, p.emit_mode == HSG_EMIT_PER_BATCH ? out_base + sobase + ebefore + einc - nem : ~0ull, key, 0};
-    mg_apply<MS>(prog, t, p.gap, rs, ra, ra + nr, e, i0, dst, reloc, p.batch_id, &sink);
-    SessKey &ke = t.kt[sl];
-    ke.off = dst;
-    ke.len = (uint32_t)(i0 + M);
-    if (reloc) ke.cap = newcap;
+    MgSess<MS> last;
+    if (fast) mg_apply_fast<MS>(prog, t, p.gap, rs, ra, ra + nr, e, i0, dst, reloc, p.batch_id, &sink, &last);
+    else mg_apply<MS>(prog, t, p.gap, rs, ra, ra + nr, e, i0, dst, reloc, p.batch_id, &sink, &last);
+    ss_entry_commit<MS>(prog, t.kt[sl], dst, (uint32_t)(i0 + M), reloc ? newcap : 0u, last);
     ld = (int64_t)M - (int64_t)(e.len - i0);
   }
   const uint64_t lsum = wave_sum_u64((uint64_t)ld);
@@ -1487,7 +1587,7 @@ __global__ __launch_bounds__(kMgNT) void k_ss_merge_big(SessParams p, SessTable 
       gcap[u] = 0;
       gM[u] = 0;
       gi0[u] = 0;
-      ge[u] = SessKey{0, 0, 0, 0, 0, 0};
+      ge[u] = ss_blank(0);
       if (g >= ngrp) continue;
       const uint32_t ra = L.gfirst[g], rb = L.gfirst[g + 1];
       bool ins;
@@ -1540,11 +1640,10 @@ __global__ __launch_bounds__(kMgNT) void k_ss_merge_big(SessParams p, SessTable 
         dst = my_alloc;
         my_alloc += gcap[u];
       }
-      mg_apply<MS>(prog, t, p.gap, rsrc, ra, rb, ge[u], gi0[u], dst, reloc, p.batch_id);
+      MgSess<MS> last;
+      mg_apply<MS>(prog, t, p.gap, rsrc, ra, rb, ge[u], gi0[u], dst, reloc, p.batch_id, nullptr, &last);
       SessKey &ke = t.kt[gslot[u]];
-      ke.off = dst;
-      ke.len = (uint32_t)(gi0[u] + gM[u]);
-      if (reloc) ke.cap = gcap[u];
+      ss_entry_commit<MS>(prog, ke, dst, (uint32_t)(gi0[u] + gM[u]), reloc ? gcap[u] : 0u, last);
       atomicMin((unsigned long long *)&ke.emark, (unsigned long long)(bmark | gi0[u]));
       sp.touched[tp++] = (uint32_t)gslot[u];
       live_delta += (int64_t)gM[u] - (int64_t)(ge[u].len - gi0[u]);

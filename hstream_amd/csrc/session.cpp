@@ -46,6 +46,7 @@ static bool has_last(const Program &prog) {
 static int alloc_keys(SessTable &t, uint64_t kcap, std::string &err) {
   DTRY(hipMalloc((void **)&t.kt, kcap * sizeof(SessKey)));
   t.kmask = kcap - 1;
+  t.kbits = log2u(kcap);
   return HSG_OK;
 }
 
@@ -187,6 +188,7 @@ static int ensure_keys(OpDevice &d, uint64_t incoming, std::string &err) {
   free_keys(d.ss);
   d.ss.kt = to.kt;
   d.ss.kmask = to.kmask;
+  d.ss.kbits = to.kbits;
   d.cap = ncap;
   d.grow_events += 1;
   return HSG_OK;
@@ -365,6 +367,7 @@ static int push_session_replay(OpDevice &d, const hsg_op_config &cfg, const Prog
 
 int push_session(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, const Batch &kb,
                  const int64_t *seq, PushResult &r, std::string &err) {
+  d.ss.hshift = d.bshift;  // fixed once the exchange is set up (before the first batch)
   int rc = clear_batch_scalars(d, err);
   if (rc != HSG_OK) return rc;
   if (!kb.n) return finish_batch(d, a.wm_in, 0, r, err);
