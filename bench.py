@@ -452,7 +452,11 @@ def pipeline_name(cfg, emit):
             return "session replay (k_ss_slot, radix sort, k_ss_process)"
         return "session merge (k_ss_phist, offsets, k_ss_pscatter, k_ss_sort, k_ss_apply)"
     if emit == "per_record":
-        return "per-record changelog (k_pr_count, k_pr_expand, radix sort, k_seg_*)"
+        if cfg.window_kind in (abi.HSG_TUMBLING, abi.HSG_UNWINDOWED):
+            return ("per-record changelog (k_part_hist_opt, offsets + decide, stable k_part_scatter_st, "
+                    "k_pr_bucket, k_pr_emit1)")
+        return ("per-record changelog (k_part_hist_opt, offsets + decide, stable k_part_scatter_st, "
+                "k_pr_local, k_pr_carry, k_pr_emit)")
     if cfg.window_kind in (abi.HSG_TUMBLING, abi.HSG_UNWINDOWED):
         return ("batch pipeline (k_part_hist_opt, offsets + decide, k_part_scatter_st, k_agg_lean, "
                 "k_pane_apply writing the changelog rows)")

@@ -42,6 +42,8 @@ struct PrPart {
   uint32_t *ccnt;     // [chunks] partials of each chunk
   uint64_t *counter;  // partials allocated in this batch
   uint64_t *partial;  // scan partials
+  int64_t *fin;       // one-window ops (k_pr_bucket): [n][ns] each record's changelog state at its
+                      // partitioned position
 };
 
 void launch_pr_count(hipStream_t s, const Batch &b, const TwParams &p, const TwTable &t, const int64_t *tprefix,

@@ -587,70 +587,126 @@ __global__ __launch_bounds__(1024) void k_seg_apply(Program prog, TwParams p, Pa
   const int64_t k_epoch = sc->k_epoch;
   uint32_t fresh = 0, err = 0;
   uint64_t run = before;
+  // SU entries per thread per pass: their partial loads, then their home-key
+  // loads, then their row loads are issued together, so one wait (which on
+  // CDNA also waits for the pass's earlier stores) covers SU entries
+  constexpr int SU = MS <= 2 ? 2 : 1;
   for (uint32_t sg = 0; sg < nseg; ++sg) {
     const uint64_t base = pb.seg[((uint64_t)blockIdx.x * kMaxSeg + sg) * 2];
     const uint64_t cnt = pb.seg[((uint64_t)blockIdx.x * kMaxSeg + sg) * 2 + 1];
-    for (uint64_t q = threadIdx.x; q < cnt; q += NT) {
-      const uint64_t *ent = pb.pane + (base + q) * pw;
-      const uint64_t g = ent[0];
-      int64_t v[MS];
+    for (uint64_t q0 = threadIdx.x; q0 < cnt; q0 += (uint64_t)NT * SU) {
+      uint64_t g[SU];
+      int64_t v[SU][MS];
 #pragma unroll
-      for (int s = 0; s < MS; ++s) v[s] = s < ns ? (int64_t)ent[1 + s] : 0;
-      const uint32_t f0 = fresh;
-      const int64_t slot = lds_claim     ? tw_claim_seg(t, g, cset, fresh)
-                           : plain_claim ? tw_claim_exclusive(t, g, fresh)
-                                         : tw_find_or_insert(t, g, fresh);
-      uint32_t tl = kTouchSkip;
-      if (slot < 0) {
-        err |= ERR_OOM;
-      } else {
-        int64_t *row = t.aggs(slot);
-        uint32_t *stp = t.stamp(slot);
-        bool first = true;
-        if (fresh == f0) {
-          int64_t c[MS];
+      for (int u = 0; u < SU; ++u) {
+        const uint64_t q = q0 + (uint64_t)u * NT;
+        const uint64_t *ent = pb.pane + (base + (q < cnt ? q : 0)) * pw;
+        g[u] = q < cnt ? ent[0] : kEmpty;
 #pragma unroll
-          for (int s = 0; s < MS; ++s)
-            c[s] = s < ns ? __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-          const uint32_t st = __hip_atomic_load(stp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int s = 0; s < MS; ++s) v[u][s] = (q < cnt && s < ns) ? (int64_t)ent[1 + s] : 0;
+      }
+      // home probes of all SU groups, then their claims (a collision takes the full probe)
+      uint64_t hs[SU], kh[SU];
 #pragma unroll
-          for (int s = 0; s < MS; ++s) {
-            if (s >= ns) break;
-            const int op = pg.op(s);
-            if (op == S_LAST_VAL) continue;
-            v[s] = op == S_LAST_SEQ ? ((uint64_t)v[s] > (uint64_t)c[s] ? v[s] : c[s]) : slot_combine(op, c[s], v[s]);
-          }
-          first = st != bid;
+      for (int u = 0; u < SU; ++u) {
+        hs[u] = 0;
+        kh[u] = kEmpty;
+        if (g[u] != kEmpty && lds_claim) {
+          hs[u] = tw_region_base(t, g[u]) + tw_home_in(t, g[u]);
+          kh[u] = __hip_atomic_load(t.key(hs[u]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+      }
+      int64_t slot[SU];
+      bool isnew[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        slot[u] = -1;
+        isnew[u] = false;
+        if (g[u] == kEmpty) continue;
+        const uint32_t f0 = fresh;
+        if (lds_claim && kh[u] == g[u]) {
+          slot[u] = (int64_t)hs[u];
+        } else if (lds_claim && kh[u] == kEmpty && seg_claim_insert(cset, (uint32_t)hs[u])) {
+          *t.key(hs[u]) = g[u];
+          t.mark(hs[u]);
+          fresh += 1;
+          slot[u] = (int64_t)hs[u];
+        } else {
+          slot[u] = lds_claim     ? tw_claim_seg(t, g[u], cset, fresh)
+                    : plain_claim ? tw_claim_exclusive(t, g[u], fresh)
+                                  : tw_find_or_insert(t, g[u], fresh);
+        }
+        isnew[u] = fresh != f0;
+      }
+      // the rows of the groups found (agent-scope: an earlier segment may have written them)
+      int64_t c[SU][MS];
+      uint32_t st[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        st[u] = 0;
+#pragma unroll
+        for (int s = 0; s < MS; ++s) c[u][s] = 0;
+        if (slot[u] < 0 || isnew[u]) continue;
+        const int64_t *row = t.aggs(slot[u]);
 #pragma unroll
         for (int s = 0; s < MS; ++s)
-          if (s < ns && pg.op(s) != S_LAST_VAL) row[s] = v[s];
-        if (first) *stp = bid;
-        if (direct) {
-          const uint64_t o = out_base + run + q;
-          if (o < out_cap) {
-            out.key[o] = (uint32_t)(g >> 32);
-            int64_t ws = 0, we = 0;
-            if (p.kind != HSG_UNWINDOWED) {
-              const int64_t k = k_epoch + (int64_t)(g & 0xFFFFFFFFull);
-              ws = (int64_t)((uint64_t)k * (uint64_t)p.adv);
-              we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
-            }
-            out.ws[o] = ws;
-            out.we[o] = we;
-            out.src[o] = -1;
-            for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value_reg<MS>(prog, j, v);
-          } else {
-            err |= ERR_OOM;
-          }
-          continue;
-        }
-        if (first) tl = (uint32_t)slot;
+          c[u][s] = s < ns ? __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        st[u] = __hip_atomic_load(t.stamp(slot[u]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (!direct) {
-        const uint64_t o = t0 + run + q;
-        if (o < pb.touched_cap) pb.touched[o] = tl;
-        else err |= ERR_OOM;
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const uint64_t q = q0 + (uint64_t)u * NT;
+        if (q >= cnt) continue;
+        uint32_t tl = kTouchSkip;
+        if (slot[u] < 0) {
+          err |= ERR_OOM;
+        } else {
+          int64_t *row = t.aggs(slot[u]);
+          uint32_t *stp = t.stamp(slot[u]);
+          bool first = true;
+          if (!isnew[u]) {
+#pragma unroll
+            for (int s = 0; s < MS; ++s) {
+              if (s >= ns) break;
+              const int op = pg.op(s);
+              if (op == S_LAST_VAL) continue;
+              v[u][s] = op == S_LAST_SEQ ? ((uint64_t)v[u][s] > (uint64_t)c[u][s] ? v[u][s] : c[u][s])
+                                         : slot_combine(op, c[u][s], v[u][s]);
+            }
+            first = st[u] != bid;
+          }
+#pragma unroll
+          for (int s = 0; s < MS; ++s)
+            if (s < ns && pg.op(s) != S_LAST_VAL) row[s] = v[u][s];
+          if (first) *stp = bid;
+          if (direct) {
+            const uint64_t o = out_base + run + q;
+            if (o < out_cap) {
+              out.key[o] = (uint32_t)(g[u] >> 32);
+              int64_t ws = 0, we = 0;
+              if (p.kind != HSG_UNWINDOWED) {
+                const int64_t k = k_epoch + (int64_t)(g[u] & 0xFFFFFFFFull);
+                ws = (int64_t)((uint64_t)k * (uint64_t)p.adv);
+                we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
+              }
+              out.ws[o] = ws;
+              out.we[o] = we;
+              out.src[o] = -1;
+#pragma unroll
+              for (int j = 0; j < kMaxAggs; ++j)
+                if (j < prog.n_out) out.agg[j][o] = out_value_reg<MS>(prog, j, v[u]);
+            } else {
+              err |= ERR_OOM;
+            }
+            continue;
+          }
+          if (first) tl = (uint32_t)slot[u];
+        }
+        if (!direct) {
+          const uint64_t o = t0 + run + q;
+          if (o < pb.touched_cap) pb.touched[o] = tl;
+          else err |= ERR_OOM;
+        }
       }
     }
     run += cnt;

@@ -67,8 +67,8 @@ struct PrRecView {
 };
 
 // contribution of the record to every slot (identity when the field is absent)
-template <int MS>
-__device__ inline void pr_elems(const Program &prog, const PrRecView &r, int64_t (&e)[MS]) {
+template <int MS, class RV>
+__device__ inline void pr_elems(const Program &prog, const RV &r, int64_t (&e)[MS]) {
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
     e[s] = 0;
@@ -464,7 +464,11 @@ __global__ __launch_bounds__(256) void k_pr_carry(Program prog, TwParams p, Part
       for (int s = 0; s < MS; ++s)
         if (s < ns) pr.part[(uint64_t)gi * ns + s] = cur[s];
     }
-    __threadfence();  // this chunk's rows at the device before the next chunk reads them
+    // this chunk's rows in L2 before the next chunk reads them: the same
+    // workgroup (one CU, one L2) reads them back with L1-bypassing loads, so
+    // draining the stores is enough (no device-scope fence: a whole-L2 write-
+    // back per chunk)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   if (err) atomicOr(&sc->err, err);
@@ -482,12 +486,14 @@ __global__ __launch_bounds__(256) void k_pr_carry(Program prog, TwParams p, Part
   }
 }
 
-// One workgroup per kPrEmitRecs arrival-order records (kPrEmitThreads threads,
-// consecutive records per thread): window runs as the partition computed
-// them, output positions, rows.
+// One workgroup per kPrEmitRecs arrival-order records, in rounds of
+// kPrEmitThreads consecutive records (record = round base + thread: the lanes
+// read the batch and write the changelog columns coalesced): window runs as
+// the partition computed them, output positions (exclusive prefix of the
+// accepted pairs in arrival order), rows.
 constexpr int kPrEmitThreads = 1024;
-constexpr int kPrEmitPer = kPrEmitRecs / kPrEmitThreads;
-static_assert(kPrEmitRecs % kPartTileRecs == 0 && kPrEmitPer * kPrEmitThreads == kPrEmitRecs, "emit tile");
+constexpr int kPrEmitRounds = kPrEmitRecs / kPrEmitThreads;
+static_assert(kPrEmitRecs % kPartTileRecs == 0 && kPrEmitRounds * kPrEmitThreads == kPrEmitRecs, "emit tile");
 
 template <int MS>
 __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit(Batch bt, Program prog, TwParams p, PartParams pp,
@@ -497,65 +503,60 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit(Batch bt, Program pr
                                                             uint64_t out_base, uint64_t out_cap, DevScalars *sc) {
   __shared__ uint32_t sw[kPrEmitThreads / 64];
   if (sc->redo) return;  // uniform
-  const uint64_t i0 = (uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)threadIdx.x * kPrEmitPer;
   const int64_t k_epoch = sc->k_epoch;
   const int64_t *wm = rec_wm ? rec_wm : (sc->no_late ? nullptr : pb.wm);
-  uint32_t krel[kPrEmitPer], nwin[kPrEmitPer], key[kPrEmitPer];
-  uint64_t late = 0;
-  uint32_t err = 0, mine = 0;
-#pragma unroll
-  for (int r = 0; r < kPrEmitPer; ++r) {
-    const uint64_t i = i0 + r;
-    nwin[r] = 0;
-    key[r] = HSG_KEY_NONE;
-    if (i >= bt.n) continue;
-    key[r] = bt.key[i];
-    const int64_t ts = bt.ts[i];
-    uint32_t a = 0, n = 0;
-    // same window run as the partition passes (k_part.hip part_record)
-    if (key[r] != HSG_KEY_NONE) {
-      uint64_t k_lo, k_hi;
-      if (record_windows(p, ts, k_lo, k_hi)) {
-        const int64_t w = wm ? wm[i] : INT64_MIN;
-        uint64_t k = k_lo;
-        while (k <= k_hi && !window_accepted(p, k, w)) ++k;
-        if (k <= k_hi) {
-          int64_t lo = (int64_t)k - k_epoch, hi = (int64_t)k_hi - k_epoch;
-          if (lo < 0) lo = 0;
-          if (hi > 0xFFFFFFFFll) hi = 0xFFFFFFFFll;
-          if (lo <= hi) {
-            a = (uint32_t)lo;
-            n = (uint32_t)(hi - lo + 1);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t rw = 1 + (uint64_t)prog.n_slots;
+  const int ns = prog.n_slots;
+  uint32_t err = 0;
+  // the workgroup's first changelog row: the tiles before it (histogram pair
+  // counts, scanned); the rounds then advance it by their pair totals
+  uint64_t base = pr.tpoff[(uint64_t)blockIdx.x * (kPrEmitRecs / kPartTileRecs)];
+  for (int rd = 0; rd < kPrEmitRounds; ++rd) {
+    const uint64_t i = (uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)rd * kPrEmitThreads + threadIdx.x;
+    if ((uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)rd * kPrEmitThreads >= bt.n) break;  // uniform
+    uint32_t a = 0, n = 0, key = HSG_KEY_NONE;
+    if (i < bt.n) {
+      key = bt.key[i];
+      const int64_t ts = bt.ts[i];
+      // same window run as the partition passes (k_part.hip part_record)
+      if (key != HSG_KEY_NONE) {
+        uint64_t k_lo, k_hi;
+        if (record_windows(p, ts, k_lo, k_hi)) {
+          const int64_t w = wm ? wm[i] : INT64_MIN;
+          uint64_t k = k_lo;
+          while (k <= k_hi && !window_accepted(p, k, w)) ++k;
+          if (k <= k_hi) {
+            int64_t lo = (int64_t)k - k_epoch, hi = (int64_t)k_hi - k_epoch;
+            if (lo < 0) lo = 0;
+            if (hi > 0xFFFFFFFFll) hi = 0xFFFFFFFFll;
+            if (lo <= hi) {
+              a = (uint32_t)lo;
+              n = (uint32_t)(hi - lo + 1);
+            }
           }
         }
       }
     }
-    krel[r] = a;
-    nwin[r] = n;
-    mine += n;
-  }
-  // exclusive prefix of the pairs in arrival order: the tiles before this one
-  // (histogram pair counts, scanned) + the threads before this one
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t incl = (uint32_t)wave_incl_sum((uint64_t)mine);
-  if (lane == 63) sw[wv] = incl;
-  __syncthreads();
-  uint64_t o = pr.tpoff[(uint64_t)blockIdx.x * (kPrEmitRecs / kPartTileRecs)] + incl - mine;
-  for (int k = 0; k < wv; ++k) o += sw[k];
-  const uint64_t rw = 1 + (uint64_t)prog.n_slots;
-  const int ns = prog.n_slots;
-#pragma unroll
-  for (int r = 0; r < kPrEmitPer; ++r) {
-    if (!nwin[r]) continue;
-    const uint64_t i = i0 + r;
+    // exclusive prefix of the round's pairs in arrival order
+    const uint32_t incl = (uint32_t)wave_incl_sum((uint64_t)n);
+    if (lane == 63) sw[wv] = incl;
+    lds_barrier();
+    uint64_t o = base + incl - n, tot = 0;
+    for (int k = 0; k < kPrEmitThreads / 64; ++k) {
+      o += k < wv ? sw[k] : 0u;
+      tot += sw[k];
+    }
+    lds_barrier();  // sw is rewritten by the next round
+    base += tot;
+    if (!n) continue;
     const uint64_t pos = pr.pos[i];
     const int64_t src = seq ? seq[i] : (int64_t)(p.rec_base + i);
     if (pos >= pb.n_cap) {  // cannot happen: the scatter placed every record with a window
       err |= ERR_OOM;
-      o += nwin[r];
       continue;
     }
-    for (uint32_t j = 0; j < nwin[r]; ++j, ++o) {
+    for (uint32_t j = 0; j < n; ++j, ++o) {
       const uint64_t *it = pr.inter + (pos * wpr + j) * rw;
       const uint32_t gi = (uint32_t)it[0];
       if ((uint64_t)gi >= pb.n_cap * wpr) {
@@ -574,18 +575,502 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit(Batch bt, Program pr
         err |= ERR_OOM;
         continue;
       }
-      out.key[ob] = key[r];
+      out.key[ob] = key;
       int64_t ws = 0, we = 0;
       if (p.kind != HSG_UNWINDOWED) {
-        const int64_t k = k_epoch + (int64_t)(krel[r] + j);
+        const int64_t k = k_epoch + (int64_t)(a + j);
         ws = (int64_t)((uint64_t)k * (uint64_t)p.adv);
         we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
       }
       out.ws[ob] = ws;
       out.we[ob] = we;
       out.src[ob] = src;
-      for (int jj = 0; jj < prog.n_out; ++jj) out.agg[jj][ob] = out_value_reg<MS>(prog, jj, R);
+#pragma unroll
+      for (int jj = 0; jj < kMaxAggs; ++jj)  // static indices: the column pointers stay in registers
+        if (jj < prog.n_out) out.agg[jj][ob] = out_value_reg<MS>(prog, jj, R);
     }
+  }
+  if (err) atomicOr(&sc->err, err);
+}
+
+// ---------------------------------------------------------------------------
+// One-window ops (tumbling, unwindowed: one pair per partitioned record):
+// k_pr_bucket, one workgroup per bucket, walks the bucket's records in arrival
+// order and leaves each record's changelog state (the group's aggregate right
+// after it) at the record's partitioned position; k_pr_emit1 then writes the
+// rows in arrival order. No chunk carries: the bucket is its workgroup's.
+//
+//   per segment of the bucket (as many records as keep the LDS table at most
+//   half full; one segment unless the bucket holds very many groups):
+//   1. the segment's groups into an LDS table (in 256-record steps);
+//   2. each group found / claimed in the HBM table, its row loaded into LDS
+//      (all groups at once: one round of HBM latency per segment);
+//   3. 256-record steps in arrival order: the four waves one after the other,
+//      each group's lowest lane of the wave folds its lanes' records into the
+//      group's LDS state in lane (= arrival) order and hands each record its
+//      state (a step's records of one group are rare except for hot keys);
+//   4. the LDS states written back to their rows.
+// ---------------------------------------------------------------------------
+constexpr int kPbNT = 256;
+constexpr int kPbNW = kPbNT / 64;
+
+__device__ inline uint32_t pb_home(uint64_t g, int log2tab) {
+  uint32_t h = (uint32_t)g * 0x9E3779B1u + (uint32_t)(g >> 32) * 0x85EBCA77u;
+  h ^= (h >> 15) * 0x7FEB352Du;
+  return h >> (32 - log2tab);
+}
+
+// find or claim group g's row in the HBM table; -1 = region full (ERR_OOM)
+__device__ inline int64_t pr_claim_row(const TwTable &t, uint64_t g, bool &isnew) {
+  const uint64_t rb = tw_region_base(t, g);
+  uint64_t sl = tw_home_in(t, g);
+  const uint64_t step = tw_step(t), np = (t.rmask + 1) / step;
+  isnew = false;
+  for (uint64_t probe = 0; probe < np && probe < kMaxProbes; ++probe) {
+    uint64_t *kp = t.key(rb + sl);
+    const uint64_t k = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k == g) return (int64_t)(rb + sl);
+    if (k == kEmpty) {
+      const uint64_t old = atomicCAS((unsigned long long *)kp, (unsigned long long)kEmpty, (unsigned long long)g);
+      if (old == kEmpty) {
+        t.mark(rb + sl);
+        isnew = true;
+        return (int64_t)(rb + sl);
+      }
+      if (old == g) return (int64_t)(rb + sl);
+    }
+    sl = (sl + step) & t.rmask;
+  }
+  return -1;
+}
+
+// A partitioned record with its first kPrRegWords words in registers
+// (prefetched a step ahead); further words (more columns) from memory. Every
+// word an op of <= 2 columns reads is a register: no load inside a step, whose
+// wait would also wait for the step's stores (vmcnt counts both).
+constexpr int kPrRegWords = 4;
+template <bool REG>  // REG: the record has <= kPrRegWords words (no memory path)
+struct PrRecRegs {
+  uint64_t r0, r1, r2, r3;  // named, not an array: a runtime index would put an array on the stack
+  const uint64_t *w;
+  bool pk;
+  int C;
+  __device__ uint32_t key() const { return (uint32_t)r0; }
+  __device__ uint32_t krel(uint32_t kbase) const {
+    return pk ? kbase + (uint32_t)((r0 >> 32) & 0xFFFFull) : (uint32_t)(r0 >> 32);
+  }
+  __device__ bool present(int c) const { return pk ? (r0 >> (56 + c)) & 1ull : (r1 >> (32 + c)) & 1ull; }
+  __device__ int64_t word(int k) const {
+    if (!REG && k >= kPrRegWords) return (int64_t)w[k];
+    return (int64_t)(k == 0 ? r0 : k == 1 ? r1 : k == 2 ? r2 : r3);
+  }
+  __device__ int64_t col(int c) const { return word((pk ? 1 : 2) + c); }
+  __device__ int64_t seq1() const { return word((pk ? 1 : 2) + C); }
+};
+
+template <int MS, int LT, bool REG>
+__global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, PartParams pp, TwTable t,
+                                                     PartBuffers pb, PrPart pr, DevScalars *sc) {
+  constexpr int TAB = 1 << LT;
+  constexpr int EPT = TAB / kPbNT;  // table entries per thread
+  constexpr int PF = 8;             // record loads in flight per thread in the one-pass insert
+  __shared__ uint64_t tkey[TAB];
+  __shared__ int64_t tst[MS][TAB];
+  __shared__ uint32_t tslot[TAB];
+  __shared__ int64_t stg[kPbNW][MS][64];  // each wave's records' contributions, then its groups' totals
+  __shared__ uint8_t widx[kPbNW][TAB];     // per wave: 1 + owner lane of each group in the step, 0 = none
+  __shared__ uint32_t s_fill;
+  __shared__ uint64_t s_red[2][kPbNW];
+  if (sc->redo) return;  // uniform: the optimistic pass found late records (bucket starts are stale)
+  const uint32_t b = blockIdx.x;
+  const uint64_t r0 = pb.bstart[b], r1 = pb.bstart[b + 1];
+  if (r0 >= r1) return;  // uniform
+  const bool pk = sc->packed != 0;
+  const int W = pk ? pp.words - 1 : pp.words;
+  const int C = pp.words - 2 - pp.has_seq;
+  const uint32_t kbase = (uint32_t)sc->kbase;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ns = prog.n_slots;
+  const uint32_t bid = (uint32_t)p.batch_id;
+  const uint64_t *rec = pb.rec;
+  uint32_t err = 0;
+  uint64_t fresh = 0, touched = 0;
+  uint64_t c_ins = 0, c_claim = 0, c_steps = 0, c_back = 0, nseg = 0;  // phase clocks (HSG_PHASES)
+  uint64_t c_phase = 0, npeer = 0;
+  const uint64_t c_start = wall_clock64();
+  // LDS insert of group g; returns false once the table passed half full
+  // (then at most TAB / 2 + kPbNT - 1 entries: every probe sequence ends)
+  auto insert = [&](uint64_t g) -> bool {
+    uint32_t h = pb_home(g, LT);
+    for (;;) {
+      const uint64_t c = tkey[h];
+      if (c == g) return true;
+      if (c == kEmpty) {
+        const uint64_t old = atomicCAS((unsigned long long *)&tkey[h], (unsigned long long)kEmpty, (unsigned long long)g);
+        if (old == kEmpty) return atomicAdd(&s_fill, 1u) + 1 <= (uint32_t)(TAB / 2);
+        if (old == g) return true;
+      }
+      h = (h + 1) & (TAB - 1);
+    }
+  };
+  for (int e = threadIdx.x; e < TAB; e += kPbNT) tkey[e] = kEmpty;
+  for (int e = threadIdx.x; e < kPbNW * TAB; e += kPbNT) (&widx[0][0])[e] = 0;
+  if (threadIdx.x == 0) s_fill = 0;
+  __syncthreads();
+  // 1a. one pass over the whole bucket, PF record loads in flight per thread:
+  // one segment when its groups fill at most half the table (the common case)
+  uint64_t ca = wall_clock64();
+  bool ok = true;
+  for (uint64_t i0 = r0 + threadIdx.x; ok && i0 < r1; i0 += (uint64_t)PF * kPbNT) {
+    uint64_t w0[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const uint64_t i = i0 + (uint64_t)u * kPbNT;
+      w0[u] = i < r1 ? rec[i * (uint64_t)W] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const uint64_t i = i0 + (uint64_t)u * kPbNT;
+      if (ok && i < r1) {
+        const PrRecRegs<REG> v{w0[u], 0, 0, 0, nullptr, pk, C};
+        ok = insert(((uint64_t)v.key() << 32) | v.krel(kbase));
+      }
+    }
+    if (s_fill > (uint32_t)(TAB / 2)) ok = false;  // another thread passed it (racy read: only stops early)
+  }
+  lds_barrier();
+  const bool one_segment = s_fill <= (uint32_t)(TAB / 2);  // uniform
+  for (uint64_t s0 = r0; s0 < r1;) {
+    ++nseg;
+    uint64_t s1 = r1;
+    if (!one_segment) {
+      // 1b. the segment's groups in kPbNT-record steps while the table stays <= half full
+      __syncthreads();
+      for (int e = threadIdx.x; e < TAB; e += kPbNT) tkey[e] = kEmpty;
+      if (threadIdx.x == 0) s_fill = 0;
+      __syncthreads();
+      s1 = s0;
+      while (s1 < r1) {
+        if (s_fill + kPbNT > (uint32_t)(TAB / 2)) break;  // uniform (read after the barrier)
+        const uint64_t i = s1 + threadIdx.x;
+        if (i < r1) {
+          const PrRecRegs<REG> v{rec[i * (uint64_t)W], 0, 0, 0, nullptr, pk, C};
+          insert(((uint64_t)v.key() << 32) | v.krel(kbase));
+        }
+        s1 = s1 + kPbNT < r1 ? s1 + kPbNT : r1;
+        lds_barrier();
+      }
+    }
+    { const uint64_t cb = wall_clock64(); c_ins += cb - ca; ca = cb; }
+    // 2. rows of the segment's groups into LDS: every entry's home probe
+    // issued at once (agent-scope loads: an earlier segment of this workgroup
+    // may have written the rows), then the rows
+    {
+      uint64_t g[EPT], kh[EPT], hs[EPT];
+#pragma unroll
+      for (int u = 0; u < EPT; ++u) {
+        g[u] = tkey[threadIdx.x + u * kPbNT];
+        hs[u] = 0;
+        kh[u] = kEmpty;
+        if (g[u] != kEmpty) {
+          hs[u] = tw_region_base(t, g[u]) + tw_home_in(t, g[u]);
+          kh[u] = __hip_atomic_load(t.key(hs[u]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      int64_t sl[EPT];
+      bool isnew[EPT];
+#pragma unroll
+      for (int u = 0; u < EPT; ++u) {
+        sl[u] = -1;
+        isnew[u] = false;
+        if (g[u] == kEmpty) continue;
+        if (kh[u] == g[u]) {
+          sl[u] = (int64_t)hs[u];
+        } else {
+          if (kh[u] == kEmpty) {
+            const uint64_t old = atomicCAS((unsigned long long *)t.key(hs[u]), (unsigned long long)kEmpty,
+                                           (unsigned long long)g[u]);
+            if (old == kEmpty) {
+              t.mark(hs[u]);
+              isnew[u] = true;
+              sl[u] = (int64_t)hs[u];
+            } else if (old == g[u]) {
+              sl[u] = (int64_t)hs[u];
+            }
+          }
+          if (sl[u] < 0) sl[u] = pr_claim_row(t, g[u], isnew[u]);  // collision: the full probe
+        }
+      }
+      int64_t cur[EPT][MS];
+      uint32_t st[EPT];
+#pragma unroll
+      for (int u = 0; u < EPT; ++u) {
+        identity_row<MS>(prog, cur[u]);
+        st[u] = 0;
+        if (sl[u] >= 0 && !isnew[u]) {
+          const int64_t *row = t.aggs(sl[u]);
+#pragma unroll
+          for (int s = 0; s < MS; ++s)
+            if (s < ns) cur[u][s] = __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          st[u] = __hip_atomic_load(t.stamp(sl[u]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < EPT; ++u) {
+        const int e = threadIdx.x + u * kPbNT;
+        if (g[u] == kEmpty) continue;
+        if (sl[u] < 0) {
+          err |= ERR_OOM;
+        } else {
+          fresh += isnew[u] ? 1 : 0;
+          if (st[u] != bid) {  // (a new row's stamp reads as 0)
+            *t.stamp(sl[u]) = bid;
+            touched += 1;
+          }
+        }
+        tslot[e] = sl[u] < 0 ? ~0u : (uint32_t)sl[u];
+#pragma unroll
+        for (int s = 0; s < MS; ++s) tst[s][e] = cur[u][s];
+      }
+    }
+    lds_barrier();
+    { const uint64_t cb = wall_clock64(); c_claim += cb - ca; ca = cb; }
+    // 3. the segment's records in arrival order (the next step's first two
+    // words loaded while this step runs). A step's four waves run side by
+    // side: (A) each lane folds its wave's earlier records of its group (lane
+    // order = arrival order) into its wave-local prefix; the group's highest
+    // lane of the wave (its owner) holds the wave's total; (B) each owner
+    // takes the group's state, folds in the totals of the earlier waves'
+    // owners of the group, and hands the result (the state before its wave)
+    // to its lanes; the owner in the group's last wave of the step keeps the
+    // state after the step. Two barriers per step.
+    // the step's record words: registers, loaded one step ahead at the top
+    // of the previous step (before its stores: the wait for them at the top
+    // of this step then leaves the stores in flight)
+    uint64_t nx0 = 0, nx1 = 0, nx2 = 0, nx3 = 0;
+    auto fetch = [&](uint64_t ii) {
+      const uint64_t *q = rec + ii * (uint64_t)W;
+      const bool f = ii < s1;
+      nx0 = f ? q[0] : 0ull;
+      nx1 = (f && W > 1) ? q[1] : 0ull;
+      nx2 = (f && W > 2) ? q[2] : 0ull;
+      nx3 = (f && W > 3) ? q[3] : 0ull;
+    };
+    fetch(s0 + threadIdx.x);
+    for (uint64_t base = s0; base < s1; base += kPbNT) {
+      const uint64_t i = base + threadIdx.x;
+      const bool in = i < s1;
+      const PrRecRegs<REG> v{nx0, nx1, nx2, nx3, rec + i * (uint64_t)W, pk, C};
+      fetch(i + kPbNT);
+      uint32_t h = 0;
+      int64_t pre[MS];
+      identity_row<MS>(prog, pre);
+      const uint64_t t0 = wall_clock64();
+      if (in) {
+        const uint64_t g = ((uint64_t)v.key() << 32) | v.krel(kbase);
+        h = pb_home(g, LT);
+        while (tkey[h] != g) h = (h + 1) & (TAB - 1);  // inserted in step 1
+        int64_t e[MS];
+        pr_elems<MS>(prog, v, e);
+#pragma unroll
+        for (int s = 0; s < MS; ++s) stg[wv][s][lane] = e[s];
+      }
+      // this wave's lanes of each group, found by one ballot per table bit
+      uint64_t peers = __ballot(in);
+#pragma unroll
+      for (int bit = 0; bit < LT; ++bit) {
+        const bool x = (h >> bit) & 1u;
+        const uint64_t bb = __ballot(x);
+        peers &= x ? bb : ~bb;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");  // the wave's elements in LDS
+      const uint64_t t1 = wall_clock64();
+      npeer += in ? (uint64_t)__popcll(peers) : 0ull;
+      // (A) wave-local inclusive prefix over the group's lanes up to this one
+      if (in) {
+        const uint64_t upto = peers & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+        for (uint64_t m = upto; m; m &= m - 1) {
+          const int q = __ffsll((long long)m) - 1;
+          int64_t e[MS];
+#pragma unroll
+          for (int s = 0; s < MS; ++s) e[s] = stg[wv][s][q];
+          combine_row<MS>(prog, pre, e);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");  // every lane read its peers' elements
+      const uint64_t t2 = wall_clock64();
+      const int owner_lane = in ? 63 - __clzll((long long)peers) : lane;
+      const bool owner = in && owner_lane == lane;
+      if (owner) {
+#pragma unroll
+        for (int s = 0; s < MS; ++s) stg[wv][s][lane] = pre[s];  // the wave's total for the group
+        widx[wv][h] = (uint8_t)(lane + 1);
+      }
+      lds_barrier();  // (LDS only: the step's global loads and stores keep flowing)
+      // (B) the owners: the state before this wave, and after the step
+      int64_t carry[MS], after[MS];
+      bool last = false;
+      if (owner) {
+#pragma unroll
+        for (int s = 0; s < MS; ++s) carry[s] = tst[s][h];
+        last = true;
+        for (int w = 0; w < kPbNW; ++w) {
+          const uint32_t k = widx[w][h];
+          if (!k || w == wv) continue;
+          if (w > wv) {
+            last = false;
+            continue;
+          }
+          int64_t e[MS];
+#pragma unroll
+          for (int s = 0; s < MS; ++s) e[s] = stg[w][s][k - 1];
+          combine_row<MS>(prog, carry, e);
+        }
+#pragma unroll
+        for (int s = 0; s < MS; ++s) after[s] = carry[s];
+        combine_row<MS>(prog, after, pre);
+      } else {
+        identity_row<MS>(prog, carry);
+      }
+      // every lane takes its owner's carry (all lanes active: plain permutes)
+#pragma unroll
+      for (int s = 0; s < MS; ++s) carry[s] = __shfl(carry[s], owner_lane, 64);
+      lds_barrier();  // every owner has read the totals and the states
+      const uint64_t t3 = wall_clock64();
+      c_phase += (t1 - t0) | ((t2 - t1) << 21) | ((t3 - t2) << 42);  // 21-bit fields (per-step deltas)
+      if (in) {
+        int64_t fin[MS];
+#pragma unroll
+        for (int s = 0; s < MS; ++s) fin[s] = carry[s];
+        combine_row<MS>(prog, fin, pre);
+        int64_t *o = pr.fin + i * (uint64_t)ns;
+#pragma unroll
+        for (int s = 0; s < MS; ++s)
+          if (s < ns) o[s] = fin[s];
+      }
+      if (owner) {
+        if (last) {
+#pragma unroll
+          for (int s = 0; s < MS; ++s) tst[s][h] = after[s];
+        }
+        widx[wv][h] = 0;
+      }
+    }
+    lds_barrier();  // the last step's owners have written their groups' states
+    { const uint64_t cb = wall_clock64(); c_steps += cb - ca; ca = cb; }
+    // 4. the groups' states back to their rows
+    for (int e = threadIdx.x; e < TAB; e += kPbNT) {
+      if (tkey[e] == kEmpty || tslot[e] == ~0u) continue;
+      int64_t *row = t.aggs(tslot[e]);
+#pragma unroll
+      for (int s = 0; s < MS; ++s)
+        if (s < ns) row[s] = tst[s][e];
+    }
+    // the next segment reads these rows back (L1-bypassing loads): drain
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    c_back += wall_clock64() - ca;
+    ca = wall_clock64();
+    s0 = s1;
+  }
+  if (err) atomicOr(&sc->err, err);
+  const uint64_t f = wave_sum_u64(fresh), tc = wave_sum_u64(touched);
+  if (lane == 0) {
+    s_red[0][wv] = f;
+    s_red[1][wv] = tc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t ff = 0, tt = 0;
+    for (int k = 0; k < kPbNW; ++k) {
+      ff += s_red[0][k];
+      tt += s_red[1][k];
+    }
+    if (ff) atomicAdd((unsigned long long *)&sc->live_x[blockIdx.x & 7], (unsigned long long)ff);
+    if (tt) atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)tt);
+    atomicAdd((unsigned long long *)&sc->scratch[36], (unsigned long long)c_ins);
+    atomicAdd((unsigned long long *)&sc->scratch[37], (unsigned long long)c_claim);
+    atomicAdd((unsigned long long *)&sc->scratch[38], (unsigned long long)c_steps);
+    atomicAdd((unsigned long long *)&sc->scratch[39], (unsigned long long)c_back);
+    atomicAdd((unsigned long long *)&sc->scratch[40], (unsigned long long)nseg);
+    atomicAdd((unsigned long long *)&sc->scratch[41], 1ull);
+    atomicAdd((unsigned long long *)&sc->scratch[42], (unsigned long long)(wall_clock64() - c_start));
+    if (blockIdx.x == 0) sc->scratch[43] = c_phase;  // one workgroup's step sub-phases
+  }
+  if (lane == 0 && npeer) atomicAdd((unsigned long long *)&sc->scratch[44], (unsigned long long)npeer);
+}
+
+// Rows of one-window ops in arrival order: the record's window as the
+// partition computed it, its state from k_pr_bucket (pr.fin at the record's
+// partitioned position). Rounds of consecutive records: coalesced lanes.
+template <int MS>
+__global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit1(Batch bt, Program prog, TwParams p, PartBuffers pb,
+                                                             PrPart pr, const int64_t *__restrict__ rec_wm,
+                                                             const int64_t *__restrict__ seq, OutCols out,
+                                                             uint64_t out_base, uint64_t out_cap, DevScalars *sc) {
+  __shared__ uint32_t sw[kPrEmitThreads / 64];
+  if (sc->redo) return;  // uniform
+  const int64_t k_epoch = sc->k_epoch;
+  const int64_t *wm = rec_wm ? rec_wm : (sc->no_late ? nullptr : pb.wm);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ns = prog.n_slots;
+  uint32_t err = 0;
+  uint64_t base = pr.tpoff[(uint64_t)blockIdx.x * (kPrEmitRecs / kPartTileRecs)];
+  for (int rd = 0; rd < kPrEmitRounds; ++rd) {
+    const uint64_t i = (uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)rd * kPrEmitThreads + threadIdx.x;
+    if ((uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)rd * kPrEmitThreads >= bt.n) break;  // uniform
+    uint32_t a = 0, n = 0, key = HSG_KEY_NONE;
+    if (i < bt.n) {
+      key = bt.key[i];
+      const int64_t ts = bt.ts[i];
+      if (key != HSG_KEY_NONE) {  // the window the partition passes accepted (k_part.hip part_record)
+        uint64_t k_lo, k_hi;
+        if (record_windows(p, ts, k_lo, k_hi)) {
+          const int64_t w = wm ? wm[i] : INT64_MIN;
+          if (window_accepted(p, k_lo, w)) {
+            const int64_t lo = (int64_t)k_lo - k_epoch;
+            if (lo >= 0 && lo <= 0xFFFFFFFFll) {
+              a = (uint32_t)lo;
+              n = 1;
+            }
+          }
+        }
+      }
+    }
+    const uint32_t incl = (uint32_t)wave_incl_sum((uint64_t)n);
+    if (lane == 63) sw[wv] = incl;
+    lds_barrier();
+    uint64_t o = base + incl - n, tot = 0;
+    for (int k = 0; k < kPrEmitThreads / 64; ++k) {
+      o += k < wv ? sw[k] : 0u;
+      tot += sw[k];
+    }
+    lds_barrier();
+    base += tot;
+    if (!n) continue;
+    const uint64_t pos = pr.pos[i];
+    const uint64_t ob = out_base + o;
+    if (pos >= pb.n_cap || ob >= out_cap) {  // cannot happen: the scatter placed every record with a window
+      err |= ERR_OOM;
+      continue;
+    }
+    int64_t R[MS];
+    const int64_t *f = pr.fin + pos * (uint64_t)ns;
+#pragma unroll
+    for (int s = 0; s < MS; ++s) R[s] = s < ns ? f[s] : 0;
+    out.key[ob] = key;
+    int64_t ws = 0, we = 0;
+    if (p.kind != HSG_UNWINDOWED) {
+      const int64_t k = k_epoch + (int64_t)a;
+      ws = (int64_t)((uint64_t)k * (uint64_t)p.adv);
+      we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
+    }
+    out.ws[ob] = ws;
+    out.we[ob] = we;
+    out.src[ob] = seq ? seq[i] : (int64_t)(p.rec_base + i);
+#pragma unroll
+    for (int jj = 0; jj < kMaxAggs; ++jj)
+      if (jj < prog.n_out) out.agg[jj][ob] = out_value_reg<MS>(prog, jj, R);
   }
   if (err) atomicOr(&sc->err, err);
 }
@@ -595,6 +1080,18 @@ static void pr_launch(hipStream_t s, const Batch &b, const Program &prog, const 
                       const TwTable &t, const PartBuffers &pb, const PrPart &pr, uint32_t wpr, const int64_t *rec_wm,
                       const int64_t *seq, const OutCols &out, uint64_t out_base, uint64_t out_cap, DevScalars *sc) {
   const uint64_t nb = 1ull << pp.np_log2;
+  if (wpr == 1) {
+    // LDS: table 12 + 8 MS bytes per entry, staging 2 KB per slot
+    constexpr int LT = MS <= 6 ? 10 : 9;
+    if (pp.words <= kPrRegWords)
+      hipLaunchKernelGGL((k_pr_bucket<MS, LT, true>), dim3((unsigned)nb), dim3(kPbNT), 0, s, prog, p, pp, t, pb, pr, sc);
+    else
+      hipLaunchKernelGGL((k_pr_bucket<MS, LT, false>), dim3((unsigned)nb), dim3(kPbNT), 0, s, prog, p, pp, t, pb, pr, sc);
+    const uint64_t tiles = (b.n + kPrEmitRecs - 1) / kPrEmitRecs;
+    hipLaunchKernelGGL(k_pr_emit1<MS>, dim3((unsigned)tiles), dim3(kPrEmitThreads), 0, s, b, prog, p, pb, pr, rec_wm,
+                       seq, out, out_base, out_cap, sc);
+    return;
+  }
   const dim3 g((unsigned)(nb + b.n / pp.chunk + 1));
   hipLaunchKernelGGL(k_pr_local<MS>, g, dim3(kPrNT), 0, s, prog, pp, pb, pr, wpr, sc);
   hipLaunchKernelGGL(k_pr_carry<MS>, dim3((unsigned)nb), dim3(256), 0, s, prog, p, pp, t, pb, pr, sc);
@@ -609,6 +1106,7 @@ void launch_pr_part(hipStream_t s, const Batch &b, const Program &prog, const Tw
   if (!b.n) return;
   if (prog.n_slots <= 2) pr_launch<2>(s, b, prog, p, pp, t, pb, pr, wpr, rec_wm, seq, out, out_base, out_cap, sc);
   else if (prog.n_slots <= 4) pr_launch<4>(s, b, prog, p, pp, t, pb, pr, wpr, rec_wm, seq, out, out_base, out_cap, sc);
+  else if (prog.n_slots <= 6) pr_launch<6>(s, b, prog, p, pp, t, pb, pr, wpr, rec_wm, seq, out, out_base, out_cap, sc);
   else pr_launch<8>(s, b, prog, p, pp, t, pb, pr, wpr, rec_wm, seq, out, out_base, out_cap, sc);
 }
 

@@ -45,6 +45,25 @@ __device__ inline SessKey ss_blank(uint32_t key) {
   return e;
 }
 
+// one entry in four 16-byte loads, fields assigned one by one (a struct copy
+// of the 64-byte entry can land on the stack)
+__device__ inline SessKey ss_load_entry(const SessKey *p) {
+  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+  const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+  SessKey e;
+  e.key = a.x;
+  e.len = a.y;
+  e.off = (uint64_t)a.z | ((uint64_t)a.w << 32);
+  e.cap = b.x;
+  e.mvalid = b.y;
+  e.emark = (uint64_t)b.z | ((uint64_t)b.w << 32);
+  e.ms = (int64_t)((uint64_t)c.x | ((uint64_t)c.y << 32));
+  e.me = (int64_t)((uint64_t)c.z | ((uint64_t)c.w << 32));
+  e.ma[0] = (int64_t)((uint64_t)d.x | ((uint64_t)d.y << 32));
+  e.ma[1] = (int64_t)((uint64_t)d.z | ((uint64_t)d.w << 32));
+  return e;
+}
+
 __global__ void k_ss_reset(SessTable t) {
   const uint64_t cap = t.kmask + 1;
   for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap; s += (uint64_t)gridDim.x * blockDim.x)
@@ -689,7 +708,7 @@ template <int MS, bool APPLY, class RS>
 __device__ inline uint32_t mg_sweep(const Program &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t r0,
                                     uint32_t r1, uint64_t off, uint64_t i0, uint64_t len, bool tail_regs,
                                     const MgSess<MS> (&tail)[kMgTail], uint64_t dst, uint32_t batch_id,
-                                    EmitSink *sink = nullptr, MgSess<MS> *lastp = nullptr) {
+                                    EmitSink *sink = nullptr, SessKey *mirror = nullptr) {
   const int ns = prog.n_slots;
   uint64_t j = i0;   // next resident
   uint32_t r = r0;   // next run
@@ -746,7 +765,16 @@ __device__ inline uint32_t mg_sweep(const Program &prog, const SessTable &t, int
     if (APPLY) ss_store<MS>(t, dst + i0 + k, cur.s, cur.e, cur.fresh ? batch_id : cur.stamp, cur.a);
     if (sink && cur.fresh) mg_emit<MS>(prog, *sink, cur);
     ++k;
-    if (lastp) *lastp = cur;  // the list's new last session (the sweep runs to its end)
+    if (mirror) {  // the list's new last session (the sweep runs to its end) into the entry's mirror
+      const bool m = prog.n_slots <= kSessMirrorSlots;
+      if (m) {
+        mirror->ms = cur.s;
+        mirror->me = cur.e;
+#pragma unroll
+        for (int s = 0; s < kSessMirrorSlots; ++s) mirror->ma[s] = s < MS ? cur.a[s] : 0;
+      }
+      mirror->mvalid = m ? 1u : 0u;
+    }
   }
   return k;
 }
@@ -774,15 +802,32 @@ __device__ inline uint64_t mg_first_end_ge(const SessTable &t, uint64_t off, uin
 
 // Plan of one key against its list: the first resident its runs can reach,
 // the merged count, and the rows of a fresh list when it cannot stay in place.
+// fast: planned from the entry's mirror of the last session, no list read
+// (mg_fast: the batch's first run starts at or after the last session's
+// start, so no resident but the last can be reached, the one before ending
+// more than gap before the last starts; the last is touched iff the first
+// run comes within gap of its end).
+template <int MS>
+__device__ inline void mg_mirror_tail(const Program &prog, const SessKey &e, uint32_t batch_id,
+                                      MgSess<MS> (&tail)[kMgTail]);
+template <class RS>
+__device__ inline bool mg_fast(const RS &rs, uint32_t ra, const SessKey &e) {
+  return e.mvalid && e.len > 0 && rs.start(ra) >= e.ms;
+}
 template <int MS, class RS>
 __device__ inline void mg_plan(const Program &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t ra,
-                               uint32_t rb, const SessKey &e, uint64_t &i0, uint32_t &M, uint32_t &newcap,
-                               uint32_t *fresh = nullptr) {
+                               uint32_t rb, const SessKey &e, bool fast, uint32_t batch_id, uint64_t &i0, uint32_t &M,
+                               uint32_t &newcap, uint32_t *fresh = nullptr) {
   const int64_t lo = (int64_t)((uint64_t)rs.start(ra) - (uint64_t)gap);
-  i0 = mg_first_end_ge(t, e.off, e.len, lo);
-  MgSess<MS> dummy[kMgTail];
+  MgSess<MS> tail[kMgTail];
+  if (fast) {
+    i0 = e.me >= lo ? e.len - 1 : e.len;
+    mg_mirror_tail<MS>(prog, e, batch_id, tail);
+  } else {
+    i0 = mg_first_end_ge(t, e.off, e.len, lo);
+  }
   EmitSink cnt{OutCols{}, ~0ull, 0, 0};
-  M = mg_sweep<MS, false>(prog, t, gap, rs, ra, rb, e.off, i0, e.len, false, dummy, 0, 0, &cnt);
+  M = mg_sweep<MS, false>(prog, t, gap, rs, ra, rb, e.off, i0, e.len, fast, tail, 0, 0, &cnt);
   if (fresh) *fresh = cnt.n;
   // in place when the merged list fits and the rewritten tail fits the
   // registers, else a fresh list (prefix copied)
@@ -807,83 +852,46 @@ __device__ inline void mg_mirror_tail(const Program &prog, const SessKey &e, uin
   for (int s = 0; s < MS; ++s) tail[0].a[s] = (s < kSessMirrorSlots && s < prog.n_slots) ? e.ma[s] : 0;
 }
 
-// Fast plan from the mirror, no list read: the batch's first run starts at or
-// after the last session's start, so no resident but the last can be reached
-// (the one before ends more than gap before the last starts); the last is
-// touched iff the first run comes within gap of its end.
-template <int MS, class RS>
-__device__ inline bool mg_plan_fast(const Program &prog, int64_t gap, const RS &rs, uint32_t ra, uint32_t rb,
-                                    const SessKey &e, uint32_t batch_id, uint64_t &i0, uint32_t &M, uint32_t &newcap,
-                                    uint32_t *fresh) {
-  if (!e.mvalid || e.len == 0 || rs.start(ra) < e.ms) return false;
-  const int64_t lo = (int64_t)((uint64_t)rs.start(ra) - (uint64_t)gap);
-  i0 = e.me >= lo ? e.len - 1 : e.len;
-  MgSess<MS> tail[kMgTail];
-  mg_mirror_tail<MS>(prog, e, batch_id, tail);
-  EmitSink cnt{OutCols{}, ~0ull, 0, 0};
-  SessTable none = {};
-  M = mg_sweep<MS, false>(prog, none, gap, rs, ra, rb, 0, i0, e.len, true, tail, 0, 0, &cnt);
-  if (fresh) *fresh = cnt.n;
-  newcap = (i0 + M > e.cap) ? ss_grow_cap(i0 + M + 1) : 0u;
-  return true;
-}
-
-// Apply a fast-planned key: residents [i0, len) come from the mirror.
-template <int MS, class RS>
-__device__ inline void mg_apply_fast(const Program &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t ra,
-                                     uint32_t rb, const SessKey &e, uint64_t i0, uint64_t dst, bool reloc,
-                                     uint32_t batch_id, EmitSink *sink, MgSess<MS> *lastp) {
-  if (reloc)
-    for (uint64_t k = 0; k < i0; ++k) ss_copy(t, dst + k, t, e.off + k);
-  MgSess<MS> tail[kMgTail];
-  mg_mirror_tail<MS>(prog, e, batch_id, tail);
-  mg_sweep<MS, true>(prog, t, gap, rs, ra, rb, e.off, i0, e.len, true, tail, dst, batch_id, sink, lastp);
-}
-
-// The entry after a merge: list position, capacity and the last-session mirror.
-template <int MS>
-__device__ inline void ss_entry_commit(const Program &prog, SessKey &ke, uint64_t off, uint32_t len, uint32_t newcap,
-                                       const MgSess<MS> &last) {
+// The entry after a merge (its mirror was written by the sweep).
+__device__ inline void ss_entry_commit(SessKey &ke, uint64_t off, uint32_t len, uint32_t newcap) {
   ke.off = off;
   ke.len = len;
   if (newcap) ke.cap = newcap;
-  const bool mirror = prog.n_slots <= kSessMirrorSlots && len > 0;
-  if (mirror) {
-    ke.ms = last.s;
-    ke.me = last.e;
-#pragma unroll
-    for (int s = 0; s < kSessMirrorSlots; ++s) ke.ma[s] = s < MS ? last.a[s] : 0;
-  }
-  ke.mvalid = mirror ? 1u : 0u;
 }
 
 // Apply a planned key: the list at dst (fresh rows: the prefix copied first).
+// The rewritten residents come from registers: the mirror (fast) or the rows
+// loaded here (in place), else from the old list (relocated).
 template <int MS, class RS>
 __device__ inline void mg_apply(const Program &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t ra,
-                                uint32_t rb, const SessKey &e, uint64_t i0, uint64_t dst, bool reloc,
-                                uint32_t batch_id, EmitSink *sink = nullptr, MgSess<MS> *lastp = nullptr) {
+                                uint32_t rb, const SessKey &e, bool fast, uint64_t i0, uint64_t dst, bool reloc,
+                                uint32_t batch_id, EmitSink *sink = nullptr, SessKey *mirror = nullptr) {
   const int ns = prog.n_slots;
   if (reloc)
     for (uint64_t k = 0; k < i0; ++k) ss_copy(t, dst + k, t, e.off + k);
   MgSess<MS> tail[kMgTail];
+  if (fast) {
+    mg_mirror_tail<MS>(prog, e, batch_id, tail);
+  } else {
 #pragma unroll
-  for (int k = 0; k < kMgTail; ++k) {
-    const uint64_t j = i0 + k;
-    tail[k].s = tail[k].e = 0;
-    tail[k].stamp = 0;
-    tail[k].fresh = false;
+    for (int k = 0; k < kMgTail; ++k) {
+      const uint64_t j = i0 + k;
+      tail[k].s = tail[k].e = 0;
+      tail[k].stamp = 0;
+      tail[k].fresh = false;
 #pragma unroll
-    for (int s = 0; s < MS; ++s) tail[k].a[s] = 0;
-    if (!reloc && j < e.len) {
-      const uint64_t *row = ss_row(t, e.off + j);
-      tail[k].s = (int64_t)row[0];
-      tail[k].e = (int64_t)row[1];
-      tail[k].stamp = (uint32_t)row[2];
+      for (int s = 0; s < MS; ++s) tail[k].a[s] = 0;
+      if (!reloc && j < e.len) {
+        const uint64_t *row = ss_row(t, e.off + j);
+        tail[k].s = (int64_t)row[0];
+        tail[k].e = (int64_t)row[1];
+        tail[k].stamp = (uint32_t)row[2];
 #pragma unroll
-      for (int s = 0; s < MS; ++s) tail[k].a[s] = s < ns ? (int64_t)row[3 + s] : 0;
+        for (int s = 0; s < MS; ++s) tail[k].a[s] = s < ns ? (int64_t)row[3 + s] : 0;
+      }
     }
   }
-  mg_sweep<MS, true>(prog, t, gap, rs, ra, rb, e.off, i0, e.len, !reloc, tail, dst, batch_id, sink, lastp);
+  mg_sweep<MS, true>(prog, t, gap, rs, ra, rb, e.off, i0, e.len, fast || !reloc, tail, dst, batch_id, sink, mirror);
 }
 
 // ---------------------------------------------------------------------------
@@ -1297,10 +1305,10 @@ __global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, P
     sl = ss_find_or_insert(t, key, ins);
     if (sl < 0) err |= ERR_OOM;
     else {
-      if (!ins) e = t.kt[sl];
+      if (!ins) e = ss_load_entry(&t.kt[sl]);
       // near-sorted arrivals: planned from the entry's mirror, no list read
-      fast = mg_plan_fast<MS>(prog, p.gap, rs, ra, ra + nr, e, p.batch_id, i0, M, newcap, &fresh);
-      if (!fast) mg_plan<MS>(prog, t, p.gap, rs, ra, ra + nr, e, i0, M, newcap, &fresh);
+      fast = mg_fast(rs, ra, e);
+      mg_plan<MS>(prog, t, p.gap, rs, ra, ra + nr, e, fast, p.batch_id, i0, M, newcap, &fresh);
     }
   }
   const bool live = act && sl >= 0;
@@ -1347,10 +1355,8 @@ __global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, P
     const bool reloc = newcap != 0;
     const uint64_t dst = reloc ? sbase + before + incl - need : e.off;
     EmitSink sink{out, p.emit_mode == HSG_EMIT_PER_BATCH ? out_base + sobase + ebefore + einc - nem : ~0ull, key, 0};
-    MgSess<MS> last;
-    if (fast) mg_apply_fast<MS>(prog, t, p.gap, rs, ra, ra + nr, e, i0, dst, reloc, p.batch_id, &sink, &last);
-    else mg_apply<MS>(prog, t, p.gap, rs, ra, ra + nr, e, i0, dst, reloc, p.batch_id, &sink, &last);
-    ss_entry_commit<MS>(prog, t.kt[sl], dst, (uint32_t)(i0 + M), reloc ? newcap : 0u, last);
+    mg_apply<MS>(prog, t, p.gap, rs, ra, ra + nr, e, fast, i0, dst, reloc, p.batch_id, &sink, &t.kt[sl]);
+    ss_entry_commit(t.kt[sl], dst, (uint32_t)(i0 + M), reloc ? newcap : 0u);
     ld = (int64_t)M - (int64_t)(e.len - i0);
   }
   const uint64_t lsum = wave_sum_u64((uint64_t)ld);
@@ -1600,7 +1606,7 @@ __global__ __launch_bounds__(kMgNT) void k_ss_merge_big(SessParams p, SessTable 
       gslot[u] = sl;
       ++nt;
       if (!ins) ge[u] = t.kt[sl];
-      mg_plan<MS>(prog, t, p.gap, rsrc, ra, rb, ge[u], gi0[u], gM[u], gcap[u]);
+      mg_plan<MS>(prog, t, p.gap, rsrc, ra, rb, ge[u], false, p.batch_id, gi0[u], gM[u], gcap[u]);
       need += gcap[u];
     }
     uint64_t tneed;
@@ -1640,10 +1646,9 @@ __global__ __launch_bounds__(kMgNT) void k_ss_merge_big(SessParams p, SessTable 
         dst = my_alloc;
         my_alloc += gcap[u];
       }
-      MgSess<MS> last;
-      mg_apply<MS>(prog, t, p.gap, rsrc, ra, rb, ge[u], gi0[u], dst, reloc, p.batch_id, nullptr, &last);
       SessKey &ke = t.kt[gslot[u]];
-      ss_entry_commit<MS>(prog, ke, dst, (uint32_t)(gi0[u] + gM[u]), reloc ? gcap[u] : 0u, last);
+      mg_apply<MS>(prog, t, p.gap, rsrc, ra, rb, ge[u], false, gi0[u], dst, reloc, p.batch_id, nullptr, &ke);
+      ss_entry_commit(ke, dst, (uint32_t)(gi0[u] + gM[u]), reloc ? gcap[u] : 0u);
       atomicMin((unsigned long long *)&ke.emark, (unsigned long long)(bmark | gi0[u]));
       sp.touched[tp++] = (uint32_t)gslot[u];
       live_delta += (int64_t)gM[u] - (int64_t)(ge[u].len - gi0[u]);

@@ -527,6 +527,15 @@ int finish_batch(OpDevice &d, int64_t wm_in, uint64_t n, PushResult &r, std::str
             (unsigned long long)s.scratch[30], s.scratch[24] * 0.01 / s.scratch[30], s.scratch[25] * 0.01 / s.scratch[30],
             s.scratch[26] * 0.01 / s.scratch[30], s.scratch[27] * 0.01 / s.scratch[30], s.scratch[28] * 0.01 / s.scratch[30],
             s.scratch[29] * 0.01 / s.scratch[30]);
+  if (phases && s.scratch[41])
+    fprintf(stderr, "[hsg phases] per-record bucket wg=%llu segments/wg=%.2f insert=%.1fus claim=%.1fus steps=%.1fus writeback=%.1fus total=%.1fus (per-wg avg)\n",
+            (unsigned long long)s.scratch[41], (double)s.scratch[40] / s.scratch[41], s.scratch[36] * 0.01 / s.scratch[41],
+            s.scratch[37] * 0.01 / s.scratch[41], s.scratch[38] * 0.01 / s.scratch[41], s.scratch[39] * 0.01 / s.scratch[41],
+            s.scratch[42] * 0.01 / s.scratch[41]);
+  if (phases && s.scratch[41])
+    fprintf(stderr, "[hsg phases] per-record bucket: pre=%.1fus A=%.1fus B=%.1fus (thread 0) peer-lanes per keyed lane=%.2f\n",
+            (s.scratch[43] & 0x1FFFFF) * 0.01, ((s.scratch[43] >> 21) & 0x1FFFFF) * 0.01,
+            ((s.scratch[43] >> 42) & 0x1FFFFF) * 0.01, (double)s.scratch[44] / (16777216.0 / 64));
 
   r.wm_out = n ? s.wm_out : wm_in;
   r.pairs = s.pairs;

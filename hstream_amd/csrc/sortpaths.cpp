@@ -119,6 +119,7 @@ int perrecord_part_init(OpDevice &d, const hsg_op_config &cfg, const Program &pr
     x.ccnt = c.take<uint32_t>(chunks);
     x.counter = c.take<uint64_t>(8);
     x.partial = c.take<uint64_t>(scan_partials_needed(tiles) + 8);
+    x.fin = c.take<int64_t>(wpr == 1 ? n * ns : 1);
   };
   Carve probe{nullptr};
   PrPart tmp;
@@ -163,7 +164,9 @@ static int push_time_perrecord_part(OpDevice &d, const hsg_op_config &cfg, const
     PartParams pp;
     memset(&pp, 0, sizeof(pp));
     pp.chunk = kPrPairs / wpr;
-    pp.np_log2 = pr_buckets_log2(kb.n, pp.chunk);
+    // one-window ops: a workgroup walks each bucket (k_pr_bucket), as many
+    // buckets as the partition makes; else buckets of a few k_pr_local chunks
+    pp.np_log2 = wpr == 1 ? pr_buckets_log2(kb.n, 1024) : pr_buckets_log2(kb.n, pp.chunk);
     pp.bshift = d.bshift;
     for (int c = 0; c < cfg.n_cols; ++c) pp.has_valid |= kb.valid[c] != nullptr;
     pp.has_seq = last ? 1 : 0;
@@ -184,7 +187,7 @@ static int push_time_perrecord_part(OpDevice &d, const hsg_op_config &cfg, const
     launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc, can_pack, true);
     wait_table_reset(d);  // the passes above do not touch the table
     DTRY(hipMemsetAsync(d.prp.counter, 0, 8, d.stream));
-    launch_part_chunks(d.stream, pp, d.part, d.sc);
+    if (wpr != 1) launch_part_chunks(d.stream, pp, d.part, d.sc);
     launch_pr_part(d.stream, kb, prog, p, pp, d.tw, d.part, d.prp, wpr, rec_wm, seq, d.out, a.pending, d.out_cap,
                    d.sc);
     DTRY(hipEventRecord(d.ev_b, d.stream));
