@@ -205,39 +205,60 @@ static int push_sharded_fast(OpDevice &d, const hsg_op_config &cfg, const Progra
   };
   const XCols snd = carve(x.send, x.batch), rcv = carve(x.recv, (uint64_t)G * x.batch);
   launch_x_scatter(s, kb, xl, unwin, any_valid, C, d.part.offt, snd);
+  // this rank's own records never cross the fabric: they are copied into
+  // their place in the receive columns on the device (one rank: aggregated
+  // from the send columns where they are, no copy), the others travel in
+  // one all-to-all-v per column without the self block
+  const size_t self_n = scount[me];
+  scount[me] = 0;
+  rcount[me] = 0;
+  XCols src = rcv;
+  if (G == 1) {
+    src = snd;
+  } else if (self_n) {
+    const size_t so_me = sdispl[me], ro_me = rdispl[me];
+    DTRY(hipMemcpyAsync(rcv.key + ro_me, snd.key + so_me, self_n * 4, hipMemcpyDeviceToDevice, s));
+    DTRY(hipMemcpyAsync(rcv.ts + ro_me, snd.ts + so_me, self_n * 8, hipMemcpyDeviceToDevice, s));
+    for (int k = 0; k < C; ++k) {
+      DTRY(hipMemcpyAsync(rcv.col[k] + ro_me, snd.col[k] + so_me, self_n * 8, hipMemcpyDeviceToDevice, s));
+      if (any_valid) DTRY(hipMemcpyAsync(rcv.valid[k] + ro_me, snd.valid[k] + so_me, self_n, hipMemcpyDeviceToDevice, s));
+    }
+  }
+  if (G > 1) {
 #define XA2A(buf, dt, el)                                                                              \
   do {                                                                                                  \
     rc = comm_alltoallv(comm, snd.buf, scount.data(), sdispl.data(), rcv.buf, rcount.data(), rdispl.data(), \
                         dt, el, s, err);                                                                \
     if (rc != HSG_OK) return rc;                                                                        \
   } while (0)
-  if ((rc = comm_group_start(comm, err)) != HSG_OK) return rc;
-  XA2A(key, ncclUint32, 4);
-  XA2A(ts, ncclInt64, 8);
-  for (int k = 0; k < C; ++k) {
-    XA2A(col[k], ncclInt64, 8);
-    if (any_valid) XA2A(valid[k], ncclUint8, 1);
-  }
-  if ((rc = comm_group_end(comm, err)) != HSG_OK) return rc;
+    if ((rc = comm_group_start(comm, err)) != HSG_OK) return rc;
+    XA2A(key, ncclUint32, 4);
+    XA2A(ts, ncclInt64, 8);
+    for (int k = 0; k < C; ++k) {
+      XA2A(col[k], ncclInt64, 8);
+      if (any_valid) XA2A(valid[k], ncclUint8, 1);
+    }
+    if ((rc = comm_group_end(comm, err)) != HSG_OK) return rc;
 #undef XA2A
+  }
   DTRY(hipEventRecord(d.ev_d, s));
   DTRY(hipGetLastError());
   // 4. aggregate the owned records (order irrelevant for these ops)
   Batch rb;
   memset(&rb, 0, sizeof(rb));
   rb.n = ro;
-  rb.key = rcv.key;
-  rb.ts = rcv.ts;
+  rb.key = src.key;
+  rb.ts = src.ts;
   for (int k = 0; k < C; ++k) {
-    rb.col[k] = rcv.col[k];
-    rb.valid[k] = any_valid ? rcv.valid[k] : nullptr;
+    rb.col[k] = src.col[k];
+    rb.valid[k] = any_valid ? src.valid[k] : nullptr;
   }
   PushArgs la = a;
   la.wm_in = carry;  // any value <= the records' stream times keeps grace exact
   rc = push_local(d, cfg, prog, la, rb, nullptr, nullptr, r, err);
   float ms = 0;
   if (hipEventElapsedTime(&ms, d.ev_c, d.ev_d) == hipSuccess) r.exchange_ms = ms;
-  r.exchange_bytes = (uint64_t)(so - scount[me]) * (12 + 8 * C + (any_valid ? C : 0));
+  r.exchange_bytes = (uint64_t)(so - self_n) * (12 + 8 * C + (any_valid ? C : 0));
   r.wm_out = wm_global;
   r.owned = ro;
   r.global_records = total;

@@ -26,6 +26,7 @@
 // The order-dependent parts are exact: a group's prefix follows its records in
 // arrival order inside a chunk, chunks of a bucket are applied in bucket (=
 // arrival) order, LAST keeps the latest present record (combine_row).
+#include "hsg_agg.h"
 #include "hsg_dev.h"
 #include "hsg_part.h"
 #include "hsg_perrecord.h"
@@ -614,6 +615,63 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit(Batch bt, Program pr
 constexpr int kPbNT = 256;
 constexpr int kPbNW = kPbNT / 64;
 
+// Slot-program helpers over a program view (ProgRT, or ProgSig<SIG> with the
+// slot ops baked in: the common aggregate sets get straight-line combines)
+template <int MS, class PV>
+__device__ inline void combine_v(const PV &pv, int64_t (&a)[MS], const int64_t (&e)[MS]) {
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    if (s >= pv.n()) break;
+    const int op = pv.op(s);
+    if (op == S_LAST_SEQ) {
+      if (e[s] != 0) {
+        a[s] = e[s];
+        if (s + 1 < MS) a[s + 1] = e[s + 1];
+      }
+    } else if (op != S_LAST_VAL) {
+      a[s] = slot_combine(op, a[s], e[s]);
+    }
+  }
+}
+template <int MS, class PV>
+__device__ inline void identity_v(const PV &pv, int64_t (&a)[MS]) {
+#pragma unroll
+  for (int s = 0; s < MS; ++s) a[s] = s < pv.n() ? slot_identity_dev(pv.op(s)) : 0;
+}
+template <int MS, class PV, class RV>
+__device__ inline void elems_v(const PV &pv, const RV &r, int64_t (&e)[MS]) {
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    e[s] = 0;
+    if (s >= pv.n()) continue;
+    const int op = pv.op(s), c = pv.col(s);
+    if (op == S_CNT_ALL) {
+      e[s] = 1;
+      continue;
+    }
+    const bool pr = r.present(c);
+    if (op == S_LAST_VAL) {
+      e[s] = pr ? r.col(c) : 0;
+      continue;
+    }
+    if (!pr) {
+      e[s] = slot_identity_dev(op);
+      continue;
+    }
+    switch (op) {
+      case S_CNT: e[s] = 1; break;
+      case S_SUM_I:
+      case S_SUM_F:
+      case S_MIN_I:
+      case S_MAX_I: e[s] = r.col(c); break;
+      case S_MIN_F:
+      case S_MAX_F: e[s] = (int64_t)f64_ord(__builtin_bit_cast(double, r.col(c))); break;
+      case S_LAST_SEQ: e[s] = r.seq1(); break;
+      default: break;
+    }
+  }
+}
+
 __device__ inline uint32_t pb_home(uint64_t g, int log2tab) {
   uint32_t h = (uint32_t)g * 0x9E3779B1u + (uint32_t)(g >> 32) * 0x85EBCA77u;
   h ^= (h >> 15) * 0x7FEB352Du;
@@ -668,9 +726,10 @@ struct PrRecRegs {
   __device__ int64_t seq1() const { return word((pk ? 1 : 2) + C); }
 };
 
-template <int MS, int LT, bool REG>
+template <int MS, int LT, bool REG, uint64_t SIG>
 __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, PartParams pp, TwTable t,
                                                      PartBuffers pb, PrPart pr, DevScalars *sc) {
+  const ProgView<SIG> pv(prog);
   constexpr int TAB = 1 << LT;
   constexpr int EPT = TAB / kPbNT;  // table entries per thread
   constexpr int PF = 8;             // record loads in flight per thread in the one-pass insert
@@ -690,7 +749,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
   const int C = pp.words - 2 - pp.has_seq;
   const uint32_t kbase = (uint32_t)sc->kbase;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int ns = prog.n_slots;
+  const int ns = pv.n();
   const uint32_t bid = (uint32_t)p.batch_id;
   const uint64_t *rec = pb.rec;
   uint32_t err = 0;
@@ -805,7 +864,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
       uint32_t st[EPT];
 #pragma unroll
       for (int u = 0; u < EPT; ++u) {
-        identity_row<MS>(prog, cur[u]);
+        identity_v<MS>(pv, cur[u]);
         st[u] = 0;
         if (sl[u] >= 0 && !isnew[u]) {
           const int64_t *row = t.aggs(sl[u]);
@@ -864,14 +923,14 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
       fetch(i + kPbNT);
       uint32_t h = 0;
       int64_t pre[MS];
-      identity_row<MS>(prog, pre);
+      identity_v<MS>(pv, pre);
       const uint64_t t0 = wall_clock64();
       if (in) {
         const uint64_t g = ((uint64_t)v.key() << 32) | v.krel(kbase);
         h = pb_home(g, LT);
         while (tkey[h] != g) h = (h + 1) & (TAB - 1);  // inserted in step 1
         int64_t e[MS];
-        pr_elems<MS>(prog, v, e);
+        elems_v<MS>(pv, v, e);
 #pragma unroll
         for (int s = 0; s < MS; ++s) stg[wv][s][lane] = e[s];
       }
@@ -894,7 +953,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
           int64_t e[MS];
 #pragma unroll
           for (int s = 0; s < MS; ++s) e[s] = stg[wv][s][q];
-          combine_row<MS>(prog, pre, e);
+          combine_v<MS>(pv, pre, e);
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");  // every lane read its peers' elements
@@ -924,13 +983,13 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
           int64_t e[MS];
 #pragma unroll
           for (int s = 0; s < MS; ++s) e[s] = stg[w][s][k - 1];
-          combine_row<MS>(prog, carry, e);
+          combine_v<MS>(pv, carry, e);
         }
 #pragma unroll
         for (int s = 0; s < MS; ++s) after[s] = carry[s];
-        combine_row<MS>(prog, after, pre);
+        combine_v<MS>(pv, after, pre);
       } else {
-        identity_row<MS>(prog, carry);
+        identity_v<MS>(pv, carry);
       }
       // every lane takes its owner's carry (all lanes active: plain permutes)
 #pragma unroll
@@ -942,7 +1001,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
         int64_t fin[MS];
 #pragma unroll
         for (int s = 0; s < MS; ++s) fin[s] = carry[s];
-        combine_row<MS>(prog, fin, pre);
+        combine_v<MS>(pv, fin, pre);
         int64_t *o = pr.fin + i * (uint64_t)ns;
 #pragma unroll
         for (int s = 0; s < MS; ++s)
@@ -1083,10 +1142,36 @@ static void pr_launch(hipStream_t s, const Batch &b, const Program &prog, const 
   if (wpr == 1) {
     // LDS: table 12 + 8 MS bytes per entry, staging 2 KB per slot
     constexpr int LT = MS <= 6 ? 10 : 9;
-    if (pp.words <= kPrRegWords)
-      hipLaunchKernelGGL((k_pr_bucket<MS, LT, true>), dim3((unsigned)nb), dim3(kPbNT), 0, s, prog, p, pp, t, pb, pr, sc);
-    else
-      hipLaunchKernelGGL((k_pr_bucket<MS, LT, false>), dim3((unsigned)nb), dim3(kPbNT), 0, s, prog, p, pp, t, pb, pr, sc);
+    const dim3 gb((unsigned)nb), tb(kPbNT);
+    const uint64_t sig = program_sig(prog);
+    const bool reg = pp.words <= kPrRegWords;
+    // the common aggregate sets run with their slot program baked in
+    bool done = false;
+    if constexpr (MS == 6) {
+      if (reg && sig == kSigAllI) {
+        hipLaunchKernelGGL((k_pr_bucket<MS, LT, true, kSigAllI>), gb, tb, 0, s, prog, p, pp, t, pb, pr, sc);
+        done = true;
+      } else if (reg && sig == kSigAllF) {
+        hipLaunchKernelGGL((k_pr_bucket<MS, LT, true, kSigAllF>), gb, tb, 0, s, prog, p, pp, t, pb, pr, sc);
+        done = true;
+      }
+    }
+    if constexpr (MS == 2) {
+      if (reg && sig == kSigCnt) {
+        hipLaunchKernelGGL((k_pr_bucket<MS, LT, true, kSigCnt>), gb, tb, 0, s, prog, p, pp, t, pb, pr, sc);
+        done = true;
+      } else if (reg && sig == kSigCntSumI) {
+        hipLaunchKernelGGL((k_pr_bucket<MS, LT, true, kSigCntSumI>), gb, tb, 0, s, prog, p, pp, t, pb, pr, sc);
+        done = true;
+      } else if (reg && sig == kSigSumMaxI) {
+        hipLaunchKernelGGL((k_pr_bucket<MS, LT, true, kSigSumMaxI>), gb, tb, 0, s, prog, p, pp, t, pb, pr, sc);
+        done = true;
+      }
+    }
+    if (!done) {
+      if (reg) hipLaunchKernelGGL((k_pr_bucket<MS, LT, true, 0>), gb, tb, 0, s, prog, p, pp, t, pb, pr, sc);
+      else hipLaunchKernelGGL((k_pr_bucket<MS, LT, false, 0>), gb, tb, 0, s, prog, p, pp, t, pb, pr, sc);
+    }
     const uint64_t tiles = (b.n + kPrEmitRecs - 1) / kPrEmitRecs;
     hipLaunchKernelGGL(k_pr_emit1<MS>, dim3((unsigned)tiles), dim3(kPrEmitThreads), 0, s, b, prog, p, pb, pr, rec_wm,
                        seq, out, out_base, out_cap, sc);

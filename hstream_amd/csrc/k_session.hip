@@ -1267,13 +1267,60 @@ struct RecItems {
   }
 };
 
+// The same with the key's first two records in registers, loaded right after
+// the group record, beside the key-table probe: the sweeps of most keys (one
+// or two records in a batch) then wait on no record load. W <= 3 (ts, word 0,
+// one column); further records from memory.
+template <int W>
+struct RecItemsPf {
+  static_assert(W >= 2 && W <= 3, "RecItemsPf");
+  const uint64_t *rows;
+  uint32_t ra;
+  uint64_t t0, t1;           // ts of records ra, ra + 1
+  uint64_t v0[W - 1], v1[W - 1];  // their word 0 and column
+  __device__ void load(uint32_t a, uint32_t n) {
+    ra = a;
+    const uint64_t *p = rows + (uint64_t)a * W;
+    t0 = n > 0 ? p[0] : 0;
+    t1 = n > 1 ? p[W] : 0;
+#pragma unroll
+    for (int k = 0; k < W - 1; ++k) {
+      v0[k] = n > 0 ? p[1 + k] : 0;
+      v1[k] = n > 1 ? p[W + 1 + k] : 0;
+    }
+  }
+  __device__ int64_t start(uint32_t r) const {
+    return (int64_t)(r == ra ? t0 : r == ra + 1 ? t1 : rows[(uint64_t)r * W]);
+  }
+  __device__ int64_t end(uint32_t r) const { return start(r); }
+  template <int MS>
+  __device__ void aggs(const Program &prog, uint32_t r, int64_t (&a)[MS]) const {
+    if (r - ra < 2) {
+      uint64_t v[W - 1];
+#pragma unroll
+      for (int k = 0; k < W - 1; ++k) v[k] = r == ra ? v0[k] : v1[k];
+      ss_vw_elem<MS>(prog, v, a);
+    } else {
+      ss_vw_elem<MS>(prog, rows + (uint64_t)r * W + 1, a);
+    }
+  }
+};
+template <int W, bool PF = (W <= 3)>
+struct ApplyItems {
+  using T = RecItems<W>;
+};
+template <int W>
+struct ApplyItems<W, true> {
+  using T = RecItemsPf<W>;
+};
+
 // ---------------------------------------------------------------------------
 // k_ss_apply: one thread per key group (every key once per batch). Plan,
 // reserve the block's fresh lists in its arena region (all or nothing: a block
 // that cannot stays undone, the host compacts and runs the pass again), apply
 // and write the changelog rows of the fresh sessions.
 // ---------------------------------------------------------------------------
-constexpr int kApNT = 1024;  // large blocks: one arena / changelog reservation per 1024 keys
+constexpr int kApNT = 512;  // one arena / changelog reservation per 512 keys; two blocks per CU
 
 template <int MS, int W>
 __global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, Program prog, SessPart sp,
@@ -1290,7 +1337,7 @@ __global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, P
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint64_t g = g0 + threadIdx.x;
   const bool act = g < ng;
-  const RecItems<W> rs{sp.srec};
+  typename ApplyItems<W>::T rs{sp.srec};
   uint32_t key = 0, ra = 0, nr = 0, newcap = 0, M = 0, fresh = 0;
   uint64_t i0 = 0;
   int64_t sl = -1;
@@ -1302,6 +1349,7 @@ __global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, P
     key = gr.x;
     ra = gr.y;
     nr = gr.z;
+    if constexpr (W <= 3) rs.load(ra, nr);  // in flight during the probe
     sl = ss_find_or_insert(t, key, ins);
     if (sl < 0) err |= ERR_OOM;
     else {
