@@ -42,8 +42,9 @@ struct PrPart {
   uint32_t *ccnt;     // [chunks] partials of each chunk
   uint64_t *counter;  // partials allocated in this batch
   uint64_t *partial;  // scan partials
-  int64_t *fin;       // one-window ops (k_pr_bucket): [n][ns] each record's changelog state at its
-                      // partitioned position
+  int64_t *fin;       // one-window ops (k_pr_bucket): [n][ns] each record's changelog state, at its
+                      // arrival index
+  uint32_t *inv;      // one-window ops: [n] arrival index of each partitioned record (the scatter)
 };
 
 void launch_pr_count(hipStream_t s, const Batch &b, const TwParams &p, const TwTable &t, const int64_t *tprefix,

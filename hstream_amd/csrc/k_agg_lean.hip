@@ -532,7 +532,7 @@ __device__ inline int64_t tw_claim_seg(const TwTable &t, uint64_t g, uint32_t *c
   return -1;
 }
 
-template <int MS>
+template <int MS, uint64_t SIG>
 __global__ __launch_bounds__(1024) void k_seg_apply(Program prog, TwParams p, PartParams pp, TwTable t, PartBuffers pb,
                                                     OutCols out, uint64_t out_base, uint64_t out_cap, int lean,
                                                     DevScalars *sc) {
@@ -544,8 +544,8 @@ __global__ __launch_bounds__(1024) void k_seg_apply(Program prog, TwParams p, Pa
   uint64_t r0, r1;
   bool exclusive;
   if (!lean_chunk(pp, pb, b, r0, r1, exclusive)) return;  // uniform
-  const ProgRT pg(prog);
-  const int ns = prog.n_slots;
+  const ProgView<SIG> pg(prog);  // the common aggregate sets: slot ops baked in
+  const int ns = pg.n();
   const uint64_t pw = 1 + (uint64_t)ns;
   const uint32_t nseg = (uint32_t)pb.pane_info[2 * blockIdx.x];
   const uint32_t mine = pb.pane_cnt[blockIdx.x];
@@ -575,7 +575,7 @@ __global__ __launch_bounds__(1024) void k_seg_apply(Program prog, TwParams p, Pa
     total += s_tot[k];
   }
   bool has_last = false;
-  for (int s = 0; s < ns; ++s) has_last |= prog.slot_op[s] == S_LAST_SEQ;
+  for (int s = 0; s < ns; ++s) has_last |= pg.op(s) == S_LAST_SEQ;
   const bool direct = out.key != nullptr && pb.chunk_start[nb + 1] == 0 && sc->scratch[5] == 0 && !has_last;
   const uint64_t t0 = sc->scratch[1];  // touched entries the aggregation kernel appended itself
   if (threadIdx.x == 0 && blockIdx.x + 1 == nch) {
@@ -730,14 +730,22 @@ void launch_seg_apply(hipStream_t s, dim3 g, const Program &prog, const TwParams
   memset(&oc, 0, sizeof(oc));
   if (out) oc = *out;
   const int l = lean ? 1 : 0;
-  if (prog.n_slots <= 2)
-    hipLaunchKernelGGL((k_seg_apply<2>), g, dim3(1024), 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
+  const uint64_t sig = program_sig(prog);
+  const dim3 th(1024);
+  if (sig == kSigCntSumI)
+    hipLaunchKernelGGL((k_seg_apply<2, kSigCntSumI>), g, th, 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
+  else if (sig == kSigCntSumF)
+    hipLaunchKernelGGL((k_seg_apply<2, kSigCntSumF>), g, th, 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
+  else if (sig == kSigAllI)
+    hipLaunchKernelGGL((k_seg_apply<6, kSigAllI>), g, th, 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
+  else if (prog.n_slots <= 2)
+    hipLaunchKernelGGL((k_seg_apply<2, 0>), g, th, 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
   else if (prog.n_slots <= 4)
-    hipLaunchKernelGGL((k_seg_apply<4>), g, dim3(1024), 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
+    hipLaunchKernelGGL((k_seg_apply<4, 0>), g, th, 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
   else if (prog.n_slots <= 6)
-    hipLaunchKernelGGL((k_seg_apply<6>), g, dim3(1024), 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
+    hipLaunchKernelGGL((k_seg_apply<6, 0>), g, th, 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
   else
-    hipLaunchKernelGGL((k_seg_apply<8>), g, dim3(1024), 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
+    hipLaunchKernelGGL((k_seg_apply<8, 0>), g, th, 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
 }
 
 template <int W, uint64_t SIG>

@@ -907,6 +907,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
     // of the previous step (before its stores: the wait for them at the top
     // of this step then leaves the stores in flight)
     uint64_t nx0 = 0, nx1 = 0, nx2 = 0, nx3 = 0;
+    uint32_t nxa = 0;  // the record's arrival index (its changelog row's state goes there)
     auto fetch = [&](uint64_t ii) {
       const uint64_t *q = rec + ii * (uint64_t)W;
       const bool f = ii < s1;
@@ -914,12 +915,14 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
       nx1 = (f && W > 1) ? q[1] : 0ull;
       nx2 = (f && W > 2) ? q[2] : 0ull;
       nx3 = (f && W > 3) ? q[3] : 0ull;
+      nxa = f ? pb.inv[ii] : 0u;
     };
     fetch(s0 + threadIdx.x);
     for (uint64_t base = s0; base < s1; base += kPbNT) {
       const uint64_t i = base + threadIdx.x;
       const bool in = i < s1;
       const PrRecRegs<REG> v{nx0, nx1, nx2, nx3, rec + i * (uint64_t)W, pk, C};
+      const uint32_t arrival = nxa;
       fetch(i + kPbNT);
       uint32_t h = 0;
       int64_t pre[MS];
@@ -1002,7 +1005,9 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
 #pragma unroll
         for (int s = 0; s < MS; ++s) fin[s] = carry[s];
         combine_v<MS>(pv, fin, pre);
-        int64_t *o = pr.fin + i * (uint64_t)ns;
+        // at the record's arrival index: k_pr_emit1 then streams the states in
+        // arrival order (the scattered stores cost the step no wait)
+        int64_t *o = pr.fin + (uint64_t)arrival * (uint64_t)ns;
 #pragma unroll
         for (int s = 0; s < MS; ++s)
           if (s < ns) o[s] = fin[s];
@@ -1061,7 +1066,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
 
 // Rows of one-window ops in arrival order: the record's window as the
 // partition computed it, its state from k_pr_bucket (pr.fin at the record's
-// partitioned position). Rounds of consecutive records: coalesced lanes.
+// arrival index). Rounds of consecutive records: every access coalesced.
 template <int MS>
 __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit1(Batch bt, Program prog, TwParams p, PartBuffers pb,
                                                              PrPart pr, const int64_t *__restrict__ rec_wm,
@@ -1107,14 +1112,13 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit1(Batch bt, Program p
     lds_barrier();
     base += tot;
     if (!n) continue;
-    const uint64_t pos = pr.pos[i];
     const uint64_t ob = out_base + o;
-    if (pos >= pb.n_cap || ob >= out_cap) {  // cannot happen: the scatter placed every record with a window
+    if (ob >= out_cap) {  // cannot happen: the output holds the batch's rows
       err |= ERR_OOM;
       continue;
     }
     int64_t R[MS];
-    const int64_t *f = pr.fin + pos * (uint64_t)ns;
+    const int64_t *f = pr.fin + i * (uint64_t)ns;  // k_pr_bucket left it at the arrival index
 #pragma unroll
     for (int s = 0; s < MS; ++s) R[s] = s < ns ? f[s] : 0;
     out.key[ob] = key;

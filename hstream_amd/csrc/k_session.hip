@@ -1,5 +1,6 @@
 // gfx950 kernels for session windows (SessionWindowedStream.hs:74-118 over the
 // session store of Store.hs:177-272). Layout and paths: hsg_session.h.
+#include "hsg_agg.h"
 #include "hsg_dev.h"
 #include "hsg_perrecord.h"
 #include "hsg_session.h"
@@ -611,14 +612,14 @@ void launch_ss_pscatter(hipStream_t s, const Batch &b, int np_log2, int bshift, 
 constexpr int kMgTail = 2;  // resident sessions a key may rewrite in place (held in registers)
 
 // contribution of one partitioned record to the slots (identity when absent)
-template <int MS>
-__device__ inline void ss_rec_elem(const Program &prog, const uint64_t *rec, int64_t (&e)[MS]) {
+template <int MS, class PV>
+__device__ __attribute__((always_inline)) inline void ss_rec_elem(const PV &prog, const uint64_t *rec, int64_t (&e)[MS]) {
   const uint64_t vb = rec[0] >> 32;
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
     e[s] = 0;
-    if (s >= prog.n_slots) continue;
-    const int op = prog.slot_op[s], c = prog.slot_col[s];
+    if (s >= prog.n()) continue;
+    const int op = prog.op(s), c = prog.col(s);
     if (op == S_CNT_ALL) {
       e[s] = 1;
       continue;
@@ -637,11 +638,11 @@ __device__ inline void ss_rec_elem(const Program &prog, const uint64_t *rec, int
   }
 }
 
-template <int MS>
-__device__ inline void acc_row(const Program &prog, int64_t (&a)[MS], const int64_t (&e)[MS]) {
+template <int MS, class PV>
+__device__ __attribute__((always_inline)) inline void acc_row(const PV &prog, int64_t (&a)[MS], const int64_t (&e)[MS]) {
 #pragma unroll
   for (int s = 0; s < MS; ++s)
-    if (s < prog.n_slots) a[s] = slot_combine(prog.slot_op[s], a[s], e[s]);
+    if (s < prog.n()) a[s] = slot_combine(prog.op(s), a[s], e[s]);
 }
 
 // One session of the sweep: start, end, aggregates, and whether a batch run
@@ -661,11 +662,13 @@ struct EmitSink {
   uint64_t pos;   // next row; ~0 = count only
   uint32_t key;
   uint32_t n;     // fresh sessions seen
+  const Program *rp;  // the op's program (output columns); unused when counting
 };
 
 template <int MS>
-__device__ inline void mg_emit(const Program &prog, EmitSink &k, const MgSess<MS> &c) {
+__device__ __attribute__((always_inline)) inline void mg_emit(EmitSink &k, const MgSess<MS> &c) {
   if (k.pos != ~0ull) {
+    const Program &prog = *k.rp;
     const uint64_t o = k.pos++;
     k.out.key[o] = k.key;
     k.out.ws[o] = c.s;
@@ -679,9 +682,17 @@ __device__ inline void mg_emit(const Program &prog, EmitSink &k, const MgSess<MS
 }
 
 template <int MS>
-__device__ inline MgSess<MS> pick_tail(const MgSess<MS> (&tail)[kMgTail], uint64_t k) {
-  MgSess<MS> x = tail[0];
-  if (k == 1) x = tail[1];
+__device__ __attribute__((always_inline)) inline MgSess<MS> pick_tail(const MgSess<MS> (&tail)[kMgTail], uint64_t k) {
+  // field-wise selects (a whole-struct pick by a runtime index puts the array on the stack)
+  static_assert(kMgTail == 2, "pick_tail");
+  const bool one = k == 1;
+  MgSess<MS> x;
+  x.s = one ? tail[1].s : tail[0].s;
+  x.e = one ? tail[1].e : tail[0].e;
+#pragma unroll
+  for (int s = 0; s < MS; ++s) x.a[s] = one ? tail[1].a[s] : tail[0].a[s];
+  x.stamp = one ? tail[1].stamp : tail[0].stamp;
+  x.fresh = one ? tail[1].fresh : tail[0].fresh;
   return x;
 }
 
@@ -692,8 +703,8 @@ struct RunsGlobal {
   int ns;
   __device__ int64_t start(uint32_t r) const { return (int64_t)runs[(uint64_t)r * rstride]; }
   __device__ int64_t end(uint32_t r) const { return (int64_t)runs[(uint64_t)r * rstride + 1]; }
-  template <int MS>
-  __device__ void aggs(const Program &, uint32_t r, int64_t (&a)[MS]) const {
+  template <int MS, class PV>
+  __device__ void aggs(const PV &, uint32_t r, int64_t (&a)[MS]) const {
     const uint64_t *q = runs + (uint64_t)r * rstride + 2;
 #pragma unroll
     for (int s = 0; s < MS; ++s) a[s] = s < ns ? (int64_t)q[s] : 0;
@@ -704,12 +715,12 @@ struct RunsGlobal {
 // `tail_regs`: then len - i0 <= kMgTail) and its runs [r0, r1), in start
 // order; items closer than gap merge (next.start - running end <= gap). With
 // APPLY the merged sessions are written at dst + i0 + k, else only counted.
-template <int MS, bool APPLY, class RS>
-__device__ inline uint32_t mg_sweep(const Program &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t r0,
+template <int MS, bool APPLY, class RS, class PV>
+__device__ __attribute__((always_inline)) inline uint32_t mg_sweep(const PV &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t r0,
                                     uint32_t r1, uint64_t off, uint64_t i0, uint64_t len, bool tail_regs,
                                     const MgSess<MS> (&tail)[kMgTail], uint64_t dst, uint32_t batch_id,
                                     EmitSink *sink = nullptr, SessKey *mirror = nullptr) {
-  const int ns = prog.n_slots;
+  const int ns = prog.n();
   uint64_t j = i0;   // next resident
   uint32_t r = r0;   // next run
   uint32_t k = 0;    // merged sessions so far
@@ -754,7 +765,7 @@ __device__ inline uint32_t mg_sweep(const Program &prog, const SessTable &t, int
     } else {
       if (have) {
         if (APPLY) ss_store<MS>(t, dst + i0 + k, cur.s, cur.e, cur.fresh ? batch_id : cur.stamp, cur.a);
-        if (sink && cur.fresh) mg_emit<MS>(prog, *sink, cur);
+        if (sink && cur.fresh) mg_emit<MS>(*sink, cur);
         ++k;
       }
       cur = it;
@@ -763,10 +774,10 @@ __device__ inline uint32_t mg_sweep(const Program &prog, const SessTable &t, int
   }
   if (have) {
     if (APPLY) ss_store<MS>(t, dst + i0 + k, cur.s, cur.e, cur.fresh ? batch_id : cur.stamp, cur.a);
-    if (sink && cur.fresh) mg_emit<MS>(prog, *sink, cur);
+    if (sink && cur.fresh) mg_emit<MS>(*sink, cur);
     ++k;
     if (mirror) {  // the list's new last session (the sweep runs to its end) into the entry's mirror
-      const bool m = prog.n_slots <= kSessMirrorSlots;
+      const bool m = prog.n() <= kSessMirrorSlots;
       if (m) {
         mirror->ms = cur.s;
         mirror->me = cur.e;
@@ -781,7 +792,7 @@ __device__ inline uint32_t mg_sweep(const Program &prog, const SessTable &t, int
 
 // first resident session with end >= lo: galloping back from the end (near-
 // sorted arrivals touch the last session or none), then binary search
-__device__ inline uint64_t mg_first_end_ge(const SessTable &t, uint64_t off, uint64_t len, int64_t lo) {
+__device__ __attribute__((always_inline)) inline uint64_t mg_first_end_ge(const SessTable &t, uint64_t off, uint64_t len, int64_t lo) {
   uint64_t hi = len, step = 1;
   while (hi > 0) {
     const uint64_t probe = hi > step ? hi - step : 0;
@@ -807,15 +818,15 @@ __device__ inline uint64_t mg_first_end_ge(const SessTable &t, uint64_t off, uin
 // start, so no resident but the last can be reached, the one before ending
 // more than gap before the last starts; the last is touched iff the first
 // run comes within gap of its end).
-template <int MS>
-__device__ inline void mg_mirror_tail(const Program &prog, const SessKey &e, uint32_t batch_id,
+template <int MS, class PV>
+__device__ __attribute__((always_inline)) inline void mg_mirror_tail(const PV &prog, const SessKey &e, uint32_t batch_id,
                                       MgSess<MS> (&tail)[kMgTail]);
 template <class RS>
 __device__ inline bool mg_fast(const RS &rs, uint32_t ra, const SessKey &e) {
   return e.mvalid && e.len > 0 && rs.start(ra) >= e.ms;
 }
-template <int MS, class RS>
-__device__ inline void mg_plan(const Program &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t ra,
+template <int MS, class RS, class PV>
+__device__ __attribute__((always_inline)) inline void mg_plan(const PV &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t ra,
                                uint32_t rb, const SessKey &e, bool fast, uint32_t batch_id, uint64_t &i0, uint32_t &M,
                                uint32_t &newcap, uint32_t *fresh = nullptr) {
   const int64_t lo = (int64_t)((uint64_t)rs.start(ra) - (uint64_t)gap);
@@ -826,7 +837,7 @@ __device__ inline void mg_plan(const Program &prog, const SessTable &t, int64_t 
   } else {
     i0 = mg_first_end_ge(t, e.off, e.len, lo);
   }
-  EmitSink cnt{OutCols{}, ~0ull, 0, 0};
+  EmitSink cnt{OutCols{}, ~0ull, 0, 0, nullptr};
   M = mg_sweep<MS, false>(prog, t, gap, rs, ra, rb, e.off, i0, e.len, fast, tail, 0, 0, &cnt);
   if (fresh) *fresh = cnt.n;
   // in place when the merged list fits and the rewritten tail fits the
@@ -835,8 +846,8 @@ __device__ inline void mg_plan(const Program &prog, const SessTable &t, int64_t 
 }
 
 // The key's last session from its entry's mirror (valid when e.mvalid).
-template <int MS>
-__device__ inline void mg_mirror_tail(const Program &prog, const SessKey &e, uint32_t batch_id,
+template <int MS, class PV>
+__device__ __attribute__((always_inline)) inline void mg_mirror_tail(const PV &prog, const SessKey &e, uint32_t batch_id,
                                       MgSess<MS> (&tail)[kMgTail]) {
 #pragma unroll
   for (int k = 0; k < kMgTail; ++k) {
@@ -849,7 +860,7 @@ __device__ inline void mg_mirror_tail(const Program &prog, const SessKey &e, uin
   tail[0].s = e.ms;
   tail[0].e = e.me;
 #pragma unroll
-  for (int s = 0; s < MS; ++s) tail[0].a[s] = (s < kSessMirrorSlots && s < prog.n_slots) ? e.ma[s] : 0;
+  for (int s = 0; s < MS; ++s) tail[0].a[s] = (s < kSessMirrorSlots && s < prog.n()) ? e.ma[s] : 0;
 }
 
 // The entry after a merge (its mirror was written by the sweep).
@@ -862,11 +873,11 @@ __device__ inline void ss_entry_commit(SessKey &ke, uint64_t off, uint32_t len, 
 // Apply a planned key: the list at dst (fresh rows: the prefix copied first).
 // The rewritten residents come from registers: the mirror (fast) or the rows
 // loaded here (in place), else from the old list (relocated).
-template <int MS, class RS>
-__device__ inline void mg_apply(const Program &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t ra,
+template <int MS, class RS, class PV>
+__device__ __attribute__((always_inline)) inline void mg_apply(const PV &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t ra,
                                 uint32_t rb, const SessKey &e, bool fast, uint64_t i0, uint64_t dst, bool reloc,
                                 uint32_t batch_id, EmitSink *sink = nullptr, SessKey *mirror = nullptr) {
-  const int ns = prog.n_slots;
+  const int ns = prog.n();
   if (reloc)
     for (uint64_t k = 0; k < i0; ++k) ss_copy(t, dst + k, t, e.off + k);
   MgSess<MS> tail[kMgTail];
@@ -942,14 +953,14 @@ __device__ inline int64_t ts_of(uint64_t img) { return (int64_t)(img ^ 0x8000000
 
 // contribution of one record (word 0 and columns in `v`, as in the LDS copy:
 // v[0] = key | valid bits << 32, v[1 + c] = column c)
-template <int MS>
-__device__ inline void ss_vw_elem(const Program &prog, const uint64_t *v, int64_t (&e)[MS]) {
+template <int MS, class PV>
+__device__ __attribute__((always_inline)) inline void ss_vw_elem(const PV &prog, const uint64_t *v, int64_t (&e)[MS]) {
   const uint64_t vb = v[0] >> 32;
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
     e[s] = 0;
-    if (s >= prog.n_slots) continue;
-    const int op = prog.slot_op[s], c = prog.slot_col[s];
+    if (s >= prog.n()) continue;
+    const int op = prog.op(s), c = prog.col(s);
     if (op == S_CNT_ALL) {
       e[s] = 1;
       continue;
@@ -1261,8 +1272,8 @@ struct RecItems {
   const uint64_t *rows;  // [n][W]: ts, word 0, columns
   __device__ int64_t start(uint32_t r) const { return (int64_t)rows[(uint64_t)r * W]; }
   __device__ int64_t end(uint32_t r) const { return (int64_t)rows[(uint64_t)r * W]; }
-  template <int MS>
-  __device__ void aggs(const Program &prog, uint32_t r, int64_t (&a)[MS]) const {
+  template <int MS, class PV>
+  __device__ void aggs(const PV &prog, uint32_t r, int64_t (&a)[MS]) const {
     ss_vw_elem<MS>(prog, rows + (uint64_t)r * W + 1, a);
   }
 };
@@ -1293,8 +1304,8 @@ struct RecItemsPf {
     return (int64_t)(r == ra ? t0 : r == ra + 1 ? t1 : rows[(uint64_t)r * W]);
   }
   __device__ int64_t end(uint32_t r) const { return start(r); }
-  template <int MS>
-  __device__ void aggs(const Program &prog, uint32_t r, int64_t (&a)[MS]) const {
+  template <int MS, class PV>
+  __device__ void aggs(const PV &prog, uint32_t r, int64_t (&a)[MS]) const {
     if (r - ra < 2) {
       uint64_t v[W - 1];
 #pragma unroll
@@ -1322,9 +1333,10 @@ struct ApplyItems<W, true> {
 // ---------------------------------------------------------------------------
 constexpr int kApNT = 512;  // one arena / changelog reservation per 512 keys; two blocks per CU
 
-template <int MS, int W>
+template <int MS, int W, uint64_t SIG>
 __global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, Program prog, SessPart sp,
                                                     OutCols out, uint64_t out_base, DevScalars *sc) {
+  const ProgView<SIG> pv(prog);  // the common aggregate sets: slot ops baked in
   __shared__ uint64_t ws[kApNT / 64];
   __shared__ uint64_t we[kApNT / 64];
   __shared__ uint64_t sbase, sobase;
@@ -1356,7 +1368,7 @@ __global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, P
       if (!ins) e = ss_load_entry(&t.kt[sl]);
       // near-sorted arrivals: planned from the entry's mirror, no list read
       fast = mg_fast(rs, ra, e);
-      mg_plan<MS>(prog, t, p.gap, rs, ra, ra + nr, e, fast, p.batch_id, i0, M, newcap, &fresh);
+      mg_plan<MS>(pv, t, p.gap, rs, ra, ra + nr, e, fast, p.batch_id, i0, M, newcap, &fresh);
     }
   }
   const bool live = act && sl >= 0;
@@ -1402,8 +1414,9 @@ __global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, P
   if (live) {
     const bool reloc = newcap != 0;
     const uint64_t dst = reloc ? sbase + before + incl - need : e.off;
-    EmitSink sink{out, p.emit_mode == HSG_EMIT_PER_BATCH ? out_base + sobase + ebefore + einc - nem : ~0ull, key, 0};
-    mg_apply<MS>(prog, t, p.gap, rs, ra, ra + nr, e, fast, i0, dst, reloc, p.batch_id, &sink, &t.kt[sl]);
+    EmitSink sink{out, p.emit_mode == HSG_EMIT_PER_BATCH ? out_base + sobase + ebefore + einc - nem : ~0ull, key, 0,
+                  &prog};
+    mg_apply<MS>(pv, t, p.gap, rs, ra, ra + nr, e, fast, i0, dst, reloc, p.batch_id, &sink, &t.kt[sl]);
     ss_entry_commit(t.kt[sl], dst, (uint32_t)(i0 + M), reloc ? newcap : 0u);
     ld = (int64_t)M - (int64_t)(e.len - i0);
   }
@@ -1413,26 +1426,33 @@ __global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, P
   if (threadIdx.x == 0) sp.done[blk] = 1;
 }
 
-template <int MS>
+template <int MS, uint64_t SIG>
 static void apply_launch_w(hipStream_t s, int words, dim3 g, const SessParams &p, const SessTable &t,
                            const Program &prog, const SessPart &sp, OutCols out, uint64_t out_base, DevScalars *sc) {
   const dim3 th(kApNT);
   switch (words) {
-    case 2: hipLaunchKernelGGL((k_ss_apply<MS, 2>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
-    case 3: hipLaunchKernelGGL((k_ss_apply<MS, 3>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
-    case 4: hipLaunchKernelGGL((k_ss_apply<MS, 4>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
-    case 5: hipLaunchKernelGGL((k_ss_apply<MS, 5>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
-    case 6: hipLaunchKernelGGL((k_ss_apply<MS, 6>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
-    default: hipLaunchKernelGGL((k_ss_apply<MS, kSessMaxWords>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 2: hipLaunchKernelGGL((k_ss_apply<MS, 2, SIG>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 3: hipLaunchKernelGGL((k_ss_apply<MS, 3, SIG>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 4: hipLaunchKernelGGL((k_ss_apply<MS, 4, 0>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 5: hipLaunchKernelGGL((k_ss_apply<MS, 5, 0>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 6: hipLaunchKernelGGL((k_ss_apply<MS, 6, 0>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    default: hipLaunchKernelGGL((k_ss_apply<MS, kSessMaxWords, 0>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
   }
 }
 
 void launch_ss_apply(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, uint64_t n_bound,
                      int words, const SessPart &sp, OutCols out, uint64_t out_base, DevScalars *sc) {
   const dim3 g((unsigned)((n_bound + kApNT - 1) / kApNT + 1));
-  if (prog.n_slots <= 2) apply_launch_w<2>(s, words, g, p, t, prog, sp, out, out_base, sc);
-  else if (prog.n_slots <= 4) apply_launch_w<4>(s, words, g, p, t, prog, sp, out, out_base, sc);
-  else apply_launch_w<8>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  // the common aggregate sets of a session GROUP BY (one column or none) with
+  // their slot program baked in; every other program reads it at run time
+  const uint64_t sig = program_sig(prog);
+  if (sig == kSigCntSumI) apply_launch_w<2, kSigCntSumI>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  else if (sig == kSigCntSumF) apply_launch_w<2, kSigCntSumF>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  else if (sig == kSigCnt) apply_launch_w<2, kSigCnt>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  else if (sig == kSigSumMaxI) apply_launch_w<2, kSigSumMaxI>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  else if (prog.n_slots <= 2) apply_launch_w<2, 0>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  else if (prog.n_slots <= 4) apply_launch_w<4, 0>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  else apply_launch_w<8, 0>(s, words, g, p, t, prog, sp, out, out_base, sc);
 }
 
 // ---------------------------------------------------------------------------
@@ -1468,9 +1488,10 @@ struct RunsLds {
   const uint64_t *recs;
   __device__ int64_t start(uint32_t r) const { return L->rs[r]; }
   __device__ int64_t end(uint32_t r) const { return L->re[r]; }
-  template <int MS>
-  __device__ void aggs(const Program &prog, uint32_t r, int64_t (&a)[MS]) const {
-    identity_row<MS>(prog, a);
+  template <int MS, class PV>
+  __device__ void aggs(const PV &prog, uint32_t r, int64_t (&a)[MS]) const {
+#pragma unroll
+    for (int s = 0; s < MS; ++s) a[s] = s < prog.n() ? slot_identity_dev(prog.op(s)) : 0;
     for (uint32_t q = L->rbeg[r]; q < L->rbeg[r + 1]; ++q) {
       int64_t e[MS];
       ss_rec_elem<MS>(prog, recs + (uint64_t)L->idx[q] * W, e);
@@ -1654,7 +1675,7 @@ __global__ __launch_bounds__(kMgNT) void k_ss_merge_big(SessParams p, SessTable 
       gslot[u] = sl;
       ++nt;
       if (!ins) ge[u] = t.kt[sl];
-      mg_plan<MS>(prog, t, p.gap, rsrc, ra, rb, ge[u], false, p.batch_id, gi0[u], gM[u], gcap[u]);
+      mg_plan<MS>(ProgRT(prog), t, p.gap, rsrc, ra, rb, ge[u], false, p.batch_id, gi0[u], gM[u], gcap[u]);
       need += gcap[u];
     }
     uint64_t tneed;
@@ -1695,7 +1716,7 @@ __global__ __launch_bounds__(kMgNT) void k_ss_merge_big(SessParams p, SessTable 
         my_alloc += gcap[u];
       }
       SessKey &ke = t.kt[gslot[u]];
-      mg_apply<MS>(prog, t, p.gap, rsrc, ra, rb, ge[u], false, gi0[u], dst, reloc, p.batch_id, nullptr, &ke);
+      mg_apply<MS>(ProgRT(prog), t, p.gap, rsrc, ra, rb, ge[u], false, gi0[u], dst, reloc, p.batch_id, nullptr, &ke);
       ss_entry_commit(ke, dst, (uint32_t)(gi0[u] + gM[u]), reloc ? gcap[u] : 0u);
       atomicMin((unsigned long long *)&ke.emark, (unsigned long long)(bmark | gi0[u]));
       sp.touched[tp++] = (uint32_t)gslot[u];
