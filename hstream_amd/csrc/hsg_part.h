@@ -49,8 +49,6 @@ struct PartBuffers {
                           // pairs of each tile, written by the histogram pass
   uint32_t *pos;          // per-record changelog only (else null): [n] partitioned index of each
                           // arrival-order record, written by the scatter
-  uint32_t *inv;          // per-record changelog of one-window ops (else null): [n] arrival index of
-                          // each partitioned record, written by the scatter
 };
 
 struct PartParams {

@@ -43,8 +43,7 @@ struct PrPart {
   uint64_t *counter;  // partials allocated in this batch
   uint64_t *partial;  // scan partials
   int64_t *fin;       // one-window ops (k_pr_bucket): [n][ns] each record's changelog state, at its
-                      // arrival index
-  uint32_t *inv;      // one-window ops: [n] arrival index of each partitioned record (the scatter)
+                      // partitioned position
 };
 
 void launch_pr_count(hipStream_t s, const Batch &b, const TwParams &p, const TwTable &t, const int64_t *tprefix,

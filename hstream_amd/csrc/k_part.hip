@@ -482,7 +482,6 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
       const uint64_t dest = (uint64_t)goff[bk] + (q - lstart[bk]);
       uint64_t v;
       if (w == 0 && pb.pos) pb.pos[i] = (uint32_t)dest;
-      if (w == 0 && pb.inv) pb.inv[dest] = (uint32_t)i;
       const uint32_t wc = packed ? w + 1 : w;  // word index in the wide layout (packed: 0 is both headers)
       if (w == 0 && packed) {
         uint64_t vb = 0;
@@ -647,7 +646,6 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
                                                           DevScalars *sc) {
   __shared__ uint8_t wcnt[STABLE ? kPW : 1][1 << kPartMaxLog2];
   __shared__ uint64_t stage[T * W];
-  __shared__ uint16_t sj[STABLE ? T : 1];  // stable (per-record): each staged record's in-tile index
   __shared__ uint32_t cnt2[1 << (kPartMaxLog2 - 1)];  // two u16 counts per word, then the u16 run starts
   __shared__ uint32_t cursor[1 << kPartMaxLog2];      // the row's next output slot per bucket
   __shared__ uint32_t swave[kPNT / 64];
@@ -744,7 +742,6 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
       if (slot[r] == ~0u) continue;
       if (pb.pos) pb.pos[base + (uint64_t)r * kPNT + threadIdx.x] = cursor[slot[r] >> 16] + (slot[r] & 0xFFFFu);
       const uint32_t q = lstart[slot[r] >> 16] + (slot[r] & 0xFFFFu);
-      if constexpr (STABLE) sj[q] = (uint16_t)(r * kPNT + threadIdx.x);
       stage[q * W] = (uint64_t)ts[r];
       if (W == 2) stage[q * W + 1] = col[r];
     }
@@ -755,8 +752,6 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
       const uint64_t h = stage[q * W];
       const uint32_t bk = bucket_of((uint32_t)h, pp.np_log2, pp.bshift);
       const uint64_t dest = (uint64_t)cursor[bk] + (q - lstart[bk]);
-      if constexpr (STABLE)
-        if (pb.inv) pb.inv[dest] = (uint32_t)(base + sj[q]);
       if (W == 2) {
         const uint64_t cc = stage[q * W + 1];
         *(ulonglong2 *)(pb.rec + dest * 2) = make_ulonglong2(h, cc);

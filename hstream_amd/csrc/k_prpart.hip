@@ -907,7 +907,6 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
     // of the previous step (before its stores: the wait for them at the top
     // of this step then leaves the stores in flight)
     uint64_t nx0 = 0, nx1 = 0, nx2 = 0, nx3 = 0;
-    uint32_t nxa = 0;  // the record's arrival index (its changelog row's state goes there)
     auto fetch = [&](uint64_t ii) {
       const uint64_t *q = rec + ii * (uint64_t)W;
       const bool f = ii < s1;
@@ -915,14 +914,12 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
       nx1 = (f && W > 1) ? q[1] : 0ull;
       nx2 = (f && W > 2) ? q[2] : 0ull;
       nx3 = (f && W > 3) ? q[3] : 0ull;
-      nxa = f ? pb.inv[ii] : 0u;
     };
     fetch(s0 + threadIdx.x);
     for (uint64_t base = s0; base < s1; base += kPbNT) {
       const uint64_t i = base + threadIdx.x;
       const bool in = i < s1;
       const PrRecRegs<REG> v{nx0, nx1, nx2, nx3, rec + i * (uint64_t)W, pk, C};
-      const uint32_t arrival = nxa;
       fetch(i + kPbNT);
       uint32_t h = 0;
       int64_t pre[MS];
@@ -1005,9 +1002,8 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
 #pragma unroll
         for (int s = 0; s < MS; ++s) fin[s] = carry[s];
         combine_v<MS>(pv, fin, pre);
-        // at the record's arrival index: k_pr_emit1 then streams the states in
-        // arrival order (the scattered stores cost the step no wait)
-        int64_t *o = pr.fin + (uint64_t)arrival * (uint64_t)ns;
+        // at the record's partitioned position: consecutive lanes, consecutive rows
+        int64_t *o = pr.fin + i * (uint64_t)ns;
 #pragma unroll
         for (int s = 0; s < MS; ++s)
           if (s < ns) o[s] = fin[s];
@@ -1066,13 +1062,20 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
 
 // Rows of one-window ops in arrival order: the record's window as the
 // partition computed it, its state from k_pr_bucket (pr.fin at the record's
-// arrival index). Rounds of consecutive records: every access coalesced.
+// partitioned position pr.pos). Each thread carries kE1 records of
+// consecutive rounds (record = round base + thread: coalesced lanes), their
+// state gathers issued together: kE1 row loads in flight per thread.
+constexpr int kE1 = 4;
+constexpr int kE1NT = 256;                         // threads of k_pr_emit1 (registers for kE1 records each)
+constexpr int kE1Rounds = kPrEmitRecs / kE1NT;
+static_assert(kE1Rounds % kE1 == 0 && kE1Rounds * kE1NT == kPrEmitRecs, "emit rounds");
+
 template <int MS>
-__global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit1(Batch bt, Program prog, TwParams p, PartBuffers pb,
+__global__ __launch_bounds__(kE1NT) void k_pr_emit1(Batch bt, Program prog, TwParams p, PartBuffers pb,
                                                              PrPart pr, const int64_t *__restrict__ rec_wm,
                                                              const int64_t *__restrict__ seq, OutCols out,
                                                              uint64_t out_base, uint64_t out_cap, DevScalars *sc) {
-  __shared__ uint32_t sw[kPrEmitThreads / 64];
+  __shared__ uint32_t sw[kE1][kE1NT / 64];
   if (sc->redo) return;  // uniform
   const int64_t k_epoch = sc->k_epoch;
   const int64_t *wm = rec_wm ? rec_wm : (sc->no_late ? nullptr : pb.wm);
@@ -1080,60 +1083,88 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit1(Batch bt, Program p
   const int ns = prog.n_slots;
   uint32_t err = 0;
   uint64_t base = pr.tpoff[(uint64_t)blockIdx.x * (kPrEmitRecs / kPartTileRecs)];
-  for (int rd = 0; rd < kPrEmitRounds; ++rd) {
-    const uint64_t i = (uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)rd * kPrEmitThreads + threadIdx.x;
-    if ((uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)rd * kPrEmitThreads >= bt.n) break;  // uniform
-    uint32_t a = 0, n = 0, key = HSG_KEY_NONE;
-    if (i < bt.n) {
-      key = bt.key[i];
-      const int64_t ts = bt.ts[i];
-      if (key != HSG_KEY_NONE) {  // the window the partition passes accepted (k_part.hip part_record)
-        uint64_t k_lo, k_hi;
-        if (record_windows(p, ts, k_lo, k_hi)) {
-          const int64_t w = wm ? wm[i] : INT64_MIN;
-          if (window_accepted(p, k_lo, w)) {
-            const int64_t lo = (int64_t)k_lo - k_epoch;
-            if (lo >= 0 && lo <= 0xFFFFFFFFll) {
-              a = (uint32_t)lo;
-              n = 1;
-            }
+  for (int rd0 = 0; rd0 < kE1Rounds; rd0 += kE1) {
+    if ((uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)rd0 * kE1NT >= bt.n) break;  // uniform
+    uint32_t a[kE1], n[kE1], key[kE1];
+    uint64_t i[kE1];
+#pragma unroll
+    for (int u = 0; u < kE1; ++u) {
+      i[u] = (uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)(rd0 + u) * kE1NT + threadIdx.x;
+      a[u] = 0;
+      n[u] = 0;
+      key[u] = i[u] < bt.n ? bt.key[i[u]] : HSG_KEY_NONE;
+    }
+#pragma unroll
+    for (int u = 0; u < kE1; ++u) {
+      if (key[u] == HSG_KEY_NONE) continue;  // the window the partition passes accepted (k_part.hip part_record)
+      const int64_t ts = bt.ts[i[u]];
+      uint64_t k_lo, k_hi;
+      if (record_windows(p, ts, k_lo, k_hi)) {
+        const int64_t w = wm ? wm[i[u]] : INT64_MIN;
+        if (window_accepted(p, k_lo, w)) {
+          const int64_t lo = (int64_t)k_lo - k_epoch;
+          if (lo >= 0 && lo <= 0xFFFFFFFFll) {
+            a[u] = (uint32_t)lo;
+            n[u] = 1;
           }
         }
       }
     }
-    const uint32_t incl = (uint32_t)wave_incl_sum((uint64_t)n);
-    if (lane == 63) sw[wv] = incl;
-    lds_barrier();
-    uint64_t o = base + incl - n, tot = 0;
-    for (int k = 0; k < kPrEmitThreads / 64; ++k) {
-      o += k < wv ? sw[k] : 0u;
-      tot += sw[k];
-    }
-    lds_barrier();
-    base += tot;
-    if (!n) continue;
-    const uint64_t ob = out_base + o;
-    if (ob >= out_cap) {  // cannot happen: the output holds the batch's rows
-      err |= ERR_OOM;
-      continue;
-    }
-    int64_t R[MS];
-    const int64_t *f = pr.fin + i * (uint64_t)ns;  // k_pr_bucket left it at the arrival index
+    // the states, every gather in flight at once
+    int64_t R[kE1][MS];
 #pragma unroll
-    for (int s = 0; s < MS; ++s) R[s] = s < ns ? f[s] : 0;
-    out.key[ob] = key;
-    int64_t ws = 0, we = 0;
-    if (p.kind != HSG_UNWINDOWED) {
-      const int64_t k = k_epoch + (int64_t)a;
-      ws = (int64_t)((uint64_t)k * (uint64_t)p.adv);
-      we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
-    }
-    out.ws[ob] = ws;
-    out.we[ob] = we;
-    out.src[ob] = seq ? seq[i] : (int64_t)(p.rec_base + i);
+    for (int u = 0; u < kE1; ++u) {
 #pragma unroll
-    for (int jj = 0; jj < kMaxAggs; ++jj)
-      if (jj < prog.n_out) out.agg[jj][ob] = out_value_reg<MS>(prog, jj, R);
+      for (int s = 0; s < MS; ++s) R[u][s] = 0;
+      if (!n[u]) continue;
+      const uint64_t pos = pr.pos[i[u]];
+      const int64_t *f = pr.fin + (pos < pb.n_cap ? pos : 0) * (uint64_t)ns;
+#pragma unroll
+      for (int s = 0; s < MS; ++s)
+        if (s < ns) R[u][s] = f[s];
+    }
+    // exclusive prefixes of the rounds' rows in arrival order
+    uint64_t o[kE1];
+#pragma unroll
+    for (int u = 0; u < kE1; ++u) {
+      const uint32_t incl = (uint32_t)wave_incl_sum((uint64_t)n[u]);
+      if (lane == 63) sw[u][wv] = incl;
+      o[u] = incl - n[u];
+    }
+    lds_barrier();
+#pragma unroll
+    for (int u = 0; u < kE1; ++u) {
+      uint64_t before = 0, tot = 0;
+      for (int k = 0; k < kE1NT / 64; ++k) {
+        before += k < wv ? sw[u][k] : 0u;
+        tot += sw[u][k];
+      }
+      o[u] += base + before;
+      base += tot;
+    }
+    lds_barrier();  // sw is rewritten by the next rounds
+#pragma unroll
+    for (int u = 0; u < kE1; ++u) {
+      if (!n[u]) continue;
+      const uint64_t ob = out_base + o[u];
+      if (ob >= out_cap || pr.pos[i[u]] >= pb.n_cap) {  // cannot happen
+        err |= ERR_OOM;
+        continue;
+      }
+      out.key[ob] = key[u];
+      int64_t ws = 0, we = 0;
+      if (p.kind != HSG_UNWINDOWED) {
+        const int64_t k = k_epoch + (int64_t)a[u];
+        ws = (int64_t)((uint64_t)k * (uint64_t)p.adv);
+        we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
+      }
+      out.ws[ob] = ws;
+      out.we[ob] = we;
+      out.src[ob] = seq ? seq[i[u]] : (int64_t)(p.rec_base + i[u]);
+#pragma unroll
+      for (int jj = 0; jj < kMaxAggs; ++jj)
+        if (jj < prog.n_out) out.agg[jj][ob] = out_value_reg<MS>(prog, jj, R[u]);
+    }
   }
   if (err) atomicOr(&sc->err, err);
 }
@@ -1177,7 +1208,7 @@ static void pr_launch(hipStream_t s, const Batch &b, const Program &prog, const 
       else hipLaunchKernelGGL((k_pr_bucket<MS, LT, false, 0>), gb, tb, 0, s, prog, p, pp, t, pb, pr, sc);
     }
     const uint64_t tiles = (b.n + kPrEmitRecs - 1) / kPrEmitRecs;
-    hipLaunchKernelGGL(k_pr_emit1<MS>, dim3((unsigned)tiles), dim3(kPrEmitThreads), 0, s, b, prog, p, pb, pr, rec_wm,
+    hipLaunchKernelGGL(k_pr_emit1<MS>, dim3((unsigned)tiles), dim3(kE1NT), 0, s, b, prog, p, pb, pr, rec_wm,
                        seq, out, out_base, out_cap, sc);
     return;
   }

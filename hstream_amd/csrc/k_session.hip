@@ -654,6 +654,19 @@ struct MgSess {
   uint32_t stamp;  // a resident's stamp (a session without a run is one resident, moved unchanged)
   bool fresh;
 };
+// the resident sessions a sweep may rewrite in place, in registers (kMgTail = 2)
+template <int MS>
+struct MgTail {
+  MgSess<MS> t0, t1;
+};
+template <int MS>
+__device__ __attribute__((always_inline)) inline void mg_clear(MgSess<MS> &x, uint32_t stamp) {
+  x.s = x.e = 0;
+  x.stamp = stamp;
+  x.fresh = false;
+#pragma unroll
+  for (int s = 0; s < MS; ++s) x.a[s] = 0;
+}
 
 // Changelog rows of the fresh sessions of one key (per-batch mode), written
 // by the sweep that produced them (k_ss_apply: every key once per batch).
@@ -682,17 +695,21 @@ __device__ __attribute__((always_inline)) inline void mg_emit(EmitSink &k, const
 }
 
 template <int MS>
-__device__ __attribute__((always_inline)) inline MgSess<MS> pick_tail(const MgSess<MS> (&tail)[kMgTail], uint64_t k) {
-  // field-wise selects (a whole-struct pick by a runtime index puts the array on the stack)
+__device__ __attribute__((always_inline)) inline MgSess<MS> pick_tail(const MgTail<MS> &tail, uint64_t k) {
+  // field-wise selects of two named sessions (an array picked by a runtime
+  // index lands on the stack)
   static_assert(kMgTail == 2, "pick_tail");
-  const bool one = k == 1;
+  // bitwise blends: a select of two loads would be folded into a load through
+  // a selected pointer, which keeps both sessions in stack memory
+  const uint64_t m = k == 1 ? ~0ull : 0ull;
+  auto blend = [m](int64_t a0, int64_t a1) { return (int64_t)(((uint64_t)a0 & ~m) | ((uint64_t)a1 & m)); };
   MgSess<MS> x;
-  x.s = one ? tail[1].s : tail[0].s;
-  x.e = one ? tail[1].e : tail[0].e;
+  x.s = blend(tail.t0.s, tail.t1.s);
+  x.e = blend(tail.t0.e, tail.t1.e);
 #pragma unroll
-  for (int s = 0; s < MS; ++s) x.a[s] = one ? tail[1].a[s] : tail[0].a[s];
-  x.stamp = one ? tail[1].stamp : tail[0].stamp;
-  x.fresh = one ? tail[1].fresh : tail[0].fresh;
+  for (int s = 0; s < MS; ++s) x.a[s] = blend(tail.t0.a[s], tail.t1.a[s]);
+  x.stamp = (uint32_t)blend(tail.t0.stamp, tail.t1.stamp);
+  x.fresh = blend(tail.t0.fresh, tail.t1.fresh) != 0;
   return x;
 }
 
@@ -718,7 +735,7 @@ struct RunsGlobal {
 template <int MS, bool APPLY, class RS, class PV>
 __device__ __attribute__((always_inline)) inline uint32_t mg_sweep(const PV &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t r0,
                                     uint32_t r1, uint64_t off, uint64_t i0, uint64_t len, bool tail_regs,
-                                    const MgSess<MS> (&tail)[kMgTail], uint64_t dst, uint32_t batch_id,
+                                    const MgTail<MS> &tail, uint64_t dst, uint32_t batch_id,
                                     EmitSink *sink = nullptr, SessKey *mirror = nullptr) {
   const int ns = prog.n();
   uint64_t j = i0;   // next resident
@@ -820,7 +837,7 @@ __device__ __attribute__((always_inline)) inline uint64_t mg_first_end_ge(const 
 // run comes within gap of its end).
 template <int MS, class PV>
 __device__ __attribute__((always_inline)) inline void mg_mirror_tail(const PV &prog, const SessKey &e, uint32_t batch_id,
-                                      MgSess<MS> (&tail)[kMgTail]);
+                                      MgTail<MS> &tail);
 template <class RS>
 __device__ inline bool mg_fast(const RS &rs, uint32_t ra, const SessKey &e) {
   return e.mvalid && e.len > 0 && rs.start(ra) >= e.ms;
@@ -830,7 +847,7 @@ __device__ __attribute__((always_inline)) inline void mg_plan(const PV &prog, co
                                uint32_t rb, const SessKey &e, bool fast, uint32_t batch_id, uint64_t &i0, uint32_t &M,
                                uint32_t &newcap, uint32_t *fresh = nullptr) {
   const int64_t lo = (int64_t)((uint64_t)rs.start(ra) - (uint64_t)gap);
-  MgSess<MS> tail[kMgTail];
+  MgTail<MS> tail;
   if (fast) {
     i0 = e.me >= lo ? e.len - 1 : e.len;
     mg_mirror_tail<MS>(prog, e, batch_id, tail);
@@ -848,19 +865,13 @@ __device__ __attribute__((always_inline)) inline void mg_plan(const PV &prog, co
 // The key's last session from its entry's mirror (valid when e.mvalid).
 template <int MS, class PV>
 __device__ __attribute__((always_inline)) inline void mg_mirror_tail(const PV &prog, const SessKey &e, uint32_t batch_id,
-                                      MgSess<MS> (&tail)[kMgTail]) {
+                                      MgTail<MS> &tail) {
+  mg_clear<MS>(tail.t0, batch_id);  // a fast-path resident always merges with a run: rewritten as fresh
+  mg_clear<MS>(tail.t1, batch_id);
+  tail.t0.s = e.ms;
+  tail.t0.e = e.me;
 #pragma unroll
-  for (int k = 0; k < kMgTail; ++k) {
-    tail[k].s = tail[k].e = 0;
-    tail[k].stamp = batch_id;  // a fast-path resident always merges with a run: rewritten as fresh
-    tail[k].fresh = false;
-#pragma unroll
-    for (int s = 0; s < MS; ++s) tail[k].a[s] = 0;
-  }
-  tail[0].s = e.ms;
-  tail[0].e = e.me;
-#pragma unroll
-  for (int s = 0; s < MS; ++s) tail[0].a[s] = (s < kSessMirrorSlots && s < prog.n()) ? e.ma[s] : 0;
+  for (int s = 0; s < MS; ++s) tail.t0.a[s] = (s < kSessMirrorSlots && s < prog.n()) ? e.ma[s] : 0;
 }
 
 // The entry after a merge (its mirror was written by the sweep).
@@ -880,27 +891,23 @@ __device__ __attribute__((always_inline)) inline void mg_apply(const PV &prog, c
   const int ns = prog.n();
   if (reloc)
     for (uint64_t k = 0; k < i0; ++k) ss_copy(t, dst + k, t, e.off + k);
-  MgSess<MS> tail[kMgTail];
+  MgTail<MS> tail;
   if (fast) {
     mg_mirror_tail<MS>(prog, e, batch_id, tail);
   } else {
-#pragma unroll
-    for (int k = 0; k < kMgTail; ++k) {
-      const uint64_t j = i0 + k;
-      tail[k].s = tail[k].e = 0;
-      tail[k].stamp = 0;
-      tail[k].fresh = false;
-#pragma unroll
-      for (int s = 0; s < MS; ++s) tail[k].a[s] = 0;
+    auto fill = [&](MgSess<MS> &x, uint64_t j) {
+      mg_clear<MS>(x, 0u);
       if (!reloc && j < e.len) {
         const uint64_t *row = ss_row(t, e.off + j);
-        tail[k].s = (int64_t)row[0];
-        tail[k].e = (int64_t)row[1];
-        tail[k].stamp = (uint32_t)row[2];
+        x.s = (int64_t)row[0];
+        x.e = (int64_t)row[1];
+        x.stamp = (uint32_t)row[2];
 #pragma unroll
-        for (int s = 0; s < MS; ++s) tail[k].a[s] = s < ns ? (int64_t)row[3 + s] : 0;
+        for (int s = 0; s < MS; ++s) x.a[s] = s < ns ? (int64_t)row[3 + s] : 0;
       }
-    }
+    };
+    fill(tail.t0, i0);
+    fill(tail.t1, i0 + 1);
   }
   mg_sweep<MS, true>(prog, t, gap, rs, ra, rb, e.off, i0, e.len, fast || !reloc, tail, dst, batch_id, sink, mirror);
 }

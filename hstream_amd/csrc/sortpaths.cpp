@@ -120,7 +120,6 @@ int perrecord_part_init(OpDevice &d, const hsg_op_config &cfg, const Program &pr
     x.counter = c.take<uint64_t>(8);
     x.partial = c.take<uint64_t>(scan_partials_needed(tiles) + 8);
     x.fin = c.take<int64_t>(wpr == 1 ? n * ns : 1);
-    x.inv = c.take<uint32_t>(wpr == 1 ? n : 1);
   };
   Carve probe{nullptr};
   PrPart tmp;
@@ -131,7 +130,6 @@ int perrecord_part_init(OpDevice &d, const hsg_op_config &cfg, const Program &pr
   layout(real, d.prp);
   d.part.tpairs = d.prp.tpairs;
   d.part.pos = d.prp.pos;
-  d.part.inv = wpr == 1 ? d.prp.inv : nullptr;
   d.pr_part = true;
   return HSG_OK;
 }

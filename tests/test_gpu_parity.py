@@ -349,3 +349,31 @@ def test_per_record_table_grows(eng):
     assert g.stats()["grow_events"] >= 1
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("sig", ["c2", "count", "full_i64"])
+def test_per_record_bucket_segments(eng, sig):
+    """EMIT CHANGES of a one-window op whose buckets hold far more groups than
+    the per-bucket LDS table (k_pr_bucket walks them in segments, each
+    reloading and writing back its groups' rows) together with hot keys whose
+    records fill whole waves (the lane-order folds): rows in arrival order and
+    the state against the oracle, for the specialised and the runtime slot
+    programs (TimeWindowedStream.hs:89-103)."""
+    cols = [] if sig == "count" else [abi.HSG_I64]
+    aggs = {"count": [(abi.HSG_COUNT_ALL, 0)], "full_i64": ALL_AGG_SETS["full_i64"],
+            "c2": [(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0), (abi.HSG_AVG, 0), (abi.HSG_MIN, 0), (abi.HSG_MAX, 0)]}[sig]
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_RECORD, size_ms=5_000, col_types=cols, aggs=aggs)
+    rng = np.random.default_rng(5)
+    batches = []
+    for bi in range(3):
+        n = 1 << 18
+        key = rng.integers(0, 200_000, size=n).astype(np.uint32)
+        hot = rng.random(n) < 0.2
+        key = np.where(hot, rng.integers(0, 4, size=n), key).astype(np.uint32)
+        ts = (80_000_000 + bi * 20_000 + (np.arange(n) * 20_000) // n + rng.integers(0, 1_500, size=n)).astype(np.int64)
+        vals = [rng.integers(-10**9, 10**9, size=n, dtype=np.int64) if t == abi.HSG_I64
+                else np.round(rng.uniform(-1e6, 1e6, size=n), 3) for t in cols]
+        valid = [(rng.random(n) >= 0.05).astype(np.uint8) for _ in cols]
+        batches.append((key, ts, vals, valid if cols else None))
+    _drive(eng, spec, batches)
+

@@ -92,3 +92,29 @@ def test_key_table_growth(eng):
         ts = (30_000_000 + bi * 40_000 + np.arange(n) // 10 + rng.integers(0, 3_000, size=n)).astype(np.int64)
         batches.append((key, ts, [rng.integers(-1000, 1000, size=n, dtype=np.int64)], None))
     _drive(eng, spec, batches, faithful=False)
+
+
+@pytest.mark.parametrize("gap", [0, 1_000, 30_000])
+def test_mirror_fast_and_slow_keys(eng, gap):
+    """COUNT(*)/SUM sessions (the apply kernel specialised on that program,
+    the entry's mirror of the last session valid): each batch mixes keys whose
+    records come after their last session (planned from the mirror alone, a
+    new session or an extension of the last) with keys whose records reach
+    back before it (a galloping search of the list, merges of older
+    sessions), and keys new to the table; every batch's changelog and the
+    final store against the faithful oracle (Store.hs:243-272)."""
+    spec = OpSpec(abi.HSG_SESSION, abi.HSG_EMIT_PER_BATCH, gap_ms=gap, col_types=[abi.HSG_I64],
+                  aggs=[(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0)])
+    rng = np.random.default_rng(71 + gap)
+    batches = []
+    t0 = 50_000_000
+    for bi in range(5):
+        n = 40_000
+        key = rng.integers(0, 6_000, size=n).astype(np.uint32)
+        ts = t0 + bi * 200_000 + rng.integers(0, 200_000, size=n)
+        back = rng.random(n) < 0.15  # reach back into earlier batches' sessions
+        ts = np.where(back, ts - rng.integers(100_000, 600_000, size=n), ts).astype(np.int64)
+        col = rng.integers(-10**6, 10**6, size=n, dtype=np.int64)
+        valid = (rng.random(n) >= 0.03).astype(np.uint8)
+        batches.append((key, ts, [col], [valid]))
+    _drive(eng, spec, batches, faithful=False)
