@@ -18,6 +18,13 @@
  * field, wrong-typed aggregated field) gets key_id = HSG_KEY_NONE: it still
  * moves stream time (Processor.hs:139), exactly as there.
  *
+ * Known divergence: the dictionary keeps the Aeson text of a key's FIRST
+ * spelling, and the sink prints every changelog row's key with it. The
+ * reference forwards each record with its own recordKey (TimeWindowedStream.hs
+ * :94,101), so under EMIT CHANGES a later {"k":1.0} after {"k":1} prints key
+ * "1.0" there and "1" here (the same group either way; only the text of
+ * equal-but-differently-spelled keys differs).
+ *
  * Where the GPU's fixed-width columns cannot hold what Scientific holds, the
  * record is rejected with its own status instead of being rounded: a
  * non-integral number, or one outside int64, in an HSG_I64 column (declare
