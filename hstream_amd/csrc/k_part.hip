@@ -131,6 +131,16 @@ __device__ inline uint32_t stable_round_rank(uint32_t bk, bool ok, int nbits, ui
     for (int w = 0; w < wv; ++w) before += wcnt[w][bk];
   return before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
+// Lanes of this wave whose (ok) bucket equals ours: one ballot per bucket bit.
+__device__ inline uint64_t match_peers(uint32_t bk, bool ok, int nbits) {
+  uint64_t m = __ballot(ok);
+  for (int bit = 0; bit < nbits; ++bit) {
+    const bool x = (bk >> bit) & 1u;
+    const uint64_t bb = __ballot(x);
+    m &= x ? bb : ~bb;
+  }
+  return m;
+}
 __device__ inline void stable_round_done(uint32_t bk, bool ok, uint64_t peers, uint8_t (*wcnt)[1 << kPartMaxLog2]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (ok && (peers >> lane) == 1ull) wcnt[wv][bk] = 0;
@@ -644,7 +654,9 @@ void launch_part_decide_offsets(hipStream_t s, DevScalars *sc, const TwParams &p
 template <int T, int W, bool STABLE>
 __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, PartParams pp, PartBuffers pb,
                                                           DevScalars *sc) {
-  __shared__ uint8_t wcnt[STABLE ? kPW : 1][1 << kPartMaxLog2];
+  // STABLE: wave w's running count of bucket b over its rounds, then the
+  // exclusive prefix of those counts over the waves
+  __shared__ uint16_t wcnt[STABLE ? kPW : 1][1 << kPartMaxLog2];
   __shared__ uint64_t stage[T * W];
   __shared__ uint32_t cnt2[1 << (kPartMaxLog2 - 1)];  // two u16 counts per word, then the u16 run starts
   __shared__ uint32_t cursor[1 << kPartMaxLog2];      // the row's next output slot per bucket
@@ -673,9 +685,14 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
     uint32_t key[R];
     int64_t ts[R];
     uint64_t col[R];
+    // STABLE: each wave takes R*64 consecutive records (64 per round), so a
+    // record's arrival rank needs no block barrier per round
+    auto rec_i = [&](int r) -> uint64_t {
+      return STABLE ? base + (uint64_t)wv * (R * 64) + (uint64_t)r * 64 + lane : base + (uint64_t)r * kPNT + threadIdx.x;
+    };
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const uint64_t i = base + (uint64_t)r * kPNT + threadIdx.x;
+      const uint64_t i = rec_i(r);
       const bool in = i < b.n;
       key[r] = in ? b.key[i] : HSG_KEY_NONE;
       ts[r] = in ? b.ts[i] : 0;
@@ -692,20 +709,19 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
       const uint32_t sh = (bk & 1u) * 16u;
       uint32_t pos;
       if constexpr (STABLE) {
-        // rank in arrival order: earlier rounds (cnt2) + this round's earlier lanes
-        uint64_t peers;
-        const uint32_t rk = stable_round_rank(bk, ok, pp.np_log2, wcnt, peers);
-        pos = ok ? ((cnt2[bk >> 1] >> sh) & 0xFFFFu) + rk : 0u;
-        lds_barrier();
-        if (ok && (peers >> (threadIdx.x & 63)) == 1ull) atomicAdd(&cnt2[bk >> 1], (uint32_t)__popcll(peers) << sh);
-        stable_round_done(bk, ok, peers, wcnt);
+        // rank within this wave: its earlier rounds + this round's lower lanes
+        // (the wave's own LDS row, read before its leader writes it)
+        const uint64_t peers = match_peers(bk, ok, pp.np_log2);
+        const uint32_t prev = ok ? wcnt[wv][bk] : 0u;
+        pos = prev + (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+        if (ok && (peers >> lane) == 1ull) wcnt[wv][bk] = (uint16_t)(prev + __popcll(peers));
         if (!ok) continue;
       } else {
         if (!ok) continue;
         pos = (atomicAdd(&cnt2[bk >> 1], 1u << sh) >> sh) & 0xFFFFu;
       }
       slot[r] = (bk << 16) | pos;
-      const uint64_t i = base + (uint64_t)r * kPNT + threadIdx.x;
+      const uint64_t i = rec_i(r);
       uint64_t vb = 0;
       if (W == 2 && !(pp.has_valid && b.valid[0] && !b.valid[0][i])) vb = 1;
       ts[r] = (int64_t)((uint64_t)key[r] | ((uint64_t)((krel - kbase) & 0xFFFFu) << 32) | ((uint64_t)nwin << 48) |
@@ -716,7 +732,17 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
     uint32_t c[4] = {0, 0, 0, 0};  // per <= 4 (2048 buckets / 512 threads)
     uint32_t loc = 0;
     for (int k = lo; k < hi; ++k) {
-      c[k - lo] = (cnt2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+      if constexpr (STABLE) {
+        uint32_t run = 0;  // the waves' counts -> their exclusive prefix
+        for (int w = 0; w < kPW; ++w) {
+          const uint32_t x = wcnt[w][k];
+          wcnt[w][k] = (uint16_t)run;
+          run += x;
+        }
+        c[k - lo] = run;
+      } else {
+        c[k - lo] = (cnt2[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+      }
       loc += c[k - lo];
     }
     uint32_t incl = loc;
@@ -740,8 +766,10 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (slot[r] == ~0u) continue;
-      if (pb.pos) pb.pos[base + (uint64_t)r * kPNT + threadIdx.x] = cursor[slot[r] >> 16] + (slot[r] & 0xFFFFu);
-      const uint32_t q = lstart[slot[r] >> 16] + (slot[r] & 0xFFFFu);
+      const uint32_t sb = slot[r] >> 16;
+      const uint32_t rk = (slot[r] & 0xFFFFu) + (STABLE ? (uint32_t)wcnt[wv][sb] : 0u);
+      if (pb.pos) pb.pos[rec_i(r)] = cursor[sb] + rk;
+      const uint32_t q = lstart[sb] + rk;
       stage[q * W] = (uint64_t)ts[r];
       if (W == 2) stage[q * W + 1] = col[r];
     }
@@ -763,6 +791,9 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
     // the row's next slots, past this sub-tile's runs; counters cleared
     for (int k = lo; k < hi; ++k) cursor[k] += c[k - lo];
     for (int k = lo; k < hi; k += 2) cnt2[k >> 1] = 0;
+    if constexpr (STABLE)
+      for (int k = lo; k < hi; ++k)
+        for (int w = 0; w < kPW; ++w) wcnt[w][k] = 0;
   }
   if (err) atomicOr(&sc->err, err);
   if (threadIdx.x == 0) {
