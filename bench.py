@@ -229,6 +229,10 @@ def main():
             "agg_kernel_share": round(agg_s / elapsed, 4) if elapsed > 0 else None,
             "pairs_per_step": int((st1["pairs_total"] - st0["pairs_total"]) / max(1, args.steps)),
             "touched_per_step": int(touched / max(1, args.steps)),
+            # HBM state table at the end of the run (slots of the time-window
+            # table, or of the session key table) and its growth events
+            "table_slots": int(st1["table_slots"]),
+            "table_grow_events": int(st1["grow_events"]),
         }
         print(json.dumps(line), flush=True)
     if op is not None:

@@ -596,6 +596,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const ProgView<SIG> prog(prog_);
   if (sc->redo) return;  // uniform: the optimistic pass found late records
   if ((sc->packed != 0) != PK) return;  // uniform: the other layout's variant runs
+  if (pp.hold) {  // uniform: the table lacks room for this batch's worst case (host grows it, runs again)
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr((unsigned long long *)&sc->scratch[32], 2ull);
+    return;
+  }
   constexpr int SUB = NT * RPT;
   const int nb = 1 << pp.np_log2;
   const uint32_t *chunk_start = pb.chunk_start;

@@ -155,6 +155,15 @@ __device__ inline int64_t out_value_w(const Program &prog, int j, int64_t a, int
   }
 }
 
+// XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs, so
+// give workgroups b, b+8, b+16, ... (one XCD) consecutive tiles; a bucket's
+// runs from consecutive tiles are adjacent in the output. Speed only.
+__device__ inline uint64_t xcd_tile(uint64_t blk, uint64_t tiles) {
+  const uint64_t per = tiles / 8, full = per * 8;
+  if (blk >= full) return blk;
+  return (blk & 7) * per + (blk >> 3);
+}
+
 // output column j from a state row in memory
 __device__ inline int64_t out_value(const Program &prog, int j, const int64_t *row) {
   return out_value_w(prog, j, row[prog.out_a[j]], row[prog.out_b[j]]);

@@ -97,7 +97,8 @@ struct DevScalars {
   uint64_t packed;       // partition path, this batch: records in the packed layout (hsg_part.h)
   uint64_t kbase;        // packed layout: window (relative to the epoch) the 16-bit window offsets count from
   uint64_t scratch[45];  // [0] groups flushed (partition path), [1] touched-list length, [8..20] phase clocks,
-                         // [21..22] optimistic pass ts extrema
+                         // [21..22] optimistic pass ts extrema, [31] lean partials of the batch (bound on
+                         // its new groups), [32] held back for table room: bit 0 lean apply, bit 1 general
   uint64_t live_x[8];    // more rows found, one shard per XCD (blockIdx & 7) for kernels whose every
                          // workgroup adds; the host folds them into `live` when it fetches the scalars
 };

@@ -113,6 +113,7 @@ struct OpDevice {
   bool pred_packed = false;     // launch prediction: the last batch was packed (wide variants not launched)
   bool pred_direct = false;     // launch prediction: the last batch's changelog came from the lean apply
   uint64_t lean_batches = 0, direct_batches = 0, replays = 0;  // hsg_stats
+  uint64_t lean_pred = 0;  // new groups the next lean batch may make (2x the last one's partials), 0 = none
   // sessions
   SessTable ss = {};
   uint64_t *h_meta = nullptr;     // pinned mirror of ss.meta
@@ -204,7 +205,7 @@ void tw_configure(TwTable &t, uint64_t cap, int window_kind);
 // table (growing it until the open rows plus the batch's bound fit at 1/2).
 // A watermark below the last spill's brings every spilled row back first.
 int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t n_in, int64_t wm_in,
-                uint64_t pending, std::string &err);
+                uint64_t pending, std::string &err, uint64_t groups_bound = UINT64_MAX);
 // append the spilled rows to a dump at row dst_off (*n_out = rows written)
 int tw_dump_spilled(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hsg_rows *out,
                     uint64_t dst_off, uint64_t *n_out, std::string &err);

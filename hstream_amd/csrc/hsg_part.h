@@ -63,9 +63,12 @@ struct PartParams {
   int32_t bshift;     // owner bits above the bucket bits in the key hash (multi-GPU, power-of-two ranks)
   int32_t defer;      // aggregation: window updates of exclusive buckets go to pb.pane segments (k_seg_apply)
   int32_t sub;        // partition passes: kPartTileRecs-record sub-tiles per offsets row (one workgroup per row)
-  int32_t pad;
+  int32_t hold;       // aggregation, general kernels: the worst case (one group per (record, window))
+                      // passes `room`: claim nothing, hold back (DevScalars scratch[32] bit 1)
   uint64_t tiles;     // offsets rows of this batch     // partition-pass tiles of this batch
   uint64_t chunk;     // records per aggregation workgroup
+  uint64_t room;      // lean path: new groups the table takes this batch (load <= 3/4); past it the
+                      // apply claims nothing and the host grows the table and runs the batch again
 };
 
 inline int part_words(int n_cols, bool has_seq) { return 2 + n_cols + (has_seq ? 1 : 0); }

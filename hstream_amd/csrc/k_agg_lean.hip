@@ -243,7 +243,10 @@ __global__ __launch_bounds__(NT) void k_agg_lean(PartParams pp, TwTable t, PartB
 #pragma unroll
     for (int s = 0; s < NS; ++s) o[1 + s] = (uint64_t)(((skip >> s) & 1u) ? call : lagg[s * E + e]);
   }
-  if (threadIdx.x == 0) s_cnt += total;
+  if (threadIdx.x == 0) {
+    s_cnt += total;
+    atomicAdd((unsigned long long *)&sc->scratch[31], (unsigned long long)s_cnt);  // the apply's room check
+  }
   __syncthreads();
   // the batch totals (pairs = records placed, groups = partials) are set by
   // the last apply workgroup: no per-workgroup atomic on a shared counter
@@ -311,6 +314,13 @@ __global__ __launch_bounds__(256) void k_pane_apply(Program rprog, TwParams p, P
   __shared__ uint64_t s_red[4], s_tot[4], s_d[4], s_t[4];
   __shared__ uint32_t cset[kClaimSet];
   if (sc->redo || !sc->packed) return;  // uniform
+  // the batch's groups (at most its partials) may not fit the table at the
+  // load it is sized for: nothing is claimed, the host grows the table and
+  // runs the batch again (uniform: k_agg_lean has finished)
+  if (sc->scratch[31] > pp.room) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr((unsigned long long *)&sc->scratch[32], 1ull);
+    return;
+  }
   uint32_t b;
   uint64_t r0, r1;
   bool exclusive;
@@ -540,6 +550,7 @@ __global__ __launch_bounds__(1024) void k_seg_apply(Program prog, TwParams p, Pa
   __shared__ uint64_t s_red[NT / 64], s_tot[NT / 64];
   __shared__ uint32_t cset[kSegClaimSet];
   if (sc->redo || (lean && sc->packed)) return;  // uniform: late batch / the lean kernels took it
+  if (pp.hold) return;                           // uniform: k_part_agg held back for table room
   uint32_t b;
   uint64_t r0, r1;
   bool exclusive;

@@ -60,14 +60,6 @@ __device__ inline bool part_record(const TwParams &p, int64_t k_epoch, uint32_t 
   return true;
 }
 
-// XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs, so
-// give workgroups b, b+8, b+16, ... (one XCD) consecutive tiles; a bucket's
-// runs from consecutive tiles are adjacent in the output. Speed only.
-__device__ inline uint64_t xcd_tile(uint64_t blk, uint64_t tiles) {
-  const uint64_t per = tiles / 8, full = per * 8;
-  if (blk >= full) return blk;
-  return (blk & 7) * per + (blk >> 3);
-}
 
 // Per-record stream time in arrival order, only when some record of the batch
 // may fail the grace check (sc->no_late == 0); otherwise every workgroup exits.

@@ -733,11 +733,13 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
   constexpr int TAB = 1 << LT;
   constexpr int EPT = TAB / kPbNT;  // table entries per thread
   constexpr int PF = 8;             // record loads in flight per thread in the one-pass insert
+  constexpr int CAP = TAB / 2;      // groups of a segment (the table runs at most half full)
   __shared__ uint64_t tkey[TAB];
-  __shared__ int64_t tst[MS][TAB];
-  __shared__ uint32_t tslot[TAB];
+  __shared__ uint16_t tidx[TAB];    // group index (insertion order) of the key at each slot
+  __shared__ int64_t tst[MS][CAP];  // per group index: state, row slot, owners of the step
+  __shared__ uint32_t tslot[CAP];
   __shared__ int64_t stg[kPbNW][MS][64];  // each wave's records' contributions, then its groups' totals
-  __shared__ uint8_t widx[kPbNW][TAB];     // per wave: 1 + owner lane of each group in the step, 0 = none
+  __shared__ uint8_t widx[kPbNW][CAP];     // per wave: 1 + owner lane of each group in the step, 0 = none
   __shared__ uint32_t s_fill;
   __shared__ uint64_t s_red[2][kPbNW];
   if (sc->redo) return;  // uniform: the optimistic pass found late records (bucket starts are stale)
@@ -766,14 +768,18 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
       if (c == g) return true;
       if (c == kEmpty) {
         const uint64_t old = atomicCAS((unsigned long long *)&tkey[h], (unsigned long long)kEmpty, (unsigned long long)g);
-        if (old == kEmpty) return atomicAdd(&s_fill, 1u) + 1 <= (uint32_t)(TAB / 2);
+        if (old == kEmpty) {
+          const uint32_t c = atomicAdd(&s_fill, 1u);
+          if (c < (uint32_t)CAP) tidx[h] = (uint16_t)c;
+          return c + 1 <= (uint32_t)CAP;
+        }
         if (old == g) return true;
       }
       h = (h + 1) & (TAB - 1);
     }
   };
   for (int e = threadIdx.x; e < TAB; e += kPbNT) tkey[e] = kEmpty;
-  for (int e = threadIdx.x; e < kPbNW * TAB; e += kPbNT) (&widx[0][0])[e] = 0;
+  for (int e = threadIdx.x; e < kPbNW * CAP; e += kPbNT) (&widx[0][0])[e] = 0;
   if (threadIdx.x == 0) s_fill = 0;
   __syncthreads();
   // 1a. one pass over the whole bucket, PF record loads in flight per thread:
@@ -887,9 +893,10 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
             touched += 1;
           }
         }
-        tslot[e] = sl[u] < 0 ? ~0u : (uint32_t)sl[u];
+        const uint32_t c = tidx[e];
+        tslot[c] = sl[u] < 0 ? ~0u : (uint32_t)sl[u];
 #pragma unroll
-        for (int s = 0; s < MS; ++s) tst[s][e] = cur[u][s];
+        for (int s = 0; s < MS; ++s) tst[s][c] = cur[u][s];
       }
     }
     lds_barrier();
@@ -921,7 +928,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
       const bool in = i < s1;
       const PrRecRegs<REG> v{nx0, nx1, nx2, nx3, rec + i * (uint64_t)W, pk, C};
       fetch(i + kPbNT);
-      uint32_t h = 0;
+      uint32_t h = 0;  // then the group's index
       int64_t pre[MS];
       identity_v<MS>(pv, pre);
       const uint64_t t0 = wall_clock64();
@@ -929,6 +936,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
         const uint64_t g = ((uint64_t)v.key() << 32) | v.krel(kbase);
         h = pb_home(g, LT);
         while (tkey[h] != g) h = (h + 1) & (TAB - 1);  // inserted in step 1
+        h = tidx[h];
         int64_t e[MS];
         elems_v<MS>(pv, v, e);
 #pragma unroll
@@ -937,7 +945,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
       // this wave's lanes of each group, found by one ballot per table bit
       uint64_t peers = __ballot(in);
 #pragma unroll
-      for (int bit = 0; bit < LT; ++bit) {
+      for (int bit = 0; bit < LT - 1; ++bit) {
         const bool x = (h >> bit) & 1u;
         const uint64_t bb = __ballot(x);
         peers &= x ? bb : ~bb;
@@ -1020,11 +1028,13 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
     { const uint64_t cb = wall_clock64(); c_steps += cb - ca; ca = cb; }
     // 4. the groups' states back to their rows
     for (int e = threadIdx.x; e < TAB; e += kPbNT) {
-      if (tkey[e] == kEmpty || tslot[e] == ~0u) continue;
-      int64_t *row = t.aggs(tslot[e]);
+      if (tkey[e] == kEmpty) continue;
+      const uint32_t c = tidx[e];
+      if (tslot[c] == ~0u) continue;
+      int64_t *row = t.aggs(tslot[c]);
 #pragma unroll
       for (int s = 0; s < MS; ++s)
-        if (s < ns) row[s] = tst[s][e];
+        if (s < ns) row[s] = tst[s][c];
     }
     // the next segment reads these rows back (L1-bypassing loads): drain
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1081,47 +1091,67 @@ __global__ __launch_bounds__(kE1NT) void k_pr_emit1(Batch bt, Program prog, TwPa
   const int64_t *wm = rec_wm ? rec_wm : (sc->no_late ? nullptr : pb.wm);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ns = prog.n_slots;
+  const int fw = ns;
   uint32_t err = 0;
-  uint64_t base = pr.tpoff[(uint64_t)blockIdx.x * (kPrEmitRecs / kPartTileRecs)];
+  // consecutive tiles on one XCD: their rows of a bucket are neighbours in pr.fin
+  const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);
+  uint64_t base = pr.tpoff[tile * (kPrEmitRecs / kPartTileRecs)];
   for (int rd0 = 0; rd0 < kE1Rounds; rd0 += kE1) {
-    if ((uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)rd0 * kE1NT >= bt.n) break;  // uniform
+    if (tile * kPrEmitRecs + (uint64_t)rd0 * kE1NT >= bt.n) break;  // uniform
+    // every load of the rounds is issued up front (indices clamped, no
+    // branches), so a thread waits on two memory round trips: the record
+    // columns + its position, then the state rows
     uint32_t a[kE1], n[kE1], key[kE1];
-    uint64_t i[kE1];
+    uint64_t i[kE1], pz[kE1];
+    int64_t tsv[kE1], wmv[kE1];
+    const uint64_t last = bt.n - 1;
 #pragma unroll
     for (int u = 0; u < kE1; ++u) {
-      i[u] = (uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)(rd0 + u) * kE1NT + threadIdx.x;
-      a[u] = 0;
-      n[u] = 0;
-      key[u] = i[u] < bt.n ? bt.key[i[u]] : HSG_KEY_NONE;
+      i[u] = tile * kPrEmitRecs + (uint64_t)(rd0 + u) * kE1NT + threadIdx.x;
+      const uint64_t ic = i[u] < bt.n ? i[u] : last;
+      key[u] = bt.key[ic];
+      tsv[u] = bt.ts[ic];
+      wmv[u] = wm ? wm[ic] : INT64_MIN;
+      pz[u] = pr.pos[ic];
+      if (i[u] >= bt.n) key[u] = HSG_KEY_NONE;
     }
-#pragma unroll
-    for (int u = 0; u < kE1; ++u) {
-      if (key[u] == HSG_KEY_NONE) continue;  // the window the partition passes accepted (k_part.hip part_record)
-      const int64_t ts = bt.ts[i[u]];
-      uint64_t k_lo, k_hi;
-      if (record_windows(p, ts, k_lo, k_hi)) {
-        const int64_t w = wm ? wm[i[u]] : INT64_MIN;
-        if (window_accepted(p, k_lo, w)) {
-          const int64_t lo = (int64_t)k_lo - k_epoch;
-          if (lo >= 0 && lo <= 0xFFFFFFFFll) {
-            a[u] = (uint32_t)lo;
-            n[u] = 1;
-          }
-        }
-      }
-    }
-    // the states, every gather in flight at once
+    // the states (a record the partition dropped has a stale position: its
+    // row is read, clamped into the buffer, and not used)
     int64_t R[kE1][MS];
 #pragma unroll
     for (int u = 0; u < kE1; ++u) {
+      const int64_t *f = pr.fin + (pz[u] < pb.n_cap ? pz[u] : 0) * (uint64_t)fw;
+      if constexpr (MS % 2 == 0) {
+        if ((fw & 1) == 0) {  // 16-B aligned rows
 #pragma unroll
-      for (int s = 0; s < MS; ++s) R[u][s] = 0;
-      if (!n[u]) continue;
-      const uint64_t pos = pr.pos[i[u]];
-      const int64_t *f = pr.fin + (pos < pb.n_cap ? pos : 0) * (uint64_t)ns;
+          for (int s = 0; s < MS; s += 2) {
+            if (s < fw) {
+              const longlong2 v = *reinterpret_cast<const longlong2 *>(f + s);
+              R[u][s] = v.x;
+              R[u][s + 1] = v.y;
+            } else {
+              R[u][s] = R[u][s + 1] = 0;
+            }
+          }
+          continue;
+        }
+      }
 #pragma unroll
-      for (int s = 0; s < MS; ++s)
-        if (s < ns) R[u][s] = f[s];
+      for (int s = 0; s < MS; ++s) R[u][s] = s < fw ? f[s] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kE1; ++u) {
+      a[u] = 0;
+      n[u] = 0;
+      if (key[u] == HSG_KEY_NONE) continue;  // the window the partition passes accepted (k_part.hip part_record)
+      uint64_t k_lo, k_hi;
+      if (record_windows(p, tsv[u], k_lo, k_hi) && window_accepted(p, k_lo, wmv[u])) {
+        const int64_t lo = (int64_t)k_lo - k_epoch;
+        if (lo >= 0 && lo <= 0xFFFFFFFFll) {
+          a[u] = (uint32_t)lo;
+          n[u] = 1;
+        }
+      }
     }
     // exclusive prefixes of the rounds' rows in arrival order
     uint64_t o[kE1];
@@ -1147,7 +1177,7 @@ __global__ __launch_bounds__(kE1NT) void k_pr_emit1(Batch bt, Program prog, TwPa
     for (int u = 0; u < kE1; ++u) {
       if (!n[u]) continue;
       const uint64_t ob = out_base + o[u];
-      if (ob >= out_cap || pr.pos[i[u]] >= pb.n_cap) {  // cannot happen
+      if (ob >= out_cap || pz[u] >= pb.n_cap) {  // cannot happen
         err |= ERR_OOM;
         continue;
       }
@@ -1175,7 +1205,7 @@ static void pr_launch(hipStream_t s, const Batch &b, const Program &prog, const 
                       const int64_t *seq, const OutCols &out, uint64_t out_base, uint64_t out_cap, DevScalars *sc) {
   const uint64_t nb = 1ull << pp.np_log2;
   if (wpr == 1) {
-    // LDS: table 12 + 8 MS bytes per entry, staging 2 KB per slot
+    // LDS: 10 B per table slot, 8 MS + 4 + 4 per group (half the slots), staging 2 KB per state slot
     constexpr int LT = MS <= 6 ? 10 : 9;
     const dim3 gb((unsigned)nb), tb(kPbNT);
     const uint64_t sig = program_sig(prog);

@@ -559,6 +559,11 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
   // kernels, which then run as on every later batch.
   const bool opt = d.use_part && !rec_wm && !has_last(prog) && cfg.grace_ms >= 0 && cfg.window_kind != HSG_SESSION;
   const bool need_epoch = !d.h_sc->epoch_set;
+  // Table room (see table_bound_hint): the partition path's claiming kernels
+  // check the batch against pp.room (3/4 load) before they claim anything --
+  // the lean apply its partials, the general kernels one group per (record,
+  // window) -- and hold back past it; the batch then runs again on a table
+  // grown for that bound. The other paths were given the worst case by op_push.
   // Launch prediction (speed only): the variants a batch does not take exit at
   // once on the device, but each costs a launch. After a packed batch whose
   // changelog the lean apply wrote itself, the next batch's wide-layout
@@ -594,6 +599,9 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       pp.chunk = kAggChunk;
       pp.big = d.agg_big ? 1 : 0;
       pp.defer = 1;
+      const uint64_t lim = d.cap - d.cap / 4;
+      pp.room = lim > d.h_sc->live ? lim - d.h_sc->live : 0;
+      pp.hold = kb.n * d.wpr > pp.room ? 1 : 0;
       if (!rec_wm && !optimistic) launch_part_recwm(d.stream, kb, d.tile_prefix, d.sc, d.part.wm);
       launch_part_hist(d.stream, kb, p, pp, rec_wm, d.part.wm, d.part, d.sc, optimistic);
       const bool can_pack = optimistic && cfg.n_cols <= 8 && d.wpr < 256;
@@ -628,25 +636,42 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     DTRY(hipGetLastError());
     return HSG_OK;
   };
-  int rc = run(opt);
-  if (rc != HSG_OK) return rc;
-  rc = finish_batch(d, a.wm_in, kb.n, r, err);
-  if (opt && kb.n && d.h_sc->redo) {
-    rc = run(false);
+  // a run whose claiming kernels held back for table room: grow the table for
+  // the bound they saw (the lean partials, else the worst case), run again
+  auto run_room = [&](bool optimistic) -> int {
+    int rc = run(optimistic);
     if (rc != HSG_OK) return rc;
     rc = finish_batch(d, a.wm_in, kb.n, r, err);
+    if (rc != HSG_OK || !kb.n || !d.h_sc->scratch[32]) return rc;
+    d.replays += 1;
+    const uint64_t bound = (d.h_sc->scratch[32] & 2) ? UINT64_MAX : d.h_sc->scratch[31];
+    rc = tw_maintain(d, cfg, prog, kb.n, a.wm_in, a.pending, err, bound);
+    if (rc != HSG_OK) return rc;
+    if (cfg.emit_mode == HSG_EMIT_PER_BATCH && a.pending + (kb.n * d.wpr < d.cap ? kb.n * d.wpr : d.cap) > d.out_cap) {
+      err = "changelog buffer full: drain before pushing (out_capacity)";
+      return HSG_E_CAPACITY;  // the batch is not applied
+    }
+    rc = run(optimistic);
+    if (rc != HSG_OK) return rc;
+    return finish_batch(d, a.wm_in, kb.n, r, err);
+  };
+  int rc = run_room(opt);
+  if (rc != HSG_OK) return rc;
+  if (opt && kb.n && d.h_sc->redo) {
+    rc = run_room(false);
   } else if (kb.n && skipped_wide && !d.h_sc->packed) {
     d.pred_packed = false;  // a wide batch: nothing was aggregated, run it with every variant
     d.replays += 1;
-    rc = run(opt);
-    if (rc != HSG_OK) return rc;
-    rc = finish_batch(d, a.wm_in, kb.n, r, err);
+    rc = run_room(opt);
   }
   const uint64_t groups = d.h_sc->scratch[0];
   if (kb.n && d.use_part) {
     d.pred_packed = d.h_sc->packed != 0;
     const uint64_t how = d.h_sc->scratch[2];  // 1/2 lean, 3/4 deferred; odd: changelog written directly
     d.pred_direct = how == 1 || how == 3;
+    // next batch's table room: twice this batch's new-group bound (its partials)
+    const uint64_t parts = d.h_sc->scratch[31];
+    d.lean_pred = (how == 1 || how == 2) ? (2 * parts > (1ull << 16) ? 2 * parts : (1ull << 16)) : 0;
     d.lean_batches += how == 1 || how == 2;
     d.direct_batches += how == 1 || how == 3;
   }
@@ -674,13 +699,31 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
   return rc;
 }
 
+// New groups to make room for ahead of a batch. The partition path's kernels
+// check their own bound against the room left and hold back past it
+// (push_time_atomic), so a lean-eligible op is sized for twice the partials
+// of its last lean batch (none before its first: the batch's own check grows
+// the table) rather than for one new group per (record, window); every other
+// path gets that worst case.
+static uint64_t table_bound_hint(const OpDevice &d, const hsg_op_config &cfg, const Program &prog) {
+  if (!d.use_part || has_last(prog) || cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.grace_ms < 0 ||
+      cfg.window_kind == HSG_SESSION || cfg.n_cols > 8 || d.wpr >= 256)
+    return UINT64_MAX;
+  PartParams q;
+  memset(&q, 0, sizeof(q));
+  q.pane_S = d.pane_S;
+  q.rbits = d.rbits;
+  q.words = part_words(cfg.n_cols, false);
+  return part_lean_eligible(prog, q) ? d.lean_pred : UINT64_MAX;
+}
+
 int op_push(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, PushResult &r,
             std::string &err) {
   const hsg_batch *b = a.batch;
   // room in the table for the batch's worst case (sharded ops: in push_local,
   // once the records this rank owns are known)
   if (!a.comm) {
-    int rc = tw_maintain(d, cfg, prog, b->n, a.wm_in, a.pending, err);
+    int rc = tw_maintain(d, cfg, prog, b->n, a.wm_in, a.pending, err, table_bound_hint(d, cfg, prog));
     if (rc != HSG_OK) return rc;
   }
   // the changelog must have room for the worst case of this batch

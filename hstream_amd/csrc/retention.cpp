@@ -112,11 +112,13 @@ static int grow_out(OpDevice &d, const hsg_op_config &cfg, uint64_t ncap, uint64
 }
 
 int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t n_in, int64_t wm_in,
-                uint64_t pending, std::string &err) {
+                uint64_t pending, std::string &err, uint64_t groups_bound) {
   if (cfg.window_kind == HSG_SESSION || !d.tw.rows) return HSG_OK;
   const bool reopen = d.spilled_rows && wm_in < d.spill_wm;
   const uint64_t live = d.h_sc->live;
-  const uint64_t bound = n_in * d.wpr;
+  // new groups of the batch: one per (record, window) at worst, or the bound
+  // of a batch whose apply checks its room (op_device.cpp push_time_atomic)
+  const uint64_t bound = n_in * d.wpr < groups_bound ? n_in * d.wpr : groups_bound;
   if (!reopen && 4 * (live + bound) <= 3 * d.cap) return HSG_OK;
   wait_table_reset(d);
   const TwParams p = retention_params(cfg, wm_in);

@@ -130,3 +130,66 @@ def test_lean_later_batch_with_identity_partials(eng, ctype):
     rows_equal(g.dump_state(), o.dump_state(), spec.agg_is_f64(), what="state dump")
     g.close()
     o.close()
+
+
+def test_table_room_holds_and_regrows(eng):
+    """The table is sized for twice the last lean batch's groups, not one group
+    per record: a batch with more new groups than the room left holds back
+    before claiming (the lean apply on its partials, the general kernels on
+    the worst case of a wide batch), and runs again on a grown table. Starts
+    from a 2048-slot table so every kind of hold happens; each changelog and
+    the final state match the oracle."""
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=10_000, col_types=[abi.HSG_I64],
+                  aggs=datagen.C_AGGS_FULL, state_capacity=1 << 10)
+    g, o = eng.op(spec), pyoracle.OracleOp(spec)
+    f64 = spec.agg_is_f64()
+    rng = np.random.default_rng(11)
+    t = 10_000_000
+    batches = []
+    # (20K keys per uniform batch: a key's windows share its table region,
+    # and a few keys with many windows each could fill one region of a table
+    # at moderate load -- an HSG_E_OOM the sizing does not try to prevent)
+    for nkeys, span, n in [(20_000, 600_000, 300_000),        # ~260K groups >> 1.5K room: lean hold
+                           (20_000, 600_000, 300_000),        # inside the prediction
+                           (5_000, 2_000_000_000, 100_000),   # > 2^16 windows: wide layout
+                           (20_000, 600_000, 300_000),
+                           (300_000, 600_000, 400_000),       # ~1.5x the predicted groups: lean hold
+                           (20_000, 600_000, 300_000)]:
+        batches.append(_uniform(rng, n, nkeys, t, span))
+        t += span
+    wg = wo = -1
+    for bi, (key, ts, cols) in enumerate(batches):
+        wg = g.push(key, ts, cols, None, watermark=wg)
+        wo = o.push(key, ts, cols, None, watermark=wo)
+        assert wg == wo, f"batch {bi}: watermark {wg} != {wo}"
+        rows_equal(g.drain(), o.drain(), f64, what=f"changelog batch {bi}")
+    rows_equal(g.dump_state(), o.dump_state(), f64, what="state dump")
+    st = g.stats()
+    assert st["grow_events"] >= 2 and st["replays"] >= 2, st
+    g.close()
+    o.close()
+
+
+def test_table_sized_by_groups_not_records(eng):
+    """A steady one-window stream (C2's shape: few groups per record) keeps a
+    table sized by its groups: 2^22-record batches over 4K keys (~45K groups
+    per batch) keep the engine's default 4M-slot table, where one new group
+    per record would grow it to 8M slots on the first batch."""
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=60_000, col_types=[abi.HSG_I64],
+                  aggs=datagen.C_AGGS_FULL)
+    g, o = eng.op(spec), pyoracle.OracleOp(spec)
+    f64 = spec.agg_is_f64()
+    rng = np.random.default_rng(12)
+    t = 0
+    wg = wo = -1
+    for bi in range(3):
+        key, ts, cols = _uniform(rng, 1 << 22, 4_096, t, 600_000)
+        t += 600_000
+        wg = g.push(key, ts, cols, None, watermark=wg)
+        wo = o.push(key, ts, cols, None, watermark=wo)
+        rows_equal(g.drain(), o.drain(), f64, what=f"changelog batch {bi}")
+    rows_equal(g.dump_state(), o.dump_state(), f64, what="state dump")
+    st = g.stats()
+    assert st["table_slots"] <= (1 << 22) and st["grow_events"] == 0, st
+    g.close()
+    o.close()
