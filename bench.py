@@ -479,7 +479,10 @@ def committed_traffic(args, world):
         return None, None
     with open(paths[-1]) as f:
         d = json.load(f)
-    if d.get("bench_args", "").strip() not in ("", f"--config {args.config}"):
+    # flags that only switch the extra blocks off measure the same pipeline
+    extra = {"--no-host-input", "--no-per-record"}
+    words = [w for w in d.get("bench_args", "").split() if w not in extra]
+    if words not in ([], ["--config", args.config]):
         return None, None
     return int(d["hbm_bytes_per_batch"]), os.path.relpath(paths[-1], ROOT)
 

@@ -135,7 +135,12 @@ typedef struct {
   int32_t n_aggs;
   const int32_t *col_types;/* n_cols hsg_col_type                                        */
   const hsg_agg *aggs;     /* n_aggs output aggregates, in output order                  */
-  uint64_t state_capacity; /* HBM state rows (groups or sessions); 0 = engine default    */
+  uint64_t state_capacity; /* HBM state rows (groups or sessions) to start with; 0 = engine
+                            * default (2^21). Time-window tables then grow before a batch
+                            * that could pass 3/4 load: by the groups the batch makes on
+                            * the lean one-window path (which checks and, if short of
+                            * room, grows and runs the batch again), else by one group
+                            * per (record, window)                                      */
   uint64_t out_capacity;   /* changelog rows buffered in HBM between drains; 0 = default */
 } hsg_op_config;
 
