@@ -513,6 +513,10 @@ __global__ __launch_bounds__(256) void k_pane_apply(Program rprog, TwParams p, P
 // mid-round flush, no LAST) gets its changelog rows here instead.
 // ---------------------------------------------------------------------------
 constexpr int kSegClaimSet = 16384;  // claims per workgroup up to half of it (else workgroup-scope CAS)
+#ifndef HSG_SEG_NT
+#define HSG_SEG_NT 1024
+#endif
+constexpr int kSegNT = HSG_SEG_NT;  // threads per workgroup
 __device__ inline bool seg_claim_insert(uint32_t *cset, uint32_t slot) {
   uint32_t h = (slot * 0x9E3779B1u) >> (32 - 14);
   for (int probe = 0; probe < kSegClaimSet; ++probe) {
@@ -543,10 +547,10 @@ __device__ inline int64_t tw_claim_seg(const TwTable &t, uint64_t g, uint32_t *c
 }
 
 template <int MS, uint64_t SIG>
-__global__ __launch_bounds__(1024) void k_seg_apply(Program prog, TwParams p, PartParams pp, TwTable t, PartBuffers pb,
+__global__ __launch_bounds__(kSegNT) void k_seg_apply(Program prog, TwParams p, PartParams pp, TwTable t, PartBuffers pb,
                                                     OutCols out, uint64_t out_base, uint64_t out_cap, int lean,
                                                     DevScalars *sc) {
-  constexpr int NT = 1024;
+  constexpr int NT = kSegNT;
   __shared__ uint64_t s_red[NT / 64], s_tot[NT / 64];
   __shared__ uint32_t cset[kSegClaimSet];
   if (sc->redo || (lean && sc->packed)) return;  // uniform: late batch / the lean kernels took it
@@ -742,7 +746,7 @@ void launch_seg_apply(hipStream_t s, dim3 g, const Program &prog, const TwParams
   if (out) oc = *out;
   const int l = lean ? 1 : 0;
   const uint64_t sig = program_sig(prog);
-  const dim3 th(1024);
+  const dim3 th(kSegNT);
   if (sig == kSigCntSumI)
     hipLaunchKernelGGL((k_seg_apply<2, kSigCntSumI>), g, th, 0, s, prog, p, pp, t, pb, oc, out_base, out_cap, l, sc);
   else if (sig == kSigCntSumF)
