@@ -7,21 +7,30 @@ libhstream_gpu and drain each batch's changelog into HBM. Default workload =
 BASELINE config C2 (tumbling 60 s COUNT/SUM/AVG/MIN/MAX, 100M records, 64K
 uniform keys, batches of 2^24), which fits one GPU.
 
-`value` is the harness contract's number: input resident in HBM when the
-timed region starts. The same JSON line also carries, at one rank:
-  host_input  BASELINE.md's reporting formula ("kernels plus H2D of the
-              input"): the same step with the batches handed over as pinned
-              host buffers through hsg_push_batch_async, whose H2D copies run
-              on the op's copy stream, overlapped with the previous batch's
-              kernels (PCIe fraction of the 63 GB/s host link);
-  per_record  the EMIT CHANGES changelog the drop-in wires:
-              one row per (record, window) in arrival order, its B_alg with
-              the E*O changelog bytes.
+`value` follows BASELINE.md's reporting formula ("records/s, end to end over
+all batches, kernels plus H2D of the input"): the reference's operator is fed
+host poll batches (Processor.hs:128-144), so every step hands its batches over
+as pinned host buffers through hsg_push_batch_async; the library copies each
+batch to HBM on the op's copy stream while the batch before it computes, so a
+step costs max(PCIe, kernels). The batches use the ABI's narrow transport
+(include/hstream_gpu.h hsg_enc: ts as int32 offsets from the batch's first
+timestamp, the i64 value column as int32 -- C2's values are in [-1e9, 1e9];
+f64 columns of decimals as int32 mantissas), which a decoder that saw every
+value can choose for free; the library widens them on the device. The
+producer's choice of encoding is made before the timed region, as decoding
+is. The same JSON line also carries:
+  hbm_resident  the same steps with the input already resident in HBM
+                (hsg_push_batch on device columns): the kernels' own rate,
+                with the batch pipeline's roofline;
+  per_record    the EMIT CHANGES changelog the drop-in wires:
+                one row per (record, window) in arrival order, HBM-resident
+                input, its B_alg with the E*O changelog bytes.
+`--input hbm` makes the HBM-resident run the headline (the kernels alone).
 
 Multi-GPU: launched by torch.distributed.run, one process per GPU; every rank
-ingests its own C2-sized slice (weak scaling) and the library exchanges
-records by key hash over RCCL, so each GPU owns its key range's state.
-Rank 0 prints ONE JSON line.
+ingests its own C2-sized slice from host memory (weak scaling) and the library
+exchanges records by key hash over RCCL, so each GPU owns its key range's
+state. Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
@@ -45,13 +54,16 @@ def parse():
     p.add_argument("--records", type=int, default=0, help="records per rank per step (default: the config's N)")
     p.add_argument("--batch", type=int, default=0, help="records per push (default: the config's batch)")
     p.add_argument("--emit", default="per_batch", choices=["per_batch", "per_record", "none"])
+    p.add_argument("--input", default="host", choices=["host", "hbm"],
+                   help="headline input: pinned host batches, H2D timed (BASELINE.md), or HBM-resident")
+    p.add_argument("--wide", action="store_true", help="host input at full width (no narrow transport)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget (0 = skip)")
     p.add_argument("--traffic-csv", default="", help="rocprofv3 --pmc counter CSV to fill roofline.traffic")
     p.add_argument("--force-exchange", action="store_true", help="N=1 through the RCCL exchange path")
     p.add_argument("--copy-drain", action="store_true", help="drain by copy instead of the registered changelog")
-    p.add_argument("--no-host-input", action="store_true", help="skip the pinned-host-input (H2D) block")
+    p.add_argument("--no-hbm", action="store_true", help="skip the HBM-resident block (host headline only)")
     p.add_argument("--no-per-record", action="store_true", help="skip the per-record (EMIT CHANGES) block")
-    p.add_argument("--extra-steps", type=int, default=3, help="timed steps of the host_input / per_record blocks")
+    p.add_argument("--extra-steps", type=int, default=3, help="timed steps of the hbm_resident / per_record blocks")
     return p.parse_args()
 
 
@@ -96,10 +108,9 @@ def main():
     groups = n_rank * world if cfg.window_kind == abi.HSG_SESSION else 0
     spec = cfg.spec(emit, state_capacity=groups)
     op = eng.op(spec)
-    f64 = spec.agg_is_f64()
 
-    # synthetic input resident in HBM before timing: this rank's slice of every step
-    # every global batch = world consecutive pieces of `batch` records; rank r
+    # synthetic input: this rank's slice of every step, drawn into HBM; every
+    # global batch = world consecutive pieces of `batch` records, rank r
     # ingests piece r of each (the C3 layout: a contiguous 1/G of every batch)
     pieces = [(s, min(batch, n_rank - s)) for s in range(0, n_rank, batch)]
     parts = [datagen.generate_torch(cfg, m, device=dev, start=s * world + rank * m, total=cfg.n * world)
@@ -108,61 +119,52 @@ def main():
     ts = torch.cat([p["ts"] for p in parts])
     cols = [torch.cat([p["cols"][0] for p in parts])] if spec.col_types else []
     del parts
-    out_cap = max(1, eng_out_capacity(op))
-    outs = {
-        "key_id": torch.empty(out_cap, dtype=torch.int32, device=dev),
-        "win_start": torch.empty(out_cap, dtype=torch.int64, device=dev),
-        "win_end": torch.empty(out_cap, dtype=torch.int64, device=dev),
-        "src_index": torch.empty(out_cap, dtype=torch.int64, device=dev),
-        "aggs": [torch.empty(out_cap, dtype=torch.float64 if f else torch.int64, device=dev) for f in f64],
-    }
-    drain_dev = make_device_drain(op, outs, out_cap, zero_copy=not args.copy_drain)
-
-    # batch descriptors over the HBM-resident slices, built once (the timed loop
-    # is then one hsg_push_batch + one hsg_drain per batch)
-    import ctypes as C
-    from hstream_amd.columnar import make_batch
-    descs = [make_batch(keys[s:s + m], ts[s:s + m], [c[s:s + m] for c in cols], None, abi.HSG_MEM_DEVICE)
-             for s, m in pieces]
-    push_fn = op._lib.hsg_push_batch
-    wm_c = C.c_int64(-1)
-
-    def step():
-        op.reset()
-        wm_c.value = -1
-        for b, _keep in descs:
-            rc = push_fn(op._h, C.byref(b), C.byref(wm_c))
-            if rc != abi.HSG_OK:
-                op._check(rc, "push_batch")
-            if emit != abi.HSG_EMIT_NONE:
-                drain_dev()
-        return wm_c.value
-
     # the synthetic columns were produced on torch's stream, which the op's
     # stream is not ordered after (include/hstream_gpu.h, hsg_batch)
     torch.cuda.synchronize()
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    st0 = op.stats()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    st1 = op.stats()
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    def timed(step, warmup, steps):
+        for _ in range(warmup):
+            step()
+        barrier()
+        st0 = op.stats()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        barrier()
+        el = time.perf_counter() - t0
+        st1 = op.stats()
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return el, st0, st1
+
+    dev_step = device_steps(op, keys, ts, cols, pieces, emit, args)
+    hbm = None
+    if args.input == "host":
+        host_step, host_info = host_steps(op, keys, ts, cols, pieces, spec, emit, world, args)
+        elapsed, st0, st1 = timed(host_step, args.warmup, args.steps)
+        if not args.no_hbm:
+            el_h, h0, h1 = timed(dev_step, 1, max(1, args.extra_steps))
+            hbm = {"value": round(n_rank * world * max(1, args.extra_steps) / el_h, 1), "unit": "records/s",
+                   "steps": max(1, args.extra_steps), "ms_per_step": round(el_h * 1e3 / max(1, args.extra_steps), 3),
+                   "input": "HBM-resident device columns, one hsg_push_batch per batch",
+                   "roofline": roofline(h0, h1, spec, emit)}
+    else:
+        host_info = None
+        elapsed, st0, st1 = timed(dev_step, args.warmup, args.steps)
 
     total_records = n_rank * world * args.steps
     value = total_records / elapsed
 
+    # roofline of the batch pipeline (HIP events on the op's stream; the same
+    # kernels whichever way the input arrived)
     roof = roofline(st0, st1, spec, emit)
     traffic, tsrc = None, None
     if args.traffic_csv:
@@ -175,6 +177,17 @@ def main():
         roof["traffic_source"] = tsrc
     agg_s = (st1["agg_kernel_ms"] - st0["agg_kernel_ms"]) / 1e3
     touched = st1["touched_total"] - st0["touched_total"]
+
+    link = None
+    if host_info is not None:
+        h2d = host_info["bytes_per_step"] * args.steps
+        xt = torch.tensor([float(h2d)], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(xt, op=dist.ReduceOp.SUM)
+        gbs = float(xt[0]) / elapsed / 1e9
+        link = {"bound": "pcie", "achieved": round(gbs, 3), "peak": PCIE_PEAK_GBS * world, "unit": "GB/s",
+                "frac": round(gbs / (PCIE_PEAK_GBS * world), 4), "bytes_per_record": host_info["bytes_per_record"],
+                "encoding": host_info["encoding"], "changelog_groups": host_info["groups"]}
 
     xchg = None
     if world > 1 or args.force_exchange:
@@ -189,11 +202,10 @@ def main():
                 round(xs_sum * 1e3 / args.steps / world, 3),
                 "xgmi_frac": round(xb_all / elapsed / links, 6) if world > 1 else None}
 
-    host_in = per_rec = None
+    per_rec = None
+    table_slots, grow_events = int(st1["table_slots"]), int(st1["grow_events"])
     if world == 1 and not args.force_exchange:
-        if not args.no_host_input:
-            host_in = host_input_block(op, keys, ts, cols, pieces, spec, emit, args, value)
-        del descs
+        del dev_step
         op.close()
         op = None
         if (not args.no_per_record and cfg.window_kind in (abi.HSG_TUMBLING, abi.HSG_UNWINDOWED)
@@ -220,10 +232,13 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"{cfg.name}: {workload_text(cfg)}", "records_per_gpu": n_rank,
                        "batch": batch, "keys": cfg.keys, "emit": args.emit,
+                       "input": ("pinned host batches, H2D in the timed region (BASELINE.md reporting formula)"
+                                 if args.input == "host" else "HBM-resident device columns"),
                        "parallelism": f"key-hash sharded x{world}" if world > 1 else "single GPU"},
             "roofline": roof,
+            "input_link": link,
             "cpu_baseline": cpu,
-            "host_input": host_in,
+            "hbm_resident": hbm,
             "per_record": per_rec,
             "exchange": xchg,
             "agg_kernel_share": round(agg_s / elapsed, 4) if elapsed > 0 else None,
@@ -231,8 +246,8 @@ def main():
             "touched_per_step": int(touched / max(1, args.steps)),
             # HBM state table at the end of the run (slots of the time-window
             # table, or of the session key table) and its growth events
-            "table_slots": int(st1["table_slots"]),
-            "table_grow_events": int(st1["grow_events"]),
+            "table_slots": table_slots,
+            "table_grow_events": grow_events,
         }
         print(json.dumps(line), flush=True)
     if op is not None:
@@ -240,6 +255,158 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def device_steps(op, keys, ts, cols, pieces, emit, args):
+    """One step over HBM-resident input: reset, then per batch one
+    hsg_push_batch on device columns and one drain into HBM columns."""
+    import ctypes as C
+    import torch
+    from hstream_amd import abi
+    from hstream_amd.columnar import make_batch
+    spec = op.spec
+    out_cap = max(1, eng_out_capacity(op))
+    dev = keys.device
+    outs = {
+        "key_id": torch.empty(out_cap, dtype=torch.int32, device=dev),
+        "win_start": torch.empty(out_cap, dtype=torch.int64, device=dev),
+        "win_end": torch.empty(out_cap, dtype=torch.int64, device=dev),
+        "src_index": torch.empty(out_cap, dtype=torch.int64, device=dev),
+        "aggs": [torch.empty(out_cap, dtype=torch.float64 if f else torch.int64, device=dev)
+                 for f in spec.agg_is_f64()],
+    }
+    drain_dev = make_device_drain(op, outs, out_cap, zero_copy=not args.copy_drain)
+    # batch descriptors over the HBM-resident slices, built once (the timed loop
+    # is then one hsg_push_batch + one hsg_drain per batch)
+    descs = [make_batch(keys[s:s + m], ts[s:s + m], [c[s:s + m] for c in cols], None, abi.HSG_MEM_DEVICE)
+             for s, m in pieces]
+    push_fn = op._lib.hsg_push_batch
+    wm_c = C.c_int64(-1)
+
+    def step():
+        op.set_changelog(drain_dev.rows)  # (None with --copy-drain: the op's own buffer)
+        op.reset()
+        wm_c.value = -1
+        for b, _keep in descs:
+            rc = push_fn(op._h, C.byref(b), C.byref(wm_c))
+            if rc != abi.HSG_OK:
+                op._check(rc, "push_batch")
+            if emit != abi.HSG_EMIT_NONE:
+                drain_dev()
+        return wm_c.value
+
+    step.keep = (descs, outs, drain_dev)
+    return step
+
+
+def host_steps(op, keys, ts, cols, pieces, spec, emit, world, args):
+    """BASELINE.md's reporting formula: each step hands every batch over as
+    pinned host buffers (what a poll loop holds) through hsg_push_batch_async;
+    the library queues each batch's H2D copies on the op's copy stream while
+    the batch before it computes (op_prestage), so a step costs
+    max(PCIe, kernels). Narrow transport unless --wide: the producer's
+    encoding (columnar.narrow_columns) is chosen here, before any timing, as a
+    decoder chooses it while decoding. The changelog goes into device columns
+    registered for a group of batches and is drained after the group; a group
+    is the whole step unless the step's worst-case rows exceed 16 GB of HBM
+    (an asynchronous queue cannot be drained mid-way)."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    from hstream_amd import abi
+    from hstream_amd.columnar import make_batch, narrow_columns
+    descs, host = [], []
+    nbytes = 0
+    encs = set()
+    dec = [3 if t == abi.HSG_F64 else None for t in spec.col_types]  # the generators' decimals (datagen vrange)
+    for s, m in pieces:
+        k = keys[s:s + m].cpu().numpy()
+        t = ts[s:s + m].cpu().numpy()
+        cs = [c[s:s + m].cpu().numpy() for c in cols]
+        if args.wide:
+            tsa, base, cs2, enc, scale = t, None, cs, [abi.HSG_ENC_FULL] * len(cs), [0] * len(cs)
+        else:
+            tsa, base, cs2, enc, scale = narrow_columns(t, cs, spec.col_types, dec)
+        pk = torch.from_numpy(np.ascontiguousarray(k)).pin_memory()
+        pt = torch.from_numpy(np.ascontiguousarray(tsa)).pin_memory()
+        pc = [torch.from_numpy(np.ascontiguousarray(c)).pin_memory() for c in cs2]
+        b, keep = make_batch(pk.numpy(), pt.numpy(), [c.numpy() for c in pc], None, abi.HSG_MEM_HOST,
+                             ts_base=base, col_enc=enc, col_scale=scale)
+        descs.append(b)
+        host.append((pk, pt, pc, keep))
+        nbytes += m * 4 + pt.element_size() * m + sum(c.element_size() * m for c in pc)
+        encs.add(("ts32" if base is not None else "ts64") + "+" + ",".join(
+            {abi.HSG_ENC_FULL: "full", abi.HSG_ENC_I32: "i32", abi.HSG_ENC_DEC32: "dec32"}[e] for e in enc))
+    n_rank = sum(m for _, m in pieces)
+    wpr = -(-spec.size_ms // spec.advance_ms) if spec.window_kind == abi.HSG_HOPPING else 1
+    row_bytes = 4 + 8 + 8 + 8 + 8 * len(spec.aggs)
+    dev = keys.device
+    state = {"cap": 0, "group": len(descs), "drain": None, "outs": None}
+
+    def plan():
+        # rows the library reserves per batch (op_push): n * ranks * wpr, per-batch
+        # mode capped by the table's slots
+        per = [m * world * wpr for _, m in pieces]
+        if emit == abi.HSG_EMIT_PER_BATCH and spec.window_kind != abi.HSG_SESSION:
+            slots = max(1, int(op.stats()["table_slots"])) + max(64, int(op.stats()["table_slots"]) // 8)
+            per = [min(x, slots) for x in per]
+        if emit == abi.HSG_EMIT_NONE:
+            return 1, len(descs)
+        budget = 16 << 30
+        g = len(descs)
+        while g > 1 and max(per) * g * row_bytes > budget:
+            g -= 1
+        return max(per) * g, g
+
+    def ensure(cap):
+        if cap <= state["cap"]:
+            return
+        state["outs"] = None
+        state["drain"] = None
+        torch.cuda.empty_cache()
+        outs = {"key_id": torch.empty(cap, dtype=torch.int32, device=dev),
+                "win_start": torch.empty(cap, dtype=torch.int64, device=dev),
+                "win_end": torch.empty(cap, dtype=torch.int64, device=dev),
+                "src_index": torch.empty(cap, dtype=torch.int64, device=dev),
+                "aggs": [torch.empty(cap, dtype=torch.float64 if f else torch.int64, device=dev)
+                         for f in spec.agg_is_f64()]}
+        state["outs"] = outs
+        state["drain"] = make_device_drain(op, outs, cap, zero_copy=True, register=False)
+        state["cap"] = cap
+
+    lib = op._lib
+    wm = C.c_int64(-1)
+    no_cb = C.cast(None, abi.HSG_DONE_FN)  # no completion callback: hsg_op_wait below
+
+    def step():
+        cap, g = plan()
+        ensure(cap)
+        state["group"] = g
+        if emit != abi.HSG_EMIT_NONE:
+            op.set_changelog(state["drain"].rows)
+        op.reset()
+        wm.value = -1
+        for i0 in range(0, len(descs), g):
+            for b in descs[i0:i0 + g]:
+                rc = lib.hsg_push_batch_async(op._h, C.byref(b), C.byref(wm), no_cb, None)
+                if rc != abi.HSG_OK:
+                    op._check(rc, "push_batch_async")
+            rc = lib.hsg_op_wait(op._h)
+            if rc != abi.HSG_OK:
+                op._check(rc, "op_wait")
+            if emit != abi.HSG_EMIT_NONE:
+                state["drain"]()
+
+    step.keep = (descs, host, state)
+    info = {"bytes_per_step": nbytes, "bytes_per_record": round(nbytes / max(1, n_rank), 3),
+            "encoding": sorted(encs), "groups": None}
+
+    class Info(dict):
+        def __getitem__(self, k):
+            if k == "groups":
+                return -(-len(descs) // state["group"])
+            return dict.__getitem__(self, k)
+    return step, Info(info)
 
 
 def roofline(st0, st1, spec, emit):
@@ -269,73 +436,6 @@ def roofline(st0, st1, spec, emit):
             "alg_bytes_per_launch": int(alg_bytes / max(1, launches)),
             "rows_emitted_per_launch": int(emitted / max(1, launches)),
             "avg_launch_ms": round(agg_s * 1e3 / max(1, launches), 4)}
-
-
-def host_input_block(op, keys, ts, cols, pieces, spec, emit, args, hbm_value):
-    """BASELINE.md's reporting formula: the same steps with every batch handed
-    over as pinned host buffers (what a poll loop holds) through
-    hsg_push_batch_async. The library queues each batch's H2D copies on the
-    op's copy stream while the batch before it computes (op_prestage), so a
-    step costs max(PCIe, kernels) rather than their sum. The step's changelog
-    goes into device columns registered for the whole step, drained once."""
-    import ctypes as C
-    import torch
-    from hstream_amd import abi
-    from hstream_amd.columnar import make_batch
-    kh = keys.cpu().pin_memory()
-    th = ts.cpu().pin_memory()
-    chs = [c.cpu().pin_memory() for c in cols]
-    descs = [make_batch(kh[s:s + m], th[s:s + m], [c[s:s + m] for c in chs], None, abi.HSG_MEM_HOST)
-             for s, m in pieces]
-    wpr = -(-spec.size_ms // spec.advance_ms) if spec.window_kind == abi.HSG_HOPPING else 1
-    n_rank = sum(m for _, m in pieces)
-    cap = max(1, n_rank * wpr) if emit != abi.HSG_EMIT_NONE else 1
-    dev = keys.device
-    outs = {"key_id": torch.empty(cap, dtype=torch.int32, device=dev),
-            "win_start": torch.empty(cap, dtype=torch.int64, device=dev),
-            "win_end": torch.empty(cap, dtype=torch.int64, device=dev),
-            "src_index": torch.empty(cap, dtype=torch.int64, device=dev),
-            "aggs": [torch.empty(cap, dtype=torch.float64 if f else torch.int64, device=dev) for f in spec.agg_is_f64()]}
-    drain = make_device_drain(op, outs, cap, zero_copy=True)
-    lib = op._lib
-    wm = C.c_int64(-1)
-    no_cb = C.cast(None, abi.HSG_DONE_FN)  # no completion callback: hsg_op_wait below
-
-    def step():
-        op.reset()
-        wm.value = -1
-        for b, _keep in descs:
-            rc = lib.hsg_push_batch_async(op._h, C.byref(b), C.byref(wm), no_cb, None)
-            if rc != abi.HSG_OK:
-                op._check(rc, "push_batch_async")
-        rc = lib.hsg_op_wait(op._h)
-        if rc != abi.HSG_OK:
-            op._check(rc, "op_wait")
-        if emit != abi.HSG_EMIT_NONE:
-            drain()
-
-    torch.cuda.synchronize()
-    step()
-    torch.cuda.synchronize()
-    k = max(1, args.extra_steps)
-    t0 = time.perf_counter()
-    for _ in range(k):
-        step()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    op.set_changelog(None)
-    rec_bytes = 4 + 8 + 8 * len(spec.col_types)
-    h2d = n_rank * rec_bytes * k
-    out = {"value": round(n_rank * k / el, 1), "unit": "records/s", "steps": k,
-           "ms_per_step": round(el * 1e3 / k, 3),
-           "input": "pinned host buffers, one hsg_push_batch_async per batch (H2D in the timed region)",
-           "h2d_bytes_per_step": n_rank * rec_bytes,
-           "pcie": {"achieved": round(h2d / el / 1e9, 3), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(h2d / el / 1e9 / PCIE_PEAK_GBS, 4)},
-           "vs_hbm_resident": round(n_rank * k / el / hbm_value, 4) if hbm_value else None}
-    del descs, kh, th, chs, outs
-    torch.cuda.empty_cache()
-    return out
 
 
 def per_record_block(eng, cfg, keys, ts, cols, pieces, args):
@@ -414,9 +514,10 @@ def eng_out_capacity(op):
         -(-spec.size_ms // spec.advance_ms) if spec.window_kind == abi.HSG_HOPPING else 1)
 
 
-def make_device_drain(op, outs, cap, zero_copy=True):
+def make_device_drain(op, outs, cap, zero_copy=True, register=True):
     """Drain each batch's changelog into HBM-resident columns: registered with
-    hsg_op_set_changelog (rows written in place, drain = count) or, with
+    hsg_op_set_changelog (rows written in place, drain = count; register=False
+    leaves the registration to the caller, through .rows) or, with
     --copy-drain, copied by hsg_drain from the op's own buffer."""
     import ctypes as C
     from hstream_amd import abi
@@ -427,7 +528,8 @@ def make_device_drain(op, outs, cap, zero_copy=True):
                         aggs=C.cast(agg_ptrs, C.POINTER(C.c_void_p)))
     got = C.c_uint64(0)
     if zero_copy:
-        op.set_changelog(rows)
+        if register:
+            op.set_changelog(rows)
 
         def drain_in_place():
             rc = op._lib.hsg_drain(op._h, None, C.byref(got))
@@ -436,6 +538,7 @@ def make_device_drain(op, outs, cap, zero_copy=True):
             return got.value
 
         drain_in_place.keep = (agg_ptrs, rows, outs)
+        drain_in_place.rows = rows
         return drain_in_place
 
     def drain():
@@ -445,6 +548,7 @@ def make_device_drain(op, outs, cap, zero_copy=True):
         return got.value
 
     drain.keep = (agg_ptrs, rows, outs)
+    drain.rows = None
     return drain
 
 
@@ -480,7 +584,7 @@ def committed_traffic(args, world):
     with open(paths[-1]) as f:
         d = json.load(f)
     # flags that only switch the extra blocks off measure the same pipeline
-    extra = {"--no-host-input", "--no-per-record"}
+    extra = {"--no-host-input", "--no-per-record", "--no-hbm", "--input", "hbm"}
     words = [w for w in d.get("bench_args", "").split() if w not in extra]
     if words not in ([], ["--config", args.config]):
         return None, None

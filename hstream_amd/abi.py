@@ -57,6 +57,12 @@ HSG_LAST = 6
 HSG_MEM_HOST = 0
 HSG_MEM_DEVICE = 1
 
+# narrow transport encodings (hsg_batch ts_enc / col_enc)
+HSG_ENC_FULL = 0
+HSG_ENC_TS32 = 1
+HSG_ENC_I32 = 2
+HSG_ENC_DEC32 = 3
+
 
 class hsg_engine_config(C.Structure):
     _fields_ = [
@@ -100,6 +106,11 @@ class hsg_batch(C.Structure):
         ("cols", C.POINTER(C.c_void_p)),
         ("valid", C.POINTER(C.c_void_p)),
         ("ready_event", C.c_void_p),
+        ("ts_enc", C.c_int32),
+        ("reserved", C.c_int32),
+        ("ts_base", C.c_int64),
+        ("col_enc", C.c_uint8 * 8),
+        ("col_scale", C.c_uint8 * 8),
     ]
 
 
@@ -142,6 +153,8 @@ class hsg_stats(C.Structure):
         ("lean_batches", C.c_uint64),
         ("direct_batches", C.c_uint64),
         ("replays", C.c_uint64),
+        ("overflow_rows", C.c_uint64),
+        ("overflow_rebuilds", C.c_uint64),
     ]
 
     def as_dict(self):

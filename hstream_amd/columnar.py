@@ -70,19 +70,24 @@ def _ptr(x):
     return x.ctypes.data
 
 
-def make_batch(key_id, ts, cols=(), valid=None, mem=None):
+def make_batch(key_id, ts, cols=(), valid=None, mem=None, ts_base=None, col_enc=None, col_scale=None):
     """Build an hsg_batch over numpy arrays (host) or torch tensors (device).
 
     Returns (hsg_batch, keepalive). Arrays must be contiguous: key_id uint32 /
     int32, ts int64, cols int64 or float64, valid uint8 (or None = all present).
+    Narrow transport (include/hstream_gpu.h hsg_enc): ts_base given = ts holds
+    int32 offsets from it (HSG_ENC_TS32); col_enc[c] HSG_ENC_I32 / HSG_ENC_DEC32
+    = column c holds int32 values / decimal mantissas (col_scale[c] digits).
     """
     if mem is None:
         mem = abi.HSG_MEM_DEVICE if (_is_torch(ts) and ts.is_cuda) else abi.HSG_MEM_HOST
+    col_enc = list(col_enc or [abi.HSG_ENC_FULL] * len(cols))
     keep = [key_id, ts]
     if not _is_torch(ts):
         key_id = np.ascontiguousarray(key_id, dtype=np.uint32)
-        ts = np.ascontiguousarray(ts, dtype=np.int64)
-        cols = [np.ascontiguousarray(c) for c in cols]
+        ts = np.ascontiguousarray(ts, dtype=np.int32 if ts_base is not None else np.int64)
+        cols = [np.ascontiguousarray(c, dtype=np.int32) if e != abi.HSG_ENC_FULL else np.ascontiguousarray(c)
+                for c, e in zip(cols, col_enc)]
         if valid is not None:
             valid = [None if v is None else np.ascontiguousarray(v, dtype=np.uint8) for v in valid]
         keep = [key_id, ts, cols, valid]
@@ -106,7 +111,45 @@ def make_batch(key_id, ts, cols=(), valid=None, mem=None):
         cols=C.cast(col_ptrs, C.POINTER(C.c_void_p)),
         valid=C.cast(valid_ptrs, C.POINTER(C.c_void_p)) if valid_ptrs is not None else None,
     )
+    if ts_base is not None:
+        b.ts_enc = abi.HSG_ENC_TS32
+        b.ts_base = int(ts_base)
+    for c, e in enumerate(col_enc):
+        b.col_enc[c] = int(e)
+        b.col_scale[c] = int(col_scale[c]) if col_scale else 0
     return b, keep
+
+
+def narrow_columns(ts, cols, col_types, dec_scale=None):
+    """What a producer that saw every value (the decoder) can send narrower:
+    ts as int32 offsets from the batch's minimum when its span fits, i64
+    columns as int32 when every value fits, f64 columns as int32 decimal
+    mantissas when every value is a decimal of at most dec_scale[c] digits that
+    fits (checked exactly: m / 10^s must give back the value). Returns
+    (ts_arr, ts_base or None, cols, col_enc, col_scale); host numpy arrays."""
+    ts = np.asarray(ts, dtype=np.int64)
+    ts_base = None
+    if ts.size:
+        lo, hi = int(ts.min()), int(ts.max())
+        if hi - lo < 2**31:
+            ts_base = lo
+            ts = (ts - lo).astype(np.int32)
+    out, enc, scale = [], [], []
+    for j, (c, t) in enumerate(zip(cols, col_types)):
+        c = np.asarray(c)
+        e, sc = abi.HSG_ENC_FULL, 0
+        if t == abi.HSG_I64:
+            if c.size == 0 or (int(c.min()) >= -2**31 and int(c.max()) < 2**31):
+                c, e = c.astype(np.int32), abi.HSG_ENC_I32
+        elif dec_scale and dec_scale[j] is not None:
+            s = int(dec_scale[j])
+            m = np.rint(c * 10.0**s)
+            if c.size == 0 or (np.abs(m).max() < 2**31 and np.array_equal(m / 10.0**s, c)):
+                c, e, sc = m.astype(np.int32), abi.HSG_ENC_DEC32, s
+        out.append(c)
+        enc.append(e)
+        scale.append(sc)
+    return ts, ts_base, out, enc, scale
 
 
 @dataclass
@@ -186,8 +229,9 @@ class OpHandle:
             msg = msg.decode() if msg else ""
             raise abi.HStreamGpuError(rc, f"{what}: {msg}")
 
-    def push(self, key_id, ts, cols=(), valid=None, watermark=-1, mem=None) -> int:
-        b, keep = make_batch(key_id, ts, cols, valid, mem)
+    def push(self, key_id, ts, cols=(), valid=None, watermark=-1, mem=None, **enc) -> int:
+        """hsg_push_batch; enc = make_batch's narrow transport (ts_base, col_enc, col_scale)."""
+        b, keep = make_batch(key_id, ts, cols, valid, mem, **enc)
         wm = C.c_int64(watermark)
         rc = self._fn("push_batch")(self._h, C.byref(b), C.byref(wm))
         del keep

@@ -131,7 +131,7 @@ static int push_sharded_fast(OpDevice &d, const hsg_op_config &cfg, const Progra
     return HSG_E_CAPACITY;
   }
   Batch kb;
-  int rc = stage_batch(d, a.batch, kb, err);
+  int rc = stage_batch(d, a.batch, kb, err, a.staged_set);
   if (rc != HSG_OK) return rc;
   bool has_valid = false;
   for (int c = 0; c < cfg.n_cols; ++c) has_valid = has_valid || kb.valid[c] != nullptr;
@@ -293,7 +293,7 @@ static int push_sharded_classic(OpDevice &d, const hsg_op_config &cfg, const Pro
   }
   // 1. stage this rank's slice and compute local facts
   Batch kb;
-  int rc = stage_batch(d, a.batch, kb, err);
+  int rc = stage_batch(d, a.batch, kb, err, a.staged_set);
   if (rc != HSG_OK) return rc;
   bool has_valid = false;
   for (int c = 0; c < cfg.n_cols; ++c) has_valid = has_valid || kb.valid[c] != nullptr;

@@ -232,12 +232,12 @@ struct hsg_op {
 
 static int push_sync(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark, int staged_set = -1);
 
-// Queue the H2D copies of a queued host batch (single-GPU ops) so that they
+// Queue the H2D copies of a queued host batch so that they
 // overlap the batch before it; the sets alternate, so the set a prestage
 // fills was last read by a push that has completed (pushes are synchronous on
 // the op's completion thread). Failure only means the push stages itself.
 static void prestage_job(hsg_op *op, AsyncJob &job) {
-  if (job.staged_set >= 0 || op->comm || job.b.mem != HSG_MEM_HOST || job.b.n == 0) return;
+  if (job.staged_set >= 0 || job.b.mem != HSG_MEM_HOST || job.b.n == 0) return;
   if (job.b.n > op->eng->batch_cap || job.b.n_cols != op->cfg.n_cols || !job.b.key_id || !job.b.ts)
     return;  // push_sync reports it
   hsg_batch b = job.b;
@@ -429,6 +429,15 @@ static int validate_batch(hsg_op *op, const hsg_batch *b, const int64_t *inout_w
   if (b->n && (!b->key_id || !b->ts)) return fail(op->err, HSG_E_INVALID, "null key_id / ts");
   for (int c = 0; c < b->n_cols; ++c)
     if (b->n && (!b->cols || !b->cols[c])) return fail(op->err, HSG_E_INVALID, "null value column");
+  // narrow transport (hsg_enc): ts as TS32 only, i64 columns as I32, f64 columns as DEC32
+  if (b->ts_enc != HSG_ENC_FULL && b->ts_enc != HSG_ENC_TS32) return fail(op->err, HSG_E_INVALID, "bad ts_enc");
+  for (int c = 0; c < b->n_cols; ++c) {
+    const int e = b->col_enc[c];
+    const bool f64 = op->col_types[c] == HSG_F64;
+    if (e != HSG_ENC_FULL && e != (f64 ? HSG_ENC_DEC32 : HSG_ENC_I32))
+      return fail(op->err, HSG_E_INVALID, "bad col_enc for the column's type");
+    if (e == HSG_ENC_DEC32 && b->col_scale[c] > 18) return fail(op->err, HSG_E_INVALID, "col_scale > 18");
+  }
   return HSG_OK;
 }
 
@@ -473,6 +482,8 @@ static int push_sync(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark, i
     op->stats.lean_batches = op->dev.lean_batches;
     op->stats.direct_batches = op->dev.direct_batches;
     op->stats.replays = op->dev.replays;
+    op->stats.overflow_rows = op->dev.ovf_rows;
+    op->stats.overflow_rebuilds = op->dev.ovf_events;
     op->stats.pending_rows = op->pending;
     op->stats.last_batch_ms = now_ms() - t0;
     op->stats.agg_kernel_ms += res.agg_ms;

@@ -98,7 +98,8 @@ struct DevScalars {
   uint64_t kbase;        // packed layout: window (relative to the epoch) the 16-bit window offsets count from
   uint64_t scratch[45];  // [0] groups flushed (partition path), [1] touched-list length, [8..20] phase clocks,
                          // [21..22] optimistic pass ts extrema, [31] lean partials of the batch (bound on
-                         // its new groups), [32] held back for table room: bit 0 lean apply, bit 1 general
+                         // its new groups), [32] held back for table room: bit 0 lean apply, bit 1 general,
+                         // [33] groups claimed in the table's overflow rows (TwTable::ovf)
   uint64_t live_x[8];    // more rows found, one shard per XCD (blockIdx & 7) for kernels whose every
                          // workgroup adds; the host folds them into `live` when it fetches the scalars
 };
@@ -134,14 +135,18 @@ struct Batch {
 // 128-byte line). The home slot keeps the 8 windows of an aligned window block
 // of one key in 8 consecutive rows (see tw_home).
 struct TwTable {
-  uint64_t *rows;   // [cap][stride]
-  uint64_t mask;    // cap - 1
+  uint64_t *rows;   // [cap + overflow][stride]
+  uint64_t mask;    // cap - 1 (the region slots)
   uint32_t stride;  // words per row
   uint32_t blocked; // window-block home slots, probe step 8 (windowed ops with >= 8 slots)
   uint64_t rmask;   // slots per region - 1 (regions = 2^rbits, see hsg_tw.h)
   int32_t rbits;    // region bits of the key hash (below the owner bits)
   int32_t bshift;   // owner bits of the key hash (multi-GPU)
-  uint8_t *dirty;   // [cap / 8]: 8-slot blocks claimed since the last clear (null: not kept)
+  uint8_t *dirty;   // [slots() / 8]: 8-slot blocks claimed since the last clear (null: not kept)
+  uint64_t omask;   // overflow slots - 1: rows [cap, cap + omask + 1) take the groups whose
+                    // region probe found no free slot (hsg_tw.h tw_ovf_claim)
+  uint64_t *ovf;    // device counter of overflow claims (DevScalars scratch[33]: per batch)
+  __host__ __device__ uint64_t slots() const { return mask + 1 + omask + 1; }
   __host__ __device__ uint64_t *key(uint64_t s) const { return rows + s * stride; }
   // every claim marks its block, so a clear rewrites only the claimed blocks
   __device__ void mark(uint64_t s) const {
@@ -150,6 +155,9 @@ struct TwTable {
   __host__ __device__ uint32_t *stamp(uint64_t s) const { return (uint32_t *)(rows + s * stride + 1); }
   __host__ __device__ int64_t *aggs(uint64_t s) const { return (int64_t *)(rows + s * stride + 2); }
 };
+
+// overflow rows after a table of `cap` region slots: 1/8 of it (>= 64)
+inline uint64_t tw_ovf_slots(uint64_t cap) { return cap / 8 > 64 ? cap / 8 : 64; }
 
 inline uint32_t tw_row_stride(int n_slots) {
   uint32_t w = 2u + (uint32_t)n_slots, s = 4;
@@ -242,6 +250,24 @@ void launch_tw_reset_dirty(hipStream_t s, const TwTable &t, const Program &prog,
 // one byte per 8-slot block, padded to 16 bytes
 inline uint64_t tw_dirty_bytes(uint64_t cap) { return ((cap >> 3) + 16) & ~15ull; }
 void launch_fill_u32(hipStream_t s, uint32_t *p, uint64_t n, uint32_t v);
+
+// narrow transport columns of a batch (include/hstream_gpu.h hsg_enc) into
+// the op's full-width staging, on the device after the H2D
+struct WidenArgs {
+  uint64_t n;
+  const int32_t *ts32;           // null: ts is not narrow
+  int64_t ts_base;
+  int64_t *ts;
+  const int32_t *c32[kMaxCols];  // null: the column is not narrow
+  int64_t *col[kMaxCols];        // int64 words (i64 or f64 bits)
+  double div[kMaxCols];          // HSG_ENC_DEC32: 10^scale; 0: HSG_ENC_I32
+};
+void launch_widen(hipStream_t s, const WidenArgs &w);
+inline bool batch_narrow(const hsg_batch *b) {
+  bool any = b->ts_enc != HSG_ENC_FULL;
+  for (int c = 0; c < b->n_cols && c < kMaxCols; ++c) any |= b->col_enc[c] != HSG_ENC_FULL;
+  return any;
+}
 
 // stream time: tile maxima -> exclusive tile prefix (+ epoch init)
 void launch_tile_stats(hipStream_t s, const Batch &b, int64_t *tile_max, int64_t *tile_min, uint64_t n_tiles);

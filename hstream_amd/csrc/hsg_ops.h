@@ -84,7 +84,9 @@ struct OpDevice {
   uint8_t *st_valid[kMaxCols] = {};
   int64_t *st_seq = nullptr;    // global record seq of received records (multi-GPU)
   int64_t *st_wm = nullptr;     // per-record watermark of received records (multi-GPU)
-  // prestaged host batches of asynchronous pushes (single-GPU ops): the H2D
+  int32_t *nar_ts = nullptr;    // narrow transport staging of synchronous host pushes (hsg_enc)
+  int32_t *nar_col[kMaxCols] = {};
+  // prestaged host batches of asynchronous pushes: the H2D
   // copies of the next queued batch run on their own stream, into the other
   // of two staging sets, while the current batch computes (op_prestage)
   struct Staging {
@@ -98,7 +100,11 @@ struct OpDevice {
   hipEvent_t ev_h2d[2] = {nullptr, nullptr};
   // time windows
   TwTable tw = {};
-  uint64_t cap = 0;             // table slots
+  uint64_t cap = 0;             // table slots (regions; tw.slots() adds the overflow rows)
+  uint64_t ovf_rows = 0;        // groups in the overflow rows (a region was full): the next batch
+                                // first rebuilds the table with twice the slots and larger regions
+  int region_log2 = 12;         // log2 of the smallest region (raised by each overflow rebuild)
+  uint64_t ovf_events = 0;      // rebuilds an overflow caused
   EmitScratch emit = {};
   // partitioned aggregation (hsg_part.h)
   PartBuffers part = {};
@@ -188,7 +194,7 @@ void op_device_free(OpDevice &d);
 int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err);
 int op_push(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, PushResult &r,
             std::string &err);
-// Queue the H2D copies of a host batch (single-GPU ops) into staging set
+// Queue the H2D copies of a host batch into staging set
 // `set` on the op's copy stream; the push that names the set (PushArgs::
 // staged_set) waits for them on the op's stream. The set must not be in use
 // by a push still running.
@@ -199,7 +205,7 @@ int op_copy_rows(OpDevice &d, const OutCols &src, uint64_t from, uint64_t n, int
 
 // retention (retention.cpp)
 // table geometry for `cap` slots (stride and bshift kept)
-void tw_configure(TwTable &t, uint64_t cap, int window_kind);
+void tw_configure(TwTable &t, uint64_t cap, int window_kind, int region_log2 = 12);
 // Before a time-window batch of n_in records at stream time wm_in: when the
 // table could pass 3/4 load, move closed windows to the host and rebuild the
 // table (growing it until the open rows plus the batch's bound fit at 1/2).

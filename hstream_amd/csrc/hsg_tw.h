@@ -35,8 +35,63 @@ __device__ inline uint64_t tw_step(const TwTable &t) { return t.blocked ? 8 : 1;
 // the table is (nearly) full; report that instead of scanning all of HBM.
 constexpr uint64_t kMaxProbes = 1ull << 14;
 
-// Returns the slot of group g, inserting it if absent; -1 when its region is
-// full. A plain load is only a hint (a stale EMPTY costs one failed CAS); the
+// Overflow rows. A region's sub-table can fill while the table as a whole is
+// moderately loaded (a few keys with many open windows each, or a region that
+// drew more than its share of keys). The group then goes to the overflow rows
+// after the regions, a plain linear-probing table every workgroup may claim
+// in with device-scope CAS (only the group's owner ever updates its row, as
+// in the regions). The reference's store never refuses a row (ksPut =
+// Map.insert, Store.hs:66-68), so neither does a region: every claim that
+// counts here makes the host rebuild the table with larger regions before the
+// next batch (retention.cpp tw_maintain). Invariant: a group is in the
+// overflow only if the probe of its sub-table found no free slot, and slots
+// are never freed between rebuilds, so a lookup whose probe meets a free slot
+// stops there and one whose probe ends without meeting one continues here.
+__device__ inline uint64_t tw_ovf_home(const TwTable &t, uint64_t g) {
+  return mix64(g ^ 0x5851F42D4C957F2Dull) & t.omask;
+}
+__device__ inline int64_t tw_ovf_claim(const TwTable &t, uint64_t g, uint32_t &fresh) {
+  const uint64_t base = t.mask + 1;
+  uint64_t s = tw_ovf_home(t, g);
+  for (uint64_t probe = 0; probe <= t.omask && probe < kMaxProbes; ++probe) {
+    uint64_t *kp = t.key(base + s);
+    const uint64_t cur = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == g) return (int64_t)(base + s);
+    if (cur == kEmpty) {
+      const uint64_t old = atomicCAS((unsigned long long *)kp, (unsigned long long)kEmpty, (unsigned long long)g);
+      if (old == kEmpty) {
+        t.mark(base + s);
+        fresh += 1;
+        atomicAdd((unsigned long long *)t.ovf, 1ull);
+        return (int64_t)(base + s);
+      }
+      if (old == g) return (int64_t)(base + s);
+    }
+    s = (s + 1) & t.omask;
+  }
+  return -1;  // the overflow rows are full too: ERR_OOM
+}
+// the same, reporting a claim through isnew instead of a counter
+__device__ inline int64_t tw_ovf_claim_new(const TwTable &t, uint64_t g, bool &isnew) {
+  uint32_t f = 0;
+  const int64_t s = tw_ovf_claim(t, g, f);
+  isnew = f != 0;
+  return s;
+}
+__device__ inline int64_t tw_ovf_find(const TwTable &t, uint64_t g) {
+  const uint64_t base = t.mask + 1;
+  uint64_t s = tw_ovf_home(t, g);
+  for (uint64_t probe = 0; probe <= t.omask && probe < kMaxProbes; ++probe) {
+    const uint64_t cur = __hip_atomic_load(t.key(base + s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == g) return (int64_t)(base + s);
+    if (cur == kEmpty) return -1;
+    s = (s + 1) & t.omask;
+  }
+  return -1;
+}
+
+// Returns the slot of group g, inserting it if absent (in the overflow rows
+// when its region's sub-table is full); -1 only when those are full too. A plain load is only a hint (a stale EMPTY costs one failed CAS); the
 // CAS result is authoritative, and a slot moves EMPTY -> g once per reset.
 __device__ inline int64_t tw_find_or_insert(const TwTable &t, uint64_t g, uint32_t &fresh) {
   const uint64_t base = tw_region_base(t, g);
@@ -57,7 +112,7 @@ __device__ inline int64_t tw_find_or_insert(const TwTable &t, uint64_t g, uint32
     }
     s = (s + step) & t.rmask;
   }
-  return -1;
+  return tw_ovf_claim(t, g, fresh);
 }
 
 // Same, for the only workgroup writing g's region in this launch: its threads
@@ -83,7 +138,7 @@ __device__ inline int64_t tw_claim_exclusive(const TwTable &t, uint64_t g, uint3
     }
     s = (s + step) & t.rmask;
   }
-  return -1;
+  return tw_ovf_claim(t, g, fresh);
 }
 
 // Lookup only (after the aggregation pass has inserted every group).
@@ -97,7 +152,7 @@ __device__ inline int64_t tw_find(const TwTable &t, uint64_t g) {
     if (cur == kEmpty) return -1;
     s = (s + step) & t.rmask;
   }
-  return -1;
+  return tw_ovf_find(t, g);  // the probe met no free slot
 }
 
 }  // namespace hsg

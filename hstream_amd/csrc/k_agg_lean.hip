@@ -290,7 +290,7 @@ __device__ inline int64_t tw_claim_lds(const TwTable &t, uint64_t g, uint32_t *c
     }
     s = (s + step) & t.rmask;
   }
-  return -1;
+  return tw_ovf_claim(t, g, fresh);  // the region's sub-table is full
 }
 
 // One workgroup per aggregation workgroup: its partials into the HBM table.
@@ -543,7 +543,7 @@ __device__ inline int64_t tw_claim_seg(const TwTable &t, uint64_t g, uint32_t *c
     }
     s = (s + step) & t.rmask;
   }
-  return -1;
+  return tw_ovf_claim(t, g, fresh);  // the region's sub-table is full
 }
 
 template <int MS, uint64_t SIG>

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(kTileThreads) void k_pr_pairs(Batch b, TwParams p, 
           uint64_t g = ((uint64_t)key[r] << 32) | (uint64_t)krel;
           int64_t slot = tw_find_or_insert(t, g, fresh);
           uint32_t s32;
-          if (slot < 0) { err |= ERR_OOM; s32 = (uint32_t)(t.mask + 1); }
+          if (slot < 0) { err |= ERR_OOM; s32 = (uint32_t)t.slots(); }
           else { s32 = (uint32_t)slot; *t.stamp(slot) = (uint32_t)p.batch_id; }
           pb.pslot[o + c] = s32;
           pb.pidx[o + c] = (uint32_t)(o + c);
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_apply(Batch b, Program prog
                                                            OutCols out, uint64_t out_base, DevScalars *sc) {
   __shared__ uint64_t sseg[4];
   const uint64_t q0 = (uint64_t)blockIdx.x * kSegTile + (uint64_t)threadIdx.x * kSegItems;
-  const uint64_t cap = t.mask + 1;
+  const uint64_t cap = t.slots();  // region + overflow slots; a pair without one has slot cap
   const int64_t k_epoch = sc->k_epoch;
   const bool unwin = p.kind == HSG_UNWINDOWED;
   // phase 1: thread-local aggregate
@@ -365,7 +365,7 @@ static void seg_launch(hipStream_t s, const Batch &b, const Program &prog, const
   hipLaunchKernelGGL(k_seg_carry<MS>, dim3(1), dim3(1024), 0, s, prog, pb.blk_v, pb.blk_f, nb, pb.carry);
   hipLaunchKernelGGL(k_seg_apply<MS>, dim3((unsigned)nb), dim3(kSegThreads), 0, s, b, prog, pb, p, t, slot, pidx, P,
                      seq, pb.carry, out, out_base, sc);
-  hipLaunchKernelGGL(k_seg_commit, dim3(grid_for(P, 256)), dim3(256), 0, s, slot, P, t.mask + 1, prog.n_slots,
+  hipLaunchKernelGGL(k_seg_commit, dim3(grid_for(P, 256)), dim3(256), 0, s, slot, P, t.slots(), prog.n_slots,
                      pb.shadow, t);
 }
 

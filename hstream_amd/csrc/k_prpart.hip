@@ -435,6 +435,10 @@ __global__ __launch_bounds__(256) void k_pr_carry(Program prog, TwParams p, Part
         }
         sl = (sl + step) & t.rmask;
       }
+      if (slot < 0) {  // the region's sub-table is full
+        slot = tw_ovf_claim_new(t, g, isnew);
+        fresh += isnew ? 1 : 0;
+      }
       if (slot < 0) {
         err |= ERR_OOM;
         identity_row<MS>(prog, cur);
@@ -678,7 +682,8 @@ __device__ inline uint32_t pb_home(uint64_t g, int log2tab) {
   return h >> (32 - log2tab);
 }
 
-// find or claim group g's row in the HBM table; -1 = region full (ERR_OOM)
+// find or claim group g's row in the HBM table (the overflow rows when its
+// region is full); -1 = those are full too (ERR_OOM)
 __device__ inline int64_t pr_claim_row(const TwTable &t, uint64_t g, bool &isnew) {
   const uint64_t rb = tw_region_base(t, g);
   uint64_t sl = tw_home_in(t, g);
@@ -699,7 +704,7 @@ __device__ inline int64_t pr_claim_row(const TwTable &t, uint64_t g, bool &isnew
     }
     sl = (sl + step) & t.rmask;
   }
-  return -1;
+  return tw_ovf_claim_new(t, g, isnew);  // the region's sub-table is full
 }
 
 // A partitioned record with its first kPrRegWords words in registers

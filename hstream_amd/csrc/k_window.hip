@@ -46,7 +46,7 @@ __device__ inline uint64_t tw_empty_word(const Program &prog, uint32_t wi) {
 // in one row: one 16-byte store per lane and iteration (the table is sized for
 // the whole run, so this is a streaming write of hundreds of MB).
 __global__ __launch_bounds__(256) void k_tw_reset(TwTable t, Program prog) {
-  const uint64_t pairs = (t.mask + 1) * (uint64_t)t.stride / 2;
+  const uint64_t pairs = t.slots() * (uint64_t)t.stride / 2;  // regions + overflow rows
   const uint32_t sp = t.stride / 2;
   const bool pow2 = (sp & (sp - 1)) == 0;
   ulonglong2 *rows = reinterpret_cast<ulonglong2 *>(t.rows);
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void k_tw_reset_dirty(TwTable t, Program prog,
   const bool pow2 = (sp & (sp - 1)) == 0;
   ulonglong2 *rows = reinterpret_cast<ulonglong2 *>(t.rows);
   if (2 * *cnt > nblk) {  // uniform: most blocks dirty, stream the table and the map
-    const uint64_t pairs = (t.mask + 1) * (uint64_t)sp;
+    const uint64_t pairs = t.slots() * (uint64_t)sp;
     const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < pairs; i += step) {
       const uint32_t wi = 2u * (pow2 ? (uint32_t)(i & (sp - 1)) : (uint32_t)(i % sp));
@@ -177,16 +177,37 @@ void launch_fill_u32(hipStream_t s, uint32_t *p, uint64_t n, uint32_t v) {
 }
 void launch_tw_reset(hipStream_t s, const TwTable &t, const Program &prog) {
   hipLaunchKernelGGL(k_tw_reset, dim3(4096), dim3(256), 0, s, t, prog);
-  if (t.dirty) hipMemsetAsync(t.dirty, 0, tw_dirty_bytes(t.mask + 1), s);
+  if (t.dirty) hipMemsetAsync(t.dirty, 0, tw_dirty_bytes(t.slots()), s);
 }
 void launch_tw_reset_dirty(hipStream_t s, const TwTable &t, const Program &prog, uint64_t *cnt) {
-  const uint64_t nblk = (t.mask + 1) >> 3;
+  const uint64_t nblk = t.slots() >> 3;
   if (!nblk) return launch_tw_reset(s, t, prog);
   hipMemsetAsync(cnt, 0, 8, s);
   hipLaunchKernelGGL(k_tw_dirty_count, dim3(grid_for(nblk / 16 + 1, 256)), dim3(256), 0, s, t, nblk,
                      (unsigned long long *)cnt);
   hipLaunchKernelGGL(k_tw_reset_dirty, dim3(4096), dim3(256), 0, s, t, prog, nblk, (const uint64_t *)cnt);
 }
+// narrow transport -> full width: one pass, coalesced 4-byte loads and
+// 8-byte stores (HBM: 4 + 8 bytes per narrow column and record)
+__global__ __launch_bounds__(256) void k_widen(WidenArgs w) {
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < w.n; i += step) {
+    if (w.ts32) w.ts[i] = w.ts_base + (int64_t)w.ts32[i];
+#pragma unroll
+    for (int c = 0; c < kMaxCols; ++c) {
+      if (!w.c32[c]) continue;  // uniform
+      const int32_t m = w.c32[c][i];
+      // DEC32: the correctly rounded quotient of two exact doubles = the
+      // double nearest the decimal m / 10^s, which its JSON text parses to
+      w.col[c][i] = w.div[c] > 0.0 ? __builtin_bit_cast(int64_t, (double)m / w.div[c]) : (int64_t)m;
+    }
+  }
+}
+
+void launch_widen(hipStream_t s, const WidenArgs &w) {
+  if (w.n) hipLaunchKernelGGL(k_widen, dim3(grid_for(w.n, 256)), dim3(256), 0, s, w);
+}
+
 void launch_fill_rows(hipStream_t s, int64_t *aggs, uint64_t rows, const Program &prog) {
   if (rows && prog.n_slots)
     hipLaunchKernelGGL(k_fill_rows, dim3(grid_for(rows * prog.n_slots, 256)), dim3(256), 0, s, aggs, rows, prog);

@@ -167,6 +167,7 @@ void wait_table_reset(OpDevice &d) {
 int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err) {
   DTRY(hipMemsetAsync(d.sc, 0, sizeof(DevScalars), d.stream));
   memset(d.h_sc, 0, sizeof(DevScalars));  // host mirror (epoch_set gates the optimistic path)
+  d.ovf_rows = 0;  // the clear below empties the overflow rows with the regions
   d.sc_clean = false;
   if (cfg.window_kind == HSG_SESSION) {
     int rc = session_device_reset(d, err);
@@ -181,7 +182,7 @@ int op_device_reset(OpDevice &d, const hsg_op_config &cfg, const Program &prog, 
     if (d.tw_cnt_pending) {  // the previous clear's count (long finished)
       DTRY(hipEventSynchronize(d.ev_reset));
       d.tw_cnt_pending = false;
-      if (2 * *d.h_tw_cnt > ((d.tw.mask + 1) >> 3)) {
+      if (2 * *d.h_tw_cnt > (d.tw.slots() >> 3)) {
         d.tw.dirty = nullptr;
         d.tw_map_valid = false;
       }
@@ -249,14 +250,16 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
     if (rc != HSG_OK) return rc;
   } else {
     d.tw.stride = tw_row_stride(prog.n_slots);
-    DTRY(dalloc(&d.tw.rows, d.cap * (uint64_t)d.tw.stride));
-    DTRY(dalloc(&d.tw_dirty_mem, tw_dirty_bytes(d.cap)));
+    d.region_log2 = 12;
+    tw_configure(d.tw, d.cap, cfg.window_kind, d.region_log2);
+    d.tw.ovf = &d.sc->scratch[33];
+    DTRY(dalloc(&d.tw.rows, d.tw.slots() * (uint64_t)d.tw.stride));
+    DTRY(dalloc(&d.tw_dirty_mem, tw_dirty_bytes(d.tw.slots())));
     d.tw.dirty = d.tw_dirty_mem;
     DTRY(dalloc(&d.tw_cnt, 1));
     DTRY(hipHostMalloc((void **)&d.h_tw_cnt, 8, hipHostMallocDefault));
-    tw_configure(d.tw, d.cap, cfg.window_kind);
     d.tw.bshift = 0;  // set with the exchange (exchange_device_init)
-    uint64_t nb = emit_chunks(d.cap);
+    uint64_t nb = emit_chunks(d.tw.slots());
     DTRY(dalloc(&d.emit.cnt, nb));
     DTRY(dalloc(&d.emit.off, nb));
     DTRY(dalloc(&d.emit.partial, scan_partials_needed(nb) + 8));
@@ -314,6 +317,8 @@ void op_device_free(OpDevice &d) {
   }
   dfree(d.st_seq);
   dfree(d.st_wm);
+  dfree(d.nar_ts);
+  for (int c = 0; c < kMaxCols; ++c) dfree(d.nar_col[c]);
   if (d.h2d) hipStreamSynchronize(d.h2d);
   for (auto &s : d.pre) {
     dfree(s.key);
@@ -368,7 +373,9 @@ void op_device_free(OpDevice &d) {
 }
 
 int op_prestage(OpDevice &d, const hsg_batch *b, int set, std::string &err) {
-  if (b->mem != HSG_MEM_HOST || set < 0 || set > 1 || b->n > d.batch_cap || b->n_cols != d.n_cols) {
+  // a rank's own ingest (d.batch_cap also counts what an exchange may deliver)
+  const uint64_t pcap = d.batch_cap / (d.nranks > 0 ? d.nranks : 1);
+  if (b->mem != HSG_MEM_HOST || set < 0 || set > 1 || b->n > pcap || b->n_cols != d.n_cols) {
     err = "prestage: not a host batch of this op";
     return HSG_E_INVALID;
   }
@@ -379,24 +386,54 @@ int op_prestage(OpDevice &d, const hsg_batch *b, int set, std::string &err) {
   }
   OpDevice::Staging &s = d.pre[set];
   if (!s.key) {
-    DTRY(dalloc(&s.key, d.batch_cap));
-    DTRY(dalloc(&s.ts, d.batch_cap));
+    DTRY(dalloc(&s.key, pcap));
+    DTRY(dalloc(&s.ts, pcap));
     for (int c = 0; c < d.n_cols; ++c) {
-      DTRY(dalloc(&s.col[c], d.batch_cap));
-      DTRY(dalloc(&s.valid[c], d.batch_cap));
+      DTRY(dalloc(&s.col[c], pcap));
+      DTRY(dalloc(&s.valid[c], pcap));
     }
   }
   const uint64_t n = b->n;
   const hipMemcpyKind k = hipMemcpyHostToDevice;
+  // narrow columns (hsg_enc) land in the first half of their full-width
+  // buffers; stage_batch widens them on the op's stream
   if (n) {
     DTRY(hipMemcpyAsync(s.key, b->key_id, n * 4, k, d.h2d));
-    DTRY(hipMemcpyAsync(s.ts, b->ts, n * 8, k, d.h2d));
+    DTRY(hipMemcpyAsync(s.ts, b->ts, n * (b->ts_enc == HSG_ENC_TS32 ? 4 : 8), k, d.h2d));
     for (int c = 0; c < b->n_cols; ++c) {
-      DTRY(hipMemcpyAsync(s.col[c], b->cols[c], n * 8, k, d.h2d));
+      DTRY(hipMemcpyAsync(s.col[c], b->cols[c], n * (b->col_enc[c] != HSG_ENC_FULL ? 4 : 8), k, d.h2d));
       if (b->valid && b->valid[c]) DTRY(hipMemcpyAsync(s.valid[c], b->valid[c], n, k, d.h2d));
     }
   }
   DTRY(hipEventRecord(d.ev_h2d[set], d.h2d));
+  return HSG_OK;
+}
+
+// Narrow transport columns (include/hstream_gpu.h hsg_enc) at device
+// addresses ts32 / c32 (null = that array is full width and already in kb)
+// -> the op's full-width staging; kb points there afterwards.
+static int widen_batch(OpDevice &d, const hsg_batch *b, const void *ts32, const void *const *c32, Batch &kb,
+                       std::string &err) {
+  WidenArgs w;
+  memset(&w, 0, sizeof(w));
+  w.n = b->n;
+  if (b->ts_enc == HSG_ENC_TS32) {
+    w.ts32 = (const int32_t *)ts32;
+    w.ts_base = b->ts_base;
+    w.ts = d.st_ts;
+    kb.ts = d.st_ts;
+  }
+  for (int c = 0; c < b->n_cols; ++c) {
+    if (b->col_enc[c] == HSG_ENC_FULL) continue;
+    w.c32[c] = (const int32_t *)c32[c];
+    w.col[c] = d.st_col[c];
+    double p = 1.0;
+    for (int q = 0; q < b->col_scale[c]; ++q) p *= 10.0;  // exact for <= 22 digits
+    w.div[c] = b->col_enc[c] == HSG_ENC_DEC32 ? p : 0.0;
+    kb.col[c] = d.st_col[c];
+  }
+  launch_widen(d.stream, w);
+  DTRY(hipGetLastError());
   return HSG_OK;
 }
 
@@ -415,6 +452,11 @@ int stage_batch(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err, in
       kb.col[c] = s.col[c];
       kb.valid[c] = (b->valid && b->valid[c]) ? s.valid[c] : nullptr;
     }
+    if (batch_narrow(b)) {
+      const void *c32[kMaxCols];
+      for (int c = 0; c < b->n_cols; ++c) c32[c] = s.col[c];
+      return widen_batch(d, b, s.ts, c32, kb, err);
+    }
     return HSG_OK;
   }
   if (b->mem == HSG_MEM_DEVICE) {
@@ -426,7 +468,35 @@ int stage_batch(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err, in
       kb.col[c] = (const int64_t *)b->cols[c];
       kb.valid[c] = (b->valid && b->valid[c]) ? b->valid[c] : nullptr;
     }
+    if (batch_narrow(b)) return widen_batch(d, b, b->ts, b->cols, kb, err);
     return HSG_OK;
+  }
+  if (batch_narrow(b)) {
+    // host narrow batch, synchronous push: H2D into the narrow staging, widen
+    if (!d.nar_ts) {
+      DTRY(dalloc(&d.nar_ts, d.batch_cap));
+      for (int c = 0; c < d.n_cols; ++c) DTRY(dalloc(&d.nar_col[c], d.batch_cap));
+    }
+    const hipMemcpyKind k = hipMemcpyHostToDevice;
+    const void *c32[kMaxCols] = {};
+    if (n) {
+      DTRY(hipMemcpyAsync(d.st_key, b->key_id, n * 4, k, d.stream));
+      if (b->ts_enc == HSG_ENC_TS32) DTRY(hipMemcpyAsync(d.nar_ts, b->ts, n * 4, k, d.stream));
+      else DTRY(hipMemcpyAsync(d.st_ts, b->ts, n * 8, k, d.stream));
+    }
+    kb.key = d.st_key;
+    kb.ts = d.st_ts;
+    for (int c = 0; c < b->n_cols; ++c) {
+      const bool nar = b->col_enc[c] != HSG_ENC_FULL;
+      if (n) DTRY(hipMemcpyAsync(nar ? (void *)d.nar_col[c] : (void *)d.st_col[c], b->cols[c], n * (nar ? 4 : 8), k, d.stream));
+      c32[c] = d.nar_col[c];
+      kb.col[c] = d.st_col[c];
+      if (b->valid && b->valid[c]) {
+        if (n) DTRY(hipMemcpyAsync(d.st_valid[c], b->valid[c], n, k, d.stream));
+        kb.valid[c] = d.st_valid[c];
+      }
+    }
+    return widen_batch(d, b, d.nar_ts, c32, kb, err);
   }
   if (n) {
     DTRY(hipMemcpyAsync(d.st_key, b->key_id, n * 4, hipMemcpyHostToDevice, d.stream));
@@ -478,6 +548,7 @@ int fetch_scalars(OpDevice &d, std::string &err) {
   DTRY(hipStreamSynchronize(d.stream));
   DTRY(hipGetLastError());
   for (int k = 0; k < 8; ++k) d.h_sc->live += d.h_sc->live_x[k];  // device: live + shards
+  d.ovf_rows += d.h_sc->scratch[33];  // groups a full region sent to the overflow rows (cleared above)
   d.sc_clean = true;
   return HSG_OK;
 }
@@ -627,7 +698,7 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       if (d.use_part) {
         if (!skipped_emit) launch_part_emit(d.stream, d.tw, prog, p, d.part, d.out, a.pending, d.out_cap, d.sc);
       } else {
-        launch_tw_emit(d.stream, d.tw, d.cap, prog, p, 0, d.out, a.pending, d.out_cap, d.sc, d.emit,
+        launch_tw_emit(d.stream, d.tw, d.tw.slots(), prog, p, 0, d.out, a.pending, d.out_cap, d.sc, d.emit,
                        (uint64_t *)&d.sc->out_rows);
       }
     }
@@ -653,7 +724,21 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     }
     rc = run(optimistic);
     if (rc != HSG_OK) return rc;
-    return finish_batch(d, a.wm_in, kb.n, r, err);
+    rc = finish_batch(d, a.wm_in, kb.n, r, err);
+    if (rc != HSG_OK || !d.h_sc->scratch[32]) return rc;
+    // held back again (the lean partial count depends on the LDS tables' fill
+    // races, so a rerun may count more): the worst case, one group per
+    // (record, window), then a last run that must not hold back
+    rc = tw_maintain(d, cfg, prog, kb.n, a.wm_in, a.pending, err, UINT64_MAX);
+    if (rc != HSG_OK) return rc;
+    rc = run(optimistic);
+    if (rc != HSG_OK) return rc;
+    rc = finish_batch(d, a.wm_in, kb.n, r, err);
+    if (rc == HSG_OK && d.h_sc->scratch[32]) {
+      err = "batch held back for table room after growing for its worst case (internal)";
+      return HSG_E_DEVICE;
+    }
+    return rc;
   };
   int rc = run_room(opt);
   if (rc != HSG_OK) return rc;
@@ -870,7 +955,7 @@ int op_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hs
     } else {
       PushArgs a;
       TwParams p = make_tw_params(cfg, a);
-      launch_tw_emit(d.stream, d.tw, d.cap, prog, p, 1, tmp, 0, live, d.sc, d.emit, counter);
+      launch_tw_emit(d.stream, d.tw, d.tw.slots(), prog, p, 1, tmp, 0, live, d.sc, d.emit, counter);
     }
     uint64_t got = 0;
     hipMemcpyAsync(&got, counter, 8, hipMemcpyDeviceToHost, d.stream);

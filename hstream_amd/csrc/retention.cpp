@@ -40,14 +40,17 @@ namespace hsg {
     }                                                                       \
   } while (0)
 
-void tw_configure(TwTable &t, uint64_t cap, int window_kind) {
+void tw_configure(TwTable &t, uint64_t cap, int window_kind, int region_log2) {
   t.mask = cap - 1;
+  t.omask = tw_ovf_slots(cap) - 1;
   t.blocked = window_kind != HSG_UNWINDOWED && cap >= 64 ? 1u : 0u;
-  // regions of >= 4096 slots (small spread of the per-region load), at most
-  // one per partition bucket (hsg_tw.h)
+  // regions of >= 2^region_log2 slots (4096 unless overflow claims made the
+  // op widen them: small spread of the per-region load), at most one per
+  // partition bucket (hsg_tw.h)
   int cl = 0;
   while ((1ull << cl) < cap) ++cl;
-  t.rbits = cl - 12 < 0 ? 0 : (cl - 12 > kPartMaxLog2 ? kPartMaxLog2 : cl - 12);
+  const int rb = cl - region_log2;
+  t.rbits = rb < 0 ? 0 : (rb > kPartMaxLog2 ? kPartMaxLog2 : rb);
   t.rmask = (cap >> t.rbits) - 1;
 }
 
@@ -119,7 +122,9 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
   // new groups of the batch: one per (record, window) at worst, or the bound
   // of a batch whose apply checks its room (op_device.cpp push_time_atomic)
   const uint64_t bound = n_in * d.wpr < groups_bound ? n_in * d.wpr : groups_bound;
-  if (!reopen && 4 * (live + bound) <= 3 * d.cap) return HSG_OK;
+  // a region was full (overflow rows in use): rebuild with larger regions
+  const bool widen = d.ovf_rows != 0;
+  if (!reopen && !widen && 4 * (live + bound) <= 3 * d.cap) return HSG_OK;
   wait_table_reset(d);
   const TwParams p = retention_params(cfg, wm_in);
   // small pinned block for the counters read back here
@@ -142,7 +147,7 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
   DTRY(hipMemsetAsync(dwords, 0, 2 * sizeof(uint64_t), d.stream));
   uint64_t closed = 0;
   if (!reopen && cfg.window_kind != HSG_UNWINDOWED) {
-    launch_tw_closed(d.stream, d.tw, d.cap, p, d.sc, d.emit, dwords, nullptr);
+    launch_tw_closed(d.stream, d.tw, d.tw.slots(), p, d.sc, d.emit, dwords, nullptr);
     DTRY(hipMemcpyAsync(h, dwords, 8, hipMemcpyDeviceToHost, d.stream));
     DTRY(hipStreamSynchronize(d.stream));
     DTRY(hipGetLastError());
@@ -150,8 +155,11 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
   }
   const uint64_t back = reopen ? d.spilled_rows : 0;
   const uint64_t keep = live - closed + back;
-  uint64_t ncap = d.cap;
+  uint64_t ncap = widen ? 2 * d.cap : d.cap;
   while (2 * (keep + bound) > ncap) ncap <<= 1;
+  // each overflow rebuild doubles the regions (a key's windows share its
+  // region: a few keys with many open windows need larger regions, not more)
+  const int rlog2 = widen ? d.region_log2 + 1 : d.region_log2;
   if (cfg.emit_mode == HSG_EMIT_PER_RECORD && ncap > 0x80000000ull) {
     err = "state table would pass 2^31 slots (per-record changelog path)";
     return HSG_E_OOM;
@@ -159,14 +167,14 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
   // every allocation first: a failure leaves the op as it was
   TwTable nt = d.tw;
   nt.rows = nullptr;
-  DTRY(hipMalloc((void **)&nt.rows, ncap * (uint64_t)nt.stride * 8));
+  tw_configure(nt, ncap, cfg.window_kind, rlog2);
+  DTRY(hipMalloc((void **)&nt.rows, nt.slots() * (uint64_t)nt.stride * 8));
   fresh.p = nt.rows;
   if (d.tw.dirty) {  // claims still mark: a map for the new table
     nt.dirty = nullptr;
-    DTRY(hipMalloc((void **)&nt.dirty, tw_dirty_bytes(ncap)));
+    DTRY(hipMalloc((void **)&nt.dirty, tw_dirty_bytes(nt.slots())));
     fresh_map.p = nt.dirty;
   }
-  tw_configure(nt, ncap, cfg.window_kind);
   if (closed) DTRY(hipMalloc(&dense.p, closed * d.tw.stride * 8));
   if (back) DTRY(hipMalloc(&up.p, back * d.tw.stride * 8));
   const uint64_t at = d.spill.size();
@@ -178,13 +186,14 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
   };
   // 1. closed rows to the host
   if (closed) {
-    launch_tw_closed(d.stream, d.tw, d.cap, p, d.sc, d.emit, nullptr, (uint64_t *)dense.p);
+    launch_tw_closed(d.stream, d.tw, d.tw.slots(), p, d.sc, d.emit, nullptr, (uint64_t *)dense.p);
     hipMemcpyAsync(d.spill.data() + at, dense.p, closed * d.tw.stride * 8, hipMemcpyDeviceToHost, d.stream);
   }
   // 2. the open rows (and, after a lowered watermark, the spilled ones) into
   //    the fresh table
   launch_tw_reset(d.stream, nt, prog);
-  launch_tw_reinsert(d.stream, d.tw.rows, d.cap, nt, p, d.sc, closed != 0, (unsigned long long *)(dwords + 1));
+  DTRY(hipMemsetAsync(nt.ovf, 0, 8, d.stream));  // overflow claims of the rebuild
+  launch_tw_reinsert(d.stream, d.tw.rows, d.tw.slots(), nt, p, d.sc, closed != 0, (unsigned long long *)(dwords + 1));
   if (back) {
     hipMemcpyAsync(up.p, d.spill.data(), back * d.tw.stride * 8, hipMemcpyHostToDevice, d.stream);
     launch_tw_reinsert(d.stream, (const uint64_t *)up.p, back, nt, p, d.sc, false, (unsigned long long *)(dwords + 1));
@@ -192,6 +201,7 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
   h[2] = 0;
   hipMemcpyAsync(h + 1, dwords + 1, 8, hipMemcpyDeviceToHost, d.stream);
   hipMemcpyAsync(h + 2, &d.sc->err, 4, hipMemcpyDeviceToHost, d.stream);
+  hipMemcpyAsync(h + 3, nt.ovf, 8, hipMemcpyDeviceToHost, d.stream);
   hipError_t e = hipStreamSynchronize(d.stream);
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) return undo(std::string("table rebuild: ") + hipGetErrorString(e), HSG_E_DEVICE);
@@ -209,6 +219,10 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
   // a clear's pending count of dirty blocks describes the old table
   if (ncap != d.cap) d.tw_cnt_pending = false;
   d.tw = nt;  // its dirty map: cleared with it, then marked by the reinsert
+  d.region_log2 = rlog2;
+  if (widen) d.ovf_events += 1;
+  d.ovf_rows = h[3];  // rows the larger regions still could not take (rebuilt again next batch)
+  DTRY(hipMemsetAsync(nt.ovf, 0, 8, d.stream));
   if (closed) {
     d.spilled_rows += closed;
     d.spill_events += 1;
@@ -221,8 +235,8 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
   if (ncap != d.cap) {
     d.grow_events += 1;
     // emit / dump scratch for the larger table
-    const uint64_t nb = emit_chunks(ncap);
-    if (nb > emit_chunks(d.cap)) {
+    const uint64_t nb = emit_chunks(nt.slots());
+    if (nb > emit_chunks(tw_ovf_slots(d.cap) + d.cap)) {
       DTRY(hipStreamSynchronize(d.stream));
       hipFree(d.emit.cnt);
       hipFree(d.emit.off);

@@ -70,11 +70,11 @@ int perrecord_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &
     err = "batch_capacity x windows per record must be < 2^32 for the per-record / session paths";
     return HSG_E_INVALID;
   }
-  if (d.cap > 0x7FFFFFFFull) {
+  if (d.tw.slots() > 0x7FFFFFFFull) {
     err = "state table too large for the sort-based paths (max 2^31 slots)";
     return HSG_E_INVALID;
   }
-  uint64_t shadow = cfg.window_kind == HSG_SESSION ? 0 : d.cap * (uint64_t)prog.n_slots;
+  uint64_t shadow = cfg.window_kind == HSG_SESSION ? 0 : d.tw.slots() * (uint64_t)prog.n_slots;
   Carve probe{nullptr};
   PrBuffers tmp;
   carve_layout(probe, tmp, n, P, shadow);
@@ -234,7 +234,7 @@ int push_time_perrecord(OpDevice &d, const hsg_op_config &cfg, const Program &pr
     }
     if (P) {
       launch_pr_expand(d.stream, kb, p, d.tw, d.tile_prefix, rec_wm, pb, d.sc);
-      int which = radix_sort_pairs(d.stream, pb.pslot, pb.pidx, pb.k1, pb.v1, P, log2u(d.cap) + 1, pb.sort_scratch);
+      int which = radix_sort_pairs(d.stream, pb.pslot, pb.pidx, pb.k1, pb.v1, P, log2u(d.tw.slots()) + 1, pb.sort_scratch);
       const uint32_t *slot = which ? pb.k1 : pb.pslot;
       const uint32_t *idx = which ? pb.v1 : pb.pidx;
       launch_pr_segscan(d.stream, kb, prog, pb, p, d.tw, slot, idx, P, seq, d.out, a.pending, d.sc);

@@ -131,13 +131,13 @@ class GpuOp(OpHandle):
         self._check(self._lib.hsg_drain(self._h, None, C.byref(got)), "drain")
         return got.value
 
-    def push_async(self, key_id, ts, cols=(), valid=None, watermark=None, done=None, mem=None):
+    def push_async(self, key_id, ts, cols=(), valid=None, watermark=None, done=None, mem=None, **enc):
         """hsg_push_batch_async: queue the batch and return at once. `watermark`
         is a ctypes.c_int64 shared by consecutive pushes (read when the batch
         starts, written before `done(rc)` runs on the op's completion thread).
         The arrays are kept alive until the completion has run."""
         from .columnar import make_batch
-        b, keep = make_batch(key_id, ts, cols, valid, mem)
+        b, keep = make_batch(key_id, ts, cols, valid, mem, **enc)
         wm = watermark if watermark is not None else C.c_int64(-1)
         entry = {}
 

@@ -100,6 +100,20 @@ enum hsg_agg_kind {
 
 enum hsg_mem { HSG_MEM_HOST = 0, HSG_MEM_DEVICE = 1 };
 
+/* Narrow transport encodings of a batch's columns (hsg_batch ts_enc / col_enc).
+ * A poll batch crosses PCIe before any kernel sees it, so its bytes per record
+ * bound a host-fed op's throughput; a producer that knows a column's range
+ * (the decoder sees every value) may send it narrower. Lossless: the library
+ * widens on the device before the batch runs. */
+enum hsg_enc {
+  HSG_ENC_FULL  = 0, /* the column's own type: int64 ts, int64 / double values          */
+  HSG_ENC_TS32  = 1, /* ts only: int32 offsets from hsg_batch.ts_base                   */
+  HSG_ENC_I32   = 2, /* an HSG_I64 column sent as int32 (every value fits)              */
+  HSG_ENC_DEC32 = 3  /* an HSG_F64 column sent as int32 decimal mantissas m:
+                        value = m / 10^col_scale, the double nearest that decimal,
+                        i.e. the double the JSON text of the decimal parses to       */
+};
+
 typedef struct hsg_engine hsg_engine;
 typedef struct hsg_op hsg_op;
 
@@ -164,6 +178,13 @@ typedef struct {
                                    NULL or a NULL entry = all present                    */
   void *ready_event;            /* optional hipEvent_t the op's stream waits on (device
                                    batches); NULL = inputs already complete              */
+  /* narrow transport (all zero = the full-width arrays above) */
+  int32_t ts_enc;               /* HSG_ENC_FULL, or HSG_ENC_TS32: `ts` points at int32_t[n]  */
+  int32_t reserved;             /* 0                                                      */
+  int64_t ts_base;              /* HSG_ENC_TS32: ts of a record = ts_base + its offset     */
+  uint8_t col_enc[8];           /* per value column: HSG_ENC_FULL, HSG_ENC_I32 (HSG_I64
+                                   columns) or HSG_ENC_DEC32 (HSG_F64 columns)            */
+  uint8_t col_scale[8];         /* HSG_ENC_DEC32: decimal digits after the point, <= 18   */
 } hsg_batch;
 
 /* Columnar changelog / state rows. */
@@ -207,6 +228,11 @@ typedef struct {
   uint64_t direct_batches;    /* ... whose changelog rows the lean apply wrote itself      */
   uint64_t replays;           /* batches completed after the fetch because the predicted
                                  kernel variants did not match the batch (speed only)     */
+  uint64_t overflow_rows;     /* groups in the table's overflow rows now: a key-hash region
+                                 was full when they were claimed (skewed keys, or keys with
+                                 many open windows); the next batch rebuilds the table    */
+  uint64_t overflow_rebuilds; /* table rebuilds (twice the slots, twice the region size)
+                                 that overflow rows caused                               */
 } hsg_stats;
 
 /* Completion callback of hsg_push_batch_async: rc is what hsg_push_batch

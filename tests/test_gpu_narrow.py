@@ -1,0 +1,97 @@
+"""The narrow transport of a batch (include/hstream_gpu.h hsg_enc): ts as int32
+offsets from a base, i64 columns as int32, f64 decimal columns as int32
+mantissas. Lossless by construction, so every result must be bit-identical
+to the same batches pushed at full width -- checked against the oracle fed the
+full-width arrays, for host batches (synchronous and asynchronous, the latter
+prestaged on the copy stream) and device batches, with absent fields,
+HSG_KEY_NONE records, negative and late timestamps."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import pyoracle
+from hstream_amd import abi
+from hstream_amd.columnar import OpSpec, narrow_columns
+from util import gen_small, rows_equal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need cuda:0"
+    from hstream_amd.engine import Engine
+    e = Engine(device=0, batch_capacity=1 << 18)
+    yield e
+    e.close()
+
+
+AGGS = [(abi.HSG_COUNT_ALL, 0), (abi.HSG_COUNT, 1), (abi.HSG_SUM, 0), (abi.HSG_MIN, 0), (abi.HSG_MAX, 0),
+        (abi.HSG_SUM, 1), (abi.HSG_MIN, 1), (abi.HSG_MAX, 1), (abi.HSG_AVG, 1)]
+SPECS = {
+    "tumbling_batch": OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=10_000,
+                             col_types=[abi.HSG_I64, abi.HSG_F64], aggs=AGGS),
+    "hopping_record": OpSpec(abi.HSG_HOPPING, abi.HSG_EMIT_PER_RECORD, size_ms=20_000, advance_ms=5_000,
+                             col_types=[abi.HSG_I64, abi.HSG_F64], aggs=AGGS),
+    "session_batch": OpSpec(abi.HSG_SESSION, abi.HSG_EMIT_PER_BATCH, gap_ms=2_000,
+                            col_types=[abi.HSG_I64, abi.HSG_F64], aggs=AGGS),
+}
+
+
+def _batches(seed, nb=3, n=40_000):
+    out = []
+    for b in range(nb):
+        key, ts, cols, valid = gen_small(seed + b, n, 300, col_types=(abi.HSG_I64, abi.HSG_F64), span=60_000,
+                                         base=3_000_000 + 60_000 * b)
+        cols[0] = cols[0] // 2  # fits int32
+        out.append((key, ts, cols, valid))
+    return out
+
+
+@pytest.mark.parametrize("mode", ["sync", "async", "device"])
+@pytest.mark.parametrize("name", sorted(SPECS))
+def test_narrow_equals_full_width(eng, name, mode):
+    import torch
+    spec = SPECS[name]
+    g, o = eng.op(spec), pyoracle.OracleOp(spec, faithful_sessions=False)
+    f64 = spec.agg_is_f64()
+    wm_o = -1
+    wm_g = C.c_int64(-1)
+    for bi, (key, ts, cols, valid) in enumerate(_batches(70 + len(name))):
+        t32, base, c32, enc, scale = narrow_columns(ts, cols, spec.col_types, [None, 3])
+        assert base is not None and enc == [abi.HSG_ENC_I32, abi.HSG_ENC_DEC32], (base, enc)
+        wm_o = o.push(key, ts, cols, valid, watermark=wm_o)
+        kw = dict(ts_base=base, col_enc=enc, col_scale=scale)
+        if mode == "sync":
+            wm_g.value = g.push(key, t32, c32, valid, watermark=wm_g.value, **kw)
+        elif mode == "async":
+            g.push_async(key, t32, c32, valid, watermark=wm_g, **kw)
+            g.wait()
+        else:
+            d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+            dv = [d(v) for v in valid]
+            torch.cuda.synchronize()
+            wm_g.value = g.push(d(key.view(np.int32)), d(t32), [d(c) for c in c32], dv, watermark=wm_g.value,
+                                mem=abi.HSG_MEM_DEVICE, **kw)
+        assert wm_g.value == wm_o, f"batch {bi}: watermark"
+        rows_equal(g.drain(), o.drain(), f64, ordered=spec.emit_mode == abi.HSG_EMIT_PER_RECORD,
+                   what=f"{name} {mode} changelog {bi}")
+    rows_equal(g.dump_state(), o.dump_state(), f64, what=f"{name} {mode} state")
+    g.close()
+    o.close()
+
+
+def test_bad_encodings_refused(eng):
+    spec = SPECS["tumbling_batch"]
+    g = eng.op(spec)
+    key = np.arange(10, dtype=np.uint32)
+    ts = np.arange(10, dtype=np.int32)
+    cols = [np.arange(10, dtype=np.int32), np.arange(10, dtype=np.int32)]
+    for enc in ([abi.HSG_ENC_DEC32, abi.HSG_ENC_FULL], [abi.HSG_ENC_FULL, abi.HSG_ENC_I32], [7, 0]):
+        with pytest.raises(abi.HStreamGpuError) as ei:
+            g.push(key, ts, [c if e != abi.HSG_ENC_FULL else c.astype(np.int64) for c, e in zip(cols, enc)],
+                   None, watermark=-1, ts_base=0, col_enc=enc, col_scale=[2, 2])
+        assert ei.value.status == abi.HSG_E_INVALID
+    g.close()

@@ -1,0 +1,43 @@
+"""Host side of the narrow transport (include/hstream_gpu.h hsg_enc): what a
+producer may send narrower, and that a DEC32 value is exactly the double its
+decimal text parses to (the device computes m / 10^s the same way)."""
+import numpy as np
+
+from hstream_amd import abi
+from hstream_amd.columnar import make_batch, narrow_columns
+
+
+def test_dec32_is_the_parsed_double():
+    rng = np.random.default_rng(3)
+    m = rng.integers(-2**31, 2**31, 3000)
+    for s in (0, 1, 3, 6, 9):
+        def text(x):
+            a = abs(int(x))
+            return ("-" if x < 0 else "") + (f"{a // 10**s}.{a % 10**s:0{s}d}" if s else str(a))
+        parsed = np.array([float(text(x)) for x in m])
+        assert np.array_equal(m / 10.0**s, parsed), s
+
+
+def test_narrow_columns_choices():
+    ts = np.array([1_700_000_000_000, 1_700_000_000_500, 1_699_999_999_000], np.int64)
+    i64 = np.array([-5, 2**31 - 1, -2**31], np.int64)
+    big = np.array([0, 2**31], np.int64)
+    f = np.array([1.5, 2.25, 123456.789], np.float64)
+    t32, base, cs, enc, scale = narrow_columns(ts, [i64, big, f, f], [abi.HSG_I64, abi.HSG_I64, abi.HSG_F64,
+                                                                      abi.HSG_F64], [None, None, 3, 2])
+    assert base == 1_699_999_999_000 and t32.dtype == np.int32
+    assert np.array_equal(base + t32.astype(np.int64), ts)
+    assert enc == [abi.HSG_ENC_I32, abi.HSG_ENC_FULL, abi.HSG_ENC_DEC32, abi.HSG_ENC_FULL], enc
+    assert scale[2] == 3 and np.array_equal(cs[2] / 1e3, f)
+    # a ts span of 2^31 ms or more stays full width
+    _, base2, _, _, _ = narrow_columns(np.array([0, 2**31], np.int64), [], [])
+    assert base2 is None
+
+
+def test_make_batch_fields():
+    key = np.arange(4, dtype=np.uint32)
+    b, _ = make_batch(key, np.arange(4, dtype=np.int32), [np.arange(4, dtype=np.int32)], None, abi.HSG_MEM_HOST,
+                      ts_base=77, col_enc=[abi.HSG_ENC_I32], col_scale=[0])
+    assert b.ts_enc == abi.HSG_ENC_TS32 and b.ts_base == 77 and b.col_enc[0] == abi.HSG_ENC_I32
+    b2, _ = make_batch(key, np.arange(4, dtype=np.int64), [np.arange(4, dtype=np.int64)], None, abi.HSG_MEM_HOST)
+    assert b2.ts_enc == abi.HSG_ENC_FULL and b2.col_enc[0] == abi.HSG_ENC_FULL
