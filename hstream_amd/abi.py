@@ -180,7 +180,12 @@ EXPORTED_SYMBOLS = [
     "hsg_state_rows",
     "hsg_dump_state",
     "hsg_op_stats",
+    "hsg_testing_set_knob",
 ]
+
+# testing knobs (hsg_testing_set_knob)
+HSG_KNOB_XPART_LOG2 = 1
+HSG_KNOB_SESS_ARENA_MIN = 2
 
 
 # Every symbol include/hstream_ingest.h declares (host ingest, no GPU needed).

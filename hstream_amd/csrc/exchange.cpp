@@ -79,12 +79,12 @@ int exchange_device_init(OpDevice &d, const hsg_op_config &cfg, uint64_t batch_c
   DTRY(hipMalloc((void **)&d.st_wm, (uint64_t)G * n * 8 + 8));
   if (!d.h_tmp) DTRY(hipHostMalloc((void **)&d.h_tmp, 8 * sizeof(uint64_t), hipHostMallocDefault));
   // owner partition of the fast exchange: log2(ranks) for a power-of-two rank
-  // count; HSG_XPART_LOG2 (tests) partitions a single rank finer, every
-  // region still going to rank 0
+  // count; the HSG_KNOB_XPART_LOG2 testing knob partitions a single rank
+  // finer, every region still going to rank 0
   d.xpart_log2 = log2_exact((uint32_t)G);
-  if (const char *e = getenv("HSG_XPART_LOG2")) {
-    const int v = atoi(e);
-    if (G == 1 && v >= 0 && v <= 6) d.xpart_log2 = v;
+  {
+    const int64_t v = testing_knob(HSG_KNOB_XPART_LOG2);
+    if (G == 1 && v >= 0 && v <= 6) d.xpart_log2 = (int)v;
   }
   d.bshift = d.xpart_log2 > 0 ? d.xpart_log2 : 0;
   if (d.bshift + kPartMaxLog2 > 60) d.bshift = 0;

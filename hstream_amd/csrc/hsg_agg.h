@@ -435,7 +435,7 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const PG &pr
                               bool defer) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t SW = S ? (uint32_t)S : 1u;
-  const uint64_t t0 = wall_clock64();
+  const uint64_t t0 = phase_clock();
   // compact the live entries (one LDS atomic per wave)
   for (int e0 = 0; e0 < E; e0 += NT) {
     const int e = e0 + threadIdx.x;
@@ -450,7 +450,7 @@ __device__ __forceinline__ uint32_t agg_flush(AggLds<MS, E, NT> &L, const PG &pr
   const uint32_t nl = L.nl;
   // pane mode: a key's panes become neighbours in pane order
   if (S > 1 && nl > 1) group_live<MS, E, NT>(L, nl);
-  t_sort += wall_clock64() - t0;
+  t_sort += phase_clock() - t0;
   // owned window run of every pane: [max(P - n + 1, previous pane + 1), P];
   // each thread takes a contiguous range of the (key-grouped) live list, so
   // the window positions below follow pane order
@@ -603,7 +603,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   constexpr int SUB = NT * RPT;
   const int nb = 1 << pp.np_log2;
   const uint32_t *chunk_start = pb.chunk_start;
-  const uint64_t t0 = wall_clock64();
+  const uint64_t t0 = phase_clock();
   if (threadIdx.x == 0) {
     // this workgroup's bucket: chunk_start[b] <= blockIdx.x < chunk_start[b + 1]
     const uint32_t bk = blockIdx.x < chunk_start[nb] ? pb.chunk_bucket[blockIdx.x] : 0;
@@ -649,11 +649,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint64_t pairs = 0, groups = 0, t_rec = 0, t_flush = 0, t_sort = 0, flushes = 0;
   uint32_t fresh = 0, err = 0;
-  const uint64_t t1 = wall_clock64();
+  const uint64_t t1 = phase_clock();
 
   for (int round = 0; round < nrounds; ++round) {
     for (uint64_t s0 = r0; s0 < r1; s0 += SUB) {
-      uint64_t ta = wall_clock64();
+      uint64_t ta = phase_clock();
       PRec<WMAX, PK> rr[RPT];
       auto load = [&]() {
 #pragma unroll
@@ -724,7 +724,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
           pend &= ~(1u << u);
         }
         const bool more = __syncthreads_or(pend != 0);
-        const uint64_t tb = wall_clock64();
+        const uint64_t tb = phase_clock();
         t_rec += tb - ta;
         if (!more) break;
         // table full with records left: flush and go on (the records are
@@ -735,7 +735,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         if (threadIdx.x == 0) atomicOr((unsigned int *)&sc->scratch[5], 1u);
         ++flushes;
         load();
-        ta = wall_clock64();
+        ta = phase_clock();
         t_flush += ta - tb;
       }
       if (!FAN && __syncthreads_or(dpend != 0)) {
@@ -753,13 +753,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         }
       }
     }
-    const uint64_t tb = wall_clock64();
+    const uint64_t tb = phase_clock();
     groups += agg_flush<MS, E, NT>(L, prog, p, t, pb, sc, S, exclusive, plain_claim, skip, cnt_all_slot, fresh, err,
                                    t_sort, defer);
     ++flushes;
-    t_flush += wall_clock64() - tb;
+    t_flush += phase_clock() - tb;
   }
-  const uint64_t t3 = wall_clock64();
+  const uint64_t t3 = phase_clock();
   pairs = wave_sum_u64(pairs);
   const uint64_t fr = wave_sum_u64(fresh);
   if (lane == 0) {
@@ -781,15 +781,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (f) atomicAdd((unsigned long long *)&sc->live, (unsigned long long)f);
     if (groups) atomicAdd((unsigned long long *)&sc->scratch[0], (unsigned long long)groups);
     // phase clock (100 MHz wall clock) sums: init, records, flush, tail, workgroups
-    const uint64_t t4 = wall_clock64();
-    atomicAdd((unsigned long long *)&sc->scratch[8], (unsigned long long)(t1 - t0));
-    atomicAdd((unsigned long long *)&sc->scratch[9], (unsigned long long)t_rec);
-    atomicAdd((unsigned long long *)&sc->scratch[10], (unsigned long long)t_flush);
-    atomicAdd((unsigned long long *)&sc->scratch[11], (unsigned long long)(t4 - t3));
-    atomicAdd((unsigned long long *)&sc->scratch[12], 1ull);
-    atomicAdd((unsigned long long *)&sc->scratch[18], (unsigned long long)t_sort);
-    atomicAdd((unsigned long long *)&sc->scratch[19], 0ull);
-    atomicAdd((unsigned long long *)&sc->scratch[20], (unsigned long long)flushes);
+    if (kPhaseClocks) {
+      const uint64_t t4 = phase_clock();
+      atomicAdd((unsigned long long *)&sc->scratch[8], (unsigned long long)(t1 - t0));
+      atomicAdd((unsigned long long *)&sc->scratch[9], (unsigned long long)t_rec);
+      atomicAdd((unsigned long long *)&sc->scratch[10], (unsigned long long)t_flush);
+      atomicAdd((unsigned long long *)&sc->scratch[11], (unsigned long long)(t4 - t3));
+      atomicAdd((unsigned long long *)&sc->scratch[12], 1ull);
+      atomicAdd((unsigned long long *)&sc->scratch[18], (unsigned long long)t_sort);
+      atomicAdd((unsigned long long *)&sc->scratch[20], (unsigned long long)flushes);
+    }
   }
 }
 

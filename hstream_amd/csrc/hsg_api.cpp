@@ -7,6 +7,7 @@
 // Every entry point catches everything: no C++ exception crosses the ABI.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -186,6 +187,33 @@ extern "C" void hsg_engine_destroy(hsg_engine *e) {
 }
 
 extern "C" const char *hsg_engine_last_error(const hsg_engine *e) { return e ? e->err.c_str() : "null engine"; }
+
+// testing knobs (include/hstream_gpu.h): process-wide, read at op creation
+static std::atomic<int64_t> g_knob_xpart{-1}, g_knob_arena{0};
+
+namespace hsg {
+int64_t testing_knob(int knob) {
+  switch (knob) {
+    case HSG_KNOB_XPART_LOG2: return g_knob_xpart.load();
+    case HSG_KNOB_SESS_ARENA_MIN: return g_knob_arena.load();
+    default: return 0;
+  }
+}
+}  // namespace hsg
+
+extern "C" int hsg_testing_set_knob(int32_t knob, int64_t value) {
+  switch (knob) {
+    case HSG_KNOB_XPART_LOG2:
+      if (value < -1 || value > 6) return HSG_E_INVALID;
+      g_knob_xpart.store(value);
+      return HSG_OK;
+    case HSG_KNOB_SESS_ARENA_MIN:
+      if (value < 0) return HSG_E_INVALID;
+      g_knob_arena.store(value);
+      return HSG_OK;
+    default: return HSG_E_INVALID;
+  }
+}
 
 // ---------------------------------------------------------------------------
 // op

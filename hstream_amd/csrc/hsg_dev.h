@@ -6,6 +6,21 @@
 
 namespace hsg {
 
+// Phase clocks of the HSG_PHASES diagnostics (per-workgroup time split of the
+// partition, aggregation, per-record and session kernels, summed into
+// DevScalars::scratch and printed by op_device.cpp). Compiled in only with
+// -DHSG_PHASE_CLOCKS=1 (make PHASES=1): otherwise phase_clock() is 0 and every
+// accumulation guarded by kPhaseClocks is dead code, so the product kernels
+// carry neither the clock reads nor the atomics.
+#ifndef HSG_PHASE_CLOCKS
+#define HSG_PHASE_CLOCKS 0
+#endif
+constexpr bool kPhaseClocks = HSG_PHASE_CLOCKS != 0;
+__device__ inline uint64_t phase_clock() {
+  if constexpr (kPhaseClocks) return wall_clock64();
+  return 0;
+}
+
 __device__ inline int64_t wave_max_i64(int64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {

@@ -16,6 +16,9 @@ struct Comm;      // RCCL communicator wrapper (hsg_exchange.h)
 struct XBuffers;  // exchange scratch (hsg_exchange.h)
 
 int comm_unique_id(uint8_t *out);
+
+// hsg_testing_set_knob (include/hstream_gpu.h): read at op creation
+int64_t testing_knob(int knob);
 int comm_create(const uint8_t *id, int rank, int nranks, int device, int transport, uint64_t batch_cap, Comm **out,
                 std::string &err);
 int comm_split(Comm *parent, Comm **out, std::string &err);

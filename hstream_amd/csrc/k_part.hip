@@ -393,7 +393,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
   const int W = packed ? pp.words - 1 : pp.words;
   const uint32_t kbase = (uint32_t)sc->kbase;
   const uint64_t row = xcd_tile(blockIdx.x, pp.tiles);
-  const uint64_t q0 = wall_clock64();
+  const uint64_t q0 = phase_clock();
   for (int i = threadIdx.x; i < nb; i += kPNT) {
     cursor[i] = 0;
     goff[i] = pb.offt[row * (uint64_t)nb + i];
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
                          atomicAdd(&cursor[bk], 1u);
                        });
     __syncthreads();
-    q1 = wall_clock64();
+    q1 = phase_clock();
     // 2) sub-tile-local exclusive scan of the histogram
     uint32_t loc = 0;
     for (int k = lo; k < hi; ++k) loc += cursor[k];
@@ -444,7 +444,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
     uint32_t placed = 0;
     for (int k = 0; k < kPNT / 64; ++k) placed += swave[k];
     __syncthreads();
-    q2 = wall_clock64();
+    q2 = phase_clock();
     // 3) bucket-sorted order of the sub-tile's records (STABLE: in arrival
     // order inside each bucket's run)
     if constexpr (STABLE) {
@@ -469,7 +469,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
       }
     }
     __syncthreads();
-    q3 = wall_clock64();
+    q3 = phase_clock();
     // 4) coalesced write-out: consecutive lanes write consecutive words of a run
     const uint32_t inv = (1u << 20) / (uint32_t)W + 1;  // t / W for t < 2^16, W <= 16
     const uint32_t total = placed * (uint32_t)W;
@@ -515,8 +515,8 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
   }
   late = wave_sum_u64(late);
   if (err) atomicOr(&sc->err, err);
-  if (threadIdx.x == 0) {
-    const uint64_t q4 = wall_clock64();
+  if (kPhaseClocks && threadIdx.x == 0) {
+    const uint64_t q4 = phase_clock();
     atomicAdd((unsigned long long *)&sc->scratch[13], (unsigned long long)(q1 - q0));
     atomicAdd((unsigned long long *)&sc->scratch[14], (unsigned long long)(q2 - q1));
     atomicAdd((unsigned long long *)&sc->scratch[15], (unsigned long long)(q3 - q2));
@@ -659,7 +659,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
   const uint32_t kbase = (uint32_t)sc->kbase;
   const int64_t k_epoch = sc->k_epoch;
   const uint64_t row = xcd_tile(blockIdx.x, pp.tiles);
-  const uint64_t q0 = wall_clock64();
+  const uint64_t q0 = phase_clock();
   uint16_t *lstart = reinterpret_cast<uint16_t *>(cnt2);
   for (int i = threadIdx.x; i < (nb + 1) / 2; i += kPNT) cnt2[i] = 0;
   for (int i = threadIdx.x; i < nb; i += kPNT) cursor[i] = pb.offt[row * (uint64_t)nb + i];
@@ -774,7 +774,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
       if (W == 2) stage[q * W + 1] = col[r];
     }
     __syncthreads();
-    q1 = wall_clock64();
+    q1 = phase_clock();
     // write-out: record q goes to the row's slot for its bucket + (q - run start)
     for (uint32_t q = threadIdx.x; q < placed; q += kPNT) {
       const uint64_t h = stage[q * W];
@@ -796,8 +796,8 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
         for (int w = 0; w < kPW; ++w) wcnt[w][k] = 0;
   }
   if (err) atomicOr(&sc->err, err);
-  if (threadIdx.x == 0) {
-    const uint64_t q4 = wall_clock64();
+  if (kPhaseClocks && threadIdx.x == 0) {
+    const uint64_t q4 = phase_clock();
     atomicAdd((unsigned long long *)&sc->scratch[13], (unsigned long long)(q1 - q0));
     atomicAdd((unsigned long long *)&sc->scratch[16], (unsigned long long)(q4 - q1));
     atomicAdd((unsigned long long *)&sc->scratch[17], 1ull);

@@ -763,7 +763,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
   uint64_t fresh = 0, touched = 0;
   uint64_t c_ins = 0, c_claim = 0, c_steps = 0, c_back = 0, nseg = 0;  // phase clocks (HSG_PHASES)
   uint64_t c_phase = 0, npeer = 0;
-  const uint64_t c_start = wall_clock64();
+  const uint64_t c_start = phase_clock();
   // LDS insert of group g; returns false once the table passed half full
   // (then at most TAB / 2 + kPbNT - 1 entries: every probe sequence ends)
   auto insert = [&](uint64_t g) -> bool {
@@ -789,7 +789,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
   __syncthreads();
   // 1a. one pass over the whole bucket, PF record loads in flight per thread:
   // one segment when its groups fill at most half the table (the common case)
-  uint64_t ca = wall_clock64();
+  uint64_t ca = phase_clock();
   bool ok = true;
   for (uint64_t i0 = r0 + threadIdx.x; ok && i0 < r1; i0 += (uint64_t)PF * kPbNT) {
     uint64_t w0[PF];
@@ -831,7 +831,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
         lds_barrier();
       }
     }
-    { const uint64_t cb = wall_clock64(); c_ins += cb - ca; ca = cb; }
+    { const uint64_t cb = phase_clock(); c_ins += cb - ca; ca = cb; }
     // 2. rows of the segment's groups into LDS: every entry's home probe
     // issued at once (agent-scope loads: an earlier segment of this workgroup
     // may have written the rows), then the rows
@@ -905,7 +905,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
       }
     }
     lds_barrier();
-    { const uint64_t cb = wall_clock64(); c_claim += cb - ca; ca = cb; }
+    { const uint64_t cb = phase_clock(); c_claim += cb - ca; ca = cb; }
     // 3. the segment's records in arrival order (the next step's first two
     // words loaded while this step runs). A step's four waves run side by
     // side: (A) each lane folds its wave's earlier records of its group (lane
@@ -936,7 +936,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
       uint32_t h = 0;  // then the group's index
       int64_t pre[MS];
       identity_v<MS>(pv, pre);
-      const uint64_t t0 = wall_clock64();
+      const uint64_t t0 = phase_clock();
       if (in) {
         const uint64_t g = ((uint64_t)v.key() << 32) | v.krel(kbase);
         h = pb_home(g, LT);
@@ -956,7 +956,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
         peers &= x ? bb : ~bb;
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");  // the wave's elements in LDS
-      const uint64_t t1 = wall_clock64();
+      const uint64_t t1 = phase_clock();
       npeer += in ? (uint64_t)__popcll(peers) : 0ull;
       // (A) wave-local inclusive prefix over the group's lanes up to this one
       if (in) {
@@ -970,7 +970,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");  // every lane read its peers' elements
-      const uint64_t t2 = wall_clock64();
+      const uint64_t t2 = phase_clock();
       const int owner_lane = in ? 63 - __clzll((long long)peers) : lane;
       const bool owner = in && owner_lane == lane;
       if (owner) {
@@ -1008,7 +1008,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
 #pragma unroll
       for (int s = 0; s < MS; ++s) carry[s] = __shfl(carry[s], owner_lane, 64);
       lds_barrier();  // every owner has read the totals and the states
-      const uint64_t t3 = wall_clock64();
+      const uint64_t t3 = phase_clock();
       c_phase += (t1 - t0) | ((t2 - t1) << 21) | ((t3 - t2) << 42);  // 21-bit fields (per-step deltas)
       if (in) {
         int64_t fin[MS];
@@ -1030,7 +1030,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
       }
     }
     lds_barrier();  // the last step's owners have written their groups' states
-    { const uint64_t cb = wall_clock64(); c_steps += cb - ca; ca = cb; }
+    { const uint64_t cb = phase_clock(); c_steps += cb - ca; ca = cb; }
     // 4. the groups' states back to their rows
     for (int e = threadIdx.x; e < TAB; e += kPbNT) {
       if (tkey[e] == kEmpty) continue;
@@ -1044,8 +1044,8 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
     // the next segment reads these rows back (L1-bypassing loads): drain
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    c_back += wall_clock64() - ca;
-    ca = wall_clock64();
+    c_back += phase_clock() - ca;
+    ca = phase_clock();
     s0 = s1;
   }
   if (err) atomicOr(&sc->err, err);
@@ -1063,16 +1063,18 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
     }
     if (ff) atomicAdd((unsigned long long *)&sc->live_x[blockIdx.x & 7], (unsigned long long)ff);
     if (tt) atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)tt);
-    atomicAdd((unsigned long long *)&sc->scratch[36], (unsigned long long)c_ins);
-    atomicAdd((unsigned long long *)&sc->scratch[37], (unsigned long long)c_claim);
-    atomicAdd((unsigned long long *)&sc->scratch[38], (unsigned long long)c_steps);
-    atomicAdd((unsigned long long *)&sc->scratch[39], (unsigned long long)c_back);
-    atomicAdd((unsigned long long *)&sc->scratch[40], (unsigned long long)nseg);
-    atomicAdd((unsigned long long *)&sc->scratch[41], 1ull);
-    atomicAdd((unsigned long long *)&sc->scratch[42], (unsigned long long)(wall_clock64() - c_start));
-    if (blockIdx.x == 0) sc->scratch[43] = c_phase;  // one workgroup's step sub-phases
+    if (kPhaseClocks) {
+      atomicAdd((unsigned long long *)&sc->scratch[36], (unsigned long long)c_ins);
+      atomicAdd((unsigned long long *)&sc->scratch[37], (unsigned long long)c_claim);
+      atomicAdd((unsigned long long *)&sc->scratch[38], (unsigned long long)c_steps);
+      atomicAdd((unsigned long long *)&sc->scratch[39], (unsigned long long)c_back);
+      atomicAdd((unsigned long long *)&sc->scratch[40], (unsigned long long)nseg);
+      atomicAdd((unsigned long long *)&sc->scratch[41], 1ull);
+      atomicAdd((unsigned long long *)&sc->scratch[42], (unsigned long long)(phase_clock() - c_start));
+      if (blockIdx.x == 0) sc->scratch[43] = c_phase;  // one workgroup's step sub-phases
+    }
   }
-  if (lane == 0 && npeer) atomicAdd((unsigned long long *)&sc->scratch[44], (unsigned long long)npeer);
+  if (kPhaseClocks && lane == 0 && npeer) atomicAdd((unsigned long long *)&sc->scratch[44], (unsigned long long)npeer);
 }
 
 // Rows of one-window ops in arrival order: the record's window as the

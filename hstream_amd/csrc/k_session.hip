@@ -990,7 +990,7 @@ template <int MS, int W>
 __global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Program prog, int np_log2, int bshift,
                                                    SessPart sp, DevScalars *sc) {
   __shared__ SortLds<W> L;
-  const uint64_t c0 = wall_clock64();
+  const uint64_t c0 = phase_clock();
   uint64_t c_ins = 0, c_scan = 0, c_place = 0, c_key = 0, c1 = 0;
   constexpr int B = 8;  // loads in flight per thread in the bucket passes
   const uint32_t b = blockIdx.x;
@@ -1075,7 +1075,7 @@ __global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Pr
     }
   __syncthreads();
   uint64_t bigmask = indexable ? 0ull : ~0ull;  // a bucket that cannot be indexed goes to the big path whole
-  c1 = wall_clock64();
+  c1 = phase_clock();
   const uint32_t rstride = 2 + prog.n_slots;
   constexpr int RP = kSoCH / kSoNT;  // records per thread in a sub-bucket pass
   for (int sub = 0; indexable && sub < nsub; ++sub) {
@@ -1086,7 +1086,7 @@ __global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Pr
       continue;
     }
     const uint16_t *lst = sidx + L.suboff[sub];
-    uint64_t ca = wall_clock64();
+    uint64_t ca = phase_clock();
     // 1. keys of the sub-bucket into the LDS table, records per key; the
     // records' words stay in registers for the placement
     for (int h = threadIdx.x; h < kSoTab; h += kSoNT) {
@@ -1130,7 +1130,7 @@ __global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Pr
       atomicAdd(&L.tcnt[h], 1u);
     }
     lds_barrier();
-    { const uint64_t cb = wall_clock64(); c_ins += cb - ca; ca = cb; }
+    { const uint64_t cb = phase_clock(); c_ins += cb - ca; ca = cb; }
     // 2. segment starts: exclusive scan of the counts
     // (records in the low 16 bits, occupied slots in the high: one scan gives
     // each key its segment start and its group index)
@@ -1178,7 +1178,7 @@ __global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Pr
     const uint64_t runbase = r0 + L.suboff[sub];
     uint32_t *gsp = sp.gsparse + (r0 + L.suboff[sub]) * 4;
     lds_barrier();
-    { const uint64_t cb = wall_clock64(); c_scan += cb - ca; ca = cb; }
+    { const uint64_t cb = phase_clock(); c_scan += cb - ca; ca = cb; }
     // 3. place (ts, words) in the key's segment
 #pragma unroll
     for (int u = 0; u < RP; ++u) {
@@ -1191,7 +1191,7 @@ __global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Pr
       L.qslot[q] = (uint16_t)hslot[u];
     }
     lds_barrier();
-    { const uint64_t cb = wall_clock64(); c_place += cb - ca; ca = cb; }
+    { const uint64_t cb = phase_clock(); c_place += cb - ca; ca = cb; }
     // 4. every record ranked by ts within its key's segment (<= kSoSmall) and
     // written out in (key, ts) order; one group record per key
     for (uint32_t q = threadIdx.x; q < m2; q += kSoNT) {
@@ -1216,7 +1216,7 @@ __global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Pr
           make_uint4(key, (uint32_t)(runbase + sa), L.tcnt[h] - sa, 0u);
     }
     lds_barrier();
-    c_key += wall_clock64() - ca;
+    c_key += phase_clock() - ca;
   }
   // the bucket's group records, dense: one reservation per bucket
   if (threadIdx.x == 0) {
@@ -1237,8 +1237,8 @@ __global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Pr
     for (uint32_t j = threadIdx.x; j < c; j += kSoNT) reinterpret_cast<uint4 *>(sp.groups)[d + j] = src[j];
     d += c;
   }
-  if (threadIdx.x == 0) {  // phase clocks (100 MHz), HSG_PHASES
-    const uint64_t c2 = wall_clock64();
+  if (kPhaseClocks && threadIdx.x == 0) {  // phase clocks (100 MHz), HSG_PHASES
+    const uint64_t c2 = phase_clock();
     atomicAdd((unsigned long long *)&sc->scratch[24], (unsigned long long)(c1 - c0));
     atomicAdd((unsigned long long *)&sc->scratch[25], (unsigned long long)c_ins);
     atomicAdd((unsigned long long *)&sc->scratch[26], (unsigned long long)c_scan);

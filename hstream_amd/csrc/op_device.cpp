@@ -580,7 +580,11 @@ int finish_batch(OpDevice &d, int64_t wm_in, uint64_t n, PushResult &r, std::str
   int rc = fetch_scalars(d, err);
   if (rc != HSG_OK) return rc;
   const DevScalars &s = *d.h_sc;
-  static const bool phases = getenv("HSG_PHASES") != nullptr;
+#ifndef HSG_PHASE_CLOCKS
+#define HSG_PHASE_CLOCKS 0
+#endif
+  // the phase clocks exist only in a PHASES=1 build (hsg_dev.h kPhaseClocks)
+  static const bool phases = HSG_PHASE_CLOCKS && getenv("HSG_PHASES") != nullptr;
   if (phases && s.scratch[12])
     fprintf(stderr, "[hsg phases] agg wg=%llu init=%.1fus records=%.1fus flush=%.1fus tail=%.1fus (per-wg avg)\n",
             (unsigned long long)s.scratch[12], s.scratch[8] * 0.01 / s.scratch[12], s.scratch[9] * 0.01 / s.scratch[12],

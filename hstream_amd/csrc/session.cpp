@@ -133,9 +133,10 @@ int session_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &pr
   if (rc != HSG_OK) return rc;
   d.cap = kcap;
   // arena: the expected live sessions, grown by compaction when a batch needs
-  // more (HSG_SESS_ARENA_MIN: a smaller floor, so tests reach the refills)
+  // more (the HSG_KNOB_SESS_ARENA_MIN testing knob: a smaller floor, so tests
+  // reach the refills)
   uint64_t amin = 1u << 20;
-  if (const char *e = getenv("HSG_SESS_ARENA_MIN")) amin = strtoull(e, nullptr, 10) ? strtoull(e, nullptr, 10) : amin;
+  if (const int64_t v = testing_knob(HSG_KNOB_SESS_ARENA_MIN); v > 0) amin = (uint64_t)v;
   rc = alloc_arena(t, pow2_at_least(rows > amin ? rows : amin), err);
   if (rc != HSG_OK) return rc;
   DTRY(hipMalloc((void **)&t.meta, M_WORDS * sizeof(uint64_t)));

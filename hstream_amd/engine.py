@@ -44,9 +44,31 @@ def load_library(path=LIB_PATH):
     L.hsg_push_batch_async.restype = C.c_int
     L.hsg_op_wait.argtypes = [vp]
     L.hsg_op_wait.restype = C.c_int
+    L.hsg_testing_set_knob.argtypes = [C.c_int32, C.c_int64]
+    L.hsg_testing_set_knob.restype = C.c_int
     declare_op_functions(L, "hsg")
     _lib = L
     return L
+
+
+class testing_knob:
+    """Context manager over hsg_testing_set_knob (tests only): the knob holds
+    for ops created inside the block, then returns to its default."""
+
+    DEFAULTS = {abi.HSG_KNOB_XPART_LOG2: -1, abi.HSG_KNOB_SESS_ARENA_MIN: 0}
+
+    def __init__(self, knob, value):
+        self.knob, self.value = knob, value
+
+    def __enter__(self):
+        rc = load_library().hsg_testing_set_knob(self.knob, self.value)
+        if rc != abi.HSG_OK:
+            raise abi.HStreamGpuError(rc, "hsg_testing_set_knob")
+        return self
+
+    def __exit__(self, *exc):
+        load_library().hsg_testing_set_knob(self.knob, self.DEFAULTS[self.knob])
+        return False
 
 
 def comm_unique_id() -> bytes:

@@ -296,6 +296,14 @@ int  hsg_dump_state(hsg_op *op, hsg_rows *out, uint64_t *n_out);
  * "last batch" fields describe the most recent hsg_push_batch. */
 int  hsg_op_stats(const hsg_op *op, hsg_stats *out);
 
+/* ---- testing hooks (not used by the drop-in) ----------------------------------
+ * Process-wide knobs that let tests reach rare paths at small sizes; they apply
+ * to ops created afterwards. Production code never sets them (defaults). */
+#define HSG_KNOB_XPART_LOG2     1 /* a 1-rank exchange partitions its records into 2^v owner
+                                     regions, all its own (0..6); -1 = log2(ranks)          */
+#define HSG_KNOB_SESS_ARENA_MIN 2 /* floor of the session arena in rows (> 0); 0 = 2^20      */
+int  hsg_testing_set_knob(int32_t knob, int64_t value);
+
 #ifdef __cplusplus
 }
 #endif

@@ -274,18 +274,19 @@ def _x_specs():
 @pytest.mark.parametrize("xpart", [None, "2"], ids=["xpart1", "xpart4"])
 @pytest.mark.parametrize("late", [False, True], ids=["no_late", "late"])
 @pytest.mark.parametrize("spec", _x_specs())
-def test_exchange_path_single_rank(xeng, spec, late, xpart, monkeypatch):
+def test_exchange_path_single_rank(xeng, spec, late, xpart):
     """xpart4: the fast exchange partitions the single rank's records into 4
-    owner regions (HSG_XPART_LOG2=2), all sent to rank 0, so the multi-owner
-    offsets and scatter run with one GPU; late batches take the classic path."""
-    if xpart:
-        monkeypatch.setenv("HSG_XPART_LOG2", xpart)
+    owner regions (testing knob HSG_KNOB_XPART_LOG2 = 2), all sent to rank 0, so
+    the multi-owner offsets and scatter run with one GPU; late batches take the
+    classic path."""
+    from hstream_amd.engine import testing_knob
     batches = []
     for bi in range(3):
         key, ts, cols, valid = gen_small(2000 + bi, 4000, 29, col_types=spec.col_types, span=60_000,
                                          base=5_000_000 + bi * 60_000, very_late=late)
         batches.append((key, ts, cols, valid))
-    g = xeng.op(spec)
+    with testing_knob(abi.HSG_KNOB_XPART_LOG2, int(xpart) if xpart else -1):
+        g = xeng.op(spec)
     o = pyoracle.OracleOp(spec)
     f64 = spec.agg_is_f64()
     wg = wo = -1

@@ -65,18 +65,19 @@ def test_hot_keys_big_buckets(eng, mode, gap):
 
 
 @pytest.mark.parametrize("mode", [abi.HSG_EMIT_PER_BATCH, abi.HSG_EMIT_PER_RECORD], ids=["merge", "replay"])
-def test_arena_refill_mid_batch(eng, mode, monkeypatch):
+def test_arena_refill_mid_batch(eng, mode):
     """A 1024-row arena floor: every batch outgrows it, so blocks / chunks that
     cannot reserve their lists stop, the host compacts and grows the arena and
     the batch resumes; the result is unchanged."""
-    monkeypatch.setenv("HSG_SESS_ARENA_MIN", "1024")
+    from hstream_amd.engine import testing_knob
     spec = OpSpec(abi.HSG_SESSION, mode, gap_ms=300, col_types=[abi.HSG_I64, abi.HSG_F64],
                   aggs=ALL_AGG_SETS["mixed"] if mode == abi.HSG_EMIT_PER_RECORD else
                   [(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0), (abi.HSG_SUM, 1)], state_capacity=16)
     batches = [gen_small(500 + bi, 40_000, 3_000, col_types=spec.col_types, span=120_000,
                          base=7_000_000 + bi * 100_000) for bi in range(4)]
     batches += _hot_batches(77, 20_000, nb=2)
-    _drive(eng, spec, batches, faithful=False)
+    with testing_knob(abi.HSG_KNOB_SESS_ARENA_MIN, 1024):
+        _drive(eng, spec, batches, faithful=False)
 
 
 def test_key_table_growth(eng):
