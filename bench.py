@@ -314,7 +314,7 @@ def host_steps(op, keys, ts, cols, pieces, spec, emit, world, args):
     import numpy as np
     import torch
     from hstream_amd import abi
-    from hstream_amd.columnar import make_batch, narrow_columns
+    from hstream_amd.columnar import make_batch, narrow_columns, narrow_keys
     descs, host = [], []
     nbytes = 0
     encs = set()
@@ -326,6 +326,7 @@ def host_steps(op, keys, ts, cols, pieces, spec, emit, world, args):
         if args.wide:
             tsa, base, cs2, enc, scale = t, None, cs, [abi.HSG_ENC_FULL] * len(cs), [0] * len(cs)
         else:
+            k = narrow_keys(k)
             tsa, base, cs2, enc, scale = narrow_columns(t, cs, spec.col_types, dec)
         pk = torch.from_numpy(np.ascontiguousarray(k)).pin_memory()
         pt = torch.from_numpy(np.ascontiguousarray(tsa)).pin_memory()
@@ -334,8 +335,8 @@ def host_steps(op, keys, ts, cols, pieces, spec, emit, world, args):
                              ts_base=base, col_enc=enc, col_scale=scale)
         descs.append(b)
         host.append((pk, pt, pc, keep))
-        nbytes += m * 4 + pt.element_size() * m + sum(c.element_size() * m for c in pc)
-        encs.add(("ts32" if base is not None else "ts64") + "+" + ",".join(
+        nbytes += pk.element_size() * m + pt.element_size() * m + sum(c.element_size() * m for c in pc)
+        encs.add(("k16" if pk.element_size() == 2 else "k32") + "+" + ("ts32" if base is not None else "ts64") + "+" + ",".join(
             {abi.HSG_ENC_FULL: "full", abi.HSG_ENC_I32: "i32", abi.HSG_ENC_DEC32: "dec32"}[e] for e in enc))
     n_rank = sum(m for _, m in pieces)
     wpr = -(-spec.size_ms // spec.advance_ms) if spec.window_kind == abi.HSG_HOPPING else 1

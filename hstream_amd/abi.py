@@ -62,6 +62,7 @@ HSG_ENC_FULL = 0
 HSG_ENC_TS32 = 1
 HSG_ENC_I32 = 2
 HSG_ENC_DEC32 = 3
+HSG_ENC_K16 = 4
 
 
 class hsg_engine_config(C.Structure):
@@ -107,7 +108,7 @@ class hsg_batch(C.Structure):
         ("valid", C.POINTER(C.c_void_p)),
         ("ready_event", C.c_void_p),
         ("ts_enc", C.c_int32),
-        ("reserved", C.c_int32),
+        ("key_enc", C.c_int32),
         ("ts_base", C.c_int64),
         ("col_enc", C.c_uint8 * 8),
         ("col_scale", C.c_uint8 * 8),

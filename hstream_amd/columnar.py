@@ -75,7 +75,8 @@ def make_batch(key_id, ts, cols=(), valid=None, mem=None, ts_base=None, col_enc=
 
     Returns (hsg_batch, keepalive). Arrays must be contiguous: key_id uint32 /
     int32, ts int64, cols int64 or float64, valid uint8 (or None = all present).
-    Narrow transport (include/hstream_gpu.h hsg_enc): ts_base given = ts holds
+    Narrow transport (include/hstream_gpu.h hsg_enc): a uint16 key_id = ids sent
+    as HSG_ENC_K16 (no HSG_KEY_NONE in the batch); ts_base given = ts holds
     int32 offsets from it (HSG_ENC_TS32); col_enc[c] HSG_ENC_I32 / HSG_ENC_DEC32
     = column c holds int32 values / decimal mantissas (col_scale[c] digits).
     """
@@ -84,7 +85,8 @@ def make_batch(key_id, ts, cols=(), valid=None, mem=None, ts_base=None, col_enc=
     col_enc = list(col_enc or [abi.HSG_ENC_FULL] * len(cols))
     keep = [key_id, ts]
     if not _is_torch(ts):
-        key_id = np.ascontiguousarray(key_id, dtype=np.uint32)
+        key_id = np.asarray(key_id)
+        key_id = np.ascontiguousarray(key_id, dtype=np.uint16 if key_id.dtype == np.uint16 else np.uint32)
         ts = np.ascontiguousarray(ts, dtype=np.int32 if ts_base is not None else np.int64)
         cols = [np.ascontiguousarray(c, dtype=np.int32) if e != abi.HSG_ENC_FULL else np.ascontiguousarray(c)
                 for c, e in zip(cols, col_enc)]
@@ -111,6 +113,8 @@ def make_batch(key_id, ts, cols=(), valid=None, mem=None, ts_base=None, col_enc=
         cols=C.cast(col_ptrs, C.POINTER(C.c_void_p)),
         valid=C.cast(valid_ptrs, C.POINTER(C.c_void_p)) if valid_ptrs is not None else None,
     )
+    if str(key_id.dtype) in ("uint16", "torch.int16", "torch.uint16"):
+        b.key_enc = abi.HSG_ENC_K16  # (HSG_ENC_K16: ids < 65536, no HSG_KEY_NONE)
     if ts_base is not None:
         b.ts_enc = abi.HSG_ENC_TS32
         b.ts_base = int(ts_base)
@@ -118,6 +122,15 @@ def make_batch(key_id, ts, cols=(), valid=None, mem=None, ts_base=None, col_enc=
         b.col_enc[c] = int(e)
         b.col_scale[c] = int(col_scale[c]) if col_scale else 0
     return b, keep
+
+
+def narrow_keys(key_id):
+    """The key column as uint16 (HSG_ENC_K16) when every id fits and no record
+    is HSG_KEY_NONE, else unchanged (uint32)."""
+    key_id = np.asarray(key_id, dtype=np.uint32)
+    if key_id.size and int(key_id.max()) < 65536:
+        return key_id.astype(np.uint16)
+    return key_id
 
 
 def narrow_columns(ts, cols, col_types, dec_scale=None):

@@ -44,11 +44,25 @@ constexpr size_t kSlotHdr = 2 * kMaxRanks * sizeof(uint64_t);
 
 static uint32_t *ctl_count(HostComm *h) { return (uint32_t *)h->base; }
 static uint32_t *ctl_gen(HostComm *h) { return (uint32_t *)(h->base + 64); }
+// set once a barrier timed out or a collective's ranks disagreed: the
+// communicator is dead, every later barrier on it fails at once on every rank
+// (a timed-out rank's arrival stays in the counter, so the generations no
+// longer line up)
+static uint32_t *ctl_failed(HostComm *h) { return (uint32_t *)(h->base + 128); }
+static int host_fail(HostComm *h, std::string &err, const std::string &why) {
+  __atomic_store_n(ctl_failed(h), 1u, __ATOMIC_RELEASE);
+  err = why;
+  return HSG_E_COMM;
+}
 static char *slot(HostComm *h, int r) { return h->base + kCtrl + (size_t)r * (kSlotHdr + h->slot_data); }
 
 // centralised barrier over the segment's counter; a peer that never arrives
 // (crashed) ends it with an error after a minute instead of hanging
 static int host_barrier(HostComm *h, std::string &err) {
+  if (__atomic_load_n(ctl_failed(h), __ATOMIC_ACQUIRE)) {
+    err = "host transport: the communicator failed earlier (a rank timed out or disagreed)";
+    return HSG_E_COMM;
+  }
   const uint32_t gen = __atomic_load_n(ctl_gen(h), __ATOMIC_ACQUIRE);
   const uint32_t arrived = __atomic_add_fetch(ctl_count(h), 1u, __ATOMIC_ACQ_REL);
   if (arrived == (uint32_t)h->nranks) {
@@ -60,10 +74,10 @@ static int host_barrier(HostComm *h, std::string &err) {
   for (uint64_t spin = 0; __atomic_load_n(ctl_gen(h), __ATOMIC_ACQUIRE) == gen; ++spin) {
     if ((spin & 1023) == 0) {
       sched_yield();
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
-        err = "host transport: a peer rank did not reach the barrier within 60 s";
-        return HSG_E_COMM;
-      }
+      if (__atomic_load_n(ctl_failed(h), __ATOMIC_ACQUIRE))
+        return host_fail(h, err, "host transport: a peer rank failed the collective");
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+        return host_fail(h, err, "host transport: a peer rank did not reach the barrier within 60 s");
     }
   }
   return HSG_OK;
@@ -164,6 +178,17 @@ int comm_create(const uint8_t *id_bytes, int rank, int nranks, int device, int t
 
 // A communicator of the same ranks for one operator (collective over the
 // parent's ranks, so every rank calls it in the same op-creation order).
+// comm_agree's stream and buffer (a failure here fails the split, before any
+// op state exists)
+static int agree_alloc(Comm *c, std::string &err) {
+  if (hipStreamCreateWithFlags(&c->agree_s, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void **)&c->agree_buf, ((size_t)c->nranks + 1) * sizeof(int64_t)) != hipSuccess) {
+    err = "comm_split: agreement stream / buffer";
+    return HSG_E_DEVICE;
+  }
+  return HSG_OK;
+}
+
 int comm_split(Comm *parent, Comm **out, std::string &err) {
   Comm *c = new Comm();
   c->rank = parent->rank;
@@ -177,7 +202,7 @@ int comm_split(Comm *parent, Comm **out, std::string &err) {
       return rc;
     }
     *out = c;
-    return HSG_OK;
+    return agree_alloc(c, err);
   }
   ncclResult_t r = ncclCommSplit(parent->comm, 0, parent->rank, &c->comm, nullptr);
   if (r != ncclSuccess) {
@@ -186,11 +211,13 @@ int comm_split(Comm *parent, Comm **out, std::string &err) {
     return HSG_E_COMM;
   }
   *out = c;
-  return HSG_OK;
+  return agree_alloc(c, err);
 }
 
 void comm_destroy(Comm *c) {
   if (!c) return;
+  if (c->agree_buf) hipFree(c->agree_buf);
+  if (c->agree_s) hipStreamDestroy(c->agree_s);
   if (c->comm) ncclCommDestroy(c->comm);
   host_close(c->host);
   delete c;
@@ -248,19 +275,24 @@ int comm_allgather(Comm *c, const void *send, void *recv, size_t count, ncclData
 // an int64 per rank. Returns the first failing rank's code (HSG_OK when all
 // succeeded), or the transport's own error.
 int comm_agree(Comm *c, int rc_local, std::string &err) {
-  hipStream_t s = nullptr;
-  int64_t *buf = nullptr;
-  CHTRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipStream_t s = c->agree_s;
+  int64_t *buf = c->agree_buf;
   std::vector<int64_t> h((size_t)c->nranks + 1, 0);
   h[0] = rc_local;
   int rc = HSG_OK;
-  hipError_t e = hipMalloc((void **)&buf, ((size_t)c->nranks + 1) * sizeof(int64_t));
-  if (e == hipSuccess) e = hipMemcpyAsync(buf, h.data(), sizeof(int64_t), hipMemcpyHostToDevice, s);
+  if (!s || !buf) {
+    err = "comm_agree: no agreement buffer (communicator setup failed)";
+    return HSG_E_DEVICE;
+  }
+  // every step below runs even after a local failure: a rank that skipped
+  // the all-gather would leave its peers waiting in it
+  hipError_t e = hipMemcpyAsync(buf, h.data(), sizeof(int64_t), hipMemcpyHostToDevice, s);
   if (e != hipSuccess) {
     err = std::string("comm_agree: ") + hipGetErrorString(e);
     rc = HSG_E_DEVICE;
   }
-  if (rc == HSG_OK) rc = comm_allgather(c, buf, buf + 1, 1, ncclInt64, sizeof(int64_t), s, err);
+  const int grc = comm_allgather(c, buf, buf + 1, 1, ncclInt64, sizeof(int64_t), s, err);
+  if (rc == HSG_OK) rc = grc;
   if (rc == HSG_OK) {
     e = hipMemcpyAsync(h.data() + 1, buf + 1, (size_t)c->nranks * sizeof(int64_t), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -276,8 +308,6 @@ int comm_agree(Comm *c, int rc_local, std::string &err) {
         rc = (int)h[1 + q];
         break;
       }
-  if (buf) hipFree(buf);
-  hipStreamDestroy(s);
   return rc;
 }
 
@@ -307,11 +337,8 @@ int comm_alltoallv(Comm *c, const void *send, const size_t *scount, const size_t
   if (rc != HSG_OK) return rc;
   for (int q = 0; q < G; ++q) {
     const uint64_t *ph = (const uint64_t *)slot(h, q);
-    if (ph[me] != rcount[q]) {
-      err = "host transport: all-to-all counts disagree";
-      host_barrier(h, err);
-      return HSG_E_COMM;
-    }
+    if (ph[me] != rcount[q])  // every waiter sees the flag: no rank is left in a barrier
+      return host_fail(h, err, "host transport: all-to-all counts disagree");
     if (rcount[q])
       CHTRY(hipMemcpy((char *)recv + rdispl[q] * elem, slot(h, q) + kSlotHdr + ph[kMaxRanks + me] * elem,
                       rcount[q] * elem, hipMemcpyHostToDevice));

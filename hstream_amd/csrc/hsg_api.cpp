@@ -376,15 +376,32 @@ extern "C" int hsg_op_create(hsg_engine *eng, const hsg_op_config *cfg, hsg_op *
       // in the same order (the same queries)
       std::lock_guard<std::mutex> lk(eng->mu);
       rc = comm_split(eng->comm, &op->comm, eng->err);
-      if (rc != HSG_OK) { delete op; return rc; }
+      if (rc != HSG_OK) {
+        comm_destroy(op->comm);
+        delete op;
+        return rc;
+      }
     }
-    rc = op_device_init(op->dev, op->cfg, op->prog, eng->batch_cap, eng->nranks, op->comm != nullptr,
-                        hsg_windows_per_record(op->cfg),
-                        eng->err);
+    // a sharded op's ranks must all reach the agreement below, whatever
+    // happened here: exceptions become a status
+    try {
+      rc = op_device_init(op->dev, op->cfg, op->prog, eng->batch_cap, eng->nranks, op->comm != nullptr,
+                          hsg_windows_per_record(op->cfg), eng->err);
+    } catch (const std::bad_alloc &) {
+      rc = HSG_E_OOM;
+      eng->err = "op_device_init: out of host memory";
+    } catch (...) {
+      rc = HSG_E_DEVICE;
+      eng->err = "op_device_init: exception";
+    }
     if (op->comm) {
       // the ranks agree on the creation: a rank whose shard failed (e.g. out
       // of memory) takes every rank's shard down with it, so no rank keeps an
-      // op whose first exchange would wait forever on the missing one
+      // op whose first exchange would wait forever on the missing one. The
+      // failed shard's memory goes first, and the agreement's stream and
+      // buffer were made with the communicator (comm_split), so nothing can
+      // fail between here and the collective.
+      if (rc != HSG_OK) op_device_free(op->dev);
       std::string aerr;
       const int arc = comm_agree(op->comm, rc, aerr);
       if (rc == HSG_OK && arc != HSG_OK) {
@@ -459,6 +476,7 @@ static int validate_batch(hsg_op *op, const hsg_batch *b, const int64_t *inout_w
     if (b->n && (!b->cols || !b->cols[c])) return fail(op->err, HSG_E_INVALID, "null value column");
   // narrow transport (hsg_enc): ts as TS32 only, i64 columns as I32, f64 columns as DEC32
   if (b->ts_enc != HSG_ENC_FULL && b->ts_enc != HSG_ENC_TS32) return fail(op->err, HSG_E_INVALID, "bad ts_enc");
+  if (b->key_enc != HSG_ENC_FULL && b->key_enc != HSG_ENC_K16) return fail(op->err, HSG_E_INVALID, "bad key_enc");
   for (int c = 0; c < b->n_cols; ++c) {
     const int e = b->col_enc[c];
     const bool f64 = op->col_types[c] == HSG_F64;

@@ -18,6 +18,11 @@ struct Comm {
   uint64_t slot_bytes = 0;
   int rank = 0;
   int nranks = 1;
+  // comm_agree's stream and [nranks + 1] buffer, made with the communicator so
+  // that a rank whose op creation failed (out of memory) still reaches the
+  // collective without allocating anything
+  hipStream_t agree_s = nullptr;
+  int64_t *agree_buf = nullptr;
 };
 
 // collectives over either transport (RCCL calls, or the host copies)

@@ -255,6 +255,8 @@ void launch_fill_u32(hipStream_t s, uint32_t *p, uint64_t n, uint32_t v);
 // the op's full-width staging, on the device after the H2D
 struct WidenArgs {
   uint64_t n;
+  const uint16_t *k16;           // null: key_id is not narrow
+  uint32_t *key;
   const int32_t *ts32;           // null: ts is not narrow
   int64_t ts_base;
   int64_t *ts;
@@ -264,7 +266,7 @@ struct WidenArgs {
 };
 void launch_widen(hipStream_t s, const WidenArgs &w);
 inline bool batch_narrow(const hsg_batch *b) {
-  bool any = b->ts_enc != HSG_ENC_FULL;
+  bool any = b->ts_enc != HSG_ENC_FULL || b->key_enc != HSG_ENC_FULL;
   for (int c = 0; c < b->n_cols && c < kMaxCols; ++c) any |= b->col_enc[c] != HSG_ENC_FULL;
   return any;
 }

@@ -88,6 +88,7 @@ struct OpDevice {
   int64_t *st_seq = nullptr;    // global record seq of received records (multi-GPU)
   int64_t *st_wm = nullptr;     // per-record watermark of received records (multi-GPU)
   int32_t *nar_ts = nullptr;    // narrow transport staging of synchronous host pushes (hsg_enc)
+  uint16_t *nar_key = nullptr;
   int32_t *nar_col[kMaxCols] = {};
   // prestaged host batches of asynchronous pushes: the H2D
   // copies of the next queued batch run on their own stream, into the other

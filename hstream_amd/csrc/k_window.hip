@@ -187,11 +187,12 @@ void launch_tw_reset_dirty(hipStream_t s, const TwTable &t, const Program &prog,
                      (unsigned long long *)cnt);
   hipLaunchKernelGGL(k_tw_reset_dirty, dim3(4096), dim3(256), 0, s, t, prog, nblk, (const uint64_t *)cnt);
 }
-// narrow transport -> full width: one pass, coalesced 4-byte loads and
-// 8-byte stores (HBM: 4 + 8 bytes per narrow column and record)
+// narrow transport -> full width: one pass, coalesced 2- / 4-byte loads and
+// 4- / 8-byte stores
 __global__ __launch_bounds__(256) void k_widen(WidenArgs w) {
   const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < w.n; i += step) {
+    if (w.k16) w.key[i] = (uint32_t)w.k16[i];
     if (w.ts32) w.ts[i] = w.ts_base + (int64_t)w.ts32[i];
 #pragma unroll
     for (int c = 0; c < kMaxCols; ++c) {

@@ -318,6 +318,7 @@ void op_device_free(OpDevice &d) {
   dfree(d.st_seq);
   dfree(d.st_wm);
   dfree(d.nar_ts);
+  dfree(d.nar_key);
   for (int c = 0; c < kMaxCols; ++c) dfree(d.nar_col[c]);
   if (d.h2d) hipStreamSynchronize(d.h2d);
   for (auto &s : d.pre) {
@@ -398,7 +399,7 @@ int op_prestage(OpDevice &d, const hsg_batch *b, int set, std::string &err) {
   // narrow columns (hsg_enc) land in the first half of their full-width
   // buffers; stage_batch widens them on the op's stream
   if (n) {
-    DTRY(hipMemcpyAsync(s.key, b->key_id, n * 4, k, d.h2d));
+    DTRY(hipMemcpyAsync(s.key, b->key_id, n * (b->key_enc == HSG_ENC_K16 ? 2 : 4), k, d.h2d));
     DTRY(hipMemcpyAsync(s.ts, b->ts, n * (b->ts_enc == HSG_ENC_TS32 ? 4 : 8), k, d.h2d));
     for (int c = 0; c < b->n_cols; ++c) {
       DTRY(hipMemcpyAsync(s.col[c], b->cols[c], n * (b->col_enc[c] != HSG_ENC_FULL ? 4 : 8), k, d.h2d));
@@ -410,13 +411,18 @@ int op_prestage(OpDevice &d, const hsg_batch *b, int set, std::string &err) {
 }
 
 // Narrow transport columns (include/hstream_gpu.h hsg_enc) at device
-// addresses ts32 / c32 (null = that array is full width and already in kb)
+// addresses k16 / ts32 / c32 (used for the arrays the batch sends narrow)
 // -> the op's full-width staging; kb points there afterwards.
-static int widen_batch(OpDevice &d, const hsg_batch *b, const void *ts32, const void *const *c32, Batch &kb,
-                       std::string &err) {
+static int widen_batch(OpDevice &d, const hsg_batch *b, const void *k16, const void *ts32, const void *const *c32,
+                       Batch &kb, std::string &err) {
   WidenArgs w;
   memset(&w, 0, sizeof(w));
   w.n = b->n;
+  if (b->key_enc == HSG_ENC_K16) {
+    w.k16 = (const uint16_t *)k16;
+    w.key = d.st_key;
+    kb.key = d.st_key;
+  }
   if (b->ts_enc == HSG_ENC_TS32) {
     w.ts32 = (const int32_t *)ts32;
     w.ts_base = b->ts_base;
@@ -455,7 +461,7 @@ int stage_batch(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err, in
     if (batch_narrow(b)) {
       const void *c32[kMaxCols];
       for (int c = 0; c < b->n_cols; ++c) c32[c] = s.col[c];
-      return widen_batch(d, b, s.ts, c32, kb, err);
+      return widen_batch(d, b, s.key, s.ts, c32, kb, err);
     }
     return HSG_OK;
   }
@@ -468,19 +474,21 @@ int stage_batch(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err, in
       kb.col[c] = (const int64_t *)b->cols[c];
       kb.valid[c] = (b->valid && b->valid[c]) ? b->valid[c] : nullptr;
     }
-    if (batch_narrow(b)) return widen_batch(d, b, b->ts, b->cols, kb, err);
+    if (batch_narrow(b)) return widen_batch(d, b, b->key_id, b->ts, b->cols, kb, err);
     return HSG_OK;
   }
   if (batch_narrow(b)) {
     // host narrow batch, synchronous push: H2D into the narrow staging, widen
     if (!d.nar_ts) {
       DTRY(dalloc(&d.nar_ts, d.batch_cap));
+      DTRY(dalloc(&d.nar_key, d.batch_cap));
       for (int c = 0; c < d.n_cols; ++c) DTRY(dalloc(&d.nar_col[c], d.batch_cap));
     }
     const hipMemcpyKind k = hipMemcpyHostToDevice;
     const void *c32[kMaxCols] = {};
     if (n) {
-      DTRY(hipMemcpyAsync(d.st_key, b->key_id, n * 4, k, d.stream));
+      if (b->key_enc == HSG_ENC_K16) DTRY(hipMemcpyAsync(d.nar_key, b->key_id, n * 2, k, d.stream));
+      else DTRY(hipMemcpyAsync(d.st_key, b->key_id, n * 4, k, d.stream));
       if (b->ts_enc == HSG_ENC_TS32) DTRY(hipMemcpyAsync(d.nar_ts, b->ts, n * 4, k, d.stream));
       else DTRY(hipMemcpyAsync(d.st_ts, b->ts, n * 8, k, d.stream));
     }
@@ -496,7 +504,7 @@ int stage_batch(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err, in
         kb.valid[c] = d.st_valid[c];
       }
     }
-    return widen_batch(d, b, d.nar_ts, c32, kb, err);
+    return widen_batch(d, b, d.nar_key, d.nar_ts, c32, kb, err);
   }
   if (n) {
     DTRY(hipMemcpyAsync(d.st_key, b->key_id, n * 4, hipMemcpyHostToDevice, d.stream));

@@ -109,9 +109,11 @@ enum hsg_enc {
   HSG_ENC_FULL  = 0, /* the column's own type: int64 ts, int64 / double values          */
   HSG_ENC_TS32  = 1, /* ts only: int32 offsets from hsg_batch.ts_base                   */
   HSG_ENC_I32   = 2, /* an HSG_I64 column sent as int32 (every value fits)              */
-  HSG_ENC_DEC32 = 3  /* an HSG_F64 column sent as int32 decimal mantissas m:
+  HSG_ENC_DEC32 = 3, /* an HSG_F64 column sent as int32 decimal mantissas m:
                         value = m / 10^col_scale, the double nearest that decimal,
                         i.e. the double the JSON text of the decimal parses to       */
+  HSG_ENC_K16   = 4  /* key_id only: uint16 ids (a dictionary of <= 65536 keys, and
+                        no HSG_KEY_NONE record in the batch)                        */
 };
 
 typedef struct hsg_engine hsg_engine;
@@ -180,7 +182,7 @@ typedef struct {
                                    batches); NULL = inputs already complete              */
   /* narrow transport (all zero = the full-width arrays above) */
   int32_t ts_enc;               /* HSG_ENC_FULL, or HSG_ENC_TS32: `ts` points at int32_t[n]  */
-  int32_t reserved;             /* 0                                                      */
+  int32_t key_enc;              /* HSG_ENC_FULL, or HSG_ENC_K16: `key_id` points at uint16_t[n] */
   int64_t ts_base;              /* HSG_ENC_TS32: ts of a record = ts_base + its offset     */
   uint8_t col_enc[8];           /* per value column: HSG_ENC_FULL, HSG_ENC_I32 (HSG_I64
                                    columns) or HSG_ENC_DEC32 (HSG_F64 columns)            */

@@ -12,7 +12,7 @@ import pytest
 
 import pyoracle
 from hstream_amd import abi
-from hstream_amd.columnar import OpSpec, narrow_columns
+from hstream_amd.columnar import OpSpec, narrow_columns, narrow_keys
 from util import gen_small, rows_equal
 
 pytestmark = pytest.mark.gpu
@@ -50,9 +50,10 @@ def _batches(seed, nb=3, n=40_000):
     return out
 
 
+@pytest.mark.parametrize("k16", [False, True], ids=["k32", "k16"])
 @pytest.mark.parametrize("mode", ["sync", "async", "device"])
 @pytest.mark.parametrize("name", sorted(SPECS))
-def test_narrow_equals_full_width(eng, name, mode):
+def test_narrow_equals_full_width(eng, name, mode, k16):
     import torch
     spec = SPECS[name]
     g, o = eng.op(spec), pyoracle.OracleOp(spec, faithful_sessions=False)
@@ -60,20 +61,25 @@ def test_narrow_equals_full_width(eng, name, mode):
     wm_o = -1
     wm_g = C.c_int64(-1)
     for bi, (key, ts, cols, valid) in enumerate(_batches(70 + len(name))):
+        if k16:  # HSG_ENC_K16 needs a batch without HSG_KEY_NONE records
+            key = np.where(key == np.uint32(abi.HSG_KEY_NONE), np.uint32(65535), key).astype(np.uint32)
+        kn = narrow_keys(key) if k16 else key
+        assert kn.dtype == (np.uint16 if k16 else np.uint32)
         t32, base, c32, enc, scale = narrow_columns(ts, cols, spec.col_types, [None, 3])
         assert base is not None and enc == [abi.HSG_ENC_I32, abi.HSG_ENC_DEC32], (base, enc)
         wm_o = o.push(key, ts, cols, valid, watermark=wm_o)
         kw = dict(ts_base=base, col_enc=enc, col_scale=scale)
         if mode == "sync":
-            wm_g.value = g.push(key, t32, c32, valid, watermark=wm_g.value, **kw)
+            wm_g.value = g.push(kn, t32, c32, valid, watermark=wm_g.value, **kw)
         elif mode == "async":
-            g.push_async(key, t32, c32, valid, watermark=wm_g, **kw)
+            g.push_async(kn, t32, c32, valid, watermark=wm_g, **kw)
             g.wait()
         else:
             d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
             dv = [d(v) for v in valid]
             torch.cuda.synchronize()
-            wm_g.value = g.push(d(key.view(np.int32)), d(t32), [d(c) for c in c32], dv, watermark=wm_g.value,
+            dk = d(kn.view(np.int16)) if k16 else d(kn.view(np.int32))
+            wm_g.value = g.push(dk, d(t32), [d(c) for c in c32], dv, watermark=wm_g.value,
                                 mem=abi.HSG_MEM_DEVICE, **kw)
         assert wm_g.value == wm_o, f"batch {bi}: watermark"
         rows_equal(g.drain(), o.drain(), f64, ordered=spec.emit_mode == abi.HSG_EMIT_PER_RECORD,
