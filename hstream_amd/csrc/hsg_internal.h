@@ -99,7 +99,8 @@ struct DevScalars {
   uint64_t scratch[45];  // [0] groups flushed (partition path), [1] touched-list length, [8..20] phase clocks,
                          // [21..22] optimistic pass ts extrema, [31] lean partials of the batch (bound on
                          // its new groups), [32] held back for table room: bit 0 lean apply, bit 1 general,
-                         // [33] groups claimed in the table's overflow rows (TwTable::ovf)
+                         // bit 2 k_seg_apply, [33] groups claimed in the table's overflow rows (TwTable::ovf),
+                         // [34] k_seg_apply's deferred window updates (bound on their new groups)
   uint64_t live_x[8];    // more rows found, one shard per XCD (blockIdx & 7) for kernels whose every
                          // workgroup adds; the host folds them into `live` when it fetches the scalars
 };
@@ -265,6 +266,12 @@ struct WidenArgs {
   double div[kMaxCols];          // HSG_ENC_DEC32: 10^scale; 0: HSG_ENC_I32
 };
 void launch_widen(hipStream_t s, const WidenArgs &w);
+// dump ordering on the device (op_device.cpp sort_dump_rows_device): the
+// window index of each row (ws / adv - k_epoch) and the identity permutation;
+// then one 4-/8-byte column gathered through a permutation
+void launch_dump_keys(hipStream_t s, const int64_t *ws, uint64_t n, int64_t adv, int64_t k_epoch, uint32_t *k, uint32_t *v);
+void launch_gather_u32(hipStream_t s, const uint32_t *src, const uint32_t *perm, uint64_t n, uint32_t *dst);
+void launch_gather_u64(hipStream_t s, const uint64_t *src, const uint32_t *perm, uint64_t n, uint64_t *dst);
 inline bool batch_narrow(const hsg_batch *b) {
   bool any = b->ts_enc != HSG_ENC_FULL || b->key_enc != HSG_ENC_FULL;
   for (int c = 0; c < b->n_cols && c < kMaxCols; ++c) any |= b->col_enc[c] != HSG_ENC_FULL;

@@ -124,6 +124,7 @@ struct OpDevice {
   bool pred_direct = false;     // launch prediction: the last batch's changelog came from the lean apply
   uint64_t lean_batches = 0, direct_batches = 0, replays = 0;  // hsg_stats
   uint64_t lean_pred = 0;  // new groups the next lean batch may make (2x the last one's partials), 0 = none
+  uint64_t defer_pred = 0; // hopping: new groups the next batch may make (2x the last one's deferred updates)
   // sessions
   SessTable ss = {};
   uint64_t *h_meta = nullptr;     // pinned mirror of ss.meta

@@ -514,7 +514,7 @@ __global__ __launch_bounds__(256) void k_pane_apply(Program rprog, TwParams p, P
 // ---------------------------------------------------------------------------
 constexpr int kSegClaimSet = 16384;  // claims per workgroup up to half of it (else workgroup-scope CAS)
 #ifndef HSG_SEG_NT
-#define HSG_SEG_NT 1024
+#define HSG_SEG_NT 512  // two workgroups per CU (their 64 KB claim sets); C3 +2 % over 1024 (profiles/r03)
 #endif
 constexpr int kSegNT = HSG_SEG_NT;  // threads per workgroup
 __device__ inline bool seg_claim_insert(uint32_t *cset, uint32_t slot) {
@@ -589,6 +589,17 @@ __global__ __launch_bounds__(kSegNT) void k_seg_apply(Program prog, TwParams p, 
     before += s_red[k];
     total += s_tot[k];
   }
+  // the deferred updates (an upper bound on the groups they make) may not fit
+  // the table at the load it is sized for: nothing is claimed here, the host
+  // grows the table and launches this kernel again on the same segments
+  // (k_part_agg's own updates are in; uniform: every workgroup sums the same)
+  if (total > pp.room) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      atomicOr((unsigned long long *)&sc->scratch[32], 4ull);
+      sc->scratch[34] = total;
+    }
+    return;
+  }
   bool has_last = false;
   for (int s = 0; s < ns; ++s) has_last |= pg.op(s) == S_LAST_SEQ;
   const bool direct = out.key != nullptr && pb.chunk_start[nb + 1] == 0 && sc->scratch[5] == 0 && !has_last;
@@ -597,6 +608,7 @@ __global__ __launch_bounds__(kSegNT) void k_seg_apply(Program prog, TwParams p, 
     sc->scratch[6] = direct ? 0 : t0 + total;
     if (direct) sc->scratch[3] = total;
     sc->scratch[2] = direct ? 3 : 4;
+    sc->scratch[34] = total;  // the host sizes the next batch's table room from it
   }
   const uint32_t bid = (uint32_t)p.batch_id;
   const int64_t k_epoch = sc->k_epoch;

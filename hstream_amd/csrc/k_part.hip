@@ -983,6 +983,7 @@ __global__ __launch_bounds__(256) void k_touch_count(const uint32_t *__restrict_
   __shared__ uint64_t sw[4];
   uint64_t n = sc->scratch[6] ? sc->scratch[6] : sc->scratch[1];  // after k_seg_apply: [6]
   if (n > cap) n = cap;
+  if (sc->scratch[32] & 4) n = 0;  // k_seg_apply held back: the chain runs again after it
   const uint64_t c0 = (uint64_t)blockIdx.x * kTouchChunk;
   uint64_t h = 0;
   if (c0 < n)
@@ -999,6 +1000,7 @@ __global__ __launch_bounds__(256) void k_touch_emit(TwTable t, Program prog, TwP
   __shared__ uint64_t swave[4];
   uint64_t n = sc->scratch[6] ? sc->scratch[6] : sc->scratch[1];  // after k_seg_apply: [6]
   if (n > cap) n = cap;
+  if (sc->scratch[32] & 4) return;  // uniform: k_seg_apply held back (k_touch_count)
   const uint64_t c0 = (uint64_t)blockIdx.x * kTouchChunk;
   if (c0 >= n) return;  // uniform
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

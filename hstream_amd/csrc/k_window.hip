@@ -205,6 +205,31 @@ __global__ __launch_bounds__(256) void k_widen(WidenArgs w) {
   }
 }
 
+__global__ __launch_bounds__(256) void k_dump_keys(const int64_t *ws, uint64_t n, int64_t adv, int64_t k_epoch,
+                                                  uint32_t *k, uint32_t *v) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    k[i] = adv > 0 ? (uint32_t)(ws[i] / adv - k_epoch) : 0u;
+    v[i] = (uint32_t)i;
+  }
+}
+__global__ __launch_bounds__(256) void k_gather_u32(const uint32_t *src, const uint32_t *perm, uint64_t n, uint32_t *dst) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[perm[i]];
+}
+__global__ __launch_bounds__(256) void k_gather_u64(const uint64_t *src, const uint32_t *perm, uint64_t n, uint64_t *dst) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[perm[i]];
+}
+void launch_dump_keys(hipStream_t s, const int64_t *ws, uint64_t n, int64_t adv, int64_t k_epoch, uint32_t *k, uint32_t *v) {
+  if (n) hipLaunchKernelGGL(k_dump_keys, dim3(grid_for(n, 256)), dim3(256), 0, s, ws, n, adv, k_epoch, k, v);
+}
+void launch_gather_u32(hipStream_t s, const uint32_t *src, const uint32_t *perm, uint64_t n, uint32_t *dst) {
+  if (n) hipLaunchKernelGGL(k_gather_u32, dim3(grid_for(n, 256)), dim3(256), 0, s, src, perm, n, dst);
+}
+void launch_gather_u64(hipStream_t s, const uint64_t *src, const uint32_t *perm, uint64_t n, uint64_t *dst) {
+  if (n) hipLaunchKernelGGL(k_gather_u64, dim3(grid_for(n, 256)), dim3(256), 0, s, src, perm, n, dst);
+}
+
 void launch_widen(hipStream_t s, const WidenArgs &w) {
   if (w.n) hipLaunchKernelGGL(k_widen, dim3(grid_for(w.n, 256)), dim3(256), 0, s, w);
 }

@@ -28,6 +28,14 @@ namespace hsg {
     }                                                                       \
   } while (0)
 
+// Hopping ops on the partition path: k_seg_apply checks its deferred window
+// updates against the table's room and holds back past it (op_device.cpp
+// resume_deferred), so the table follows the groups the batches make.
+static bool has_last(const Program &prog);
+static bool defer_room_checked(const OpDevice &d, const hsg_op_config &cfg, const Program &prog) {
+  return d.use_part && cfg.window_kind == HSG_HOPPING && cfg.emit_mode != HSG_EMIT_PER_RECORD && !has_last(prog);
+}
+
 static uint64_t next_pow2(uint64_t v) {
   uint64_t p = 1;
   while (p < v) p <<= 1;
@@ -655,6 +663,13 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
   // kernels exited without touching the state; emit: the chain runs on the
   // touched list the apply left).
   bool skipped_wide = false, skipped_emit = false;
+  // hopping ops: the general kernel defers its window updates to k_seg_apply,
+  // which checks them against the room (its partials bound the batch's new
+  // groups), so the table is sized from the last batch's deferred updates
+  // rather than one group per (record, window) (table_bound_hint)
+  const bool defer_sized = defer_room_checked(d, cfg, prog);
+  PartParams last_pp;
+  memset(&last_pp, 0, sizeof(last_pp));
   auto run = [&](bool optimistic) -> int {
     int rc = clear_batch_scalars(d, err);
     if (rc != HSG_OK) return rc;
@@ -684,7 +699,8 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       pp.defer = 1;
       const uint64_t lim = d.cap - d.cap / 4;
       pp.room = lim > d.h_sc->live ? lim - d.h_sc->live : 0;
-      pp.hold = kb.n * d.wpr > pp.room ? 1 : 0;
+      pp.hold = !defer_sized && kb.n * d.wpr > pp.room ? 1 : 0;
+      last_pp = pp;
       if (!rec_wm && !optimistic) launch_part_recwm(d.stream, kb, d.tile_prefix, d.sc, d.part.wm);
       launch_part_hist(d.stream, kb, p, pp, rec_wm, d.part.wm, d.part, d.sc, optimistic);
       const bool can_pack = optimistic && cfg.n_cols <= 8 && d.wpr < 256;
@@ -719,6 +735,42 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     DTRY(hipGetLastError());
     return HSG_OK;
   };
+  // k_seg_apply held its deferred window updates back for table room after
+  // k_part_agg's own updates went in (the batch is half applied, so it is not
+  // run again): grow the table for the deferred updates, restore the batch's
+  // scalars (the fetch cleared them on the device) and launch k_seg_apply, and
+  // the changelog chain after it, again on the same segments
+  auto resume_deferred = [&]() -> int {
+    DevScalars keep;
+    memcpy(&keep, d.h_sc, sizeof(keep));
+    const uint64_t bound = keep.scratch[34];
+    int rc = tw_maintain(d, cfg, prog, kb.n, a.wm_in, a.pending, err, bound);
+    if (rc != HSG_OK) return rc;
+    keep.live = d.h_sc->live;  // the rebuilt table's rows, the batch's claims so far included
+    memset(keep.live_x, 0, sizeof(keep.live_x));
+    keep.scratch[32] = 0;
+    keep.scratch[33] = 0;  // (counted into ovf_rows by the fetch)
+    memcpy(d.h_sc, &keep, sizeof(keep));
+    DTRY(hipMemcpyAsync(d.sc, d.h_sc, sizeof(DevScalars), hipMemcpyHostToDevice, d.stream));
+    d.sc_clean = false;
+    PartParams pp = last_pp;
+    const uint64_t lim = d.cap - d.cap / 4;
+    pp.room = lim > keep.live ? lim - keep.live : 0;  // >= bound (tw_maintain)
+    const bool emit_batch = cfg.emit_mode == HSG_EMIT_PER_BATCH;
+    DTRY(hipEventRecord(d.ev_a, d.stream));
+    const dim3 g((unsigned)((1ull << pp.np_log2) + kb.n / pp.chunk + 1));
+    launch_seg_apply(d.stream, g, prog, p, pp, d.tw, d.part, d.sc, emit_batch ? &d.out : nullptr, a.pending, d.out_cap,
+                     false);
+    if (emit_batch && !skipped_emit) launch_part_emit(d.stream, d.tw, prog, p, d.part, d.out, a.pending, d.out_cap, d.sc);
+    DTRY(hipEventRecord(d.ev_b, d.stream));
+    DTRY(hipGetLastError());
+    rc = finish_batch(d, a.wm_in, kb.n, r, err);
+    if (rc == HSG_OK && d.h_sc->scratch[32]) {
+      err = "deferred updates held back after the table grew for them (internal)";
+      return HSG_E_DEVICE;
+    }
+    return rc;
+  };
   // a run whose claiming kernels held back for table room: grow the table for
   // the bound they saw (the lean partials, else the worst case), run again
   auto run_room = [&](bool optimistic) -> int {
@@ -727,6 +779,7 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     rc = finish_batch(d, a.wm_in, kb.n, r, err);
     if (rc != HSG_OK || !kb.n || !d.h_sc->scratch[32]) return rc;
     d.replays += 1;
+    if (d.h_sc->scratch[32] & 4) return resume_deferred();
     const uint64_t bound = (d.h_sc->scratch[32] & 2) ? UINT64_MAX : d.h_sc->scratch[31];
     rc = tw_maintain(d, cfg, prog, kb.n, a.wm_in, a.pending, err, bound);
     if (rc != HSG_OK) return rc;
@@ -769,6 +822,9 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     // next batch's table room: twice this batch's new-group bound (its partials)
     const uint64_t parts = d.h_sc->scratch[31];
     d.lean_pred = (how == 1 || how == 2) ? (2 * parts > (1ull << 16) ? 2 * parts : (1ull << 16)) : 0;
+    // and for a deferred (hopping) batch: twice its deferred window updates
+    const uint64_t dfr = d.h_sc->scratch[34];
+    if (how == 3 || how == 4) d.defer_pred = 2 * dfr > (1ull << 16) ? 2 * dfr : (1ull << 16);
     d.lean_batches += how == 1 || how == 2;
     d.direct_batches += how == 1 || how == 3;
   }
@@ -803,6 +859,7 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
 // the table) rather than for one new group per (record, window); every other
 // path gets that worst case.
 static uint64_t table_bound_hint(const OpDevice &d, const hsg_op_config &cfg, const Program &prog) {
+  if (defer_room_checked(d, cfg, prog)) return d.defer_pred;  // (0 before the first batch: its own check grows)
   if (!d.use_part || has_last(prog) || cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.grace_ms < 0 ||
       cfg.window_kind == HSG_SESSION || cfg.n_cols > 8 || d.wpr >= 256)
     return UINT64_MAX;
@@ -889,6 +946,60 @@ int op_copy_rows(OpDevice &d, const OutCols &src, uint64_t from, uint64_t n, int
 // 238-241), independent of where the rows sit in the HBM table. Host-side
 // permutation of the caller's columns (views are read back rarely; the rows
 // of a device-memory dump make one round trip).
+// The same order on the device, for a device-memory dump of time windows
+// (views of large states: C3's 731M rows would take minutes on the host): the
+// rows' window index (32 bits relative to the epoch, HSG_E_RANGE keeps it
+// there) then the key, two stable LSD radix sorts of (u32, row) pairs, every
+// column gathered through the permutation. Rows of one (key, window) are one
+// row, so the order is the host sort's.
+static int sort_dump_rows_device(OpDevice &d, const hsg_op_config &cfg, const hsg_rows *out, uint64_t n, int n_aggs,
+                                 std::string &err) {
+  struct Tmp {
+    void *p = nullptr;
+    ~Tmp() {
+      if (p) hipFree(p);
+    }
+  } scratch, gat;
+  const uint64_t sb = sort_scratch_bytes(n);
+  DTRY(hipMalloc(&scratch.p, 4 * n * 4 + sb + 256));
+  DTRY(hipMalloc(&gat.p, n * 8));
+  uint32_t *k0 = (uint32_t *)scratch.p, *v0 = k0 + n, *k1 = v0 + n, *v1 = k1 + n;
+  void *ss = (void *)(((uintptr_t)(v1 + n) + 255) & ~(uintptr_t)255);
+  const int64_t adv = cfg.window_kind == HSG_UNWINDOWED ? 0
+                      : cfg.window_kind == HSG_HOPPING  ? cfg.advance_ms
+                                                        : cfg.size_ms;
+  launch_dump_keys(d.stream, out->win_start, n, adv, d.h_sc->k_epoch, k0, v0);
+  uint32_t *perm = v0;
+  if (adv > 0) {
+    const int w = radix_sort_pairs(d.stream, k0, v0, k1, v1, n, 32, ss);
+    perm = w ? v1 : v0;
+  }
+  // keys in window order, then a stable sort by key
+  uint32_t *kk = perm == v0 ? k1 : k0, *kv = perm == v0 ? v1 : v0;
+  launch_gather_u32(d.stream, out->key_id, perm, n, kk);
+  hipMemcpyAsync(kv, perm, n * 4, hipMemcpyDeviceToDevice, d.stream);
+  uint32_t *ok = perm == v0 ? k0 : k1, *ov = perm == v0 ? v0 : v1;  // (ok, ov) the free pair
+  const int w2 = radix_sort_pairs(d.stream, kk, kv, ok, ov, n, 32, ss);
+  const uint32_t *fin = w2 ? ov : kv;
+  // every column through the permutation (a column at a time through gat)
+  auto col = [&](void *c, int bytes) -> int {
+    if (!c) return HSG_OK;
+    if (bytes == 4) launch_gather_u32(d.stream, (const uint32_t *)c, fin, n, (uint32_t *)gat.p);
+    else launch_gather_u64(d.stream, (const uint64_t *)c, fin, n, (uint64_t *)gat.p);
+    DTRY(hipMemcpyAsync(c, gat.p, n * (uint64_t)bytes, hipMemcpyDeviceToDevice, d.stream));
+    return HSG_OK;
+  };
+  int rc = col(out->key_id, 4);
+  if (rc == HSG_OK) rc = col(out->win_start, 8);
+  if (rc == HSG_OK) rc = col(out->win_end, 8);
+  if (rc == HSG_OK) rc = col(out->src_index, 8);
+  for (int j = 0; rc == HSG_OK && j < n_aggs && out->aggs; ++j) rc = col(out->aggs[j], 8);
+  if (rc != HSG_OK) return rc;
+  DTRY(hipGetLastError());
+  DTRY(hipStreamSynchronize(d.stream));
+  return HSG_OK;
+}
+
 static int sort_dump_rows(OpDevice &d, const hsg_rows *out, uint64_t n, int n_aggs, std::string &err) {
   if (n < 2) return HSG_OK;
   const bool dev = out->mem == HSG_MEM_DEVICE;
@@ -989,7 +1100,12 @@ int op_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hs
     rc = tw_dump_spilled(d, cfg, prog, out, *n_out, &more, err);
     *n_out += more;
   }
-  if (rc == HSG_OK) rc = sort_dump_rows(d, out, *n_out, cfg.n_aggs, err);
+  if (rc == HSG_OK) {
+    const bool dev_sort = out->mem == HSG_MEM_DEVICE && cfg.window_kind != HSG_SESSION && *n_out >= (1ull << 20) &&
+                          *n_out < 0xFFFFFFFFull && out->key_id && out->win_start && out->win_end;
+    rc = dev_sort ? sort_dump_rows_device(d, cfg, out, *n_out, cfg.n_aggs, err)
+                  : sort_dump_rows(d, out, *n_out, cfg.n_aggs, err);
+  }
   return rc;
 }
 

@@ -145,6 +145,35 @@ def test_c2_full_conservation(eng):
     op.close()
 
 
+def test_c3_full_hopping(eng):
+    """C3 at full size (1B records, 1M keys, hopping 60 s / 5 s, COUNT(*) +
+    SUM): every record is at ts >= 60 s and none is late, so each lands in
+    exactly 12 windows (TimeWindowedStream.hs:105-117): COUNT(*) summed over
+    the state is 12 x the records, SUM 12 x the column sum, every (key, window)
+    has one row, and the table (sized by the groups the batches make, the
+    deferred updates' room check) stays at most 2^30 slots for the ~731M
+    groups."""
+    import torch
+    cfg = datagen.CONFIGS["C3"]
+    spec = cfg.spec(abi.HSG_EMIT_NONE)
+    op = eng.op(spec)
+    _, cnt, tot = _push_device(op, cfg, cfg.n, cfg.batch, sums=True)
+    st = op.stats()
+    live = st["state_rows"]
+    assert st["table_slots"] <= (1 << 30), st
+    cols, aggs = _device_state(op, spec, live)
+    assert int(cols["key"].numel()) == live
+    assert int(aggs[0].sum().item()) == 12 * cnt and cnt == cfg.n
+    assert int(aggs[1].sum().item()) == 12 * tot
+    ws = cols["ws"]
+    assert bool(((ws % cfg.advance_ms) == 0).all()) and bool((cols["we"] - ws == cfg.size_ms).all())
+    g = cols["key"].to(torch.int64) * (1 << 32) + (ws - datagen.TS0 + 3_600_000) // cfg.advance_ms
+    del cols, aggs
+    g, _ = torch.sort(g)
+    assert not bool((g[1:] == g[:-1]).any()), "a (key, window) with two rows"
+    op.close()
+
+
 def test_c4_full_sessions_disjoint(eng):
     """C4 at full size (500M records, 10M keys, gap 30 s): after every batch
     the sessions of one key are disjoint and more than the gap apart (the
