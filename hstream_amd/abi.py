@@ -64,6 +64,9 @@ HSG_ENC_I32 = 2
 HSG_ENC_DEC32 = 3
 HSG_ENC_K16 = 4
 
+# hsg_op_config.flags
+HSG_OPF_LITERAL_FORMS = 1
+
 
 class hsg_engine_config(C.Structure):
     _fields_ = [
@@ -94,6 +97,8 @@ class hsg_op_config(C.Structure):
         ("aggs", C.POINTER(hsg_agg)),
         ("state_capacity", C.c_uint64),
         ("out_capacity", C.c_uint64),
+        ("flags", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 
@@ -125,6 +130,7 @@ class hsg_rows(C.Structure):
         ("win_end", C.c_void_p),
         ("src_index", C.c_void_p),
         ("aggs", C.POINTER(C.c_void_p)),
+        ("form", C.c_void_p),
     ]
 
 
@@ -196,10 +202,14 @@ INGEST_SYMBOLS = [
     "hsg_keydict_size",
     "hsg_keydict_encode",
     "hsg_keydict_text",
+    "hsg_keydict_spelling_text",
     "hsg_decoder_create",
     "hsg_decoder_destroy",
     "hsg_decode_json",
+    "hsg_decode_json_spelled",
 ]
+
+HSG_SPELL_ALT = 0x80000000
 
 # hsg_decode_status
 HSG_DEC_OK = 0
@@ -217,6 +227,7 @@ class hsg_decoder_config(C.Structure):
         ("col_fields", C.POINTER(C.c_char_p)),
         ("col_types", C.POINTER(C.c_int32)),
         ("col_numeric", C.POINTER(C.c_uint8)),
+        ("literal_forms", C.c_int32),
     ]
 
 
@@ -227,6 +238,16 @@ class hsg_sink_config(C.Structure):
         ("key_field", C.c_char_p),
         ("aliases", C.POINTER(C.c_char_p)),
         ("agg_index", C.POINTER(C.c_int32)),
+    ]
+
+
+class hsg_sink_spellings(C.Structure):
+    _fields_ = [
+        ("spell", C.c_void_p),
+        ("n", C.c_uint64),
+        ("src_base", C.c_int64),
+        ("mem", C.c_int32),
+        ("reserved", C.c_int32),
     ]
 
 
@@ -245,7 +266,8 @@ class hsg_sink_records(C.Structure):
 
 
 # Every symbol include/hstream_sink.h declares.
-SINK_SYMBOLS = ["hsg_sink_create", "hsg_sink_destroy", "hsg_sink_encode", "hsg_sink_member_order", "hsg_format_number"]
+SINK_SYMBOLS = ["hsg_sink_create", "hsg_sink_destroy", "hsg_sink_encode", "hsg_sink_encode_spelled",
+                "hsg_sink_member_order", "hsg_format_number"]
 
 
 class hsg_join_config(C.Structure):

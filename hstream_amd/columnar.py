@@ -28,6 +28,11 @@ class OpSpec:
     aggs: Sequence[Tuple[int, int]] = ()  # (hsg_agg_kind, column)
     state_capacity: int = 0
     out_capacity: int = 0
+    flags: int = 0  # HSG_OPF_* (abi.HSG_OPF_LITERAL_FORMS)
+
+    @property
+    def literal_forms(self) -> bool:
+        return bool(self.flags & abi.HSG_OPF_LITERAL_FORMS)
 
     def agg_is_f64(self) -> List[bool]:
         out = []
@@ -54,6 +59,7 @@ class OpSpec:
             aggs=C.cast(agg_arr, C.POINTER(abi.hsg_agg)),
             state_capacity=self.state_capacity,
             out_capacity=self.out_capacity,
+            flags=self.flags,
         )
         return cfg, (col_arr, agg_arr)
 
@@ -174,6 +180,7 @@ class Rows:
     win_end: np.ndarray
     src_index: np.ndarray
     aggs: List[np.ndarray] = field(default_factory=list)
+    form: Optional[np.ndarray] = None  # literal forms (hsg_rows.form), ops with HSG_OPF_LITERAL_FORMS
 
     def __len__(self):
         return int(self.key_id.shape[0])
@@ -185,7 +192,8 @@ class Rows:
         else:
             order = np.lexsort((self.win_end, self.win_start, self.key_id))
         return Rows(self.key_id[order], self.win_start[order], self.win_end[order],
-                    self.src_index[order], [a[order] for a in self.aggs])
+                    self.src_index[order], [a[order] for a in self.aggs],
+                    self.form[order] if self.form is not None else None)
 
     def tuples(self):
         out = []
@@ -195,7 +203,7 @@ class Rows:
         return out
 
 
-def alloc_rows(n: int, agg_is_f64: Sequence[bool]):
+def alloc_rows(n: int, agg_is_f64: Sequence[bool], form: bool = False):
     n = int(n)
     arrs = Rows(
         key_id=np.zeros(n, dtype=np.uint32),
@@ -203,6 +211,7 @@ def alloc_rows(n: int, agg_is_f64: Sequence[bool]):
         win_end=np.zeros(n, dtype=np.int64),
         src_index=np.zeros(n, dtype=np.int64),
         aggs=[np.zeros(n, dtype=np.float64 if f else np.int64) for f in agg_is_f64],
+        form=np.zeros(n, dtype=np.uint32) if form else None,
     )
     agg_ptrs = (C.c_void_p * max(1, len(agg_is_f64)))(*[a.ctypes.data for a in arrs.aggs])
     rows = abi.hsg_rows(
@@ -214,13 +223,14 @@ def alloc_rows(n: int, agg_is_f64: Sequence[bool]):
         win_end=arrs.win_end.ctypes.data,
         src_index=arrs.src_index.ctypes.data,
         aggs=C.cast(agg_ptrs, C.POINTER(C.c_void_p)),
+        form=arrs.form.ctypes.data if form else None,
     )
     return rows, arrs, agg_ptrs
 
 
 def truncate(rows: Rows, n: int) -> Rows:
     return Rows(rows.key_id[:n], rows.win_start[:n], rows.win_end[:n], rows.src_index[:n],
-                [a[:n] for a in rows.aggs])
+                [a[:n] for a in rows.aggs], rows.form[:n] if rows.form is not None else None)
 
 
 class OpHandle:
@@ -232,6 +242,7 @@ class OpHandle:
         self._h = handle
         self.spec = spec
         self._f64 = spec.agg_is_f64()
+        self._forms = spec.literal_forms and prefix == "hsg"  # (the oracle keeps no forms)
 
     def _fn(self, name):
         return getattr(self._lib, f"{self._p}_{name}")
@@ -258,7 +269,7 @@ class OpHandle:
 
     def drain(self) -> Rows:
         n = self.pending()
-        rows, arrs, keep = alloc_rows(n, self._f64)
+        rows, arrs, keep = alloc_rows(n, self._f64, self._forms)
         got = C.c_uint64(0)
         self._check(self._fn("drain")(self._h, C.byref(rows), C.byref(got)), "drain")
         return truncate(arrs, got.value)
@@ -266,7 +277,7 @@ class OpHandle:
     def dump_state(self) -> Rows:
         n = C.c_uint64(0)
         self._check(self._fn("state_rows")(self._h, C.byref(n)), "state_rows")
-        rows, arrs, keep = alloc_rows(n.value, self._f64)
+        rows, arrs, keep = alloc_rows(n.value, self._f64, self._forms)
         got = C.c_uint64(0)
         self._check(self._fn("dump_state")(self._h, C.byref(rows), C.byref(got)), "dump_state")
         return truncate(arrs, got.value)

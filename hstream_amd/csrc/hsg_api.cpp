@@ -62,7 +62,7 @@ double now_ms() {
 namespace hsg {
 
 int build_program(const hsg_op_config &cfg, const std::vector<int32_t> &col_types, const std::vector<hsg_agg> &aggs,
-                  Program &prog, std::string &err) {
+                  Program &prog, std::string &err, bool forms) {
   memset(&prog, 0, sizeof(prog));
   auto find_slot = [&](int op, int col) -> int {
     for (int s = 0; s < prog.n_slots; ++s)
@@ -76,6 +76,18 @@ int build_program(const hsg_op_config &cfg, const std::vector<int32_t> &col_type
     prog.slot_op[prog.n_slots] = op;
     prog.slot_col[prog.n_slots] = col;
     return prog.n_slots++;
+  };
+  // LAST: the (record seq, value) slot pair of column c; -1 = no room
+  auto last_pair = [&](int c) -> int {
+    int s = find_slot(S_LAST_SEQ, c);
+    if (s < 0) {
+      if (prog.n_slots + 2 > kMaxSlots) return -1;
+      s = add_slot(S_LAST_SEQ, c);
+      prog.slot_op[prog.n_slots] = S_LAST_VAL;
+      prog.slot_col[prog.n_slots] = c;
+      prog.n_slots++;
+    }
+    return s;
   };
   if ((int)aggs.size() > kMaxAggs) return fail(err, HSG_E_INVALID, "too many aggregates (max 16)");
   for (size_t j = 0; j < aggs.size(); ++j) {
@@ -96,14 +108,8 @@ int build_program(const hsg_op_config &cfg, const std::vector<int32_t> &col_type
         break;
       case HSG_LAST: {
         // sessions: merges keep the existing session's value (k_session.hip)
-        int s = find_slot(S_LAST_SEQ, c);
-        if (s < 0) {
-          if (prog.n_slots + 2 > kMaxSlots) return fail(err, HSG_E_INVALID, "too many state slots");
-          s = add_slot(S_LAST_SEQ, c);
-          prog.slot_op[prog.n_slots] = S_LAST_VAL;
-          prog.slot_col[prog.n_slots] = c;
-          prog.n_slots++;
-        }
+        const int s = last_pair(c);
+        if (s < 0) return fail(err, HSG_E_INVALID, "too many state slots");
         a = s + 1;
         kind = isf ? O_F64 : O_I64;
         break;
@@ -114,6 +120,26 @@ int build_program(const hsg_op_config &cfg, const std::vector<int32_t> &col_type
     prog.out_kind[j] = kind;
     prog.out_a[j] = a;
     prog.out_b[j] = b;
+    // the literal form (hsg_internal.h FormKind; the user's column c is the
+    // internal column 3c here, followed by its decimal / integral shadows)
+    int fk = F_NONE, fa = 0, fb = 0;
+    if (forms) {
+      switch (g.kind) {
+        case HSG_SUM: fk = F_SUM, fa = add_slot(S_CNT, c + 1); break;
+        case HSG_MIN:
+          fk = F_MINMAX, fa = add_slot(isf ? S_MIN_F : S_MIN_I, c + 2), fb = add_slot(S_CNT, c);
+          break;
+        case HSG_MAX:
+          fk = F_MINMAX, fa = add_slot(isf ? S_MAX_F : S_MAX_I, c + 2), fb = add_slot(S_CNT, c);
+          break;
+        case HSG_LAST: fk = F_LAST, fa = last_pair(c + 1), fb = last_pair(c + 2); break;
+        default: break;
+      }
+      if (fa < 0 || fb < 0) return fail(err, HSG_E_INVALID, "too many state slots");
+    }
+    prog.form_kind[j] = fk;
+    prog.form_a[j] = fa;
+    prog.form_b[j] = fb;
   }
   prog.n_out = (int)aggs.size();
   return HSG_OK;
@@ -233,8 +259,9 @@ struct AsyncJob {
 struct hsg_op {
   hsg_engine *eng = nullptr;
   hsg_op_config cfg;
-  std::vector<int32_t> col_types;
+  std::vector<int32_t> col_types;  // the user's value columns
   std::vector<hsg_agg> aggs;
+  int32_t user_cols = 0;           // cfg.n_cols is the kernels' (internal) count: 3x with literal forms
   Program prog;
   OpDevice dev;  // every HBM buffer + stream + events (hsg_ops.h)
   // Sharded ops own a communicator split from the engine's at creation, so
@@ -266,7 +293,7 @@ static int push_sync(hsg_op *op, const hsg_batch *b, int64_t *inout_watermark, i
 // the op's completion thread). Failure only means the push stages itself.
 static void prestage_job(hsg_op *op, AsyncJob &job) {
   if (job.staged_set >= 0 || job.b.mem != HSG_MEM_HOST || job.b.n == 0) return;
-  if (job.b.n > op->eng->batch_cap || job.b.n_cols != op->cfg.n_cols || !job.b.key_id || !job.b.ts)
+  if (job.b.n > op->eng->batch_cap || job.b.n_cols != op->user_cols || !job.b.key_id || !job.b.ts)
     return;  // push_sync reports it
   hsg_batch b = job.b;
   b.cols = job.cols.empty() ? nullptr : job.cols.data();
@@ -368,8 +395,28 @@ extern "C" int hsg_op_create(hsg_engine *eng, const hsg_op_config *cfg, hsg_op *
     op->cfg.aggs = nullptr;
     if (op->cfg.window_kind == HSG_TUMBLING) op->cfg.advance_ms = op->cfg.size_ms;
     memset(&op->stats, 0, sizeof(op->stats));
-    rc = build_program(op->cfg, op->col_types, op->aggs, op->prog, eng->err);
+    // literal forms: every user column c is the internal columns 3c, 3c + 1,
+    // 3c + 2 (all values / decimal / integral literals, stage_batch derives
+    // their validity); the kernels see only the internal ones
+    const bool forms = (cfg->flags & HSG_OPF_LITERAL_FORMS) != 0;
+    std::vector<int32_t> itypes = op->col_types;
+    std::vector<hsg_agg> iaggs = op->aggs;
+    if (forms) {
+      if (3 * cfg->n_cols > kMaxCols) {
+        delete op;
+        eng->err = "HSG_OPF_LITERAL_FORMS takes at most 2 value columns";
+        return HSG_E_INVALID;
+      }
+      itypes.clear();
+      for (int c = 0; c < cfg->n_cols; ++c) itypes.insert(itypes.end(), 3, op->col_types[c]);
+      for (auto &g : iaggs) g.column *= 3;
+      op->cfg.n_cols = 3 * cfg->n_cols;
+    }
+    op->user_cols = cfg->n_cols;
+    rc = build_program(op->cfg, itypes, iaggs, op->prog, eng->err, forms);
     if (rc != HSG_OK) { delete op; return rc; }
+    op->dev.user_cols = cfg->n_cols;
+    op->dev.forms = forms;
     if (hipSetDevice(eng->device) != hipSuccess) { delete op; return HSG_E_DEVICE; }
     if (eng->comm) {
       // collective over the engine's ranks: every rank creates its sharded ops
@@ -468,7 +515,7 @@ extern "C" int hsg_op_reset(hsg_op *op) {
 
 static int validate_batch(hsg_op *op, const hsg_batch *b, const int64_t *inout_watermark) {
   if (!b || !inout_watermark) return fail(op->err, HSG_E_INVALID, "null batch or watermark");
-  if (b->n_cols != op->cfg.n_cols) return fail(op->err, HSG_E_INVALID, "batch n_cols != op n_cols");
+  if (b->n_cols != op->user_cols) return fail(op->err, HSG_E_INVALID, "batch n_cols != op n_cols");
   if (b->mem != HSG_MEM_HOST && b->mem != HSG_MEM_DEVICE) return fail(op->err, HSG_E_INVALID, "bad batch mem");
   if (b->n > op->eng->batch_cap) return fail(op->err, HSG_E_CAPACITY, "batch larger than the engine's batch_capacity");
   if (b->n && (!b->key_id || !b->ts)) return fail(op->err, HSG_E_INVALID, "null key_id / ts");
@@ -625,6 +672,7 @@ extern "C" int hsg_op_set_changelog(hsg_op *op, const hsg_rows *dst) {
       if (!dst->aggs[j]) return fail(op->err, HSG_E_INVALID, "set_changelog: every column is required");
       o.agg[j] = (int64_t *)dst->aggs[j];
     }
+    o.form = op->dev.forms ? dst->form : nullptr;  // (optional: rows then carry no forms)
     d.out = o;
     d.out_cap = dst->capacity;
     d.ext_out = true;
@@ -690,14 +738,19 @@ extern "C" int hsg_op_stats(const hsg_op *op, hsg_stats *out) {
 namespace hsg {
 // For the sink encoder (sink.cpp): the op's device and which changelog
 // aggregate columns hold f64 bits.
-int op_sink_info(const hsg_op *op, int *device, int *n_aggs, uint32_t *f64_mask) {
+int op_sink_info(const hsg_op *op, int *device, int *n_aggs, uint32_t *f64_mask, uint32_t *form_mask, int8_t *ident) {
   if (!op) return HSG_E_INVALID;
   *device = op->eng->device;
   *n_aggs = op->prog.n_out;
-  uint32_t m = 0;
-  for (int j = 0; j < op->prog.n_out; ++j)
+  uint32_t m = 0, fm = 0;
+  for (int j = 0; j < op->prog.n_out; ++j) {
     if (op->prog.out_kind[j] != O_I64) m |= 1u << j;
+    if (op->prog.form_kind[j] != F_NONE) fm |= 1u << j;
+    // the reference's initial values: MIN maxBound, MAX minBound, else 0 (Codegen.hs:425-469)
+    ident[j] = op->aggs[j].kind == HSG_MIN ? 1 : op->aggs[j].kind == HSG_MAX ? 2 : 0;
+  }
   *f64_mask = m;
+  *form_mask = fm;
   return HSG_OK;
 }
 }  // namespace hsg

@@ -195,6 +195,43 @@ __device__ inline int64_t out_value_reg(const Program &prog, int j, const int64_
   return out_value_w(prog, j, a, b);
 }
 
+// Literal forms of a row's outputs (hsg_rows.form; hsg_internal.h FormKind):
+// bit 2j = output j prints as an integer, bit 2j + 1 = it is the aggregate's
+// initial value. `own` = the output's own slot, fa / fb its form slots.
+__device__ inline uint32_t form_bits_w(int kind, int64_t own, int64_t fa, int64_t fb) {
+  switch (kind) {
+    case F_SUM: return fa == 0 ? 1u : 0u;
+    case F_MINMAX: return fb == 0 ? 3u : (fa == own ? 1u : 0u);
+    case F_LAST:
+      if (fa == 0 && fb == 0) return 3u;
+      return (uint64_t)fb > (uint64_t)fa ? 1u : 0u;
+    default: return 0u;
+  }
+}
+__device__ inline uint32_t out_form(const Program &prog, const int64_t *row) {
+  uint32_t f = 0;
+  for (int j = 0; j < prog.n_out; ++j)
+    if (prog.form_kind[j] != F_NONE)
+      f |= form_bits_w(prog.form_kind[j], row[prog.out_a[j]], row[prog.form_a[j]], row[prog.form_b[j]]) << (2 * j);
+  return f;
+}
+template <int MS>
+__device__ inline uint32_t out_form_reg(const Program &prog, const int64_t (&r)[MS]) {
+  uint32_t f = 0;
+  for (int j = 0; j < prog.n_out; ++j) {
+    if (prog.form_kind[j] == F_NONE) continue;
+    int64_t own = 0, fa = 0, fb = 0;
+#pragma unroll
+    for (int s = 0; s < MS; ++s) {
+      if (s == prog.out_a[j]) own = r[s];
+      if (s == prog.form_a[j]) fa = r[s];
+      if (s == prog.form_b[j]) fb = r[s];
+    }
+    f |= form_bits_w(prog.form_kind[j], own, fa, fb) << (2 * j);
+  }
+  return f;
+}
+
 // Per-record stream time for the records of one tile (record (r, thread) =
 // tile_base + r*kTileThreads + thread), inclusive prefix max in arrival order
 // seeded with the tile's exclusive prefix. Block-wide: every thread must call.

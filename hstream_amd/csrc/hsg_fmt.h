@@ -30,6 +30,8 @@ struct Pow5Tables {
 
 // longest text of one number (sign + 20 digits, or d.ddddddddddddddddde-324)
 constexpr int kNumTextMax = 32;
+// an integral f64 printed as an integer (literal forms): up to 309 digits
+constexpr int kNumTextIntMax = 328;
 
 HSG_HD int fmt_u64_digits(uint64_t v, char *out) {
   char t[20];
@@ -200,8 +202,10 @@ HSG_HD void ryu_d2d(uint64_t ieee_m, uint32_t ieee_e, const Pow5Tables &T, uint6
   e10_out = e10 + removed;
 }
 
-// f64 -> aeson text; returns the length (<= kNumTextMax)
-HSG_HD int fmt_f64(double v, const Pow5Tables &T, char *out) {
+// f64 -> aeson text; returns the length (<= kNumTextMax). ident: map the
+// aggregate identities to the reference's integer initial values (rows
+// without literal forms; with them the sink knows which rows are identities)
+HSG_HD int fmt_f64(double v, const Pow5Tables &T, char *out, bool ident = true) {
   uint64_t bits;
   memcpy(&bits, &v, 8);
   const bool neg = (bits >> 63) != 0;
@@ -216,12 +220,12 @@ HSG_HD int fmt_f64(double v, const Pow5Tables &T, char *out) {
   // plainly. Here a SUM no value reached keeps its identity -0.0
   // (slot_identity), a MIN / MAX the f64 image of maxBound (2^63, rounded) /
   // minBound (-2^63).
-  if (bits == 0x8000000000000000ull) {
+  if (ident && bits == 0x8000000000000000ull) {
     out[0] = '0';
     return 1;
   }
-  if (v == 9223372036854775808.0) return fmt_i64(INT64_MAX, out);
-  if (v == -9223372036854775808.0) return fmt_i64(INT64_MIN, out);
+  if (ident && v == 9223372036854775808.0) return fmt_i64(INT64_MAX, out);
+  if (ident && v == -9223372036854775808.0) return fmt_i64(INT64_MIN, out);
   if (ie == 0 && im == 0) return fmt_generic(false, nullptr, 0, 0, out);
   uint64_t m;
   int32_t e;
@@ -233,6 +237,40 @@ HSG_HD int fmt_f64(double v, const Pow5Tables &T, char *out) {
   char d[20];
   const int nd = fmt_u64_digits(m, d);
   return fmt_generic(neg, d, nd, e, out);
+}
+
+// An int64 whose Scientific has a negative exponent (a sum of decimal
+// literals that came out integral, "6.0"): Scientific's Generic form.
+HSG_HD int fmt_i64_decimal(int64_t v, char *out) {
+  if (v == 0) return fmt_generic(false, nullptr, 0, 0, out);
+  uint64_t m = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+  int e = 0;
+  while (m % 10 == 0) {
+    m /= 10;
+    ++e;
+  }
+  char d[20];
+  const int nd = fmt_u64_digits(m, d);
+  return fmt_generic(v < 0, d, nd, e, out);
+}
+
+// An integral f64 whose Scientific has an exponent >= 0 (a sum of integer
+// literals, "6"): the integer; below 2^63 exactly, above it the shortest
+// round-trip digits followed by zeros (the f64 holds no more). <= kNumTextIntMax.
+HSG_HD int fmt_f64_integral(double v, const Pow5Tables &T, char *out) {
+  if (v > -9223372036854775808.0 && v < 9223372036854775808.0) return fmt_i64((int64_t)v, out);
+  uint64_t bits;
+  memcpy(&bits, &v, 8);
+  const uint32_t ie = (uint32_t)((bits >> 52) & 0x7FF);
+  if (ie == 0x7FF) return fmt_f64(v, T, out, false);
+  uint64_t m;
+  int32_t e;
+  ryu_d2d(bits & ((1ull << 52) - 1), ie, T, m, e);
+  int k = 0;
+  if (bits >> 63) out[k++] = '-';
+  k += fmt_u64_digits(m, out + k);
+  for (int32_t q = 0; q < e && k < kNumTextIntMax; ++q) out[k++] = '0';
+  return k;
 }
 
 #undef HSG_HD

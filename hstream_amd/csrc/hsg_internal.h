@@ -37,6 +37,17 @@ enum OutKind : int32_t {
   O_AVG_F = 4,    // slot a (f64 sum) / slot b (count)
 };
 
+// How output j's literal form is read (HSG_OPF_LITERAL_FORMS): from slots
+// over the internal columns 3c (every value), 3c + 1 (values with a decimal
+// literal), 3c + 2 (values with an integral literal) of user column c.
+enum FormKind : int32_t {
+  F_NONE = 0,    // no form bits (COUNT, COUNT(col), AVG; ops without the flag)
+  F_SUM = 1,     // a = COUNT over 3c + 1: integral iff 0 (a Scientific sum takes the smaller exponent)
+  F_MINMAX = 2,  // a = MIN / MAX over 3c + 2, b = COUNT over 3c: identity iff b = 0, else
+                 //     integral iff a equals the output's own slot (an integral literal won)
+  F_LAST = 3,    // a / b = LAST_SEQ over 3c + 1 / 3c + 2: identity iff both 0, else integral iff b > a
+};
+
 struct Program {
   int32_t n_slots;
   int32_t n_out;
@@ -45,6 +56,9 @@ struct Program {
   int32_t out_kind[kMaxAggs];
   int32_t out_a[kMaxAggs];
   int32_t out_b[kMaxAggs];
+  int32_t form_kind[kMaxAggs];  // FormKind
+  int32_t form_a[kMaxAggs];
+  int32_t form_b[kMaxAggs];
 };
 
 // u64 division by an invariant divisor (Granlund–Montgomery), exact for all n.
@@ -117,6 +131,7 @@ struct OutCols {
   int64_t *we;
   int64_t *src;
   int64_t *agg[kMaxAggs];  // 8-byte words (i64 or f64 bits)
+  uint32_t *form;          // literal forms (hsg_rows.form), null = not kept
 };
 
 struct Batch {
@@ -239,7 +254,7 @@ struct RowPtrs {
 };
 void launch_clear_scalars(hipStream_t s, DevScalars *sc);
 void launch_copy_rows(hipStream_t s, const OutCols &src, uint64_t from, uint64_t n, int n_aggs, uint32_t *key,
-                      int64_t *ws, int64_t *we, int64_t *si, const RowPtrs &aggs);
+                      int64_t *ws, int64_t *we, int64_t *si, const RowPtrs &aggs, uint32_t *form = nullptr);
 void launch_fill_u64(hipStream_t s, uint64_t *p, uint64_t n, uint64_t v);
 void launch_fill_rows(hipStream_t s, int64_t *aggs, uint64_t rows, const Program &prog);
 // every row of a time-window table: key EMPTY, stamp 0, aggregate identities
@@ -266,6 +281,16 @@ struct WidenArgs {
   double div[kMaxCols];          // HSG_ENC_DEC32: 10^scale; 0: HSG_ENC_I32
 };
 void launch_widen(hipStream_t s, const WidenArgs &w);
+// literal forms (HSG_OPF_LITERAL_FORMS): validity of the internal columns
+// 3c / 3c + 1 / 3c + 2 from user column c's valid bytes (bit 0 present, bit 1
+// decimal literal; null = every value present with an integral literal)
+struct FormArgs {
+  uint64_t n;
+  int32_t ncols;                 // user columns (<= kMaxCols / 3)
+  const uint8_t *valid[kMaxCols];
+  uint8_t *out[kMaxCols];
+};
+void launch_forms(hipStream_t s, const FormArgs &f);
 // dump ordering on the device (op_device.cpp sort_dump_rows_device): the
 // window index of each row (ws / adv - k_epoch) and the identity permutation;
 // then one 4-/8-byte column gathered through a permutation

@@ -24,6 +24,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <unordered_map>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -281,7 +282,11 @@ bool skip_value(Cur &c, int depth) {
 // ---------------------------------------------------------------------------
 void put_u32(std::string &o, uint32_t v) { o.append((const char *)&v, 4); }
 
-bool canon_value(Cur &c, std::string &o, Dec &tmp, int depth = 0);
+// form: when given, one char per number of the value in canonical order --
+// 'i' if aeson prints it as an integer (its literal's exponent in [0, 1024]),
+// 'd' if in Scientific's Generic form (aeson_number below). Equal values print
+// alike iff their forms are equal: the form picks the spelling of a key.
+bool canon_value(Cur &c, std::string &o, Dec &tmp, int depth = 0, std::string *form = nullptr);
 
 bool canon_string(Cur &c, std::string &o) {
   const char *s;
@@ -322,7 +327,7 @@ void canon_number(const Dec &x, std::string &o) {
   o.push_back(';');
 }
 
-bool canon_value(Cur &c, std::string &o, Dec &tmp, int depth) {
+bool canon_value(Cur &c, std::string &o, Dec &tmp, int depth, std::string *form) {
   if (depth > 512) return false;
   c.ws();
   if (c.p >= c.e) return false;
@@ -334,7 +339,7 @@ bool canon_value(Cur &c, std::string &o, Dec &tmp, int depth) {
     c.ws();
     if (!c.eat(']')) {
       for (;;) {
-        if (!canon_value(c, o, tmp, depth + 1)) return false;
+        if (!canon_value(c, o, tmp, depth + 1, form)) return false;
         c.ws();
         if (c.eat(']')) break;
         if (!c.eat(',')) return false;
@@ -345,16 +350,19 @@ bool canon_value(Cur &c, std::string &o, Dec &tmp, int depth) {
   }
   if (ch == '{') {
     ++c.p;
-    std::vector<std::pair<std::string, std::string>> mem;
+    struct Mem {
+      std::string key, val, form;
+    };
+    std::vector<Mem> mem;
     c.ws();
     if (!c.eat('}')) {
       for (;;) {
         c.ws();
-        std::pair<std::string, std::string> m;
-        if (!canon_string(c, m.first)) return false;
+        Mem m;
+        if (!canon_string(c, m.key)) return false;
         c.ws();
         if (!c.eat(':')) return false;
-        if (!canon_value(c, m.second, tmp, depth + 1)) return false;
+        if (!canon_value(c, m.val, tmp, depth + 1, form ? &m.form : nullptr)) return false;
         mem.push_back(std::move(m));
         c.ws();
         if (c.eat('}')) break;
@@ -362,12 +370,13 @@ bool canon_value(Cur &c, std::string &o, Dec &tmp, int depth) {
       }
     }
     // a map: sorted by key; a repeated key keeps its last value
-    std::stable_sort(mem.begin(), mem.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    std::stable_sort(mem.begin(), mem.end(), [](const Mem &a, const Mem &b) { return a.key < b.key; });
     o.push_back('{');
     for (size_t i = 0; i < mem.size(); ++i) {
-      if (i + 1 < mem.size() && mem[i + 1].first == mem[i].first) continue;
-      o.append(mem[i].first);
-      o.append(mem[i].second);
+      if (i + 1 < mem.size() && mem[i + 1].key == mem[i].key) continue;
+      o.append(mem[i].key);
+      o.append(mem[i].val);
+      if (form) form->append(mem[i].form);
     }
     o.push_back('}');
     return true;
@@ -382,6 +391,7 @@ bool canon_value(Cur &c, std::string &o, Dec &tmp, int depth) {
   if (!parse_number(c, n)) return false;
   normalise(n, tmp);
   canon_number(tmp, o);
+  if (form) form->push_back(tmp.spelled_exp >= 0 && tmp.spelled_exp <= 1024 ? 'i' : 'd');
   return true;
 }
 
@@ -566,6 +576,36 @@ struct hsg_keydict {
   std::vector<uint64_t> coff{0};
   std::string text;           // Aeson text of the first spelling, id after id
   std::vector<uint64_t> toff{0};
+  std::string form;           // canon_value form of the first spelling, id after id
+  std::vector<uint64_t> foff{0};
+  // alternate spellings: (key id, form) of a key printed unlike its first
+  // spelling (1 vs 1.0), their Aeson text by alternate index
+  std::unordered_map<std::string, uint32_t> alt_ix;
+  std::string alt_text;
+  std::vector<uint64_t> alt_off{0};
+
+  // the spelling of a record whose key has id `id` and form `f` (raw JSON of
+  // the key for a new alternate's text): id, or HSG_SPELL_ALT | alternate
+  int spelling(uint32_t id, const char *f, size_t fn, const char *raw, size_t rn, uint32_t *spell) {
+    const uint64_t a = foff[id], b = foff[id + 1];
+    if (b - a == fn && (!fn || !memcmp(form.data() + a, f, fn))) {
+      *spell = id;
+      return HSG_OK;
+    }
+    std::string k((const char *)&id, 4);
+    k.append(f, fn);
+    auto it = alt_ix.find(k);
+    if (it == alt_ix.end()) {
+      if (alt_ix.size() >= (size_t)HSG_SPELL_ALT) return HSG_E_CAPACITY;
+      const uint32_t ix = (uint32_t)alt_ix.size();
+      Cur cur{raw, raw + rn};
+      if (!aeson_value(cur, alt_text)) alt_text.append("null");
+      alt_off.push_back(alt_text.size());
+      it = alt_ix.emplace(std::move(k), ix).first;
+    }
+    *spell = HSG_SPELL_ALT | it->second;
+    return HSG_OK;
+  }
 
   uint64_t size() const { return coff.size() - 1; }
 
@@ -602,7 +642,9 @@ struct hsg_keydict {
   }
 
   // insert a new key: canonical bytes + the raw JSON of its first spelling
-  int insert(const char *c, size_t n, uint64_t h, const char *raw, size_t rn, uint32_t *id) {
+  // (and that spelling's form)
+  int insert(const char *c, size_t n, uint64_t h, const char *raw, size_t rn, uint32_t *id, const char *f = nullptr,
+             size_t fn = 0) {
     if (size() >= (uint64_t)HSG_KEY_NONE) return HSG_E_CAPACITY;
     if (2 * (size() + 1) > th.size()) rehash(th.empty() ? 1024 : 2 * th.size());
     uint64_t q = 0;
@@ -615,6 +657,14 @@ struct hsg_keydict {
     Cur cur{raw, raw + rn};
     if (!aeson_value(cur, text)) text.append("null");
     toff.push_back(text.size());
+    if (fn) form.append(f, fn);
+    else if (!f) {  // (hsg_keydict_encode: the form from the raw text)
+      std::string cb, ff;
+      Dec tmp;
+      Cur c2{raw, raw + rn};
+      if (canon_value(c2, cb, tmp, 0, &ff)) form.append(ff);
+    }
+    foff.push_back(form.size());
     *id = nid;
     return HSG_OK;
   }
@@ -625,6 +675,7 @@ struct hsg_keydict {
 // ---------------------------------------------------------------------------
 struct hsg_decoder {
   std::string key_field;
+  bool literal_forms = false;  // valid bit 1: the number's literal has a negative exponent
   struct Col {
     std::string field;
     int32_t type;
@@ -638,6 +689,8 @@ namespace {
 struct Chunk {
   std::string arena;              // canonical key bytes of the chunk's records
   std::vector<uint64_t> koff;     // per record: start in arena (len via next)
+  std::string forms;              // per record: the key's form (canon_value), when spellings are asked
+  std::vector<uint64_t> fof;      // per record: start in forms (len via next)
   std::vector<uint64_t> khash;
   std::vector<const char *> raw;  // per record: the key's raw JSON span
   std::vector<uint32_t> rawn;
@@ -652,7 +705,7 @@ bool name_is(const char *s, size_t n, bool esc, const std::string &want, std::st
 
 // One record: fills its columns and the chunk's key entry; returns its status.
 int decode_one(const hsg_decoder &dec, const char *s, size_t n, uint64_t i, void *const *cols,
-               uint8_t *const *valid, Chunk &ch, Dec &dtmp, std::string &tmp) {
+               uint8_t *const *valid, Chunk &ch, Dec &dtmp, std::string &tmp, bool spell) {
   const int C = (int)dec.cols.size();
   for (int c = 0; c < C; ++c) {
     if (valid && valid[c]) valid[c][i] = 0;
@@ -662,6 +715,8 @@ int decode_one(const hsg_decoder &dec, const char *s, size_t n, uint64_t i, void
   ch.raw.push_back(nullptr);
   ch.rawn.push_back(0);
   ch.koff.push_back(ch.arena.size());
+  if (spell) ch.fof.push_back(ch.forms.size());
+  const size_t form_at = ch.forms.size();
   Cur cur{s, s + n};
   cur.ws();
   if (!cur.eat('{')) return HSG_DEC_NOT_OBJECT;
@@ -686,8 +741,9 @@ int decode_one(const hsg_decoder &dec, const char *s, size_t n, uint64_t i, void
       if (name_is(ks, kn, kesc, dec.key_field, tmp)) {
         // the last occurrence wins (Aeson objects are maps)
         ch.arena.resize(key_at);
+        if (spell) ch.forms.resize(form_at);
         const char *r0 = cur.p;
-        if (!canon_value(cur, ch.arena, dtmp)) return HSG_DEC_NOT_OBJECT;
+        if (!canon_value(cur, ch.arena, dtmp, 0, spell ? &ch.forms : nullptr)) return HSG_DEC_NOT_OBJECT;
         ch.raw.back() = r0;
         ch.rawn.back() = (uint32_t)(cur.p - r0);
         have_key = true;
@@ -786,7 +842,10 @@ int decode_one(const hsg_decoder &dec, const char *s, size_t n, uint64_t i, void
         ((int64_t *)cols[c])[i] = dtmp.neg ? (int64_t)(0 - (uint64_t)v) : (int64_t)(uint64_t)v;
       }
     }
-    valid[c][i] = 1;
+    // literal forms: aeson prints this Scientific as an integer iff its
+    // exponent (the literal's, e.g. 25e-1 -> -1) is in [0, 1024]
+    const int64_t se = cnum[c].exp - (int64_t)(cnum[c].fe - cnum[c].fp);
+    valid[c][i] = (uint8_t)(1u | ((dec.literal_forms && (se < 0 || se > 1024)) ? 2u : 0u));
   }
   if (status != HSG_DEC_OK) return status;
   ch.khash.back() = hash_bytes(ch.arena.data() + key_at, ch.arena.size() - key_at);
@@ -841,6 +900,7 @@ extern "C" int hsg_decoder_create(const hsg_decoder_config *cfg, hsg_decoder **o
   try {
     hsg_decoder *d = new hsg_decoder();
     d->key_field = cfg->key_field;
+    d->literal_forms = cfg->literal_forms != 0;
     for (int c = 0; c < cfg->n_cols; ++c) {
       if (!cfg->col_fields[c] || (cfg->col_types[c] != HSG_I64 && cfg->col_types[c] != HSG_F64)) {
         delete d;
@@ -857,9 +917,10 @@ extern "C" int hsg_decoder_create(const hsg_decoder_config *cfg, hsg_decoder **o
 
 extern "C" void hsg_decoder_destroy(hsg_decoder *d) { delete d; }
 
-extern "C" int hsg_decode_json(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, const char *buf, const uint64_t *off,
-                               const int64_t *rec_ts, uint32_t *key_id, int64_t *ts, void *const *cols,
-                               uint8_t *const *valid, uint8_t *status, uint64_t *rejected, int n_threads) {
+extern "C" int hsg_decode_json_spelled(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, const char *buf,
+                                       const uint64_t *off, const int64_t *rec_ts, uint32_t *key_id, int64_t *ts,
+                                       void *const *cols, uint8_t *const *valid, uint8_t *status, uint64_t *rejected,
+                                       uint32_t *spell, int n_threads) {
   if (!dec || !dict || (n && (!buf || !off || !key_id))) return HSG_E_INVALID;
   const int C = (int)dec->cols.size();
   if (C && (!cols || !valid)) return HSG_E_INVALID;
@@ -880,6 +941,7 @@ extern "C" int hsg_decode_json(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, 
       const uint64_t lo = n * (uint64_t)t / (uint64_t)T, hi = n * (uint64_t)(t + 1) / (uint64_t)T;
       Chunk &ch = chunks[(size_t)t];
       ch.koff.reserve(hi - lo + 1);
+      if (spell) ch.fof.reserve(hi - lo + 1);
       ch.khash.reserve(hi - lo);
       ch.raw.reserve(hi - lo);
       ch.rawn.reserve(hi - lo);
@@ -887,9 +949,11 @@ extern "C" int hsg_decode_json(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, 
       std::string tmp;
       for (uint64_t i = lo; i < hi; ++i) {
         if (ts) ts[i] = rec_ts ? rec_ts[i] : 0;
-        st[i] = (uint8_t)decode_one(*dec, buf + off[i], (size_t)(off[i + 1] - off[i]), i, cols, valid, ch, dtmp, tmp);
+        st[i] = (uint8_t)decode_one(*dec, buf + off[i], (size_t)(off[i + 1] - off[i]), i, cols, valid, ch, dtmp, tmp,
+                                    spell != nullptr);
       }
       ch.koff.push_back(ch.arena.size());
+      if (spell) ch.fof.push_back(ch.forms.size());
     };
     if (T == 1) {
       work(0);
@@ -908,20 +972,27 @@ extern "C" int hsg_decode_json(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, 
         const uint64_t j = i - lo;
         if (st[i] != HSG_DEC_OK) {
           key_id[i] = HSG_KEY_NONE;
+          if (spell) spell[i] = HSG_KEY_NONE;
           for (int c = 0; c < C; ++c) valid[c][i] = 0;
           ++rej;
           continue;
         }
         const char *cb = ch.arena.data() + ch.koff[j];
         const size_t cn = (size_t)(ch.koff[j + 1] - ch.koff[j]);
+        const char *fb = spell ? ch.forms.data() + ch.fof[j] : nullptr;
+        const size_t fnb = spell ? (size_t)(ch.fof[j + 1] - ch.fof[j]) : 0;
         int64_t f = dict->find(cb, cn, ch.khash[j], nullptr);
         if (f < 0) {
           uint32_t id;
-          const int rc = dict->insert(cb, cn, ch.khash[j], ch.raw[j], ch.rawn[j], &id);
+          const int rc = dict->insert(cb, cn, ch.khash[j], ch.raw[j], ch.rawn[j], &id, spell ? fb : nullptr, fnb);
           if (rc != HSG_OK) return rc;
           f = id;
         }
         key_id[i] = (uint32_t)f;
+        if (spell) {
+          const int rc = dict->spelling((uint32_t)f, fb, fnb, ch.raw[j], ch.rawn[j], &spell[i]);
+          if (rc != HSG_OK) return rc;
+        }
       }
     }
     if (rejected) *rejected = rej;
@@ -933,7 +1004,32 @@ extern "C" int hsg_decode_json(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, 
   }
 }
 
+extern "C" int hsg_decode_json(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, const char *buf, const uint64_t *off,
+                               const int64_t *rec_ts, uint32_t *key_id, int64_t *ts, void *const *cols,
+                               uint8_t *const *valid, uint8_t *status, uint64_t *rejected, int n_threads) {
+  return hsg_decode_json_spelled(dec, dict, n, buf, off, rec_ts, key_id, ts, cols, valid, status, rejected, nullptr,
+                                 n_threads);
+}
+
+extern "C" int hsg_keydict_spelling_text(const hsg_keydict *d, uint32_t spell, char *buf, size_t cap, size_t *len) {
+  if (!d || !len) return HSG_E_INVALID;
+  if (!(spell & HSG_SPELL_ALT)) return hsg_keydict_text(d, spell, buf, cap, len);
+  const uint32_t ix = spell & ~HSG_SPELL_ALT;
+  if (ix + 1 >= d->alt_off.size()) return HSG_E_INVALID;
+  const uint64_t a = d->alt_off[ix], b = d->alt_off[ix + 1];
+  *len = (size_t)(b - a);
+  if (cap < *len || (!buf && *len)) return HSG_E_CAPACITY;
+  if (*len) memcpy(buf, d->alt_text.data() + a, *len);
+  return HSG_OK;
+}
+
 namespace hsg {
+// For the sink encoder (sink.cpp): the alternate spellings' texts, index after index.
+void keydict_alt_texts(const hsg_keydict *d, const char **text, const uint64_t **off, uint64_t *n) {
+  *text = d->alt_text.data();
+  *off = d->alt_off.data();
+  *n = d->alt_off.size() - 1;
+}
 // For the sink encoder (sink.cpp): the key texts, id after id.
 void keydict_texts(const hsg_keydict *d, const char **text, const uint64_t **off, uint64_t *n) {
   *text = d->text.data();

@@ -437,6 +437,7 @@ __global__ __launch_bounds__(256) void k_pane_apply(Program rprog, TwParams p, P
             out.we[o] = we;
             out.src[o] = -1;
             for (int j = 0; j < rprog.n_out; ++j) out.agg[j][o] = out_value_reg<NS>(rprog, j, v);
+            if (out.form) out.form[o] = out_form_reg<NS>(rprog, v);
           } else {
             err |= ERR_OOM;
           }
@@ -722,6 +723,7 @@ __global__ __launch_bounds__(kSegNT) void k_seg_apply(Program prog, TwParams p, 
 #pragma unroll
               for (int j = 0; j < kMaxAggs; ++j)
                 if (j < prog.n_out) out.agg[j][o] = out_value_reg<MS>(prog, j, v[u]);
+              if (out.form) out.form[o] = out_form_reg<MS>(prog, v[u]);
             } else {
               err |= ERR_OOM;
             }

@@ -1038,6 +1038,7 @@ __global__ __launch_bounds__(256) void k_touch_emit(TwTable t, Program prog, TwP
     out.we[o] = we;
     out.src[o] = -1;
     for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, row);
+    if (out.form) out.form[o] = out_form(prog, row);
   }
 }
 

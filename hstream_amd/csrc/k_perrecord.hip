@@ -325,6 +325,7 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_apply(Batch b, Program prog
     out.we[o] = we;
     out.src[o] = seq ? seq[rec] : (int64_t)(p.rec_base + rec);
     for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value_reg<MS>(prog, j, R);
+    if (out.form) out.form[o] = out_form_reg<MS>(prog, R);
     // segment end: final state into the shadow table
     if (q + 1 == P || slot[q + 1] != sl) {
       segs += 1;

@@ -593,6 +593,7 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit(Batch bt, Program pr
 #pragma unroll
       for (int jj = 0; jj < kMaxAggs; ++jj)  // static indices: the column pointers stay in registers
         if (jj < prog.n_out) out.agg[jj][ob] = out_value_reg<MS>(prog, jj, R);
+      if (out.form) out.form[ob] = out_form_reg<MS>(prog, R);
     }
   }
   if (err) atomicOr(&sc->err, err);
@@ -1201,6 +1202,7 @@ __global__ __launch_bounds__(kE1NT) void k_pr_emit1(Batch bt, Program prog, TwPa
 #pragma unroll
       for (int jj = 0; jj < kMaxAggs; ++jj)
         if (jj < prog.n_out) out.agg[jj][ob] = out_value_reg<MS>(prog, jj, R[u]);
+      if (out.form) out.form[ob] = out_form_reg<MS>(prog, R[u]);
     }
   }
   if (err) atomicOr(&sc->err, err);

@@ -374,6 +374,7 @@ __global__ __launch_bounds__(256) void k_ss_process(Batch b, SessParams p, SessT
         out.we[o] = e0;
         out.src[o] = (int64_t)(seq1 - 1);
         for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value_reg<MS>(prog, j, acc);
+        if (out.form) out.form[o] = out_form_reg<MS>(prog, acc);
       }
     }
     t.kt[sl].off = off;
@@ -405,6 +406,7 @@ __global__ __launch_bounds__(256) void k_ss_process(Batch b, SessParams p, SessT
       out.we[o] = (int64_t)row[1];
       out.src[o] = -1;
       for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, (const int64_t *)row + 3);
+      if (out.form) out.form[o] = out_form(prog, (const int64_t *)row + 3);
       ++o;
     }
   }
@@ -690,6 +692,7 @@ __device__ __attribute__((always_inline)) inline void mg_emit(EmitSink &k, const
 #pragma unroll
     for (int j = 0; j < kMaxAggs; ++j)  // static indices: the column pointers stay in registers
       if (j < prog.n_out) k.out.agg[j][o] = out_value_reg<MS>(prog, j, c.a);
+    if (k.out.form) k.out.form[o] = out_form_reg<MS>(prog, c.a);
   }
   ++k.n;
 }
@@ -1809,6 +1812,7 @@ __global__ __launch_bounds__(256) void k_ss_emit(SessTable t, Program prog, Sess
         out.we[o] = (int64_t)row[1];
         out.src[o] = -1;
         for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, (const int64_t *)row + 3);
+      if (out.form) out.form[o] = out_form(prog, (const int64_t *)row + 3);
         ++o;
       }
     }
@@ -1863,6 +1867,7 @@ __global__ __launch_bounds__(256) void k_ss_dump(SessTable t, Program prog, OutC
       out.we[o] = (int64_t)row[1];
       out.src[o] = -1;
       for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, (const int64_t *)row + 3);
+      if (out.form) out.form[o] = out_form(prog, (const int64_t *)row + 3);
     }
     __syncthreads();
   }

@@ -15,13 +15,33 @@ static __constant__ uint64_t kPow5Dev[HSG_POW5_COUNT][2] = {HSG_POW5_ROWS};
 __device__ inline uint32_t frag_len(const SinkDev &S, int f) { return S.frag_off[f + 1] - S.frag_off[f]; }
 
 __device__ inline void key_text(const SinkDev &S, uint32_t k, const char *&p, uint32_t &n) {
-  if (k < S.nkeys) {
+  if ((k & HSG_SPELL_ALT) && k != HSG_KEY_NONE && (uint64_t)(k & ~HSG_SPELL_ALT) < S.nalt) {
+    const uint32_t a = k & ~HSG_SPELL_ALT;
+    p = S.atext + S.atoff[a];
+    n = (uint32_t)(S.atoff[a + 1] - S.atoff[a]);
+  } else if (k < S.nkeys) {
     p = S.ktext + S.ktoff[k];
     n = (uint32_t)(S.ktoff[k + 1] - S.ktoff[k]);
   } else {  // HSG_KEY_NONE never reaches a changelog; an unknown id prints as null
     p = "null";
     n = 4;
   }
+}
+
+// the text a row's key prints with: its record's own spelling when the rows
+// carry their source records and the batch's spellings are given (the
+// reference forwards each record with its own key, TimeWindowedStream.hs:94,101),
+// else the key's first spelling
+__device__ inline uint32_t row_key(const SinkDev &S, uint64_t i) {
+  const uint32_t k = S.key[i];
+  if (S.spell && S.src) {
+    const int64_t r = S.src[i] - S.src_base;
+    if (r >= 0 && (uint64_t)r < S.nspell) {
+      const uint32_t sp = S.spell[r];
+      if (sp != HSG_KEY_NONE) return sp;
+    }
+  }
+  return k;
 }
 
 // text of value member m of row i into buf (numbers) or as a pointer (key text)
@@ -34,23 +54,29 @@ __device__ inline uint32_t member_text(const SinkDev &S, int m, uint64_t i, uint
   }
   p = buf;
   const int64_t v = S.agg[j][i];
-  if ((S.f64_mask >> j) & 1u) {
-    const Pow5Tables T{kPow5InvDev, kPow5Dev};
-    return (uint32_t)fmt_f64(__builtin_bit_cast(double, v), T, buf);
+  const bool f64 = (S.f64_mask >> j) & 1u;
+  const Pow5Tables T{kPow5InvDev, kPow5Dev};
+  if (S.form && ((S.form_mask >> j) & 1u)) {
+    // literal forms: how aeson prints the reference's Scientific
+    const uint32_t fb = (S.form[i] >> (2 * j)) & 3u;
+    if (fb & 2u) return (uint32_t)fmt_i64(S.ident[j] == 1 ? INT64_MAX : S.ident[j] == 2 ? INT64_MIN : 0, buf);
+    if (fb & 1u) return (uint32_t)(f64 ? fmt_f64_integral(__builtin_bit_cast(double, v), T, buf) : fmt_i64(v, buf));
+    return (uint32_t)(f64 ? fmt_f64(__builtin_bit_cast(double, v), T, buf, false) : fmt_i64_decimal(v, buf));
   }
+  if (f64) return (uint32_t)fmt_f64(__builtin_bit_cast(double, v), T, buf);
   return (uint32_t)fmt_i64(v, buf);
 }
 
 __global__ __launch_bounds__(256) void k_sink_len(SinkDev S, uint64_t n, uint32_t *__restrict__ klen,
                                                   uint32_t *__restrict__ vlen) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t k = S.key[i];
+    const uint32_t k = row_key(S, i);
     const char *p;
     uint32_t kn;
     key_text(S, k, p, kn);
     klen[i] = (S.windowed ? 16u : 0u) + frag_len(S, 0) + kn + frag_len(S, 1);
     uint32_t vn = frag_len(S, 2 + S.n_members);
-    char buf[kNumTextMax];
+    char buf[kNumTextIntMax];
     for (int m = 0; m < S.n_members; ++m) vn += frag_len(S, 2 + m) + member_text(S, m, i, k, buf, p);
     vlen[i] = vn;
   }
@@ -69,7 +95,7 @@ __global__ __launch_bounds__(256) void k_sink_write(SinkDev S, uint64_t n, const
                                                     const uint64_t *__restrict__ voff, char *__restrict__ kbytes,
                                                     char *__restrict__ vbytes) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t k = S.key[i];
+    const uint32_t k = row_key(S, i);
     char *o = kbytes + koff[i];
     if (S.windowed) {
       // timeWindowSerde: int64BE start ++ int64BE 0
@@ -85,7 +111,7 @@ __global__ __launch_bounds__(256) void k_sink_write(SinkDev S, uint64_t n, const
     o = put(o, p, kn);
     put_frag(o, S, 1);
     char *v = vbytes + voff[i];
-    char buf[kNumTextMax];
+    char buf[kNumTextIntMax];
     for (int m = 0; m < S.n_members; ++m) {
       v = put_frag(v, S, 2 + m);
       const uint32_t tn = member_text(S, m, i, k, buf, p);

@@ -146,7 +146,7 @@ void launch_clear_scalars(hipStream_t s, DevScalars *sc) { hipLaunchKernelGGL(k_
 
 // changelog rows [from, from + n) of src into device columns (null = skip), one launch
 __global__ void k_copy_rows(OutCols src, uint64_t from, uint64_t n, int n_aggs, uint32_t *key, int64_t *ws, int64_t *we,
-                            int64_t *si, RowPtrs aggs) {
+                            int64_t *si, RowPtrs aggs, uint32_t *form) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t q = from + i;
     if (key) key[i] = src.key[q];
@@ -155,11 +155,14 @@ __global__ void k_copy_rows(OutCols src, uint64_t from, uint64_t n, int n_aggs, 
     if (si) si[i] = src.src[q];
     for (int j = 0; j < n_aggs; ++j)
       if (aggs.p[j]) aggs.p[j][i] = src.agg[j][q];
+    if (form) form[i] = src.form ? src.form[q] : 0u;
   }
 }
 void launch_copy_rows(hipStream_t s, const OutCols &src, uint64_t from, uint64_t n, int n_aggs, uint32_t *key,
-                      int64_t *ws, int64_t *we, int64_t *si, const RowPtrs &aggs) {
-  if (n) hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(n, 256)), dim3(256), 0, s, src, from, n, n_aggs, key, ws, we, si, aggs);
+                      int64_t *ws, int64_t *we, int64_t *si, const RowPtrs &aggs, uint32_t *form) {
+  if (n)
+    hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(n, 256)), dim3(256), 0, s, src, from, n, n_aggs, key, ws, we, si, aggs,
+                       form);
 }
 
 unsigned grid_for(uint64_t n, unsigned tpb) {
@@ -228,6 +231,24 @@ void launch_gather_u32(hipStream_t s, const uint32_t *src, const uint32_t *perm,
 }
 void launch_gather_u64(hipStream_t s, const uint64_t *src, const uint32_t *perm, uint64_t n, uint64_t *dst) {
   if (n) hipLaunchKernelGGL(k_gather_u64, dim3(grid_for(n, 256)), dim3(256), 0, s, src, perm, n, dst);
+}
+
+__global__ __launch_bounds__(256) void k_forms(FormArgs f) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < f.n; i += (uint64_t)gridDim.x * blockDim.x) {
+#pragma unroll
+    for (int c = 0; c < kMaxCols / 3; ++c) {
+      if (c >= f.ncols) break;
+      const uint8_t v = f.valid[c] ? f.valid[c][i] : (uint8_t)1;
+      const uint8_t p = v & 1u, dec = (v >> 1) & 1u;
+      f.out[3 * c][i] = p;
+      f.out[3 * c + 1][i] = p & dec;
+      f.out[3 * c + 2][i] = p & (dec ^ 1u);
+    }
+  }
+}
+
+void launch_forms(hipStream_t s, const FormArgs &f) {
+  if (f.n) hipLaunchKernelGGL(k_forms, dim3(grid_for(f.n, 256)), dim3(256), 0, s, f);
 }
 
 void launch_widen(hipStream_t s, const WidenArgs &w) {
@@ -549,6 +570,7 @@ __global__ __launch_bounds__(256) void k_tw_emit_rows(TwTable t, uint64_t cap, P
     out.we[o] = we;
     out.src[o] = -1;
     for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, row);
+    if (out.form) out.form[o] = out_form(prog, row);
   }
 }
 

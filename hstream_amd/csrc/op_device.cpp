@@ -60,7 +60,8 @@ static bool has_last(const Program &prog) {
   return false;
 }
 
-static int alloc_out(OutCols &o, uint64_t cap, int n_aggs, std::string &err) {
+static int alloc_out(OutCols &o, uint64_t cap, int n_aggs, std::string &err, bool forms = false) {
+  if (forms) DTRY(dalloc(&o.form, cap));
   DTRY(dalloc(&o.key, cap));
   DTRY(dalloc(&o.ws, cap));
   DTRY(dalloc(&o.we, cap));
@@ -75,6 +76,7 @@ static void free_out(OutCols &o) {
   dfree(o.we);
   dfree(o.src);
   for (int j = 0; j < kMaxAggs; ++j) dfree(o.agg[j]);
+  dfree(o.form);
 }
 
 // Partitioned-aggregation scratch, carved from one allocation.
@@ -279,7 +281,7 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
     if (cfg.emit_mode == HSG_EMIT_PER_BATCH && cfg.window_kind != HSG_SESSION && oc > d.cap) oc = d.cap;
   }
   d.out_cap = oc;
-  int rc = alloc_out(d.out, d.out_cap, cfg.n_aggs, err);
+  int rc = alloc_out(d.out, d.out_cap, cfg.n_aggs, err, d.forms);
   d.own_out = d.out;
   d.own_out_cap = d.out_cap;
   if (rc != HSG_OK) return rc;
@@ -325,6 +327,7 @@ void op_device_free(OpDevice &d) {
   }
   dfree(d.st_seq);
   dfree(d.st_wm);
+  dfree(d.form_valid);
   dfree(d.nar_ts);
   dfree(d.nar_key);
   for (int c = 0; c < kMaxCols; ++c) dfree(d.nar_col[c]);
@@ -384,7 +387,7 @@ void op_device_free(OpDevice &d) {
 int op_prestage(OpDevice &d, const hsg_batch *b, int set, std::string &err) {
   // a rank's own ingest (d.batch_cap also counts what an exchange may deliver)
   const uint64_t pcap = d.batch_cap / (d.nranks > 0 ? d.nranks : 1);
-  if (b->mem != HSG_MEM_HOST || set < 0 || set > 1 || b->n > pcap || b->n_cols != d.n_cols) {
+  if (b->mem != HSG_MEM_HOST || set < 0 || set > 1 || b->n > pcap || b->n_cols != d.user_cols) {
     err = "prestage: not a host batch of this op";
     return HSG_E_INVALID;
   }
@@ -451,9 +454,38 @@ static int widen_batch(OpDevice &d, const hsg_batch *b, const void *k16, const v
   return HSG_OK;
 }
 
+static int stage_batch_raw(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err, int staged_set);
+
 // Resolve the batch into device pointers, copying host arrays into staging
-// (or taking the ones op_prestage queued for it).
+// (or taking the ones op_prestage queued for it). Ops with literal forms
+// (HSG_OPF_LITERAL_FORMS) then see every user column c as the internal columns
+// 3c, 3c + 1, 3c + 2: the same values, valid where present / present with a
+// decimal literal / present with an integral literal (bit 1 of the valid byte).
 int stage_batch(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err, int staged_set) {
+  int rc = stage_batch_raw(d, b, kb, err, staged_set);
+  if (rc != HSG_OK || !d.forms) return rc;
+  if (!d.form_valid) DTRY(dalloc(&d.form_valid, (uint64_t)d.n_cols * d.batch_cap));
+  FormArgs fa;
+  memset(&fa, 0, sizeof(fa));
+  fa.n = kb.n;
+  fa.ncols = d.user_cols;
+  Batch x = kb;
+  for (int c = 0; c < d.user_cols; ++c) {
+    fa.valid[c] = kb.valid[c];
+    for (int k = 0; k < 3; ++k) {
+      uint8_t *v = d.form_valid + (uint64_t)(3 * c + k) * d.batch_cap;
+      fa.out[3 * c + k] = v;
+      x.col[3 * c + k] = kb.col[c];
+      x.valid[3 * c + k] = v;
+    }
+  }
+  launch_forms(d.stream, fa);
+  DTRY(hipGetLastError());
+  kb = x;
+  return HSG_OK;
+}
+
+static int stage_batch_raw(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err, int staged_set) {
   memset(&kb, 0, sizeof(kb));
   kb.n = b->n;
   const uint64_t n = b->n;
@@ -822,8 +854,9 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     // next batch's table room: twice this batch's new-group bound (its partials)
     const uint64_t parts = d.h_sc->scratch[31];
     d.lean_pred = (how == 1 || how == 2) ? (2 * parts > (1ull << 16) ? 2 * parts : (1ull << 16)) : 0;
-    // and for a deferred (hopping) batch: twice its deferred window updates
-    const uint64_t dfr = d.h_sc->scratch[34];
+    // and for a deferred (hopping) batch: twice its window updates, deferred
+    // (k_seg_apply) and in-kernel (k_part_agg's touched-list entries)
+    const uint64_t dfr = d.h_sc->scratch[34] + d.h_sc->scratch[1];
     if (how == 3 || how == 4) d.defer_pred = 2 * dfr > (1ull << 16) ? 2 * dfr : (1ull << 16);
     d.lean_batches += how == 1 || how == 2;
     d.direct_batches += how == 1 || how == 3;
@@ -859,7 +892,10 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
 // the table) rather than for one new group per (record, window); every other
 // path gets that worst case.
 static uint64_t table_bound_hint(const OpDevice &d, const hsg_op_config &cfg, const Program &prog) {
-  if (defer_room_checked(d, cfg, prog)) return d.defer_pred;  // (0 before the first batch: its own check grows)
+  // hopping: twice the last batch's window updates (k_part_agg's own and the
+  // deferred ones: a superset of its new groups); the first batch, whose
+  // in-kernel updates have no check of their own, gets the worst case
+  if (defer_room_checked(d, cfg, prog)) return d.defer_pred ? d.defer_pred : UINT64_MAX;
   if (!d.use_part || has_last(prog) || cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.grace_ms < 0 ||
       cfg.window_kind == HSG_SESSION || cfg.n_cols > 8 || d.wpr >= 256)
     return UINT64_MAX;
@@ -923,9 +959,10 @@ int op_copy_rows(OpDevice &d, const OutCols &src, uint64_t from, uint64_t n, int
   RowPtrs ap;
   memset(&ap, 0, sizeof(ap));
   for (int j = 0; j < n_aggs && out->aggs; ++j) ap.p[j] = out->aggs[j] ? (int64_t *)out->aggs[j] + o : nullptr;
+  uint32_t *fm = out->form ? out->form + o : nullptr;
   if (out->mem == HSG_MEM_DEVICE) {
     // device-resident destination: every column in one launch
-    launch_copy_rows(d.stream, src, from, n, n_aggs, key, ws, we, si, ap);
+    launch_copy_rows(d.stream, src, from, n, n_aggs, key, ws, we, si, ap, fm);
     DTRY(hipGetLastError());
     DTRY(hipStreamSynchronize(d.stream));
     return HSG_OK;
@@ -937,6 +974,8 @@ int op_copy_rows(OpDevice &d, const OutCols &src, uint64_t from, uint64_t n, int
   if (si) DTRY(hipMemcpyAsync(si, src.src + from, n * 8, k, d.stream));
   for (int j = 0; j < n_aggs; ++j)
     if (ap.p[j]) DTRY(hipMemcpyAsync(ap.p[j], src.agg[j] + from, n * 8, k, d.stream));
+  if (fm && src.form) DTRY(hipMemcpyAsync(fm, src.form + from, n * 4, k, d.stream));
+  else if (fm) memset(fm, 0, n * 4);
   DTRY(hipStreamSynchronize(d.stream));
   return HSG_OK;
 }
@@ -994,6 +1033,7 @@ static int sort_dump_rows_device(OpDevice &d, const hsg_op_config &cfg, const hs
   if (rc == HSG_OK) rc = col(out->win_end, 8);
   if (rc == HSG_OK) rc = col(out->src_index, 8);
   for (int j = 0; rc == HSG_OK && j < n_aggs && out->aggs; ++j) rc = col(out->aggs[j], 8);
+  if (rc == HSG_OK) rc = col(out->form, 4);
   if (rc != HSG_OK) return rc;
   DTRY(hipGetLastError());
   DTRY(hipStreamSynchronize(d.stream));
@@ -1004,7 +1044,7 @@ static int sort_dump_rows(OpDevice &d, const hsg_rows *out, uint64_t n, int n_ag
   if (n < 2) return HSG_OK;
   const bool dev = out->mem == HSG_MEM_DEVICE;
   const hipMemcpyKind d2h = hipMemcpyDeviceToHost, h2d = hipMemcpyHostToDevice;
-  std::vector<uint32_t> key(n);
+  std::vector<uint32_t> key(n), form(out->form ? n : 0);
   std::vector<int64_t> ws(n), we(n);
   std::vector<std::vector<int64_t>> cols;  // src + aggs, 8-byte words
   std::vector<int64_t *> ptrs;
@@ -1025,6 +1065,7 @@ static int sort_dump_rows(OpDevice &d, const hsg_rows *out, uint64_t n, int n_ag
   int rc = fetch(key.data(), out->key_id, n * 4);
   if (rc == HSG_OK) rc = fetch(ws.data(), out->win_start, n * 8);
   if (rc == HSG_OK) rc = fetch(we.data(), out->win_end, n * 8);
+  if (rc == HSG_OK && out->form) rc = fetch(form.data(), out->form, n * 4);
   cols.resize(ptrs.size());
   for (size_t c = 0; rc == HSG_OK && c < ptrs.size(); ++c) {
     cols[c].resize(n);
@@ -1045,10 +1086,12 @@ static int sort_dump_rows(OpDevice &d, const hsg_rows *out, uint64_t n, int n_ag
   permute(key);
   permute(ws);
   permute(we);
+  if (out->form) permute(form);
   for (auto &c : cols) permute(c);
   rc = store(out->key_id, key.data(), n * 4);
   if (rc == HSG_OK) rc = store(out->win_start, ws.data(), n * 8);
   if (rc == HSG_OK) rc = store(out->win_end, we.data(), n * 8);
+  if (rc == HSG_OK && out->form) rc = store(out->form, form.data(), n * 4);
   for (size_t c = 0; rc == HSG_OK && c < ptrs.size(); ++c) rc = store(ptrs[c], cols[c].data(), n * 8);
   (void)d;
   return rc;
@@ -1064,7 +1107,7 @@ int op_dump(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const hs
   if (live == 0) return tw_dump_spilled(d, cfg, prog, out, 0, n_out, err);
   OutCols tmp;
   memset(&tmp, 0, sizeof(tmp));
-  rc = alloc_out(tmp, live, cfg.n_aggs, err);
+  rc = alloc_out(tmp, live, cfg.n_aggs, err, d.forms);
   if (rc == HSG_OK) {
     uint64_t *counter = nullptr;
     if (hipMalloc((void **)&counter, 8) != hipSuccess) {

@@ -83,6 +83,7 @@ static int grow_out(OpDevice &d, const hsg_op_config &cfg, uint64_t ncap, uint64
   if (e == hipSuccess) e = alloc((void **)&n.we, want * 8);
   if (e == hipSuccess) e = alloc((void **)&n.src, want * 8);
   for (int j = 0; j < cfg.n_aggs && e == hipSuccess; ++j) e = alloc((void **)&n.agg[j], want * 8);
+  if (d.forms && e == hipSuccess) e = alloc((void **)&n.form, want * 4);
   auto release = [](OutCols &o) {
     hipFree(o.key);
     hipFree(o.ws);
@@ -90,6 +91,7 @@ static int grow_out(OpDevice &d, const hsg_op_config &cfg, uint64_t ncap, uint64
     hipFree(o.src);
     for (int j = 0; j < kMaxAggs; ++j)
       if (o.agg[j]) hipFree(o.agg[j]);
+    if (o.form) hipFree(o.form);
     memset(&o, 0, sizeof(o));
   };
   if (e != hipSuccess) {
@@ -104,6 +106,7 @@ static int grow_out(OpDevice &d, const hsg_op_config &cfg, uint64_t ncap, uint64
     DTRY(hipMemcpyAsync(n.we, d.own_out.we, pending * 8, k, d.stream));
     DTRY(hipMemcpyAsync(n.src, d.own_out.src, pending * 8, k, d.stream));
     for (int j = 0; j < cfg.n_aggs; ++j) DTRY(hipMemcpyAsync(n.agg[j], d.own_out.agg[j], pending * 8, k, d.stream));
+    if (n.form && d.own_out.form) DTRY(hipMemcpyAsync(n.form, d.own_out.form, pending * 4, k, d.stream));
   }
   DTRY(hipStreamSynchronize(d.stream));
   release(d.own_out);
@@ -286,6 +289,7 @@ int tw_dump_spilled(OpDevice &d, const hsg_op_config &cfg, const Program &prog, 
   if (e == hipSuccess) e = hipMalloc((void **)&tmp.we, chunk_rows * 8);
   if (e == hipSuccess) e = hipMalloc((void **)&tmp.src, chunk_rows * 8);
   for (int j = 0; j < cfg.n_aggs && e == hipSuccess; ++j) e = hipMalloc((void **)&tmp.agg[j], chunk_rows * 8);
+  if (d.forms && e == hipSuccess) e = hipMalloc((void **)&tmp.form, chunk_rows * 4);
   int rc = HSG_OK;
   if (e != hipSuccess) {
     err = std::string("dump of spilled rows: ") + hipGetErrorString(e);
@@ -318,6 +322,7 @@ int tw_dump_spilled(OpDevice &d, const hsg_op_config &cfg, const Program &prog, 
   hipFree(tmp.src);
   for (int j = 0; j < kMaxAggs; ++j)
     if (tmp.agg[j]) hipFree(tmp.agg[j]);
+  if (tmp.form) hipFree(tmp.form);
   return rc;
 }
 

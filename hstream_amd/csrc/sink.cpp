@@ -16,9 +16,11 @@
 
 namespace hsg {
 // hsg_api.cpp: the op's device and aggregate output types
-int op_sink_info(const hsg_op *op, int *device, int *n_aggs, uint32_t *f64_mask);
-// ingest.cpp: the dictionary's key texts (Aeson encoding), back to back
+int op_sink_info(const hsg_op *op, int *device, int *n_aggs, uint32_t *f64_mask, uint32_t *form_mask, int8_t *ident);
+// ingest.cpp: the dictionary's key texts (Aeson encoding), back to back, and
+// its alternate spellings
 void keydict_texts(const hsg_keydict *d, const char **text, const uint64_t **off, uint64_t *n);
+void keydict_alt_texts(const hsg_keydict *d, const char **text, const uint64_t **off, uint64_t *n);
 
 static const uint64_t kPow5InvHost[HSG_POW5_INV_COUNT][2] = {HSG_POW5_INV_ROWS};
 static const uint64_t kPow5Host[HSG_POW5_COUNT][2] = {HSG_POW5_ROWS};
@@ -38,6 +40,15 @@ struct hsg_sink {
   uint64_t ktext_cap = 0, ktext_dev = 0;
   uint64_t *d_ktoff = nullptr;
   uint64_t ktoff_cap = 0, nkeys_dev = 0;
+  // alternate spellings in HBM (append-only)
+  char *d_atext = nullptr;
+  uint64_t atext_cap = 0, atext_dev = 0;
+  uint64_t *d_atoff = nullptr;
+  uint64_t atoff_cap = 0, nalt_dev = 0;
+  // host rows' form / src and host spellings staged to HBM
+  uint32_t *st_form = nullptr, *st_spell = nullptr;
+  int64_t *st_src = nullptr;
+  uint64_t st_form_cap = 0, st_spell_cap = 0, st_src_cap = 0;
   // per-row scratch
   uint64_t rows_cap = 0;
   uint32_t *klen = nullptr, *vlen = nullptr;
@@ -102,7 +113,7 @@ void free_sink(hsg_sink *s) {
   hipSetDevice(s->device);
   if (s->stream) hipStreamSynchronize(s->stream);
   void *ptrs[] = {s->d_frag, s->d_ktext, s->d_ktoff, s->klen, s->vlen, s->koff, s->voff, s->partial, s->tot,
-                  s->st_key, s->st_ws, s->d_k, s->d_v};
+                  s->st_key, s->st_ws, s->d_k, s->d_v, s->d_atext, s->d_atoff, s->st_form, s->st_spell, s->st_src};
   for (void *p : ptrs)
     if (p) hipFree(p);
   for (int j = 0; j < kMaxAggs; ++j)
@@ -137,6 +148,27 @@ int sync_keys(hsg_sink *s) {
   STRY(hipStreamSynchronize(s->stream));  // the dictionary's arrays may move on its next insert
   s->ktext_dev = bytes;
   s->nkeys_dev = n;
+  return HSG_OK;
+}
+
+// mirror the dictionary's new alternate spellings in HBM
+int sync_alts(hsg_sink *s) {
+  const char *text;
+  const uint64_t *off;
+  uint64_t n;
+  keydict_alt_texts(s->dict, &text, &off, &n);
+  if (n == s->nalt_dev && s->d_atoff) return HSG_OK;
+  const uint64_t bytes = off[n];
+  STRY(regrow(s->d_atext, s->atext_cap, bytes ? bytes : 1, true, s->stream));
+  STRY(regrow(s->d_atoff, s->atoff_cap, n + 1, true, s->stream));
+  if (bytes > s->atext_dev)
+    STRY(hipMemcpyAsync(s->d_atext + s->atext_dev, text + s->atext_dev, bytes - s->atext_dev, hipMemcpyHostToDevice,
+                        s->stream));
+  const uint64_t from = s->nalt_dev ? s->nalt_dev + 1 : 0;
+  STRY(hipMemcpyAsync(s->d_atoff + from, off + from, (n + 1 - from) * 8, hipMemcpyHostToDevice, s->stream));
+  STRY(hipStreamSynchronize(s->stream));
+  s->atext_dev = bytes;
+  s->nalt_dev = n;
   return HSG_OK;
 }
 
@@ -210,8 +242,8 @@ extern "C" int hsg_sink_create(hsg_op *op, const hsg_keydict *dict, const hsg_si
   hsg_sink *s = new (std::nothrow) hsg_sink();
   if (!s) return HSG_E_OOM;
   memset(&s->S, 0, sizeof(s->S));
-  uint32_t f64 = 0;
-  int rc = op_sink_info(op, &s->device, &s->n_aggs, &f64);
+  uint32_t f64 = 0, fmask = 0;
+  int rc = op_sink_info(op, &s->device, &s->n_aggs, &f64, &fmask, s->S.ident);
   if (rc != HSG_OK) {
     delete s;
     return rc;
@@ -250,6 +282,7 @@ extern "C" int hsg_sink_create(hsg_op *op, const hsg_keydict *dict, const hsg_si
   s->S.windowed = cfg->windowed ? 1 : 0;
   s->S.n_members = cfg->n_members;
   s->S.f64_mask = f64;
+  s->S.form_mask = fmask;
   hipError_t e = hipSetDevice(s->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc((void **)&s->d_frag, frag.size());
@@ -279,9 +312,11 @@ extern "C" int hsg_sink_member_order(const char *const *aliases, int32_t n, int3
   return HSG_OK;
 }
 
-extern "C" int hsg_sink_encode(hsg_sink *s, const hsg_rows *rows, uint64_t n, hsg_sink_records *out,
-                               uint64_t *key_need, uint64_t *value_need) {
+extern "C" int hsg_sink_encode_spelled(hsg_sink *s, const hsg_rows *rows, uint64_t n, const hsg_sink_spellings *sp,
+                                       hsg_sink_records *out, uint64_t *key_need, uint64_t *value_need) {
   if (!s || !rows || !out || !key_need || !value_need) return HSG_E_INVALID;
+  if (sp && sp->n && (!sp->spell || !rows->src_index || (sp->mem != HSG_MEM_HOST && sp->mem != HSG_MEM_DEVICE)))
+    return HSG_E_INVALID;
   if (rows->n_aggs != s->n_aggs || (rows->mem != HSG_MEM_HOST && rows->mem != HSG_MEM_DEVICE) ||
       (out->mem != HSG_MEM_HOST && out->mem != HSG_MEM_DEVICE))
     return HSG_E_INVALID;
@@ -296,6 +331,7 @@ extern "C" int hsg_sink_encode(hsg_sink *s, const hsg_rows *rows, uint64_t n, hs
   try {
     STRY(hipSetDevice(s->device));
     int rc = sync_keys(s);
+    if (rc == HSG_OK) rc = sync_alts(s);
     if (rc != HSG_OK) return rc;
     hipStream_t st = s->stream;
     *key_need = *value_need = 0;
@@ -313,6 +349,38 @@ extern "C" int hsg_sink_encode(hsg_sink *s, const hsg_rows *rows, uint64_t n, hs
     S.ktext = s->d_ktext;
     S.ktoff = s->d_ktoff;
     S.nkeys = s->nkeys_dev;
+    S.atext = s->d_atext;
+    S.atoff = s->d_atoff;
+    S.nalt = s->nalt_dev;
+    // literal forms and record spellings: device pointers (host arrays staged)
+    const bool hrows = rows->mem == HSG_MEM_HOST;
+    if (rows->form && s->S.form_mask) {
+      if (hrows) {
+        STRY(regrow(s->st_form, s->st_form_cap, n));
+        STRY(hipMemcpyAsync(s->st_form, rows->form, n * 4, hipMemcpyHostToDevice, st));
+        S.form = s->st_form;
+      } else {
+        S.form = rows->form;
+      }
+    }
+    if (sp && sp->n) {
+      if (hrows) {
+        STRY(regrow(s->st_src, s->st_src_cap, n));
+        STRY(hipMemcpyAsync(s->st_src, rows->src_index, n * 8, hipMemcpyHostToDevice, st));
+        S.src = s->st_src;
+      } else {
+        S.src = rows->src_index;
+      }
+      if (sp->mem == HSG_MEM_HOST) {
+        STRY(regrow(s->st_spell, s->st_spell_cap, sp->n));
+        STRY(hipMemcpyAsync(s->st_spell, sp->spell, sp->n * 4, hipMemcpyHostToDevice, st));
+        S.spell = s->st_spell;
+      } else {
+        S.spell = sp->spell;
+      }
+      S.src_base = sp->src_base;
+      S.nspell = sp->n;
+    }
     if (rows->mem == HSG_MEM_DEVICE) {
       S.key = rows->key_id;
       S.ws = rows->win_start;
@@ -383,6 +451,11 @@ extern "C" int hsg_sink_encode(hsg_sink *s, const hsg_rows *rows, uint64_t n, hs
   } catch (const std::bad_alloc &) {
     return HSG_E_OOM;
   }
+}
+
+extern "C" int hsg_sink_encode(hsg_sink *s, const hsg_rows *rows, uint64_t n, hsg_sink_records *out,
+                               uint64_t *key_need, uint64_t *value_need) {
+  return hsg_sink_encode_spelled(s, rows, n, nullptr, out, key_need, value_need);
 }
 
 extern "C" int hsg_format_number(int32_t is_f64, int64_t bits, char *buf, size_t cap, size_t *len) {

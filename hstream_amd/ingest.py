@@ -39,6 +39,11 @@ def _lib():
         L.hsg_decode_json.argtypes = [vp, vp, C.c_uint64, C.c_char_p, vp, vp, vp, vp, P(vp), P(vp), vp,
                                       P(C.c_uint64), C.c_int]
         L.hsg_decode_json.restype = C.c_int
+        L.hsg_decode_json_spelled.argtypes = [vp, vp, C.c_uint64, C.c_char_p, vp, vp, vp, vp, P(vp), P(vp), vp,
+                                              P(C.c_uint64), vp, C.c_int]
+        L.hsg_decode_json_spelled.restype = C.c_int
+        L.hsg_keydict_spelling_text.argtypes = [vp, C.c_uint32, C.c_char_p, C.c_size_t, P(C.c_size_t)]
+        L.hsg_keydict_spelling_text.restype = C.c_int
         _declared = True
     return L
 
@@ -83,6 +88,17 @@ class KeyDict:
     def decode(self, i: int):
         return json.loads(self.text(i))
 
+    def spelling_text(self, spell: int) -> str:
+        """Text of a record's key spelling (Decoder.decode(..., spellings=True))."""
+        n = C.c_size_t()
+        rc = self._L.hsg_keydict_spelling_text(self._h, int(spell), None, 0, C.byref(n))
+        if rc not in (abi.HSG_OK, abi.HSG_E_CAPACITY):
+            _check(rc, "hsg_keydict_spelling_text")
+        buf = C.create_string_buffer(max(1, n.value))
+        _check(self._L.hsg_keydict_spelling_text(self._h, int(spell), buf, n.value, C.byref(n)),
+               "hsg_keydict_spelling_text")
+        return buf.raw[: n.value].decode()
+
     @property
     def handle(self):
         return self._h
@@ -104,9 +120,11 @@ class Decoder:
 
     cols: [(field, hsg_col_type, numeric)] in the op's column order; numeric
     = the column feeds SUM/MIN/MAX/AVG/LAST (a value must be a Number), else
-    COUNT(col) only (any present value counts)."""
+    COUNT(col) only (any present value counts). literal_forms: valid bytes
+    carry bit 1 for numbers written with a negative exponent (ops with
+    HSG_OPF_LITERAL_FORMS)."""
 
-    def __init__(self, key_field: str, cols: Sequence[Tuple[str, int, bool]]):
+    def __init__(self, key_field: str, cols: Sequence[Tuple[str, int, bool]], literal_forms: bool = False):
         self._L = _lib()
         self.key_field = key_field
         self.cols = list(cols)
@@ -115,15 +133,18 @@ class Decoder:
         self._types = (C.c_int32 * max(1, n))(*[t for _, t, _ in self.cols])
         self._num = (C.c_uint8 * max(1, n))(*[1 if num else 0 for _, _, num in self.cols])
         cfg = abi.hsg_decoder_config(key_field=key_field.encode(), n_cols=n, col_fields=self._fields,
-                                     col_types=self._types, col_numeric=self._num)
+                                     col_types=self._types, col_numeric=self._num,
+                                     literal_forms=1 if literal_forms else 0)
         h = C.c_void_p()
         _check(self._L.hsg_decoder_create(C.byref(cfg), C.byref(h)), "hsg_decoder_create")
         self._h = h
 
-    def decode(self, keys: KeyDict, buf: bytes, off: np.ndarray, ts: np.ndarray, threads: int = 0):
+    def decode(self, keys: KeyDict, buf: bytes, off: np.ndarray, ts: np.ndarray, threads: int = 0,
+               spellings: bool = False):
         """One poll batch: buf holds the record values back to back, record i
         at buf[off[i]:off[i+1]]. Returns (key_id u32[n], ts i64[n], cols,
-        valid, status u8[n], rejected)."""
+        valid, status u8[n], rejected), and with spellings=True also spell
+        u32[n] (hsg_decode_json_spelled: each record's key spelling)."""
         n = len(off) - 1
         off = np.ascontiguousarray(off, dtype=np.uint64)
         ts_in = np.ascontiguousarray(ts, dtype=np.int64)
@@ -135,6 +156,13 @@ class Decoder:
         cp = (C.c_void_p * max(1, len(cols)))(*[c.ctypes.data for c in cols])
         vp = (C.c_void_p * max(1, len(valid)))(*[v.ctypes.data for v in valid])
         rej = C.c_uint64()
+        if spellings:
+            spell = np.empty(n, np.uint32)
+            _check(self._L.hsg_decode_json_spelled(self._h, keys.handle, n, buf, off.ctypes.data, ts_in.ctypes.data,
+                                                   key.ctypes.data, ts_out.ctypes.data, cp, vp, status.ctypes.data,
+                                                   C.byref(rej), spell.ctypes.data, int(threads)),
+                   "hsg_decode_json_spelled")
+            return key, ts_out, cols, valid, status, int(rej.value), spell
         _check(self._L.hsg_decode_json(self._h, keys.handle, n, buf, off.ctypes.data, ts_in.ctypes.data,
                                        key.ctypes.data, ts_out.ctypes.data, cp, vp, status.ctypes.data,
                                        C.byref(rej), int(threads)), "hsg_decode_json")

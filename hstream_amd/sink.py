@@ -29,6 +29,9 @@ def _lib():
         L.hsg_sink_encode.argtypes = [vp, P(abi.hsg_rows), C.c_uint64, P(hsg_sink_records), P(C.c_uint64),
                                       P(C.c_uint64)]
         L.hsg_sink_encode.restype = C.c_int
+        L.hsg_sink_encode_spelled.argtypes = [vp, P(abi.hsg_rows), C.c_uint64, P(abi.hsg_sink_spellings),
+                                              P(hsg_sink_records), P(C.c_uint64), P(C.c_uint64)]
+        L.hsg_sink_encode_spelled.restype = C.c_int
         L.hsg_sink_member_order.argtypes = [P(C.c_char_p), C.c_int32, P(C.c_int32)]
         L.hsg_sink_member_order.restype = C.c_int
         L.hsg_format_number.argtypes = [C.c_int32, C.c_int64, C.c_char_p, C.c_size_t, P(C.c_size_t)]
@@ -80,29 +83,44 @@ class Sink:
         self._h = h
         self.n_aggs = len(op.spec.aggs)
 
-    def encode(self, rows) -> List[Tuple[bytes, bytes]]:
-        """Host rows (columnar.Rows) -> [(key bytes, value bytes)]."""
+    def encode(self, rows, spellings=None, src_base: int = 0) -> List[Tuple[bytes, bytes]]:
+        """Host rows (columnar.Rows) -> [(key bytes, value bytes)]. The rows'
+        literal forms (rows.form) are used when present; spellings = the
+        records' key spellings (Decoder.decode(..., spellings=True)) of the
+        records whose global indices start at src_base
+        (hsg_sink_encode_spelled)."""
         n = len(rows)
         key = np.ascontiguousarray(rows.key_id, np.uint32)
         ws = np.ascontiguousarray(rows.win_start, np.int64)
+        src = np.ascontiguousarray(rows.src_index, np.int64)
         aggs = [np.ascontiguousarray(a).view(np.int64) for a in rows.aggs]
         ap = (C.c_void_p * max(1, len(aggs)))(*[a.ctypes.data for a in aggs])
+        form = np.ascontiguousarray(rows.form, np.uint32) if rows.form is not None else None
         r = abi.hsg_rows(capacity=n, mem=abi.HSG_MEM_HOST, n_aggs=len(aggs), key_id=key.ctypes.data,
-                         win_start=ws.ctypes.data, win_end=None, src_index=None,
-                         aggs=C.cast(ap, C.POINTER(C.c_void_p)))
+                         win_start=ws.ctypes.data, win_end=None, src_index=src.ctypes.data,
+                         aggs=C.cast(ap, C.POINTER(C.c_void_p)),
+                         form=form.ctypes.data if form is not None else None)
+        sp = None
+        if spellings is not None:
+            spa = np.ascontiguousarray(spellings, np.uint32)
+            sp = abi.hsg_sink_spellings(spell=spa.ctypes.data, n=len(spa), src_base=int(src_base),
+                                        mem=abi.HSG_MEM_HOST)
+            self._keep_sp = spa
         koff = np.zeros(n + 1, np.uint64)
         voff = np.zeros(n + 1, np.uint64)
         kneed, vneed = C.c_uint64(), C.c_uint64()
         out = hsg_sink_records(mem=abi.HSG_MEM_HOST, key_capacity=0, value_capacity=0, key_bytes=None,
                                key_off=koff.ctypes.data, value_bytes=None, value_off=voff.ctypes.data)
-        rc = self._L.hsg_sink_encode(self._h, C.byref(r), n, C.byref(out), C.byref(kneed), C.byref(vneed))
+        rc = self._L.hsg_sink_encode_spelled(self._h, C.byref(r), n, C.byref(sp) if sp is not None else None,
+                                             C.byref(out), C.byref(kneed), C.byref(vneed))
         if rc not in (abi.HSG_OK, abi.HSG_E_CAPACITY):
             raise abi.HStreamGpuError(rc, "hsg_sink_encode")
         kb = np.zeros(max(1, kneed.value), np.uint8)
         vb = np.zeros(max(1, vneed.value), np.uint8)
         out.key_capacity, out.value_capacity = kneed.value, vneed.value
         out.key_bytes, out.value_bytes = kb.ctypes.data, vb.ctypes.data
-        rc = self._L.hsg_sink_encode(self._h, C.byref(r), n, C.byref(out), C.byref(kneed), C.byref(vneed))
+        rc = self._L.hsg_sink_encode_spelled(self._h, C.byref(r), n, C.byref(sp) if sp is not None else None,
+                                             C.byref(out), C.byref(kneed), C.byref(vneed))
         if rc != abi.HSG_OK:
             raise abi.HStreamGpuError(rc, "hsg_sink_encode")
         kbb, vbb = kb.tobytes(), vb.tobytes()

@@ -158,7 +158,22 @@ typedef struct {
                             * room, grows and runs the batch again), else by one group
                             * per (record, window)                                      */
   uint64_t out_capacity;   /* changelog rows buffered in HBM between drains; 0 = default */
+  uint32_t flags;          /* HSG_OPF_* (0 = none)                                        */
+  uint32_t reserved;       /* 0                                                           */
 } hsg_op_config;
+
+/* hsg_op_config.flags */
+#define HSG_OPF_LITERAL_FORMS 1u /* Track how aeson prints each SUM / MIN / MAX / LAST output:
+   the reference aggregates Data.Scientific values, and aeson prints a Scientific
+   whose exponent is >= 0 as an integer, else in Generic form ("6" vs "6.0",
+   hstream-sql/src/HStream/SQL/Codegen/Boilerplate.hs:32-37 objectSerde over
+   Codegen.hs:423-469). Batches then mark, in bit 1 of each valid byte, the values
+   whose JSON literal had a negative exponent (hstream_ingest.h literal_forms); a
+   SUM prints as an integer iff none of its values did (a Scientific sum takes the
+   smaller exponent), a MIN / MAX / LAST as its winning value was spelled, an
+   aggregate nothing reached as the reference's initial value. Changelog and dump
+   rows then carry hsg_rows.form. At most 2 value columns (each is tracked as
+   three internal columns). */
 
 /* One micro-batch in columnar form, records in arrival order.
  *
@@ -199,6 +214,9 @@ typedef struct {
   int64_t *win_end;    /* time windows: start + size; sessions: session end (inclusive) */
   int64_t *src_index;  /* per-record mode: global index of the producing record; else -1 */
   void *const *aggs;   /* n_aggs arrays: int64_t (COUNT*, SUM/MIN/MAX/LAST of i64) or double */
+  uint32_t *form;      /* optional (NULL = not wanted), ops with HSG_OPF_LITERAL_FORMS:
+                          per row, bits 2j / 2j+1 of aggregate j: aeson prints it as an
+                          integer / it is the aggregate's initial value (nothing reached it) */
 } hsg_rows;
 
 typedef struct {

@@ -18,12 +18,14 @@
  * field, wrong-typed aggregated field) gets key_id = HSG_KEY_NONE: it still
  * moves stream time (Processor.hs:139), exactly as there.
  *
- * Known divergence: the dictionary keeps the Aeson text of a key's FIRST
- * spelling, and the sink prints every changelog row's key with it. The
- * reference forwards each record with its own recordKey (TimeWindowedStream.hs
- * :94,101), so under EMIT CHANGES a later {"k":1.0} after {"k":1} prints key
- * "1.0" there and "1" here (the same group either way; only the text of
- * equal-but-differently-spelled keys differs).
+ * Key spellings: equal keys can print differently, because aeson prints a
+ * number by its literal's exponent (1 and 1e0 print "1", 1.0 and 10e-1
+ * "1.0"). The reference forwards each record with its own recordKey
+ * (TimeWindowedStream.hs:94,101), so under EMIT CHANGES a row's key prints as
+ * its record spelled it. hsg_decode_json_spelled reports each record's
+ * spelling: the key id when it prints like the key's first spelling, else an
+ * alternate spelling (HSG_SPELL_ALT | index) with its own text; the sink
+ * (hstream_sink.h hsg_sink_encode_spelled) prints each row's key with it.
  *
  * Where the GPU's fixed-width columns cannot hold what Scientific holds, the
  * record is rejected with its own status instead of being rounded: a
@@ -54,6 +56,10 @@ enum hsg_decode_status {
   HSG_DEC_RANGE = 5         /* integral Number outside int64 in an HSG_I64 column   */
 };
 
+/* spelling of a record's key (hsg_decode_json_spelled): a key id, or this bit
+ * with the index of an alternate spelling */
+#define HSG_SPELL_ALT 0x80000000u
+
 /* ---- key dictionary: Aeson Value -> dense u32 id (first-seen order) ------- */
 typedef struct hsg_keydict hsg_keydict;
 int  hsg_keydict_create(hsg_keydict **out);
@@ -67,6 +73,9 @@ int  hsg_keydict_encode(hsg_keydict *d, const char *json, size_t len, uint32_t *
  * sorted order). *len = bytes needed; HSG_E_CAPACITY (nothing copied) when
  * cap is smaller, HSG_E_INVALID for an unknown id. */
 int  hsg_keydict_text(const hsg_keydict *d, uint32_t id, char *buf, size_t cap, size_t *len);
+/* The text of a spelling from hsg_decode_json_spelled (a key id: its first
+ * spelling's text, as hsg_keydict_text). Same capacity rule. */
+int  hsg_keydict_spelling_text(const hsg_keydict *d, uint32_t spell, char *buf, size_t cap, size_t *len);
 
 /* ---- record decoder --------------------------------------------------------- */
 typedef struct {
@@ -76,6 +85,9 @@ typedef struct {
   const int32_t *col_types;       /* hsg_col_type                                       */
   const uint8_t *col_numeric;     /* 1: must be a Number (SUM/MIN/MAX/AVG/LAST);
                                      0: presence only (COUNT(col): any value, null too) */
+  int32_t literal_forms;          /* 1: valid bytes are 1 | (the number's JSON literal had a
+                                     negative Scientific exponent, e.g. 2.0 or 25e-1) << 1, for
+                                     ops with HSG_OPF_LITERAL_FORMS (hstream_gpu.h)        */
 } hsg_decoder_config;
 
 typedef struct hsg_decoder hsg_decoder;
@@ -92,6 +104,13 @@ void hsg_decoder_destroy(hsg_decoder *d);
 int  hsg_decode_json(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, const char *buf, const uint64_t *off,
                      const int64_t *rec_ts, uint32_t *key_id, int64_t *ts, void *const *cols,
                      uint8_t *const *valid, uint8_t *status, uint64_t *rejected, int n_threads);
+/* hsg_decode_json plus spell[i], record i's key spelling (HSG_KEY_NONE for a
+ * rejected record): its key id when the key prints like its first spelling,
+ * else HSG_SPELL_ALT | an alternate spelling (texts: hsg_keydict_spelling_text). */
+int  hsg_decode_json_spelled(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, const char *buf, const uint64_t *off,
+                             const int64_t *rec_ts, uint32_t *key_id, int64_t *ts, void *const *cols,
+                             uint8_t *const *valid, uint8_t *status, uint64_t *rejected, uint32_t *spell,
+                             int n_threads);
 
 #ifdef __cplusplus
 }

@@ -12,14 +12,20 @@
  * so the bytes handed to the stream append (Processor.hs:252-266) come out of
  * one kernel pass over the changelog instead of one Aeson encode per row.
  * The key object is {key_field: key value} (Codegen.hs:485-487) with the key's
- * text from the ingest dictionary (hstream_ingest.h). Numbers print as aeson
- * prints Data.Scientific: integers plainly, f64 aggregates in Scientific's
- * Generic form of their shortest round-trip decimal ("2.5", "4.0", "1.0e-3");
- * an aggregate identity prints as the reference's integer initial value
- * (Codegen.hs:425,438,451: a decimal SUM nothing reached "0", MAX / MIN
- * "-9223372036854775808" / "9223372036854775807"). Known divergence: a decimal
- * aggregate of integer JSON literals only (Scientific exponent >= 0) prints
- * "6.0" where aeson prints "6" (the f64 column keeps no exponent).
+ * text from the ingest dictionary (hstream_ingest.h): under EMIT CHANGES each
+ * row's key in its own record's spelling (hsg_sink_encode_spelled with the
+ * batch's spellings from hsg_decode_json_spelled: 1 vs 1.0), as the reference
+ * forwards each record with its own key (TimeWindowedStream.hs:94,101).
+ * Numbers print as aeson prints the reference's Data.Scientific
+ * (Boilerplate.hs:32-37 objectSerde): an exponent >= 0 as an integer, else
+ * Scientific's Generic form of the shortest round-trip decimal ("2.5", "4.0",
+ * "1.0e-3"). For an op with HSG_OPF_LITERAL_FORMS the rows' form column says
+ * which (a SUM of integer literals prints "6", of decimal ones "6.0"; a MIN /
+ * MAX / LAST as its winning value was written) and which rows hold an
+ * aggregate's initial value ("0", MIN "9223372036854775807", MAX
+ * "-9223372036854775808", Codegen.hs:404-469). Rows without forms print
+ * integer columns plainly and f64 columns in Generic form, identities as those
+ * initial values.
  * Members are written in aeson's order for an Object, the traversal order of
  * its HashMap (hashable-1.3.0.0 Text hash, unordered-containers-0.2.10.0,
  * Stack lts-16.21; restated in sink.cpp, pinned by that restatement only: no
@@ -67,6 +73,22 @@ void hsg_sink_destroy(hsg_sink *s);
  * they exceed the capacities nothing is written and HSG_E_CAPACITY returned. */
 int  hsg_sink_encode(hsg_sink *s, const hsg_rows *rows, uint64_t n, hsg_sink_records *out, uint64_t *key_need,
                      uint64_t *value_need);
+
+/* The records' own key spellings (hsg_decode_json_spelled) for the rows of
+ * hsg_sink_encode_spelled: a row whose src_index is in [src_base, src_base + n)
+ * prints its key as spell[src_index - src_base]; other rows (per-batch rows,
+ * src_index -1) print the key's first spelling. */
+typedef struct {
+  const uint32_t *spell;
+  uint64_t n;
+  int64_t src_base;    /* global index of spell[0]'s record (the batch's first record) */
+  int32_t mem;         /* hsg_mem of spell */
+  int32_t reserved;
+} hsg_sink_spellings;
+/* hsg_sink_encode with the records' key spellings (sp may be NULL); rows'
+ * src_index is read when sp is given. */
+int  hsg_sink_encode_spelled(hsg_sink *s, const hsg_rows *rows, uint64_t n, const hsg_sink_spellings *sp,
+                             hsg_sink_records *out, uint64_t *key_need, uint64_t *value_need);
 /* The order the value object's members are written in: order[k] = index (in
  * aliases) of the k-th member written. For tests and hosts that build the
  * same objects. */

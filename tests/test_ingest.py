@@ -297,3 +297,48 @@ def test_keydict_encode_and_text():
     with pytest.raises(abi.HStreamGpuError):
         kd.encode_json("{")
     assert len(kd) == 3
+
+
+def test_literal_form_valid_bits():
+    """literal_forms: a present number's valid byte is 1 for an exponent >= 0
+    ("2", "1e1", "-4") and 3 for a negative one ("2.0", "25e-1", "20e-1",
+    Data.Scientific keeps the literal's exponent); absent fields stay 0."""
+    lits = ["2", "2.0", "25e-1", "1e1", "-4", "-4.0", "20e-1", "0.5", "1E2", None]
+    vals = [("{\"k\":1" + ("" if x is None else ",\"x\":" + x + ",\"v\":" + x) + "}").encode() for x in lits]
+    dec = Decoder("k", [("x", abi.HSG_F64, True), ("v", abi.HSG_I64, False)], literal_forms=True)
+    buf, off = pack_records(vals)
+    keys = KeyDict()
+    _, _, cols, valid, st, rej = dec.decode(keys, buf, off, np.zeros(len(vals), np.int64))
+    assert rej == 0
+    want = [1, 3, 3, 1, 1, 3, 3, 3, 1, 0]
+    assert valid[0].tolist() == want
+    assert cols[0][:9].tolist() == [2.0, 2.0, 2.5, 10.0, -4.0, -4.0, 2.0, 0.5, 100.0]
+    # a COUNT-only column keeps plain 0 / 1
+    assert valid[1].tolist() == [1] * 9 + [0]
+    # without literal_forms every present value is 1
+    plain = Decoder("k", [("x", abi.HSG_F64, True)])
+    _, _, _, valid2, _, _ = plain.decode(keys, buf, off, np.zeros(len(vals), np.int64))
+    assert valid2[0].tolist() == [1] * 9 + [0]
+
+
+def test_key_spellings():
+    """Keys 1 / 1.0 / 1e0 / 10e-1 / 100e-2 are one group (Aeson Value
+    equality); a record's spelling id is the key id when it prints as the
+    group's text and HSG_SPELL_ALT | i for another spelling (aeson prints
+    "1" for an exponent >= 0 and "1.0" for a negative one)."""
+    lits = ["1", "1.0", "1e0", "10e-1", "100e-2", "\"a\"", "2.5", "25e-1", "1.0"]
+    vals = [("{\"k\":" + k + "}").encode() for k in lits]
+    keys = KeyDict()
+    dec = Decoder("k", [])
+    buf, off = pack_records(vals)
+    kid, _, _, _, _, rej, spell = dec.decode(keys, buf, off, np.zeros(len(vals), np.int64), spellings=True)
+    assert rej == 0
+    assert len(set(kid[:5].tolist())) == 1 and kid[8] == kid[0] and kid[6] == kid[7]
+    assert keys.text(int(kid[0])) == "1"
+    texts = [keys.spelling_text(int(s)) for s in spell]
+    assert texts == ["1", "1.0", "1", "1.0", "1.0", "\"a\"", "2.5", "2.5", "1.0"]
+    assert spell[0] == kid[0] and spell[2] == kid[0]
+    assert spell[1] & abi.HSG_SPELL_ALT and spell[1] == spell[3] == spell[4] == spell[8]
+    # spellings across batches reuse the alternate ids
+    kid2, _, _, _, _, _, spell2 = dec.decode(keys, buf, off, np.zeros(len(vals), np.int64), spellings=True)
+    assert kid2.tolist() == kid.tolist() and spell2.tolist() == spell.tolist()

@@ -18,10 +18,11 @@ is pinned by this restatement of the libraries' published algorithm only.
 Aggregate identities (Codegen.hs:425,438,451: Number 0, minBound / maxBound
 :: Int, exponent 0) print as integers: a decimal column's SUM / MAX / MIN no
 value reached is "0" / "-9223372036854775808" / "9223372036854775807"
-(test_sink_identity_text, hand-derived). Known divergence, parity
-unpinned: a decimal aggregate whose value came only from integer JSON
-literals (Scientific exponent >= 0) prints "6" in the reference and "6.0"
-here (the f64 column keeps no exponent).
+(test_sink_identity_text, hand-derived). With HSG_OPF_LITERAL_FORMS every
+SUM / MIN / MAX prints as the reference's Scientific does (an exponent >= 0 as
+an integer), and under EMIT CHANGES each row's key prints in its record's own
+spelling: test_sink_literal_forms_and_key_spellings, against a restatement of
+Data.Scientific's sum / min / max and aeson's number encoding.
 """
 import json
 import math
@@ -206,6 +207,132 @@ def test_sink_records_match_serdes(windowed):
         assert vb == ev, (i, vb, ev)
     # the value bytes parse as JSON with the projected members
     assert set(json.loads(got[0][1].decode())) == {a for a, _ in members}
+    sink.close()
+    op.close()
+    eng.close()
+
+
+# ---------------------------------------------------------------------------
+# GPU: literal forms and key spellings (HSG_OPF_LITERAL_FORMS,
+# hsg_decode_json_spelled, hsg_sink_encode_spelled) against a restatement of
+# Data.Scientific arithmetic and aeson's number encoding
+# ---------------------------------------------------------------------------
+def sci_parse(text: str):
+    """A JSON number literal as Data.Scientific keeps it: (coefficient,
+    exponent), not normalised (2.50 is 250e-2)."""
+    t = text.lower()
+    mant, _, ex = t.partition("e")
+    ip, _, fp = mant.partition(".")
+    neg = ip.startswith("-")
+    digits = ip.lstrip("-") + fp
+    c = int(digits) * (-1 if neg else 1)
+    return c, (int(ex) if ex else 0) - len(fp)
+
+
+def sci_add(a, b):
+    e = min(a[1], b[1])
+    return a[0] * 10 ** (a[1] - e) + b[0] * 10 ** (b[1] - e), e
+
+
+def sci_val(a):
+    from fractions import Fraction
+    return Fraction(a[0]) * Fraction(10) ** a[1]
+
+
+def aeson_sci(a) -> str:
+    """aeson 1.4's Number encoding: exponent in [0, 1024] as an integer, else
+    formatScientific Generic."""
+    c, e = a
+    if 0 <= e <= 1024:
+        return str(c * 10 ** e)
+    return generic(Decimal(c).scaleb(e))
+
+
+MAXB, MINB = ((1 << 63) - 1, 0), (-(1 << 63), 0)  # maxBound / minBound :: Int (Codegen.hs:438,451)
+
+
+def _ref_changelog_rows(recs, size):
+    """The reference's per-record fold per (key, window) (TimeWindowedStream.hs
+    :86-103 with Codegen.hs:404-469's components), one row per record: the
+    state after it. recs: (key value text, ts, x literal or None, v literal)."""
+    state = {}
+    out = []
+    for key_text, ts, x, v in recs:
+        ws = (ts // size) * size
+        key = json.loads(key_text)
+        kk = (float(key) if isinstance(key, (int, float)) else json.dumps(key), ws)
+        st = state.setdefault(kk, {"cnt": 0, "sx": (0, 0), "mnx": MAXB, "mxx": MINB, "sv": (0, 0), "mxv": MINB})
+        st["cnt"] += 1
+        if x is not None:
+            sx = sci_parse(x)
+            st["sx"] = sci_add(st["sx"], sx)
+            st["mnx"] = st["mnx"] if sci_val(st["mnx"]) <= sci_val(sx) else sx    # min n x: n on ties
+            st["mxx"] = sx if sci_val(st["mxx"]) <= sci_val(sx) else st["mxx"]    # max n x: x on ties
+        sv = sci_parse(v)
+        st["sv"] = sci_add(st["sv"], sv)
+        st["mxv"] = sv if sci_val(st["mxv"]) <= sci_val(sv) else st["mxv"]
+        out.append((key_text, ws, {"cnt": str(st["cnt"]), "sum_x": aeson_sci(st["sx"]), "min_x": aeson_sci(st["mnx"]),
+                                   "max_x": aeson_sci(st["mxx"]), "sum_v": aeson_sci(st["sv"]),
+                                   "max_v": aeson_sci(st["mxv"])}))
+    return out
+
+
+@pytest.mark.gpu
+def test_sink_literal_forms_and_key_spellings():
+    """Decimal columns fed integral literals print integers ("6" for 2 + 4),
+    mixed 2 / 2.0 / 25e-1 / 1e1 spellings follow the Scientific exponent
+    rules (a SUM's exponent is the smaller one, MAX keeps the later of equal
+    values, MIN the earlier), absent fields leave the reference's initial
+    values (0, maxBound, minBound), an i64 column fed 20e-1 prints "2.0"; keys
+    1 / 1.0 / 1e0 / 10e-1 are one group whose rows print each record's own
+    spelling ("1" or "1.0")."""
+    import torch
+    assert torch.cuda.is_available()
+    from hstream_amd.columnar import OpSpec
+    from hstream_amd.engine import Engine
+    from hstream_amd.ingest import Decoder, KeyDict, pack_records
+    from hstream_amd.sink import Sink
+    rng = random.Random(17)
+    keylits = ["1", "1.0", "1e0", "10e-1", '"a"', "2.5", "25e-1"]
+    xlits = ["2", "2.0", "4", "25e-1", "2.50", "1e1", "-4", "-4.0", "0.5", "7", "3.25", None, None]
+    vlits = ["5", "-3", "20e-1", "2e1", "7", "7.0", "-1"]
+    recs, vals, ts = [], [], []
+    for i in range(3000):
+        kt, x, v = rng.choice(keylits), rng.choice(xlits), rng.choice(vlits)
+        t = 1_000_000 + 7 * i
+        recs.append((kt, t, x, v))
+        body = '{"k":' + kt + ',"v":' + v + ("" if x is None else ',"x":' + x) + "}"
+        vals.append(body.encode())
+        ts.append(t)
+    size = 5000
+    eng = Engine(device=0, batch_capacity=1 << 14)
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_RECORD, size_ms=size, col_types=[abi.HSG_I64, abi.HSG_F64],
+                  aggs=[(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 1), (abi.HSG_MIN, 1), (abi.HSG_MAX, 1), (abi.HSG_SUM, 0),
+                        (abi.HSG_MAX, 0)], flags=abi.HSG_OPF_LITERAL_FORMS)
+    op = eng.op(spec)
+    keys = KeyDict()
+    dec = Decoder("k", [("v", abi.HSG_I64, True), ("x", abi.HSG_F64, True)], literal_forms=True)
+    buf, off = pack_records(vals)
+    kid, t, cols, valid, st, rej, spell = dec.decode(keys, buf, off, np.array(ts, np.int64), spellings=True)
+    assert rej == 0
+    assert len(set(int(k) for k, r in zip(kid, recs) if r[0] in ("1", "1.0", "1e0", "10e-1"))) == 1
+    op.push(kid, t, cols, valid)
+    rows = op.drain()
+    assert rows.form is not None and len(rows) == len(recs)
+    members = [("cnt", 0), ("sum_x", 1), ("min_x", 2), ("max_x", 3), ("sum_v", 4), ("max_v", 5), ("k", -1)]
+    sink = Sink(op, keys, "k", members, windowed=True)
+    got = sink.encode(rows, spellings=spell, src_base=0)
+    ref = _ref_changelog_rows(recs, size)
+    written = [members[m] for m in aeson_member_order([a for a, _ in members])]
+    for i, (kb, vb) in enumerate(got):
+        r = int(rows.src_index[i])
+        key_text, ws, texts = ref[r]
+        own = json.dumps(json.loads(key_text)) if key_text.startswith('"') else aeson_sci(sci_parse(key_text))
+        mem = [(a, own if j < 0 else texts[a]) for a, j in written]
+        ek, ev = _ref_record(own, "k", ws, mem, True)
+        assert kb == ek, (i, r, kb, ek)
+        assert vb == ev, (i, r, recs[r], vb, ev)
+    # the dump of the state carries the forms too (last rows of each group)
     sink.close()
     op.close()
     eng.close()
