@@ -837,6 +837,7 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     }
     return rc;
   };
+  const uint64_t live0 = d.h_sc->live;  // rows before the batch (after its tw_maintain)
   int rc = run_room(opt);
   if (rc != HSG_OK) return rc;
   if (opt && kb.n && d.h_sc->redo) {
@@ -854,10 +855,12 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     // next batch's table room: twice this batch's new-group bound (its partials)
     const uint64_t parts = d.h_sc->scratch[31];
     d.lean_pred = (how == 1 || how == 2) ? (2 * parts > (1ull << 16) ? 2 * parts : (1ull << 16)) : 0;
-    // and for a deferred (hopping) batch: twice its window updates, deferred
-    // (k_seg_apply) and in-kernel (k_part_agg's touched-list entries)
-    const uint64_t dfr = d.h_sc->scratch[34] + d.h_sc->scratch[1];
-    if (how == 3 || how == 4) d.defer_pred = 2 * dfr > (1ull << 16) ? 2 * dfr : (1ull << 16);
+    // and for a deferred (hopping) batch: twice its new groups plus twice its
+    // in-kernel window updates (k_part_agg's touched-list entries, the claims
+    // no room check covers); k_seg_apply checks the deferred ones itself
+    const uint64_t grew = d.h_sc->live > live0 ? d.h_sc->live - live0 : 0;
+    const uint64_t dfr = 2 * grew + 2 * d.h_sc->scratch[1];
+    if (how == 3 || how == 4) d.defer_pred = dfr > (1ull << 16) ? dfr : (1ull << 16);
     d.lean_batches += how == 1 || how == 2;
     d.direct_batches += how == 1 || how == 3;
   }

@@ -173,7 +173,10 @@ typedef struct {
    smaller exponent), a MIN / MAX / LAST as its winning value was spelled, an
    aggregate nothing reached as the reference's initial value. Changelog and dump
    rows then carry hsg_rows.form. At most 2 value columns (each is tracked as
-   three internal columns). */
+   three internal columns). One case is decided without arrival order: a MIN /
+   MAX whose value was reached both by an integral and by a decimal literal
+   (7 and 7.0) prints as an integer, where the reference prints the later tied
+   literal for MAX and the earlier for MIN (max n x = x, min n x = n on ties). */
 
 /* One micro-batch in columnar form, records in arrival order.
  *

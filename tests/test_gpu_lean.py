@@ -146,9 +146,8 @@ def test_table_room_holds_and_regrows(eng):
     rng = np.random.default_rng(11)
     t = 10_000_000
     batches = []
-    # (20K keys per uniform batch: a key's windows share its table region,
-    # and a few keys with many windows each could fill one region of a table
-    # at moderate load -- an HSG_E_OOM the sizing does not try to prevent)
+    # (a region filled by a few keys with many windows spills into the
+    # overflow rows: test_gpu_regions.py)
     for nkeys, span, n in [(20_000, 600_000, 300_000),        # ~260K groups >> 1.5K room: lean hold
                            (20_000, 600_000, 300_000),        # inside the prediction
                            (5_000, 2_000_000_000, 100_000),   # > 2^16 windows: wide layout
