@@ -327,16 +327,21 @@ def host_steps(op, keys, ts, cols, pieces, spec, emit, world, args):
             tsa, base, cs2, enc, scale = t, None, cs, [abi.HSG_ENC_FULL] * len(cs), [0] * len(cs)
         else:
             k = narrow_keys(k)
-            tsa, base, cs2, enc, scale = narrow_columns(t, cs, spec.col_types, dec)
+            tsa, base, cs2, enc, scale = narrow_columns(t, cs, spec.col_types, dec, ts16=True)
         pk = torch.from_numpy(np.ascontiguousarray(k)).pin_memory()
         pt = torch.from_numpy(np.ascontiguousarray(tsa)).pin_memory()
         pc = [torch.from_numpy(np.ascontiguousarray(c)).pin_memory() for c in cs2]
+        frames = isinstance(base, np.ndarray)
+        pf = torch.from_numpy(base).pin_memory() if frames else None
         b, keep = make_batch(pk.numpy(), pt.numpy(), [c.numpy() for c in pc], None, abi.HSG_MEM_HOST,
-                             ts_base=base, col_enc=enc, col_scale=scale)
+                             ts_base=None if frames else base, col_enc=enc, col_scale=scale,
+                             ts_frames=pf.numpy() if frames else None)
         descs.append(b)
-        host.append((pk, pt, pc, keep))
+        host.append((pk, pt, pc, pf, keep))
         nbytes += pk.element_size() * m + pt.element_size() * m + sum(c.element_size() * m for c in pc)
-        encs.add(("k16" if pk.element_size() == 2 else "k32") + "+" + ("ts32" if base is not None else "ts64") + "+" + ",".join(
+        nbytes += pf.numel() * 8 if frames else 0
+        tsn = "ts16" if frames else "ts32" if base is not None else "ts64"
+        encs.add(("k16" if pk.element_size() == 2 else "k32") + "+" + tsn + "+" + ",".join(
             {abi.HSG_ENC_FULL: "full", abi.HSG_ENC_I32: "i32", abi.HSG_ENC_DEC32: "dec32"}[e] for e in enc))
     n_rank = sum(m for _, m in pieces)
     wpr = -(-spec.size_ms // spec.advance_ms) if spec.window_kind == abi.HSG_HOPPING else 1

@@ -63,6 +63,8 @@ HSG_ENC_TS32 = 1
 HSG_ENC_I32 = 2
 HSG_ENC_DEC32 = 3
 HSG_ENC_K16 = 4
+HSG_ENC_TS16 = 5
+HSG_TS16_FRAME = 4096
 
 # hsg_op_config.flags
 HSG_OPF_LITERAL_FORMS = 1
@@ -117,6 +119,7 @@ class hsg_batch(C.Structure):
         ("ts_base", C.c_int64),
         ("col_enc", C.c_uint8 * 8),
         ("col_scale", C.c_uint8 * 8),
+        ("ts_frames", C.c_void_p),
     ]
 
 

@@ -76,15 +76,18 @@ def _ptr(x):
     return x.ctypes.data
 
 
-def make_batch(key_id, ts, cols=(), valid=None, mem=None, ts_base=None, col_enc=None, col_scale=None):
+def make_batch(key_id, ts, cols=(), valid=None, mem=None, ts_base=None, col_enc=None, col_scale=None,
+               ts_frames=None):
     """Build an hsg_batch over numpy arrays (host) or torch tensors (device).
 
     Returns (hsg_batch, keepalive). Arrays must be contiguous: key_id uint32 /
     int32, ts int64, cols int64 or float64, valid uint8 (or None = all present).
     Narrow transport (include/hstream_gpu.h hsg_enc): a uint16 key_id = ids sent
     as HSG_ENC_K16 (no HSG_KEY_NONE in the batch); ts_base given = ts holds
-    int32 offsets from it (HSG_ENC_TS32); col_enc[c] HSG_ENC_I32 / HSG_ENC_DEC32
-    = column c holds int32 values / decimal mantissas (col_scale[c] digits).
+    int32 offsets from it (HSG_ENC_TS32); ts_frames given = ts holds uint16
+    offsets from the base of each HSG_TS16_FRAME-record frame (HSG_ENC_TS16);
+    col_enc[c] HSG_ENC_I32 / HSG_ENC_DEC32 = column c holds int32 values /
+    decimal mantissas (col_scale[c] digits).
     """
     if mem is None:
         mem = abi.HSG_MEM_DEVICE if (_is_torch(ts) and ts.is_cuda) else abi.HSG_MEM_HOST
@@ -93,13 +96,17 @@ def make_batch(key_id, ts, cols=(), valid=None, mem=None, ts_base=None, col_enc=
     if not _is_torch(ts):
         key_id = np.asarray(key_id)
         key_id = np.ascontiguousarray(key_id, dtype=np.uint16 if key_id.dtype == np.uint16 else np.uint32)
-        ts = np.ascontiguousarray(ts, dtype=np.int32 if ts_base is not None else np.int64)
+        ts = np.ascontiguousarray(ts, dtype=np.int32 if ts_base is not None else
+                                  np.uint16 if ts_frames is not None else np.int64)
+        if ts_frames is not None:
+            ts_frames = np.ascontiguousarray(ts_frames, dtype=np.int64)
         cols = [np.ascontiguousarray(c, dtype=np.int32) if e != abi.HSG_ENC_FULL else np.ascontiguousarray(c)
                 for c, e in zip(cols, col_enc)]
         if valid is not None:
             valid = [None if v is None else np.ascontiguousarray(v, dtype=np.uint8) for v in valid]
-        keep = [key_id, ts, cols, valid]
+        keep = [key_id, ts, cols, valid, ts_frames]
     else:
+        keep.append(ts_frames)
         keep.append(cols)
         keep.append(valid)
     n = int(ts.shape[0])
@@ -124,6 +131,9 @@ def make_batch(key_id, ts, cols=(), valid=None, mem=None, ts_base=None, col_enc=
     if ts_base is not None:
         b.ts_enc = abi.HSG_ENC_TS32
         b.ts_base = int(ts_base)
+    if ts_frames is not None:
+        b.ts_enc = abi.HSG_ENC_TS16
+        b.ts_frames = _ptr(ts_frames)
     for c, e in enumerate(col_enc):
         b.col_enc[c] = int(e)
         b.col_scale[c] = int(col_scale[c]) if col_scale else 0
@@ -139,16 +149,40 @@ def narrow_keys(key_id):
     return key_id
 
 
-def narrow_columns(ts, cols, col_types, dec_scale=None):
+def narrow_ts16(ts):
+    """ts as HSG_ENC_TS16 (frame of reference): (uint16 offsets, int64 frame
+    bases) when every frame of HSG_TS16_FRAME records spans < 65536 ms, else
+    None."""
+    ts = np.asarray(ts, dtype=np.int64)
+    f = abi.HSG_TS16_FRAME
+    nf = -(-ts.size // f)
+    pad = np.empty(nf * f, np.int64)
+    pad[:ts.size] = ts
+    pad[ts.size:] = ts[-1] if ts.size else 0
+    fr = pad.reshape(nf, f)
+    lo = fr.min(axis=1)
+    if nf and int((fr.max(axis=1) - lo).max()) >= 65536:
+        return None
+    off = (pad - np.repeat(lo, f))[:ts.size].astype(np.uint16)
+    return off, lo
+
+
+def narrow_columns(ts, cols, col_types, dec_scale=None, ts16=False):
     """What a producer that saw every value (the decoder) can send narrower:
-    ts as int32 offsets from the batch's minimum when its span fits, i64
-    columns as int32 when every value fits, f64 columns as int32 decimal
-    mantissas when every value is a decimal of at most dec_scale[c] digits that
-    fits (checked exactly: m / 10^s must give back the value). Returns
-    (ts_arr, ts_base or None, cols, col_enc, col_scale); host numpy arrays."""
+    ts as uint16 offsets from per-frame bases when ts16 and every frame fits
+    (the second result is then the int64 frame bases: make_batch ts_frames),
+    else as int32 offsets from the batch's minimum when its span fits (the
+    second result is that base: make_batch ts_base); i64 columns as int32 when
+    every value fits, f64 columns as int32 decimal mantissas when every value
+    is a decimal of at most dec_scale[c] digits that fits (checked exactly:
+    m / 10^s must give back the value). Returns (ts_arr, ts_base / frames /
+    None, cols, col_enc, col_scale); host numpy arrays."""
     ts = np.asarray(ts, dtype=np.int64)
     ts_base = None
-    if ts.size:
+    t16 = narrow_ts16(ts) if ts16 and ts.size else None
+    if t16 is not None:
+        ts, ts_base = t16
+    elif ts.size:
         lo, hi = int(ts.min()), int(ts.max())
         if hi - lo < 2**31:
             ts_base = lo

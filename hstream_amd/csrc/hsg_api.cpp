@@ -521,8 +521,10 @@ static int validate_batch(hsg_op *op, const hsg_batch *b, const int64_t *inout_w
   if (b->n && (!b->key_id || !b->ts)) return fail(op->err, HSG_E_INVALID, "null key_id / ts");
   for (int c = 0; c < b->n_cols; ++c)
     if (b->n && (!b->cols || !b->cols[c])) return fail(op->err, HSG_E_INVALID, "null value column");
-  // narrow transport (hsg_enc): ts as TS32 only, i64 columns as I32, f64 columns as DEC32
-  if (b->ts_enc != HSG_ENC_FULL && b->ts_enc != HSG_ENC_TS32) return fail(op->err, HSG_E_INVALID, "bad ts_enc");
+  // narrow transport (hsg_enc): ts as TS32 / TS16, i64 columns as I32, f64 columns as DEC32
+  if (b->ts_enc != HSG_ENC_FULL && b->ts_enc != HSG_ENC_TS32 && b->ts_enc != HSG_ENC_TS16)
+    return fail(op->err, HSG_E_INVALID, "bad ts_enc");
+  if (b->ts_enc == HSG_ENC_TS16 && b->n && !b->ts_frames) return fail(op->err, HSG_E_INVALID, "TS16 without ts_frames");
   if (b->key_enc != HSG_ENC_FULL && b->key_enc != HSG_ENC_K16) return fail(op->err, HSG_E_INVALID, "bad key_enc");
   for (int c = 0; c < b->n_cols; ++c) {
     const int e = b->col_enc[c];

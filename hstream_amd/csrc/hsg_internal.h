@@ -273,8 +273,10 @@ struct WidenArgs {
   uint64_t n;
   const uint16_t *k16;           // null: key_id is not narrow
   uint32_t *key;
-  const int32_t *ts32;           // null: ts is not narrow
+  const int32_t *ts32;           // null: ts is not TS32
   int64_t ts_base;
+  const uint16_t *ts16;          // null: ts is not TS16
+  const int64_t *frames;         // TS16: a base per HSG_TS16_FRAME records
   int64_t *ts;
   const int32_t *c32[kMaxCols];  // null: the column is not narrow
   int64_t *col[kMaxCols];        // int64 words (i64 or f64 bits)

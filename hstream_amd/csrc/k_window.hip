@@ -197,6 +197,7 @@ __global__ __launch_bounds__(256) void k_widen(WidenArgs w) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < w.n; i += step) {
     if (w.k16) w.key[i] = (uint32_t)w.k16[i];
     if (w.ts32) w.ts[i] = w.ts_base + (int64_t)w.ts32[i];
+    if (w.ts16) w.ts[i] = w.frames[i / HSG_TS16_FRAME] + (int64_t)w.ts16[i];
 #pragma unroll
     for (int c = 0; c < kMaxCols; ++c) {
       if (!w.c32[c]) continue;  // uniform

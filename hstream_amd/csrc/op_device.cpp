@@ -54,6 +54,16 @@ static void dfree(T *&p) {
   p = nullptr;
 }
 
+// transport bytes of a batch's ts column; TS16 frame bases follow the offsets
+// in the same staging buffer (n * 2 bytes, 256-aligned)
+static uint64_t ts_bytes(const hsg_batch *b) {
+  return b->ts_enc == HSG_ENC_TS32 ? 4 : b->ts_enc == HSG_ENC_TS16 ? 2 : 8;
+}
+static uint64_t ts16_frames(uint64_t n) { return (n + HSG_TS16_FRAME - 1) / HSG_TS16_FRAME; }
+static int64_t *ts16_frames_at(const void *buf, uint64_t n) {
+  return (int64_t *)((char *)buf + ((n * 2 + 255) & ~255ull));
+}
+
 static bool has_last(const Program &prog) {
   for (int s = 0; s < prog.n_slots; ++s)
     if (prog.slot_op[s] == S_LAST_SEQ) return true;
@@ -411,7 +421,9 @@ int op_prestage(OpDevice &d, const hsg_batch *b, int set, std::string &err) {
   // buffers; stage_batch widens them on the op's stream
   if (n) {
     DTRY(hipMemcpyAsync(s.key, b->key_id, n * (b->key_enc == HSG_ENC_K16 ? 2 : 4), k, d.h2d));
-    DTRY(hipMemcpyAsync(s.ts, b->ts, n * (b->ts_enc == HSG_ENC_TS32 ? 4 : 8), k, d.h2d));
+    DTRY(hipMemcpyAsync(s.ts, b->ts, n * ts_bytes(b), k, d.h2d));
+    if (b->ts_enc == HSG_ENC_TS16)
+      DTRY(hipMemcpyAsync(ts16_frames_at(s.ts, n), b->ts_frames, ts16_frames(n) * 8, k, d.h2d));
     for (int c = 0; c < b->n_cols; ++c) {
       DTRY(hipMemcpyAsync(s.col[c], b->cols[c], n * (b->col_enc[c] != HSG_ENC_FULL ? 4 : 8), k, d.h2d));
       if (b->valid && b->valid[c]) DTRY(hipMemcpyAsync(s.valid[c], b->valid[c], n, k, d.h2d));
@@ -422,10 +434,11 @@ int op_prestage(OpDevice &d, const hsg_batch *b, int set, std::string &err) {
 }
 
 // Narrow transport columns (include/hstream_gpu.h hsg_enc) at device
-// addresses k16 / ts32 / c32 (used for the arrays the batch sends narrow)
-// -> the op's full-width staging; kb points there afterwards.
-static int widen_batch(OpDevice &d, const hsg_batch *b, const void *k16, const void *ts32, const void *const *c32,
-                       Batch &kb, std::string &err) {
+// addresses k16 / ts32 / c32 (used for the arrays the batch sends narrow;
+// TS16: offsets at ts32, frame bases at frames) -> the op's full-width
+// staging; kb points there afterwards.
+static int widen_batch(OpDevice &d, const hsg_batch *b, const void *k16, const void *ts32, const int64_t *frames,
+                       const void *const *c32, Batch &kb, std::string &err) {
   WidenArgs w;
   memset(&w, 0, sizeof(w));
   w.n = b->n;
@@ -434,9 +447,14 @@ static int widen_batch(OpDevice &d, const hsg_batch *b, const void *k16, const v
     w.key = d.st_key;
     kb.key = d.st_key;
   }
-  if (b->ts_enc == HSG_ENC_TS32) {
-    w.ts32 = (const int32_t *)ts32;
-    w.ts_base = b->ts_base;
+  if (b->ts_enc == HSG_ENC_TS32 || b->ts_enc == HSG_ENC_TS16) {
+    if (b->ts_enc == HSG_ENC_TS32) {
+      w.ts32 = (const int32_t *)ts32;
+      w.ts_base = b->ts_base;
+    } else {
+      w.ts16 = (const uint16_t *)ts32;
+      w.frames = frames;
+    }
     w.ts = d.st_ts;
     kb.ts = d.st_ts;
   }
@@ -501,7 +519,7 @@ static int stage_batch_raw(OpDevice &d, const hsg_batch *b, Batch &kb, std::stri
     if (batch_narrow(b)) {
       const void *c32[kMaxCols];
       for (int c = 0; c < b->n_cols; ++c) c32[c] = s.col[c];
-      return widen_batch(d, b, s.key, s.ts, c32, kb, err);
+      return widen_batch(d, b, s.key, s.ts, ts16_frames_at(s.ts, n), c32, kb, err);
     }
     return HSG_OK;
   }
@@ -514,7 +532,7 @@ static int stage_batch_raw(OpDevice &d, const hsg_batch *b, Batch &kb, std::stri
       kb.col[c] = (const int64_t *)b->cols[c];
       kb.valid[c] = (b->valid && b->valid[c]) ? b->valid[c] : nullptr;
     }
-    if (batch_narrow(b)) return widen_batch(d, b, b->key_id, b->ts, b->cols, kb, err);
+    if (batch_narrow(b)) return widen_batch(d, b, b->key_id, b->ts, b->ts_frames, b->cols, kb, err);
     return HSG_OK;
   }
   if (batch_narrow(b)) {
@@ -529,8 +547,10 @@ static int stage_batch_raw(OpDevice &d, const hsg_batch *b, Batch &kb, std::stri
     if (n) {
       if (b->key_enc == HSG_ENC_K16) DTRY(hipMemcpyAsync(d.nar_key, b->key_id, n * 2, k, d.stream));
       else DTRY(hipMemcpyAsync(d.st_key, b->key_id, n * 4, k, d.stream));
-      if (b->ts_enc == HSG_ENC_TS32) DTRY(hipMemcpyAsync(d.nar_ts, b->ts, n * 4, k, d.stream));
+      if (b->ts_enc != HSG_ENC_FULL) DTRY(hipMemcpyAsync(d.nar_ts, b->ts, n * ts_bytes(b), k, d.stream));
       else DTRY(hipMemcpyAsync(d.st_ts, b->ts, n * 8, k, d.stream));
+      if (b->ts_enc == HSG_ENC_TS16)
+        DTRY(hipMemcpyAsync(ts16_frames_at(d.nar_ts, n), b->ts_frames, ts16_frames(n) * 8, k, d.stream));
     }
     kb.key = d.st_key;
     kb.ts = d.st_ts;
@@ -544,7 +564,7 @@ static int stage_batch_raw(OpDevice &d, const hsg_batch *b, Batch &kb, std::stri
         kb.valid[c] = d.st_valid[c];
       }
     }
-    return widen_batch(d, b, d.nar_key, d.nar_ts, c32, kb, err);
+    return widen_batch(d, b, d.nar_key, d.nar_ts, ts16_frames_at(d.nar_ts, n), c32, kb, err);
   }
   if (n) {
     DTRY(hipMemcpyAsync(d.st_key, b->key_id, n * 4, hipMemcpyHostToDevice, d.stream));

@@ -112,9 +112,14 @@ enum hsg_enc {
   HSG_ENC_DEC32 = 3, /* an HSG_F64 column sent as int32 decimal mantissas m:
                         value = m / 10^col_scale, the double nearest that decimal,
                         i.e. the double the JSON text of the decimal parses to       */
-  HSG_ENC_K16   = 4  /* key_id only: uint16 ids (a dictionary of <= 65536 keys, and
+  HSG_ENC_K16   = 4, /* key_id only: uint16 ids (a dictionary of <= 65536 keys, and
                         no HSG_KEY_NONE record in the batch)                        */
+  HSG_ENC_TS16  = 5  /* ts only: uint16 offsets from per-frame bases (frame of
+                        reference): record i's ts = ts_frames[i / HSG_TS16_FRAME] +
+                        offset[i]; a poll batch's near-sorted timestamps fit when
+                        every frame of HSG_TS16_FRAME records spans < 65536 ms     */
 };
+#define HSG_TS16_FRAME 4096
 
 typedef struct hsg_engine hsg_engine;
 typedef struct hsg_op hsg_op;
@@ -199,12 +204,15 @@ typedef struct {
   void *ready_event;            /* optional hipEvent_t the op's stream waits on (device
                                    batches); NULL = inputs already complete              */
   /* narrow transport (all zero = the full-width arrays above) */
-  int32_t ts_enc;               /* HSG_ENC_FULL, or HSG_ENC_TS32: `ts` points at int32_t[n]  */
+  int32_t ts_enc;               /* HSG_ENC_FULL, HSG_ENC_TS32 (`ts` points at int32_t[n]) or
+                                   HSG_ENC_TS16 (`ts` points at uint16_t[n], + ts_frames) */
   int32_t key_enc;              /* HSG_ENC_FULL, or HSG_ENC_K16: `key_id` points at uint16_t[n] */
   int64_t ts_base;              /* HSG_ENC_TS32: ts of a record = ts_base + its offset     */
   uint8_t col_enc[8];           /* per value column: HSG_ENC_FULL, HSG_ENC_I32 (HSG_I64
                                    columns) or HSG_ENC_DEC32 (HSG_F64 columns)            */
   uint8_t col_scale[8];         /* HSG_ENC_DEC32: decimal digits after the point, <= 18   */
+  const int64_t *ts_frames;     /* HSG_ENC_TS16: ceil(n / HSG_TS16_FRAME) frame bases (the
+                                   batch's hsg_mem); NULL otherwise                       */
 } hsg_batch;
 
 /* Columnar changelog / state rows. */

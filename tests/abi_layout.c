@@ -13,7 +13,7 @@ int main(void) {
   S(hsg_agg);
   S(hsg_op_config); F(hsg_op_config, size_ms); F(hsg_op_config, grace_ms); F(hsg_op_config, n_cols);
   F(hsg_op_config, col_types); F(hsg_op_config, aggs); F(hsg_op_config, state_capacity); F(hsg_op_config, out_capacity); F(hsg_op_config, flags);
-  S(hsg_batch); F(hsg_batch, key_id); F(hsg_batch, ts); F(hsg_batch, cols); F(hsg_batch, valid); F(hsg_batch, ready_event); F(hsg_batch, key_enc); F(hsg_batch, ts_base); F(hsg_batch, col_enc); F(hsg_batch, col_scale);
+  S(hsg_batch); F(hsg_batch, key_id); F(hsg_batch, ts); F(hsg_batch, cols); F(hsg_batch, valid); F(hsg_batch, ready_event); F(hsg_batch, key_enc); F(hsg_batch, ts_base); F(hsg_batch, col_enc); F(hsg_batch, col_scale); F(hsg_batch, ts_frames);
   S(hsg_rows); F(hsg_rows, key_id); F(hsg_rows, win_start); F(hsg_rows, src_index); F(hsg_rows, aggs); F(hsg_rows, form);
   S(hsg_stats); F(hsg_stats, last_batch_ms); F(hsg_stats, exchange_bytes); F(hsg_stats, touched_total); F(hsg_stats, state_row_bytes); F(hsg_stats, spill_events); F(hsg_stats, grow_events); F(hsg_stats, replays); F(hsg_stats, overflow_rebuilds);
   S(hsg_decoder_config); F(hsg_decoder_config, n_cols); F(hsg_decoder_config, col_fields); F(hsg_decoder_config, col_numeric); F(hsg_decoder_config, literal_forms);

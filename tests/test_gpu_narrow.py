@@ -101,3 +101,46 @@ def test_bad_encodings_refused(eng):
                    None, watermark=-1, ts_base=0, col_enc=enc, col_scale=[2, 2])
         assert ei.value.status == abi.HSG_E_INVALID
     g.close()
+
+
+@pytest.mark.parametrize("mode", ["sync", "async", "device"])
+@pytest.mark.parametrize("name", ["tumbling_batch", "hopping_record"])
+def test_ts16_frames_equal_full_width(eng, name, mode):
+    """HSG_ENC_TS16: uint16 offsets from a base per HSG_TS16_FRAME records
+    (batches of 40 000 records: the last frame is partial), with the other
+    narrow columns, bit-identical to the full-width oracle."""
+    import torch
+    from hstream_amd.columnar import narrow_ts16
+    spec = SPECS[name]
+    g, o = eng.op(spec), pyoracle.OracleOp(spec)
+    f64 = spec.agg_is_f64()
+    wm_o = -1
+    wm_g = C.c_int64(-1)
+    for b in range(3):
+        key, ts, cols, valid = gen_small(90 + b, 40_000, 300, col_types=(abi.HSG_I64, abi.HSG_F64), span=60_000,
+                                         base=3_000_000 + 60_000 * b, very_late=False, neg_frac=0.0)
+        cols[0] = cols[0] // 2
+        t16, frames, c32, enc, scale = narrow_columns(ts, cols, spec.col_types, [None, 3], ts16=True)
+        assert t16.dtype == np.uint16 and frames.size == -(-ts.size // abi.HSG_TS16_FRAME)
+        assert np.array_equal(np.repeat(frames, abi.HSG_TS16_FRAME)[:ts.size] + t16, ts)
+        assert narrow_ts16(ts) is not None
+        wm_o = o.push(key, ts, cols, valid, watermark=wm_o)
+        kw = dict(ts_frames=frames, col_enc=enc, col_scale=scale)
+        if mode == "sync":
+            wm_g.value = g.push(key, t16, c32, valid, watermark=wm_g.value, **kw)
+        elif mode == "async":
+            g.push_async(key, t16, c32, valid, watermark=wm_g, **kw)
+            g.wait()
+        else:
+            d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+            kw["ts_frames"] = d(frames)
+            dv = [d(v) for v in valid]
+            torch.cuda.synchronize()
+            wm_g.value = g.push(d(key.view(np.int32)), d(t16.view(np.int16)), [d(c) for c in c32], dv,
+                                watermark=wm_g.value, mem=abi.HSG_MEM_DEVICE, **kw)
+        assert wm_g.value == wm_o, f"batch {b}: watermark"
+        rows_equal(g.drain(), o.drain(), f64, ordered=spec.emit_mode == abi.HSG_EMIT_PER_RECORD,
+                   what=f"{name} {mode} ts16 changelog {b}")
+    rows_equal(g.dump_state(), o.dump_state(), f64, what=f"{name} {mode} ts16 state")
+    g.close()
+    o.close()

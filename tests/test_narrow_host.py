@@ -41,3 +41,23 @@ def test_make_batch_fields():
     assert b.ts_enc == abi.HSG_ENC_TS32 and b.ts_base == 77 and b.col_enc[0] == abi.HSG_ENC_I32
     b2, _ = make_batch(key, np.arange(4, dtype=np.int64), [np.arange(4, dtype=np.int64)], None, abi.HSG_MEM_HOST)
     assert b2.ts_enc == abi.HSG_ENC_FULL and b2.col_enc[0] == abi.HSG_ENC_FULL
+
+
+def test_ts16_frames():
+    from hstream_amd.columnar import narrow_ts16
+    rng = np.random.default_rng(5)
+    n = 3 * abi.HSG_TS16_FRAME + 17
+    ts = 1_700_000_000_000 + np.arange(n) * 3 + rng.integers(0, 2000, n)
+    off, fr = narrow_ts16(ts)
+    assert off.dtype == np.uint16 and fr.size == 4
+    assert np.array_equal(np.repeat(fr, abi.HSG_TS16_FRAME)[:n] + off.astype(np.int64), ts)
+    # a frame spanning 65536 ms or more: not TS16 (narrow_columns falls back to TS32)
+    ts2 = ts.copy()
+    ts2[5] += 70_000
+    assert narrow_ts16(ts2) is None
+    t, base, _, _, _ = narrow_columns(ts2, [], [], ts16=True)
+    assert t.dtype == np.int32 and isinstance(base, int)
+    t, fr2, _, _, _ = narrow_columns(ts, [], [], ts16=True)
+    assert t.dtype == np.uint16 and np.array_equal(fr2, fr)
+    b, _ = make_batch(np.arange(n, dtype=np.uint32), off, [], None, abi.HSG_MEM_HOST, ts_frames=fr)
+    assert b.ts_enc == abi.HSG_ENC_TS16 and b.ts_frames
