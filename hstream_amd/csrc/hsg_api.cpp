@@ -748,8 +748,10 @@ int op_sink_info(const hsg_op *op, int *device, int *n_aggs, uint32_t *f64_mask,
   for (int j = 0; j < op->prog.n_out; ++j) {
     if (op->prog.out_kind[j] != O_I64) m |= 1u << j;
     if (op->prog.form_kind[j] != F_NONE) fm |= 1u << j;
-    // the reference's initial values: MIN maxBound, MAX minBound, else 0 (Codegen.hs:425-469)
-    ident[j] = op->aggs[j].kind == HSG_MIN ? 1 : op->aggs[j].kind == HSG_MAX ? 2 : 0;
+    // the reference's initial values: SUM Number 0, MIN maxBound, MAX minBound
+    // (Codegen.hs:425-469); -1: an aggregate whose f64 prints exactly
+    const int32_t kd = op->aggs[j].kind;
+    ident[j] = kd == HSG_MIN ? 1 : kd == HSG_MAX ? 2 : kd == HSG_SUM ? 0 : -1;
   }
   *f64_mask = m;
   *form_mask = fm;

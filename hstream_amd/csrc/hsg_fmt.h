@@ -202,10 +202,11 @@ HSG_HD void ryu_d2d(uint64_t ieee_m, uint32_t ieee_e, const Pow5Tables &T, uint6
   e10_out = e10 + removed;
 }
 
-// f64 -> aeson text; returns the length (<= kNumTextMax). ident: map the
-// aggregate identities to the reference's integer initial values (rows
-// without literal forms; with them the sink knows which rows are identities)
-HSG_HD int fmt_f64(double v, const Pow5Tables &T, char *out, bool ident = true) {
+// f64 -> aeson text; returns the length (<= kNumTextMax). ident: the kind of
+// aggregate the value is, for rows without literal forms (with them the sink
+// knows which rows are identities): 0 SUM, 1 MIN, 2 MAX map that aggregate's
+// identity to the reference's integer initial value; -1 prints exactly.
+HSG_HD int fmt_f64(double v, const Pow5Tables &T, char *out, int ident = -1) {
   uint64_t bits;
   memcpy(&bits, &v, 8);
   const bool neg = (bits >> 63) != 0;
@@ -220,12 +221,12 @@ HSG_HD int fmt_f64(double v, const Pow5Tables &T, char *out, bool ident = true) 
   // plainly. Here a SUM no value reached keeps its identity -0.0
   // (slot_identity), a MIN / MAX the f64 image of maxBound (2^63, rounded) /
   // minBound (-2^63).
-  if (ident && bits == 0x8000000000000000ull) {
+  if (ident == 0 && bits == 0x8000000000000000ull) {
     out[0] = '0';
     return 1;
   }
-  if (ident && v == 9223372036854775808.0) return fmt_i64(INT64_MAX, out);
-  if (ident && v == -9223372036854775808.0) return fmt_i64(INT64_MIN, out);
+  if (ident == 1 && v == 9223372036854775808.0) return fmt_i64(INT64_MAX, out);
+  if (ident == 2 && v == -9223372036854775808.0) return fmt_i64(INT64_MIN, out);
   if (ie == 0 && im == 0) return fmt_generic(false, nullptr, 0, 0, out);
   uint64_t m;
   int32_t e;
@@ -262,7 +263,7 @@ HSG_HD int fmt_f64_integral(double v, const Pow5Tables &T, char *out) {
   uint64_t bits;
   memcpy(&bits, &v, 8);
   const uint32_t ie = (uint32_t)((bits >> 52) & 0x7FF);
-  if (ie == 0x7FF) return fmt_f64(v, T, out, false);
+  if (ie == 0x7FF) return fmt_f64(v, T, out);
   uint64_t m;
   int32_t e;
   ryu_d2d(bits & ((1ull << 52) - 1), ie, T, m, e);

@@ -61,9 +61,9 @@ __device__ inline uint32_t member_text(const SinkDev &S, int m, uint64_t i, uint
     const uint32_t fb = (S.form[i] >> (2 * j)) & 3u;
     if (fb & 2u) return (uint32_t)fmt_i64(S.ident[j] == 1 ? INT64_MAX : S.ident[j] == 2 ? INT64_MIN : 0, buf);
     if (fb & 1u) return (uint32_t)(f64 ? fmt_f64_integral(__builtin_bit_cast(double, v), T, buf) : fmt_i64(v, buf));
-    return (uint32_t)(f64 ? fmt_f64(__builtin_bit_cast(double, v), T, buf, false) : fmt_i64_decimal(v, buf));
+    return (uint32_t)(f64 ? fmt_f64(__builtin_bit_cast(double, v), T, buf) : fmt_i64_decimal(v, buf));
   }
-  if (f64) return (uint32_t)fmt_f64(__builtin_bit_cast(double, v), T, buf);
+  if (f64) return (uint32_t)fmt_f64(__builtin_bit_cast(double, v), T, buf, S.ident[j]);
   return (uint32_t)fmt_i64(v, buf);
 }
 

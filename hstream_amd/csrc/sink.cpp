@@ -466,7 +466,7 @@ extern "C" int hsg_format_number(int32_t is_f64, int64_t bits, char *buf, size_t
     const Pow5Tables T{kPow5InvHost, kPow5Host};
     double v;
     memcpy(&v, &bits, 8);
-    n = fmt_f64(v, T, t);
+    n = fmt_f64(v, T, t, is_f64 >= 2 ? is_f64 - 2 : -1);
   } else {
     n = fmt_i64(bits, t);
   }

@@ -40,12 +40,16 @@ def _lib():
     return L
 
 
-def format_number(value, is_f64: bool) -> str:
+def format_number(value, is_f64: bool, agg: str = "") -> str:
+    """hsg_format_number; agg "sum" / "min" / "max": the double of that
+    aggregate in a row without literal forms (its identity prints as the
+    reference's initial value), else printed exactly."""
     L = _lib()
     bits = int(np.array([value], np.float64).view(np.int64)[0]) if is_f64 else int(value)
     buf = C.create_string_buffer(64)
     n = C.c_size_t()
-    rc = L.hsg_format_number(1 if is_f64 else 0, bits, buf, 64, C.byref(n))
+    kind = {"": 1, "sum": 2, "min": 3, "max": 4}[agg] if is_f64 else 0
+    rc = L.hsg_format_number(kind, bits, buf, 64, C.byref(n))
     if rc != abi.HSG_OK:
         raise abi.HStreamGpuError(rc, "hsg_format_number")
     return buf.raw[: n.value].decode()

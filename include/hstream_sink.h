@@ -93,8 +93,11 @@ int  hsg_sink_encode_spelled(hsg_sink *s, const hsg_rows *rows, uint64_t n, cons
  * aliases) of the k-th member written. For tests and hosts that build the
  * same objects. */
 int  hsg_sink_member_order(const char *const *aliases, int32_t n, int32_t *order);
-/* One value's text as the encoder prints it (is_f64: bits is a double's bit
- * pattern, else an int64). *len = text bytes; HSG_E_CAPACITY if cap < *len. */
+/* One value's text as the encoder prints it (is_f64: 0 bits is an int64, 1 a
+ * double's bit pattern printed exactly, 2 / 3 / 4 the double of a SUM / MIN /
+ * MAX aggregate of a row without literal forms, whose identity -0.0 / 2^63 /
+ * -2^63 prints as the reference's initial value 0 / maxBound / minBound).
+ * *len = text bytes; HSG_E_CAPACITY if cap < *len. */
 int  hsg_format_number(int32_t is_f64, int64_t bits, char *buf, size_t cap, size_t *len);
 
 #ifdef __cplusplus

@@ -53,18 +53,20 @@ def generic(d: Decimal) -> str:
     return pre + (s + "0" * E)[:E] + "." + (s[E:] or "0")
 
 
-def ref_f64(v: float) -> str:
+def ref_f64(v: float, agg: str = "") -> str:
     if math.isnan(v) or math.isinf(v):
         return "null"
     # the identities of the f64 slots (a SUM nothing was added to is -0.0 on
     # the device, MIN / MAX +-2^63): the reference's Number 0 / maxBound /
-    # minBound, exponent 0, printed as integers
-    if v == 0.0 and math.copysign(1.0, v) < 0:
+    # minBound, exponent 0, printed as integers; any other value exactly
+    if agg == "sum" and v == 0.0 and math.copysign(1.0, v) < 0:
         return "0"
-    if v == 2.0 ** 63:
+    if agg == "min" and v == 2.0 ** 63:
         return str((1 << 63) - 1)
-    if v == -(2.0 ** 63):
+    if agg == "max" and v == -(2.0 ** 63):
         return str(-(1 << 63))
+    if v == 0.0:
+        return "0.0"  # (a Scientific has no negative zero)
     return generic(Decimal(repr(v)))
 
 
@@ -109,9 +111,13 @@ def test_sink_identity_text():
     """Hand-derived from Codegen.hs:423-461 and aeson's Scientific encoding: a
     group whose decimal field was absent in every record keeps the initial
     values Number 0 / minBound / maxBound (exponent 0), printed as integers."""
-    assert format_number(-0.0, True) == "0"                       # SUM: Number 0
-    assert format_number(-(2.0 ** 63), True) == "-9223372036854775808"  # MAX: minBound :: Int
-    assert format_number(2.0 ** 63, True) == "9223372036854775807"      # MIN: maxBound :: Int
+    assert format_number(-0.0, True, "sum") == "0"                       # SUM: Number 0
+    assert format_number(-(2.0 ** 63), True, "max") == "-9223372036854775808"  # MAX: minBound :: Int
+    assert format_number(2.0 ** 63, True, "min") == "9223372036854775807"      # MIN: maxBound :: Int
+    # the same values as other aggregates (or plain numbers) print exactly
+    for v, agg in ((2.0 ** 63, ""), (2.0 ** 63, "sum"), (2.0 ** 63, "max"), (-(2.0 ** 63), "min"),
+                   (-(2.0 ** 63), ""), (-0.0, "min")):
+        assert format_number(v, True, agg) == ref_f64(v), (v, agg)
 
 
 def test_member_order_restatement():
@@ -201,7 +207,8 @@ def test_sink_records_match_serdes(windowed):
                 mem.append((alias, ktext))
             else:
                 v = rows.aggs[j][i]
-                mem.append((alias, ref_f64(float(v)) if f64[j] else str(int(v))))
+                kind = {abi.HSG_SUM: "sum", abi.HSG_MIN: "min", abi.HSG_MAX: "max"}.get(spec.aggs[j][0], "")
+                mem.append((alias, ref_f64(float(v), kind) if f64[j] else str(int(v))))
         ek, ev = _ref_record(ktext, "k", int(rows.win_start[i]), mem, windowed)
         assert kb == ek, (i, kb, ek)
         assert vb == ev, (i, vb, ev)
