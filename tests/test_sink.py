@@ -333,7 +333,7 @@ def test_sink_literal_forms_and_key_spellings():
     recs, vals, ts = [], [], []
     for i in range(3000):
         kt, x, v = rng.choice(keylits), rng.choice(xlits), rng.choice(vlits)
-        t = 1_000_000 + 7 * i
+        t = 1_000_000 + 200 * i  # ~3-4 records per (key, window): few cross-form ties
         recs.append((kt, t, x, v))
         body = '{"k":' + kt + ',"v":' + v + ("" if x is None else ',"x":' + x) + "}"
         vals.append(body.encode())
