@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--copy-drain", action="store_true", help="drain by copy instead of the registered changelog")
     p.add_argument("--no-hbm", action="store_true", help="skip the HBM-resident block (host headline only)")
     p.add_argument("--no-per-record", action="store_true", help="skip the per-record (EMIT CHANGES) block")
+    p.add_argument("--state-capacity", type=int, default=0,
+                   help="hsg_op_config state_capacity (default 0: the engine sizes the table itself)")
     p.add_argument("--extra-steps", type=int, default=3, help="timed steps of the hbm_resident / per_record blocks")
     return p.parse_args()
 
@@ -106,7 +108,7 @@ def main():
     # state_capacity = 0), as a query with no cardinality hint; sessions: an
     # arena for at most one session per record
     groups = n_rank * world if cfg.window_kind == abi.HSG_SESSION else 0
-    spec = cfg.spec(emit, state_capacity=groups)
+    spec = cfg.spec(emit, state_capacity=args.state_capacity or groups)
     op = eng.op(spec)
 
     # synthetic input: this rank's slice of every step, drawn into HBM; every
@@ -234,7 +236,8 @@ def main():
                        "batch": batch, "keys": cfg.keys, "emit": args.emit,
                        "input": ("pinned host batches, H2D in the timed region (BASELINE.md reporting formula)"
                                  if args.input == "host" else "HBM-resident device columns"),
-                       "parallelism": f"key-hash sharded x{world}" if world > 1 else "single GPU"},
+                       "parallelism": f"key-hash sharded x{world}" if world > 1 else "single GPU",
+                       **({"state_capacity": args.state_capacity} if args.state_capacity else {})},
             "roofline": roof,
             "input_link": link,
             "cpu_baseline": cpu,
@@ -308,7 +311,7 @@ def host_steps(op, keys, ts, cols, pieces, spec, emit, world, args):
     encoding (columnar.narrow_columns) is chosen here, before any timing, as a
     decoder chooses it while decoding. The changelog goes into device columns
     registered for a group of batches and is drained after the group; a group
-    is the whole step unless the step's worst-case rows exceed 16 GB of HBM
+    is the whole step unless the step's worst-case rows exceed 96 GB of HBM
     (an asynchronous queue cannot be drained mid-way)."""
     import ctypes as C
     import numpy as np
@@ -350,15 +353,13 @@ def host_steps(op, keys, ts, cols, pieces, spec, emit, world, args):
     state = {"cap": 0, "group": len(descs), "drain": None, "outs": None}
 
     def plan():
-        # rows the library reserves per batch (op_push): n * ranks * wpr, per-batch
-        # mode capped by the table's slots
+        # rows the library reserves per batch (op_push): n * ranks * wpr (per-batch
+        # mode: capped by the table's capacity at the push, which the batches of
+        # a step may grow, so the plan takes the uncapped worst case)
         per = [m * world * wpr for _, m in pieces]
-        if emit == abi.HSG_EMIT_PER_BATCH and spec.window_kind != abi.HSG_SESSION:
-            slots = max(1, int(op.stats()["table_slots"])) + max(64, int(op.stats()["table_slots"]) // 8)
-            per = [min(x, slots) for x in per]
         if emit == abi.HSG_EMIT_NONE:
             return 1, len(descs)
-        budget = 16 << 30
+        budget = min(96 << 30, int(0.4 * torch.cuda.get_device_properties(dev).total_memory))
         g = len(descs)
         while g > 1 and max(per) * g * row_bytes > budget:
             g -= 1

@@ -30,7 +30,10 @@ struct PrBuffers {
 // (k_prpart.hip). Pairs = (record, accepted window); "bucket-major pair
 // position" = the record's index in the partitioned array x wpr + window.
 constexpr int kPrPairs = 2048;         // pairs per k_pr_local chunk (its LDS sort)
-constexpr int kPrEmitRecs = 16384;     // arrival-order records per k_pr_emit workgroup (4 partition tiles)
+#ifndef HSG_PR_EMIT_RECS
+#define HSG_PR_EMIT_RECS 16384  // (a build-time constant; tools/dbg/ab.py builds variants)
+#endif
+constexpr int kPrEmitRecs = HSG_PR_EMIT_RECS;  // arrival-order records per k_pr_emit workgroup (default: 4 partition tiles)
 struct PrPart {
   uint32_t *tpairs;   // [tiles] accepted pairs of each partition tile (the histogram pass)
   uint64_t *tpoff;    // [tiles] exclusive prefix of tpairs: the tile's first changelog row

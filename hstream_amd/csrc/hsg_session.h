@@ -43,6 +43,7 @@ enum SessMeta : int {
   M_FAIL = 3,       // a workgroup could not reserve arena rows (the host compacts, then resumes)
   M_TLEN = 4,       // merge path: touched-list entries this batch
   M_BIG = 7,        // merge path: buckets left to k_ss_merge_big
+  M_RELOC = 8,      // merge path: relocated lists whose prefix k_ss_reloc_copy still copies
   M_SCRATCH = 15,   // device landing word (compaction total)
   M_RNEED = 16,                              // [kArenaRegions] replay path: rows its list growth needs
   M_RTOP = M_RNEED + kArenaRegions,          // [kArenaRegions x kRegionStride] region bump pointers
@@ -92,7 +93,8 @@ struct SessPart {
   uint32_t *touched;   // [n] key slots rewritten by k_ss_merge_big (one entry per chunk and key)
   uint64_t *bigmask;   // [nb] sub-buckets left to k_ss_merge_big
   uint64_t *sdone;     // [nb] sub-buckets k_ss_fuse applied (~0: the whole bucket; resumable)
-  uint16_t *sidx;      // [n] per bucket: its record indices grouped by sub-bucket
+  uint64_t *srec;      // [n][words] per bucket: its records grouped by sub-bucket
+  uint64_t *reloc;     // [n][3] relocated lists (old row, new row, rows of the prefix to copy)
 };
 // bshift: owner bits of the key hash above the bucket bits (multi-GPU)
 void launch_ss_phist(hipStream_t s, const Batch &b, int np_log2, int bshift, uint64_t tiles, const SessPart &sp);
@@ -106,6 +108,9 @@ void launch_ss_fuse(hipStream_t s, const SessParams &p, const SessTable &t, cons
                     int bshift, int words, const SessPart &sp, OutCols out, uint64_t out_base, DevScalars *sc);
 void launch_ss_merge_big(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, int np_log2,
                          int bshift, int words, const SessPart &sp, DevScalars *sc);
+// the prefixes of the lists k_ss_fuse relocated (sp.reloc, t.meta[M_RELOC]
+// entries), copied after it and before anything reads those lists
+void launch_ss_reloc_copy(hipStream_t s, const SessTable &t, const SessPart &sp, uint64_t n_bound);
 // per-batch changelog of the keys k_ss_merge_big touched (emit = 0: count only)
 void launch_ss_emit(hipStream_t s, const SessTable &t, const Program &prog, const SessPart &sp, uint32_t batch_id,
                     int emit, uint64_t n_bound, OutCols out, uint64_t out_base, DevScalars *sc);

@@ -529,11 +529,12 @@ __device__ inline bool seg_claim_insert(uint32_t *cset, uint32_t slot) {
   return false;
 }
 
-__device__ inline int64_t tw_claim_seg(const TwTable &t, uint64_t g, uint32_t *cset, uint32_t &fresh) {
+__device__ inline int64_t tw_claim_seg(const TwTable &t, uint64_t g, uint32_t *cset, uint32_t &fresh,
+                                       uint64_t skip = 0) {
   const uint64_t base = tw_region_base(t, g);
-  uint64_t s = tw_home_in(t, g);
   const uint64_t step = tw_step(t), n = (t.rmask + 1) / step;
-  for (uint64_t probe = 0; probe < n && probe < kMaxProbes; ++probe) {
+  uint64_t s = (tw_home_in(t, g) + skip * step) & t.rmask;
+  for (uint64_t probe = skip; probe < n && probe < kMaxProbes; ++probe) {
     const uint64_t cur = __hip_atomic_load(t.key(base + s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cur == g) return (int64_t)(base + s);
     if (cur == kEmpty && seg_claim_insert(cset, (uint32_t)(base + s))) {
@@ -633,15 +634,26 @@ __global__ __launch_bounds__(kSegNT) void k_seg_apply(Program prog, TwParams p, 
 #pragma unroll
         for (int s = 0; s < MS; ++s) v[u][s] = (q < cnt && s < ns) ? (int64_t)ent[1 + s] : 0;
       }
-      // home probes of all SU groups, then their claims (a collision takes the full probe)
-      uint64_t hs[SU], kh[SU];
+      // the first NP probe positions of all SU groups loaded together (the
+      // table runs at up to 3/4 load, where a linear probe often needs more
+      // than its home: one round trip instead of one per probe), then
+      // resolved in probe order: the group, or the first empty slot claimed
+      // through the LDS claim set; past NP positions the full probe
+      constexpr int NP = 4;
+      uint64_t hb[SU], hh[SU], kh[SU][NP];
+      const uint64_t pstep = tw_step(t);
 #pragma unroll
       for (int u = 0; u < SU; ++u) {
-        hs[u] = 0;
-        kh[u] = kEmpty;
+        hb[u] = hh[u] = 0;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) kh[u][j] = ~kEmpty;
         if (g[u] != kEmpty && lds_claim) {
-          hs[u] = tw_region_base(t, g[u]) + tw_home_in(t, g[u]);
-          kh[u] = __hip_atomic_load(t.key(hs[u]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          hb[u] = tw_region_base(t, g[u]);
+          hh[u] = tw_home_in(t, g[u]);
+#pragma unroll
+          for (int j = 0; j < NP; ++j)
+            kh[u][j] = __hip_atomic_load(t.key(hb[u] + ((hh[u] + j * pstep) & t.rmask)), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
         }
       }
       int64_t slot[SU];
@@ -652,17 +664,25 @@ __global__ __launch_bounds__(kSegNT) void k_seg_apply(Program prog, TwParams p, 
         isnew[u] = false;
         if (g[u] == kEmpty) continue;
         const uint32_t f0 = fresh;
-        if (lds_claim && kh[u] == g[u]) {
-          slot[u] = (int64_t)hs[u];
-        } else if (lds_claim && kh[u] == kEmpty && seg_claim_insert(cset, (uint32_t)hs[u])) {
-          *t.key(hs[u]) = g[u];
-          t.mark(hs[u]);
-          fresh += 1;
-          slot[u] = (int64_t)hs[u];
+        if (lds_claim) {
+#pragma unroll
+          for (int j = 0; j < NP; ++j) {
+            if (slot[u] >= 0) break;
+            const uint64_t pos = hb[u] + ((hh[u] + j * pstep) & t.rmask);
+            if (kh[u][j] == g[u]) {
+              slot[u] = (int64_t)pos;
+            } else if (kh[u][j] == kEmpty && seg_claim_insert(cset, (uint32_t)pos)) {
+              // (a failed claim: a peer took the slot for another group, since
+              // a group is in one entry of a segment; the probe goes on)
+              *t.key(pos) = g[u];
+              t.mark(pos);
+              fresh += 1;
+              slot[u] = (int64_t)pos;
+            }
+          }
+          if (slot[u] < 0) slot[u] = tw_claim_seg(t, g[u], cset, fresh, NP);
         } else {
-          slot[u] = lds_claim     ? tw_claim_seg(t, g[u], cset, fresh)
-                    : plain_claim ? tw_claim_exclusive(t, g[u], fresh)
-                                  : tw_find_or_insert(t, g[u], fresh);
+          slot[u] = plain_claim ? tw_claim_exclusive(t, g[u], fresh) : tw_find_or_insert(t, g[u], fresh);
         }
         isnew[u] = fresh != f0;
       }

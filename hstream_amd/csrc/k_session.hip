@@ -875,9 +875,10 @@ __device__ inline void ss_entry_commit(SessKey &ke, uint64_t off, uint32_t len, 
 template <int MS, class RS, class PV>
 __device__ __attribute__((always_inline)) inline void mg_apply(const PV &prog, const SessTable &t, int64_t gap, const RS &rs, uint32_t ra,
                                 uint32_t rb, const SessKey &e, bool fast, uint64_t i0, uint64_t dst, bool reloc,
-                                uint32_t batch_id, EmitSink *sink = nullptr, SessKey *mirror = nullptr) {
+                                uint32_t batch_id, EmitSink *sink = nullptr, SessKey *mirror = nullptr,
+                                bool prefix_copied = false) {
   const int ns = prog.n();
-  if (reloc)
+  if (reloc && !prefix_copied)
     for (uint64_t k = 0; k < i0; ++k) ss_copy(t, dst + k, t, e.off + k);
   MgTail<MS> tail;
   if (fast) {
@@ -942,7 +943,7 @@ struct FuseLds {
   uint32_t subcnt[1 << kSoMaxSubLog2];
   uint32_t suboff[1 << kSoMaxSubLog2];  // first entry of each sub-bucket in the bucket's index list
   uint32_t ngrp, maxseg;
-  uint64_t abase, obase;
+  uint64_t abase, obase, rbase;
   int fail;
 };
 
@@ -1035,12 +1036,12 @@ __device__ inline int64_t ss_resolve(const SessTable &t, uint32_t key, uint64_t 
   return -1;
 }
 
-// block exclusive scan of one u64 per thread (two barriers)
+// block exclusive scan of one u64 per thread (one LDS barrier)
 __device__ inline uint64_t fu_scan64(uint64_t *red, uint64_t v, uint64_t &total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint64_t incl = wave_incl_sum(v);
   if (lane == 63) red[wv] = incl;
-  __syncthreads();
+  lds_barrier();
   uint64_t before = 0;
   total = 0;
   for (int k = 0; k < kSoNT / 64; ++k) {
@@ -1056,6 +1057,14 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
   __shared__ FuseLds<W> L;
   const ProgView<SIG> pv(prog);  // the common aggregate sets: slot ops baked in
   constexpr int B = 8;  // loads in flight per thread in the bucket passes
+  uint64_t ck = phase_clock(), c_idx = 0, c_ins = 0, c_lds = 0, c_plan = 0, c_res = 0, c_app = 0;
+  auto lap = [&](uint64_t &acc) {
+    if constexpr (kPhaseClocks) {
+      const uint64_t c = phase_clock();
+      acc += c - ck;
+      ck = c;
+    }
+  };
   const uint32_t b = blockIdx.x;
   const uint64_t r0 = sp.bstart[b], r1 = sp.bstart[b + 1];
   const uint64_t m = r1 - r0;
@@ -1068,9 +1077,8 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
   const uint64_t *recs = sp.rec + r0 * W;
   const int sl = ss_sub_log2(m), hs = bshift + np_log2;
   const int nsub = 1 << sl;
-  // the bucket's record indices grouped by sub-bucket (sp.sidx, the bucket's
-  // own range): every later pass visits only its sub-bucket's records
-  uint16_t *sidx = sp.sidx + r0;
+  // the bucket's records copied grouped by sub-bucket (sp.srec, the bucket's
+  // own range): a sub-bucket then reads its records contiguously
   if (threadIdx.x < (1 << kSoMaxSubLog2)) L.subcnt[threadIdx.x] = 0;
   __syncthreads();
   const bool indexable = m < 65536;
@@ -1114,30 +1122,40 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
   __syncthreads();
   if (threadIdx.x < (1 << kSoMaxSubLog2)) L.subcnt[threadIdx.x] = 0;
   __syncthreads();
+  uint64_t *srec = sp.srec + r0 * W;
+  constexpr int B2 = W <= 3 ? 4 : 2;  // records in flight per thread in the copy pass
   if (indexable)
-    for (uint64_t i0 = 0; i0 < m; i0 += (uint64_t)kSoNT * B) {
-      uint32_t q[B];
+    for (uint64_t i0 = 0; i0 < m; i0 += (uint64_t)kSoNT * B2) {
+      uint64_t v[B2][W];
 #pragma unroll
-      for (int u = 0; u < B; ++u) {
+      for (int u = 0; u < B2; ++u) {
         const uint64_t i = i0 + (uint64_t)u * kSoNT + threadIdx.x;
-        q[u] = i < m ? ss_sub((uint32_t)recs[i * W], hs, sl) : ~0u;
+#pragma unroll
+        for (int w = 0; w < W; ++w) v[u][w] = i < m ? recs[i * W + w] : 0;
       }
 #pragma unroll
-      for (int u = 0; u < B; ++u) {
-        const bool in = q[u] != ~0u;
-        const uint64_t pm = peers(q[u], in);
+      for (int u = 0; u < B2; ++u) {
+        const uint64_t i = i0 + (uint64_t)u * kSoNT + threadIdx.x;
+        const uint32_t q = i < m ? ss_sub((uint32_t)v[u][0], hs, sl) : ~0u;
+        const bool in = q != ~0u;
+        const uint64_t pm = peers(q, in);
         const uint32_t rk = (uint32_t)__popcll(pm & lt);
         // the group's lowest lane reserves for the group; the others read its base
         uint32_t base = 0;
-        if (in && rk == 0) base = atomicAdd(&L.subcnt[q[u]], (uint32_t)__popcll(pm));
+        if (in && rk == 0) base = atomicAdd(&L.subcnt[q], (uint32_t)__popcll(pm));
         const int leader = in ? __ffsll((long long)pm) - 1 : lane0;
         base = __shfl(base, leader, 64);
-        if (in) sidx[L.suboff[q[u]] + base + rk] = (uint16_t)(i0 + (uint64_t)u * kSoNT + threadIdx.x);
+        if (in) {
+          uint64_t *d = srec + (uint64_t)(L.suboff[q] + base + rk) * W;
+#pragma unroll
+          for (int w = 0; w < W; ++w) d[w] = v[u][w];
+        }
       }
     }
   __syncthreads();
   uint64_t bigmask = indexable ? 0ull : ~0ull;  // a bucket that cannot be indexed goes to the big path whole
   bool failed = false;
+  lap(c_idx);
   int64_t live_delta = 0;
   uint64_t keys_new = 0;
   uint32_t err = 0;
@@ -1152,7 +1170,7 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
       continue;
     }
     if (((sdone >> sub) & 1ull) || failed) continue;  // applied by an earlier launch / after a failed reservation
-    const uint16_t *lst = sidx + L.suboff[sub];
+    const uint64_t *lst = srec + (uint64_t)L.suboff[sub] * W;
     // 1. keys of the sub-bucket into the LDS table, records per key; the
     // records' words stay in registers for the placement
     for (int h = threadIdx.x; h < kSoTab; h += kSoNT) {
@@ -1164,9 +1182,8 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
 #pragma unroll
     for (int u = 0; u < RP; ++u) {
       const uint32_t j = u * kSoNT + threadIdx.x;
-      const uint64_t i = j < m2 ? lst[j] : 0;
 #pragma unroll
-      for (int w = 0; w < W; ++w) rw[u][w] = j < m2 ? recs[i * W + w] : 0;
+      for (int w = 0; w < W; ++w) rw[u][w] = j < m2 ? lst[(uint64_t)j * W + w] : 0;
     }
     lds_barrier();
     uint32_t hslot[RP];
@@ -1192,6 +1209,7 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
       atomicAdd(&L.tcnt[h], 1u);
     }
     lds_barrier();
+    lap(c_ins);
     // 2. segment starts: exclusive scan of the counts
     // (records in the low 16 bits, occupied slots in the high: one scan gives
     // each key its segment start and its group index)
@@ -1234,6 +1252,14 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
     }
     if (threadIdx.x == 0) L.ngrp = all >> 16;
     lds_barrier();
+    // the key entries of this thread's groups (tid and tid + NT), loaded at
+    // their home slots now so the loads are in flight during the placement
+    // and the ranking
+    const uint32_t ngrp = L.ngrp;
+    const uint32_t ga = threadIdx.x, gb = kSoNT + threadIdx.x;
+    SessKey ea = ss_blank(0), eb = ss_blank(0);
+    if (ga < ngrp) ea = ss_load_entry(&t.kt[ss_home(t, L.tkey[L.gslot[ga]])]);
+    if (gb < ngrp) eb = ss_load_entry(&t.kt[ss_home(t, L.tkey[L.gslot[gb]])]);
     // 3. place (ts, words) in the key's segment
 #pragma unroll
     for (int u = 0; u < RP; ++u) {
@@ -1259,17 +1285,12 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
       L.perm[sa + rank] = (uint16_t)q;
     }
     lds_barrier();
+    lap(c_lds);
     // 5. plan every key group (thread owns groups tid and tid + NT; the second
     // is re-planned from its reloaded entry when it is applied, so only the
-    // first group's plan is held in registers): the home entries of both
-    // loaded together, then resolved
-    const uint32_t ngrp = L.ngrp;
-    const uint32_t ga = threadIdx.x, gb = kSoNT + threadIdx.x;
-    SessKey ea = ss_blank(0), eb = ss_blank(0);
-    if (ga < ngrp) ea = ss_load_entry(&t.kt[ss_home(t, L.tkey[L.gslot[ga]])]);
-    if (gb < ngrp) eb = ss_load_entry(&t.kt[ss_home(t, L.tkey[L.gslot[gb]])]);
+    // first group's plan is held in registers): the home entries resolved
     int64_t sla = -1, slb = -1;
-    uint64_t i0a = 0;
+    uint64_t i0a = 0, i0b = 0, offb = 0;
     uint32_t Ma = 0, capa = 0, fra = 0, capb = 0, frb = 0;
     bool fasta = false;
     uint64_t need = 0, nem = 0;
@@ -1295,58 +1316,86 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
       if (slb < 0) err |= ERR_OOM;
       else {
         keys_new += ins ? 1 : 0;
-        uint64_t i0b;
         uint32_t Mb;
         mg_plan<MS>(pv, t, p.gap, rs, ra, rb, eb, mg_fast(rs, ra, eb), p.batch_id, i0b, Mb, capb, &frb);
+        offb = eb.off;
         need += capb;
         nem += frb;
       }
     }
-    // 6. one arena and one changelog reservation for the sub-bucket
-    uint64_t tneed, tnem;
+    lap(c_plan);
+    // 6. one arena, one changelog and one relocation-list reservation for the
+    // sub-bucket (changelog rows in the low 32 bits of one scan, relocated
+    // lists in the high)
+    const uint32_t nrel = (sla >= 0 && capa && i0a ? 1u : 0u) + (slb >= 0 && capb && i0b ? 1u : 0u);
+    uint64_t tneed, tpk;
     const uint64_t nbefore = fu_scan64(L.red[0], need, tneed);
-    const uint64_t ebefore = fu_scan64(L.red[1], nem, tnem);
+    const uint64_t pbefore = fu_scan64(L.red[1], nem | ((uint64_t)nrel << 32), tpk);
+    const uint64_t ebefore = pbefore & 0xFFFFFFFFull, tnem = tpk & 0xFFFFFFFFull;
     if (threadIdx.x == 0) {
       uint64_t base = 0;
       const int fail = tneed ? !arena_take(t, arena_region(b), tneed, base) : 0;
       L.fail = fail;
       L.abase = base;
       L.obase = 0;
-      if (fail) atomicOr((unsigned int *)&t.meta[M_FAIL], 1u);
-      else if (tnem) {
-        // per-batch mode: touched = rows (the host takes it from out_rows)
-        if (emit_batch) L.obase = atomicAdd((unsigned long long *)&sc->out_rows, (unsigned long long)tnem);
-        else atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)tnem);
+      L.rbase = 0;
+      if (fail) {
+        atomicOr((unsigned int *)&t.meta[M_FAIL], 1u);
+      } else {
+        if (tnem) {
+          // per-batch mode: touched = rows (the host takes it from out_rows)
+          if (emit_batch) L.obase = atomicAdd((unsigned long long *)&sc->out_rows, (unsigned long long)tnem);
+          else atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)tnem);
+        }
+        if (tpk >> 32) L.rbase = atomicAdd((unsigned long long *)&t.meta[M_RELOC], (unsigned long long)(tpk >> 32));
       }
     }
-    __syncthreads();
+    lds_barrier();
+    lap(c_res);
     if (L.fail) {  // uniform: this sub-bucket and the rest stay for the next launch (inserted keys stay)
       failed = true;
-      __syncthreads();
+      lds_barrier();
       continue;
     }
-    // 7. merge, write the sessions, the changelog rows and the entry
-    uint64_t adst = L.abase + nbefore;
+    // 7. relocated lists: the prefix [0, i0) their merge leaves untouched is
+    // copied after this kernel (k_ss_reloc_copy, every row of every list in
+    // parallel), not by the key's thread row by row: a sub-bucket waits at
+    // its barrier for its slowest key, and ~1 key in 12 per C4 batch outgrows
+    // its rows. Nothing reads those rows before the copy (a key is in one
+    // sub-bucket; compaction and the next batch come after it).
+    const uint64_t dsta = capa ? L.abase + nbefore : 0, dstb = capb ? L.abase + nbefore + capa : 0;
+    {
+      uint64_t rp = L.rbase + (pbefore >> 32);
+      if (sla >= 0 && capa && i0a) {
+        uint64_t *e = sp.reloc + 3 * rp++;
+        e[0] = ea.off;
+        e[1] = dsta;
+        e[2] = i0a;
+      }
+      if (slb >= 0 && capb && i0b) {
+        uint64_t *e = sp.reloc + 3 * rp;
+        e[0] = offb;
+        e[1] = dstb;
+        e[2] = i0b;
+      }
+    }
+    // 8. merge, write the sessions, the changelog rows and the entry
     uint64_t opos = out_base + L.obase + ebefore;
     auto apply = [&](uint32_t g, int64_t slot, const SessKey &e, bool fast, uint64_t i0, uint32_t M, uint32_t cap,
-                     uint32_t fr) {
+                     uint32_t fr, uint64_t rdst) {
       const uint32_t h = L.gslot[g];
       const uint32_t key = L.tkey[h], ra = L.tstart[h], rb = L.tcnt[h];
       const bool reloc = cap != 0;
-      uint64_t dst = e.off;
-      if (reloc) {
-        dst = adst;
-        adst += cap;
-      }
+      const uint64_t dst = reloc ? rdst : e.off;
       EmitSink sink{out, emit_batch ? opos : ~0ull, key, 0, &prog};
       if (emit_batch) opos += fr;
       SessKey ne = e;
-      mg_apply<MS>(pv, t, p.gap, rs, ra, rb, e, fast, i0, dst, reloc, p.batch_id, &sink, &ne);
+      mg_apply<MS>(pv, t, p.gap, rs, ra, rb, e, fast, i0, dst, reloc, p.batch_id, &sink, &ne, true);
       ss_entry_commit(ne, dst, (uint32_t)(i0 + M), reloc ? cap : 0u);
       ss_store_entry(&t.kt[slot], ne);
       live_delta += (int64_t)M - (int64_t)(e.len - i0);
     };
-    if (sla >= 0) apply(ga, sla, ea, fasta, i0a, Ma, capa, fra);
+    if (sla >= 0) apply(ga, sla, ea, fasta, i0a, Ma, capa, fra, dsta);
     if (slb >= 0) {
       // the entry as planned (no other thread writes it): the same plan again
       const SessKey e = ss_load_entry(&t.kt[slb]);
@@ -1356,10 +1405,22 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
       uint64_t i0;
       uint32_t M, cap;
       mg_plan<MS>(pv, t, p.gap, rs, ra, rb, e, fast, p.batch_id, i0, M, cap);
-      apply(gb, slb, e, fast, i0, M, capb, frb);
+      apply(gb, slb, e, fast, i0, M, capb, frb, dstb);
     }
     sdone |= 1ull << sub;
-    __syncthreads();  // the next sub-bucket reuses the LDS
+    // the next sub-bucket reuses the LDS only: its keys, rows and changelog
+    // positions are not this one's, so its stores need not have landed
+    lds_barrier();
+    lap(c_app);
+  }
+  if (kPhaseClocks && threadIdx.x == 0) {  // phase clocks (100 MHz), PHASES=1 builds with HSG_PHASES set
+    atomicAdd((unsigned long long *)&sc->scratch[24], (unsigned long long)c_idx);
+    atomicAdd((unsigned long long *)&sc->scratch[25], (unsigned long long)c_ins);
+    atomicAdd((unsigned long long *)&sc->scratch[26], (unsigned long long)c_lds);
+    atomicAdd((unsigned long long *)&sc->scratch[27], (unsigned long long)c_plan);
+    atomicAdd((unsigned long long *)&sc->scratch[28], (unsigned long long)c_res);
+    atomicAdd((unsigned long long *)&sc->scratch[29], (unsigned long long)c_app);
+    atomicAdd((unsigned long long *)&sc->scratch[30], 1ull);
   }
   {
     const int lane = threadIdx.x & 63;
@@ -1392,7 +1453,10 @@ static void fuse_launch_w(hipStream_t s, int words, dim3 g, const SessParams &p,
     case 4: HSG_FUSE(4, 0); break;
     case 5: HSG_FUSE(5, 0); break;
     case 6: HSG_FUSE(6, 0); break;
-    default: HSG_FUSE(kSessMaxWords, 0); break;
+    case 7: HSG_FUSE(7, 0); break;
+    case 8: HSG_FUSE(8, 0); break;
+    case 9: HSG_FUSE(9, 0); break;
+    default: HSG_FUSE(kSessMaxWords, 0); break;  // (the partition's record stride: 2 + columns)
   }
 #undef HSG_FUSE
 }
@@ -1410,6 +1474,40 @@ void launch_ss_fuse(hipStream_t s, const SessParams &p, const SessTable &t, cons
   else if (prog.n_slots <= 2) fuse_launch_w<2, 0>(s, words, g, p, t, prog, np_log2, bshift, sp, out, out_base, sc);
   else if (prog.n_slots <= 4) fuse_launch_w<4, 0>(s, words, g, p, t, prog, np_log2, bshift, sp, out, out_base, sc);
   else fuse_launch_w<8, 0>(s, words, g, p, t, prog, np_log2, bshift, sp, out, out_base, sc);
+}
+
+// the prefixes of relocated lists: 16 lanes per list on consecutive words
+// (four loads in flight each; a list is ~10-60 rows of 3 + slots words)
+constexpr int kRcLanes = 16;
+__global__ __launch_bounds__(256) void k_ss_reloc_copy(SessTable t, SessPart sp) {
+  const uint64_t n = t.meta[M_RELOC];
+  const int lane = threadIdx.x & (kRcLanes - 1);
+  const uint64_t w0 = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kRcLanes;
+  const uint64_t nw_all = ((uint64_t)gridDim.x * blockDim.x) / kRcLanes;
+  const uint32_t sw = t.stride;
+  for (uint64_t e = w0; e < n; e += nw_all) {
+    const uint64_t src = sp.reloc[3 * e] * sw, dst = sp.reloc[3 * e + 1] * sw, nw = sp.reloc[3 * e + 2] * sw;
+    for (uint64_t b = 0; b < nw; b += 4 * kRcLanes) {
+      uint64_t v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint64_t w = b + (uint64_t)j * kRcLanes + lane;
+        v[j] = w < nw ? t.rows[src + w] : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint64_t w = b + (uint64_t)j * kRcLanes + lane;
+        if (w < nw) t.rows[dst + w] = v[j];
+      }
+    }
+  }
+}
+
+void launch_ss_reloc_copy(hipStream_t s, const SessTable &t, const SessPart &sp, uint64_t n_bound) {
+  uint64_t blocks = (n_bound / 4 * kRcLanes + 255) / 256;  // (lists: at most one per key)
+  if (blocks > 8192) blocks = 8192;
+  if (!blocks) blocks = 1;
+  hipLaunchKernelGGL(k_ss_reloc_copy, dim3((unsigned)blocks), dim3(256), 0, s, t, sp);
 }
 
 // ---------------------------------------------------------------------------
@@ -1699,6 +1797,11 @@ static void big_launch_w(hipStream_t s, int words, dim3 g, const SessParams &p, 
     case 2: hipLaunchKernelGGL((k_ss_merge_big<MS, 2>), g, th, 0, s, p, t, prog, nl, bs, sp, sc); break;
     case 3: hipLaunchKernelGGL((k_ss_merge_big<MS, 3>), g, th, 0, s, p, t, prog, nl, bs, sp, sc); break;
     case 4: hipLaunchKernelGGL((k_ss_merge_big<MS, 4>), g, th, 0, s, p, t, prog, nl, bs, sp, sc); break;
+    case 5: hipLaunchKernelGGL((k_ss_merge_big<MS, 5>), g, th, 0, s, p, t, prog, nl, bs, sp, sc); break;
+    case 6: hipLaunchKernelGGL((k_ss_merge_big<MS, 6>), g, th, 0, s, p, t, prog, nl, bs, sp, sc); break;
+    case 7: hipLaunchKernelGGL((k_ss_merge_big<MS, 7>), g, th, 0, s, p, t, prog, nl, bs, sp, sc); break;
+    case 8: hipLaunchKernelGGL((k_ss_merge_big<MS, 8>), g, th, 0, s, p, t, prog, nl, bs, sp, sc); break;
+    case 9: hipLaunchKernelGGL((k_ss_merge_big<MS, 9>), g, th, 0, s, p, t, prog, nl, bs, sp, sc); break;
     default: hipLaunchKernelGGL((k_ss_merge_big<MS, kSessMaxWords>), g, th, 0, s, p, t, prog, nl, bs, sp, sc); break;
   }
 }

@@ -103,7 +103,8 @@ static uint64_t ss_part_layout(uint64_t n, int words, SessPart *sp, char *m) {
   x.bigmask = (uint64_t *)take(nb * 8);
   x.touched = (uint32_t *)take(n * 4);
   x.sdone = (uint64_t *)take(nb * 8);
-  x.sidx = (uint16_t *)take(n * 2);
+  x.srec = (uint64_t *)take(n * (uint64_t)words * 8);
+  x.reloc = (uint64_t *)take(n * 24);
   if (sp) *sp = x;
   return off;
 }
@@ -279,6 +280,8 @@ static int push_session_merge(OpDevice &d, const hsg_op_config &cfg, const Progr
   // is skipped)
   for (int attempt = 0;; ++attempt) {
     launch_ss_fuse(d.stream, sp, d.ss, prog, nl, d.bshift, words, pt, d.out, a.pending, d.sc);
+    launch_ss_reloc_copy(d.stream, d.ss, pt, n);
+    DTRY(hipMemsetAsync(d.ss.meta + M_RELOC, 0, sizeof(uint64_t), d.stream));
     launch_ss_merge_big(d.stream, sp, d.ss, prog, nl, d.bshift, words, pt, d.sc);
     DTRY(hipMemcpyAsync(d.h_meta, d.ss.meta, M_WORDS * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
     DTRY(hipStreamSynchronize(d.stream));
@@ -368,7 +371,7 @@ int push_session(OpDevice &d, const hsg_op_config &cfg, const Program &prog, con
   rc = ensure_keys(d, kb.n, err);
   if (rc != HSG_OK) return rc;
   // per-batch words: need, fail, touched list, groups, runs, big buckets
-  DTRY(hipMemsetAsync(d.ss.meta + M_FAIL, 0, (M_BIG - M_FAIL + 1) * sizeof(uint64_t), d.stream));
+  DTRY(hipMemsetAsync(d.ss.meta + M_FAIL, 0, (M_RELOC - M_FAIL + 1) * sizeof(uint64_t), d.stream));
   DTRY(hipMemsetAsync(d.ss.meta + M_RNEED, 0, kArenaRegions * sizeof(uint64_t), d.stream));
   rc = d.ss_merge ? push_session_merge(d, cfg, prog, a, kb, r, err) : push_session_replay(d, cfg, prog, a, kb, seq, r, err);
   if (d.ss_merge) r.pairs = kb.n;  // keyed records (HSG_KEY_NONE are counted too; stats only)

@@ -119,3 +119,21 @@ def test_mirror_fast_and_slow_keys(eng, gap):
         valid = (rng.random(n) >= 0.03).astype(np.uint8)
         batches.append((key, ts, [col], [valid]))
     _drive(eng, spec, batches, faithful=False)
+
+
+@pytest.mark.parametrize("ncols", [3, 5, 8])
+def test_many_columns_merge_path(eng, ncols):
+    """Records of 2 + C words for every C up to kMaxCols through the partition,
+    the fused per-sub-bucket merge and the hot-key chunks (each record stride
+    is its own kernel instantiation), per-batch mode, with absent fields."""
+    types = [abi.HSG_I64 if c % 2 == 0 else abi.HSG_F64 for c in range(ncols)]
+    aggs = [(abi.HSG_COUNT_ALL, 0)] + [(abi.HSG_SUM if c % 3 else abi.HSG_MAX, c) for c in range(ncols)]
+    spec = OpSpec(abi.HSG_SESSION, abi.HSG_EMIT_PER_BATCH, gap_ms=700, col_types=types, aggs=aggs[:8])
+    batches = []
+    for bi in range(3):
+        key, ts, cols, valid = gen_small(900 + bi, 60_000, 4_000, col_types=tuple(types), span=150_000,
+                                         base=9_000_000 + bi * 120_000)
+        if bi == 2:  # one hot key: its sub-bucket goes to k_ss_merge_big
+            key = np.where((np.arange(key.size) % 3 == 0) & (key != abi.HSG_KEY_NONE), np.uint32(7), key)
+        batches.append((key.astype(np.uint32), ts, cols, valid))
+    _drive(eng, spec, batches, faithful=False)
