@@ -12,10 +12,11 @@
 //
 // Batch paths:
 //   merge   (per-batch / state-only emission, no LAST): key-hash partition;
-//           per bucket (k_ss_fuse) sub-buckets by further key-hash bits, each
-//           grouped by key and ranked by ts in LDS; one thread per key then
-//           sweep-merges its points, read from LDS, with its resident
-//           sessions (points closer than the gap chain into one session).
+//           per bucket (k_ss_sort) sub-buckets by further key-hash bits, each
+//           grouped by key in an LDS hash table and written out sorted by
+//           (key, ts), one group record per key; then one thread per key
+//           (k_ss_apply) sweep-merges its points with its resident sessions
+//           (points closer than the gap chain into one session).
 //           Buckets whose sub-buckets do not fit one sort (hot keys) are merged
 //           chunk by chunk by one workgroup (k_ss_merge_big). Order-free: the
 //           aggregates commute.
@@ -42,6 +43,8 @@ enum SessMeta : int {
   M_KEYS = 1,       // live keys in the key table
   M_FAIL = 3,       // a workgroup could not reserve arena rows (the host compacts, then resumes)
   M_TLEN = 4,       // merge path: touched-list entries this batch
+  M_GRP = 5,        // merge path: key groups written by k_ss_sort
+  M_RUNS = 6,       // merge path: runs written by k_ss_sort
   M_BIG = 7,        // merge path: buckets left to k_ss_merge_big
   M_RELOC = 8,      // merge path: relocated lists whose prefix k_ss_reloc_copy still copies
   M_SCRATCH = 15,   // device landing word (compaction total)
@@ -90,10 +93,13 @@ struct SessPart {
   uint64_t *rec;       // [n * words] partitioned records
   uint64_t *tmax;      // [tiles] ts max image per tile (stream time)
   uint32_t *progress;  // [nb] chunks of each big bucket applied (resumable after an arena refill)
-  uint32_t *touched;   // [n] key slots rewritten by k_ss_merge_big (one entry per chunk and key)
+  uint32_t *touched;   // [n] key slots rewritten (a big bucket: one entry per chunk and key)
+  uint64_t *srec;      // [n][words] records sorted by (key, ts): ts, word 0, columns
+  uint32_t *groups;    // [n][4] key groups: key, first record in srec, records, -
+  uint8_t *done;       // [n / 256 + 1] apply blocks done (resumable)
   uint64_t *bigmask;   // [nb] sub-buckets left to k_ss_merge_big
-  uint64_t *sdone;     // [nb] sub-buckets k_ss_fuse applied (~0: the whole bucket; resumable)
-  uint64_t *srec;      // [n][words] per bucket: its records grouped by sub-bucket
+  uint16_t *sidx;      // [n] per bucket: its record indices grouped by sub-bucket
+  uint32_t *gsparse;   // [n][4] group records at their sub-bucket's record positions
   uint64_t *reloc;     // [n][3] relocated lists (old row, new row, rows of the prefix to copy)
 };
 // bshift: owner bits of the key hash above the bucket bits (multi-GPU)
@@ -101,14 +107,15 @@ void launch_ss_phist(hipStream_t s, const Batch &b, int np_log2, int bshift, uin
 void launch_ss_wm(hipStream_t s, const SessPart &sp, uint64_t tiles, int64_t wm_in, DevScalars *sc);
 void launch_ss_pscatter(hipStream_t s, const Batch &b, int np_log2, int bshift, uint64_t tiles, int words,
                         bool has_valid, const SessPart &sp);
-// per bucket: sub-buckets grouped by key in LDS and merged into the store
-// (one thread per key); writes the changelog rows of its keys at out_base +
-// sc->out_rows
-void launch_ss_fuse(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, int np_log2,
-                    int bshift, int words, const SessPart &sp, OutCols out, uint64_t out_base, DevScalars *sc);
+void launch_ss_sort(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, int np_log2,
+                    int bshift, int words, const SessPart &sp, DevScalars *sc);
+// n_bound: records of the batch (an upper bound on the groups); writes the
+// changelog rows of its keys at out_base + sc->out_rows
+void launch_ss_apply(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, uint64_t n_bound,
+                     int words, const SessPart &sp, OutCols out, uint64_t out_base, DevScalars *sc);
 void launch_ss_merge_big(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, int np_log2,
                          int bshift, int words, const SessPart &sp, DevScalars *sc);
-// the prefixes of the lists k_ss_fuse relocated (sp.reloc, t.meta[M_RELOC]
+// the prefixes of the lists k_ss_apply relocated (sp.reloc, t.meta[M_RELOC]
 // entries), copied after it and before anything reads those lists
 void launch_ss_reloc_copy(hipStream_t s, const SessTable &t, const SessPart &sp, uint64_t n_bound);
 // per-batch changelog of the keys k_ss_merge_big touched (emit = 0: count only)

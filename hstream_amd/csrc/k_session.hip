@@ -716,6 +716,21 @@ __device__ __attribute__((always_inline)) inline MgSess<MS> pick_tail(const MgTa
   return x;
 }
 
+// runs precomputed by k_ss_sort: rows [start][end][aggs]
+struct RunsGlobal {
+  const uint64_t *runs;
+  uint32_t rstride;
+  int ns;
+  __device__ int64_t start(uint32_t r) const { return (int64_t)runs[(uint64_t)r * rstride]; }
+  __device__ int64_t end(uint32_t r) const { return (int64_t)runs[(uint64_t)r * rstride + 1]; }
+  template <int MS, class PV>
+  __device__ void aggs(const PV &, uint32_t r, int64_t (&a)[MS]) const {
+    const uint64_t *q = runs + (uint64_t)r * rstride + 2;
+#pragma unroll
+    for (int s = 0; s < MS; ++s) a[s] = s < ns ? (int64_t)q[s] : 0;
+  }
+};
+
 // Sweep of one key: its resident sessions [i0, len) (in registers when
 // `tail_regs`: then len - i0 <= kMgTail) and its runs [r0, r1), in start
 // order; items closer than gap merge (next.start - running end <= gap). With
@@ -902,49 +917,36 @@ __device__ __attribute__((always_inline)) inline void mg_apply(const PV &prog, c
 }
 
 // ---------------------------------------------------------------------------
-// k_ss_fuse: one workgroup per bucket, in sub-buckets (further key-hash bits)
-// of about half an LDS chunk each. A sub-bucket's records are grouped by key
-// in an LDS hash table (count, scan, place with their values) and ranked by
-// ts within their key's segment; each key is then merged into its sessions
-// by one thread straight from LDS (points closer than the gap chain into one
-// session, the closure of SessionWindowedStream.hs:84-118 over the
-// findSessions test of Store.hs:243-272): the key's entry probed and loaded
-// at its home slot (the keys of a sub-bucket sit in one stretch of the key
-// table, in the LDS table's order), the merge planned from the entry's mirror
-// of the last session, one arena and one changelog reservation per
-// sub-bucket, the merged sessions, the changelog rows and the entry written
-// back whole. Nothing of the batch's records goes back to HBM between the
-// partition and the store.
-// A sub-bucket with a key of more than kSoSmall records (hot keys), or more
-// than kSoCH records, is left to k_ss_merge_big (sp.bigmask). Resumable per
-// sub-bucket (sp.sdone): a sub-bucket whose arena reservation fails is left
-// untouched, the host compacts the arena and launches again.
+// k_ss_sort: one workgroup per bucket, in sub-buckets (further key-hash bits)
+// of about half a sort chunk each. A sub-bucket's records are grouped by key
+// through an LDS hash table (count, scan, place with their values), each key's
+// few records are sorted by ts by its thread and walked into gap-delimited
+// runs (aggregates folded from the LDS copy) and one group record per key. A
+// sub-bucket with a key of more than kSoSmall records (hot keys), or more than
+// kSoCH records, is left to k_ss_merge_big (its bit in sp.bigmask).
 // ---------------------------------------------------------------------------
 constexpr int kSoNT = 512;
 constexpr int kSoCH = 1024;        // records per sub-bucket
 constexpr int kSoTabLog2 = 11;
 constexpr int kSoTab = 1 << kSoTabLog2;  // LDS hash table entries
 constexpr int kSoMaxSubLog2 = 6;   // up to 64 sub-buckets (buckets of < 2^16 records)
-constexpr int kSoSmall = 32;       // a key's records ranked by its own thread
-constexpr int kFuPer = kSoCH / kSoNT;  // key groups per thread
+constexpr int kSoSmall = 32;       // a key's records sorted by its own thread
 
 template <int W>
-struct FuseLds {
+struct SortLds {
   uint32_t tkey[kSoTab];
-  uint32_t tcnt[kSoTab];    // records of the key; after the scan the placement cursor (then the segment end)
+  uint32_t tcnt[kSoTab];    // records of the key; after the scan the placement cursor
   uint32_t tstart[kSoTab];  // first position of the key's segment
-  uint16_t gslot[kSoCH];    // table slot of each key group
-  int64_t ts[kSoCH];        // placed records: ts and the other words (word 0, columns)
+  uint16_t tgid[kSoTab];    // group index of the key in the sub-bucket
+  int64_t ts[kSoCH];        // segments: ts and the record's other words (word 0, columns)
   uint64_t vw[kSoCH * (W - 1)];
-  uint16_t qslot[kSoCH];    // table slot of the record at each placed position
-  uint16_t perm[kSoCH];     // segment position -> placed record, ts order within each segment
+  uint16_t qslot[kSoCH];    // table slot of the record at each segment position
   uint32_t wsum[kSoNT / 64];
-  uint64_t red[2][kSoNT / 64];
   uint32_t subcnt[1 << kSoMaxSubLog2];
   uint32_t suboff[1 << kSoMaxSubLog2];  // first entry of each sub-bucket in the bucket's index list
-  uint32_t ngrp, maxseg;
-  uint64_t abase, obase, rbase;
-  int fail;
+  uint32_t subgrp[1 << kSoMaxSubLog2];  // key groups of each sub-bucket
+  uint32_t ngrp, nrun, maxseg;
+  uint64_t grpbase;
 };
 
 // sub-bucket of a key: the sl key-hash bits below the owner and bucket bits
@@ -988,98 +990,30 @@ __device__ __attribute__((always_inline)) inline void ss_vw_elem(const PV &prog,
   }
 }
 
-// a key's placed records in ts order (segment positions [ra, rb)) as sweep
-// items: record r is the point [ts, ts]; the sweep merges items closer than
-// the gap, so feeding points instead of pre-merged runs gives the same sessions
-template <int W>
-struct FuseItems {
-  const FuseLds<W> *L;
-  __device__ int64_t start(uint32_t r) const { return L->ts[L->perm[r]]; }
-  __device__ int64_t end(uint32_t r) const { return start(r); }
-  template <int MS, class PV>
-  __device__ void aggs(const PV &prog, uint32_t r, int64_t (&a)[MS]) const {
-    ss_vw_elem<MS>(prog, &L->vw[(uint32_t)L->perm[r] * (W - 1)], a);
-  }
-};
-
-__device__ inline void ss_store_entry(SessKey *p, const SessKey &e) {
-  uint4 *q = reinterpret_cast<uint4 *>(p);
-  q[0] = make_uint4(e.key, e.len, (uint32_t)e.off, (uint32_t)(e.off >> 32));
-  q[1] = make_uint4(e.cap, e.mvalid, (uint32_t)e.emark, (uint32_t)(e.emark >> 32));
-  q[2] = make_uint4((uint32_t)(uint64_t)e.ms, (uint32_t)((uint64_t)e.ms >> 32), (uint32_t)(uint64_t)e.me,
-                    (uint32_t)((uint64_t)e.me >> 32));
-  q[3] = make_uint4((uint32_t)(uint64_t)e.ma[0], (uint32_t)((uint64_t)e.ma[0] >> 32), (uint32_t)(uint64_t)e.ma[1],
-                    (uint32_t)((uint64_t)e.ma[1] >> 32));
-}
-
-// the key's slot (inserting it when absent) and its entry, probing from the
-// slot whose entry `home` was already loaded; -1 = table full
-__device__ inline int64_t ss_resolve(const SessTable &t, uint32_t key, uint64_t s, SessKey home, SessKey &e,
-                                     bool &inserted) {
-  inserted = false;
-  for (uint64_t probe = 0; probe <= t.kmask; ++probe) {
-    const SessKey cur = probe ? ss_load_entry(&t.kt[s]) : home;
-    if (cur.key == key) {
-      e = cur;
-      return (int64_t)s;
-    }
-    if (cur.key == kSessEmptyKey) {
-      const uint32_t old = atomicCAS(&t.kt[s].key, kSessEmptyKey, key);
-      if (old == kSessEmptyKey) {
-        inserted = true;
-        e = ss_blank(key);
-        return (int64_t)s;
-      }
-    }
-    s = (s + 1) & t.kmask;
-  }
-  return -1;
-}
-
-// block exclusive scan of one u64 per thread (one LDS barrier)
-__device__ inline uint64_t fu_scan64(uint64_t *red, uint64_t v, uint64_t &total) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint64_t incl = wave_incl_sum(v);
-  if (lane == 63) red[wv] = incl;
-  lds_barrier();
-  uint64_t before = 0;
-  total = 0;
-  for (int k = 0; k < kSoNT / 64; ++k) {
-    if (k < wv) before += red[k];
-    total += red[k];
-  }
-  return before + incl - v;
-}
-
-template <int MS, int W, uint64_t SIG>
-__global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 && W <= 5) ? 4 : 2))) void k_ss_fuse(SessParams p, SessTable t, Program prog, int np_log2, int bshift,
-                                                   SessPart sp, OutCols out, uint64_t out_base, DevScalars *sc) {
-  __shared__ FuseLds<W> L;
-  const ProgView<SIG> pv(prog);  // the common aggregate sets: slot ops baked in
+template <int MS, int W>
+__global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Program prog, int np_log2, int bshift,
+                                                   SessPart sp, DevScalars *sc) {
+  __shared__ SortLds<W> L;
+  const uint64_t c0 = phase_clock();
+  uint64_t c_ins = 0, c_scan = 0, c_place = 0, c_key = 0, c1 = 0;
   constexpr int B = 8;  // loads in flight per thread in the bucket passes
-  uint64_t ck = phase_clock(), c_idx = 0, c_ins = 0, c_lds = 0, c_plan = 0, c_res = 0, c_app = 0;
-  auto lap = [&](uint64_t &acc) {
-    if constexpr (kPhaseClocks) {
-      const uint64_t c = phase_clock();
-      acc += c - ck;
-      ck = c;
-    }
-  };
   const uint32_t b = blockIdx.x;
   const uint64_t r0 = sp.bstart[b], r1 = sp.bstart[b + 1];
   const uint64_t m = r1 - r0;
-  uint64_t sdone = sp.sdone[b];
   if (m == 0) {
     if (threadIdx.x == 0) sp.bigmask[b] = 0;
     return;
   }
-  if (sdone == ~0ull) return;  // uniform: applied by an earlier launch of this batch (bigmask stays)
   const uint64_t *recs = sp.rec + r0 * W;
   const int sl = ss_sub_log2(m), hs = bshift + np_log2;
   const int nsub = 1 << sl;
-  // the bucket's records copied grouped by sub-bucket (sp.srec, the bucket's
-  // own range): a sub-bucket then reads its records contiguously
-  if (threadIdx.x < (1 << kSoMaxSubLog2)) L.subcnt[threadIdx.x] = 0;
+  // the bucket's record indices grouped by sub-bucket (sp.sidx, the bucket's
+  // own range): every later pass visits only its sub-bucket's records
+  uint16_t *sidx = sp.sidx + r0;
+  if (threadIdx.x < (1 << kSoMaxSubLog2)) {
+    L.subcnt[threadIdx.x] = 0;
+    L.subgrp[threadIdx.x] = 0;
+  }
   __syncthreads();
   const bool indexable = m < 65536;
   // (lanes of a wave with the same sub-bucket found by ballots: one LDS
@@ -1122,45 +1056,31 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
   __syncthreads();
   if (threadIdx.x < (1 << kSoMaxSubLog2)) L.subcnt[threadIdx.x] = 0;
   __syncthreads();
-  uint64_t *srec = sp.srec + r0 * W;
-  constexpr int B2 = W <= 3 ? 4 : 2;  // records in flight per thread in the copy pass
   if (indexable)
-    for (uint64_t i0 = 0; i0 < m; i0 += (uint64_t)kSoNT * B2) {
-      uint64_t v[B2][W];
+    for (uint64_t i0 = 0; i0 < m; i0 += (uint64_t)kSoNT * B) {
+      uint32_t q[B];
 #pragma unroll
-      for (int u = 0; u < B2; ++u) {
+      for (int u = 0; u < B; ++u) {
         const uint64_t i = i0 + (uint64_t)u * kSoNT + threadIdx.x;
-#pragma unroll
-        for (int w = 0; w < W; ++w) v[u][w] = i < m ? recs[i * W + w] : 0;
+        q[u] = i < m ? ss_sub((uint32_t)recs[i * W], hs, sl) : ~0u;
       }
 #pragma unroll
-      for (int u = 0; u < B2; ++u) {
-        const uint64_t i = i0 + (uint64_t)u * kSoNT + threadIdx.x;
-        const uint32_t q = i < m ? ss_sub((uint32_t)v[u][0], hs, sl) : ~0u;
-        const bool in = q != ~0u;
-        const uint64_t pm = peers(q, in);
+      for (int u = 0; u < B; ++u) {
+        const bool in = q[u] != ~0u;
+        const uint64_t pm = peers(q[u], in);
         const uint32_t rk = (uint32_t)__popcll(pm & lt);
         // the group's lowest lane reserves for the group; the others read its base
         uint32_t base = 0;
-        if (in && rk == 0) base = atomicAdd(&L.subcnt[q], (uint32_t)__popcll(pm));
+        if (in && rk == 0) base = atomicAdd(&L.subcnt[q[u]], (uint32_t)__popcll(pm));
         const int leader = in ? __ffsll((long long)pm) - 1 : lane0;
         base = __shfl(base, leader, 64);
-        if (in) {
-          uint64_t *d = srec + (uint64_t)(L.suboff[q] + base + rk) * W;
-#pragma unroll
-          for (int w = 0; w < W; ++w) d[w] = v[u][w];
-        }
+        if (in) sidx[L.suboff[q[u]] + base + rk] = (uint16_t)(i0 + (uint64_t)u * kSoNT + threadIdx.x);
       }
     }
   __syncthreads();
   uint64_t bigmask = indexable ? 0ull : ~0ull;  // a bucket that cannot be indexed goes to the big path whole
-  bool failed = false;
-  lap(c_idx);
-  int64_t live_delta = 0;
-  uint64_t keys_new = 0;
-  uint32_t err = 0;
-  const FuseItems<W> rs{&L};
-  const bool emit_batch = p.emit_mode == HSG_EMIT_PER_BATCH;
+  c1 = phase_clock();
+  const uint32_t rstride = 2 + prog.n_slots;
   constexpr int RP = kSoCH / kSoNT;  // records per thread in a sub-bucket pass
   for (int sub = 0; indexable && sub < nsub; ++sub) {
     const uint32_t m2 = L.subcnt[sub];
@@ -1169,21 +1089,26 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
       bigmask |= 1ull << sub;
       continue;
     }
-    if (((sdone >> sub) & 1ull) || failed) continue;  // applied by an earlier launch / after a failed reservation
-    const uint64_t *lst = srec + (uint64_t)L.suboff[sub] * W;
+    const uint16_t *lst = sidx + L.suboff[sub];
+    uint64_t ca = phase_clock();
     // 1. keys of the sub-bucket into the LDS table, records per key; the
     // records' words stay in registers for the placement
     for (int h = threadIdx.x; h < kSoTab; h += kSoNT) {
       L.tkey[h] = 0xFFFFFFFFu;
       L.tcnt[h] = 0;
     }
-    if (threadIdx.x == 0) L.maxseg = 0;
+    if (threadIdx.x == 0) {
+      L.ngrp = 0;
+      L.nrun = 0;
+      L.maxseg = 0;
+    }
     uint64_t rw[RP][W];
 #pragma unroll
     for (int u = 0; u < RP; ++u) {
       const uint32_t j = u * kSoNT + threadIdx.x;
+      const uint64_t i = j < m2 ? lst[j] : 0;
 #pragma unroll
-      for (int w = 0; w < W; ++w) rw[u][w] = j < m2 ? lst[(uint64_t)j * W + w] : 0;
+      for (int w = 0; w < W; ++w) rw[u][w] = j < m2 ? recs[i * W + w] : 0;
     }
     lds_barrier();
     uint32_t hslot[RP];
@@ -1193,8 +1118,8 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
       if (u * kSoNT + threadIdx.x >= m2) continue;
       const uint32_t key = (uint32_t)rw[u][0];
       // the key-hash bits below the bucket and sub-bucket bits: the groups
-      // come out in key-table home order (ss_home), so neighbouring lanes
-      // probe neighbouring key entries
+      // come out in key-table home order (ss_home), so k_ss_apply's
+      // neighbouring lanes touch neighbouring key entries
       uint32_t h = (uint32_t)((key_hash(key) << (hs + sl)) >> (64 - kSoTabLog2));
       for (;;) {
         const uint32_t cur = L.tkey[h];
@@ -1209,7 +1134,7 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
       atomicAdd(&L.tcnt[h], 1u);
     }
     lds_barrier();
-    lap(c_ins);
+    { const uint64_t cb = phase_clock(); c_ins += cb - ca; ca = cb; }
     // 2. segment starts: exclusive scan of the counts
     // (records in the low 16 bits, occupied slots in the high: one scan gives
     // each key its segment start and its group index)
@@ -1247,19 +1172,17 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
       const uint32_t c = L.tcnt[h];
       L.tstart[h] = run & 0xFFFFu;
       L.tcnt[h] = run & 0xFFFFu;
-      if (c) L.gslot[run >> 16] = (uint16_t)h;
+      L.tgid[h] = (uint16_t)(run >> 16);
       run += c + (c ? 0x10000u : 0u);
     }
     if (threadIdx.x == 0) L.ngrp = all >> 16;
+    if (threadIdx.x == 0) L.subgrp[sub] = L.ngrp;
+    // a sub-bucket's sorted records and (sparse) group records live at its
+    // records' positions in the bucket
+    const uint64_t runbase = r0 + L.suboff[sub];
+    uint32_t *gsp = sp.gsparse + (r0 + L.suboff[sub]) * 4;
     lds_barrier();
-    // the key entries of this thread's groups (tid and tid + NT), loaded at
-    // their home slots now so the loads are in flight during the placement
-    // and the ranking
-    const uint32_t ngrp = L.ngrp;
-    const uint32_t ga = threadIdx.x, gb = kSoNT + threadIdx.x;
-    SessKey ea = ss_blank(0), eb = ss_blank(0);
-    if (ga < ngrp) ea = ss_load_entry(&t.kt[ss_home(t, L.tkey[L.gslot[ga]])]);
-    if (gb < ngrp) eb = ss_load_entry(&t.kt[ss_home(t, L.tkey[L.gslot[gb]])]);
+    { const uint64_t cb = phase_clock(); c_scan += cb - ca; ca = cb; }
     // 3. place (ts, words) in the key's segment
 #pragma unroll
     for (int u = 0; u < RP; ++u) {
@@ -1272,7 +1195,9 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
       L.qslot[q] = (uint16_t)hslot[u];
     }
     lds_barrier();
-    // 4. every record ranked by ts within its key's segment (<= kSoSmall)
+    { const uint64_t cb = phase_clock(); c_place += cb - ca; ca = cb; }
+    // 4. every record ranked by ts within its key's segment (<= kSoSmall) and
+    // written out in (key, ts) order; one group record per key
     for (uint32_t q = threadIdx.x; q < m2; q += kSoNT) {
       const uint32_t h = L.qslot[q];
       const uint32_t sa = L.tstart[h], se = L.tcnt[h];
@@ -1282,198 +1207,326 @@ __global__ __launch_bounds__(kSoNT) __attribute__((amdgpu_waves_per_eu((MS <= 2 
         const int64_t tj = L.ts[j];
         rank += (tj < v || (tj == v && j < q)) ? 1u : 0u;
       }
-      L.perm[sa + rank] = (uint16_t)q;
+      uint64_t *row = sp.srec + (runbase + sa + rank) * W;
+      row[0] = (uint64_t)v;
+#pragma unroll
+      for (int w = 0; w < W - 1; ++w) row[1 + w] = L.vw[q * (W - 1) + w];
+    }
+    for (int h = threadIdx.x; h < kSoTab; h += kSoNT) {
+      const uint32_t key = L.tkey[h];
+      if (key == 0xFFFFFFFFu) continue;
+      const uint32_t sa = L.tstart[h];
+      *reinterpret_cast<uint4 *>(gsp + (uint64_t)L.tgid[h] * 4) =
+          make_uint4(key, (uint32_t)(runbase + sa), L.tcnt[h] - sa, 0u);
     }
     lds_barrier();
-    lap(c_lds);
-    // 5. plan every key group (thread owns groups tid and tid + NT; the second
-    // is re-planned from its reloaded entry when it is applied, so only the
-    // first group's plan is held in registers): the home entries resolved
-    int64_t sla = -1, slb = -1;
-    uint64_t i0a = 0, i0b = 0, offb = 0;
-    uint32_t Ma = 0, capa = 0, fra = 0, capb = 0, frb = 0;
-    bool fasta = false;
-    uint64_t need = 0, nem = 0;
-    if (ga < ngrp) {
-      const uint32_t h = L.gslot[ga];
-      const uint32_t key = L.tkey[h], ra = L.tstart[h], rb = L.tcnt[h];
-      bool ins;
-      sla = ss_resolve(t, key, ss_home(t, key), ea, ea, ins);
-      if (sla < 0) err |= ERR_OOM;
-      else {
-        keys_new += ins ? 1 : 0;
-        fasta = mg_fast(rs, ra, ea);
-        mg_plan<MS>(pv, t, p.gap, rs, ra, rb, ea, fasta, p.batch_id, i0a, Ma, capa, &fra);
-        need += capa;
-        nem += fra;
-      }
-    }
-    if (gb < ngrp) {
-      const uint32_t h = L.gslot[gb];
-      const uint32_t key = L.tkey[h], ra = L.tstart[h], rb = L.tcnt[h];
-      bool ins;
-      slb = ss_resolve(t, key, ss_home(t, key), eb, eb, ins);
-      if (slb < 0) err |= ERR_OOM;
-      else {
-        keys_new += ins ? 1 : 0;
-        uint32_t Mb;
-        mg_plan<MS>(pv, t, p.gap, rs, ra, rb, eb, mg_fast(rs, ra, eb), p.batch_id, i0b, Mb, capb, &frb);
-        offb = eb.off;
-        need += capb;
-        nem += frb;
-      }
-    }
-    lap(c_plan);
-    // 6. one arena, one changelog and one relocation-list reservation for the
-    // sub-bucket (changelog rows in the low 32 bits of one scan, relocated
-    // lists in the high)
-    const uint32_t nrel = (sla >= 0 && capa && i0a ? 1u : 0u) + (slb >= 0 && capb && i0b ? 1u : 0u);
-    uint64_t tneed, tpk;
-    const uint64_t nbefore = fu_scan64(L.red[0], need, tneed);
-    const uint64_t pbefore = fu_scan64(L.red[1], nem | ((uint64_t)nrel << 32), tpk);
-    const uint64_t ebefore = pbefore & 0xFFFFFFFFull, tnem = tpk & 0xFFFFFFFFull;
-    if (threadIdx.x == 0) {
-      uint64_t base = 0;
-      const int fail = tneed ? !arena_take(t, arena_region(b), tneed, base) : 0;
-      L.fail = fail;
-      L.abase = base;
-      L.obase = 0;
-      L.rbase = 0;
-      if (fail) {
-        atomicOr((unsigned int *)&t.meta[M_FAIL], 1u);
-      } else {
-        if (tnem) {
-          // per-batch mode: touched = rows (the host takes it from out_rows)
-          if (emit_batch) L.obase = atomicAdd((unsigned long long *)&sc->out_rows, (unsigned long long)tnem);
-          else atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)tnem);
-        }
-        if (tpk >> 32) L.rbase = atomicAdd((unsigned long long *)&t.meta[M_RELOC], (unsigned long long)(tpk >> 32));
-      }
-    }
-    lds_barrier();
-    lap(c_res);
-    if (L.fail) {  // uniform: this sub-bucket and the rest stay for the next launch (inserted keys stay)
-      failed = true;
-      lds_barrier();
-      continue;
-    }
-    // 7. relocated lists: the prefix [0, i0) their merge leaves untouched is
-    // copied after this kernel (k_ss_reloc_copy, every row of every list in
-    // parallel), not by the key's thread row by row: a sub-bucket waits at
-    // its barrier for its slowest key, and ~1 key in 12 per C4 batch outgrows
-    // its rows. Nothing reads those rows before the copy (a key is in one
-    // sub-bucket; compaction and the next batch come after it).
-    const uint64_t dsta = capa ? L.abase + nbefore : 0, dstb = capb ? L.abase + nbefore + capa : 0;
-    {
-      uint64_t rp = L.rbase + (pbefore >> 32);
-      if (sla >= 0 && capa && i0a) {
-        uint64_t *e = sp.reloc + 3 * rp++;
-        e[0] = ea.off;
-        e[1] = dsta;
-        e[2] = i0a;
-      }
-      if (slb >= 0 && capb && i0b) {
-        uint64_t *e = sp.reloc + 3 * rp;
-        e[0] = offb;
-        e[1] = dstb;
-        e[2] = i0b;
-      }
-    }
-    // 8. merge, write the sessions, the changelog rows and the entry
-    uint64_t opos = out_base + L.obase + ebefore;
-    auto apply = [&](uint32_t g, int64_t slot, const SessKey &e, bool fast, uint64_t i0, uint32_t M, uint32_t cap,
-                     uint32_t fr, uint64_t rdst) {
-      const uint32_t h = L.gslot[g];
-      const uint32_t key = L.tkey[h], ra = L.tstart[h], rb = L.tcnt[h];
-      const bool reloc = cap != 0;
-      const uint64_t dst = reloc ? rdst : e.off;
-      EmitSink sink{out, emit_batch ? opos : ~0ull, key, 0, &prog};
-      if (emit_batch) opos += fr;
-      SessKey ne = e;
-      mg_apply<MS>(pv, t, p.gap, rs, ra, rb, e, fast, i0, dst, reloc, p.batch_id, &sink, &ne, true);
-      ss_entry_commit(ne, dst, (uint32_t)(i0 + M), reloc ? cap : 0u);
-      ss_store_entry(&t.kt[slot], ne);
-      live_delta += (int64_t)M - (int64_t)(e.len - i0);
-    };
-    if (sla >= 0) apply(ga, sla, ea, fasta, i0a, Ma, capa, fra, dsta);
-    if (slb >= 0) {
-      // the entry as planned (no other thread writes it): the same plan again
-      const SessKey e = ss_load_entry(&t.kt[slb]);
-      const uint32_t h = L.gslot[gb];
-      const uint32_t ra = L.tstart[h], rb = L.tcnt[h];
-      const bool fast = mg_fast(rs, ra, e);
-      uint64_t i0;
-      uint32_t M, cap;
-      mg_plan<MS>(pv, t, p.gap, rs, ra, rb, e, fast, p.batch_id, i0, M, cap);
-      apply(gb, slb, e, fast, i0, M, capb, frb, dstb);
-    }
-    sdone |= 1ull << sub;
-    // the next sub-bucket reuses the LDS only: its keys, rows and changelog
-    // positions are not this one's, so its stores need not have landed
-    lds_barrier();
-    lap(c_app);
+    c_key += phase_clock() - ca;
   }
-  if (kPhaseClocks && threadIdx.x == 0) {  // phase clocks (100 MHz), PHASES=1 builds with HSG_PHASES set
-    atomicAdd((unsigned long long *)&sc->scratch[24], (unsigned long long)c_idx);
+  // the bucket's group records, dense: one reservation per bucket
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int q = 0; q < nsub; ++q) {
+      if (!indexable || ((bigmask >> q) & 1ull) || L.subcnt[q] == 0 || L.subcnt[q] > (uint32_t)kSoCH) L.subgrp[q] = 0;
+      tot += L.subgrp[q];
+    }
+    L.grpbase = tot ? atomicAdd((unsigned long long *)&t.meta[M_GRP], (unsigned long long)tot) : 0;
+    sp.bigmask[b] = bigmask;
+    if (bigmask) atomicAdd((unsigned long long *)&t.meta[M_BIG], 1ull);
+  }
+  __syncthreads();
+  uint64_t d = L.grpbase;
+  for (int q = 0; q < nsub; ++q) {
+    const uint32_t c = L.subgrp[q];
+    const uint4 *src = reinterpret_cast<const uint4 *>(sp.gsparse + (r0 + L.suboff[q]) * 4);
+    for (uint32_t j = threadIdx.x; j < c; j += kSoNT) reinterpret_cast<uint4 *>(sp.groups)[d + j] = src[j];
+    d += c;
+  }
+  if (kPhaseClocks && threadIdx.x == 0) {  // phase clocks (100 MHz), HSG_PHASES
+    const uint64_t c2 = phase_clock();
+    atomicAdd((unsigned long long *)&sc->scratch[24], (unsigned long long)(c1 - c0));
     atomicAdd((unsigned long long *)&sc->scratch[25], (unsigned long long)c_ins);
-    atomicAdd((unsigned long long *)&sc->scratch[26], (unsigned long long)c_lds);
-    atomicAdd((unsigned long long *)&sc->scratch[27], (unsigned long long)c_plan);
-    atomicAdd((unsigned long long *)&sc->scratch[28], (unsigned long long)c_res);
-    atomicAdd((unsigned long long *)&sc->scratch[29], (unsigned long long)c_app);
+    atomicAdd((unsigned long long *)&sc->scratch[26], (unsigned long long)c_scan);
+    atomicAdd((unsigned long long *)&sc->scratch[27], (unsigned long long)c_place);
+    atomicAdd((unsigned long long *)&sc->scratch[28], (unsigned long long)c_key);
+    atomicAdd((unsigned long long *)&sc->scratch[29], (unsigned long long)(c2 - c0));
     atomicAdd((unsigned long long *)&sc->scratch[30], 1ull);
   }
-  {
-    const int lane = threadIdx.x & 63;
-    const uint64_t ld = wave_sum_u64((uint64_t)live_delta);
-    const uint64_t kn = wave_sum_u64(keys_new);
-    if (lane == 0) {
-      if (ld) atomicAdd((unsigned long long *)&sc->live, (unsigned long long)ld);
-      if (kn) atomicAdd((unsigned long long *)&t.meta[M_KEYS], (unsigned long long)kn);
+}
+
+template <int MS>
+static void sort_launch_w(hipStream_t s, int words, dim3 g, const SessParams &p, const SessTable &t,
+                          const Program &prog, int np_log2, int bshift, const SessPart &sp, DevScalars *sc) {
+  const dim3 th(kSoNT);
+  switch (words) {
+    case 2: hipLaunchKernelGGL((k_ss_sort<MS, 2>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+    case 3: hipLaunchKernelGGL((k_ss_sort<MS, 3>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+    case 4: hipLaunchKernelGGL((k_ss_sort<MS, 4>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+    case 5: hipLaunchKernelGGL((k_ss_sort<MS, 5>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+    case 6: hipLaunchKernelGGL((k_ss_sort<MS, 6>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+    case 7: hipLaunchKernelGGL((k_ss_sort<MS, 7>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+    case 8: hipLaunchKernelGGL((k_ss_sort<MS, 8>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+    case 9: hipLaunchKernelGGL((k_ss_sort<MS, 9>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+    default: hipLaunchKernelGGL((k_ss_sort<MS, kSessMaxWords>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, sc); break;
+  }
+}
+
+void launch_ss_sort(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, int np_log2,
+                    int bshift, int words, const SessPart &sp, DevScalars *sc) {
+  const dim3 g(1u << np_log2);
+  if (prog.n_slots <= 2) sort_launch_w<2>(s, words, g, p, t, prog, np_log2, bshift, sp, sc);
+  else if (prog.n_slots <= 4) sort_launch_w<4>(s, words, g, p, t, prog, np_log2, bshift, sp, sc);
+  else sort_launch_w<8>(s, words, g, p, t, prog, np_log2, bshift, sp, sc);
+}
+
+// a key's batch records, sorted by ts (k_ss_sort), as sweep items: record r
+// is the point [ts, ts]; the sweep merges items closer than the gap, so
+// feeding points instead of pre-merged runs gives the same sessions
+template <int W>
+struct RecItems {
+  const uint64_t *rows;  // [n][W]: ts, word 0, columns
+  __device__ int64_t start(uint32_t r) const { return (int64_t)rows[(uint64_t)r * W]; }
+  __device__ int64_t end(uint32_t r) const { return (int64_t)rows[(uint64_t)r * W]; }
+  template <int MS, class PV>
+  __device__ void aggs(const PV &prog, uint32_t r, int64_t (&a)[MS]) const {
+    ss_vw_elem<MS>(prog, rows + (uint64_t)r * W + 1, a);
+  }
+};
+
+// The same with the key's first two records in registers, loaded right after
+// the group record, beside the key-table probe: the sweeps of most keys (one
+// or two records in a batch) then wait on no record load. W <= 3 (ts, word 0,
+// one column); further records from memory.
+template <int W>
+struct RecItemsPf {
+  static_assert(W >= 2 && W <= 3, "RecItemsPf");
+  const uint64_t *rows;
+  uint32_t ra;
+  uint64_t t0, t1;           // ts of records ra, ra + 1
+  uint64_t v0[W - 1], v1[W - 1];  // their word 0 and column
+  __device__ void load(uint32_t a, uint32_t n) {
+    ra = a;
+    const uint64_t *p = rows + (uint64_t)a * W;
+    t0 = n > 0 ? p[0] : 0;
+    t1 = n > 1 ? p[W] : 0;
+#pragma unroll
+    for (int k = 0; k < W - 1; ++k) {
+      v0[k] = n > 0 ? p[1 + k] : 0;
+      v1[k] = n > 1 ? p[W + 1 + k] : 0;
     }
+  }
+  __device__ int64_t start(uint32_t r) const {
+    return (int64_t)(r == ra ? t0 : r == ra + 1 ? t1 : rows[(uint64_t)r * W]);
+  }
+  __device__ int64_t end(uint32_t r) const { return start(r); }
+  template <int MS, class PV>
+  __device__ void aggs(const PV &prog, uint32_t r, int64_t (&a)[MS]) const {
+    if (r - ra < 2) {
+      uint64_t v[W - 1];
+#pragma unroll
+      for (int k = 0; k < W - 1; ++k) v[k] = r == ra ? v0[k] : v1[k];
+      ss_vw_elem<MS>(prog, v, a);
+    } else {
+      ss_vw_elem<MS>(prog, rows + (uint64_t)r * W + 1, a);
+    }
+  }
+};
+template <int W, bool PF = (W <= 3)>
+struct ApplyItems {
+  using T = RecItems<W>;
+};
+template <int W>
+struct ApplyItems<W, true> {
+  using T = RecItemsPf<W>;
+};
+
+__device__ inline void ss_store_entry(SessKey *p, const SessKey &e) {
+  uint4 *q = reinterpret_cast<uint4 *>(p);
+  q[0] = make_uint4(e.key, e.len, (uint32_t)e.off, (uint32_t)(e.off >> 32));
+  q[1] = make_uint4(e.cap, e.mvalid, (uint32_t)e.emark, (uint32_t)(e.emark >> 32));
+  q[2] = make_uint4((uint32_t)(uint64_t)e.ms, (uint32_t)((uint64_t)e.ms >> 32), (uint32_t)(uint64_t)e.me,
+                    (uint32_t)((uint64_t)e.me >> 32));
+  q[3] = make_uint4((uint32_t)(uint64_t)e.ma[0], (uint32_t)((uint64_t)e.ma[0] >> 32), (uint32_t)(uint64_t)e.ma[1],
+                    (uint32_t)((uint64_t)e.ma[1] >> 32));
+}
+
+// the key's slot (inserting it when absent) and its entry, probing from the
+// slot whose entry `home` was already loaded; -1 = table full
+__device__ inline int64_t ss_resolve(const SessTable &t, uint32_t key, uint64_t s, SessKey home, SessKey &e,
+                                     bool &inserted) {
+  inserted = false;
+  for (uint64_t probe = 0; probe <= t.kmask; ++probe) {
+    const SessKey cur = probe ? ss_load_entry(&t.kt[s]) : home;
+    if (cur.key == key) {
+      e = cur;
+      return (int64_t)s;
+    }
+    if (cur.key == kSessEmptyKey) {
+      const uint32_t old = atomicCAS(&t.kt[s].key, kSessEmptyKey, key);
+      if (old == kSessEmptyKey) {
+        inserted = true;
+        e = ss_blank(key);
+        return (int64_t)s;
+      }
+    }
+    s = (s + 1) & t.kmask;
+  }
+  return -1;
+}
+
+// ---------------------------------------------------------------------------
+// k_ss_apply: one thread per key group (every key once per batch). Plan,
+// reserve the block's fresh lists in its arena region (all or nothing: a block
+// that cannot stays undone, the host compacts and runs the pass again), apply
+// and write the changelog rows of the fresh sessions.
+// ---------------------------------------------------------------------------
+constexpr int kApNT = 512;  // one arena / changelog reservation per 512 keys; two blocks per CU
+
+template <int MS, int W, uint64_t SIG>
+__global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, Program prog, SessPart sp,
+                                                    OutCols out, uint64_t out_base, DevScalars *sc) {
+  const ProgView<SIG> pv(prog);  // the common aggregate sets: slot ops baked in
+  __shared__ uint64_t ws[kApNT / 64];
+  __shared__ uint64_t we[kApNT / 64];
+  __shared__ uint64_t sbase, sobase, srbase;
+  __shared__ int sfail;
+  const uint32_t blk = blockIdx.x;
+  if (sp.done[blk]) return;  // uniform: applied by an earlier pass of this batch
+  const uint64_t ng = t.meta[M_GRP];
+  const uint64_t g0 = (uint64_t)blk * kApNT;
+  if (g0 >= ng) return;  // uniform
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t g = g0 + threadIdx.x;
+  const bool act = g < ng;
+  typename ApplyItems<W>::T rs{sp.srec};
+  uint32_t key = 0, ra = 0, nr = 0, newcap = 0, M = 0, fresh = 0;
+  uint64_t i0 = 0;
+  int64_t sl = -1;
+  bool ins = false, fast = false;
+  SessKey e = ss_blank(0);
+  uint32_t err = 0;
+  if (act) {
+    const uint4 gr = *reinterpret_cast<const uint4 *>(sp.groups + g * 4);
+    key = gr.x;
+    ra = gr.y;
+    nr = gr.z;
+    if constexpr (W <= 3) rs.load(ra, nr);  // in flight during the probe
+    // the entry at the key's home slot, loaded whole with the probe (the key
+    // is found there unless a collision displaced it)
+    const uint64_t home = ss_home(t, key);
+    sl = ss_resolve(t, key, home, ss_load_entry(&t.kt[home]), e, ins);
+    if (sl < 0) err |= ERR_OOM;
+    else {
+      // near-sorted arrivals: planned from the entry's mirror, no list read
+      fast = mg_fast(rs, ra, e);
+      mg_plan<MS>(pv, t, p.gap, rs, ra, ra + nr, e, fast, p.batch_id, i0, M, newcap, &fresh);
+    }
+  }
+  const bool live = act && sl >= 0;
+  {
+    // keys inserted count now: a block that fails below finds them next pass
+    const uint64_t ksum = wave_sum_u64(ins ? 1ull : 0ull);
+    if (lane == 0 && ksum) atomicAdd((unsigned long long *)&t.meta[M_KEYS], (unsigned long long)ksum);
     if (err) atomicOr(&sc->err, err);
   }
-  if (threadIdx.x == 0) {
-    // after a failed reservation the big sub-buckets wait for the launch that
-    // completes the bucket (k_ss_merge_big walks the bucket's chunks once)
-    sp.sdone[b] = failed ? sdone : ~0ull;
-    sp.bigmask[b] = failed ? 0ull : bigmask;
+  // block exclusive scans of the fresh list rows and of the changelog rows
+  // (with, in the high 32 bits, the relocated lists whose prefix
+  // k_ss_reloc_copy copies after this kernel)
+  const bool rel = live && newcap != 0 && i0 != 0;
+  const uint64_t need = newcap, nem = (live ? fresh : 0) | ((uint64_t)(rel ? 1 : 0) << 32);
+  const uint64_t incl = wave_incl_sum(need), einc = wave_incl_sum(nem);
+  if (lane == 63) {
+    ws[wv] = incl;
+    we[wv] = einc;
   }
+  __syncthreads();
+  uint64_t before = 0, total = 0, ebefore = 0, etotal = 0;
+  for (int k = 0; k < kApNT / 64; ++k) {
+    if (k < wv) {
+      before += ws[k];
+      ebefore += we[k];
+    }
+    total += ws[k];
+    etotal += we[k];
+  }
+  const uint64_t etot = etotal & 0xFFFFFFFFull, rtot = etotal >> 32;
+  if (threadIdx.x == 0) {
+    uint64_t base = 0;
+    const int fail = total ? !arena_take(t, arena_region(blk), total, base) : 0;
+    sfail = fail;
+    sbase = base;
+    sobase = 0;
+    srbase = 0;
+    if (fail) {
+      atomicOr((unsigned int *)&t.meta[M_FAIL], 1u);
+    } else {
+      if (etot) {
+        // per-batch mode: touched = rows (the host takes it from out_rows)
+        if (p.emit_mode == HSG_EMIT_PER_BATCH) sobase = atomicAdd((unsigned long long *)&sc->out_rows, (unsigned long long)etot);
+        else atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)etot);
+      }
+      if (rtot) srbase = atomicAdd((unsigned long long *)&t.meta[M_RELOC], (unsigned long long)rtot);
+    }
+  }
+  __syncthreads();
+  if (sfail) return;  // uniform: keys inserted above stay (idempotent); the block runs again
+  int64_t ld = 0;
+  if (live) {
+    const bool reloc = newcap != 0;
+    const uint64_t dst = reloc ? sbase + before + incl - need : e.off;
+    const uint64_t eb = (ebefore & 0xFFFFFFFFull) + (einc & 0xFFFFFFFFull) - (nem & 0xFFFFFFFFull);
+    EmitSink sink{out, p.emit_mode == HSG_EMIT_PER_BATCH ? out_base + sobase + eb : ~0ull, key, 0, &prog};
+    if (rel) {
+      // the untouched prefix [0, i0) of a relocated list is copied after this
+      // kernel (k_ss_reloc_copy, every row of every list in parallel): a
+      // thread copying its own list row by row would hold its whole wave
+      // (~1 key in 12 per C4 batch outgrows its rows)
+      uint64_t *r = sp.reloc + 3 * (srbase + (ebefore >> 32) + (einc >> 32) - 1);
+      r[0] = e.off;
+      r[1] = dst;
+      r[2] = i0;
+    }
+    SessKey ne = e;
+    mg_apply<MS>(pv, t, p.gap, rs, ra, ra + nr, e, fast, i0, dst, reloc, p.batch_id, &sink, &ne, true);
+    ss_entry_commit(ne, dst, (uint32_t)(i0 + M), reloc ? newcap : 0u);
+    ss_store_entry(&t.kt[sl], ne);
+    ld = (int64_t)M - (int64_t)(e.len - i0);
+  }
+  const uint64_t lsum = wave_sum_u64((uint64_t)ld);
+  if (lane == 0 && lsum) atomicAdd((unsigned long long *)&sc->live, (unsigned long long)lsum);
+  __syncthreads();
+  if (threadIdx.x == 0) sp.done[blk] = 1;
 }
 
 template <int MS, uint64_t SIG>
-static void fuse_launch_w(hipStream_t s, int words, dim3 g, const SessParams &p, const SessTable &t,
-                          const Program &prog, int np_log2, int bshift, const SessPart &sp, OutCols out,
-                          uint64_t out_base, DevScalars *sc) {
-  const dim3 th(kSoNT);
-#define HSG_FUSE(WW, SS) \
-  hipLaunchKernelGGL((k_ss_fuse<MS, WW, SS>), g, th, 0, s, p, t, prog, np_log2, bshift, sp, out, out_base, sc)
+static void apply_launch_w(hipStream_t s, int words, dim3 g, const SessParams &p, const SessTable &t,
+                           const Program &prog, const SessPart &sp, OutCols out, uint64_t out_base, DevScalars *sc) {
+  const dim3 th(kApNT);
   switch (words) {
-    case 2: HSG_FUSE(2, SIG); break;
-    case 3: HSG_FUSE(3, SIG); break;
-    case 4: HSG_FUSE(4, 0); break;
-    case 5: HSG_FUSE(5, 0); break;
-    case 6: HSG_FUSE(6, 0); break;
-    case 7: HSG_FUSE(7, 0); break;
-    case 8: HSG_FUSE(8, 0); break;
-    case 9: HSG_FUSE(9, 0); break;
-    default: HSG_FUSE(kSessMaxWords, 0); break;  // (the partition's record stride: 2 + columns)
+    case 2: hipLaunchKernelGGL((k_ss_apply<MS, 2, SIG>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 3: hipLaunchKernelGGL((k_ss_apply<MS, 3, SIG>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 4: hipLaunchKernelGGL((k_ss_apply<MS, 4, 0>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 5: hipLaunchKernelGGL((k_ss_apply<MS, 5, 0>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 6: hipLaunchKernelGGL((k_ss_apply<MS, 6, 0>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 7: hipLaunchKernelGGL((k_ss_apply<MS, 7, 0>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 8: hipLaunchKernelGGL((k_ss_apply<MS, 8, 0>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    case 9: hipLaunchKernelGGL((k_ss_apply<MS, 9, 0>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
+    default: hipLaunchKernelGGL((k_ss_apply<MS, kSessMaxWords, 0>), g, th, 0, s, p, t, prog, sp, out, out_base, sc); break;
   }
-#undef HSG_FUSE
 }
 
-void launch_ss_fuse(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, int np_log2,
-                    int bshift, int words, const SessPart &sp, OutCols out, uint64_t out_base, DevScalars *sc) {
-  const dim3 g(1u << np_log2);
+void launch_ss_apply(hipStream_t s, const SessParams &p, const SessTable &t, const Program &prog, uint64_t n_bound,
+                     int words, const SessPart &sp, OutCols out, uint64_t out_base, DevScalars *sc) {
+  const dim3 g((unsigned)((n_bound + kApNT - 1) / kApNT + 1));
   // the common aggregate sets of a session GROUP BY (one column or none) with
   // their slot program baked in; every other program reads it at run time
   const uint64_t sig = program_sig(prog);
-  if (sig == kSigCntSumI) fuse_launch_w<2, kSigCntSumI>(s, words, g, p, t, prog, np_log2, bshift, sp, out, out_base, sc);
-  else if (sig == kSigCntSumF) fuse_launch_w<2, kSigCntSumF>(s, words, g, p, t, prog, np_log2, bshift, sp, out, out_base, sc);
-  else if (sig == kSigCnt) fuse_launch_w<2, kSigCnt>(s, words, g, p, t, prog, np_log2, bshift, sp, out, out_base, sc);
-  else if (sig == kSigSumMaxI) fuse_launch_w<2, kSigSumMaxI>(s, words, g, p, t, prog, np_log2, bshift, sp, out, out_base, sc);
-  else if (prog.n_slots <= 2) fuse_launch_w<2, 0>(s, words, g, p, t, prog, np_log2, bshift, sp, out, out_base, sc);
-  else if (prog.n_slots <= 4) fuse_launch_w<4, 0>(s, words, g, p, t, prog, np_log2, bshift, sp, out, out_base, sc);
-  else fuse_launch_w<8, 0>(s, words, g, p, t, prog, np_log2, bshift, sp, out, out_base, sc);
+  if (sig == kSigCntSumI) apply_launch_w<2, kSigCntSumI>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  else if (sig == kSigCntSumF) apply_launch_w<2, kSigCntSumF>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  else if (sig == kSigCnt) apply_launch_w<2, kSigCnt>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  else if (sig == kSigSumMaxI) apply_launch_w<2, kSigSumMaxI>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  else if (prog.n_slots <= 2) apply_launch_w<2, 0>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  else if (prog.n_slots <= 4) apply_launch_w<4, 0>(s, words, g, p, t, prog, sp, out, out_base, sc);
+  else apply_launch_w<8, 0>(s, words, g, p, t, prog, sp, out, out_base, sc);
 }
 
 // the prefixes of relocated lists: 16 lanes per list on consecutive words

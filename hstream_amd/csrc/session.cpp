@@ -85,8 +85,8 @@ static int set_regions(OpDevice &d, uint64_t used, std::string &err) {
 }
 
 // Session partition scratch (besides d.part's histogram, offsets and
-// records): per-tile ts maxima, per-bucket progress, big and done flags, the
-// touched list of the big path, the sub-bucket record index.
+// records): per-tile ts maxima, per-bucket progress and big flags, the touched
+// list, the runs and key groups of k_ss_sort, the apply blocks' done flags.
 static uint64_t ss_part_layout(uint64_t n, int words, SessPart *sp, char *m) {
   uint64_t off = 0;
   auto take = [&](uint64_t bytes) {
@@ -102,8 +102,11 @@ static uint64_t ss_part_layout(uint64_t n, int words, SessPart *sp, char *m) {
   x.progress = (uint32_t *)take(nb * 4);
   x.bigmask = (uint64_t *)take(nb * 8);
   x.touched = (uint32_t *)take(n * 4);
-  x.sdone = (uint64_t *)take(nb * 8);
   x.srec = (uint64_t *)take(n * (uint64_t)words * 8);
+  x.groups = (uint32_t *)take(n * 16);
+  x.done = (uint8_t *)take(n / 256 + 2);
+  x.sidx = (uint16_t *)take(n * 2);
+  x.gsparse = (uint32_t *)take(n * 16);
   x.reloc = (uint64_t *)take(n * 24);
   if (sp) *sp = x;
   return off;
@@ -245,8 +248,8 @@ static int clear_fail(OpDevice &d, std::string &err) {
   return HSG_OK;
 }
 
-// merge path: partition by key hash; per bucket, sub-buckets grouped by key
-// in LDS and merged into the store by one thread per key (k_ss_fuse)
+// merge path: partition by key hash, per bucket sort / runs / key groups,
+// one thread per key merges its runs into its sessions
 static int push_session_merge(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
                               const Batch &kb, PushResult &r, std::string &err) {
   const uint64_t n = kb.n;
@@ -269,17 +272,21 @@ static int push_session_merge(OpDevice &d, const hsg_op_config &cfg, const Progr
   pp.tiles = tiles;
   DTRY(hipEventRecord(d.ev_a, d.stream));
   DTRY(hipMemsetAsync(pt.progress, 0, (1ull << nl) * 4, d.stream));
-  DTRY(hipMemsetAsync(pt.sdone, 0, (1ull << nl) * 8, d.stream));
+  DTRY(hipMemsetAsync(pt.done, 0, n / 256 + 2, d.stream));
   launch_ss_phist(d.stream, kb, nl, d.bshift, tiles, pt);
   launch_ss_wm(d.stream, pt, tiles, a.wm_in, d.sc);
   launch_part_offsets(d.stream, pp, d.part, d.sc);
   launch_ss_pscatter(d.stream, kb, nl, d.bshift, tiles, words, has_valid, pt);
-  // a pass stops short (M_FAIL) only where the arena could not take a
-  // sub-bucket's (or a big-bucket chunk's) fresh lists: those were left
-  // untouched; compact / grow the arena, then run the pass again (done work
-  // is skipped)
+  launch_ss_sort(d.stream, sp, d.ss, prog, nl, d.bshift, words, pt, d.sc);
+  // the key groups k_ss_sort found size the apply grid
+  DTRY(hipMemcpyAsync(d.h_meta + M_GRP, d.ss.meta + M_GRP, sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
+  DTRY(hipStreamSynchronize(d.stream));
+  const uint64_t ngrp = d.h_meta[M_GRP];
+  // a pass stops short (M_FAIL) only where the arena could not take a key's
+  // fresh list: those apply blocks / big-bucket chunks were left untouched;
+  // compact / grow the arena, then run the pass again (done work is skipped)
   for (int attempt = 0;; ++attempt) {
-    launch_ss_fuse(d.stream, sp, d.ss, prog, nl, d.bshift, words, pt, d.out, a.pending, d.sc);
+    launch_ss_apply(d.stream, sp, d.ss, prog, ngrp, words, pt, d.out, a.pending, d.sc);
     launch_ss_reloc_copy(d.stream, d.ss, pt, n);
     DTRY(hipMemsetAsync(d.ss.meta + M_RELOC, 0, sizeof(uint64_t), d.stream));
     launch_ss_merge_big(d.stream, sp, d.ss, prog, nl, d.bshift, words, pt, d.sc);

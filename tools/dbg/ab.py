@@ -4,6 +4,7 @@
 import os, runpy, sys
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
 sys.path.insert(0, ROOT)
+import torch  # (HIP runtime first, as bench.py does, then the library)
 from hstream_amd import engine
 engine.load_library(os.path.abspath(sys.argv[1]))
 sys.argv = ["bench.py"] + sys.argv[2:]
