@@ -336,9 +336,12 @@ __global__ __launch_bounds__(kPrNT) void k_pr_local(Program prog, PartParams pp,
     pr_seg_earlier<MS>(prog, xf, xv, pf, pv);
     xh += ph;
   }
-  // the chunk's partials: one per group (head), allocated in one atomic
+  // the chunk's partials: one per group (head), at the chunk's own pair
+  // range (partials <= pairs; chunks' record ranges are disjoint), so no
+  // chunk waits on a shared counter (one device-scope atomic per chunk on a
+  // single word serialised ~100K chunks per C3 batch)
   if (threadIdx.x == 0) {
-    const uint32_t base = (uint32_t)atomicAdd((unsigned long long *)pr.counter, (unsigned long long)heads);
+    const uint32_t base = (uint32_t)(r0 * wpr);
     s_cbase = base;
     pr.cbase[blockIdx.x] = base;
     pr.ccnt[blockIdx.x] = heads;
@@ -400,19 +403,41 @@ __global__ __launch_bounds__(256) void k_pr_carry(Program prog, TwParams p, Part
   uint64_t touched = 0;
   for (uint32_t c = c0; c < c1; ++c) {
     const uint32_t base = pr.cbase[c], cnt = pr.ccnt[c];
-    for (uint32_t e = threadIdx.x; e < cnt; e += 256) {
+    // CU partials per thread and pass: their group keys, totals and home-slot
+    // keys loaded together (one wait instead of one per partial)
+    constexpr int CU = 4;
+    for (uint32_t e0 = threadIdx.x; e0 < cnt; e0 += 256 * CU) {
+    uint64_t gk[CU], hk[CU];
+    int64_t tt[CU][MS];
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+      const uint32_t e = e0 + u * 256;
+      gk[u] = e < cnt ? pr.gkey[base + e] : kEmpty;
+#pragma unroll
+      for (int s = 0; s < MS; ++s) tt[u][s] = (e < cnt && s < ns) ? pr.part[(uint64_t)(base + e) * ns + s] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < CU; ++u)
+      hk[u] = gk[u] != kEmpty ? __hip_atomic_load(t.key(tw_region_base(t, gk[u]) + tw_home_in(t, gk[u])),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : kEmpty;
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+      const uint32_t e = e0 + u * 256;
+      if (e >= cnt) continue;
       const uint32_t gi = base + e;
-      const uint64_t g = pr.gkey[gi];
+      const uint64_t g = gk[u];
       int64_t tot[MS], cur[MS];
 #pragma unroll
-      for (int s = 0; s < MS; ++s) tot[s] = s < ns ? pr.part[(uint64_t)gi * ns + s] : 0;
+      for (int s = 0; s < MS; ++s) tot[s] = tt[u][s];
       // find or claim (agent-scope loads: an earlier chunk of this workgroup may have claimed it)
       const uint64_t rb = tw_region_base(t, g);
       uint64_t sl = tw_home_in(t, g);
       const uint64_t step = tw_step(t), np = (t.rmask + 1) / step;
       int64_t slot = -1;
       bool isnew = false;
-      for (uint64_t probe = 0; probe < np && probe < kMaxProbes; ++probe) {
+      if (hk[u] == g) slot = (int64_t)(rb + sl);  // found at its home slot (the usual case)
+      for (uint64_t probe = 0; slot < 0 && probe < np && probe < kMaxProbes; ++probe) {
         uint64_t *kp = t.key(rb + sl);
         const uint64_t k = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k == g) {
@@ -468,6 +493,7 @@ __global__ __launch_bounds__(256) void k_pr_carry(Program prog, TwParams p, Part
 #pragma unroll
       for (int s = 0; s < MS; ++s)
         if (s < ns) pr.part[(uint64_t)gi * ns + s] = cur[s];
+    }
     }
     // this chunk's rows in L2 before the next chunk reads them: the same
     // workgroup (one CU, one L2) reads them back with L1-bypassing loads, so
@@ -561,19 +587,41 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit(Batch bt, Program pr
       err |= ERR_OOM;
       continue;
     }
-    for (uint32_t j = 0; j < n; ++j, ++o) {
-      const uint64_t *it = pr.inter + (pos * wpr + j) * rw;
-      const uint32_t gi = (uint32_t)it[0];
-      if ((uint64_t)gi >= pb.n_cap * wpr) {
+    // the record's windows EJ at a time, every load of a group in flight
+    // together (its pairs' partial indices and prefixes, then the carries):
+    // a window after the other waited two round trips each (C3: 12 windows)
+    constexpr int EJ = MS <= 2 ? 4 : MS <= 4 ? 2 : 1;
+    for (uint32_t j0 = 0; j0 < n; j0 += EJ) {
+    uint32_t gq[EJ];
+    int64_t Lq[EJ][MS], Rq[EJ][MS];
+#pragma unroll
+    for (int u = 0; u < EJ; ++u) {
+      const uint32_t j = j0 + u;
+      const uint64_t *it = pr.inter + (pos * wpr + (j < n ? j : 0)) * rw;
+      gq[u] = j < n ? (uint32_t)it[0] : 0u;
+#pragma unroll
+      for (int s = 0; s < MS; ++s) Lq[u][s] = (j < n && s < ns) ? (int64_t)it[1 + s] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < EJ; ++u) {
+      const bool ok = j0 + u < n && (uint64_t)gq[u] < pb.n_cap * wpr;
+#pragma unroll
+      for (int s = 0; s < MS; ++s) Rq[u][s] = (ok && s < ns) ? pr.part[(uint64_t)gq[u] * ns + s] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < EJ; ++u, ++o) {
+      const uint32_t j = j0 + u;
+      if (j >= n) break;
+      if ((uint64_t)gq[u] >= pb.n_cap * wpr) {
         err |= ERR_OOM;
         continue;
       }
-      int64_t R[MS];
+      int64_t R[MS], L[MS];
 #pragma unroll
-      for (int s = 0; s < MS; ++s) R[s] = s < ns ? pr.part[(uint64_t)gi * ns + s] : 0;
-      int64_t L[MS];
-#pragma unroll
-      for (int s = 0; s < MS; ++s) L[s] = s < ns ? (int64_t)it[1 + s] : 0;
+      for (int s = 0; s < MS; ++s) {
+        R[s] = Rq[u][s];
+        L[s] = Lq[u][s];
+      }
       combine_row<MS>(prog, R, L);
       const uint64_t ob = out_base + o;
       if (ob >= out_cap) {
@@ -594,6 +642,7 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit(Batch bt, Program pr
       for (int jj = 0; jj < kMaxAggs; ++jj)  // static indices: the column pointers stay in registers
         if (jj < prog.n_out) out.agg[jj][ob] = out_value_reg<MS>(prog, jj, R);
       if (out.form) out.form[ob] = out_form_reg<MS>(prog, R);
+    }
     }
   }
   if (err) atomicOr(&sc->err, err);

@@ -142,7 +142,11 @@ def generate_torch(cfg: Config, n, device="cuda", seed=None, start=0, total=None
     ts = base + torch.randint(0, cfg.jitter, (n,), device=device, generator=g, dtype=torch.int64)
     lo, hi = cfg.vrange
     if cfg.col_type == abi.HSG_F64:
-        v = torch.round((torch.rand(n, device=device, generator=g, dtype=torch.float64) * (hi - lo) + lo) * 1000) / 1000
+        m = torch.round((torch.rand(n, device=device, generator=g, dtype=torch.float64) * (hi - lo) + lo) * 1000)
+        # a tensor divisor: true division (a scalar one becomes a multiply by
+        # its rounded reciprocal on the GPU), so every value is the double a
+        # 3-decimal JSON literal parses to, as numpy's round(x, 3) gives
+        v = m / torch.full_like(m, 1000.0)
     else:
         v = torch.randint(int(lo), int(hi) + 1, (n,), device=device, generator=g, dtype=torch.int64)
     return {"key_id": key, "ts": ts, "cols": [v]}
