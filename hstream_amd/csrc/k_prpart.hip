@@ -154,6 +154,14 @@ __global__ __launch_bounds__(kPrNT) void k_pr_local(Program prog, PartParams pp,
   uint32_t b;
   uint64_t r0, r1;
   if (!pr_chunk(pp, pb, b, r0, r1)) return;  // uniform
+  uint64_t ck = phase_clock(), c_rec = 0, c_ins = 0, c_sort = 0, c_scan = 0;
+  auto lap = [&](uint64_t &acc) {
+    if constexpr (kPhaseClocks) {
+      const uint64_t c = phase_clock();
+      acc += c - ck;
+      ck = c;
+    }
+  };
   const bool pk = sc->packed != 0;
   const int W = pk ? pp.words - 1 : pp.words;
   const int C = pp.words - 2 - pp.has_seq;
@@ -177,6 +185,7 @@ __global__ __launch_bounds__(kPrNT) void k_pr_local(Program prog, PartParams pp,
   }
   uint32_t P;
   const uint32_t pbase = pr_block_excl(nw[0] + nw[1], sw, P);  // (barrier inside: the table clear is seen)
+  lap(c_rec);
   // 2) groups into the LDS table; pair p = (slot << 16 | p) for the sort
   uint32_t p = pbase;
 #pragma unroll
@@ -200,6 +209,7 @@ __global__ __launch_bounds__(kPrNT) void k_pr_local(Program prog, PartParams pp,
     }
   }
   __syncthreads();
+  lap(c_ins);
 
   // 3) stable LSD radix sort of the pairs by slot (two 6-bit digits). Wave w
   // ranks positions [w * 128, w * 128 + 128) in two rounds of 64 lanes, so
@@ -246,6 +256,7 @@ __global__ __launch_bounds__(kPrNT) void k_pr_local(Program prog, PartParams pp,
     dst = t;
   }
   const uint32_t *sorted = src;
+  lap(c_sort);
 
   // 4) segmented inclusive scan in sorted order, thread t: positions 2t, 2t+1
   int64_t e[2][MS];
@@ -347,6 +358,7 @@ __global__ __launch_bounds__(kPrNT) void k_pr_local(Program prog, PartParams pp,
     pr.ccnt[blockIdx.x] = heads;
   }
   __syncthreads();
+  lap(c_scan);
   const uint32_t cbase = s_cbase;
   // 5) each pair's inclusive prefix at its bucket-major pair position; each
   // group's last prefix (its chunk total) and key as the partial
@@ -381,6 +393,20 @@ __global__ __launch_bounds__(kPrNT) void k_pr_local(Program prog, PartParams pp,
 #pragma unroll
       for (int s = 0; s < MS; ++s)
         if (s < ns) pr.part[(uint64_t)gi * ns + s] = run[s];
+    }
+  }
+  if (kPhaseClocks) {  // phase clocks (100 MHz), PHASES=1 builds with HSG_PHASES set
+    __syncthreads();
+    uint64_t c_out = 0;
+    lap(c_out);
+    if (threadIdx.x == 0) {
+      atomicAdd((unsigned long long *)&sc->scratch[24], (unsigned long long)c_rec);
+      atomicAdd((unsigned long long *)&sc->scratch[25], (unsigned long long)c_ins);
+      atomicAdd((unsigned long long *)&sc->scratch[26], (unsigned long long)c_sort);
+      atomicAdd((unsigned long long *)&sc->scratch[27], (unsigned long long)c_scan);
+      atomicAdd((unsigned long long *)&sc->scratch[28], (unsigned long long)c_out);
+      atomicAdd((unsigned long long *)&sc->scratch[29], 0ull);
+      atomicAdd((unsigned long long *)&sc->scratch[30], 1ull);
     }
   }
 }
@@ -518,10 +544,14 @@ __global__ __launch_bounds__(256) void k_pr_carry(Program prog, TwParams p, Part
 }
 
 // One workgroup per kPrEmitRecs arrival-order records, in rounds of
-// kPrEmitThreads consecutive records (record = round base + thread: the lanes
-// read the batch and write the changelog columns coalesced): window runs as
-// the partition computed them, output positions (exclusive prefix of the
-// accepted pairs in arrival order), rows.
+// kPrEmitThreads consecutive records. A round's rows are consecutive in the
+// changelog (its records' accepted pairs in arrival order), so after each
+// thread has found its record's window run and the round's prefix, the rows
+// are written row-parallel: thread t writes rows t, t + NT, ... of the round,
+// each column store of a wave covering 64 consecutive rows (a record-per-
+// thread loop over its windows stored 8-byte pieces 12 rows apart: partial
+// lines that the L2 could not merge before writing them back). A row finds
+// its record by a binary search over the round's record offsets in LDS.
 constexpr int kPrEmitThreads = 1024;
 constexpr int kPrEmitRounds = kPrEmitRecs / kPrEmitThreads;
 static_assert(kPrEmitRecs % kPartTileRecs == 0 && kPrEmitRounds * kPrEmitThreads == kPrEmitRecs, "emit tile");
@@ -533,6 +563,9 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit(Batch bt, Program pr
                                                             const int64_t *__restrict__ seq, OutCols out,
                                                             uint64_t out_base, uint64_t out_cap, DevScalars *sc) {
   __shared__ uint32_t sw[kPrEmitThreads / 64];
+  __shared__ uint32_t roff[kPrEmitThreads + 1];  // round-relative first row of each record
+  __shared__ uint32_t rpos[kPrEmitThreads];      // its partitioned position
+  __shared__ uint32_t rkey[kPrEmitThreads], rwin[kPrEmitThreads];
   if (sc->redo) return;  // uniform
   const int64_t k_epoch = sc->k_epoch;
   const int64_t *wm = rec_wm ? rec_wm : (sc->no_late ? nullptr : pb.wm);
@@ -544,8 +577,9 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit(Batch bt, Program pr
   // counts, scanned); the rounds then advance it by their pair totals
   uint64_t base = pr.tpoff[(uint64_t)blockIdx.x * (kPrEmitRecs / kPartTileRecs)];
   for (int rd = 0; rd < kPrEmitRounds; ++rd) {
-    const uint64_t i = (uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)rd * kPrEmitThreads + threadIdx.x;
-    if ((uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)rd * kPrEmitThreads >= bt.n) break;  // uniform
+    const uint64_t i0 = (uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)rd * kPrEmitThreads;
+    if (i0 >= bt.n) break;  // uniform
+    const uint64_t i = i0 + threadIdx.x;
     uint32_t a = 0, n = 0, key = HSG_KEY_NONE;
     if (i < bt.n) {
       key = bt.key[i];
@@ -573,77 +607,87 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit(Batch bt, Program pr
     const uint32_t incl = (uint32_t)wave_incl_sum((uint64_t)n);
     if (lane == 63) sw[wv] = incl;
     lds_barrier();
-    uint64_t o = base + incl - n, tot = 0;
+    uint32_t before = incl - n, tot = 0;
     for (int k = 0; k < kPrEmitThreads / 64; ++k) {
-      o += k < wv ? sw[k] : 0u;
+      before += k < wv ? sw[k] : 0u;
       tot += sw[k];
     }
-    lds_barrier();  // sw is rewritten by the next round
+    roff[threadIdx.x] = before;
+    if (threadIdx.x == kPrEmitThreads - 1) roff[kPrEmitThreads] = before + n;
+    rpos[threadIdx.x] = n ? pr.pos[i] : 0u;
+    rkey[threadIdx.x] = key;
+    rwin[threadIdx.x] = a;
+    lds_barrier();
+    // rows of the round, row-parallel: q -> its record (the last record whose
+    // first row is <= q), window j = q - first row
+    constexpr int EQ = MS <= 4 ? 4 : 2;  // rows per thread with their loads in flight together
+    for (uint32_t q0 = 0; q0 < tot; q0 += (uint32_t)kPrEmitThreads * EQ) {
+      uint32_t rr[EQ], jj[EQ], gq[EQ];
+      int64_t Lq[EQ][MS], Rq[EQ][MS];
+#pragma unroll
+      for (int u = 0; u < EQ; ++u) {
+        const uint32_t q = q0 + (uint32_t)u * kPrEmitThreads + threadIdx.x;
+        uint32_t lo = 0, hi = kPrEmitThreads;  // roff[lo] <= q < roff[hi]
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (roff[mid] <= q) lo = mid;
+          else hi = mid;
+        }
+        rr[u] = lo;
+        jj[u] = q - roff[lo];
+        const bool ok = q < tot;
+        const uint64_t pos = rpos[lo];
+        const uint64_t *it = pr.inter + (ok ? (pos * wpr + jj[u]) * rw : 0);
+        gq[u] = ok ? (uint32_t)it[0] : 0u;
+#pragma unroll
+        for (int s = 0; s < MS; ++s) Lq[u][s] = (ok && s < ns) ? (int64_t)it[1 + s] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < EQ; ++u) {
+        const uint32_t q = q0 + (uint32_t)u * kPrEmitThreads + threadIdx.x;
+        const bool ok = q < tot && (uint64_t)gq[u] < pb.n_cap * wpr;
+#pragma unroll
+        for (int s = 0; s < MS; ++s) Rq[u][s] = (ok && s < ns) ? pr.part[(uint64_t)gq[u] * ns + s] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < EQ; ++u) {
+        const uint32_t q = q0 + (uint32_t)u * kPrEmitThreads + threadIdx.x;
+        if (q >= tot) break;
+        if ((uint64_t)gq[u] >= pb.n_cap * wpr || rpos[rr[u]] >= pb.n_cap) {  // cannot happen
+          err |= ERR_OOM;
+          continue;
+        }
+        int64_t R[MS], L[MS];
+#pragma unroll
+        for (int s = 0; s < MS; ++s) {
+          R[s] = Rq[u][s];
+          L[s] = Lq[u][s];
+        }
+        combine_row<MS>(prog, R, L);
+        const uint64_t ob = out_base + base + q;
+        if (ob >= out_cap) {
+          err |= ERR_OOM;
+          continue;
+        }
+        const uint64_t irec = i0 + rr[u];
+        out.key[ob] = rkey[rr[u]];
+        int64_t ws = 0, we = 0;
+        if (p.kind != HSG_UNWINDOWED) {
+          const int64_t k = k_epoch + (int64_t)(rwin[rr[u]] + jj[u]);
+          ws = (int64_t)((uint64_t)k * (uint64_t)p.adv);
+          we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
+        }
+        out.ws[ob] = ws;
+        out.we[ob] = we;
+        out.src[ob] = seq ? seq[irec] : (int64_t)(p.rec_base + irec);
+#pragma unroll
+        for (int c = 0; c < kMaxAggs; ++c)  // static indices: the column pointers stay in registers
+          if (c < prog.n_out) out.agg[c][ob] = out_value_reg<MS>(prog, c, R);
+        if (out.form) out.form[ob] = out_form_reg<MS>(prog, R);
+      }
+    }
     base += tot;
-    if (!n) continue;
-    const uint64_t pos = pr.pos[i];
-    const int64_t src = seq ? seq[i] : (int64_t)(p.rec_base + i);
-    if (pos >= pb.n_cap) {  // cannot happen: the scatter placed every record with a window
-      err |= ERR_OOM;
-      continue;
-    }
-    // the record's windows EJ at a time, every load of a group in flight
-    // together (its pairs' partial indices and prefixes, then the carries):
-    // a window after the other waited two round trips each (C3: 12 windows)
-    constexpr int EJ = MS <= 2 ? 4 : MS <= 4 ? 2 : 1;
-    for (uint32_t j0 = 0; j0 < n; j0 += EJ) {
-    uint32_t gq[EJ];
-    int64_t Lq[EJ][MS], Rq[EJ][MS];
-#pragma unroll
-    for (int u = 0; u < EJ; ++u) {
-      const uint32_t j = j0 + u;
-      const uint64_t *it = pr.inter + (pos * wpr + (j < n ? j : 0)) * rw;
-      gq[u] = j < n ? (uint32_t)it[0] : 0u;
-#pragma unroll
-      for (int s = 0; s < MS; ++s) Lq[u][s] = (j < n && s < ns) ? (int64_t)it[1 + s] : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < EJ; ++u) {
-      const bool ok = j0 + u < n && (uint64_t)gq[u] < pb.n_cap * wpr;
-#pragma unroll
-      for (int s = 0; s < MS; ++s) Rq[u][s] = (ok && s < ns) ? pr.part[(uint64_t)gq[u] * ns + s] : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < EJ; ++u, ++o) {
-      const uint32_t j = j0 + u;
-      if (j >= n) break;
-      if ((uint64_t)gq[u] >= pb.n_cap * wpr) {
-        err |= ERR_OOM;
-        continue;
-      }
-      int64_t R[MS], L[MS];
-#pragma unroll
-      for (int s = 0; s < MS; ++s) {
-        R[s] = Rq[u][s];
-        L[s] = Lq[u][s];
-      }
-      combine_row<MS>(prog, R, L);
-      const uint64_t ob = out_base + o;
-      if (ob >= out_cap) {
-        err |= ERR_OOM;
-        continue;
-      }
-      out.key[ob] = key;
-      int64_t ws = 0, we = 0;
-      if (p.kind != HSG_UNWINDOWED) {
-        const int64_t k = k_epoch + (int64_t)(a + j);
-        ws = (int64_t)((uint64_t)k * (uint64_t)p.adv);
-        we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
-      }
-      out.ws[ob] = ws;
-      out.we[ob] = we;
-      out.src[ob] = src;
-#pragma unroll
-      for (int jj = 0; jj < kMaxAggs; ++jj)  // static indices: the column pointers stay in registers
-        if (jj < prog.n_out) out.agg[jj][ob] = out_value_reg<MS>(prog, jj, R);
-      if (out.form) out.form[ob] = out_form_reg<MS>(prog, R);
-    }
-    }
+    lds_barrier();  // sw / roff / rpos are rewritten by the next round
   }
   if (err) atomicOr(&sc->err, err);
 }

@@ -14,7 +14,8 @@ from hstream_amd.engine import Engine
 cfg = datagen.CONFIGS[sys.argv[1]]
 nb = int(sys.argv[2]) if len(sys.argv) > 2 else 12
 eng = Engine(device=0, batch_capacity=cfg.batch)
-op = eng.op(cfg.spec(abi.HSG_EMIT_NONE))
+emit = {"none": abi.HSG_EMIT_NONE, "per_record": abi.HSG_EMIT_PER_RECORD}[sys.argv[3] if len(sys.argv) > 3 else "none"]
+op = eng.op(cfg.spec(emit, out_capacity=cfg.batch * 16 if emit == abi.HSG_EMIT_PER_RECORD else 0))
 wm = -1
 for bi in range(nb):
     s = bi * cfg.batch
@@ -22,5 +23,7 @@ for bi in range(nb):
     torch.cuda.synchronize()
     print(f"batch {bi}", file=sys.stderr, flush=True)
     wm = op.push(h["key_id"], h["ts"], h["cols"], None, watermark=wm)
+    if emit != abi.HSG_EMIT_NONE:
+        op.drain()
 op.close()
 eng.close()
