@@ -492,6 +492,14 @@ def per_record_block(eng, cfg, keys, ts, cols, pieces, args):
     n_rank = sum(m for _, m in pieces)
     roof = roofline(st0, st1, spec, emit)
     roof["kernel"] = pipeline_name(cfg, "per_record")
+    if not (args.records or args.batch):
+        # the committed PMC summary of this pipeline (tools/traffic.sh <cfg>_pr --emit per_record)
+        import glob
+        paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"traffic_{cfg.name.lower()}_pr.json")))
+        if paths:
+            with open(paths[-1]) as f:
+                roof["traffic"] = int(json.load(f)["hbm_bytes_per_batch"])
+            roof["traffic_source"] = os.path.relpath(paths[-1], ROOT)
     out = {"value": round(n_rank * k / el, 1), "unit": "records/s", "steps": k,
            "ms_per_step": round(el * 1e3 / k, 3), "emit": "per_record",
            "rows_per_step": int((st1["pairs_total"] - st0["pairs_total"]) / k), "roofline": roof}

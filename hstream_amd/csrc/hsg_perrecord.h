@@ -47,6 +47,8 @@ struct PrPart {
   uint64_t *partial;  // scan partials
   int64_t *fin;       // one-window ops (k_pr_bucket): [n][ns] each record's changelog state, at its
                       // partitioned position
+  uint64_t *krec;     // multi-window ops: [n][words] the partitioned records, key-grouped in each bucket
+  uint32_t *kpos;     // [n] partitioned position -> its position in krec
 };
 
 void launch_pr_count(hipStream_t s, const Batch &b, const TwParams &p, const TwTable &t, const int64_t *tprefix,

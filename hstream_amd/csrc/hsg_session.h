@@ -98,7 +98,7 @@ struct SessPart {
   uint32_t *groups;    // [n][4] key groups: key, first record in srec, records, -
   uint8_t *done;       // [n / 256 + 1] apply blocks done (resumable)
   uint64_t *bigmask;   // [nb] sub-buckets left to k_ss_merge_big
-  uint16_t *sidx;      // [n] per bucket: its record indices grouped by sub-bucket
+  uint64_t *scopy;     // [n][words] per bucket: its records grouped by sub-bucket (k_ss_sort)
   uint32_t *gsparse;   // [n][4] group records at their sub-bucket's record positions
   uint64_t *reloc;     // [n][3] relocated lists (old row, new row, rows of the prefix to copy)
 };

@@ -139,6 +139,97 @@ __device__ inline uint32_t pr_block_excl(uint32_t v, uint32_t *sw, uint32_t &tot
   return before + incl - v;
 }
 
+// Multi-window ops: each bucket's records regrouped by key, arrival order kept
+// within a key (a stable LSD radix sort on 12 key-hash bits below the bucket
+// bits, two 6-bit digits, in LDS). The partition leaves a bucket in tile
+// order, so a k_pr_local chunk (kPrPairs / wpr records) holds records of as
+// many different keys: for C3 (12 windows, 16 records per key per batch)
+// ~2000 partials per chunk for ~2000 pairs, each a find / claim and a
+// read-modify-write of an HBM row in k_pr_carry. Key-grouped, a chunk covers
+// ~10 keys' records and makes ~270 partials. kpos maps each partitioned
+// position to its place in krec (the emit's pair positions). A bucket
+// larger than the LDS sort is copied as it is.
+constexpr int kKsMax = 8192;  // records a workgroup sorts in LDS
+__global__ __launch_bounds__(kPrNT) void k_pr_keysort(PartParams pp, PartBuffers pb, PrPart pr, DevScalars *sc) {
+  __shared__ uint32_t ka[kKsMax], kb[kKsMax];  // hash digits << 16 | record (bucket-relative)
+  __shared__ uint32_t dcnt[kPrNW][64];
+  __shared__ uint32_t sw[kPrNW];
+  if (sc->redo) return;  // uniform
+  const uint32_t b = blockIdx.x;
+  const uint64_t b0 = pb.bstart[b], b1 = pb.bstart[b + 1];
+  const uint32_t m = (uint32_t)(b1 - b0);
+  const int W = sc->packed ? pp.words - 1 : pp.words;
+  const int hs = pp.bshift + pp.np_log2;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (m > (uint32_t)kKsMax) {  // uniform: copied in partition order
+    for (uint64_t w = threadIdx.x; w < (uint64_t)m * W; w += kPrNT) pr.krec[b0 * W + w] = pb.rec[b0 * W + w];
+    for (uint32_t r = threadIdx.x; r < m; r += kPrNT) pr.kpos[b0 + r] = (uint32_t)(b0 + r);
+    return;
+  }
+  for (uint32_t r = threadIdx.x; r < m; r += kPrNT) {
+    const uint32_t key = (uint32_t)pb.rec[(b0 + r) * W];
+    const uint32_t h = (uint32_t)((key_hash(key) << hs) >> (64 - 12));
+    ka[r] = (h << 16) | r;
+  }
+  __syncthreads();
+  // stable LSD radix sort (2 x 6 bits): wave w ranks positions w*RW .. in
+  // rounds of 64 lanes, digit-major wave-minor offsets (as k_pr_local)
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t RW = (m + kPrNW - 1) / kPrNW;  // positions per wave, contiguous
+  uint32_t *src = ka, *dst = kb;
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    const int shift = 16 + 6 * pass;
+    for (int k = threadIdx.x; k < kPrNW * 64; k += kPrNT) (&dcnt[0][0])[k] = 0;
+    __syncthreads();
+    for (uint32_t q0 = 0; q0 < RW; q0 += 64) {  // count (wave-local, in order)
+      const uint32_t q = wv * RW + q0 + lane;
+      const bool ok = q0 + lane < RW && q < m;
+      const uint32_t dig = ok ? (src[q] >> shift) & 63u : 64u;
+      uint64_t mm = __ballot(ok);
+#pragma unroll
+      for (int bit = 0; bit < 6; ++bit) {
+        const bool x = (dig >> bit) & 1u;
+        const uint64_t bb = __ballot(x);
+        mm &= x ? bb : ~bb;
+      }
+      if (ok && (mm >> lane) == 1ull) dcnt[wv][dig] += (uint32_t)__popcll(mm);
+    }
+    __syncthreads();
+    const int d = threadIdx.x / kPrNW, ww = threadIdx.x % kPrNW;
+    uint32_t tot;
+    const uint32_t off = pr_block_excl(dcnt[ww][d], sw, tot);
+    dcnt[ww][d] = off;
+    __syncthreads();
+    for (uint32_t q0 = 0; q0 < RW; q0 += 64) {  // place (the same order: stable)
+      const uint32_t q = wv * RW + q0 + lane;
+      const bool ok = q0 + lane < RW && q < m;
+      const uint32_t v = ok ? src[q] : 0u;
+      const uint32_t dig = ok ? (v >> shift) & 63u : 64u;
+      uint64_t mm = __ballot(ok);
+#pragma unroll
+      for (int bit = 0; bit < 6; ++bit) {
+        const bool x = (dig >> bit) & 1u;
+        const uint64_t bb = __ballot(x);
+        mm &= x ? bb : ~bb;
+      }
+      const uint32_t before = ok ? dcnt[wv][dig] : 0u;
+      if (ok) dst[before + (uint32_t)__popcll(mm & lt)] = v;
+      if (ok && (mm >> lane) == 1ull) dcnt[wv][dig] = before + (uint32_t)__popcll(mm);
+    }
+    __syncthreads();
+    uint32_t *t = src;
+    src = dst;
+    dst = t;
+  }
+  // records to their key-grouped places, and the position map
+  for (uint32_t q = threadIdx.x; q < m; q += kPrNT) pr.kpos[b0 + (src[q] & 0xFFFFu)] = (uint32_t)(b0 + q);
+  for (uint64_t w = threadIdx.x; w < (uint64_t)m * W; w += kPrNT) {
+    const uint32_t q = (uint32_t)(w / W), k = (uint32_t)(w - (uint64_t)q * W);
+    pr.krec[(b0 + q) * W + k] = pb.rec[(b0 + (src[q] & 0xFFFFu)) * W + k];
+  }
+}
+
 template <int MS>
 __global__ __launch_bounds__(kPrNT) void k_pr_local(Program prog, PartParams pp, PartBuffers pb, PrPart pr,
                                                     uint32_t wpr, DevScalars *sc) {
@@ -614,7 +705,7 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit(Batch bt, Program pr
     }
     roff[threadIdx.x] = before;
     if (threadIdx.x == kPrEmitThreads - 1) roff[kPrEmitThreads] = before + n;
-    rpos[threadIdx.x] = n ? pr.pos[i] : 0u;
+    rpos[threadIdx.x] = n ? pr.kpos[pr.pos[i]] : 0u;  // (k_pr_keysort's place of the record)
     rkey[threadIdx.x] = key;
     rwin[threadIdx.x] = a;
     lds_barrier();
@@ -1345,8 +1436,11 @@ static void pr_launch(hipStream_t s, const Batch &b, const Program &prog, const 
     return;
   }
   const dim3 g((unsigned)(nb + b.n / pp.chunk + 1));
-  hipLaunchKernelGGL(k_pr_local<MS>, g, dim3(kPrNT), 0, s, prog, pp, pb, pr, wpr, sc);
-  hipLaunchKernelGGL(k_pr_carry<MS>, dim3((unsigned)nb), dim3(256), 0, s, prog, p, pp, t, pb, pr, sc);
+  hipLaunchKernelGGL(k_pr_keysort, dim3((unsigned)nb), dim3(kPrNT), 0, s, pp, pb, pr, sc);
+  PartBuffers kpb = pb;
+  kpb.rec = pr.krec;  // the chunks read the key-grouped records
+  hipLaunchKernelGGL(k_pr_local<MS>, g, dim3(kPrNT), 0, s, prog, pp, kpb, pr, wpr, sc);
+  hipLaunchKernelGGL(k_pr_carry<MS>, dim3((unsigned)nb), dim3(256), 0, s, prog, p, pp, t, kpb, pr, sc);
   const uint64_t tiles = (b.n + kPrEmitRecs - 1) / kPrEmitRecs;
   hipLaunchKernelGGL(k_pr_emit<MS>, dim3((unsigned)tiles), dim3(kPrEmitThreads), 0, s, b, prog, p, pp, pb, pr, wpr,
                      rec_wm, seq, out, out_base, out_cap, sc);

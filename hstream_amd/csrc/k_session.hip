@@ -1007,9 +1007,9 @@ __global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Pr
   const uint64_t *recs = sp.rec + r0 * W;
   const int sl = ss_sub_log2(m), hs = bshift + np_log2;
   const int nsub = 1 << sl;
-  // the bucket's record indices grouped by sub-bucket (sp.sidx, the bucket's
-  // own range): every later pass visits only its sub-bucket's records
-  uint16_t *sidx = sp.sidx + r0;
+  // the bucket's records copied grouped by sub-bucket (sp.scopy, the bucket's
+  // own range): every later pass reads only its sub-bucket's records
+  uint64_t *scopy = sp.scopy + r0 * W;
   if (threadIdx.x < (1 << kSoMaxSubLog2)) {
     L.subcnt[threadIdx.x] = 0;
     L.subgrp[threadIdx.x] = 0;
@@ -1056,25 +1056,35 @@ __global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Pr
   __syncthreads();
   if (threadIdx.x < (1 << kSoMaxSubLog2)) L.subcnt[threadIdx.x] = 0;
   __syncthreads();
+  // the records copied grouped by sub-bucket: each sub-bucket then reads its
+  // records contiguously (no per-record index, no gather)
+  constexpr int B2 = W <= 3 ? 4 : 2;
   if (indexable)
-    for (uint64_t i0 = 0; i0 < m; i0 += (uint64_t)kSoNT * B) {
-      uint32_t q[B];
+    for (uint64_t i0 = 0; i0 < m; i0 += (uint64_t)kSoNT * B2) {
+      uint64_t v[B2][W];
 #pragma unroll
-      for (int u = 0; u < B; ++u) {
+      for (int u = 0; u < B2; ++u) {
         const uint64_t i = i0 + (uint64_t)u * kSoNT + threadIdx.x;
-        q[u] = i < m ? ss_sub((uint32_t)recs[i * W], hs, sl) : ~0u;
+#pragma unroll
+        for (int w = 0; w < W; ++w) v[u][w] = i < m ? recs[i * W + w] : 0;
       }
 #pragma unroll
-      for (int u = 0; u < B; ++u) {
-        const bool in = q[u] != ~0u;
-        const uint64_t pm = peers(q[u], in);
+      for (int u = 0; u < B2; ++u) {
+        const uint64_t i = i0 + (uint64_t)u * kSoNT + threadIdx.x;
+        const uint32_t q = i < m ? ss_sub((uint32_t)v[u][0], hs, sl) : ~0u;
+        const bool in = q != ~0u;
+        const uint64_t pm = peers(q, in);
         const uint32_t rk = (uint32_t)__popcll(pm & lt);
         // the group's lowest lane reserves for the group; the others read its base
         uint32_t base = 0;
-        if (in && rk == 0) base = atomicAdd(&L.subcnt[q[u]], (uint32_t)__popcll(pm));
+        if (in && rk == 0) base = atomicAdd(&L.subcnt[q], (uint32_t)__popcll(pm));
         const int leader = in ? __ffsll((long long)pm) - 1 : lane0;
         base = __shfl(base, leader, 64);
-        if (in) sidx[L.suboff[q[u]] + base + rk] = (uint16_t)(i0 + (uint64_t)u * kSoNT + threadIdx.x);
+        if (in) {
+          uint64_t *d = scopy + (uint64_t)(L.suboff[q] + base + rk) * W;
+#pragma unroll
+          for (int w = 0; w < W; ++w) d[w] = v[u][w];
+        }
       }
     }
   __syncthreads();
@@ -1089,7 +1099,7 @@ __global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Pr
       bigmask |= 1ull << sub;
       continue;
     }
-    const uint16_t *lst = sidx + L.suboff[sub];
+    const uint64_t *lst = scopy + (uint64_t)L.suboff[sub] * W;
     uint64_t ca = phase_clock();
     // 1. keys of the sub-bucket into the LDS table, records per key; the
     // records' words stay in registers for the placement
@@ -1106,9 +1116,8 @@ __global__ __launch_bounds__(kSoNT) void k_ss_sort(SessParams p, SessTable t, Pr
 #pragma unroll
     for (int u = 0; u < RP; ++u) {
       const uint32_t j = u * kSoNT + threadIdx.x;
-      const uint64_t i = j < m2 ? lst[j] : 0;
 #pragma unroll
-      for (int w = 0; w < W; ++w) rw[u][w] = j < m2 ? recs[i * W + w] : 0;
+      for (int w = 0; w < W; ++w) rw[u][w] = j < m2 ? lst[(uint64_t)j * W + w] : 0;
     }
     lds_barrier();
     uint32_t hslot[RP];

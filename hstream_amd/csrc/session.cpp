@@ -105,7 +105,7 @@ static uint64_t ss_part_layout(uint64_t n, int words, SessPart *sp, char *m) {
   x.srec = (uint64_t *)take(n * (uint64_t)words * 8);
   x.groups = (uint32_t *)take(n * 16);
   x.done = (uint8_t *)take(n / 256 + 2);
-  x.sidx = (uint16_t *)take(n * 2);
+  x.scopy = (uint64_t *)take(n * (uint64_t)words * 8);
   x.gsparse = (uint32_t *)take(n * 16);
   x.reloc = (uint64_t *)take(n * 24);
   if (sp) *sp = x;

@@ -120,6 +120,8 @@ int perrecord_part_init(OpDevice &d, const hsg_op_config &cfg, const Program &pr
     x.counter = c.take<uint64_t>(8);
     x.partial = c.take<uint64_t>(scan_partials_needed(tiles) + 8);
     x.fin = c.take<int64_t>(wpr == 1 ? n * ns : 1);
+    x.krec = c.take<uint64_t>(wpr == 1 ? 1 : n * (uint64_t)part_words(cfg.n_cols, true));
+    x.kpos = c.take<uint32_t>(wpr == 1 ? 1 : n);
   };
   Carve probe{nullptr};
   PrPart tmp;
