@@ -43,12 +43,15 @@ struct PrPart {
   int64_t *part;      // [n * wpr][ns] each partial's chunk total, then its carry (the row before the chunk)
   uint32_t *cbase;    // [chunks] first partial of each k_pr_local chunk
   uint32_t *ccnt;     // [chunks] partials of each chunk
-  uint64_t *counter;  // partials allocated in this batch
+  uint64_t *counter;  // [8] per-batch device words: [1] != 0 = a bucket too large for k_pr_keysort
+                      // (the batch takes the chunked path); cleared before each batch
   uint64_t *partial;  // scan partials
   int64_t *fin;       // one-window ops (k_pr_bucket): [n][ns] each record's changelog state, at its
                       // partitioned position
   uint64_t *krec;     // multi-window ops: [n][words] the partitioned records, key-grouped in each bucket
   uint32_t *kpos;     // [n] partitioned position -> its position in krec
+  uint64_t *roff;     // [n] at krec positions: the record's first changelog row (k_pr_keys)
+  uint32_t *kidx;     // [n] at krec positions: the record's arrival index
 };
 
 void launch_pr_count(hipStream_t s, const Batch &b, const TwParams &p, const TwTable &t, const int64_t *tprefix,

@@ -141,15 +141,68 @@ __device__ inline uint32_t pr_block_excl(uint32_t v, uint32_t *sw, uint32_t &tot
 
 // Multi-window ops: each bucket's records regrouped by key, arrival order kept
 // within a key (a stable LSD radix sort on 12 key-hash bits below the bucket
-// bits, two 6-bit digits, in LDS). The partition leaves a bucket in tile
-// order, so a k_pr_local chunk (kPrPairs / wpr records) holds records of as
-// many different keys: for C3 (12 windows, 16 records per key per batch)
-// ~2000 partials per chunk for ~2000 pairs, each a find / claim and a
-// read-modify-write of an HBM row in k_pr_carry. Key-grouped, a chunk covers
-// ~10 keys' records and makes ~270 partials. kpos maps each partitioned
-// position to its place in krec (the emit's pair positions). A bucket
-// larger than the LDS sort is copied as it is.
-constexpr int kKsMax = 8192;  // records a workgroup sorts in LDS
+// bits, two 6-bit digits). k_pr_keys then replays a key's records from one
+// contiguous run. A bucket of up to kKsMax records sorts in LDS; up to
+// kKsBig in global scratch (the roff buffer, written only later by
+// k_pr_offs: record indices only, each digit recomputed from the record's
+// key); a larger bucket (a very hot key) is copied as it is and sets
+// pr.counter[1]: the batch then takes the chunked path, whose chunks also
+// read the key-grouped records. kpos maps each partitioned position to its
+// place in krec.
+constexpr int kKsMax = 16384;  // records a workgroup sorts in LDS (2 x 64 KB)
+constexpr int kKsBig = 65536;  // records it sorts in global scratch
+// the 12 key-hash bits below the bucket bits (hs = bshift + np_log2)
+__device__ inline uint32_t ks_digits(uint32_t key, int hs) { return (uint32_t)((key_hash(key) << hs) >> (64 - 12)); }
+
+// one stable LSD pass over m entries src -> dst (6-bit digit `dig(v)`): wave w
+// ranks positions [w * RW, (w + 1) * RW) in rounds of 64 lanes, digit-major
+// wave-minor offsets (as k_pr_local)
+template <class D>
+__device__ inline void ks_pass(const uint32_t *src, uint32_t *dst, uint32_t m, D dig, uint32_t (&dcnt)[kPrNW][64],
+                               uint32_t *sw) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t RW = (m + kPrNW - 1) / kPrNW;
+  for (int k = threadIdx.x; k < kPrNW * 64; k += kPrNT) (&dcnt[0][0])[k] = 0;
+  __syncthreads();
+  for (uint32_t q0 = 0; q0 < RW; q0 += 64) {  // count (wave-local, in order)
+    const uint32_t q = wv * RW + q0 + lane;
+    const bool ok = q0 + lane < RW && q < m;
+    const uint32_t d = ok ? dig(src[q]) : 64u;
+    uint64_t mm = __ballot(ok);
+#pragma unroll
+    for (int bit = 0; bit < 6; ++bit) {
+      const bool x = (d >> bit) & 1u;
+      const uint64_t bb = __ballot(x);
+      mm &= x ? bb : ~bb;
+    }
+    if (ok && (mm >> lane) == 1ull) dcnt[wv][d] += (uint32_t)__popcll(mm);
+  }
+  __syncthreads();
+  const int dd = threadIdx.x / kPrNW, ww = threadIdx.x % kPrNW;
+  uint32_t tot;
+  const uint32_t off = pr_block_excl(dcnt[ww][dd], sw, tot);
+  dcnt[ww][dd] = off;
+  __syncthreads();
+  for (uint32_t q0 = 0; q0 < RW; q0 += 64) {  // place (the same order: stable)
+    const uint32_t q = wv * RW + q0 + lane;
+    const bool ok = q0 + lane < RW && q < m;
+    const uint32_t v = ok ? src[q] : 0u;
+    const uint32_t d = ok ? dig(v) : 64u;
+    uint64_t mm = __ballot(ok);
+#pragma unroll
+    for (int bit = 0; bit < 6; ++bit) {
+      const bool x = (d >> bit) & 1u;
+      const uint64_t bb = __ballot(x);
+      mm &= x ? bb : ~bb;
+    }
+    const uint32_t before = ok ? dcnt[wv][d] : 0u;
+    if (ok) dst[before + (uint32_t)__popcll(mm & lt)] = v;
+    if (ok && (mm >> lane) == 1ull) dcnt[wv][d] = before + (uint32_t)__popcll(mm);
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(kPrNT) void k_pr_keysort(PartParams pp, PartBuffers pb, PrPart pr, DevScalars *sc) {
   __shared__ uint32_t ka[kKsMax], kb[kKsMax];  // hash digits << 16 | record (bucket-relative)
   __shared__ uint32_t dcnt[kPrNW][64];
@@ -160,73 +213,37 @@ __global__ __launch_bounds__(kPrNT) void k_pr_keysort(PartParams pp, PartBuffers
   const uint32_t m = (uint32_t)(b1 - b0);
   const int W = sc->packed ? pp.words - 1 : pp.words;
   const int hs = pp.bshift + pp.np_log2;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (m > (uint32_t)kKsMax) {  // uniform: copied in partition order
-    for (uint64_t w = threadIdx.x; w < (uint64_t)m * W; w += kPrNT) pr.krec[b0 * W + w] = pb.rec[b0 * W + w];
+  const uint64_t *rec = pb.rec + b0 * (uint64_t)W;
+  if (m > (uint32_t)kKsBig) {  // uniform: copied in partition order, and the batch takes the chunked path
+    if (threadIdx.x == 0) __hip_atomic_store(&pr.counter[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint64_t w = threadIdx.x; w < (uint64_t)m * W; w += kPrNT) pr.krec[b0 * W + w] = rec[w];
     for (uint32_t r = threadIdx.x; r < m; r += kPrNT) pr.kpos[b0 + r] = (uint32_t)(b0 + r);
     return;
   }
-  for (uint32_t r = threadIdx.x; r < m; r += kPrNT) {
-    const uint32_t key = (uint32_t)pb.rec[(b0 + r) * W];
-    const uint32_t h = (uint32_t)((key_hash(key) << hs) >> (64 - 12));
-    ka[r] = (h << 16) | r;
-  }
-  __syncthreads();
-  // stable LSD radix sort (2 x 6 bits): wave w ranks positions w*RW .. in
-  // rounds of 64 lanes, digit-major wave-minor offsets (as k_pr_local)
-  const uint64_t lt = (1ull << lane) - 1ull;
-  const uint32_t RW = (m + kPrNW - 1) / kPrNW;  // positions per wave, contiguous
-  uint32_t *src = ka, *dst = kb;
-#pragma unroll 1
-  for (int pass = 0; pass < 2; ++pass) {
-    const int shift = 16 + 6 * pass;
-    for (int k = threadIdx.x; k < kPrNW * 64; k += kPrNT) (&dcnt[0][0])[k] = 0;
+  const uint32_t *order;  // bucket-relative record of each sorted position
+  uint32_t omask;
+  if (m <= (uint32_t)kKsMax) {  // uniform
+    for (uint32_t r = threadIdx.x; r < m; r += kPrNT) ka[r] = (ks_digits((uint32_t)rec[(uint64_t)r * W], hs) << 16) | r;
     __syncthreads();
-    for (uint32_t q0 = 0; q0 < RW; q0 += 64) {  // count (wave-local, in order)
-      const uint32_t q = wv * RW + q0 + lane;
-      const bool ok = q0 + lane < RW && q < m;
-      const uint32_t dig = ok ? (src[q] >> shift) & 63u : 64u;
-      uint64_t mm = __ballot(ok);
-#pragma unroll
-      for (int bit = 0; bit < 6; ++bit) {
-        const bool x = (dig >> bit) & 1u;
-        const uint64_t bb = __ballot(x);
-        mm &= x ? bb : ~bb;
-      }
-      if (ok && (mm >> lane) == 1ull) dcnt[wv][dig] += (uint32_t)__popcll(mm);
-    }
+    ks_pass(ka, kb, m, [](uint32_t v) { return (v >> 16) & 63u; }, dcnt, sw);
+    ks_pass(kb, ka, m, [](uint32_t v) { return (v >> 22) & 63u; }, dcnt, sw);
+    order = ka;
+    omask = 0xFFFFu;
+  } else {
+    uint32_t *ga = reinterpret_cast<uint32_t *>(pr.roff) + b0, *gb = ga + pb.n_cap;
+    for (uint32_t r = threadIdx.x; r < m; r += kPrNT) ga[r] = r;
     __syncthreads();
-    const int d = threadIdx.x / kPrNW, ww = threadIdx.x % kPrNW;
-    uint32_t tot;
-    const uint32_t off = pr_block_excl(dcnt[ww][d], sw, tot);
-    dcnt[ww][d] = off;
-    __syncthreads();
-    for (uint32_t q0 = 0; q0 < RW; q0 += 64) {  // place (the same order: stable)
-      const uint32_t q = wv * RW + q0 + lane;
-      const bool ok = q0 + lane < RW && q < m;
-      const uint32_t v = ok ? src[q] : 0u;
-      const uint32_t dig = ok ? (v >> shift) & 63u : 64u;
-      uint64_t mm = __ballot(ok);
-#pragma unroll
-      for (int bit = 0; bit < 6; ++bit) {
-        const bool x = (dig >> bit) & 1u;
-        const uint64_t bb = __ballot(x);
-        mm &= x ? bb : ~bb;
-      }
-      const uint32_t before = ok ? dcnt[wv][dig] : 0u;
-      if (ok) dst[before + (uint32_t)__popcll(mm & lt)] = v;
-      if (ok && (mm >> lane) == 1ull) dcnt[wv][dig] = before + (uint32_t)__popcll(mm);
-    }
-    __syncthreads();
-    uint32_t *t = src;
-    src = dst;
-    dst = t;
+    ks_pass(ga, gb, m, [&](uint32_t r) { return ks_digits((uint32_t)rec[(uint64_t)r * W], hs) & 63u; }, dcnt, sw);
+    ks_pass(gb, ga, m, [&](uint32_t r) { return (ks_digits((uint32_t)rec[(uint64_t)r * W], hs) >> 6) & 63u; }, dcnt,
+            sw);
+    order = ga;
+    omask = 0xFFFFFFFFu;
   }
   // records to their key-grouped places, and the position map
-  for (uint32_t q = threadIdx.x; q < m; q += kPrNT) pr.kpos[b0 + (src[q] & 0xFFFFu)] = (uint32_t)(b0 + q);
+  for (uint32_t q = threadIdx.x; q < m; q += kPrNT) pr.kpos[b0 + (order[q] & omask)] = (uint32_t)(b0 + q);
   for (uint64_t w = threadIdx.x; w < (uint64_t)m * W; w += kPrNT) {
     const uint32_t q = (uint32_t)(w / W), k = (uint32_t)(w - (uint64_t)q * W);
-    pr.krec[(b0 + q) * W + k] = pb.rec[(b0 + (src[q] & 0xFFFFu)) * W + k];
+    pr.krec[(b0 + q) * W + k] = rec[(uint64_t)(order[q] & omask) * W + k];
   }
 }
 
@@ -241,7 +258,7 @@ __global__ __launch_bounds__(kPrNT) void k_pr_local(Program prog, PartParams pp,
   __shared__ int64_t swv[kPrNW][MS];
   __shared__ uint32_t swf[kPrNW], swh[kPrNW];
   __shared__ uint32_t s_cbase;
-  if (sc->redo) return;  // uniform: the optimistic pass found late records (bucket starts are stale)
+  if (sc->redo || !pr.counter[1]) return;  // uniform: stale bucket starts / the batch takes k_pr_keys
   uint32_t b;
   uint64_t r0, r1;
   if (!pr_chunk(pp, pb, b, r0, r1)) return;  // uniform
@@ -511,7 +528,7 @@ template <int MS>
 __global__ __launch_bounds__(256) void k_pr_carry(Program prog, TwParams p, PartParams pp, TwTable t, PartBuffers pb,
                                                   PrPart pr, DevScalars *sc) {
   __shared__ uint64_t s_red[4], s_tch[4];
-  if (sc->redo) return;  // uniform
+  if (sc->redo || !pr.counter[1]) return;  // uniform
   const uint32_t b = blockIdx.x;
   const uint32_t c0 = pb.chunk_start[b], c1 = pb.chunk_start[b + 1];
   const int ns = prog.n_slots;
@@ -657,7 +674,7 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit(Batch bt, Program pr
   __shared__ uint32_t roff[kPrEmitThreads + 1];  // round-relative first row of each record
   __shared__ uint32_t rpos[kPrEmitThreads];      // its partitioned position
   __shared__ uint32_t rkey[kPrEmitThreads], rwin[kPrEmitThreads];
-  if (sc->redo) return;  // uniform
+  if (sc->redo || !pr.counter[1]) return;  // uniform
   const int64_t k_epoch = sc->k_epoch;
   const int64_t *wm = rec_wm ? rec_wm : (sc->no_late ? nullptr : pb.wm);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -907,6 +924,7 @@ struct PrRecRegs {
   __device__ uint32_t krel(uint32_t kbase) const {
     return pk ? kbase + (uint32_t)((r0 >> 32) & 0xFFFFull) : (uint32_t)(r0 >> 32);
   }
+  __device__ uint32_t nwin() const { return pk ? (uint32_t)((r0 >> 48) & 0xFFull) : (uint32_t)r1; }
   __device__ bool present(int c) const { return pk ? (r0 >> (56 + c)) & 1ull : (r1 >> (32 + c)) & 1ull; }
   __device__ int64_t word(int k) const {
     if (!REG && k >= kPrRegWords) return (int64_t)w[k];
@@ -1392,6 +1410,331 @@ __global__ __launch_bounds__(kE1NT) void k_pr_emit1(Batch bt, Program prog, TwPa
   if (err) atomicOr(&sc->err, err);
 }
 
+// ---------------------------------------------------------------------------
+// Multi-window ops when every bucket fits k_pr_keysort (the usual case; a
+// larger bucket sets pr.counter[1] and the batch takes k_pr_local /
+// k_pr_carry / k_pr_emit above instead): a key's records are contiguous in
+// krec, arrival order kept, so one wave replays them straight into its rows.
+//
+//   k_pr_offs  one workgroup per arrival tile: each record's first changelog
+//              row (exclusive prefix of accepted windows in arrival order) and
+//              its arrival index, written at its krec position.
+//   k_pr_keys  one workgroup per bucket, a wave per run of equal key digits
+//              (one key, rarely a few sharing the 12 bits): lane l owns window
+//              lo + l of the key's window range (one pass of 64 windows for a
+//              hopping key's ~2 x size / advance windows in a batch), finds /
+//              claims its HBM row, then the key's records in arrival order are
+//              broadcast one by one: the lanes of the record's windows fold it
+//              into their state and write its rows (consecutive in the
+//              changelog: one contiguous store per column). The states go back
+//              once per key. No chunk partials, no carries, no emit gathers.
+// ---------------------------------------------------------------------------
+constexpr int kPkNT = 256;  // k_pr_keys threads
+constexpr int kPkNW = kPkNT / 64;
+
+// record i's accepted window run in arrival order [a, a + n) (k_epoch-relative),
+// the same run as the partition passes (k_part.hip part_record)
+__device__ inline uint32_t pr_record_run(const Batch &bt, const TwParams &p, const int64_t *wm, int64_t k_epoch,
+                                         uint64_t i, uint32_t &a, uint32_t &key) {
+  a = 0;
+  key = HSG_KEY_NONE;
+  if (i >= bt.n) return 0;
+  key = bt.key[i];
+  if (key == HSG_KEY_NONE) return 0;
+  uint64_t k_lo, k_hi;
+  if (!record_windows(p, bt.ts[i], k_lo, k_hi)) return 0;
+  const int64_t w = wm ? wm[i] : INT64_MIN;
+  uint64_t k = k_lo;
+  while (k <= k_hi && !window_accepted(p, k, w)) ++k;
+  if (k > k_hi) return 0;
+  int64_t lo = (int64_t)k - k_epoch, hi = (int64_t)k_hi - k_epoch;
+  if (lo < 0) lo = 0;
+  if (hi > 0xFFFFFFFFll) hi = 0xFFFFFFFFll;
+  if (lo > hi) return 0;
+  a = (uint32_t)lo;
+  return (uint32_t)(hi - lo + 1);
+}
+
+__global__ __launch_bounds__(kPrEmitThreads) void k_pr_offs(Batch bt, TwParams p, PartBuffers pb, PrPart pr,
+                                                            const int64_t *__restrict__ rec_wm, DevScalars *sc) {
+  __shared__ uint32_t sw[kPrEmitThreads / 64];
+  if (sc->redo || pr.counter[1]) return;  // uniform
+  const int64_t k_epoch = sc->k_epoch;
+  const int64_t *wm = rec_wm ? rec_wm : (sc->no_late ? nullptr : pb.wm);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t base = pr.tpoff[(uint64_t)blockIdx.x * (kPrEmitRecs / kPartTileRecs)];
+  for (int rd = 0; rd < kPrEmitRounds; ++rd) {
+    const uint64_t i0 = (uint64_t)blockIdx.x * kPrEmitRecs + (uint64_t)rd * kPrEmitThreads;
+    if (i0 >= bt.n) break;  // uniform
+    const uint64_t i = i0 + threadIdx.x;
+    uint32_t a, key;
+    const uint32_t n = pr_record_run(bt, p, wm, k_epoch, i, a, key);
+    const uint32_t incl = (uint32_t)wave_incl_sum((uint64_t)n);
+    if (lane == 63) sw[wv] = incl;
+    lds_barrier();
+    uint32_t before = incl - n, tot = 0;
+    for (int k = 0; k < kPrEmitThreads / 64; ++k) {
+      before += k < wv ? sw[k] : 0u;
+      tot += sw[k];
+    }
+    if (n) {
+      const uint32_t x = pr.kpos[pr.pos[i]];
+      pr.roff[x] = base + before;
+      pr.kidx[x] = (uint32_t)i;
+    }
+    base += tot;
+    lds_barrier();  // sw is rewritten by the next round
+  }
+}
+
+__device__ inline int64_t rl64(int64_t v, int j) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), j);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ inline uint32_t rl32(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
+
+template <int MS>
+__global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, PartParams pp, TwTable t,
+                                                   PartBuffers pb, PrPart pr, const int64_t *__restrict__ seq,
+                                                   OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc) {
+  // each wave stages its rows' states (and record lane << 8 | window offset)
+  // in LDS while it replays, then writes them row-parallel: the replay step
+  // of a record (~12 active lanes) only folds and stages, the output
+  // conversion runs on full waves
+  constexpr int CAP = MS <= 2 ? 384 : MS <= 4 ? 192 : 128;  // staged rows per wave (>= 64: one record's pass)
+  __shared__ int64_t sst[kPkNW][MS][CAP];
+  __shared__ uint16_t smeta[kPkNW][CAP];
+  __shared__ uint16_t gst[4096];  // group starts (bucket-relative), in no particular order: one per digit value
+  __shared__ uint32_t s_ng, s_next;
+  if (sc->redo || pr.counter[1]) return;  // uniform
+  const uint32_t b = blockIdx.x;
+  const uint64_t b0 = pb.bstart[b], b1 = pb.bstart[b + 1];
+  const uint32_t m = (uint32_t)(b1 - b0);  // <= kKsBig (else counter[1])
+  if (m == 0) return;                      // uniform
+  const bool pk = sc->packed != 0;
+  const int W = pk ? pp.words - 1 : pp.words;
+  const int C = pp.words - 2 - pp.has_seq;
+  const uint32_t kbase = (uint32_t)sc->kbase;
+  const int hs = pp.bshift + pp.np_log2;
+  const int64_t k_epoch = sc->k_epoch;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ns = prog.n_slots;
+  const uint32_t bid = (uint32_t)p.batch_id;
+  const uint64_t *rec = pr.krec + b0 * (uint64_t)W;
+  uint32_t err = 0;
+  uint64_t fresh = 0, touched = 0;
+  uint64_t ck = phase_clock(), c_head = 0, c_load = 0, c_claim = 0, c_replay = 0, c_flush = 0, c_wb = 0;
+  auto lap = [&](uint64_t &acc) {
+    if constexpr (kPhaseClocks) {
+      const uint64_t c = phase_clock();
+      acc += c - ck;
+      ck = c;
+    }
+  };
+  if (threadIdx.x == 0) {
+    s_ng = 0;
+    s_next = 0;
+  }
+  __syncthreads();
+  // 1) group heads: the first record of each run of equal key digits
+  for (uint32_t r = threadIdx.x; r < m; r += kPkNT) {
+    const uint32_t d = ks_digits((uint32_t)rec[(uint64_t)r * W], hs);
+    if (r == 0 || ks_digits((uint32_t)rec[(uint64_t)(r - 1) * W], hs) != d) gst[atomicAdd(&s_ng, 1u)] = (uint16_t)r;
+  }
+  __syncthreads();
+  const uint32_t ng = s_ng;
+  lap(c_head);
+  int64_t(&st_v)[MS][CAP] = sst[wv];
+  uint16_t(&st_m)[CAP] = smeta[wv];
+  // 2) each wave takes the next group until none is left
+  for (;;) {
+    uint32_t gi = 0;
+    if (lane == 0) gi = atomicAdd(&s_next, 1u);
+    gi = rl32(gi, 0);
+    if (gi >= ng) break;  // uniform (wave)
+    const uint32_t s = gst[gi];
+    uint32_t d0 = 0;
+    for (uint32_t c0 = s;; c0 += 64) {  // the group's records, 64 at a time
+      // each lane's record, its arrival index and first row: one round of loads
+      const uint32_t r = c0 + lane;
+      const uint64_t rr = r < m ? r : s;
+      const uint64_t *wp = rec + rr * W;
+      const PrRecRegs<false> v{wp[0], W > 1 ? wp[1] : 0ull, W > 2 ? wp[2] : 0ull, W > 3 ? wp[3] : 0ull, wp, pk, C};
+      const uint32_t idx = pr.kidx[b0 + rr];
+      const uint64_t ro = pr.roff[b0 + rr];
+      const uint32_t key = v.key();
+      if (c0 == s) d0 = ks_digits(rl32(key, 0), hs);  // the group's digits (its first record)
+      const bool in = r < m && ks_digits(key, hs) == d0;
+      const uint64_t outm = __ballot(!in);
+      const uint32_t len = outm ? (uint32_t)__builtin_ctzll(outm) : 64u;  // records of the group here
+      const bool mine = (uint32_t)lane < len;
+      const uint32_t kr = v.krel(kbase), nw = mine ? v.nwin() : 0u;
+      const int64_t src = seq ? seq[idx] : (int64_t)(p.rec_base + idx);
+      int64_t e[MS];
+      pr_elems<MS>(prog, v, e);
+      lap(c_load);
+      uint64_t todo = len == 64 ? ~0ull : ((1ull << len) - 1ull);
+      while (todo) {  // each key of the chunk (one, unless keys share the digits)
+        const uint32_t kk = rl32(key, __builtin_ctzll(todo));
+        const uint64_t km = __ballot(mine && key == kk);
+        todo &= ~km;
+        const bool mk = (km >> lane) & 1ull;
+        const uint32_t lo = (uint32_t)wave_min_i64(mk && nw ? (int64_t)kr : (int64_t)0xFFFFFFFFll);
+        const uint32_t hi = (uint32_t)wave_max_i64(mk && nw ? (int64_t)kr + nw - 1 : 0);
+        // the staged rows out, row-parallel: row q = (record lane j, window
+        // offset jj) -> changelog row ro_j + jj, window kr_j + jj
+        auto flush = [&](uint32_t nst) {
+          lap(c_replay);
+          __builtin_amdgcn_wave_barrier();
+          for (uint32_t q0 = 0; q0 < nst; q0 += 64) {  // uniform trip count (the shuffles)
+            const uint32_t q = q0 + lane;
+            const bool ok = q < nst;
+            const uint32_t mt = ok ? st_m[q] : 0u;
+            const int j = (int)(mt >> 8), jj = (int)(mt & 0xFFu);
+            const uint64_t roj = (uint64_t)__shfl((long long)ro, j, 64);
+            const uint32_t krj = (uint32_t)__shfl((int)kr, j, 64);
+            const int64_t srcj = __shfl((long long)src, j, 64);
+            if (!ok) continue;
+            int64_t R[MS];
+#pragma unroll
+            for (int z = 0; z < MS; ++z) R[z] = st_v[z][q];
+            const uint64_t ob = out_base + roj + (uint64_t)jj;
+            if (ob >= out_cap) {
+              err |= ERR_OOM;
+              continue;
+            }
+            int64_t ws = 0, we = 0;
+            if (p.kind != HSG_UNWINDOWED) {
+              ws = (int64_t)((uint64_t)(k_epoch + (int64_t)(krj + (uint32_t)jj)) * (uint64_t)p.adv);
+              we = (int64_t)((uint64_t)ws + (uint64_t)p.size);
+            }
+            out.key[ob] = kk;
+            out.ws[ob] = ws;
+            out.we[ob] = we;
+            out.src[ob] = srcj;
+#pragma unroll
+            for (int c = 0; c < kMaxAggs; ++c)  // static indices: the column pointers stay in registers
+              if (c < prog.n_out) out.agg[c][ob] = out_value_reg<MS>(prog, c, R);
+            if (out.form) out.form[ob] = out_form_reg<MS>(prog, R);
+          }
+          __builtin_amdgcn_wave_barrier();
+          lap(c_flush);
+        };
+        for (uint64_t wb = lo; wb <= hi; wb += 64) {  // windows, 64 lanes at a time
+          const uint64_t w = wb + (uint64_t)lane;
+          const uint64_t we_ = wb + 63 < hi ? wb + 63 : hi;
+          // the lane's window is some record's (a key's records can leave gaps)
+          bool act = false;
+          for (uint64_t rm = km; rm; rm &= rm - 1ull) {
+            const int j = __builtin_ctzll(rm);
+            act = act || (w >= rl32(kr, j) && w - rl32(kr, j) < rl32(nw, j));
+          }
+          act = act && w <= hi;
+          if (!__ballot(act)) continue;  // uniform
+          int64_t cur[MS];
+          identity_row<MS>(prog, cur);
+          int64_t slot = -1;
+          bool isnew = false;
+          uint32_t stp = 0;
+          if (act) {
+            // find (or claim) at the home slot, the home row and stamp loaded
+            // with its key (the group's usual place); else probe on
+            const uint64_t g = ((uint64_t)kk << 32) | (uint32_t)w;
+            const uint64_t h = tw_region_base(t, g) + tw_home_in(t, g);
+            int64_t hv[MS];
+#pragma unroll
+            for (int q = 0; q < MS; ++q)
+              hv[q] = q < ns ? __hip_atomic_load(t.aggs(h) + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+            const uint32_t hst = __hip_atomic_load(t.stamp(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint64_t old = __hip_atomic_load(t.key(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (old == kEmpty)
+              old = atomicCAS((unsigned long long *)t.key(h), (unsigned long long)kEmpty, (unsigned long long)g);
+            if (old == kEmpty) {
+              t.mark(h);
+              isnew = true;
+              slot = (int64_t)h;
+            } else if (old == g) {
+              slot = (int64_t)h;
+              stp = hst;
+#pragma unroll
+              for (int q = 0; q < MS; ++q) cur[q] = hv[q];
+            } else {
+              slot = pr_claim_row(t, g, isnew);
+              if (slot < 0) {
+                err |= ERR_OOM;
+              } else if (!isnew) {
+                const int64_t *row = t.aggs(slot);
+#pragma unroll
+                for (int q = 0; q < MS; ++q)
+                  if (q < ns) cur[q] = __hip_atomic_load(row + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                stp = __hip_atomic_load(t.stamp(slot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              }
+            }
+          }
+          // the key's records in arrival order: fold, stage each record's rows
+          lap(c_claim);
+          uint32_t nst = 0;
+          for (uint64_t rm = km; rm; rm &= rm - 1ull) {
+            const int j = __builtin_ctzll(rm);
+            const uint32_t krj = rl32(kr, j), nwj = rl32(nw, j);
+            const uint64_t a = krj > wb ? krj : wb, z = (uint64_t)krj + nwj - 1 < we_ ? (uint64_t)krj + nwj - 1 : we_;
+            if (a > z) continue;  // uniform: none of the record's windows in this pass
+            const uint32_t cnt = (uint32_t)(z - a + 1);
+            if (nst + cnt > (uint32_t)CAP) {  // uniform
+              flush(nst);
+              nst = 0;
+            }
+            int64_t ej[MS];
+#pragma unroll
+            for (int q = 0; q < MS; ++q) ej[q] = q < ns ? rl64(e[q], j) : 0;
+            if (act && w >= a && w <= z) {
+              combine_row<MS>(prog, cur, ej);
+              const uint32_t q = nst + (uint32_t)(w - a);
+#pragma unroll
+              for (int y = 0; y < MS; ++y) st_v[y][q] = cur[y];
+              st_m[q] = (uint16_t)(((uint32_t)j << 8) | (uint32_t)(w - krj));
+            }
+            nst += cnt;
+          }
+          flush(nst);
+          if (act && slot >= 0) {
+            int64_t *row = t.aggs(slot);
+#pragma unroll
+            for (int q = 0; q < MS; ++q)
+              if (q < ns) row[q] = cur[q];
+            if (stp != bid) {
+              *t.stamp(slot) = bid;
+              touched += 1;
+            }
+            fresh += isnew ? 1 : 0;
+          }
+          lap(c_wb);
+        }
+      }
+      if (len < 64 || c0 + 64 >= m) break;  // uniform: the group ended
+      // the rows in L2 before the group's next chunk loads them again
+      // (L1-bypassing loads of this wave; vmcnt counts stores on gfx9)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  if (err) atomicOr(&sc->err, err);
+  const uint64_t f = wave_sum_u64(fresh), tc = wave_sum_u64(touched);
+  if (kPhaseClocks && lane == 0) {  // per-wave phase clocks (HSG_PHASES builds)
+    atomicAdd((unsigned long long *)&sc->scratch[24], (unsigned long long)c_head);
+    atomicAdd((unsigned long long *)&sc->scratch[25], (unsigned long long)c_load);
+    atomicAdd((unsigned long long *)&sc->scratch[26], (unsigned long long)c_claim);
+    atomicAdd((unsigned long long *)&sc->scratch[27], (unsigned long long)c_replay);
+    atomicAdd((unsigned long long *)&sc->scratch[28], (unsigned long long)c_flush);
+    atomicAdd((unsigned long long *)&sc->scratch[29], (unsigned long long)c_wb);
+    atomicAdd((unsigned long long *)&sc->scratch[30], 1ull);
+  }
+  if (lane == 0) {
+    if (f) atomicAdd((unsigned long long *)&sc->live_x[blockIdx.x & 7], (unsigned long long)f);
+    if (tc) atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)tc);
+  }
+}
+
 template <int MS>
 static void pr_launch(hipStream_t s, const Batch &b, const Program &prog, const TwParams &p, const PartParams &pp,
                       const TwTable &t, const PartBuffers &pb, const PrPart &pr, uint32_t wpr, const int64_t *rec_wm,
@@ -1437,6 +1780,12 @@ static void pr_launch(hipStream_t s, const Batch &b, const Program &prog, const 
   }
   const dim3 g((unsigned)(nb + b.n / pp.chunk + 1));
   hipLaunchKernelGGL(k_pr_keysort, dim3((unsigned)nb), dim3(kPrNT), 0, s, pp, pb, pr, sc);
+  const uint64_t etiles = (b.n + kPrEmitRecs - 1) / kPrEmitRecs;
+  // the key-grouped replay (returns at once when a bucket was too large) ...
+  hipLaunchKernelGGL(k_pr_offs, dim3((unsigned)etiles), dim3(kPrEmitThreads), 0, s, b, p, pb, pr, rec_wm, sc);
+  hipLaunchKernelGGL(k_pr_keys<MS>, dim3((unsigned)nb), dim3(kPkNT), 0, s, prog, p, pp, t, pb, pr, seq, out,
+                     out_base, out_cap, sc);
+  // ... or the chunked path (returns at once otherwise)
   PartBuffers kpb = pb;
   kpb.rec = pr.krec;  // the chunks read the key-grouped records
   hipLaunchKernelGGL(k_pr_local<MS>, g, dim3(kPrNT), 0, s, prog, pp, kpb, pr, wpr, sc);

@@ -122,6 +122,8 @@ int perrecord_part_init(OpDevice &d, const hsg_op_config &cfg, const Program &pr
     x.fin = c.take<int64_t>(wpr == 1 ? n * ns : 1);
     x.krec = c.take<uint64_t>(wpr == 1 ? 1 : n * (uint64_t)part_words(cfg.n_cols, true));
     x.kpos = c.take<uint32_t>(wpr == 1 ? 1 : n);
+    x.roff = c.take<uint64_t>(wpr == 1 ? 1 : n);
+    x.kidx = c.take<uint32_t>(wpr == 1 ? 1 : n);
   };
   Carve probe{nullptr};
   PrPart tmp;
@@ -168,7 +170,8 @@ static int push_time_perrecord_part(OpDevice &d, const hsg_op_config &cfg, const
     pp.chunk = kPrPairs / wpr;
     // one-window ops: a workgroup walks each bucket (k_pr_bucket), as many
     // buckets as the partition makes; else buckets of a few k_pr_local chunks
-    pp.np_log2 = wpr == 1 ? pr_buckets_log2(kb.n, 1024) : pr_buckets_log2(kb.n, pp.chunk);
+    // (multi-window: ~2048 records per bucket, ~128 keys for k_pr_keys' waves)
+    pp.np_log2 = pr_buckets_log2(kb.n, wpr == 1 ? 1024 : 512);
     pp.bshift = d.bshift;
     for (int c = 0; c < cfg.n_cols; ++c) pp.has_valid |= kb.valid[c] != nullptr;
     pp.has_seq = last ? 1 : 0;
@@ -188,7 +191,11 @@ static int push_time_perrecord_part(OpDevice &d, const hsg_op_config &cfg, const
     scan_excl_u32(d.stream, d.prp.tpairs, d.prp.tpoff, pp.tiles, d.prp.partial, &d.sc->out_rows);
     launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc, can_pack, true);
     wait_table_reset(d);  // the passes above do not touch the table
-    DTRY(hipMemsetAsync(d.prp.counter, 0, 8, d.stream));
+    DTRY(hipMemsetAsync(d.prp.counter, 0, 16, d.stream));
+    // HSG_PR_CHUNKED=1: multi-window batches take the chunked path (k_pr_local /
+    // k_pr_carry / k_pr_emit) even when every bucket fits the key sort (tests, A/B)
+    static const bool chunked = getenv("HSG_PR_CHUNKED") != nullptr;
+    if (wpr != 1 && chunked) DTRY(hipMemsetAsync(d.prp.counter + 1, 1, 1, d.stream));
     if (wpr != 1) launch_part_chunks(d.stream, pp, d.part, d.sc);
     launch_pr_part(d.stream, kb, prog, p, pp, d.tw, d.part, d.prp, wpr, rec_wm, seq, d.out, a.pending, d.out_cap,
                    d.sc);

@@ -308,19 +308,40 @@ def test_exchange_path_single_rank(xeng, spec, late, xpart):
 @pytest.mark.parametrize("late", [False, True], ids=["in_time", "late"])
 def test_per_record_groups_span_chunks(eng, kind, kw, late):
     """EMIT CHANGES (TimeWindowedStream.hs:89-103) where a few keys carry
-    whole batches: each group's records span many k_pr_local chunks of its
-    bucket, which k_pr_carry applies in arrival order; rows in arrival x
-    window order, bit-exact against the oracle (LAST included)."""
+    whole batches (~66K records each, buckets beyond the key sort: hopping
+    takes the chunked path): each group's records span many k_pr_local chunks
+    of its bucket, which k_pr_carry applies in arrival order; rows in arrival
+    x window order, bit-exact against the oracle (LAST included)."""
     spec = OpSpec(kind, abi.HSG_EMIT_PER_RECORD, col_types=[abi.HSG_I64], aggs=ALL_AGG_SETS["full_i64"], **kw)
     batches = []
     for bi in range(3):
-        key, ts, cols, valid = gen_small(77 + bi, 60_000, 3, span=40_000, base=5_000_000 + bi * 40_000,
+        key, ts, cols, valid = gen_small(77 + bi, 200_000, 3, span=40_000, base=5_000_000 + bi * 40_000,
                                          very_late=late)
         batches.append((key, ts, cols, valid))
     _drive(eng, spec, batches)
 
 
-@pytest.mark.parametrize("name", ["C2", "C2f", "C5"])
+@pytest.mark.parametrize("nkeys,span", [(20_000, 400_000), (500, 100_000), (4, 100_000)],
+                         ids=["wide_ranges", "long_runs", "hot_buckets"])
+@pytest.mark.parametrize("late", [False, True], ids=["in_time", "late"])
+def test_per_record_key_replay(eng, nkeys, span, late):
+    """EMIT CHANGES of hopping windows on the key-grouped replay (k_pr_keys):
+    many keys per bucket, so keys share the sort's 12 hash bits (runs of
+    several keys); keys whose windows in a batch span more than one wave
+    (wide_ranges: ~80 windows), keys with more than 64 records in a batch
+    (long_runs) and buckets beyond the LDS key sort (hot_buckets: ~32K
+    records, sorted in global scratch); LAST, absent fields, late and keyless records. Rows in
+    arrival x window order and the state against the oracle
+    (TimeWindowedStream.hs:89-103)."""
+    spec = OpSpec(abi.HSG_HOPPING, abi.HSG_EMIT_PER_RECORD, size_ms=60_000, advance_ms=5_000,
+                  col_types=[abi.HSG_I64], aggs=ALL_AGG_SETS["full_i64"])
+    batches = []
+    for bi in range(3):
+        batches.append(gen_small(910 + bi, 1 << 17, nkeys, span=span, base=7_000_000 + bi * span, very_late=late))
+    _drive(eng, spec, batches)
+
+
+@pytest.mark.parametrize("name", ["C2", "C2f", "C5", "C3"])
 def test_per_record_configs_reduced(eng, name):
     """The per-record changelog on the C2 / C2f / C5 workloads at reduced size
     (2 batches of 2^18 records), ordered rows against the oracle."""
