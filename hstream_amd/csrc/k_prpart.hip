@@ -1547,28 +1547,56 @@ __global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, Par
   lap(c_head);
   int64_t(&st_v)[MS][CAP] = sst[wv];
   uint16_t(&st_m)[CAP] = smeta[wv];
-  // 2) each wave takes the next group until none is left
-  for (;;) {
-    uint32_t gi = 0;
-    if (lane == 0) gi = atomicAdd(&s_next, 1u);
-    gi = rl32(gi, 0);
-    if (gi >= ng) break;  // uniform (wave)
+  // 2) each wave takes the next group until none is left. A chunk's records
+  // (each lane's record, its arrival index and first row) are one round of
+  // loads; the next group's first chunk is loaded with this group's claims,
+  // so a group waits for one round of memory before its replay
+  struct ChunkRegs {
+    uint64_t w0, w1, w2, w3, ro;
+    uint32_t idx;
+  };
+  auto load_chunk = [&](uint32_t s_, uint32_t c0_) {
+    const uint32_t r = c0_ + lane;
+    const uint64_t rr = r < m ? r : s_;
+    const uint64_t *wp = rec + rr * W;
+    ChunkRegs c;
+    c.w0 = wp[0];
+    c.w1 = W > 1 ? wp[1] : 0ull;
+    c.w2 = W > 2 ? wp[2] : 0ull;
+    c.w3 = W > 3 ? wp[3] : 0ull;
+    c.idx = pr.kidx[b0 + rr];
+    c.ro = pr.roff[b0 + rr];
+    return c;
+  };
+  auto take_group = [&]() {
+    uint32_t g_ = 0;
+    if (lane == 0) g_ = atomicAdd(&s_next, 1u);
+    return rl32(g_, 0);
+  };
+  uint32_t gi = take_group();
+  ChunkRegs pre{};
+  if (gi < ng) pre = load_chunk(gst[gi], gst[gi]);
+  while (gi < ng) {  // uniform (wave)
     const uint32_t s = gst[gi];
-    uint32_t d0 = 0;
+    uint32_t gnext = ng, d0 = 0;
     for (uint32_t c0 = s;; c0 += 64) {  // the group's records, 64 at a time
-      // each lane's record, its arrival index and first row: one round of loads
+      const ChunkRegs cr = c0 == s ? pre : load_chunk(s, c0);
       const uint32_t r = c0 + lane;
       const uint64_t rr = r < m ? r : s;
-      const uint64_t *wp = rec + rr * W;
-      const PrRecRegs<false> v{wp[0], W > 1 ? wp[1] : 0ull, W > 2 ? wp[2] : 0ull, W > 3 ? wp[3] : 0ull, wp, pk, C};
-      const uint32_t idx = pr.kidx[b0 + rr];
-      const uint64_t ro = pr.roff[b0 + rr];
+      const PrRecRegs<false> v{cr.w0, cr.w1, cr.w2, cr.w3, rec + rr * W, pk, C};
+      const uint32_t idx = cr.idx;
+      const uint64_t ro = cr.ro;
       const uint32_t key = v.key();
       if (c0 == s) d0 = ks_digits(rl32(key, 0), hs);  // the group's digits (its first record)
       const bool in = r < m && ks_digits(key, hs) == d0;
       const uint64_t outm = __ballot(!in);
       const uint32_t len = outm ? (uint32_t)__builtin_ctzll(outm) : 64u;  // records of the group here
       const bool mine = (uint32_t)lane < len;
+      const bool last = len < 64 || c0 + 64 >= m;  // uniform: the group's last chunk
+      if (last) {
+        gnext = take_group();
+        if (gnext < ng) pre = load_chunk(gst[gnext], gst[gnext]);
+      }
       const uint32_t kr = v.krel(kbase), nw = mine ? v.nwin() : 0u;
       const int64_t src = seq ? seq[idx] : (int64_t)(p.rec_base + idx);
       int64_t e[MS];
@@ -1637,6 +1665,8 @@ __global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, Par
           int64_t slot = -1;
           bool isnew = false;
           uint32_t stp = 0;
+          bool pending = false;  // a claim at home whose result (cas) is read at the write-back
+          uint64_t cas = kEmpty;
           if (act) {
             // find (or claim) at the home slot, the home row and stamp loaded
             // with its key (the group's usual place); else probe on
@@ -1648,10 +1678,10 @@ __global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, Par
               hv[q] = q < ns ? __hip_atomic_load(t.aggs(h) + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
             const uint32_t hst = __hip_atomic_load(t.stamp(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             uint64_t old = __hip_atomic_load(t.key(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (old == kEmpty)
-              old = atomicCAS((unsigned long long *)t.key(h), (unsigned long long)kEmpty, (unsigned long long)g);
             if (old == kEmpty) {
-              t.mark(h);
+              // claimed at home; the claim's result is waited for at the write-back
+              cas = atomicCAS((unsigned long long *)t.key(h), (unsigned long long)kEmpty, (unsigned long long)g);
+              pending = true;
               isnew = true;
               slot = (int64_t)h;
             } else if (old == g) {
@@ -1698,6 +1728,14 @@ __global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, Par
             nst += cnt;
           }
           flush(nst);
+          if (pending && cas == kEmpty) t.mark(slot);  // the home claim held
+          if (pending && cas != kEmpty) {
+            // another key took the home slot first: the next free one (the
+            // group is new: only this wave holds the key's groups)
+            bool nn;
+            slot = pr_claim_row(t, ((uint64_t)kk << 32) | (uint32_t)w, nn);
+            if (slot < 0) err |= ERR_OOM;
+          }
           if (act && slot >= 0) {
             int64_t *row = t.aggs(slot);
 #pragma unroll
@@ -1712,11 +1750,12 @@ __global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, Par
           lap(c_wb);
         }
       }
-      if (len < 64 || c0 + 64 >= m) break;  // uniform: the group ended
+      if (last) break;
       // the rows in L2 before the group's next chunk loads them again
       // (L1-bypassing loads of this wave; vmcnt counts stores on gfx9)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    gi = gnext;
   }
   if (err) atomicOr(&sc->err, err);
   const uint64_t f = wave_sum_u64(fresh), tc = wave_sum_u64(touched);
