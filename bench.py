@@ -590,10 +590,14 @@ def committed_traffic(args, world):
     """Per-batch HBM bytes of this configuration from the committed PMC summary
     (tools/traffic.sh -> profiles/<round>/traffic_<config>.json), when the run
     uses the configuration's default sizes; else None."""
-    if world != 1 or args.records or args.batch or args.emit != "per_batch" or args.force_exchange:
+    pr = args.emit == "per_record"  # the EMIT CHANGES lines: traffic_<config>_pr.json
+    if world != 1 or args.batch or args.emit not in ("per_batch", "per_record") or args.force_exchange:
+        return None, None
+    if args.records and not pr:
         return None, None
     import glob
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"traffic_{args.config.lower()}.json")))
+    suffix = "_pr" if pr else ""
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"traffic_{args.config.lower()}{suffix}.json")))
     if not paths:
         return None, None
     with open(paths[-1]) as f:
@@ -601,7 +605,10 @@ def committed_traffic(args, world):
     # flags that only switch the extra blocks off measure the same pipeline
     extra = {"--no-host-input", "--no-per-record", "--no-hbm", "--input", "hbm"}
     words = [w for w in d.get("bench_args", "").split() if w not in extra]
-    if words not in ([], ["--config", args.config]):
+    want = ["--config", args.config]
+    if pr:
+        want += ["--emit", "per_record"] + (["--records", str(args.records)] if args.records else [])
+    if words not in (want, [] if not pr else None):
         return None, None
     return int(d["hbm_bytes_per_batch"]), os.path.relpath(paths[-1], ROOT)
 

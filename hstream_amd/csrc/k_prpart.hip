@@ -41,13 +41,14 @@ constexpr int kPrTabLog2 = 12;
 static_assert(kPrPairs * 2 <= kPrTab && kPrPairs == 2 * kPrNT, "k_pr_local sizes");
 
 // chunk of this workgroup: records [r0, r1) of bucket b; false past the chunks
-__device__ inline bool pr_chunk(const PartParams &pp, const PartBuffers &pb, uint32_t &b, uint64_t &r0, uint64_t &r1) {
+__device__ inline bool pr_chunk(const PartParams &pp, const PartBuffers &pb, uint32_t cid, uint32_t &b, uint64_t &r0,
+                                uint64_t &r1) {
   const int nb = 1 << pp.np_log2;
-  if (blockIdx.x >= pb.chunk_start[nb]) return false;
-  b = pb.chunk_bucket[blockIdx.x];
+  if (cid >= pb.chunk_start[nb]) return false;
+  b = pb.chunk_bucket[cid];
   const uint32_t c0 = pb.chunk_start[b];
   const uint64_t b0 = pb.bstart[b], b1 = pb.bstart[b + 1];
-  r0 = b0 + (uint64_t)(blockIdx.x - c0) * pp.chunk;
+  r0 = b0 + (uint64_t)(cid - c0) * pp.chunk;
   r1 = r0 + pp.chunk < b1 ? r0 + pp.chunk : b1;
   return true;
 }
@@ -259,9 +260,12 @@ __global__ __launch_bounds__(kPrNT) void k_pr_local(Program prog, PartParams pp,
   __shared__ uint32_t swf[kPrNW], swh[kPrNW];
   __shared__ uint32_t s_cbase;
   if (sc->redo || !pr.counter[1]) return;  // uniform: stale bucket starts / the batch takes k_pr_keys
+  // grid-stride over the chunks (the grid is capped: a batch that takes
+  // k_pr_keys launches this kernel for nothing)
+  for (uint32_t cid = blockIdx.x;; cid += gridDim.x) {
   uint32_t b;
   uint64_t r0, r1;
-  if (!pr_chunk(pp, pb, b, r0, r1)) return;  // uniform
+  if (!pr_chunk(pp, pb, cid, b, r0, r1)) break;  // uniform
   uint64_t ck = phase_clock(), c_rec = 0, c_ins = 0, c_sort = 0, c_scan = 0;
   auto lap = [&](uint64_t &acc) {
     if constexpr (kPhaseClocks) {
@@ -462,8 +466,8 @@ __global__ __launch_bounds__(kPrNT) void k_pr_local(Program prog, PartParams pp,
   if (threadIdx.x == 0) {
     const uint32_t base = (uint32_t)(r0 * wpr);
     s_cbase = base;
-    pr.cbase[blockIdx.x] = base;
-    pr.ccnt[blockIdx.x] = heads;
+    pr.cbase[cid] = base;
+    pr.ccnt[cid] = heads;
   }
   __syncthreads();
   lap(c_scan);
@@ -516,6 +520,8 @@ __global__ __launch_bounds__(kPrNT) void k_pr_local(Program prog, PartParams pp,
       atomicAdd((unsigned long long *)&sc->scratch[29], 0ull);
       atomicAdd((unsigned long long *)&sc->scratch[30], 1ull);
     }
+  }
+  __syncthreads();  // the LDS table and sort arrays are reused by the next chunk
   }
 }
 
@@ -1817,7 +1823,8 @@ static void pr_launch(hipStream_t s, const Batch &b, const Program &prog, const 
                        seq, out, out_base, out_cap, sc);
     return;
   }
-  const dim3 g((unsigned)(nb + b.n / pp.chunk + 1));
+  const uint64_t nchunks = nb + b.n / pp.chunk + 1;  // >= the partition's chunks
+  const dim3 g((unsigned)(nchunks < 4096 ? nchunks : 4096));
   hipLaunchKernelGGL(k_pr_keysort, dim3((unsigned)nb), dim3(kPrNT), 0, s, pp, pb, pr, sc);
   const uint64_t etiles = (b.n + kPrEmitRecs - 1) / kPrEmitRecs;
   // the key-grouped replay (returns at once when a bucket was too large) ...
