@@ -1706,6 +1706,9 @@ __global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, Par
                   if (q < ns) cur[q] = __hip_atomic_load(row + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 stp = __hip_atomic_load(t.stamp(slot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               }
+              // vmcnt(0) here (the rare path): after the branches only a home
+              // claim is outstanding, and the replay does not wait for it
+              __builtin_amdgcn_s_waitcnt(0x0F70);
             }
           }
           // the key's records in arrival order: fold, stage each record's rows
