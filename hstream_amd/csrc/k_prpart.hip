@@ -1500,7 +1500,7 @@ __device__ inline int64_t rl64(int64_t v, int j) {
 }
 __device__ inline uint32_t rl32(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
 
-template <int MS>
+template <int MS, uint64_t SIG>
 __global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, PartParams pp, TwTable t,
                                                    PartBuffers pb, PrPart pr, const int64_t *__restrict__ seq,
                                                    OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc) {
@@ -1514,6 +1514,7 @@ __global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, Par
   __shared__ uint16_t gst[4096];  // group starts (bucket-relative), in no particular order: one per digit value
   __shared__ uint32_t s_ng, s_next;
   if (sc->redo || pr.counter[1]) return;  // uniform
+  const ProgView<SIG> pv(prog);  // the slot program, baked in for the common aggregate sets
   const uint32_t b = blockIdx.x;
   const uint64_t b0 = pb.bstart[b], b1 = pb.bstart[b + 1];
   const uint32_t m = (uint32_t)(b1 - b0);  // <= kKsBig (else counter[1])
@@ -1525,7 +1526,7 @@ __global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, Par
   const int hs = pp.bshift + pp.np_log2;
   const int64_t k_epoch = sc->k_epoch;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int ns = prog.n_slots;
+  const int ns = pv.n();
   const uint32_t bid = (uint32_t)p.batch_id;
   const uint64_t *rec = pr.krec + b0 * (uint64_t)W;
   uint32_t err = 0;
@@ -1606,7 +1607,7 @@ __global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, Par
       const uint32_t kr = v.krel(kbase), nw = mine ? v.nwin() : 0u;
       const int64_t src = seq ? seq[idx] : (int64_t)(p.rec_base + idx);
       int64_t e[MS];
-      pr_elems<MS>(prog, v, e);
+      elems_v<MS>(pv, v, e);
       lap(c_load);
       uint64_t todo = len == 64 ? ~0ull : ((1ull << len) - 1ull);
       while (todo) {  // each key of the chunk (one, unless keys share the digits)
@@ -1667,7 +1668,7 @@ __global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, Par
           act = act && w <= hi;
           if (!__ballot(act)) continue;  // uniform
           int64_t cur[MS];
-          identity_row<MS>(prog, cur);
+          identity_v<MS>(pv, cur);
           int64_t slot = -1;
           bool isnew = false;
           uint32_t stp = 0;
@@ -1728,7 +1729,7 @@ __global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, Par
 #pragma unroll
             for (int q = 0; q < MS; ++q) ej[q] = q < ns ? rl64(e[q], j) : 0;
             if (act && w >= a && w <= z) {
-              combine_row<MS>(prog, cur, ej);
+              combine_v<MS>(pv, cur, ej);
               const uint32_t q = nst + (uint32_t)(w - a);
 #pragma unroll
               for (int y = 0; y < MS; ++y) st_v[y][q] = cur[y];
@@ -1832,8 +1833,36 @@ static void pr_launch(hipStream_t s, const Batch &b, const Program &prog, const 
   const uint64_t etiles = (b.n + kPrEmitRecs - 1) / kPrEmitRecs;
   // the key-grouped replay (returns at once when a bucket was too large) ...
   hipLaunchKernelGGL(k_pr_offs, dim3((unsigned)etiles), dim3(kPrEmitThreads), 0, s, b, p, pb, pr, rec_wm, sc);
-  hipLaunchKernelGGL(k_pr_keys<MS>, dim3((unsigned)nb), dim3(kPkNT), 0, s, prog, p, pp, t, pb, pr, seq, out,
-                     out_base, out_cap, sc);
+  {
+    const uint64_t sig = program_sig(prog);
+    const bool reg = pp.words <= kPrRegWords;  // (the specialised programs read one column)
+    const dim3 gk((unsigned)nb), tk(kPkNT);
+    bool done = false;
+    if constexpr (MS == 2) {
+      if (reg && sig == kSigCntSumI) {
+        hipLaunchKernelGGL((k_pr_keys<MS, kSigCntSumI>), gk, tk, 0, s, prog, p, pp, t, pb, pr, seq, out, out_base,
+                           out_cap, sc);
+        done = true;
+      } else if (reg && sig == kSigCntSumF) {
+        hipLaunchKernelGGL((k_pr_keys<MS, kSigCntSumF>), gk, tk, 0, s, prog, p, pp, t, pb, pr, seq, out, out_base,
+                           out_cap, sc);
+        done = true;
+      }
+    }
+    if constexpr (MS == 6) {
+      if (reg && sig == kSigAllI) {
+        hipLaunchKernelGGL((k_pr_keys<MS, kSigAllI>), gk, tk, 0, s, prog, p, pp, t, pb, pr, seq, out, out_base,
+                           out_cap, sc);
+        done = true;
+      } else if (reg && sig == kSigAllF) {
+        hipLaunchKernelGGL((k_pr_keys<MS, kSigAllF>), gk, tk, 0, s, prog, p, pp, t, pb, pr, seq, out, out_base,
+                           out_cap, sc);
+        done = true;
+      }
+    }
+    if (!done)
+      hipLaunchKernelGGL((k_pr_keys<MS, 0>), gk, tk, 0, s, prog, p, pp, t, pb, pr, seq, out, out_base, out_cap, sc);
+  }
   // ... or the chunked path (returns at once otherwise)
   PartBuffers kpb = pb;
   kpb.rec = pr.krec;  // the chunks read the key-grouped records
