@@ -50,8 +50,7 @@ struct PrPart {
                       // partitioned position
   uint64_t *krec;     // multi-window ops: [n][words] the partitioned records, key-grouped in each bucket
   uint32_t *kpos;     // [n] partitioned position -> its position in krec
-  uint64_t *roff;     // [n] at krec positions: the record's first changelog row (k_pr_keys)
-  uint32_t *kidx;     // [n] at krec positions: the record's arrival index
+  uint64_t *roff;     // [n] at krec positions: the record's first changelog row << 32 | its arrival index
 };
 
 void launch_pr_count(hipStream_t s, const Batch &b, const TwParams &p, const TwTable &t, const int64_t *tprefix,

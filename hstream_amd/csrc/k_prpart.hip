@@ -1424,7 +1424,7 @@ __global__ __launch_bounds__(kE1NT) void k_pr_emit1(Batch bt, Program prog, TwPa
 //
 //   k_pr_offs  one workgroup per arrival tile: each record's first changelog
 //              row (exclusive prefix of accepted windows in arrival order) and
-//              its arrival index, written at its krec position.
+//              its arrival index, packed in one word at its krec position.
 //   k_pr_keys  one workgroup per bucket, a wave per run of equal key digits
 //              (one key, rarely a few sharing the 12 bits): lane l owns window
 //              lo + l of the key's window range (one pass of 64 windows for a
@@ -1483,10 +1483,9 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_offs(Batch bt, TwParams p
       before += k < wv ? sw[k] : 0u;
       tot += sw[k];
     }
-    if (n) {
+    if (n) {  // one 8-byte store per record: the row (batch-relative, < 2^32 pairs) and the arrival index
       const uint32_t x = pr.kpos[pr.pos[i]];
-      pr.roff[x] = base + before;
-      pr.kidx[x] = (uint32_t)i;
+      pr.roff[x] = ((base + before) << 32) | (uint64_t)(uint32_t)i;
     }
     base += tot;
     lds_barrier();  // sw is rewritten by the next round
@@ -1571,8 +1570,9 @@ __global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, Par
     c.w1 = W > 1 ? wp[1] : 0ull;
     c.w2 = W > 2 ? wp[2] : 0ull;
     c.w3 = W > 3 ? wp[3] : 0ull;
-    c.idx = pr.kidx[b0 + rr];
-    c.ro = pr.roff[b0 + rr];
+    const uint64_t ri = pr.roff[b0 + rr];
+    c.idx = (uint32_t)ri;
+    c.ro = ri >> 32;
     return c;
   };
   auto take_group = [&]() {

@@ -123,7 +123,6 @@ int perrecord_part_init(OpDevice &d, const hsg_op_config &cfg, const Program &pr
     x.krec = c.take<uint64_t>(wpr == 1 ? 1 : n * (uint64_t)part_words(cfg.n_cols, true));
     x.kpos = c.take<uint32_t>(wpr == 1 ? 1 : n);
     x.roff = c.take<uint64_t>(wpr == 1 ? 1 : n);
-    x.kidx = c.take<uint32_t>(wpr == 1 ? 1 : n);
   };
   Carve probe{nullptr};
   PrPart tmp;
