@@ -579,7 +579,7 @@ def pipeline_name(cfg, emit):
             return ("per-record changelog (k_part_hist_opt, offsets + decide, stable k_part_scatter_st, "
                     "k_pr_bucket, k_pr_emit1)")
         return ("per-record changelog (k_part_hist_opt, offsets + decide, stable k_part_scatter_st, "
-                "k_pr_local, k_pr_carry, k_pr_emit)")
+                "k_pr_keysort, k_pr_offs, k_pr_keys)")
     if cfg.window_kind in (abi.HSG_TUMBLING, abi.HSG_UNWINDOWED):
         return ("batch pipeline (k_part_hist_opt, offsets + decide, k_part_scatter_st, k_agg_lean, "
                 "k_pane_apply writing the changelog rows)")
@@ -677,6 +677,13 @@ def cpu_baseline(cfg, spec, seconds):
     from concurrent.futures import ThreadPoolExecutor
     from hstream_amd import abi, datagen
     chunk = 1 << 18
+    # sessions: the faithful store's findSessions scans every end time
+    # (Store.hs:245-272, quadratic), so C4 is timed on its SURVEY.md 8d
+    # sample, N = 5M / K = 100K (the same 50 records per key per hour)
+    if cfg.window_kind == abi.HSG_SESSION and cfg.keys > 100_000:
+        import dataclasses
+        cfg = dataclasses.replace(cfg, keys=100_000, n=5_000_000)
+        chunk = 1 << 14
 
     def run_single(budget):
         o = pyoracle.OracleOp(spec, faithful_sessions=True)
@@ -723,8 +730,10 @@ def cpu_baseline(cfg, spec, seconds):
     T = cpu_threads()
     nT, tT = run_parallel(seconds, T) if T > 1 else (n1, t1)
     return {"value": round(n1 / t1, 1), "unit": "records/s", "cores": 1, "kind": "port",
-            "sample": f"first {n1} records of {cfg.name} (same generator), oracle/hsoracle.cpp ordered-map "
-                      f"restatement, 1 thread",
+            "sample": f"first {n1} records of {cfg.name} (same generator, N={cfg.n}, K={cfg.keys}), "
+                      f"oracle/hsoracle.cpp restatement ("
+                      f"{'faithful end->key->start session store' if cfg.window_kind == abi.HSG_SESSION else 'ordered-map store'}"
+                      f"), 1 thread",
             "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
             "key_partitioned": {"value": round(nT / tT, 1), "unit": "records/s", "cores": T,
                                 "sample": f"first {nT} records, {T} oracle ops, records routed by key hash"}}

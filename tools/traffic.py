@@ -25,7 +25,7 @@ def load(path):
 fetch, names = load(sys.argv[1])
 write, _ = load(sys.argv[2])
 disp = sorted(names)
-first = "k_ss_phist" if any("k_ss_phist" in names[d] for d in disp) else "k_part_hist"
+first = next((f for f in ("k_ss_phist", "k_ss_slot") if any(f in names[d] for d in disp)), "k_part_hist")
 starts = [d for d in disp if first in names[d]]
 half = starts[len(starts) // 2:]  # the timed step (warmup step first)
 batches = []
