@@ -13,12 +13,13 @@ host poll batches (Processor.hs:128-144), so every step hands its batches over
 as pinned host buffers through hsg_push_batch_async; the library copies each
 batch to HBM on the op's copy stream while the batch before it computes, so a
 step costs max(PCIe, kernels). The batches use the ABI's narrow transport
-(include/hstream_gpu.h hsg_enc: ts as int32 offsets from the batch's first
-timestamp, the i64 value column as int32 -- C2's values are in [-1e9, 1e9];
-f64 columns of decimals as int32 mantissas), which a decoder that saw every
-value can choose for free; the library widens them on the device. The
-producer's choice of encoding is made before the timed region, as decoding
-is. The same JSON line also carries:
+(include/hstream_gpu.h hsg_enc: 16-bit key ids, ts as 16-bit offsets from
+per-frame bases, the i64 value column as int32 -- C2's values are in
+[-1e9, 1e9]; f64 columns of decimals as int32 mantissas), chosen per batch by
+the product's hsg_batch_narrow, the pass the decoder (hsg_decode_json_batch)
+runs on every batch it decodes; the library widens them on the device. The
+narrowing runs before the timed region, as decoding does; its host rate is
+reported (input_link.narrowed_by). The same JSON line also carries:
   hbm_resident  the same steps with the input already resident in HBM
                 (hsg_push_batch on device columns): the kernels' own rate,
                 with the batch pipeline's roofline;
@@ -189,7 +190,8 @@ def main():
         gbs = float(xt[0]) / elapsed / 1e9
         link = {"bound": "pcie", "achieved": round(gbs, 3), "peak": PCIE_PEAK_GBS * world, "unit": "GB/s",
                 "frac": round(gbs / (PCIE_PEAK_GBS * world), 4), "bytes_per_record": host_info["bytes_per_record"],
-                "encoding": host_info["encoding"], "changelog_groups": host_info["groups"]}
+                "encoding": host_info["encoding"], "narrowed_by": host_info["narrowed_by"],
+                "changelog_groups": host_info["groups"]}
 
     xchg = None
     if world > 1 or args.force_exchange:
@@ -307,9 +309,9 @@ def host_steps(op, keys, ts, cols, pieces, spec, emit, world, args):
     pinned host buffers (what a poll loop holds) through hsg_push_batch_async;
     the library queues each batch's H2D copies on the op's copy stream while
     the batch before it computes (op_prestage), so a step costs
-    max(PCIe, kernels). Narrow transport unless --wide: the producer's
-    encoding (columnar.narrow_columns) is chosen here, before any timing, as a
-    decoder chooses it while decoding. The changelog goes into device columns
+    max(PCIe, kernels). Narrow transport unless --wide: the encoding is
+    chosen here by hsg_batch_narrow (the decoder's pass), before any timing,
+    as a decoder chooses it while decoding. The changelog goes into device columns
     registered for a group of batches and is drained after the group; a group
     is the whole step unless the step's worst-case rows exceed 96 GB of HBM
     (an asynchronous queue cannot be drained mid-way)."""
@@ -317,35 +319,45 @@ def host_steps(op, keys, ts, cols, pieces, spec, emit, world, args):
     import numpy as np
     import torch
     from hstream_amd import abi
-    from hstream_amd.columnar import make_batch, narrow_columns, narrow_keys
+    from hstream_amd.columnar import make_batch
+    from hstream_amd.ingest import _lib as ingest_lib
+    L = ingest_lib()
     descs, host = [], []
     nbytes = 0
     encs = set()
-    dec = [3 if t == abi.HSG_F64 else None for t in spec.col_types]  # the generators' decimals (datagen vrange)
+    narrow_s = 0.0
+    types = (C.c_int32 * max(1, len(spec.col_types)))(*spec.col_types)
     for s, m in pieces:
-        k = keys[s:s + m].cpu().numpy()
-        t = ts[s:s + m].cpu().numpy()
-        cs = [c[s:s + m].cpu().numpy() for c in cols]
-        if args.wide:
-            tsa, base, cs2, enc, scale = t, None, cs, [abi.HSG_ENC_FULL] * len(cs), [0] * len(cs)
-        else:
-            k = narrow_keys(k)
-            tsa, base, cs2, enc, scale = narrow_columns(t, cs, spec.col_types, dec, ts16=True)
-        pk = torch.from_numpy(np.ascontiguousarray(k)).pin_memory()
-        pt = torch.from_numpy(np.ascontiguousarray(tsa)).pin_memory()
-        pc = [torch.from_numpy(np.ascontiguousarray(c)).pin_memory() for c in cs2]
-        frames = isinstance(base, np.ndarray)
-        pf = torch.from_numpy(base).pin_memory() if frames else None
-        b, keep = make_batch(pk.numpy(), pt.numpy(), [c.numpy() for c in pc], None, abi.HSG_MEM_HOST,
-                             ts_base=None if frames else base, col_enc=enc, col_scale=scale,
-                             ts_frames=pf.numpy() if frames else None)
+        # the batch as a decoder holds it (full width, pinned), then narrowed
+        # in place by the product's hsg_batch_narrow -- the call
+        # hsg_decode_json_batch makes on every batch it decodes
+        pk = torch.empty(m, dtype=torch.int32).pin_memory()
+        pt = torch.empty(m, dtype=torch.int64).pin_memory()
+        pc = [torch.empty(m, dtype=c.dtype).pin_memory() for c in cols]
+        pf = torch.empty(-(-m // abi.HSG_TS16_FRAME), dtype=torch.int64).pin_memory()
+        pk.copy_(keys[s:s + m])
+        pt.copy_(ts[s:s + m])
+        for d, c in zip(pc, cols):
+            d.copy_(c[s:s + m])
+        b, keep = make_batch(pk.numpy().view(np.uint32), pt.numpy(), [c.numpy() for c in pc], None,
+                             abi.HSG_MEM_HOST)
+        if not args.wide:
+            t0 = time.perf_counter()
+            rc = L.hsg_batch_narrow(C.byref(b), C.cast(types, C.c_void_p), abi.HSG_NARROW_ALL, pf.data_ptr(), None,
+                                    cpu_threads())
+            narrow_s += time.perf_counter() - t0
+            if rc != abi.HSG_OK:
+                raise abi.HStreamGpuError(rc, "hsg_batch_narrow")
         descs.append(b)
         host.append((pk, pt, pc, pf, keep))
-        nbytes += pk.element_size() * m + pt.element_size() * m + sum(c.element_size() * m for c in pc)
-        nbytes += pf.numel() * 8 if frames else 0
-        tsn = "ts16" if frames else "ts32" if base is not None else "ts64"
-        encs.add(("k16" if pk.element_size() == 2 else "k32") + "+" + tsn + "+" + ",".join(
-            {abi.HSG_ENC_FULL: "full", abi.HSG_ENC_I32: "i32", abi.HSG_ENC_DEC32: "dec32"}[e] for e in enc))
+        kb = 2 if b.key_enc == abi.HSG_ENC_K16 else 4
+        tb = {abi.HSG_ENC_TS16: 2, abi.HSG_ENC_TS32: 4}.get(b.ts_enc, 8)
+        cb = [4 if b.col_enc[c] != abi.HSG_ENC_FULL else 8 for c in range(len(cols))]
+        nbytes += (kb + tb + sum(cb)) * m + (pf.numel() * 8 if b.ts_enc == abi.HSG_ENC_TS16 else 0)
+        tsn = {abi.HSG_ENC_TS16: "ts16", abi.HSG_ENC_TS32: "ts32"}.get(b.ts_enc, "ts64")
+        encs.add(("k16" if kb == 2 else "k32") + "+" + tsn + "+" + ",".join(
+            {abi.HSG_ENC_FULL: "full", abi.HSG_ENC_I32: "i32", abi.HSG_ENC_DEC32: "dec32"}[b.col_enc[c]]
+            for c in range(len(cols))))
     n_rank = sum(m for _, m in pieces)
     wpr = -(-spec.size_ms // spec.advance_ms) if spec.window_kind == abi.HSG_HOPPING else 1
     row_bytes = 4 + 8 + 8 + 8 + 8 * len(spec.aggs)
@@ -406,7 +418,10 @@ def host_steps(op, keys, ts, cols, pieces, spec, emit, world, args):
 
     step.keep = (descs, host, state)
     info = {"bytes_per_step": nbytes, "bytes_per_record": round(nbytes / max(1, n_rank), 3),
-            "encoding": sorted(encs), "groups": None}
+            "encoding": sorted(encs), "groups": None,
+            "narrowed_by": None if args.wide else
+            f"hsg_batch_narrow (the decoder's own pass), {cpu_threads()} host threads: "
+            f"{round(n_rank / max(narrow_s, 1e-9) / 1e6, 1)} M records/s"}
 
     class Info(dict):
         def __getitem__(self, k):
@@ -492,6 +507,28 @@ def per_record_block(eng, cfg, keys, ts, cols, pieces, args):
     n_rank = sum(m for _, m in pieces)
     roof = roofline(st0, st1, spec, emit)
     roof["kernel"] = pipeline_name(cfg, "per_record")
+    host = None
+    if args.input == "host":
+        # the drop-in's mode with host input (BASELINE.md's formula): pinned
+        # batches in the decoder's transport, H2D timed, rows into HBM
+        del descs, outs, drain
+        torch.cuda.empty_cache()
+        hstep, hinfo = host_steps(op, keys, ts, cols, pieces, spec, emit, 1, args)
+        hstep()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            hstep()
+        torch.cuda.synchronize()
+        elh = time.perf_counter() - t0
+        gbs = hinfo["bytes_per_step"] * k / elh / 1e9
+        host = {"value": round(n_rank * k / elh, 1), "unit": "records/s", "steps": k,
+                "ms_per_step": round(elh * 1e3 / k, 3),
+                "input": "pinned host batches, H2D in the timed region (BASELINE.md reporting formula)",
+                "input_link": {"bound": "pcie", "achieved": round(gbs, 3), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(gbs / PCIE_PEAK_GBS, 4),
+                               "bytes_per_record": hinfo["bytes_per_record"], "encoding": hinfo["encoding"]}}
+        del hstep
     if not (args.records or args.batch):
         # the committed PMC summary of this pipeline (tools/traffic.sh <cfg>_pr --emit per_record)
         import glob
@@ -502,9 +539,10 @@ def per_record_block(eng, cfg, keys, ts, cols, pieces, args):
             roof["traffic_source"] = os.path.relpath(paths[-1], ROOT)
     out = {"value": round(n_rank * k / el, 1), "unit": "records/s", "steps": k,
            "ms_per_step": round(el * 1e3 / k, 3), "emit": "per_record",
-           "rows_per_step": int((st1["pairs_total"] - st0["pairs_total"]) / k), "roofline": roof}
+           "input": "HBM-resident device columns",
+           "rows_per_step": int((st1["pairs_total"] - st0["pairs_total"]) / k), "roofline": roof,
+           "host_input": host}
     op.close()
-    del descs, outs
     torch.cuda.empty_cache()
     return out
 

@@ -65,6 +65,13 @@ HSG_ENC_DEC32 = 3
 HSG_ENC_K16 = 4
 HSG_ENC_TS16 = 5
 HSG_TS16_FRAME = 4096
+# hsg_batch_narrow / hsg_decode_json_batch: encodings the consumer accepts (hstream_ingest.h)
+HSG_NARROW_K16 = 1
+HSG_NARROW_TS16 = 2
+HSG_NARROW_TS32 = 4
+HSG_NARROW_I32 = 8
+HSG_NARROW_DEC32 = 16
+HSG_NARROW_ALL = 31
 
 # hsg_op_config.flags
 HSG_OPF_LITERAL_FORMS = 1
@@ -120,6 +127,21 @@ class hsg_batch(C.Structure):
         ("col_enc", C.c_uint8 * 8),
         ("col_scale", C.c_uint8 * 8),
         ("ts_frames", C.c_void_p),
+    ]
+
+
+class hsg_decode_buffers(C.Structure):
+    _fields_ = [
+        ("capacity", C.c_uint64),
+        ("key_id", C.c_void_p),
+        ("ts", C.c_void_p),
+        ("ts_frames", C.c_void_p),
+        ("cols", C.POINTER(C.c_void_p)),
+        ("valid", C.POINTER(C.c_void_p)),
+        ("allow", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("col_ptrs", C.c_void_p * 8),
+        ("valid_ptrs", C.c_void_p * 8),
     ]
 
 
@@ -208,6 +230,8 @@ INGEST_SYMBOLS = [
     "hsg_keydict_spelling_text",
     "hsg_decoder_create",
     "hsg_decoder_destroy",
+    "hsg_batch_narrow",
+    "hsg_decode_json_batch",
     "hsg_decode_json",
     "hsg_decode_json_spelled",
 ]

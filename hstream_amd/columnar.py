@@ -197,7 +197,11 @@ def narrow_columns(ts, cols, col_types, dec_scale=None, ts16=False):
         elif dec_scale and dec_scale[j] is not None:
             s = int(dec_scale[j])
             m = np.rint(c * 10.0**s)
-            if c.size == 0 or (np.abs(m).max() < 2**31 and np.array_equal(m / 10.0**s, c)):
+            # lossless means bit-identical: -0.0 == 0.0 numerically, but it
+            # would come back as +0.0 (f64 MIN / MAX order them, the SUM's
+            # text differs), so the comparison is on the bit patterns
+            if c.size == 0 or (np.abs(m).max() < 2**31 and np.array_equal(
+                    (m.astype(np.int64) / 10.0**s).view(np.int64), np.asarray(c, np.float64).view(np.int64))):
                 c, e, sc = m.astype(np.int32), abi.HSG_ENC_DEC32, s
         out.append(c)
         enc.append(e)
@@ -293,6 +297,14 @@ class OpHandle:
         wm = C.c_int64(watermark)
         rc = self._fn("push_batch")(self._h, C.byref(b), C.byref(wm))
         del keep
+        self._check(rc, "push_batch")
+        return wm.value
+
+    def push_batch(self, batch, watermark=-1) -> int:
+        """hsg_push_batch of a ready hsg_batch (e.g. DecodedBatch.batch, in the
+        decoder's transport encoding)."""
+        wm = C.c_int64(watermark)
+        rc = self._fn("push_batch")(self._h, C.byref(batch), C.byref(wm))
         self._check(rc, "push_batch")
         return wm.value
 

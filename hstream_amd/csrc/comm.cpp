@@ -136,6 +136,18 @@ int comm_unique_id(uint8_t *out) {
   return HSG_OK;
 }
 
+// comm_agree's stream and buffer, made with the communicator so that a rank
+// whose op creation fails later still reaches the agreement without
+// allocating anything
+static int agree_alloc(Comm *c, std::string &err) {
+  if (hipStreamCreateWithFlags(&c->agree_s, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void **)&c->agree_buf, ((size_t)c->nranks + 1) * sizeof(int64_t)) != hipSuccess) {
+    err = "communicator: agreement stream / buffer";
+    return HSG_E_DEVICE;
+  }
+  return HSG_OK;
+}
+
 int comm_create(const uint8_t *id_bytes, int rank, int nranks, int device, int transport, uint64_t batch_cap,
                 Comm **out, std::string &err) {
   if (nranks > kMaxRanks) {
@@ -156,20 +168,27 @@ int comm_create(const uint8_t *id_bytes, int rank, int nranks, int device, int t
     }
     // the largest collective: the classic exchange's packed records (<= 12 words each)
     c->slot_bytes = batch_cap * 12 * 8 + 4096;
-    int rc = host_open(name, rank, nranks, c->slot_bytes, &c->host, err);
+    int rc = agree_alloc(c, err);
+    if (rc == HSG_OK) rc = host_open(name, rank, nranks, c->slot_bytes, &c->host, err);
     if (rc != HSG_OK) {
-      delete c;
+      comm_destroy(c);
       return rc;
     }
     *out = c;
     return HSG_OK;
+  }
+  // the agreement buffer first: a failure here comes before any collective
+  int arc = agree_alloc(c, err);
+  if (arc != HSG_OK) {
+    comm_destroy(c);
+    return arc;
   }
   ncclUniqueId id;
   memcpy(&id, id_bytes, sizeof(id));
   ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
   if (r != ncclSuccess) {
     err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
-    delete c;
+    comm_destroy(c);
     return HSG_E_COMM;
   }
   *out = c;
@@ -178,40 +197,43 @@ int comm_create(const uint8_t *id_bytes, int rank, int nranks, int device, int t
 
 // A communicator of the same ranks for one operator (collective over the
 // parent's ranks, so every rank calls it in the same op-creation order).
-// comm_agree's stream and buffer (a failure here fails the split, before any
-// op state exists)
-static int agree_alloc(Comm *c, std::string &err) {
-  if (hipStreamCreateWithFlags(&c->agree_s, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc((void **)&c->agree_buf, ((size_t)c->nranks + 1) * sizeof(int64_t)) != hipSuccess) {
-    err = "comm_split: agreement stream / buffer";
-    return HSG_E_DEVICE;
-  }
-  return HSG_OK;
-}
-
+// The split is collective over the parent's ranks, and so is its outcome:
+// every rank allocates the child's agreement buffer first (nothing collective
+// yet), takes part in the split whatever that allocation did, and then the
+// ranks agree on the parent -- whose agreement buffer exists since the engine
+// was created -- so that a failure on one rank (its allocation or its split)
+// fails the split on every rank, and no rank goes on to a collective of the
+// child that a peer never reaches. Callers serialize splits of one parent
+// (hsg_op_create holds the engine's lock), which the parent's one agreement
+// buffer needs.
 int comm_split(Comm *parent, Comm **out, std::string &err) {
+  *out = nullptr;
   Comm *c = new Comm();
   c->rank = parent->rank;
   c->nranks = parent->nranks;
+  std::string lerr;
+  int rc = agree_alloc(c, lerr);
   if (parent->host) {
     c->slot_bytes = parent->slot_bytes;
     const std::string name = parent->host->name + "." + std::to_string(++parent->host->splits);
-    int rc = host_open(name, c->rank, c->nranks, c->slot_bytes, &c->host, err);
-    if (rc != HSG_OK) {
-      delete c;
-      return rc;
+    const int src = host_open(name, c->rank, c->nranks, c->slot_bytes, &c->host, lerr);
+    if (rc == HSG_OK) rc = src;
+  } else {
+    const ncclResult_t r = ncclCommSplit(parent->comm, 0, parent->rank, &c->comm, nullptr);
+    if (r != ncclSuccess && rc == HSG_OK) {
+      lerr = std::string("ncclCommSplit: ") + ncclGetErrorString(r);
+      rc = HSG_E_COMM;
     }
-    *out = c;
-    return agree_alloc(c, err);
   }
-  ncclResult_t r = ncclCommSplit(parent->comm, 0, parent->rank, &c->comm, nullptr);
-  if (r != ncclSuccess) {
-    err = std::string("ncclCommSplit: ") + ncclGetErrorString(r);
-    delete c;
-    return HSG_E_COMM;
+  std::string aerr;
+  const int arc = comm_agree(parent, rc, aerr);
+  if (rc != HSG_OK || arc != HSG_OK) {
+    err = rc != HSG_OK ? lerr : aerr;
+    comm_destroy(c);
+    return rc != HSG_OK ? rc : arc;
   }
   *out = c;
-  return agree_alloc(c, err);
+  return HSG_OK;
 }
 
 void comm_destroy(Comm *c) {

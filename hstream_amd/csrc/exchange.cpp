@@ -271,7 +271,7 @@ static int push_sharded_classic(OpDevice &d, const hsg_op_config &cfg, const Pro
 int push_sharded(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, PushResult &r,
                  std::string &err) {
   bool need_seq = cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.window_kind == HSG_SESSION;
-  for (int q = 0; q < prog.n_slots; ++q) need_seq = need_seq || prog.slot_op[q] == S_LAST_SEQ;
+  need_seq = need_seq || prog_needs_seq(prog) || prog_has_forms(prog);
   if (d.use_part && d.xpart_log2 >= 0 && !need_seq) {
     bool fallback = false;
     int rc = push_sharded_fast(d, cfg, prog, a, r, err, fallback);
@@ -333,12 +333,7 @@ static int push_sharded_classic(OpDevice &d, const hsg_op_config &cfg, const Pro
   const bool time_win = cfg.window_kind == HSG_TUMBLING || cfg.window_kind == HSG_HOPPING;
   const bool may_be_late =
       time_win && min_ts != INT64_MAX && wm_global > (int64_t)((uint64_t)min_ts + (uint64_t)cfg.grace_ms);
-  const bool need_seq = cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.window_kind == HSG_SESSION ||
-                        [&] {
-                          for (int q = 0; q < prog.n_slots; ++q)
-                            if (prog.slot_op[q] == S_LAST_SEQ) return true;
-                          return false;
-                        }();
+  const bool need_seq = cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.window_kind == HSG_SESSION || prog_needs_seq(prog);
   XLayout L = layout_for(cfg, need_seq, may_be_late, any_valid);
   // 3. per-record stream time in the global order (rare)
   if (may_be_late) {

@@ -120,28 +120,30 @@ int build_program(const hsg_op_config &cfg, const std::vector<int32_t> &col_type
     prog.out_kind[j] = kind;
     prog.out_a[j] = a;
     prog.out_b[j] = b;
-    // the literal form (hsg_internal.h FormKind; the user's column c is the
-    // internal column 3c here, followed by its decimal / integral shadows)
-    int fk = F_NONE, fa = 0, fb = 0;
+    // the literal form (hsg_internal.h FormKind): a form slot over the
+    // output's column that reads bit 1 of its valid bytes
+    int fk = F_NONE, fa = 0;
     if (forms) {
       switch (g.kind) {
-        case HSG_SUM: fk = F_SUM, fa = add_slot(S_CNT, c + 1); break;
+        case HSG_SUM: fk = F_SUM, fa = add_slot(S_CNT_DEC, c); break;
         case HSG_MIN:
-          fk = F_MINMAX, fa = add_slot(isf ? S_MIN_F : S_MIN_I, c + 2), fb = add_slot(S_CNT, c);
+        case HSG_MAX: {
+          const int op = g.kind == HSG_MIN ? S_TIE_MIN : S_TIE_MAX;
+          fk = g.kind == HSG_MIN ? F_MIN : F_MAX;
+          fa = add_slot(op, c);
+          if (fa >= 0) prog.slot_aux[fa] = a;  // the MIN / MAX slot it breaks ties of
           break;
-        case HSG_MAX:
-          fk = F_MINMAX, fa = add_slot(isf ? S_MAX_F : S_MAX_I, c + 2), fb = add_slot(S_CNT, c);
-          break;
-        case HSG_LAST: fk = F_LAST, fa = last_pair(c + 1), fb = last_pair(c + 2); break;
+        }
+        case HSG_LAST: fk = F_LAST, fa = add_slot(S_LAST_FORM, c); break;
         default: break;
       }
-      if (fa < 0 || fb < 0) return fail(err, HSG_E_INVALID, "too many state slots");
+      if (fa < 0) return fail(err, HSG_E_INVALID, "too many state slots");
     }
     prog.form_kind[j] = fk;
     prog.form_a[j] = fa;
-    prog.form_b[j] = fb;
   }
   prog.n_out = (int)aggs.size();
+  for (int s = 0; s < prog.n_slots; ++s) prog.ties |= slot_is_tie(prog.slot_op[s]) ? 1 : 0;
   return HSG_OK;
 }
 
@@ -261,7 +263,7 @@ struct hsg_op {
   hsg_op_config cfg;
   std::vector<int32_t> col_types;  // the user's value columns
   std::vector<hsg_agg> aggs;
-  int32_t user_cols = 0;           // cfg.n_cols is the kernels' (internal) count: 3x with literal forms
+  int32_t user_cols = 0;           // value columns of the caller's batches (= cfg.n_cols)
   Program prog;
   OpDevice dev;  // every HBM buffer + stream + events (hsg_ops.h)
   // Sharded ops own a communicator split from the engine's at creation, so
@@ -395,23 +397,10 @@ extern "C" int hsg_op_create(hsg_engine *eng, const hsg_op_config *cfg, hsg_op *
     op->cfg.aggs = nullptr;
     if (op->cfg.window_kind == HSG_TUMBLING) op->cfg.advance_ms = op->cfg.size_ms;
     memset(&op->stats, 0, sizeof(op->stats));
-    // literal forms: every user column c is the internal columns 3c, 3c + 1,
-    // 3c + 2 (all values / decimal / integral literals, stage_batch derives
-    // their validity); the kernels see only the internal ones
+    // literal forms: extra slots read the literal bit of the valid bytes
     const bool forms = (cfg->flags & HSG_OPF_LITERAL_FORMS) != 0;
-    std::vector<int32_t> itypes = op->col_types;
-    std::vector<hsg_agg> iaggs = op->aggs;
-    if (forms) {
-      if (3 * cfg->n_cols > kMaxCols) {
-        delete op;
-        eng->err = "HSG_OPF_LITERAL_FORMS takes at most 2 value columns";
-        return HSG_E_INVALID;
-      }
-      itypes.clear();
-      for (int c = 0; c < cfg->n_cols; ++c) itypes.insert(itypes.end(), 3, op->col_types[c]);
-      for (auto &g : iaggs) g.column *= 3;
-      op->cfg.n_cols = 3 * cfg->n_cols;
-    }
+    const std::vector<int32_t> &itypes = op->col_types;
+    const std::vector<hsg_agg> &iaggs = op->aggs;
     op->user_cols = cfg->n_cols;
     rc = build_program(op->cfg, itypes, iaggs, op->prog, eng->err, forms);
     if (rc != HSG_OK) { delete op; return rc; }

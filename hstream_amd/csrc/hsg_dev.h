@@ -78,12 +78,22 @@ __device__ inline int64_t slot_identity_dev(int32_t op) {
     case S_MIN_F: return (int64_t)f64_ord(9223372036854775807.0);
     case S_MAX_F: return (int64_t)f64_ord(-9223372036854775808.0);
     case S_SUM_F: return INT64_MIN;  // -0.0 (slot_identity)
+    case S_TIE_MIN: return 1;        // seq 0, integral: the initial maxBound
     default: return 0;
   }
 }
 
 __device__ inline bool rec_present(const Batch &b, int c, uint64_t i) {
   return b.valid[c] == nullptr || b.valid[c][i] != 0;
+}
+// the value's JSON literal prints in Generic form (bit 1 of its valid byte,
+// hstream_ingest.h literal_forms)
+__device__ inline bool rec_decimal(const Batch &b, int c, uint64_t i) {
+  return b.valid[c] != nullptr && (b.valid[c][i] & 2u) != 0;
+}
+// a form slot's word for a present record: (seq + 1) << 1 | integral literal
+__device__ inline int64_t form_word(const Batch &b, int c, uint64_t i, uint64_t seq1) {
+  return (int64_t)((seq1 << 1) | (rec_decimal(b, c, i) ? 0u : 1u));
 }
 
 // Contribution of record i to state slot s (identity when the field is absent).
@@ -105,6 +115,10 @@ __device__ inline int64_t slot_elem(const Program &prog, int s, const Batch &b, 
     case S_MIN_F:
     case S_MAX_F: return (int64_t)f64_ord(__builtin_bit_cast(double, b.col[c][i]));
     case S_LAST_SEQ: return (int64_t)seq1;
+    case S_CNT_DEC: return rec_decimal(b, c, i) ? 1 : 0;
+    case S_TIE_MIN:
+    case S_TIE_MAX:
+    case S_LAST_FORM: return form_word(b, c, i, seq1);
     default: return 0;
   }
 }
@@ -121,13 +135,60 @@ __device__ inline int64_t slot_combine(int op, int64_t a, int64_t e) {
     case S_MAX_I: return e > a ? e : a;
     case S_MIN_F: return (uint64_t)e < (uint64_t)a ? e : a;
     case S_MAX_F: return (uint64_t)e > (uint64_t)a ? e : a;
-    default: return a;
+    case S_CNT_DEC: return (int64_t)((uint64_t)a + (uint64_t)e);
+    case S_LAST_FORM: return (uint64_t)e > (uint64_t)a ? e : a;
+    default: return a;  // S_TIE_*: combined with their MIN / MAX slot (tie_combine)
   }
 }
 
+// "e is better than a" for the MIN / MAX slot op vop (equal: a tie)
+__device__ inline bool extreme_better(int vop, int64_t e, int64_t a) {
+  switch (vop) {
+    case S_MIN_I: return e < a;
+    case S_MAX_I: return e > a;
+    case S_MIN_F: return (uint64_t)e < (uint64_t)a;
+    case S_MAX_F: return (uint64_t)e > (uint64_t)a;
+    default: return false;
+  }
+}
+// tie word after a <- a (+) e, from the MIN / MAX values before the combine
+// (va, ve): the better value's word; on a tie the earlier literal for MIN
+// (min n x = n) and the later for MAX (max n x = x) -- by record sequence, so
+// any grouping of a record fold gives the sequential fold's word
+__device__ inline int64_t tie_combine(int op, int vop, int64_t va, int64_t ve, int64_t ta, int64_t te) {
+  if (extreme_better(vop, ve, va)) return te;
+  if (va != ve) return ta;
+  if (op == S_TIE_MIN) return (uint64_t)te < (uint64_t)ta ? te : ta;
+  return (uint64_t)te > (uint64_t)ta ? te : ta;
+}
+
 // Row-wise combine over MS compile-time-bounded slots (registers, no scratch).
+// the value of slot v of a register row (v not a compile-time index)
+template <int MS>
+__device__ inline int64_t reg_at(const int64_t (&r)[MS], int v) {
+  int64_t x = 0;
+#pragma unroll
+  for (int s = 0; s < MS; ++s)
+    if (s == v) x = r[s];
+  return x;
+}
+
+// tie words first, against the MIN / MAX values before the combine
+template <int MS>
+__device__ inline void combine_ties(const Program &prog, int64_t (&a)[MS], const int64_t (&e)[MS]) {
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    if (s >= prog.n_slots) break;
+    const int op = prog.slot_op[s];
+    if (!slot_is_tie(op)) continue;
+    const int v = prog.slot_aux[s];
+    a[s] = tie_combine(op, prog.slot_op[v], reg_at<MS>(a, v), reg_at<MS>(e, v), a[s], e[s]);
+  }
+}
+
 template <int MS>
 __device__ inline void combine_row(const Program &prog, int64_t (&a)[MS], const int64_t (&e)[MS]) {
+  if (prog.ties) combine_ties<MS>(prog, a, e);
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
     if (s >= prog.n_slots) break;
@@ -197,39 +258,56 @@ __device__ inline int64_t out_value_reg(const Program &prog, int j, const int64_
 
 // Literal forms of a row's outputs (hsg_rows.form; hsg_internal.h FormKind):
 // bit 2j = output j prints as an integer, bit 2j + 1 = it is the aggregate's
-// initial value. `own` = the output's own slot, fa / fb its form slots.
-__device__ inline uint32_t form_bits_w(int kind, int64_t own, int64_t fa, int64_t fb) {
+// initial value. fa = the output's form slot.
+__device__ inline uint32_t form_bits_w(int kind, int64_t fa) {
   switch (kind) {
     case F_SUM: return fa == 0 ? 1u : 0u;
-    case F_MINMAX: return fb == 0 ? 3u : (fa == own ? 1u : 0u);
-    case F_LAST:
-      if (fa == 0 && fb == 0) return 3u;
-      return (uint64_t)fb > (uint64_t)fa ? 1u : 0u;
+    case F_MIN: return fa == 1 ? 3u : (uint32_t)(fa & 1);
+    case F_MAX:
+    case F_LAST: return fa == 0 ? 3u : (uint32_t)(fa & 1);
     default: return 0u;
   }
 }
 __device__ inline uint32_t out_form(const Program &prog, const int64_t *row) {
   uint32_t f = 0;
   for (int j = 0; j < prog.n_out; ++j)
-    if (prog.form_kind[j] != F_NONE)
-      f |= form_bits_w(prog.form_kind[j], row[prog.out_a[j]], row[prog.form_a[j]], row[prog.form_b[j]]) << (2 * j);
+    if (prog.form_kind[j] != F_NONE) f |= form_bits_w(prog.form_kind[j], row[prog.form_a[j]]) << (2 * j);
   return f;
 }
 template <int MS>
 __device__ inline uint32_t out_form_reg(const Program &prog, const int64_t (&r)[MS]) {
   uint32_t f = 0;
-  for (int j = 0; j < prog.n_out; ++j) {
-    if (prog.form_kind[j] == F_NONE) continue;
-    int64_t own = 0, fa = 0, fb = 0;
+  for (int j = 0; j < prog.n_out; ++j)
+    if (prog.form_kind[j] != F_NONE) f |= form_bits_w(prog.form_kind[j], reg_at<MS>(r, prog.form_a[j])) << (2 * j);
+  return f;
+}
+
+// Session merge, acc <- sessionMergeF rk acc cur (SessionWindowedStream.hs
+// :100-114; acc = the new record with the sessions merged so far, cur = the
+// next overlapped session in end order): the aggregate components'
+// aggregateMergeF (Codegen.hs:409-469) -- counts and sums add, MIN / MAX keep
+// the extreme with min n1 n2 / max n1 n2 on ties (n1 = acc's literal for
+// MIN, n2 = cur's for MAX), passthrough columns take cur's (o2)
+template <int MS>
+__device__ inline void merge_row(const Program &prog, int64_t (&acc)[MS], const int64_t (&cur)[MS]) {
+  if (prog.ties) {
 #pragma unroll
     for (int s = 0; s < MS; ++s) {
-      if (s == prog.out_a[j]) own = r[s];
-      if (s == prog.form_a[j]) fa = r[s];
-      if (s == prog.form_b[j]) fb = r[s];
+      if (s >= prog.n_slots) break;
+      const int op = prog.slot_op[s];
+      if (!slot_is_tie(op)) continue;
+      const int v = prog.slot_aux[s], vop = prog.slot_op[v];
+      const int64_t va = reg_at<MS>(acc, v), vc = reg_at<MS>(cur, v);
+      if (extreme_better(vop, vc, va) || (va == vc && op == S_TIE_MAX)) acc[s] = cur[s];
     }
-    f |= form_bits_w(prog.form_kind[j], own, fa, fb) << (2 * j);
   }
-  return f;
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    if (s >= prog.n_slots) break;
+    const int op = prog.slot_op[s];
+    if (op == S_LAST_SEQ || op == S_LAST_VAL || op == S_LAST_FORM) acc[s] = cur[s];
+    else acc[s] = slot_combine(op, acc[s], cur[s]);
+  }
 }
 
 // Per-record stream time for the records of one tile (record (r, thread) =

@@ -26,7 +26,18 @@ enum SlotOp : int32_t {
   S_MAX_F = 7,    // max over order-preserving u64 image, identity img(-2^63)
   S_LAST_SEQ = 8, // max over (global record seq + 1) of present records
   S_LAST_VAL = 9, // value of the record named by the LAST_SEQ slot just before it
+  // literal forms (HSG_OPF_LITERAL_FORMS; bit 1 of a valid byte: the value's
+  // JSON literal prints in Generic form, hstream_ingest.h literal_forms)
+  S_CNT_DEC = 10,   // += present(col) with a decimal literal        (SUM's form)
+  S_TIE_MIN = 11,   // tie word of the MIN slot slot_aux[s]: (seq + 1) << 1 | integral literal of the
+                    // earliest record holding the minimum (min n x = n on ties); identity 1 (seq 0,
+                    // integral: the initial maxBound wins a tie with it)
+  S_TIE_MAX = 12,   // same for the MAX slot slot_aux[s], the latest record (max n x = x); identity 0
+  S_LAST_FORM = 13, // max over (seq + 1) << 1 | integral literal of present records (LAST's form)
 };
+
+__host__ __device__ inline bool slot_is_form(int32_t op) { return op >= S_CNT_DEC && op <= S_LAST_FORM; }
+__host__ __device__ inline bool slot_is_tie(int32_t op) { return op == S_TIE_MIN || op == S_TIE_MAX; }
 
 // Output column j = f(slot a [, slot b]).
 enum OutKind : int32_t {
@@ -37,15 +48,14 @@ enum OutKind : int32_t {
   O_AVG_F = 4,    // slot a (f64 sum) / slot b (count)
 };
 
-// How output j's literal form is read (HSG_OPF_LITERAL_FORMS): from slots
-// over the internal columns 3c (every value), 3c + 1 (values with a decimal
-// literal), 3c + 2 (values with an integral literal) of user column c.
+// How output j's literal form is read (HSG_OPF_LITERAL_FORMS) from its form
+// slot a (the S_CNT_DEC / S_TIE_* / S_LAST_FORM slot over the output's column)
 enum FormKind : int32_t {
-  F_NONE = 0,    // no form bits (COUNT, COUNT(col), AVG; ops without the flag)
-  F_SUM = 1,     // a = COUNT over 3c + 1: integral iff 0 (a Scientific sum takes the smaller exponent)
-  F_MINMAX = 2,  // a = MIN / MAX over 3c + 2, b = COUNT over 3c: identity iff b = 0, else
-                 //     integral iff a equals the output's own slot (an integral literal won)
-  F_LAST = 3,    // a / b = LAST_SEQ over 3c + 1 / 3c + 2: identity iff both 0, else integral iff b > a
+  F_NONE = 0,  // no form bits (COUNT, COUNT(col), AVG; ops without the flag)
+  F_SUM = 1,   // a = S_CNT_DEC: integral iff 0 (a Scientific sum takes the smaller exponent)
+  F_MIN = 2,   // a = S_TIE_MIN: the winning literal's bit 0; the initial value iff a == 1
+  F_MAX = 3,   // a = S_TIE_MAX: the winning literal's bit 0; the initial value iff a == 0
+  F_LAST = 4,  // a = S_LAST_FORM: the last present literal's bit 0; the initial value iff a == 0
 };
 
 struct Program {
@@ -58,7 +68,8 @@ struct Program {
   int32_t out_b[kMaxAggs];
   int32_t form_kind[kMaxAggs];  // FormKind
   int32_t form_a[kMaxAggs];
-  int32_t form_b[kMaxAggs];
+  int32_t slot_aux[kMaxSlots];  // S_TIE_*: the MIN / MAX slot the tie word belongs to
+  int32_t ties;                 // the program has S_TIE_* slots
 };
 
 // u64 division by an invariant divisor (Granlund–Montgomery), exact for all n.
@@ -244,8 +255,27 @@ inline int64_t slot_identity(int32_t op) {
     case S_MIN_F: return (int64_t)f64_ord((double)INT64_MAX);
     case S_MAX_F: return (int64_t)f64_ord((double)INT64_MIN);
     case S_SUM_F: return INT64_MIN;  // -0.0: x + -0.0 == x for every x, and a SUM nothing reached stays -0.0
+    case S_TIE_MIN: return 1;
     default: return 0;
   }
+}
+// the op keeps literal forms (its slots read bit 1 of the valid bytes, which
+// only the generic record paths carry: not the partition layouts)
+inline bool prog_has_forms(const Program &p) {
+  for (int s = 0; s < p.n_slots; ++s)
+    if (slot_is_form(p.slot_op[s])) return true;
+  return false;
+}
+// the op's slots need each record's global sequence number
+inline bool prog_needs_seq(const Program &p) {
+  for (int s = 0; s < p.n_slots; ++s)
+    if (p.slot_op[s] == S_LAST_SEQ || slot_is_tie(p.slot_op[s]) || p.slot_op[s] == S_LAST_FORM) return true;
+  return false;
+}
+inline bool prog_has_tie(const Program &p) {
+  for (int s = 0; s < p.n_slots; ++s)
+    if (slot_is_tie(p.slot_op[s])) return true;
+  return false;
 }
 
 // ---- kernel launchers (defined in the .hip files) --------------------------
@@ -283,16 +313,6 @@ struct WidenArgs {
   double div[kMaxCols];          // HSG_ENC_DEC32: 10^scale; 0: HSG_ENC_I32
 };
 void launch_widen(hipStream_t s, const WidenArgs &w);
-// literal forms (HSG_OPF_LITERAL_FORMS): validity of the internal columns
-// 3c / 3c + 1 / 3c + 2 from user column c's valid bytes (bit 0 present, bit 1
-// decimal literal; null = every value present with an integral literal)
-struct FormArgs {
-  uint64_t n;
-  int32_t ncols;                 // user columns (<= kMaxCols / 3)
-  const uint8_t *valid[kMaxCols];
-  uint8_t *out[kMaxCols];
-};
-void launch_forms(hipStream_t s, const FormArgs &f);
 // dump ordering on the device (op_device.cpp sort_dump_rows_device): the
 // window index of each row (ws / adv - k_epoch) and the identity permutation;
 // then one 4-/8-byte column gathered through a permutation
@@ -343,6 +363,11 @@ void launch_tw_closed(hipStream_t s, const TwTable &t, uint64_t cap, const TwPar
 void launch_tw_reinsert(hipStream_t s, const uint64_t *src, uint64_t n, const TwTable &dst, const TwParams &p,
                         DevScalars *sc, bool skip_closed, unsigned long long *kept);
 unsigned grid_for(uint64_t n, unsigned tpb);
+// touched list (hsg_part.h) across a table rebuild: slots -> group keys in the
+// old table, group keys -> slots in the new one (kTouchSkipEntry kept)
+constexpr uint32_t kTouchSkipEntry = 0xFFFFFFFFu;
+void launch_touch_keys(hipStream_t s, const TwTable &t, const uint32_t *touched, uint64_t n, uint64_t *keys);
+void launch_touch_slots(hipStream_t s, const TwTable &t, const uint64_t *keys, uint64_t n, uint32_t *touched);
 
 constexpr int kTileThreads = 256;
 constexpr int kRecPerThread = 4;

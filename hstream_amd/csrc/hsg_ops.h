@@ -78,8 +78,7 @@ struct OpDevice {
   bool sc_clean = false;        // per-batch scalars already cleared on the stream
   uint64_t batch_cap = 0;       // records this op can take in one push (after exchange)
   int32_t user_cols = 0;        // value columns of the caller's batches (n_cols: the kernels', internal)
-  bool forms = false;           // HSG_OPF_LITERAL_FORMS: columns tripled by stage_batch (expand_forms)
-  uint8_t *form_valid = nullptr;  // [n_cols][batch_cap] validity of the internal columns
+  bool forms = false;           // HSG_OPF_LITERAL_FORMS: rows carry literal forms (hsg_rows.form)
   uint64_t wpr = 1;             // max windows per record
   uint64_t n_tiles_cap = 0;
   int64_t *tile_max = nullptr, *tile_min = nullptr, *tile_prefix = nullptr;

@@ -11,7 +11,7 @@ constexpr int kPartThreads = 256;
 constexpr int kPartMaxLog2 = 11;                      // up to 2048 partitions
 constexpr int kPartMaxWords = 11;                     // 2 + 8 columns + seq
 constexpr uint64_t kTouchChunk = 4096;                // touched-list entries per emit workgroup
-constexpr uint32_t kTouchSkip = 0xFFFFFFFFu;           // touched-list entry of a later update of a group
+constexpr uint32_t kTouchSkip = kTouchSkipEntry;          // touched-list entry of a later update of a group
 constexpr int kMaxSeg = 8;                            // deferred flush segments per aggregation workgroup
 
 // A partitioned record is `words` 8-byte words (wide layout):

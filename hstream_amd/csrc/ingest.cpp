@@ -1011,6 +1011,38 @@ extern "C" int hsg_decode_json(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, 
                                  n_threads);
 }
 
+extern "C" int hsg_decode_json_batch(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, const char *buf,
+                                     const uint64_t *off, const int64_t *rec_ts, hsg_decode_buffers *bufs,
+                                     hsg_batch *out, uint8_t *status, uint64_t *rejected, uint32_t *spell,
+                                     int n_threads) {
+  if (!dec || !bufs || !out || n > bufs->capacity || !bufs->key_id || !bufs->ts) return HSG_E_INVALID;
+  const int C = (int)dec->cols.size();
+  if (C > 8 || (C && (!bufs->cols || !bufs->valid))) return HSG_E_INVALID;
+  int rc = hsg_decode_json_spelled(dec, dict, n, buf, off, rec_ts, bufs->key_id, bufs->ts, bufs->cols, bufs->valid,
+                                   status, rejected, spell, n_threads);
+  if (rc != HSG_OK) return rc;
+  memset(out, 0, sizeof(*out));
+  out->n = n;
+  out->mem = HSG_MEM_HOST;
+  out->n_cols = C;
+  out->key_id = bufs->key_id;
+  out->ts = bufs->ts;
+  int32_t types[8] = {};
+  for (int c = 0; c < C; ++c) {
+    bufs->col_ptrs[c] = bufs->cols[c];
+    bufs->valid_ptrs[c] = bufs->valid[c];
+    types[c] = dec->cols[c].type;
+  }
+  out->cols = bufs->col_ptrs;
+  out->valid = bufs->valid_ptrs;
+  uint32_t present = 0;
+  rc = hsg_batch_narrow(out, types, bufs->allow, bufs->ts_frames, &present, n_threads);
+  if (rc != HSG_OK) return rc;
+  for (int c = 0; c < C; ++c)
+    if ((present >> c) & 1u) bufs->valid_ptrs[c] = nullptr;
+  return HSG_OK;
+}
+
 extern "C" int hsg_keydict_spelling_text(const hsg_keydict *d, uint32_t spell, char *buf, size_t cap, size_t *len) {
   if (!d || !len) return HSG_E_INVALID;
   if (!(spell & HSG_SPELL_ALT)) return hsg_keydict_text(d, spell, buf, cap, len);

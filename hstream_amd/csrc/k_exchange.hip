@@ -2,7 +2,7 @@
 // stable partition by owner, packing into 8-byte-word records for one RCCL
 // all-to-all-v, unpacking into columnar staging on the receiving rank.
 //
-// Record words: [key | valid bits << 32] [ts] [col 0..C-1] [seq]? [wm]?
+// Record words: [key | valid bits << 32 | literal-form bits << 40] [ts] [col 0..C-1] [seq]? [wm]?
 // seq = the record's index in the global arrival order (rank slices in rank
 // order), wm = its stream time (only when some record could be late).
 #include "hsg_dev.h"
@@ -86,9 +86,12 @@ __global__ void k_x_pack(Batch b, XLayout L, const uint32_t *sidx, uint64_t m, u
   for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < m; q += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t i = sidx[q];
     uint64_t *w = send + q * L.words;
-    uint64_t vb = 0;
-    for (int c = 0; c < L.ncols; ++c) vb |= (uint64_t)(rec_present(b, c, i) ? 1u : 0u) << c;
-    w[0] = (uint64_t)b.key[i] | (vb << 32);
+    uint64_t vb = 0, db = 0;  // presence, and the literal-form bit of the valid bytes
+    for (int c = 0; c < L.ncols; ++c) {
+      vb |= (uint64_t)(rec_present(b, c, i) ? 1u : 0u) << c;
+      db |= (uint64_t)(rec_decimal(b, c, i) ? 1u : 0u) << c;
+    }
+    w[0] = (uint64_t)b.key[i] | (vb << 32) | (db << 40);
     w[1] = (uint64_t)b.ts[i];
     for (int c = 0; c < L.ncols; ++c) w[2 + c] = (uint64_t)b.col[c][i];
     int k = 2 + L.ncols;
@@ -104,7 +107,7 @@ __global__ void k_x_unpack(XLayout L, const uint64_t *recv, uint64_t m, XStaging
     st.ts[q] = (int64_t)w[1];
     for (int c = 0; c < L.ncols; ++c) {
       st.col[c][q] = (int64_t)w[2 + c];
-      if (L.has_valid) st.valid[c][q] = (uint8_t)((w[0] >> (32 + c)) & 1u);
+      if (L.has_valid) st.valid[c][q] = (uint8_t)(((w[0] >> (32 + c)) & 1u) | (((w[0] >> (40 + c)) & 1u) << 1));
     }
     int k = 2 + L.ncols;
     if (L.has_seq) st.seq[q] = (int64_t)w[k++];

@@ -967,7 +967,9 @@ __global__ __launch_bounds__(1024) void k_part_chunks(const uint64_t *bstart, in
   if (threadIdx.x == 0) chunk_start[nb + 1] = split;
 }
 
-bool part_supported(const Program &prog) { return prog.n_slots <= 8; }
+// ops with literal forms read bit 1 of the valid bytes, which the partition
+// layouts do not carry: the generic record kernels run them
+bool part_supported(const Program &prog) { return prog.n_slots <= 8 && !prog_has_forms(prog); }
 
 void launch_part_chunks(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc) {
   hipLaunchKernelGGL(k_part_chunks, dim3(1), dim3(1024), 0, s, pb.bstart, pp.np_log2, pp.chunk, pb.chunk_start,

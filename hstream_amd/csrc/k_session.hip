@@ -348,13 +348,10 @@ __global__ __launch_bounds__(256) void k_ss_process(Batch b, SessParams p, SessT
         e0 = ce > e0 ? ce : e0;
         int64_t cur[MS];
         ss_load<MS>(t, off + k, cur);
-        combine_row<MS>(prog, acc, cur);
         // passthrough columns: aggregateMergeF _ _ o2 keeps the existing
         // session's value (Codegen.hs:467), so after the fold the last
         // overlapped session in end order (k = i1 - 1) decides
-#pragma unroll
-        for (int s = 0; s < MS; ++s)
-          if (s < ns && (prog.slot_op[s] == S_LAST_SEQ || prog.slot_op[s] == S_LAST_VAL)) acc[s] = cur[s];
+        merge_row<MS>(prog, acc, cur);
       }
       const uint64_t c = i1 - i0;
       if (c == 0) {

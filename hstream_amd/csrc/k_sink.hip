@@ -44,7 +44,11 @@ __device__ inline uint32_t row_key(const SinkDev &S, uint64_t i) {
   return k;
 }
 
-// text of value member m of row i into buf (numbers) or as a pointer (key text)
+// text of value member m of row i into buf (numbers) or as a pointer (key text).
+// FORMS: the op kept literal forms (an integral f64 may print all its digits,
+// up to kNumTextIntMax bytes); else every number fits kNumTextMax, so the
+// default kernels keep a 32-byte buffer per thread instead of a 328-byte one
+template <bool FORMS>
 __device__ inline uint32_t member_text(const SinkDev &S, int m, uint64_t i, uint32_t k, char *buf, const char *&p) {
   const int j = S.agg_index[m];
   if (j < 0) {
@@ -56,7 +60,7 @@ __device__ inline uint32_t member_text(const SinkDev &S, int m, uint64_t i, uint
   const int64_t v = S.agg[j][i];
   const bool f64 = (S.f64_mask >> j) & 1u;
   const Pow5Tables T{kPow5InvDev, kPow5Dev};
-  if (S.form && ((S.form_mask >> j) & 1u)) {
+  if (FORMS && S.form && ((S.form_mask >> j) & 1u)) {
     // literal forms: how aeson prints the reference's Scientific
     const uint32_t fb = (S.form[i] >> (2 * j)) & 3u;
     if (fb & 2u) return (uint32_t)fmt_i64(S.ident[j] == 1 ? INT64_MAX : S.ident[j] == 2 ? INT64_MIN : 0, buf);
@@ -67,6 +71,7 @@ __device__ inline uint32_t member_text(const SinkDev &S, int m, uint64_t i, uint
   return (uint32_t)fmt_i64(v, buf);
 }
 
+template <bool FORMS>
 __global__ __launch_bounds__(256) void k_sink_len(SinkDev S, uint64_t n, uint32_t *__restrict__ klen,
                                                   uint32_t *__restrict__ vlen) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -76,8 +81,8 @@ __global__ __launch_bounds__(256) void k_sink_len(SinkDev S, uint64_t n, uint32_
     key_text(S, k, p, kn);
     klen[i] = (S.windowed ? 16u : 0u) + frag_len(S, 0) + kn + frag_len(S, 1);
     uint32_t vn = frag_len(S, 2 + S.n_members);
-    char buf[kNumTextIntMax];
-    for (int m = 0; m < S.n_members; ++m) vn += frag_len(S, 2 + m) + member_text(S, m, i, k, buf, p);
+    char buf[FORMS ? kNumTextIntMax : kNumTextMax];
+    for (int m = 0; m < S.n_members; ++m) vn += frag_len(S, 2 + m) + member_text<FORMS>(S, m, i, k, buf, p);
     vlen[i] = vn;
   }
 }
@@ -91,6 +96,7 @@ __device__ inline char *put_frag(char *o, const SinkDev &S, int f) {
   return put(o, S.frag + S.frag_off[f], frag_len(S, f));
 }
 
+template <bool FORMS>
 __global__ __launch_bounds__(256) void k_sink_write(SinkDev S, uint64_t n, const uint64_t *__restrict__ koff,
                                                     const uint64_t *__restrict__ voff, char *__restrict__ kbytes,
                                                     char *__restrict__ vbytes) {
@@ -111,10 +117,10 @@ __global__ __launch_bounds__(256) void k_sink_write(SinkDev S, uint64_t n, const
     o = put(o, p, kn);
     put_frag(o, S, 1);
     char *v = vbytes + voff[i];
-    char buf[kNumTextIntMax];
+    char buf[FORMS ? kNumTextIntMax : kNumTextMax];
     for (int m = 0; m < S.n_members; ++m) {
       v = put_frag(v, S, 2 + m);
-      const uint32_t tn = member_text(S, m, i, k, buf, p);
+      const uint32_t tn = member_text<FORMS>(S, m, i, k, buf, p);
       v = put(v, p, tn);
     }
     put_frag(v, S, 2 + S.n_members);
@@ -122,12 +128,20 @@ __global__ __launch_bounds__(256) void k_sink_write(SinkDev S, uint64_t n, const
 }
 
 void launch_sink_len(hipStream_t s, const SinkDev &S, uint64_t n, uint32_t *klen, uint32_t *vlen) {
-  if (n) hipLaunchKernelGGL(k_sink_len, dim3(grid_for(n, 256)), dim3(256), 0, s, S, n, klen, vlen);
+  if (!n) return;
+  if (S.form && S.form_mask)
+    hipLaunchKernelGGL(k_sink_len<true>, dim3(grid_for(n, 256)), dim3(256), 0, s, S, n, klen, vlen);
+  else
+    hipLaunchKernelGGL(k_sink_len<false>, dim3(grid_for(n, 256)), dim3(256), 0, s, S, n, klen, vlen);
 }
 
 void launch_sink_write(hipStream_t s, const SinkDev &S, uint64_t n, const uint64_t *koff, const uint64_t *voff,
                        char *kbytes, char *vbytes) {
-  if (n) hipLaunchKernelGGL(k_sink_write, dim3(grid_for(n, 256)), dim3(256), 0, s, S, n, koff, voff, kbytes, vbytes);
+  if (!n) return;
+  if (S.form && S.form_mask)
+    hipLaunchKernelGGL(k_sink_write<true>, dim3(grid_for(n, 256)), dim3(256), 0, s, S, n, koff, voff, kbytes, vbytes);
+  else
+    hipLaunchKernelGGL(k_sink_write<false>, dim3(grid_for(n, 256)), dim3(256), 0, s, S, n, koff, voff, kbytes, vbytes);
 }
 
 }  // namespace hsg

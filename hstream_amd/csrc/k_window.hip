@@ -234,24 +234,6 @@ void launch_gather_u64(hipStream_t s, const uint64_t *src, const uint32_t *perm,
   if (n) hipLaunchKernelGGL(k_gather_u64, dim3(grid_for(n, 256)), dim3(256), 0, s, src, perm, n, dst);
 }
 
-__global__ __launch_bounds__(256) void k_forms(FormArgs f) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < f.n; i += (uint64_t)gridDim.x * blockDim.x) {
-#pragma unroll
-    for (int c = 0; c < kMaxCols / 3; ++c) {
-      if (c >= f.ncols) break;
-      const uint8_t v = f.valid[c] ? f.valid[c][i] : (uint8_t)1;
-      const uint8_t p = v & 1u, dec = (v >> 1) & 1u;
-      f.out[3 * c][i] = p;
-      f.out[3 * c + 1][i] = p & dec;
-      f.out[3 * c + 2][i] = p & (dec ^ 1u);
-    }
-  }
-}
-
-void launch_forms(hipStream_t s, const FormArgs &f) {
-  if (f.n) hipLaunchKernelGGL(k_forms, dim3(grid_for(f.n, 256)), dim3(256), 0, s, f);
-}
-
 void launch_widen(hipStream_t s, const WidenArgs &w) {
   if (w.n) hipLaunchKernelGGL(k_widen, dim3(grid_for(w.n, 256)), dim3(256), 0, s, w);
 }
@@ -389,6 +371,14 @@ void launch_tile_scan(hipStream_t s, const int64_t *tile_max, const int64_t *til
 // ---------------------------------------------------------------------------
 // window assignment + hash aggregation, one tile of kTileRecords per workgroup
 // ---------------------------------------------------------------------------
+// the tie words of MIN slot v: unset (the resolution pass takes the minimum
+// over this batch's records holding the new value)
+__device__ inline void tie_reset(const Program &prog, int64_t *__restrict__ row, int v) {
+  for (int s = 0; s < prog.n_slots; ++s)
+    if (prog.slot_op[s] == S_TIE_MIN && prog.slot_aux[s] == v)
+      atomicExch((unsigned long long *)(row + s), ~0ull);
+}
+
 __device__ inline void apply_slots(const Program &prog, int64_t *__restrict__ row, const Batch &b, uint64_t i,
                                    uint64_t seq1) {
   for (int s = 0; s < prog.n_slots; ++s) {
@@ -402,27 +392,56 @@ __device__ inline void apply_slots(const Program &prog, int64_t *__restrict__ ro
       case S_SUM_F:
         if (rec_present(b, c, i)) unsafeAtomicAdd((double *)(row + s), __builtin_bit_cast(double, b.col[c][i]));
         break;
-      case S_MIN_I: if (rec_present(b, c, i)) atomicMin((long long *)(row + s), (long long)b.col[c][i]); break;
+      case S_MIN_I:
+        if (rec_present(b, c, i)) {
+          const long long x = (long long)b.col[c][i];
+          const long long old = atomicMin((long long *)(row + s), x);
+          if (prog.ties && x < old) tie_reset(prog, row, s);
+        }
+        break;
       case S_MAX_I: if (rec_present(b, c, i)) atomicMax((long long *)(row + s), (long long)b.col[c][i]); break;
       case S_MIN_F:
-        if (rec_present(b, c, i)) atomicMin(u, (unsigned long long)f64_ord(__builtin_bit_cast(double, b.col[c][i])));
+        if (rec_present(b, c, i)) {
+          const unsigned long long x = f64_ord(__builtin_bit_cast(double, b.col[c][i]));
+          const unsigned long long old = atomicMin(u, x);
+          if (prog.ties && x < old) tie_reset(prog, row, s);
+        }
         break;
       case S_MAX_F:
         if (rec_present(b, c, i)) atomicMax(u, (unsigned long long)f64_ord(__builtin_bit_cast(double, b.col[c][i])));
         break;
       case S_LAST_SEQ: if (rec_present(b, c, i)) atomicMax(u, (unsigned long long)seq1); break;
-      default: break;
+      case S_CNT_DEC: if (rec_decimal(b, c, i)) atomicAdd(u, 1ull); break;
+      case S_LAST_FORM: if (rec_present(b, c, i)) atomicMax(u, (unsigned long long)form_word(b, c, i, seq1)); break;
+      default: break;  // S_LAST_VAL, S_TIE_*: the resolution pass
     }
   }
 }
 
-// LAST resolution: the record whose sequence won LAST_SEQ writes LAST_VAL.
+// Resolution pass, once the batch's LAST_SEQ / MIN / MAX words are final:
+// the record whose sequence won LAST_SEQ writes LAST_VAL, and every record
+// holding a MIN / MAX's value offers its literal to the tie word (the
+// earliest for MIN, the latest for MAX: min n x = n, max n x = x). A MAX's
+// word from earlier batches needs no reset (a record of this batch is later);
+// a MIN's is reset by the aggregation pass when the batch lowers the minimum.
 __device__ inline void apply_last(const Program &prog, int64_t *__restrict__ row, const Batch &b, uint64_t i,
                                   uint64_t seq1) {
   for (int s = 0; s < prog.n_slots; ++s) {
-    if (prog.slot_op[s] != S_LAST_SEQ) continue;
+    const int op = prog.slot_op[s];
     const int c = prog.slot_col[s];
-    if (rec_present(b, c, i) && (uint64_t)row[s] == seq1) row[s + 1] = b.col[c][i];
+    if (op == S_LAST_SEQ) {
+      if (rec_present(b, c, i) && (uint64_t)row[s] == seq1) row[s + 1] = b.col[c][i];
+    } else if (slot_is_tie(op) && rec_present(b, c, i)) {
+      const int v = prog.slot_aux[s], vop = prog.slot_op[v];
+      const int64_t x = (vop == S_MIN_F || vop == S_MAX_F)
+                            ? (int64_t)f64_ord(__builtin_bit_cast(double, b.col[c][i]))
+                            : b.col[c][i];
+      if (x != row[v]) continue;
+      unsigned long long *u = (unsigned long long *)(row + s);
+      const unsigned long long w = (unsigned long long)form_word(b, c, i, seq1);
+      if (op == S_TIE_MIN) atomicMin(u, w);
+      else atomicMax(u, w);
+    }
   }
 }
 
@@ -651,6 +670,33 @@ __global__ __launch_bounds__(256) void k_tw_reinsert(const uint64_t *__restrict_
   }
   const uint64_t tot = wave_sum_u64(fresh);
   if ((threadIdx.x & 63) == 0 && tot) atomicAdd(kept, (unsigned long long)tot);
+}
+
+// A touched list across a table rebuild in the middle of a batch
+// (op_device.cpp resume_deferred): its entries are slots of the old table,
+// so they go through the group keys (k_touch_keys, before the rebuild) back
+// to the slots of the new one (k_touch_slots, after it). kTouchSkip entries
+// and groups the rebuild did not keep stay kTouchSkip.
+__global__ __launch_bounds__(256) void k_touch_keys(TwTable t, const uint32_t *__restrict__ touched, uint64_t n,
+                                                    uint64_t *__restrict__ keys) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t s = touched[i];
+    keys[i] = s == kTouchSkipEntry ? kEmpty : *t.key(s);
+  }
+}
+__global__ __launch_bounds__(256) void k_touch_slots(TwTable t, const uint64_t *__restrict__ keys, uint64_t n,
+                                                     uint32_t *__restrict__ touched) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t g = keys[i];
+    const int64_t s = g == kEmpty ? -1 : tw_find(t, g);
+    touched[i] = s < 0 ? kTouchSkipEntry : (uint32_t)s;
+  }
+}
+void launch_touch_keys(hipStream_t s, const TwTable &t, const uint32_t *touched, uint64_t n, uint64_t *keys) {
+  if (n) hipLaunchKernelGGL(k_touch_keys, dim3(grid_for(n, 256)), dim3(256), 0, s, t, touched, n, keys);
+}
+void launch_touch_slots(hipStream_t s, const TwTable &t, const uint64_t *keys, uint64_t n, uint32_t *touched) {
+  if (n) hipLaunchKernelGGL(k_touch_slots, dim3(grid_for(n, 256)), dim3(256), 0, s, t, keys, n, touched);
 }
 
 void launch_tw_closed(hipStream_t s, const TwTable &t, uint64_t cap, const TwParams &p, const DevScalars *sc,

@@ -63,12 +63,18 @@ static uint64_t ts16_frames(uint64_t n) { return (n + HSG_TS16_FRAME - 1) / HSG_
 static int64_t *ts16_frames_at(const void *buf, uint64_t n) {
   return (int64_t *)((char *)buf + ((n * 2 + 255) & ~255ull));
 }
-
-static bool has_last(const Program &prog) {
-  for (int s = 0; s < prog.n_slots; ++s)
-    if (prog.slot_op[s] == S_LAST_SEQ) return true;
-  return false;
+// elements of T a ts staging buffer of `cap` records needs: the widest
+// transport (T itself: int32 offsets or int64 ts), or TS16 offsets followed
+// by their frame bases, whichever is larger
+template <typename T>
+static uint64_t ts_stage_count(uint64_t cap) {
+  const uint64_t ts16 = ((cap * 2 + 255) & ~255ull) + ts16_frames(cap) * 8;
+  const uint64_t full = cap * sizeof(T);
+  return ((full > ts16 ? full : ts16) + sizeof(T) - 1) / sizeof(T);
 }
+
+// LAST, or literal-form slots: the records' global sequence numbers are needed
+static bool has_last(const Program &prog) { return prog_needs_seq(prog); }
 
 static int alloc_out(OutCols &o, uint64_t cap, int n_aggs, std::string &err, bool forms = false) {
   if (forms) DTRY(dalloc(&o.form, cap));
@@ -337,7 +343,6 @@ void op_device_free(OpDevice &d) {
   }
   dfree(d.st_seq);
   dfree(d.st_wm);
-  dfree(d.form_valid);
   dfree(d.nar_ts);
   dfree(d.nar_key);
   for (int c = 0; c < kMaxCols; ++c) dfree(d.nar_col[c]);
@@ -409,7 +414,7 @@ int op_prestage(OpDevice &d, const hsg_batch *b, int set, std::string &err) {
   OpDevice::Staging &s = d.pre[set];
   if (!s.key) {
     DTRY(dalloc(&s.key, pcap));
-    DTRY(dalloc(&s.ts, pcap));
+    DTRY(dalloc(&s.ts, ts_stage_count<int64_t>(pcap)));
     for (int c = 0; c < d.n_cols; ++c) {
       DTRY(dalloc(&s.col[c], pcap));
       DTRY(dalloc(&s.valid[c], pcap));
@@ -475,32 +480,10 @@ static int widen_batch(OpDevice &d, const hsg_batch *b, const void *k16, const v
 static int stage_batch_raw(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err, int staged_set);
 
 // Resolve the batch into device pointers, copying host arrays into staging
-// (or taking the ones op_prestage queued for it). Ops with literal forms
-// (HSG_OPF_LITERAL_FORMS) then see every user column c as the internal columns
-// 3c, 3c + 1, 3c + 2: the same values, valid where present / present with a
-// decimal literal / present with an integral literal (bit 1 of the valid byte).
+// (or taking the ones op_prestage queued for it). The valid bytes go to the
+// kernels as they are: bit 1 is the literal form the forms slots read.
 int stage_batch(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err, int staged_set) {
-  int rc = stage_batch_raw(d, b, kb, err, staged_set);
-  if (rc != HSG_OK || !d.forms) return rc;
-  if (!d.form_valid) DTRY(dalloc(&d.form_valid, (uint64_t)d.n_cols * d.batch_cap));
-  FormArgs fa;
-  memset(&fa, 0, sizeof(fa));
-  fa.n = kb.n;
-  fa.ncols = d.user_cols;
-  Batch x = kb;
-  for (int c = 0; c < d.user_cols; ++c) {
-    fa.valid[c] = kb.valid[c];
-    for (int k = 0; k < 3; ++k) {
-      uint8_t *v = d.form_valid + (uint64_t)(3 * c + k) * d.batch_cap;
-      fa.out[3 * c + k] = v;
-      x.col[3 * c + k] = kb.col[c];
-      x.valid[3 * c + k] = v;
-    }
-  }
-  launch_forms(d.stream, fa);
-  DTRY(hipGetLastError());
-  kb = x;
-  return HSG_OK;
+  return stage_batch_raw(d, b, kb, err, staged_set);
 }
 
 static int stage_batch_raw(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err, int staged_set) {
@@ -538,7 +521,7 @@ static int stage_batch_raw(OpDevice &d, const hsg_batch *b, Batch &kb, std::stri
   if (batch_narrow(b)) {
     // host narrow batch, synchronous push: H2D into the narrow staging, widen
     if (!d.nar_ts) {
-      DTRY(dalloc(&d.nar_ts, d.batch_cap));
+      DTRY(dalloc(&d.nar_ts, ts_stage_count<int32_t>(d.batch_cap)));
       DTRY(dalloc(&d.nar_key, d.batch_cap));
       for (int c = 0; c < d.n_cols; ++c) DTRY(dalloc(&d.nar_col[c], d.batch_cap));
     }
@@ -796,8 +779,27 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     DevScalars keep;
     memcpy(&keep, d.h_sc, sizeof(keep));
     const uint64_t bound = keep.scratch[34];
+    // the touched-list entries k_part_agg made (its in-kernel updates) are
+    // slots of the table tw_maintain may rebuild: carried through their group
+    // keys (k_seg_apply lists only the groups the batch had not touched yet,
+    // by their stamps, which the rebuild keeps)
+    const uint64_t t0 = cfg.emit_mode == HSG_EMIT_PER_BATCH
+                            ? (keep.scratch[1] < d.part.touched_cap ? keep.scratch[1] : d.part.touched_cap)
+                            : 0;
+    uint64_t *tkeys = nullptr;
+    struct KeysFree {
+      uint64_t *&p;
+      ~KeysFree() {
+        if (p) hipFree(p);
+      }
+    } kf{tkeys};
+    if (t0) {
+      DTRY(hipMalloc((void **)&tkeys, t0 * sizeof(uint64_t)));
+      launch_touch_keys(d.stream, d.tw, d.part.touched, t0, tkeys);
+    }
     int rc = tw_maintain(d, cfg, prog, kb.n, a.wm_in, a.pending, err, bound);
     if (rc != HSG_OK) return rc;
+    if (t0) launch_touch_slots(d.stream, d.tw, tkeys, t0, d.part.touched);
     keep.live = d.h_sc->live;  // the rebuilt table's rows, the batch's claims so far included
     memset(keep.live_x, 0, sizeof(keep.live_x));
     keep.scratch[32] = 0;

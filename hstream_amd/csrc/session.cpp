@@ -37,11 +37,8 @@ static int log2u(uint64_t v) {
   return l;
 }
 
-static bool has_last(const Program &prog) {
-  for (int s = 0; s < prog.n_slots; ++s)
-    if (prog.slot_op[s] == S_LAST_SEQ) return true;
-  return false;
-}
+// LAST, or literal-form slots: the records' global sequence numbers are needed
+static bool has_last(const Program &prog) { return prog_needs_seq(prog); }
 
 static int alloc_keys(SessTable &t, uint64_t kcap, std::string &err) {
   DTRY(hipMalloc((void **)&t.kt, kcap * sizeof(SessKey)));
@@ -143,7 +140,7 @@ int session_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &pr
   DTRY(hipMalloc((void **)&t.meta, M_WORDS * sizeof(uint64_t)));
   DTRY(hipHostMalloc((void **)&d.h_meta, M_WORDS * sizeof(uint64_t), hipHostMallocDefault));
   DTRY(hipHostMalloc((void **)&d.h_regions, kArenaRegions * kRegionStride * sizeof(uint64_t), hipHostMallocDefault));
-  d.ss_merge = cfg.emit_mode != HSG_EMIT_PER_RECORD && !has_last(prog) && prog.n_slots <= 8;
+  d.ss_merge = cfg.emit_mode != HSG_EMIT_PER_RECORD && !has_last(prog) && !prog_has_forms(prog) && prog.n_slots <= 8;
   if (d.ss_merge) {
     rc = part_device_init(d, cfg, prog, err);
     if (rc != HSG_OK) return rc;

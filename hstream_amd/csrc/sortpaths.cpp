@@ -90,11 +90,8 @@ int perrecord_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &
 // Per-record changelog on the partitioned pipeline (k_prpart.hip): ops with
 // <= 8 state slots and < 256 windows per record. Others: the sort path below.
 // ---------------------------------------------------------------------------
-static bool has_last_slot(const Program &prog) {
-  for (int s = 0; s < prog.n_slots; ++s)
-    if (prog.slot_op[s] == S_LAST_SEQ) return true;
-  return false;
-}
+// LAST, or literal-form slots: the records' global sequence numbers are needed
+static bool has_last_slot(const Program &prog) { return prog_needs_seq(prog); }
 
 bool perrecord_part_eligible(const Program &prog, uint64_t wpr) { return part_supported(prog) && wpr < 256; }
 

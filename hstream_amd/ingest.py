@@ -42,6 +42,11 @@ def _lib():
         L.hsg_decode_json_spelled.argtypes = [vp, vp, C.c_uint64, C.c_char_p, vp, vp, vp, vp, P(vp), P(vp), vp,
                                               P(C.c_uint64), vp, C.c_int]
         L.hsg_decode_json_spelled.restype = C.c_int
+        L.hsg_decode_json_batch.argtypes = [vp, vp, C.c_uint64, C.c_char_p, vp, vp, P(abi.hsg_decode_buffers),
+                                            P(abi.hsg_batch), vp, P(C.c_uint64), vp, C.c_int]
+        L.hsg_decode_json_batch.restype = C.c_int
+        L.hsg_batch_narrow.argtypes = [P(abi.hsg_batch), vp, C.c_uint32, vp, P(C.c_uint32), C.c_int]
+        L.hsg_batch_narrow.restype = C.c_int
         L.hsg_keydict_spelling_text.argtypes = [vp, C.c_uint32, C.c_char_p, C.c_size_t, P(C.c_size_t)]
         L.hsg_keydict_spelling_text.restype = C.c_int
         _declared = True
@@ -168,6 +173,50 @@ class Decoder:
                                        C.byref(rej), int(threads)), "hsg_decode_json")
         return key, ts_out, cols, valid, status, int(rej.value)
 
+    def decode_batch(self, keys: KeyDict, buf: bytes, off: np.ndarray, ts: np.ndarray, allow: int = abi.HSG_NARROW_ALL,
+                     threads: int = 0, spellings: bool = False, alloc=None):
+        """One poll batch straight into a ready hsg_batch
+        (hsg_decode_json_batch): decoded, then narrowed in place to the
+        narrowest lossless transport `allow` permits (hsg_batch_narrow).
+        alloc(nbytes) -> (numpy uint8 view, owner) lets the caller put the
+        arrays in pinned memory for hsg_push_batch_async. Returns a
+        DecodedBatch."""
+        n = len(off) - 1
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        ts_in = np.ascontiguousarray(ts, dtype=np.int64)
+        C_ = len(self.cols)
+        if alloc is None:
+            def alloc(nb):
+                a = np.empty(max(1, nb), np.uint8)
+                return a, a
+        owners = []
+
+        def take(nb, dtype):
+            a, own = alloc(nb * np.dtype(dtype).itemsize)
+            owners.append(own)
+            return a[: nb * np.dtype(dtype).itemsize].view(dtype)
+        frames = -(-max(1, n) // abi.HSG_TS16_FRAME)
+        key = take(n, np.uint32)
+        tsb = take(n, np.int64)
+        fr = take(frames, np.int64)
+        cols = [take(n, np.int64) for _ in range(C_)]
+        valid = [take(n, np.uint8) for _ in range(C_)]
+        cp = (C.c_void_p * max(1, C_))(*[c.ctypes.data for c in cols])
+        vp = (C.c_void_p * max(1, C_))(*[v.ctypes.data for v in valid])
+        bufs = abi.hsg_decode_buffers(capacity=n, key_id=key.ctypes.data, ts=tsb.ctypes.data, ts_frames=fr.ctypes.data,
+                                      cols=C.cast(cp, C.POINTER(C.c_void_p)), valid=C.cast(vp, C.POINTER(C.c_void_p)),
+                                      allow=int(allow))
+        out = abi.hsg_batch()
+        status = np.empty(n, np.uint8)
+        rej = C.c_uint64()
+        spell = np.empty(n, np.uint32) if spellings else None
+        _check(self._L.hsg_decode_json_batch(self._h, keys.handle, n, buf, off.ctypes.data, ts_in.ctypes.data,
+                                             C.byref(bufs), C.byref(out), status.ctypes.data, C.byref(rej),
+                                             spell.ctypes.data if spellings else None, int(threads)),
+               "hsg_decode_json_batch")
+        return DecodedBatch(out, bufs, (owners, cp, vp, key, tsb, fr, cols, valid), status, int(rej.value), spell,
+                            [t for _, t, _ in self.cols])
+
     def close(self):
         if self._h:
             self._L.hsg_decoder_destroy(self._h)
@@ -178,6 +227,55 @@ class Decoder:
             self.close()
         except Exception:
             pass
+
+
+class DecodedBatch:
+    """A decoded poll batch in its transport encoding (hsg_decode_json_batch):
+    .batch is the hsg_batch to push (OpHandle.push_batch), the arrays it
+    points into are kept alive here."""
+
+    def __init__(self, batch, bufs, keep, status, rejected, spell, col_types):
+        self.batch, self._bufs, self._keep = batch, bufs, keep
+        self.status, self.rejected, self.spell, self.col_types = status, rejected, spell, col_types
+
+    @property
+    def n(self):
+        return int(self.batch.n)
+
+    def bytes_per_record(self) -> float:
+        """Transport bytes of the batch (what crosses PCIe) per record."""
+        b = self.batch
+        n = max(1, self.n)
+        kb = 2 if b.key_enc == abi.HSG_ENC_K16 else 4
+        tb = {abi.HSG_ENC_TS16: 2, abi.HSG_ENC_TS32: 4}.get(b.ts_enc, 8)
+        fr = 8 * (-(-self.n // abi.HSG_TS16_FRAME)) / n if b.ts_enc == abi.HSG_ENC_TS16 else 0.0
+        cb = sum(4 if b.col_enc[c] != abi.HSG_ENC_FULL else 8 for c in range(b.n_cols))
+        vb = sum(1 for c in range(b.n_cols) if self._bufs.valid_ptrs[c])
+        return kb + tb + fr + cb + vb
+
+    def widen(self):
+        """The batch back at full width on the host (key_id u32, ts i64, cols,
+        valid or None per column): what the device's widening produces."""
+        b, n = self.batch, self.n
+        _owners, _cp, _vp, key, tsb, fr, cols, valid = self._keep
+        k = key.view(np.uint16)[:n].astype(np.uint32) if b.key_enc == abi.HSG_ENC_K16 else key[:n].copy()
+        if b.ts_enc == abi.HSG_ENC_TS16:
+            t = np.repeat(fr[: -(-n // abi.HSG_TS16_FRAME)], abi.HSG_TS16_FRAME)[:n] + tsb.view(np.uint16)[:n]
+        elif b.ts_enc == abi.HSG_ENC_TS32:
+            t = b.ts_base + tsb.view(np.int32)[:n].astype(np.int64)
+        else:
+            t = tsb[:n].copy()
+        out = []
+        for c, ty in enumerate(self.col_types):
+            e = b.col_enc[c]
+            if e == abi.HSG_ENC_I32:
+                out.append(cols[c].view(np.int32)[:n].astype(np.int64))
+            elif e == abi.HSG_ENC_DEC32:
+                out.append(cols[c].view(np.int32)[:n].astype(np.float64) / 10.0 ** b.col_scale[c])
+            else:
+                out.append(cols[c][:n].view(np.float64 if ty == abi.HSG_F64 else np.int64).copy())
+        vs = [valid[c][:n].copy() if self._bufs.valid_ptrs[c] else None for c in range(len(self.col_types))]
+        return k, t, out, vs
 
 
 def pack_records(values: Sequence[bytes]):

@@ -175,13 +175,16 @@ typedef struct {
    Codegen.hs:423-469). Batches then mark, in bit 1 of each valid byte, the values
    whose JSON literal had a negative exponent (hstream_ingest.h literal_forms); a
    SUM prints as an integer iff none of its values did (a Scientific sum takes the
-   smaller exponent), a MIN / MAX / LAST as its winning value was spelled, an
-   aggregate nothing reached as the reference's initial value. Changelog and dump
-   rows then carry hsg_rows.form. At most 2 value columns (each is tracked as
-   three internal columns). One case is decided without arrival order: a MIN /
-   MAX whose value was reached both by an integral and by a decimal literal
-   (7 and 7.0) prints as an integer, where the reference prints the later tied
-   literal for MAX and the earlier for MIN (max n x = x, min n x = n on ties). */
+   smaller exponent), a MIN / MAX / LAST as its winning literal was spelled, an
+   aggregate nothing reached as the reference's initial value. Ties between equal
+   values spelled differently (7 and 7.0) resolve as the reference's folds do:
+   a time window's or a session's record fold keeps the earlier literal for MIN
+   and takes the later for MAX (min n x = n, max n x = x, Codegen.hs:442,455); a
+   session merge keeps the merged side's for MIN and takes the existing
+   session's for MAX (min n1 n2 / max n1 n2, Codegen.hs:447,460). Changelog and
+   dump rows then carry hsg_rows.form. Any number of value columns; such ops run
+   on the generic record kernels (the fast partition layouts carry no literal
+   bits). */
 
 /* One micro-batch in columnar form, records in arrival order.
  *

@@ -42,6 +42,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "hstream_gpu.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -111,6 +113,53 @@ int  hsg_decode_json_spelled(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, co
                              const int64_t *rec_ts, uint32_t *key_id, int64_t *ts, void *const *cols,
                              uint8_t *const *valid, uint8_t *status, uint64_t *rejected, uint32_t *spell,
                              int n_threads);
+
+/* ---- narrow transport ---------------------------------------------------------
+ * A poll batch crosses PCIe before any kernel sees it, so its bytes per record
+ * bound a host-fed operator (hstream_gpu.h hsg_enc). The decoder sees every
+ * value, so it can pick, per batch, the narrowest encoding that is lossless
+ * for the values it decoded; the library widens on the device. */
+#define HSG_NARROW_K16   1u  /* key ids as uint16 when every id < 2^16                    */
+#define HSG_NARROW_TS16  2u  /* ts as uint16 offsets from per-frame minima (HSG_TS16_FRAME) */
+#define HSG_NARROW_TS32  4u  /* ts as int32 offsets from the batch's minimum               */
+#define HSG_NARROW_I32   8u  /* HSG_I64 columns as int32 when every value fits             */
+#define HSG_NARROW_DEC32 16u /* HSG_F64 columns as int32 decimal mantissas (scale <= 9)     */
+#define HSG_NARROW_ALL   31u
+
+/* Rewrite a full-width host batch in place into the narrowest lossless
+ * transport `allow` permits: io's arrays are reinterpreted (K16 keys in the
+ * first 2n bytes of key_id, TS16 / TS32 offsets in the first 2n / 4n bytes of
+ * ts, I32 / DEC32 values in the first 4n bytes of a column) and its encoding
+ * fields set. ts_frames: ceil(n / HSG_TS16_FRAME) entries for TS16 (NULL: no
+ * TS16). *present_mask (optional): bit c = column c is present in every
+ * record with no literal-form bit, so its valid array may be left out.
+ * HSG_E_INVALID for a device batch or one already narrow. */
+int  hsg_batch_narrow(hsg_batch *io, const int32_t *col_types, uint32_t allow, int64_t *ts_frames,
+                      uint32_t *present_mask, int n_threads);
+
+/* Caller-owned host arrays one decoded batch is built in (pinned memory for
+ * hsg_push_batch_async), sized for `capacity` records at full width. */
+typedef struct {
+  uint64_t capacity;
+  uint32_t *key_id;             /* capacity entries                                   */
+  int64_t *ts;                  /* capacity entries                                   */
+  int64_t *ts_frames;           /* ceil(capacity / HSG_TS16_FRAME) entries (TS16)     */
+  void *const *cols;            /* n_cols arrays of capacity 8-byte values            */
+  uint8_t *const *valid;        /* n_cols arrays of capacity bytes                    */
+  uint32_t allow;               /* HSG_NARROW_* the consumer takes; 0 = full width    */
+  uint32_t reserved;
+  const void *col_ptrs[8];      /* filled by the decoder: the batch's column pointers */
+  const uint8_t *valid_ptrs[8]; /* filled: valid pointers, NULL for a column present in every
+                                   record (no valid bytes to send)                     */
+} hsg_decode_buffers;
+
+/* hsg_decode_json_spelled into `bufs`, then hsg_batch_narrow: *out is a
+ * ready hsg_batch (mem = HSG_MEM_HOST) over bufs' arrays, in the narrowest
+ * lossless transport bufs->allow permits. spell optional. At most 8 value
+ * columns. The batch stays valid until bufs is reused. */
+int  hsg_decode_json_batch(hsg_decoder *dec, hsg_keydict *dict, uint64_t n, const char *buf, const uint64_t *off,
+                           const int64_t *rec_ts, hsg_decode_buffers *bufs, hsg_batch *out, uint8_t *status,
+                           uint64_t *rejected, uint32_t *spell, int n_threads);
 
 #ifdef __cplusplus
 }

@@ -17,6 +17,7 @@ int main(void) {
   S(hsg_rows); F(hsg_rows, key_id); F(hsg_rows, win_start); F(hsg_rows, src_index); F(hsg_rows, aggs); F(hsg_rows, form);
   S(hsg_stats); F(hsg_stats, last_batch_ms); F(hsg_stats, exchange_bytes); F(hsg_stats, touched_total); F(hsg_stats, state_row_bytes); F(hsg_stats, spill_events); F(hsg_stats, grow_events); F(hsg_stats, replays); F(hsg_stats, overflow_rebuilds);
   S(hsg_decoder_config); F(hsg_decoder_config, n_cols); F(hsg_decoder_config, col_fields); F(hsg_decoder_config, col_numeric); F(hsg_decoder_config, literal_forms);
+  S(hsg_decode_buffers); F(hsg_decode_buffers, ts_frames); F(hsg_decode_buffers, valid); F(hsg_decode_buffers, allow); F(hsg_decode_buffers, col_ptrs); F(hsg_decode_buffers, valid_ptrs);
   S(hsg_sink_config); F(hsg_sink_config, key_field); F(hsg_sink_config, agg_index);
   S(hsg_sink_records); F(hsg_sink_records, key_capacity); F(hsg_sink_records, key_bytes); F(hsg_sink_records, value_off);
   S(hsg_sink_spellings); F(hsg_sink_spellings, n); F(hsg_sink_spellings, src_base); F(hsg_sink_spellings, mem);

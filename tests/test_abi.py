@@ -57,7 +57,7 @@ def test_ctypes_layout_matches_c():
             want[k] = int(v)
     types = {"hsg_engine_config": abi.hsg_engine_config, "hsg_agg": abi.hsg_agg, "hsg_op_config": abi.hsg_op_config,
              "hsg_batch": abi.hsg_batch, "hsg_rows": abi.hsg_rows, "hsg_stats": abi.hsg_stats,
-             "hsg_decoder_config": abi.hsg_decoder_config,
+             "hsg_decoder_config": abi.hsg_decoder_config, "hsg_decode_buffers": abi.hsg_decode_buffers,
              "hsg_sink_config": abi.hsg_sink_config, "hsg_sink_records": abi.hsg_sink_records,
              "hsg_sink_spellings": abi.hsg_sink_spellings,
              "hsg_join_config": abi.hsg_join_config, "hsg_join_batch": abi.hsg_join_batch,

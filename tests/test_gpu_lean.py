@@ -192,3 +192,41 @@ def test_table_sized_by_groups_not_records(eng):
     assert st["table_slots"] <= (1 << 22) and st["grow_events"] == 0, st
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("hot", [False, True], ids=["uniform", "hot_key"])
+def test_hopping_deferred_hold_across_rebuild(eng, hot):
+    """Hopping per-batch changelog when k_seg_apply holds its deferred window
+    updates back for table room: the table is rebuilt in the middle of the
+    batch (after k_part_agg's own updates went in), so the touched-list
+    entries k_part_agg made -- slots of the old table -- must follow their
+    groups into the new one. The table is sized from the last batch's
+    deferred updates, so a batch with several times the previous batch's new
+    groups holds; a hot key splits its bucket over workgroups, whose
+    in-kernel updates fill the touched list before the hold. Every changelog
+    and the final state match the oracle (TimeWindowedStream.hs:86-103)."""
+    spec = OpSpec(abi.HSG_HOPPING, abi.HSG_EMIT_PER_BATCH, size_ms=60_000, advance_ms=5_000,
+                  col_types=[abi.HSG_I64], aggs=[(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0), (abi.HSG_MAX, 0)])
+    g, o = eng.op(spec), pyoracle.OracleOp(spec)
+    f64 = spec.agg_is_f64()
+    rng = np.random.default_rng(23 + hot)
+    t = 10_000_000
+    wg = wo = -1
+    for bi, (nkeys, span, n) in enumerate([(2_000, 120_000, 200_000),     # ~48K groups
+                                           (2_000, 120_000, 200_000),
+                                           (400_000, 600_000, 1_000_000),  # several times the room predicted
+                                           (2_000, 120_000, 200_000),
+                                           (1_000_000, 1_200_000, 2_000_000)]):
+        key, ts, cols = _uniform(rng, n, nkeys, t, span)
+        if hot and bi >= 2:
+            key[rng.random(n) < 0.3] = 11
+        t += span
+        wg = g.push(key, ts, cols, None, watermark=wg)
+        wo = o.push(key, ts, cols, None, watermark=wo)
+        assert wg == wo, f"batch {bi}: watermark {wg} != {wo}"
+        rows_equal(g.drain(), o.drain(), f64, what=f"changelog batch {bi}")
+    rows_equal(g.dump_state(), o.dump_state(), f64, what="state dump")
+    st = g.stats()
+    assert st["grow_events"] >= 1 and st["replays"] >= 1, st
+    g.close()
+    o.close()

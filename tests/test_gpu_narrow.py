@@ -144,3 +144,81 @@ def test_ts16_frames_equal_full_width(eng, name, mode):
     rows_equal(g.dump_state(), o.dump_state(), f64, what=f"{name} {mode} ts16 state")
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("mode", ["sync", "async"])
+@pytest.mark.parametrize("cap", [16, 64, 200])
+def test_ts16_small_capacity_engine(cap, mode):
+    """TS16 frame bases sit after the offsets (256-byte aligned) in the op's ts
+    staging buffer: an engine whose batch capacity is a few records must size
+    that buffer for them too (offsets + bases exceed 4 or 8 bytes per record
+    below ~130 records). Many small batches, bit-identical to the oracle."""
+    import torch
+    assert torch.cuda.is_available()
+    from hstream_amd.engine import Engine
+    e = Engine(device=0, batch_capacity=cap)
+    spec = SPECS["tumbling_batch"]
+    g, o = e.op(spec), pyoracle.OracleOp(spec)
+    f64 = spec.agg_is_f64()
+    wm_o = -1
+    wm_g = C.c_int64(-1)
+    for b in range(6):
+        key, ts, cols, valid = gen_small(300 + b, cap, 20, col_types=(abi.HSG_I64, abi.HSG_F64), span=30_000,
+                                         base=3_000_000 + 30_000 * b, very_late=False, neg_frac=0.0)
+        cols[0] = cols[0] // 2
+        t16, frames, c32, enc, scale = narrow_columns(ts, cols, spec.col_types, [None, 3], ts16=True)
+        wm_o = o.push(key, ts, cols, valid, watermark=wm_o)
+        kw = dict(ts_frames=frames, col_enc=enc, col_scale=scale)
+        if mode == "sync":
+            wm_g.value = g.push(key, t16, c32, valid, watermark=wm_g.value, **kw)
+        else:
+            g.push_async(key, t16, c32, valid, watermark=wm_g, **kw)
+            g.wait()
+        assert wm_g.value == wm_o, f"batch {b}: watermark"
+        rows_equal(g.drain(), o.drain(), f64, what=f"cap {cap} {mode} ts16 changelog {b}")
+    rows_equal(g.dump_state(), o.dump_state(), f64, what=f"cap {cap} {mode} ts16 state")
+    g.close()
+    o.close()
+    e.close()
+
+
+@pytest.mark.parametrize("name", ["tumbling_batch", "hopping_record", "session_batch"])
+def test_decoder_batches_equal_full_width(eng, name):
+    """The product decoder's own transport (hsg_decode_json_batch: JSON poll
+    batch -> narrowest lossless hsg_batch, 16-bit keys, TS16 frames, int32 /
+    DEC32 values, no valid bytes for always-present fields) pushed as it
+    comes, against the oracle fed the full-width decode of the same records."""
+    import json
+    from hstream_amd.ingest import Decoder, KeyDict, pack_records
+    spec = SPECS[name]
+    g, o = eng.op(spec), pyoracle.OracleOp(spec, faithful_sessions=False)
+    f64 = spec.agg_is_f64()
+    rng = np.random.default_rng(41)
+    cols = [("v", abi.HSG_I64, True), ("x", abi.HSG_F64, True)]
+    dec_w, dec_n = Decoder("k", cols), Decoder("k", cols)
+    kw, kn = KeyDict(), KeyDict()
+    wm_o = wm_g = -1
+    for b in range(3):
+        n = 30_000
+        vals = []
+        for i in range(n):
+            r = {"k": int(rng.integers(0, 300))}
+            if rng.random() > 0.05:
+                r["v"] = int(rng.integers(-10**6, 10**6))
+            if rng.random() > 0.05 or b == 1:  # batch 1: x in every record (no valid bytes for it)
+                r["x"] = round(float(rng.uniform(-1e4, 1e4)), 2)
+            vals.append(json.dumps(r).encode())
+        ts = 3_000_000 + 60_000 * b + (np.arange(n) * 60_000) // n + rng.integers(0, 3000, n)
+        buf, off = pack_records(vals)
+        k, t, cs, valid, _st, _rej = dec_w.decode(kw, buf, off, ts)
+        db = dec_n.decode_batch(kn, buf, off, ts)
+        assert db.batch.key_enc == abi.HSG_ENC_K16 and db.batch.ts_enc == abi.HSG_ENC_TS16
+        assert db.batch.col_enc[0] == abi.HSG_ENC_I32 and db.batch.col_enc[1] == abi.HSG_ENC_DEC32
+        wm_o = o.push(k, t, cs, valid, watermark=wm_o)
+        wm_g = g.push_batch(db.batch, watermark=wm_g)
+        assert wm_g == wm_o, f"batch {b}: watermark"
+        rows_equal(g.drain(), o.drain(), f64, ordered=spec.emit_mode == abi.HSG_EMIT_PER_RECORD,
+                   what=f"{name} decoder batch {b}")
+    rows_equal(g.dump_state(), o.dump_state(), f64, what=f"{name} decoder state")
+    g.close()
+    o.close()

@@ -342,3 +342,87 @@ def test_key_spellings():
     # spellings across batches reuse the alternate ids
     kid2, _, _, _, _, _, spell2 = dec.decode(keys, buf, off, np.zeros(len(vals), np.int64), spellings=True)
     assert kid2.tolist() == kid.tolist() and spell2.tolist() == spell.tolist()
+
+
+def _c2_like_records(rng, n, nkeys, t0, decimals=3, vmax=10**9, span=60_000):
+    vals, ts = [], []
+    for i in range(n):
+        v = int(rng.integers(-vmax, vmax))
+        x = round(float(rng.uniform(0, 1e6)), decimals)
+        vals.append(json.dumps({"k": int(rng.integers(0, nkeys)), "v": v, "x": x}).encode())
+        ts.append(t0 + (i * span) // n + int(rng.integers(0, 2000)))
+    return vals, np.array(ts, np.int64)
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_decode_batch_narrow_equals_wide(threads):
+    """hsg_decode_json_batch: the decoder picks the narrow transport per batch
+    from the values it decoded (16-bit keys, TS16 frames, int32 values, DEC32
+    mantissas of 3-decimal values) and the batch it hands over widens back to
+    exactly the full-width decode (Processor.hs:192-204 decodes the same
+    values); columns present in every record carry no valid bytes. C2's
+    record: 8 bytes + 4 for the decimal column instead of 28."""
+    rng = np.random.default_rng(8)
+    vals, ts = _c2_like_records(rng, 20_000, 5000, 1_700_000_000_000)
+    buf, off = pack_records(vals)
+    cols = [("v", abi.HSG_I64, True), ("x", abi.HSG_F64, True)]
+    wide_keys, nar_keys = KeyDict(), KeyDict()
+    k, t, cs, valid, st, rej = Decoder("k", cols).decode(wide_keys, buf, off, ts, threads=threads)
+    db = Decoder("k", cols).decode_batch(nar_keys, buf, off, ts, threads=threads)
+    b = db.batch
+    assert (b.key_enc, b.ts_enc, list(b.col_enc[:2])) == (abi.HSG_ENC_K16, abi.HSG_ENC_TS16,
+                                                          [abi.HSG_ENC_I32, abi.HSG_ENC_DEC32])
+    assert b.col_scale[1] == 3 and db.rejected == rej == 0
+    assert db.bytes_per_record() < 12.01
+    k2, t2, cs2, v2 = db.widen()
+    assert np.array_equal(k2, k) and np.array_equal(t2, t)
+    assert np.array_equal(cs2[0], cs[0])
+    assert np.array_equal(cs2[1].view(np.int64), cs[1].view(np.int64))  # bit-identical doubles
+    assert v2 == [None, None] and all(np.all(v == 1) for v in valid)
+
+
+def test_decode_batch_keeps_what_does_not_fit():
+    """Each column narrows only when lossless for every value of the batch:
+    a value outside int32 keeps its i64 column wide, a -0.0 or a 12-decimal
+    value keeps the f64 column wide, a rejected record (HSG_KEY_NONE) or more
+    than 2^16 key ids keeps the keys wide, a frame spanning 2^16 ms or more
+    falls back to TS32 and a batch spanning 2^31 ms to full ts; absent
+    fields keep their valid bytes. Every batch widens back exactly."""
+    cols = [("v", abi.HSG_I64, True), ("x", abi.HSG_F64, True)]
+    base = [{"k": 1, "v": 5, "x": 1.5}, {"k": 2, "v": -7, "x": 2.25}, {"k": 3, "v": 0, "x": 0.0}]
+    cases = [
+        ([dict(base[0], v=2**31)] + base[1:], [0, 1, 2], (abi.HSG_ENC_FULL, abi.HSG_ENC_DEC32)),
+        ([dict(base[0], x=-0.0)] + base[1:], [0, 1, 2], (abi.HSG_ENC_I32, abi.HSG_ENC_FULL)),
+        ([dict(base[0], x=0.123456789012)] + base[1:], [0, 1, 2], (abi.HSG_ENC_I32, abi.HSG_ENC_FULL)),
+        (base, [0, 70_000, 2], (abi.HSG_ENC_I32, abi.HSG_ENC_DEC32)),
+        (base, [0, 2**31, 2], (abi.HSG_ENC_I32, abi.HSG_ENC_DEC32)),
+        ([{"k": 1, "x": 1.5}, {"v": 1}, {"k": 3, "v": 4}], [0, 1, 2], (abi.HSG_ENC_I32, abi.HSG_ENC_DEC32)),
+    ]
+    for ci, (recs, ts, enc) in enumerate(cases):
+        vals = [json.dumps(r).encode() for r in recs]
+        buf, off = pack_records(vals)
+        tsa = np.array(ts, np.int64)
+        k, t, cs, valid, st, rej = Decoder("k", cols).decode(KeyDict(), buf, off, tsa)
+        db = Decoder("k", cols).decode_batch(KeyDict(), buf, off, tsa)
+        b = db.batch
+        assert (b.col_enc[0], b.col_enc[1]) == enc, (ci, list(b.col_enc[:2]))
+        want_k = abi.HSG_ENC_FULL if rej else abi.HSG_ENC_K16
+        assert b.key_enc == want_k, ci
+        want_t = abi.HSG_ENC_TS16 if ts[1] < 65536 else abi.HSG_ENC_TS32 if ts[1] < 2**31 else abi.HSG_ENC_FULL
+        assert b.ts_enc == want_t, ci
+        k2, t2, cs2, v2 = db.widen()
+        assert np.array_equal(k2, k) and np.array_equal(t2, t), ci
+        assert np.array_equal(cs2[0], cs[0]) and np.array_equal(cs2[1].view(np.int64), cs[1].view(np.int64)), ci
+        for c in range(2):
+            assert np.array_equal(v2[c] if v2[c] is not None else np.ones(3, np.uint8), valid[c]), (ci, c)
+    # more than 2^16 key ids: 32-bit keys
+    kd = KeyDict()
+    for i in range(70_000):
+        kd.encode(i)
+    vals = [json.dumps({"k": 69_999, "v": 1, "x": 1.0}).encode()] * 3
+    buf, off = pack_records(vals)
+    db = Decoder("k", cols).decode_batch(kd, buf, off, np.zeros(3, np.int64))
+    assert db.batch.key_enc == abi.HSG_ENC_FULL
+    # allow = 0: full width
+    db = Decoder("k", cols).decode_batch(KeyDict(), buf, off, np.zeros(3, np.int64), allow=0)
+    assert (db.batch.key_enc, db.batch.ts_enc, db.batch.col_enc[0]) == (0, 0, 0)

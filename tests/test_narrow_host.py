@@ -61,3 +61,14 @@ def test_ts16_frames():
     assert t.dtype == np.uint16 and np.array_equal(fr2, fr)
     b, _ = make_batch(np.arange(n, dtype=np.uint32), off, [], None, abi.HSG_MEM_HOST, ts_frames=fr)
     assert b.ts_enc == abi.HSG_ENC_TS16 and b.ts_frames
+
+
+def test_dec32_keeps_signed_zero_full_width():
+    """-0.0 equals 0.0 numerically but a DEC32 mantissa 0 widens to +0.0: a
+    column holding -0.0 is not lossless as DEC32 and stays full width."""
+    f = np.array([1.5, -0.0, 2.25], np.float64)
+    _, _, cs, enc, _ = narrow_columns(np.zeros(3, np.int64), [f], [abi.HSG_F64], [2])
+    assert enc == [abi.HSG_ENC_FULL] and np.signbit(cs[0][1])
+    g = np.array([1.5, 0.0, 2.25], np.float64)
+    _, _, _, enc, _ = narrow_columns(np.zeros(3, np.int64), [g], [abi.HSG_F64], [2])
+    assert enc == [abi.HSG_ENC_DEC32]

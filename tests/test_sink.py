@@ -256,127 +256,245 @@ def aeson_sci(a) -> str:
 
 
 MAXB, MINB = ((1 << 63) - 1, 0), (-(1 << 63), 0)  # maxBound / minBound :: Int (Codegen.hs:438,451)
+ZERO = (0, 0)                                      # Number 0 (Codegen.hs:406,425,466)
 
 
-def _ref_changelog_rows(recs, size):
-    """The reference's per-record fold per (key, window) (TimeWindowedStream.hs
-    :86-103 with Codegen.hs:404-469's components), one row per record: the
-    state after it. recs: (key value text, ts, x literal or None, v literal).
-    Per MIN / MAX also the text under this build's tie rule (see
-    test_sink_literal_forms_and_key_spellings) and whether the two differ: the
-    extreme value was reached by both an integral and a decimal literal."""
-    state = {}
+_TIES = [0]  # folds / merges of equal MIN / MAX values with different literal forms
+
+
+def _tie(a, b):
+    if sci_val(a) == sci_val(b) and (a[1] >= 0) != (b[1] >= 0):
+        _TIES[0] += 1
+
+
+def _init(kind):
+    return {"cnt": 0, "sum": ZERO, "min": MAXB, "max": MINB, "last": ZERO}[kind]
+
+
+def _fold(kind, n, x):
+    """aggregateF of one component (Codegen.hs:404-469) on a present literal
+    x (None: the field is absent). Haskell's min n x = if n <= x then n else
+    x, max n x = if n <= x then x else n: on equal values MIN keeps the
+    earlier literal, MAX takes the later."""
+    if kind == "cnt":
+        return n + 1
+    if x is None:
+        return n
+    if kind == "sum":
+        return sci_add(n, x)
+    if kind in ("min", "max"):
+        _tie(n, x)
+    if kind == "min":
+        return n if sci_val(n) <= sci_val(x) else x
+    if kind == "max":
+        return x if sci_val(n) <= sci_val(x) else n
+    return x  # last: the record's own value (HM.adjust updateV)
+
+
+def _merge(kind, n1, n2):
+    """aggregateMergeF (Codegen.hs:409-469): n1 = the merged side (the new
+    record and the sessions merged so far), n2 = the next overlapped session
+    (SessionWindowedStream.hs:100-114)."""
+    if kind == "cnt":
+        return n1 + n2
+    if kind == "sum":
+        return sci_add(n1, n2)
+    if kind in ("min", "max"):
+        _tie(n1, n2)
+    if kind == "min":
+        return n1 if sci_val(n1) <= sci_val(n2) else n2
+    if kind == "max":
+        return n2 if sci_val(n1) <= sci_val(n2) else n1
+    return n2  # passthrough: o2
+
+
+def _lit(vals, col):
+    x = vals.get(col) if col else None
+    return None if x is None else sci_parse(x)
+
+
+def _text(kind, v):
+    return str(v) if kind == "cnt" else aeson_sci(v)
+
+
+def _group_key(key_text):
+    """Aeson Value equality of a key: numbers by their Scientific value."""
+    key = json.loads(key_text)
+    return float(key) if isinstance(key, (int, float)) and not isinstance(key, bool) else json.dumps(key)
+
+
+def _ref_literal_rows(recs, comps, window, emit, batches):
+    """The reference's fold over literal records (key text, ts, {column:
+    literal or None}), one changelog row per record (EMIT CHANGES) or, per
+    batch, the state after the batch of every group it touched. Rows:
+    (record index or -1, key text, window start, {alias: text}).
+    window = ("tumbling", size) (TimeWindowedStream.hs:86-103) or
+    ("session", gap) (SessionWindowedStream.hs:84-118, findSessions order:
+    end, then start, ascending, Store.hs:243-272)."""
+    kind, size = window
+    state = {}   # tumbling: (group, ws) -> comps state; session: group -> [[start, end, state], ...]
+    first_text = {}
     out = []
-
-    def ext(cur, new, is_max):
-        # cur: (sci, integral seen at the value, decimal seen at the value) or None
-        v = sci_val(new)
-        integral = new[1] >= 0
-        if cur is None or (v > sci_val(cur[0]) if is_max else v < sci_val(cur[0])):
-            return (new, integral, not integral)
-        if v == sci_val(cur[0]):
-            # Haskell's max n x = x on ties (the later literal); min n x = n (the earlier)
-            lit = new if is_max else cur[0]
-            return (lit, cur[1] or integral, cur[2] or not integral)
-        return cur
-
-    def texts(cur, ident):
-        if cur is None:
-            return aeson_sci(ident), aeson_sci(ident), False
-        ref = aeson_sci(cur[0])
-        v = sci_val(cur[0])
-        ours = str(int(v)) if cur[1] else ref  # (an integral literal's value is an integer)
-        return ref, ours, cur[1] and cur[2]
-
-    for key_text, ts, x, v in recs:
-        ws = (ts // size) * size
-        key = json.loads(key_text)
-        kk = (float(key) if isinstance(key, (int, float)) else json.dumps(key), ws)
-        st = state.setdefault(kk, {"cnt": 0, "sx": (0, 0), "mnx": None, "mxx": None, "sv": (0, 0), "mxv": None})
-        st["cnt"] += 1
-        if x is not None:
-            sx = sci_parse(x)
-            st["sx"] = sci_add(st["sx"], sx)
-            st["mnx"] = ext(st["mnx"], sx, False)
-            st["mxx"] = ext(st["mxx"], sx, True)
-        sv = sci_parse(v)
-        st["sv"] = sci_add(st["sv"], sv)
-        st["mxv"] = ext(st["mxv"], sv, True)
-        ref, ours, tie = {}, {}, False
-        for name, cur, ident in (("min_x", st["mnx"], MAXB), ("max_x", st["mxx"], MINB), ("max_v", st["mxv"], MINB)):
-            ref[name], ours[name], t = texts(cur, ident)
-            tie = tie or t
-        row = {"cnt": str(st["cnt"]), "sum_x": aeson_sci(st["sx"]), "sum_v": aeson_sci(st["sv"])}
-        out.append((key_text, ws, dict(row, **ref), dict(row, **ours), tie))
+    rec_at = 0
+    for nb in batches:
+        touched = {}
+        for r in range(rec_at, rec_at + nb):
+            key_text, ts, vals = recs[r]
+            gk = _group_key(key_text)
+            first_text.setdefault(gk, key_text)
+            if kind == "tumbling":
+                ws = (ts // size) * size
+                st = state.setdefault((gk, ws), {a: _init(k) for a, k, _ in comps})
+                for a, k, col in comps:
+                    st[a] = _fold(k, st[a], _lit(vals, col))
+                row_key, row_st = (gk, ws), st
+            else:
+                sess = state.setdefault(gk, [])
+                acc = {a: _fold(k, _init(k), _lit(vals, col)) for a, k, col in comps}
+                s0 = e0 = ts
+                over = sorted((x for x in sess if x[1] >= ts - size and x[0] <= ts + size), key=lambda x: (x[1], x[0]))
+                for cur in over:
+                    acc = {a: _merge(k, acc[a], cur[2][a]) for a, k, _ in comps}
+                    s0, e0 = min(s0, cur[0]), max(e0, cur[1])
+                    sess.remove(cur)
+                sess.append([s0, e0, acc])
+                ws, row_st = s0, acc
+                row_key = (gk, s0)
+                for o in over:  # merged sessions are gone from this batch's rows
+                    touched.pop((gk, o[0]), None)
+            texts = {a: _text(k, row_st[a]) for a, k, _ in comps}
+            if emit == abi.HSG_EMIT_PER_RECORD:
+                own = json.dumps(json.loads(key_text)) if key_text.startswith('"') else aeson_sci(sci_parse(key_text))
+                out.append((r, own, ws, texts))
+            else:
+                touched[row_key] = (-1, first_text[gk], ws, texts)
+        rec_at += nb
+        if emit != abi.HSG_EMIT_PER_RECORD:
+            out.append(sorted(touched.values(), key=lambda x: (x[1], x[2])))
     return out
 
 
+def _first_text(kt):
+    return json.dumps(json.loads(kt)) if kt.startswith('"') else aeson_sci(sci_parse(kt))
+
+
+LITERAL_CASES = {
+    # tumbling, EMIT CHANGES: the changelog, key spellings per record
+    "tumbling_changes": (("tumbling", 5000), abi.HSG_EMIT_PER_RECORD, 2),
+    # tumbling, per batch: the last row of each group the batch touched
+    "tumbling_batch": (("tumbling", 5000), abi.HSG_EMIT_PER_BATCH, 2),
+    # four value columns (each aggregated), per batch and EMIT CHANGES
+    "tumbling_changes_4col": (("tumbling", 5000), abi.HSG_EMIT_PER_RECORD, 4),
+    "tumbling_batch_4col": (("tumbling", 5000), abi.HSG_EMIT_PER_BATCH, 4),
+    # sessions: record folds and session merges (min n1 n2 / max n1 n2)
+    "session_changes": (("session", 900), abi.HSG_EMIT_PER_RECORD, 2),
+    "session_batch": (("session", 900), abi.HSG_EMIT_PER_BATCH, 4),
+}
+
+
 @pytest.mark.gpu
-def test_sink_literal_forms_and_key_spellings():
+@pytest.mark.parametrize("case", sorted(LITERAL_CASES))
+def test_sink_literal_forms_and_key_spellings(case):
     """Decimal columns fed integral literals print integers ("6" for 2 + 4),
     mixed 2 / 2.0 / 25e-1 / 1e1 spellings follow the Scientific exponent
-    rules (a SUM's exponent is the smaller one, MAX keeps the later of equal
-    values, MIN the earlier), absent fields leave the reference's initial
-    values (0, maxBound, minBound), an i64 column fed 20e-1 prints "2.0"; keys
-    1 / 1.0 / 1e0 / 10e-1 are one group whose rows print each record's own
-    spelling ("1" or "1.0")."""
+    rules (a SUM's exponent is the smaller one; a MIN / MAX reached by equal
+    values spelled differently keeps the literal the reference's fold keeps:
+    min n x = n, max n x = x, and on session merges min n1 n2 / max n1 n2),
+    absent fields leave the reference's initial values (0, maxBound,
+    minBound), an i64 column fed 20e-1 prints "2.0", a passthrough column
+    prints its last literal; keys 1 / 1.0 / 1e0 / 10e-1 are one group whose
+    EMIT CHANGES rows print each record's own spelling ("1" or "1.0"). Every
+    row is compared with the restatement, ties included."""
     import torch
     assert torch.cuda.is_available()
     from hstream_amd.columnar import OpSpec
     from hstream_amd.engine import Engine
     from hstream_amd.ingest import Decoder, KeyDict, pack_records
     from hstream_amd.sink import Sink
-    rng = random.Random(17)
+    window, emit, ncols = LITERAL_CASES[case]
+    rng = random.Random(17 + ncols + 7 * (window[0] == "session") + emit)
     keylits = ["1", "1.0", "1e0", "10e-1", '"a"', "2.5", "25e-1"]
-    xlits = ["2", "2.0", "4", "25e-1", "2.50", "1e1", "-4", "-4.0", "0.5", "7", "3.25", None, None]
-    vlits = ["5", "-3", "20e-1", "2e1", "7", "7.0", "-1"]
+    ilits = ["5", "-3", "20e-1", "2e1", "7", "7.0", "70e-1", "-1", "-1.0", "2"]           # integral values
+    flits = ["2", "2.0", "4", "25e-1", "2.50", "1e1", "-4", "-4.0", "0.5", "7", "7.0", "3.25", None, None]
+    cols = [("v", abi.HSG_I64, ilits), ("x", abi.HSG_F64, flits)]
+    if ncols == 4:
+        cols += [("y", abi.HSG_F64, ["1", "1.0", "10e-1", "0.25", "-2", "-2.00", None]),
+                 ("z", abi.HSG_I64, ["3", "3.0", "30e-1", "-8", "-8.0", "0", "0.0", None])]
+    comps = [("cnt", "cnt", None)]
+    for name, _t, _l in cols:
+        comps += [("sum_" + name, "sum", name), ("min_" + name, "min", name), ("max_" + name, "max", name)]
+    comps.append(("last_v", "last", "v"))
+    kinds = {"cnt": abi.HSG_COUNT_ALL, "sum": abi.HSG_SUM, "min": abi.HSG_MIN, "max": abi.HSG_MAX,
+             "last": abi.HSG_LAST}
+    colidx = {name: c for c, (name, _t, _l) in enumerate(cols)}
+    aggs = [(kinds[k], colidx[col] if col else 0) for _a, k, col in comps]
+    n = 3000
     recs, vals, ts = [], [], []
-    for i in range(3000):
-        kt, x, v = rng.choice(keylits), rng.choice(xlits), rng.choice(vlits)
-        t = 1_000_000 + 200 * i  # ~3-4 records per (key, window): few cross-form ties
-        recs.append((kt, t, x, v))
-        body = '{"k":' + kt + ',"v":' + v + ("" if x is None else ',"x":' + x) + "}"
+    t = 1_000_000
+    for i in range(n):
+        kt = rng.choice(keylits)
+        # ~3-4 records per (key, window); sessions: gaps around the 900 ms
+        # gap and some records out of order, so merges of several sessions
+        t += rng.randrange(0, 400)
+        tt = t - (rng.randrange(0, 3000) if rng.random() < 0.15 else 0)
+        v = {name: rng.choice(lits) for name, _t, lits in cols}
+        v["v"] = v["v"] or "1"
+        recs.append((kt, tt, v))
+        body = '{"k":' + kt + "".join(f',"{c}":{x}' for c, x in v.items() if x is not None) + "}"
         vals.append(body.encode())
-        ts.append(t)
-    size = 5000
+        ts.append(tt)
+    batches = [1000, 1200, 800]
     eng = Engine(device=0, batch_capacity=1 << 14)
-    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_RECORD, size_ms=size, col_types=[abi.HSG_I64, abi.HSG_F64],
-                  aggs=[(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 1), (abi.HSG_MIN, 1), (abi.HSG_MAX, 1), (abi.HSG_SUM, 0),
-                        (abi.HSG_MAX, 0)], flags=abi.HSG_OPF_LITERAL_FORMS)
+    wk = abi.HSG_TUMBLING if window[0] == "tumbling" else abi.HSG_SESSION
+    spec = OpSpec(wk, emit, size_ms=window[1] if wk == abi.HSG_TUMBLING else 0,
+                  gap_ms=window[1] if wk == abi.HSG_SESSION else 0, col_types=[ty for _n, ty, _l in cols],
+                  aggs=aggs, flags=abi.HSG_OPF_LITERAL_FORMS)
     op = eng.op(spec)
     keys = KeyDict()
-    dec = Decoder("k", [("v", abi.HSG_I64, True), ("x", abi.HSG_F64, True)], literal_forms=True)
-    buf, off = pack_records(vals)
-    kid, t, cols, valid, st, rej, spell = dec.decode(keys, buf, off, np.array(ts, np.int64), spellings=True)
-    assert rej == 0
-    assert len(set(int(k) for k, r in zip(kid, recs) if r[0] in ("1", "1.0", "1e0", "10e-1"))) == 1
-    op.push(kid, t, cols, valid)
-    rows = op.drain()
-    assert rows.form is not None and len(rows) == len(recs)
-    members = [("cnt", 0), ("sum_x", 1), ("min_x", 2), ("max_x", 3), ("sum_v", 4), ("max_v", 5), ("k", -1)]
+    dec = Decoder("k", [(name, ty, True) for name, ty, _l in cols], literal_forms=True)
+    members = [(a, j) for j, (a, _k, _c) in enumerate(comps)] + [("k", -1)]
     sink = Sink(op, keys, "k", members, windowed=True)
-    got = sink.encode(rows, spellings=spell, src_base=0)
-    ref = _ref_changelog_rows(recs, size)
     written = [members[m] for m in aeson_member_order([a for a, _ in members])]
-    ties = 0
-    for i, (kb, vb) in enumerate(got):
-        r = int(rows.src_index[i])
-        key_text, ws, texts, ours, tie = ref[r]
-        own = json.dumps(json.loads(key_text)) if key_text.startswith('"') else aeson_sci(sci_parse(key_text))
-        mem = [(a, own if j < 0 else texts[a]) for a, j in written]
-        ek, ev = _ref_record(own, "k", ws, mem, True)
-        assert kb == ek, (i, r, kb, ek)
-        if tie:
-            # a MIN / MAX reached by an integral and a decimal literal of the
-            # same value: this build prints the integral form (the reference
-            # the later tied literal for MAX, the earlier for MIN); parity
-            # unpinned on exactly those rows, checked against that rule
-            ties += 1
-            mem = [(a, own if j < 0 else ours[a]) for a, j in written]
-            ev = _ref_record(own, "k", ws, mem, True)[1]
-        assert vb == ev, (i, r, recs[r], vb, ev)
-    assert ties < len(got) // 2
-    # the dump of the state carries the forms too (last rows of each group)
+    _TIES[0] = 0
+    ref = _ref_literal_rows(recs, comps, window, emit, batches)
+    at = 0
+    wm = -1
+    for bi, nb in enumerate(batches):
+        buf, off = pack_records(vals[at:at + nb])
+        kid, tb, cs, valid, _st, rej, spell = dec.decode(keys, buf, off, np.array(ts[at:at + nb], np.int64),
+                                                          spellings=True)
+        assert rej == 0
+        wm = op.push(kid, tb, cs, valid, watermark=wm)
+        rows = op.drain()
+        assert rows.form is not None
+        if emit == abi.HSG_EMIT_PER_RECORD:
+            got = sink.encode(rows, spellings=spell, src_base=at)
+            assert len(got) == nb
+            want = {x[0]: x for x in ref if at <= x[0] < at + nb}
+            for i, (kb, vb) in enumerate(got):
+                r = int(rows.src_index[i])
+                _r, own, ws, texts = want[r]
+                mem = [(a, own if j < 0 else texts[a]) for a, j in written]
+                ek, ev = _ref_record(own, "k", ws, mem, True)
+                assert kb == ek, (case, i, r, kb, ek)
+                assert vb == ev, (case, i, r, recs[r], vb, ev)
+        else:
+            got = sink.encode(rows)
+            exp = ref[bi]
+            assert len(got) == len(exp), (case, bi, len(got), len(exp))
+            mine = sorted(got)
+            exp_b = []
+            for _r, ktext, ws, texts in exp:
+                own = _first_text(ktext)
+                mem = [(a, own if j < 0 else texts[a]) for a, j in written]
+                ek, ev = _ref_record(own, "k", ws, mem, True)
+                exp_b.append((ek, ev))
+            exp_b.sort()
+            for g, e in zip(mine, exp_b):
+                assert g == e, (case, bi, g, e)
+        at += nb
+    # folds and merges that met equal MIN / MAX values spelled both ways
+    assert _TIES[0] > 0, case
     sink.close()
     op.close()
     eng.close()
