@@ -47,6 +47,8 @@ enum SessMeta : int {
   M_RUNS = 6,       // merge path: runs written by k_ss_sort
   M_BIG = 7,        // merge path: buckets left to k_ss_merge_big
   M_RELOC = 8,      // merge path: relocated lists whose prefix k_ss_reloc_copy still copies
+  M_BRBIG = 9,      // bucket replay: a sub-bucket exceeds kBrCap records (the sort-based replay runs)
+  M_BRROWS = 10,    // bucket replay: keyed records of the batch (its per-record changelog rows)
   M_SCRATCH = 15,   // device landing word (compaction total)
   M_RNEED = 16,                              // [kArenaRegions] replay path: rows its list growth needs
   M_RTOP = M_RNEED + kArenaRegions,          // [kArenaRegions x kRegionStride] region bump pointers
@@ -101,6 +103,13 @@ struct SessPart {
   uint64_t *scopy;     // [n][words] per bucket: its records grouped by sub-bucket (k_ss_sort)
   uint32_t *gsparse;   // [n][4] group records at their sub-bucket's record positions
   uint64_t *reloc;     // [n][3] relocated lists (old row, new row, rows of the prefix to copy)
+  // bucket replay (per-record changelog, LAST, literal forms)
+  uint32_t *tkeyed;    // [tiles] keyed records of each arrival tile (k_ss_phist)
+  uint64_t *toff;      // [tiles + 1] exclusive prefix: the tile's first changelog row
+  uint32_t *subst;     // [nb][65] each bucket's sub-bucket starts (k_br_subhist)
+  uint32_t *bperm;     // [n] record positions grouped by sub-bucket within each bucket
+  int64_t *fin;        // [n][2 + n_slots] per arrival index: session start, end, state after the record
+  uint64_t *tpartial;  // scan partials over the tiles
 };
 // bshift: owner bits of the key hash above the bucket bits (multi-GPU)
 void launch_ss_phist(hipStream_t s, const Batch &b, int np_log2, int bshift, uint64_t tiles, const SessPart &sp);
@@ -121,6 +130,25 @@ void launch_ss_reloc_copy(hipStream_t s, const SessTable &t, const SessPart &sp,
 // per-batch changelog of the keys k_ss_merge_big touched (emit = 0: count only)
 void launch_ss_emit(hipStream_t s, const SessTable &t, const Program &prog, const SessPart &sp, uint32_t batch_id,
                     int emit, uint64_t n_bound, OutCols out, uint64_t out_base, DevScalars *sc);
+
+// bucket replay (per-record changelog, LAST, literal forms): records carry
+// their arrival index ([word 0 | literal-form bits << 40] [ts] [cols] [index]);
+// per bucket, sub-buckets of at most kBrCap records are grouped by key in LDS
+// and each key's records replayed in arrival order against its list, the
+// state after every record written to sp.fin at its arrival index; the
+// changelog is then written in arrival order (k_br_emit). A sub-bucket of more
+// than kBrCap records (a hot key) sets M_BRBIG before anything is modified,
+// and the batch takes the sort-based replay instead.
+constexpr int kBrCap = 1024;
+int br_words(int n_cols);
+void launch_br_scatter(hipStream_t s, const Batch &b, int np_log2, int bshift, uint64_t tiles, int words,
+                       const SessPart &sp);
+void launch_br_subhist(hipStream_t s, const SessTable &t, int np_log2, int bshift, int words, const SessPart &sp);
+void launch_br_replay(hipStream_t s, const Batch &b, const SessParams &p, const SessTable &t, const Program &prog,
+                      int np_log2, int bshift, int words, const SessPart &sp, const int64_t *seq, OutCols out,
+                      uint64_t out_base, DevScalars *sc);
+void launch_br_emit(hipStream_t s, const Batch &b, const SessParams &p, const Program &prog, const SessPart &sp,
+                    uint64_t tiles, const int64_t *seq, OutCols out, uint64_t out_base);
 
 void launch_ss_dump(hipStream_t s, const SessTable &t, const Program &prog, OutCols out, uint64_t out_cap,
                     uint64_t *counter);

@@ -450,12 +450,14 @@ __device__ inline uint64_t i64_img(int64_t v) { return (uint64_t)v ^ 0x800000000
 __global__ __launch_bounds__(kSsPNT) void k_ss_phist(Batch b, int np_log2, int bshift, SessPart sp) {
   __shared__ uint32_t cnt[1 << 11];
   __shared__ uint64_t smx[kSsPNT / 64];
+  __shared__ uint32_t skey[kSsPNT / 64];
   const int nb = 1 << np_log2;
   const uint64_t tile = blockIdx.x;
   for (int i = threadIdx.x; i < nb; i += kSsPNT) cnt[i] = 0;
   __syncthreads();
   const uint64_t base = tile * kSsTile;
   uint64_t mx = 0;
+  uint32_t keyed = 0;
 #pragma unroll
   for (int r = 0; r < kSsTile / kSsPNT; ++r) {
     const uint64_t i = base + (uint64_t)r * kSsPNT + threadIdx.x;
@@ -463,19 +465,31 @@ __global__ __launch_bounds__(kSsPNT) void k_ss_phist(Batch b, int np_log2, int b
     const uint32_t key = b.key[i];
     const uint64_t o = i64_img(b.ts[i]);
     mx = o > mx ? o : mx;
-    if (key != HSG_KEY_NONE) atomicAdd(&cnt[ss_bucket(key, np_log2, bshift)], 1u);
+    if (key != HSG_KEY_NONE) {
+      atomicAdd(&cnt[ss_bucket(key, np_log2, bshift)], 1u);
+      ++keyed;
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const uint64_t x = __shfl_xor(mx, o, 64);
     mx = x > mx ? x : mx;
+    keyed += __shfl_xor(keyed, o, 64);
   }
-  if ((threadIdx.x & 63) == 0) smx[threadIdx.x >> 6] = mx;
+  if ((threadIdx.x & 63) == 0) {
+    smx[threadIdx.x >> 6] = mx;
+    skey[threadIdx.x >> 6] = keyed;
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < nb; i += kSsPNT) sp.hist[tile * (uint64_t)nb + i] = cnt[i];
   if (threadIdx.x == 0) {
-    for (int k = 0; k < kSsPNT / 64; ++k) mx = smx[k] > mx ? smx[k] : mx;
+    uint32_t kt = 0;
+    for (int k = 0; k < kSsPNT / 64; ++k) {
+      mx = smx[k] > mx ? smx[k] : mx;
+      kt += skey[k];
+    }
     sp.tmax[tile] = mx;
+    if (sp.tkeyed) sp.tkeyed[tile] = kt;  // (bucket replay: the tile's changelog rows)
   }
 }
 
@@ -508,7 +522,7 @@ void launch_ss_wm(hipStream_t s, const SessPart &sp, uint64_t tiles, int64_t wm_
 // Records of one tile to their bucket runs: sub-tiles of kSsSub records are
 // counting-sorted by bucket into an LDS copy and written out with consecutive
 // lanes on consecutive words of a run. Record: [key | valid bits << 32] [ts] [cols].
-template <int W>
+template <int W, bool IDX = false>
 __global__ __launch_bounds__(kSsPNT) void k_ss_pscatter(Batch b, int np_log2, int bshift, int has_valid, SessPart sp) {
   __shared__ uint64_t stage[kSsSub * W];
   __shared__ uint32_t cursor[1 << 11];  // records of each bucket placed by earlier sub-tiles
@@ -516,11 +530,12 @@ __global__ __launch_bounds__(kSsPNT) void k_ss_pscatter(Batch b, int np_log2, in
   __shared__ uint32_t lstart[1 << 11];
   __shared__ uint16_t lbk[kSsSub];
   __shared__ uint32_t swave[kSsPNT / 64];
-  constexpr int C = W - 2;
+  constexpr int C = IDX ? W - 3 : W - 2;  // IDX: the record's arrival index in the last word
   constexpr int R = kSsSub / kSsPNT;
   const int nb = 1 << np_log2;
   const uint64_t tile = blockIdx.x;
   const uint32_t *orow = sp.offt + tile * (uint64_t)nb;
+  uint64_t *out = IDX ? (uint64_t *)sp.srec : sp.rec;
   for (int i = threadIdx.x; i < nb; i += kSsPNT) cursor[i] = 0;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int sub = 0; sub < kSsTile / kSsSub; ++sub) {
@@ -566,12 +581,15 @@ __global__ __launch_bounds__(kSsPNT) void k_ss_pscatter(Batch b, int np_log2, in
       const uint32_t q = lstart[bk] + pos[r];
       uint64_t vb = 0;
 #pragma unroll
-      for (int c = 0; c < C; ++c)
+      for (int c = 0; c < C; ++c) {
         if (!(has_valid && b.valid[c] && !b.valid[c][i])) vb |= 1ull << c;
+        if (IDX && has_valid && rec_decimal(b, c, i)) vb |= 1ull << (8 + c);  // literal-form bits
+      }
       stage[q * W] = (uint64_t)key[r] | (vb << 32);
       stage[q * W + 1] = (uint64_t)b.ts[i];
 #pragma unroll
       for (int c = 0; c < C; ++c) stage[q * W + 2 + c] = (uint64_t)b.col[c][i];
+      if (IDX) stage[q * W + W - 1] = i;
       lbk[q] = (uint16_t)bk;
     }
     __syncthreads();
@@ -580,7 +598,7 @@ __global__ __launch_bounds__(kSsPNT) void k_ss_pscatter(Batch b, int np_log2, in
       const uint32_t q = t / W, w = t - q * W;
       const uint32_t bk = lbk[q];
       const uint64_t dest = (uint64_t)orow[bk] + cursor[bk] + (q - lstart[bk]);
-      sp.rec[dest * W + w] = stage[t];
+      out[dest * W + w] = stage[t];
     }
     lds_barrier();  // the next sub-tile reuses the LDS stage only
     for (int i = threadIdx.x; i < nb; i += kSsPNT) cursor[i] += scnt[i];
@@ -1987,6 +2005,471 @@ void launch_ss_dump(hipStream_t s, const SessTable &t, const Program &prog, OutC
   uint64_t blocks = (t.kmask + 1 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(k_ss_dump, dim3((unsigned)blocks), dim3(256), 0, s, t, prog, out, out_cap, counter);
+}
+
+// ---------------------------------------------------------------------------
+// Bucket replay (hsg_session.h): per-record changelog, LAST, literal forms.
+// ---------------------------------------------------------------------------
+constexpr int kBrNT = 256;
+constexpr int kBrTab = 2 * kBrCap;  // LDS key table entries (load <= 1/2)
+constexpr int kBrMaxSubLog2 = 6;
+constexpr int kBrSubNT = 256;
+
+int br_words(int n_cols) { return 3 + n_cols; }
+
+// sub-bucket bits of a bucket of m records: sub-buckets of about kBrCap / 2
+__device__ inline int br_sub_log2(uint64_t m) {
+  int sl = 0;
+  while (((uint64_t)(kBrCap / 2) << sl) < m && sl < kBrMaxSubLog2) ++sl;
+  return sl;
+}
+
+void launch_br_scatter(hipStream_t s, const Batch &b, int np_log2, int bshift, uint64_t tiles, int words,
+                       const SessPart &sp) {
+  if (!tiles) return;
+  const dim3 g((unsigned)tiles), th(kSsPNT);
+  bool hv = false;
+  for (int c = 0; c < kMaxCols; ++c) hv = hv || b.valid[c] != nullptr;
+  const int v = hv ? 1 : 0;
+  switch (words) {
+    case 3: hipLaunchKernelGGL((k_ss_pscatter<3, true>), g, th, 0, s, b, np_log2, bshift, v, sp); break;
+    case 4: hipLaunchKernelGGL((k_ss_pscatter<4, true>), g, th, 0, s, b, np_log2, bshift, v, sp); break;
+    case 5: hipLaunchKernelGGL((k_ss_pscatter<5, true>), g, th, 0, s, b, np_log2, bshift, v, sp); break;
+    case 6: hipLaunchKernelGGL((k_ss_pscatter<6, true>), g, th, 0, s, b, np_log2, bshift, v, sp); break;
+    case 7: hipLaunchKernelGGL((k_ss_pscatter<7, true>), g, th, 0, s, b, np_log2, bshift, v, sp); break;
+    case 8: hipLaunchKernelGGL((k_ss_pscatter<8, true>), g, th, 0, s, b, np_log2, bshift, v, sp); break;
+    case 9: hipLaunchKernelGGL((k_ss_pscatter<9, true>), g, th, 0, s, b, np_log2, bshift, v, sp); break;
+    case 10: hipLaunchKernelGGL((k_ss_pscatter<10, true>), g, th, 0, s, b, np_log2, bshift, v, sp); break;
+    default: hipLaunchKernelGGL((k_ss_pscatter<11, true>), g, th, 0, s, b, np_log2, bshift, v, sp); break;
+  }
+}
+
+// Per bucket: its records' positions grouped by sub-bucket (sp.bperm, within
+// the bucket's own range) and the sub-bucket starts (sp.subst[b][0 .. 2^sl]);
+// a sub-bucket of more than kBrCap records flags the batch (M_BRBIG) before
+// any state is touched.
+__global__ __launch_bounds__(kBrSubNT) void k_br_subhist(SessTable t, int np_log2, int bshift, int W, SessPart sp) {
+  __shared__ uint32_t cnt[1 << kBrMaxSubLog2];
+  __shared__ uint32_t cur[1 << kBrMaxSubLog2];
+  const uint32_t b = blockIdx.x;
+  const uint64_t r0 = sp.bstart[b], m = sp.bstart[b + 1] - r0;
+  const int sl = br_sub_log2(m), nsub = 1 << sl, hs = bshift + np_log2;
+  if (threadIdx.x < (1 << kBrMaxSubLog2)) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint64_t q = threadIdx.x; q < m; q += kBrSubNT) {
+    const uint32_t key = (uint32_t)sp.srec[(r0 + q) * W];
+    atomicAdd(&cnt[ss_sub(key, hs, sl)], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    bool big = false;
+    for (int k = 0; k < nsub; ++k) {
+      cur[k] = run;
+      sp.subst[b * 65ull + k] = run;
+      run += cnt[k];
+      big = big || cnt[k] > (uint32_t)kBrCap;
+    }
+    sp.subst[b * 65ull + nsub] = run;
+    if (big) atomicOr((unsigned long long *)&t.meta[M_BRBIG], 1ull);
+  }
+  __syncthreads();
+  for (uint64_t q = threadIdx.x; q < m; q += kBrSubNT) {
+    const uint32_t key = (uint32_t)sp.srec[(r0 + q) * W];
+    const uint32_t at = atomicAdd(&cur[ss_sub(key, hs, sl)], 1u);
+    sp.bperm[r0 + at] = (uint32_t)(r0 + q);
+  }
+}
+
+void launch_br_subhist(hipStream_t s, const SessTable &t, int np_log2, int bshift, int words, const SessPart &sp) {
+  hipLaunchKernelGGL(k_br_subhist, dim3(1u << np_log2), dim3(kBrSubNT), 0, s, t, np_log2, bshift, words, sp);
+}
+
+// contribution of a bucket-replay record (present bits 32..39, literal-form
+// bits 40..47 of word 0) to every slot, LAST / form slots included
+template <int MS>
+__device__ inline void br_elem(const Program &prog, const uint64_t *rec, uint64_t seq1, int64_t (&e)[MS]) {
+  const uint64_t vb = rec[0] >> 32;
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    e[s] = 0;
+    if (s >= prog.n_slots) continue;
+    const int op = prog.slot_op[s], c = prog.slot_col[s];
+    if (op == S_CNT_ALL) {
+      e[s] = 1;
+      continue;
+    }
+    const bool present = ((vb >> c) & 1ull) != 0, dec = ((vb >> (8 + c)) & 1ull) != 0;
+    const int64_t x = (int64_t)rec[2 + c];
+    if (op == S_LAST_VAL) {
+      e[s] = present ? x : 0;
+      continue;
+    }
+    if (!present) {
+      e[s] = slot_identity_dev(op);
+      continue;
+    }
+    switch (op) {
+      case S_CNT: e[s] = 1; break;
+      case S_MIN_F:
+      case S_MAX_F: e[s] = (int64_t)f64_ord(__builtin_bit_cast(double, x)); break;
+      case S_LAST_SEQ: e[s] = (int64_t)seq1; break;
+      case S_CNT_DEC: e[s] = dec ? 1 : 0; break;
+      case S_TIE_MIN:
+      case S_TIE_MAX:
+      case S_LAST_FORM: e[s] = (int64_t)((seq1 << 1) | (dec ? 0u : 1u)); break;
+      default: e[s] = x; break;
+    }
+  }
+}
+
+struct BrLds {
+  uint32_t tkey[kBrTab];  // key table; after the grouping: the group's key-table slot
+  uint32_t tcnt[kBrTab];  // records per key; after the grouping: the key's group, then the group's fresh rows
+  uint32_t rpos[kBrCap];  // record -> its position in sp.srec
+  uint32_t ridx[kBrCap];  // record -> its arrival index
+  uint16_t rtab[kBrCap];  // record -> its key's table entry
+  uint16_t seg[kBrCap];   // records placed by group
+  uint16_t ord[kBrCap];   // records placed by group, in arrival order within a group
+  uint32_t gkey[kBrCap];
+  uint16_t gstart[kBrCap];
+  uint16_t gcnt[kBrCap];
+  uint32_t gcur[kBrCap];
+  uint32_t wsum[kBrNT / 64];
+  uint64_t wsum64[kBrNT / 64];
+  uint32_t ngrp, nrec;
+  uint64_t abase;
+  uint32_t fail;
+};
+
+template <int MS, int W>
+__global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, SessTable t, Program prog, int np_log2,
+                                                     int bshift, SessPart sp, const int64_t *seq, OutCols out,
+                                                     uint64_t out_base, DevScalars *sc) {
+  __shared__ BrLds L;
+  if (t.meta[M_BRBIG] || t.meta[M_FAIL]) return;  // uniform: the other replay runs / the arena is refilled first
+  const uint32_t bk = blockIdx.x;
+  const uint64_t r0 = sp.bstart[bk], m = sp.bstart[bk + 1] - r0;
+  const int sl = br_sub_log2(m), nsub = 1 << sl;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t fs = 2 + (uint32_t)prog.n_slots;
+  const uint32_t region = arena_region(bk);
+  int64_t live_delta = 0;
+  uint64_t inserted = 0;
+  for (int sub = (int)sp.progress[bk]; sub < nsub; ++sub) {
+    const uint32_t s0 = sp.subst[bk * 65ull + sub], cnt = sp.subst[bk * 65ull + sub + 1] - s0;
+    // 1. group the sub-bucket's records by key (LDS hash table)
+    for (int i = threadIdx.x; i < kBrTab; i += kBrNT) {
+      L.tkey[i] = kSessEmptyKey;
+      L.tcnt[i] = 0;
+    }
+    if (threadIdx.x == 0) {
+      L.ngrp = 0;
+      L.fail = 0;
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < cnt; q += kBrNT) {
+      const uint32_t pos = sp.bperm[r0 + s0 + q];
+      const uint64_t *rec = sp.srec + (uint64_t)pos * W;
+      const uint32_t key = (uint32_t)rec[0];
+      uint32_t h = (uint32_t)key_hash(key) & (kBrTab - 1);
+      for (;;) {
+        const uint32_t old = atomicCAS(&L.tkey[h], kSessEmptyKey, key);
+        if (old == kSessEmptyKey || old == key) break;
+        h = (h + 1) & (kBrTab - 1);
+      }
+      atomicAdd(&L.tcnt[h], 1u);
+      L.rpos[q] = pos;
+      L.ridx[q] = (uint32_t)rec[W - 1];
+      L.rtab[q] = (uint16_t)h;
+    }
+    __syncthreads();
+    // 2. groups: the keys in table order, their segments (block scan over the table)
+    {
+      constexpr int PER = kBrTab / kBrNT;
+      uint32_t c[PER], nz = 0, tot = 0;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        c[k] = L.tcnt[threadIdx.x * PER + k];
+        nz += c[k] ? 1u : 0u;
+        tot += c[k];
+      }
+      const uint64_t packed = ((uint64_t)nz << 32) | tot;
+      const uint64_t incl = wave_incl_sum(packed);
+      if (lane == 63) L.wsum64[w] = incl;
+      __syncthreads();
+      uint64_t pre = incl - packed;
+      for (int k = 0; k < w; ++k) pre += L.wsum64[k];
+      uint32_t g = (uint32_t)(pre >> 32), at = (uint32_t)pre;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int slot = threadIdx.x * PER + k;
+        if (!c[k]) continue;
+        L.gkey[g] = L.tkey[slot];
+        L.gstart[g] = (uint16_t)at;
+        L.gcnt[g] = (uint16_t)c[k];
+        L.gcur[g] = 0;
+        L.tcnt[slot] = g;
+        ++g;
+        at += c[k];
+      }
+      if (threadIdx.x == kBrNT - 1) L.ngrp = g;
+    }
+    __syncthreads();
+    const uint32_t ngrp = L.ngrp;
+    // 3. records into their group's segment, then ranked by arrival index
+    for (uint32_t q = threadIdx.x; q < cnt; q += kBrNT) {
+      const uint32_t g = L.tcnt[L.rtab[q]];
+      L.seg[L.gstart[g] + atomicAdd(&L.gcur[g], 1u)] = (uint16_t)q;
+      L.rtab[q] = (uint16_t)g;  // (now: the record's group)
+    }
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < cnt; x += kBrNT) {
+      const uint32_t q = L.seg[x], g = L.rtab[q], st = L.gstart[g], c = L.gcnt[g], me = L.ridx[q];
+      uint32_t rank = 0;
+      for (uint32_t y = st; y < st + c; ++y) rank += L.ridx[L.seg[y]] < me ? 1u : 0u;
+      L.ord[st + rank] = (uint16_t)q;
+    }
+    // 4. every group's key-table entry; the fresh list rows the sub-bucket needs
+    uint64_t need = 0;
+    for (uint32_t g = threadIdx.x; g < ngrp; g += kBrNT) {
+      bool ins = false;
+      const int64_t ks = ss_find_or_insert(t, L.gkey[g], ins);
+      inserted += ins ? 1u : 0u;
+      uint32_t nc = 0;
+      if (ks < 0) {
+        atomicOr(&sc->err, ERR_OOM);
+      } else {
+        const SessKey e = ss_load_entry(&t.kt[ks]);
+        const uint64_t want = (uint64_t)e.len + L.gcnt[g];
+        nc = want > e.cap ? ss_grow_cap(want) : 0u;
+      }
+      L.tkey[g] = ks < 0 ? ~0u : (uint32_t)ks;
+      L.tcnt[g] = nc;
+      need += nc;
+    }
+    const uint64_t wneed = wave_sum_u64(need);
+    if (lane == 0) L.wsum64[w] = wneed;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t tot = 0;
+      for (int k = 0; k < kBrNT / 64; ++k) tot += L.wsum64[k];
+      uint64_t base = 0;
+      if (tot && !arena_take(t, region, tot, base)) {
+        // no room: this sub-bucket (and the rest of the bucket) runs again after
+        // the host compacts / grows the arena (sp.progress resumes it here)
+        L.fail = 1;
+        t.meta[M_FAIL] = 1;
+        atomicAdd((unsigned long long *)&t.meta[M_RNEED + region], (unsigned long long)tot);
+      }
+      L.abase = base;
+    }
+    __syncthreads();
+    if (L.fail) break;
+    // fresh-list offsets: exclusive scan of the groups' fresh rows (group order)
+    {
+      const uint32_t per = (ngrp + kBrNT - 1) / kBrNT;
+      const uint32_t g0 = threadIdx.x * per, g1 = g0 + per < ngrp ? g0 + per : ngrp;
+      uint64_t loc = 0;
+      for (uint32_t g = g0; g < g1; ++g) loc += L.tcnt[g];
+      const uint64_t incl = wave_incl_sum(loc);
+      __syncthreads();
+      if (lane == 63) L.wsum64[w] = incl;
+      __syncthreads();
+      uint64_t run = incl - loc;
+      for (int k = 0; k < w; ++k) run += L.wsum64[k];
+      for (uint32_t g = g0; g < g1; ++g) {
+        const uint32_t nc = L.tcnt[g];
+        L.tcnt[g] = nc ? (uint32_t)run + 1u : 0u;  // (row offset + 1 within the reservation; 0: in place)
+        run += nc;
+      }
+    }
+    __syncthreads();
+    // 5. replay: one thread per key, its records in arrival order against its list
+    for (uint32_t g = threadIdx.x; g < ngrp; g += kBrNT) {
+      const uint32_t ks = L.tkey[g];
+      if (ks == ~0u) continue;
+      const SessKey e = ss_load_entry(&t.kt[ks]);
+      uint64_t off = e.off, len = e.len;
+      uint32_t lcap = e.cap;
+      if (L.tcnt[g]) {
+        const uint64_t noff = L.abase + L.tcnt[g] - 1;
+        for (uint64_t k = 0; k < len; ++k) ss_copy(t, noff + k, t, off + k);
+        off = noff;
+        lcap = ss_grow_cap(len + L.gcnt[g]);
+      }
+      const uint32_t st = L.gstart[g], c = L.gcnt[g];
+      for (uint32_t x = st; x < st + c; ++x) {
+        const uint32_t q = L.ord[x];
+        const uint64_t *rec = sp.srec + (uint64_t)L.rpos[q] * W;
+        const uint32_t i = L.ridx[q];
+        const int64_t ts = (int64_t)rec[1];
+        const uint64_t seq1 = (seq ? (uint64_t)seq[i] : p.rec_base + i) + 1;
+        const int64_t lo = (int64_t)((uint64_t)ts - (uint64_t)p.gap);
+        const int64_t hi = (int64_t)((uint64_t)ts + (uint64_t)p.gap);
+        // first session with end >= lo (ends ascend: sessions are disjoint)
+        uint64_t a = 0, z = len;
+        while (a < z) {
+          const uint64_t mid = (a + z) >> 1;
+          if ((int64_t)ss_row(t, off + mid)[1] < lo) a = mid + 1;
+          else z = mid;
+        }
+        const uint64_t i0 = a;
+        uint64_t i1 = i0;
+        while (i1 < len && (int64_t)ss_row(t, off + i1)[0] <= hi) ++i1;
+        // aggF initialValue r, then mergeF acc cur over the overlapped sessions
+        int64_t acc[MS], ev[MS];
+        identity_row<MS>(prog, acc);
+        br_elem<MS>(prog, rec, seq1, ev);
+        combine_row<MS>(prog, acc, ev);
+        int64_t ss = ts, se = ts;
+        for (uint64_t k = i0; k < i1; ++k) {
+          const uint64_t *row = ss_row(t, off + k);
+          const int64_t cs = (int64_t)row[0], ce = (int64_t)row[1];
+          ss = cs < ss ? cs : ss;
+          se = ce > se ? ce : se;
+          int64_t cur[MS];
+          ss_load<MS>(t, off + k, cur);
+          merge_row<MS>(prog, acc, cur);
+        }
+        const uint64_t mc = i1 - i0;
+        if (mc == 0) {
+          for (uint64_t k = len; k > i0; --k) ss_copy(t, off + k, t, off + k - 1);
+          len += 1;
+        } else if (mc > 1) {
+          for (uint64_t k = i1; k < len; ++k) ss_copy(t, off + k - (mc - 1), t, off + k);
+          len -= mc - 1;
+        }
+        live_delta += 1 - (int64_t)mc;
+        ss_store<MS>(t, off + i0, ss, se, p.batch_id, acc);
+        int64_t *f = sp.fin + (uint64_t)i * fs;
+        f[0] = ss;
+        f[1] = se;
+#pragma unroll
+        for (int s = 0; s < MS; ++s)
+          if (s < prog.n_slots) f[2 + s] = acc[s];
+      }
+      t.kt[ks].off = off;
+      t.kt[ks].len = (uint32_t)len;
+      t.kt[ks].cap = lcap;
+      t.kt[ks].mvalid = 0;  // the replay keeps no mirror of the last session
+    }
+    // per-batch changelog (LAST / literal forms per batch): the keys' sessions stamped by this batch
+    if (p.emit_mode == HSG_EMIT_PER_BATCH) {
+      uint64_t mine = 0;
+      for (uint32_t g = threadIdx.x; g < ngrp; g += kBrNT) {
+        if (L.tkey[g] == ~0u) continue;
+        const SessKey e = ss_load_entry(&t.kt[L.tkey[g]]);
+        for (uint64_t k = 0; k < e.len; ++k) mine += (uint32_t)ss_row(t, e.off + k)[2] == p.batch_id;
+      }
+      const uint64_t incl = wave_incl_sum(mine);
+      __syncthreads();
+      if (lane == 63) L.wsum64[w] = incl;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint64_t tot = 0;
+        for (int k = 0; k < kBrNT / 64; ++k) tot += L.wsum64[k];
+        L.abase = tot ? atomicAdd((unsigned long long *)&sc->out_rows, (unsigned long long)tot) : 0;
+        if (tot) atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)tot);
+      }
+      __syncthreads();
+      uint64_t o = out_base + L.abase + incl - mine;
+      for (int k = 0; k < w; ++k) o += L.wsum64[k];
+      for (uint32_t g = threadIdx.x; g < ngrp && mine; g += kBrNT) {
+        if (L.tkey[g] == ~0u) continue;
+        const SessKey e = ss_load_entry(&t.kt[L.tkey[g]]);
+        for (uint64_t k = 0; k < e.len; ++k) {
+          const uint64_t *row = ss_row(t, e.off + k);
+          if ((uint32_t)row[2] != p.batch_id) continue;
+          out.key[o] = e.key;
+          out.ws[o] = (int64_t)row[0];
+          out.we[o] = (int64_t)row[1];
+          out.src[o] = -1;
+          for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, (const int64_t *)row + 3);
+          if (out.form) out.form[o] = out_form(prog, (const int64_t *)row + 3);
+          ++o;
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) sp.progress[bk] = (uint32_t)(sub + 1);
+  }
+  const uint64_t ld = wave_sum_u64((uint64_t)live_delta);
+  if (lane == 0 && ld) atomicAdd((unsigned long long *)&sc->live, (unsigned long long)ld);
+  const uint64_t ins = wave_sum_u64(inserted);
+  if (lane == 0 && ins) atomicAdd((unsigned long long *)&t.meta[M_KEYS], (unsigned long long)ins);
+}
+
+template <int MS>
+static void br_replay_launch(hipStream_t s, int W, dim3 g, const Batch &b, const SessParams &p, const SessTable &t,
+                             const Program &prog, int np_log2, int bshift, const SessPart &sp, const int64_t *seq,
+                             OutCols out, uint64_t out_base, DevScalars *sc) {
+  const dim3 th(kBrNT);
+#define BR_W(WW)                                                                                              \
+  case WW:                                                                                                    \
+    hipLaunchKernelGGL((k_br_replay<MS, WW>), g, th, 0, s, b, p, t, prog, np_log2, bshift, sp, seq, out, out_base, \
+                       sc);                                                                                   \
+    break;
+  switch (W) {
+    BR_W(3) BR_W(4) BR_W(5) BR_W(6) BR_W(7) BR_W(8) BR_W(9) BR_W(10)
+    default: hipLaunchKernelGGL((k_br_replay<MS, 11>), g, th, 0, s, b, p, t, prog, np_log2, bshift, sp, seq, out,
+                                out_base, sc);
+  }
+#undef BR_W
+}
+
+void launch_br_replay(hipStream_t s, const Batch &b, const SessParams &p, const SessTable &t, const Program &prog,
+                      int np_log2, int bshift, int words, const SessPart &sp, const int64_t *seq, OutCols out,
+                      uint64_t out_base, DevScalars *sc) {
+  const dim3 g(1u << np_log2);
+  if (prog.n_slots <= 2) br_replay_launch<2>(s, words, g, b, p, t, prog, np_log2, bshift, sp, seq, out, out_base, sc);
+  else if (prog.n_slots <= 4) br_replay_launch<4>(s, words, g, b, p, t, prog, np_log2, bshift, sp, seq, out, out_base, sc);
+  else if (prog.n_slots <= 8) br_replay_launch<8>(s, words, g, b, p, t, prog, np_log2, bshift, sp, seq, out, out_base, sc);
+  else if (prog.n_slots <= 16) br_replay_launch<16>(s, words, g, b, p, t, prog, np_log2, bshift, sp, seq, out, out_base, sc);
+  else br_replay_launch<kMaxSlots>(s, words, g, b, p, t, prog, np_log2, bshift, sp, seq, out, out_base, sc);
+}
+
+// The per-record changelog in arrival order: tile t's keyed records take rows
+// from sp.toff[t] on (an in-tile exclusive scan of the keyed flags), each row
+// from the state its record left in sp.fin. Coalesced columns.
+__global__ __launch_bounds__(256) void k_br_emit(Batch b, SessParams p, Program prog, SessPart sp, const int64_t *seq,
+                                                 OutCols out, uint64_t out_base) {
+  __shared__ uint32_t sw[4];
+  const uint64_t base = (uint64_t)blockIdx.x * kSsTile;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t fs = 2 + (uint32_t)prog.n_slots;
+  uint64_t o = out_base + sp.toff[blockIdx.x];
+  for (int r = 0; r < kSsTile / 256; ++r) {
+    const uint64_t i = base + (uint64_t)r * 256 + threadIdx.x;
+    const uint32_t key = i < b.n ? b.key[i] : HSG_KEY_NONE;
+    const bool keyed = key != HSG_KEY_NONE;
+    const uint64_t m = __ballot(keyed);
+    const uint32_t pre = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) sw[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t wpre = 0, tot = 0;
+    for (int k = 0; k < 4; ++k) {
+      wpre += k < w ? sw[k] : 0u;
+      tot += sw[k];
+    }
+    if (keyed) {
+      const uint64_t q = o + wpre + pre;
+      const int64_t *f = sp.fin + i * fs;
+      out.key[q] = key;
+      out.ws[q] = f[0];
+      out.we[q] = f[1];
+      out.src[q] = seq ? seq[i] : (int64_t)(p.rec_base + i);
+      for (int j = 0; j < prog.n_out; ++j) out.agg[j][q] = out_value(prog, j, f + 2);
+      if (out.form) out.form[q] = out_form(prog, f + 2);
+    }
+    o += tot;
+    __syncthreads();
+  }
+}
+
+void launch_br_emit(hipStream_t s, const Batch &b, const SessParams &p, const Program &prog, const SessPart &sp,
+                    uint64_t tiles, const int64_t *seq, OutCols out, uint64_t out_base) {
+  if (tiles) hipLaunchKernelGGL(k_br_emit, dim3((unsigned)tiles), dim3(256), 0, s, b, p, prog, sp, seq, out, out_base);
 }
 
 }  // namespace hsg

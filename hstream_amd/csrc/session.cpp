@@ -84,7 +84,7 @@ static int set_regions(OpDevice &d, uint64_t used, std::string &err) {
 // Session partition scratch (besides d.part's histogram, offsets and
 // records): per-tile ts maxima, per-bucket progress and big flags, the touched
 // list, the runs and key groups of k_ss_sort, the apply blocks' done flags.
-static uint64_t ss_part_layout(uint64_t n, int words, SessPart *sp, char *m) {
+static uint64_t ss_part_layout(uint64_t n, int words, SessPart *sp, char *m, bool br = false, uint32_t ns = 0) {
   uint64_t off = 0;
   auto take = [&](uint64_t bytes) {
     off = (off + 255) & ~255ull;
@@ -97,21 +97,32 @@ static uint64_t ss_part_layout(uint64_t n, int words, SessPart *sp, char *m) {
   memset(&x, 0, sizeof(x));
   x.tmax = (uint64_t *)take(tiles * 8);
   x.progress = (uint32_t *)take(nb * 4);
-  x.bigmask = (uint64_t *)take(nb * 8);
-  x.touched = (uint32_t *)take(n * 4);
   x.srec = (uint64_t *)take(n * (uint64_t)words * 8);
-  x.groups = (uint32_t *)take(n * 16);
-  x.done = (uint8_t *)take(n / 256 + 2);
-  x.scopy = (uint64_t *)take(n * (uint64_t)words * 8);
-  x.gsparse = (uint32_t *)take(n * 16);
-  x.reloc = (uint64_t *)take(n * 24);
+  if (br) {
+    // bucket replay: its records (srec, with their arrival index), the
+    // states by arrival index, the tiles' changelog offsets, the sub-buckets
+    x.fin = (int64_t *)take(n * (2ull + ns) * 8);
+    x.tkeyed = (uint32_t *)take(tiles * 4);
+    x.toff = (uint64_t *)take((tiles + 1) * 8);
+    x.tpartial = (uint64_t *)take((scan_partials_needed(tiles) + 8) * 8);
+    x.subst = (uint32_t *)take(nb * 65 * 4);
+    x.bperm = (uint32_t *)take(n * 4);
+  } else {
+    x.bigmask = (uint64_t *)take(nb * 8);
+    x.touched = (uint32_t *)take(n * 4);
+    x.groups = (uint32_t *)take(n * 16);
+    x.done = (uint8_t *)take(n / 256 + 2);
+    x.scopy = (uint64_t *)take(n * (uint64_t)words * 8);
+    x.gsparse = (uint32_t *)take(n * 16);
+    x.reloc = (uint64_t *)take(n * 24);
+  }
   if (sp) *sp = x;
   return off;
 }
 
-static SessPart sess_part(OpDevice &d, int words) {
+static SessPart sess_part(OpDevice &d, int words, bool br = false) {
   SessPart sp;
-  ss_part_layout(d.batch_cap, words, &sp, (char *)d.ss_part);
+  ss_part_layout(d.batch_cap, words, &sp, (char *)d.ss_part, br, d.ss.ns);
   sp.hist = d.part.hist;
   sp.offt = d.part.offt;
   sp.bstart = d.part.bstart;
@@ -141,10 +152,15 @@ int session_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &pr
   DTRY(hipHostMalloc((void **)&d.h_meta, M_WORDS * sizeof(uint64_t), hipHostMallocDefault));
   DTRY(hipHostMalloc((void **)&d.h_regions, kArenaRegions * kRegionStride * sizeof(uint64_t), hipHostMallocDefault));
   d.ss_merge = cfg.emit_mode != HSG_EMIT_PER_RECORD && !has_last(prog) && !prog_has_forms(prog) && prog.n_slots <= 8;
+  rc = part_device_init(d, cfg, prog, err);
+  if (rc != HSG_OK) return rc;
   if (d.ss_merge) {
-    rc = part_device_init(d, cfg, prog, err);
-    if (rc != HSG_OK) return rc;
     DTRY(hipMalloc(&d.ss_part, ss_part_layout(d.batch_cap, 2 + cfg.n_cols, nullptr, nullptr)));
+  } else {
+    // the bucket replay (the sort-based replay's buffers, perrecord_device_init,
+    // stay for batches with a hot key)
+    DTRY(hipMalloc(&d.ss_part, ss_part_layout(d.batch_cap, br_words(cfg.n_cols), nullptr, nullptr, true,
+                                              (uint32_t)prog.n_slots)));
   }
   return HSG_OK;
 }
@@ -310,6 +326,71 @@ static int push_session_merge(OpDevice &d, const hsg_op_config &cfg, const Progr
   return rc;
 }
 
+// bucket replay (hsg_session.h): key-hash partition with the records'
+// arrival indices, per bucket sub-buckets grouped by key in LDS and replayed
+// one key per thread, the state after each record at its arrival index, the
+// changelog written in arrival order. false in *done when a sub-bucket holds
+// more than kBrCap records (a hot key): nothing was touched, the sort-based
+// replay runs the batch.
+static int push_session_bucket(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
+                               const Batch &kb, const int64_t *seq, PushResult &r, bool &done, std::string &err) {
+  done = false;
+  const uint64_t n = kb.n;
+  SessParams sp;
+  sp.gap = cfg.gap_ms;
+  sp.rec_base = a.rec_base;
+  sp.batch_id = a.batch_id;
+  sp.emit_mode = cfg.emit_mode;
+  const int words = br_words(cfg.n_cols);
+  SessPart pt = sess_part(d, words, true);
+  const uint64_t tiles = part_tiles(n, kPartTileRecs);
+  // buckets of about 8 sub-buckets (k_br_replay's LDS holds kBrCap records)
+  int nl = log2u((n + 4 * kBrCap - 1) / (4 * kBrCap));
+  nl = nl < 4 ? 4 : (nl > kPartMaxLog2 ? kPartMaxLog2 : nl);
+  PartParams pp;
+  memset(&pp, 0, sizeof(pp));
+  pp.np_log2 = nl;
+  pp.tiles = tiles;
+  DTRY(hipEventRecord(d.ev_a, d.stream));
+  DTRY(hipMemsetAsync(pt.progress, 0, (1ull << nl) * 4, d.stream));
+  launch_ss_phist(d.stream, kb, nl, d.bshift, tiles, pt);
+  launch_ss_wm(d.stream, pt, tiles, a.wm_in, d.sc);
+  launch_part_offsets(d.stream, pp, d.part, d.sc);
+  launch_br_scatter(d.stream, kb, nl, d.bshift, tiles, words, pt);
+  launch_br_subhist(d.stream, d.ss, nl, d.bshift, words, pt);
+  scan_excl_u32(d.stream, pt.tkeyed, pt.toff, tiles, pt.tpartial, d.ss.meta + M_BRROWS);
+  for (int attempt = 0;; ++attempt) {
+    launch_br_replay(d.stream, kb, sp, d.ss, prog, nl, d.bshift, words, pt, seq, d.out, a.pending, d.sc);
+    DTRY(hipMemcpyAsync(d.h_meta, d.ss.meta, M_WORDS * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
+    DTRY(hipStreamSynchronize(d.stream));
+    DTRY(hipGetLastError());
+    if (d.h_meta[M_BRBIG]) return HSG_OK;  // (done stays false)
+    if (!d.h_meta[M_FAIL]) break;
+    if (attempt >= 8) {
+      err = "session arena: no room after compaction";
+      return HSG_E_OOM;
+    }
+    // regions are equal after compaction: room for the largest region's need in each
+    uint64_t need = 0;
+    for (int q = 0; q < kArenaRegions; ++q) need = d.h_meta[M_RNEED + q] > need ? d.h_meta[M_RNEED + q] : need;
+    int rc = refill_arena(d, prog, (kArenaRegions * need + 2 * n) << attempt, err);
+    if (rc != HSG_OK) return rc;
+    rc = clear_fail(d, err);
+    if (rc != HSG_OK) return rc;
+  }
+  if (cfg.emit_mode == HSG_EMIT_PER_RECORD)
+    launch_br_emit(d.stream, kb, sp, prog, pt, tiles, seq, d.out, a.pending);
+  DTRY(hipEventRecord(d.ev_b, d.stream));
+  DTRY(hipGetLastError());
+  done = true;
+  int rc = finish_session_batch(d, a.wm_in, n, r, err);
+  const uint64_t V = d.h_meta[M_BRROWS];
+  if (cfg.emit_mode == HSG_EMIT_PER_RECORD) r.out_rows = V;
+  else if (cfg.emit_mode == HSG_EMIT_PER_BATCH) r.touched = r.out_rows;
+  r.pairs = V;
+  return rc;
+}
+
 // replay path: stable sort by key slot, one thread per key replays its
 // records in arrival order
 static int push_session_replay(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
@@ -375,9 +456,22 @@ int push_session(OpDevice &d, const hsg_op_config &cfg, const Program &prog, con
   rc = ensure_keys(d, kb.n, err);
   if (rc != HSG_OK) return rc;
   // per-batch words: need, fail, touched list, groups, runs, big buckets
-  DTRY(hipMemsetAsync(d.ss.meta + M_FAIL, 0, (M_RELOC - M_FAIL + 1) * sizeof(uint64_t), d.stream));
+  DTRY(hipMemsetAsync(d.ss.meta + M_FAIL, 0, (M_BRROWS - M_FAIL + 1) * sizeof(uint64_t), d.stream));
   DTRY(hipMemsetAsync(d.ss.meta + M_RNEED, 0, kArenaRegions * sizeof(uint64_t), d.stream));
-  rc = d.ss_merge ? push_session_merge(d, cfg, prog, a, kb, r, err) : push_session_replay(d, cfg, prog, a, kb, seq, r, err);
+  if (d.ss_merge) {
+    rc = push_session_merge(d, cfg, prog, a, kb, r, err);
+  } else {
+    // HSG_SS_SORT_REPLAY=1: every batch on the sort-based replay (tests, A/B)
+    static const bool sort_replay = getenv("HSG_SS_SORT_REPLAY") != nullptr;
+    bool done = false;
+    if (!sort_replay) rc = push_session_bucket(d, cfg, prog, a, kb, seq, r, done, err);
+    if (rc == HSG_OK && !done) {
+      d.replays += sort_replay ? 0 : 1;
+      DTRY(hipMemsetAsync(d.ss.meta + M_FAIL, 0, (M_BRROWS - M_FAIL + 1) * sizeof(uint64_t), d.stream));
+      rc = clear_batch_scalars(d, err);
+      if (rc == HSG_OK) rc = push_session_replay(d, cfg, prog, a, kb, seq, r, err);
+    }
+  }
   if (d.ss_merge) r.pairs = kb.n;  // keyed records (HSG_KEY_NONE are counted too; stats only)
   d.ss_keys = d.h_meta[M_KEYS];
   float ms = 0;

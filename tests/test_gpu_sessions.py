@@ -137,3 +137,37 @@ def test_many_columns_merge_path(eng, ncols):
             key = np.where((np.arange(key.size) % 3 == 0) & (key != abi.HSG_KEY_NONE), np.uint32(7), key)
         batches.append((key.astype(np.uint32), ts, cols, valid))
     _drive(eng, spec, batches, faithful=False)
+
+
+@pytest.mark.parametrize("mode", [abi.HSG_EMIT_PER_RECORD, abi.HSG_EMIT_PER_BATCH], ids=["changes", "per_batch_last"])
+@pytest.mark.parametrize("gap", [0, 700, 20_000])
+def test_bucket_replay(eng, mode, gap):
+    """The bucket replay (EMIT CHANGES, LAST): records partitioned by key hash
+    with their arrival indices, grouped by key per sub-bucket in LDS, each
+    key's records replayed in arrival order (findSessions / merge, Store.hs
+    :243-272, SessionWindowedStream.hs:84-118), the changelog written in
+    arrival order from the per-record states. Out-of-order records, records
+    that merge several sessions, absent fields, HSG_KEY_NONE; per batch with
+    a passthrough column (LAST: the session's own record order decides)."""
+    aggs = ALL_AGG_SETS["mixed"] if mode == abi.HSG_EMIT_PER_RECORD else \
+        [(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0), (abi.HSG_LAST, 1), (abi.HSG_MAX, 1)]
+    spec = OpSpec(abi.HSG_SESSION, mode, gap_ms=gap, col_types=[abi.HSG_I64, abi.HSG_F64], aggs=aggs)
+    batches = [gen_small(610 + bi, 150_000, 20_000, col_types=spec.col_types, span=300_000,
+                         base=9_000_000 + bi * 200_000) for bi in range(4)]
+    st = _drive(eng, spec, batches, faithful=False)
+    assert st["replays"] == 0, st  # no sub-bucket over the LDS capacity: every batch took the bucket replay
+
+
+@pytest.mark.parametrize("mode", [abi.HSG_EMIT_PER_RECORD, abi.HSG_EMIT_PER_BATCH], ids=["changes", "per_batch_last"])
+def test_bucket_replay_hot_key_falls_back(eng, mode):
+    """A key with more records in one batch than a bucket-replay sub-bucket
+    holds (kBrCap = 1024): the batch is flagged before any state changes and
+    runs on the sort-based replay instead; batches without one go back to
+    the bucket replay. Same results either way."""
+    aggs = ALL_AGG_SETS["mixed"] if mode == abi.HSG_EMIT_PER_RECORD else \
+        [(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0), (abi.HSG_LAST, 0)]
+    spec = OpSpec(abi.HSG_SESSION, mode, gap_ms=400, col_types=[abi.HSG_I64, abi.HSG_F64], aggs=aggs)
+    batches = _hot_batches(31, 60_000, nb=2)
+    batches.insert(1, gen_small(700, 60_000, 5_000, col_types=spec.col_types, span=200_000, base=20_100_000))
+    st = _drive(eng, spec, batches, faithful=False)
+    assert st["replays"] == 2, st
