@@ -2286,10 +2286,11 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
     }
     __syncthreads();
     // 5. replay: one thread per key, its records in arrival order against its list
+    const bool mir = prog.n_slots <= kSessMirrorSlots;
     for (uint32_t g = threadIdx.x; g < ngrp; g += kBrNT) {
       const uint32_t ks = L.tkey[g];
       if (ks == ~0u) continue;
-      const SessKey e = ss_load_entry(&t.kt[ks]);
+      SessKey e = ss_load_entry(&t.kt[ks]);
       uint64_t off = e.off, len = e.len;
       uint32_t lcap = e.cap;
       if (L.tcnt[g]) {
@@ -2298,6 +2299,14 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
         off = noff;
         lcap = ss_grow_cap(len + L.gcnt[g]);
       }
+      // the list's last session in registers (the entry's mirror, <= 2 slots):
+      // a record at or after its start can reach no other session (the one
+      // before ends more than gap before it), so it either merges into the
+      // last session or follows it, without reading the list
+      bool lv = mir && e.mvalid && len > 0;
+      int64_t ls = e.ms, le = e.me, la[MS];
+#pragma unroll
+      for (int s = 0; s < MS; ++s) la[s] = s < kSessMirrorSlots ? e.ma[s] : 0;
       const uint32_t st = L.gstart[g], c = L.gcnt[g];
       for (uint32_t x = st; x < st + c; ++x) {
         const uint32_t q = L.ord[x];
@@ -2307,41 +2316,72 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
         const uint64_t seq1 = (seq ? (uint64_t)seq[i] : p.rec_base + i) + 1;
         const int64_t lo = (int64_t)((uint64_t)ts - (uint64_t)p.gap);
         const int64_t hi = (int64_t)((uint64_t)ts + (uint64_t)p.gap);
-        // first session with end >= lo (ends ascend: sessions are disjoint)
-        uint64_t a = 0, z = len;
-        while (a < z) {
-          const uint64_t mid = (a + z) >> 1;
-          if ((int64_t)ss_row(t, off + mid)[1] < lo) a = mid + 1;
-          else z = mid;
-        }
-        const uint64_t i0 = a;
-        uint64_t i1 = i0;
-        while (i1 < len && (int64_t)ss_row(t, off + i1)[0] <= hi) ++i1;
         // aggF initialValue r, then mergeF acc cur over the overlapped sessions
         int64_t acc[MS], ev[MS];
         identity_row<MS>(prog, acc);
         br_elem<MS>(prog, rec, seq1, ev);
         combine_row<MS>(prog, acc, ev);
         int64_t ss = ts, se = ts;
-        for (uint64_t k = i0; k < i1; ++k) {
-          const uint64_t *row = ss_row(t, off + k);
-          const int64_t cs = (int64_t)row[0], ce = (int64_t)row[1];
-          ss = cs < ss ? cs : ss;
-          se = ce > se ? ce : se;
-          int64_t cur[MS];
-          ss_load<MS>(t, off + k, cur);
-          merge_row<MS>(prog, acc, cur);
+        if (lv && ts >= ls) {
+          if (le >= lo) {  // overlaps the last session: merged into it
+            merge_row<MS>(prog, acc, la);
+            ss = ls;
+            se = le > ts ? le : ts;
+            ss_store<MS>(t, off + len - 1, ss, se, p.batch_id, acc);
+          } else {  // a new last session
+            ss_store<MS>(t, off + len, ss, se, p.batch_id, acc);
+            len += 1;
+            live_delta += 1;
+          }
+          ls = ss;
+          le = se;
+#pragma unroll
+          for (int s = 0; s < MS; ++s) la[s] = acc[s];
+        } else {
+          // first session with end >= lo (ends ascend: sessions are disjoint)
+          uint64_t a = 0, z = len;
+          while (a < z) {
+            const uint64_t mid = (a + z) >> 1;
+            if ((int64_t)ss_row(t, off + mid)[1] < lo) a = mid + 1;
+            else z = mid;
+          }
+          const uint64_t i0 = a;
+          uint64_t i1 = i0;
+          while (i1 < len && (int64_t)ss_row(t, off + i1)[0] <= hi) ++i1;
+          for (uint64_t k = i0; k < i1; ++k) {
+            const uint64_t *row = ss_row(t, off + k);
+            const int64_t cs = (int64_t)row[0], ce = (int64_t)row[1];
+            ss = cs < ss ? cs : ss;
+            se = ce > se ? ce : se;
+            int64_t cur[MS];
+            ss_load<MS>(t, off + k, cur);
+            merge_row<MS>(prog, acc, cur);
+          }
+          const uint64_t mc = i1 - i0;
+          if (mc == 0) {
+            for (uint64_t k = len; k > i0; --k) ss_copy(t, off + k, t, off + k - 1);
+            len += 1;
+          } else if (mc > 1) {
+            for (uint64_t k = i1; k < len; ++k) ss_copy(t, off + k - (mc - 1), t, off + k);
+            len -= mc - 1;
+          }
+          live_delta += 1 - (int64_t)mc;
+          ss_store<MS>(t, off + i0, ss, se, p.batch_id, acc);
+          if (mir) {  // the last session again
+            if (i0 + 1 == len) {
+              ls = ss;
+              le = se;
+#pragma unroll
+              for (int s = 0; s < MS; ++s) la[s] = acc[s];
+            } else {
+              const uint64_t *row = ss_row(t, off + len - 1);
+              ls = (int64_t)row[0];
+              le = (int64_t)row[1];
+              ss_load<MS>(t, off + len - 1, la);
+            }
+            lv = true;
+          }
         }
-        const uint64_t mc = i1 - i0;
-        if (mc == 0) {
-          for (uint64_t k = len; k > i0; --k) ss_copy(t, off + k, t, off + k - 1);
-          len += 1;
-        } else if (mc > 1) {
-          for (uint64_t k = i1; k < len; ++k) ss_copy(t, off + k - (mc - 1), t, off + k);
-          len -= mc - 1;
-        }
-        live_delta += 1 - (int64_t)mc;
-        ss_store<MS>(t, off + i0, ss, se, p.batch_id, acc);
         int64_t *f = sp.fin + (uint64_t)i * fs;
         f[0] = ss;
         f[1] = se;
@@ -2349,10 +2389,15 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
         for (int s = 0; s < MS; ++s)
           if (s < prog.n_slots) f[2 + s] = acc[s];
       }
-      t.kt[ks].off = off;
-      t.kt[ks].len = (uint32_t)len;
-      t.kt[ks].cap = lcap;
-      t.kt[ks].mvalid = 0;  // the replay keeps no mirror of the last session
+      e.off = off;
+      e.len = (uint32_t)len;
+      e.cap = lcap;
+      e.mvalid = lv && len > 0 ? 1u : 0u;
+      e.ms = ls;
+      e.me = le;
+      e.ma[0] = MS > 0 ? la[0] : 0;
+      e.ma[1] = MS > 1 ? la[1] : 0;
+      ss_store_entry(&t.kt[ks], e);
     }
     // per-batch changelog (LAST / literal forms per batch): the keys' sessions stamped by this batch
     if (p.emit_mode == HSG_EMIT_PER_BATCH) {

@@ -151,7 +151,10 @@ int session_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &pr
   DTRY(hipMalloc((void **)&t.meta, M_WORDS * sizeof(uint64_t)));
   DTRY(hipHostMalloc((void **)&d.h_meta, M_WORDS * sizeof(uint64_t), hipHostMallocDefault));
   DTRY(hipHostMalloc((void **)&d.h_regions, kArenaRegions * kRegionStride * sizeof(uint64_t), hipHostMallocDefault));
-  d.ss_merge = cfg.emit_mode != HSG_EMIT_PER_RECORD && !has_last(prog) && !prog_has_forms(prog) && prog.n_slots <= 8;
+  // HSG_SS_REPLAY_ALL=1: per-batch / state-only ops on the bucket replay too (A/B)
+  static const bool replay_all = getenv("HSG_SS_REPLAY_ALL") != nullptr;
+  d.ss_merge = cfg.emit_mode != HSG_EMIT_PER_RECORD && !has_last(prog) && !prog_has_forms(prog) &&
+               prog.n_slots <= 8 && !replay_all;
   rc = part_device_init(d, cfg, prog, err);
   if (rc != HSG_OK) return rc;
   if (d.ss_merge) {
