@@ -107,6 +107,9 @@ struct OpDevice {
   // time windows
   TwTable tw = {};
   uint64_t cap = 0;             // table slots (regions; tw.slots() adds the overflow rows)
+  uint32_t load8 = 6;           // the table's load limit in eighths: 3/4, and 1/2 for hopping
+                                // tables, whose window-block probes grow long past it (the
+                                // room checks and growth, op_device.cpp / retention.cpp)
   uint64_t ovf_rows = 0;        // groups in the overflow rows (a region was full): the next batch
                                 // first rebuilds the table with twice the slots and larger regions
   int region_log2 = 12;         // log2 of the smallest region (raised by each overflow rebuild)

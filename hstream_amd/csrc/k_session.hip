@@ -2010,7 +2010,7 @@ void launch_ss_dump(hipStream_t s, const SessTable &t, const Program &prog, OutC
 // ---------------------------------------------------------------------------
 // Bucket replay (hsg_session.h): per-record changelog, LAST, literal forms.
 // ---------------------------------------------------------------------------
-constexpr int kBrNT = 256;
+constexpr int kBrNT = 512;
 constexpr int kBrTab = 2 * kBrCap;  // LDS key table entries (load <= 1/2)
 constexpr int kBrMaxSubLog2 = 6;
 constexpr int kBrSubNT = 256;
@@ -2123,21 +2123,26 @@ __device__ inline void br_elem(const Program &prog, const uint64_t *rec, uint64_
   }
 }
 
+// LDS of k_br_replay. CW: words of each record cached here (its word 0, ts
+// and columns, for records of <= 5 words), so the replay reads no record
+// from HBM; wider records are read from the bucket (L2).
+template <int W>
 struct BrLds {
-  uint32_t tkey[kBrTab];  // key table; after the grouping: the group's key-table slot
-  uint32_t tcnt[kBrTab];  // records per key; after the grouping: the key's group, then the group's fresh rows
+  static constexpr int CW = W <= 5 ? W - 1 : 0;
+  uint32_t tkey[kBrTab];  // key table
+  uint32_t tcnt[kBrTab];  // records per key; after the grouping: the key's group
   uint32_t rpos[kBrCap];  // record -> its position in sp.srec
   uint32_t ridx[kBrCap];  // record -> its arrival index
-  uint16_t rtab[kBrCap];  // record -> its key's table entry
+  uint16_t rtab[kBrCap];  // record -> its key's table entry, then its group
   uint16_t seg[kBrCap];   // records placed by group
   uint16_t ord[kBrCap];   // records placed by group, in arrival order within a group
   uint32_t gkey[kBrCap];
   uint16_t gstart[kBrCap];
   uint16_t gcnt[kBrCap];
   uint32_t gcur[kBrCap];
-  uint32_t wsum[kBrNT / 64];
+  uint64_t rw[CW ? kBrCap * CW : 1];
   uint64_t wsum64[kBrNT / 64];
-  uint32_t ngrp, nrec;
+  uint32_t ngrp;
   uint64_t abase;
   uint32_t fail;
 };
@@ -2146,7 +2151,8 @@ template <int MS, int W>
 __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, SessTable t, Program prog, int np_log2,
                                                      int bshift, SessPart sp, const int64_t *seq, OutCols out,
                                                      uint64_t out_base, DevScalars *sc) {
-  __shared__ BrLds L;
+  __shared__ BrLds<W> L;
+  constexpr int CW = BrLds<W>::CW;
   if (t.meta[M_BRBIG] || t.meta[M_FAIL]) return;  // uniform: the other replay runs / the arena is refilled first
   const uint32_t bk = blockIdx.x;
   const uint64_t r0 = sp.bstart[bk], m = sp.bstart[bk + 1] - r0;
@@ -2154,8 +2160,23 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t fs = 2 + (uint32_t)prog.n_slots;
   const uint32_t region = arena_region(bk);
+  const bool mir = prog.n_slots <= kSessMirrorSlots;
   int64_t live_delta = 0;
   uint64_t inserted = 0;
+  // block-wide exclusive scan of one value per thread (every thread calls)
+  auto block_excl = [&](uint64_t v, uint64_t &total) -> uint64_t {
+    const uint64_t incl = wave_incl_sum(v);
+    __syncthreads();
+    if (lane == 63) L.wsum64[w] = incl;
+    __syncthreads();
+    uint64_t pre = incl - v;
+    total = 0;
+    for (int k = 0; k < kBrNT / 64; ++k) {
+      pre += k < w ? L.wsum64[k] : 0;
+      total += L.wsum64[k];
+    }
+    return pre;
+  };
   for (int sub = (int)sp.progress[bk]; sub < nsub; ++sub) {
     const uint32_t s0 = sp.subst[bk * 65ull + sub], cnt = sp.subst[bk * 65ull + sub + 1] - s0;
     // 1. group the sub-bucket's records by key (LDS hash table)
@@ -2163,15 +2184,16 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       L.tkey[i] = kSessEmptyKey;
       L.tcnt[i] = 0;
     }
-    if (threadIdx.x == 0) {
-      L.ngrp = 0;
-      L.fail = 0;
-    }
+    if (threadIdx.x == 0) L.fail = 0;
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < cnt; q += kBrNT) {
       const uint32_t pos = sp.bperm[r0 + s0 + q];
       const uint64_t *rec = sp.srec + (uint64_t)pos * W;
       const uint32_t key = (uint32_t)rec[0];
+      L.ridx[q] = (uint32_t)rec[W - 1];
+      L.rpos[q] = pos;
+#pragma unroll
+      for (int k = 0; k < CW; ++k) L.rw[q * CW + k] = rec[k];
       uint32_t h = (uint32_t)key_hash(key) & (kBrTab - 1);
       for (;;) {
         const uint32_t old = atomicCAS(&L.tkey[h], kSessEmptyKey, key);
@@ -2179,8 +2201,6 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
         h = (h + 1) & (kBrTab - 1);
       }
       atomicAdd(&L.tcnt[h], 1u);
-      L.rpos[q] = pos;
-      L.ridx[q] = (uint32_t)rec[W - 1];
       L.rtab[q] = (uint16_t)h;
     }
     __syncthreads();
@@ -2194,12 +2214,8 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
         nz += c[k] ? 1u : 0u;
         tot += c[k];
       }
-      const uint64_t packed = ((uint64_t)nz << 32) | tot;
-      const uint64_t incl = wave_incl_sum(packed);
-      if (lane == 63) L.wsum64[w] = incl;
-      __syncthreads();
-      uint64_t pre = incl - packed;
-      for (int k = 0; k < w; ++k) pre += L.wsum64[k];
+      uint64_t all;
+      const uint64_t pre = block_excl(((uint64_t)nz << 32) | tot, all);
       uint32_t g = (uint32_t)(pre >> 32), at = (uint32_t)pre;
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
@@ -2213,7 +2229,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
         ++g;
         at += c[k];
       }
-      if (threadIdx.x == kBrNT - 1) L.ngrp = g;
+      if (threadIdx.x == 0) L.ngrp = (uint32_t)(all >> 32);
     }
     __syncthreads();
     const uint32_t ngrp = L.ngrp;
@@ -2221,7 +2237,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
     for (uint32_t q = threadIdx.x; q < cnt; q += kBrNT) {
       const uint32_t g = L.tcnt[L.rtab[q]];
       L.seg[L.gstart[g] + atomicAdd(&L.gcur[g], 1u)] = (uint16_t)q;
-      L.rtab[q] = (uint16_t)g;  // (now: the record's group)
+      L.rtab[q] = (uint16_t)g;
     }
     __syncthreads();
     for (uint32_t x = threadIdx.x; x < cnt; x += kBrNT) {
@@ -2230,87 +2246,74 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       for (uint32_t y = st; y < st + c; ++y) rank += L.ridx[L.seg[y]] < me ? 1u : 0u;
       L.ord[st + rank] = (uint16_t)q;
     }
-    // 4. every group's key-table entry; the fresh list rows the sub-bucket needs
+    // 4. every group's key-table entry (rounds of kBrNT groups, one per
+    //    thread), the fresh list rows it needs; one arena reservation for the
+    //    sub-bucket before anything is written (L.tkey[g]: the entry's slot,
+    //    L.gcur[g]: the group's fresh rows' offset in the reservation)
+    SessKey E;  // the entry of this thread's group in the last round (one round: all of them)
     uint64_t need = 0;
-    for (uint32_t g = threadIdx.x; g < ngrp; g += kBrNT) {
-      bool ins = false;
-      const int64_t ks = ss_find_or_insert(t, L.gkey[g], ins);
-      inserted += ins ? 1u : 0u;
+    for (uint32_t g0 = 0; g0 < ngrp; g0 += kBrNT) {
+      const uint32_t g = g0 + threadIdx.x;
       uint32_t nc = 0;
-      if (ks < 0) {
-        atomicOr(&sc->err, ERR_OOM);
-      } else {
-        const SessKey e = ss_load_entry(&t.kt[ks]);
-        const uint64_t want = (uint64_t)e.len + L.gcnt[g];
-        nc = want > e.cap ? ss_grow_cap(want) : 0u;
+      if (g < ngrp) {
+        bool ins = false;
+        const int64_t ks = ss_find_or_insert(t, L.gkey[g], ins);
+        inserted += ins ? 1u : 0u;
+        if (ks < 0) {
+          atomicOr(&sc->err, ERR_OOM);
+        } else {
+          E = ss_load_entry(&t.kt[ks]);
+          const uint64_t want = (uint64_t)E.len + L.gcnt[g];
+          nc = want > E.cap ? ss_grow_cap(want) : 0u;
+        }
+        L.tkey[g] = ks < 0 ? ~0u : (uint32_t)ks;
       }
-      L.tkey[g] = ks < 0 ? ~0u : (uint32_t)ks;
-      L.tcnt[g] = nc;
-      need += nc;
+      uint64_t tot;
+      const uint64_t pre = block_excl(nc, tot);
+      if (g < ngrp) L.gcur[g] = (uint32_t)(need + pre);
+      need += tot;
     }
-    const uint64_t wneed = wave_sum_u64(need);
-    if (lane == 0) L.wsum64[w] = wneed;
-    __syncthreads();
     if (threadIdx.x == 0) {
-      uint64_t tot = 0;
-      for (int k = 0; k < kBrNT / 64; ++k) tot += L.wsum64[k];
       uint64_t base = 0;
-      if (tot && !arena_take(t, region, tot, base)) {
-        // no room: this sub-bucket (and the rest of the bucket) runs again after
-        // the host compacts / grows the arena (sp.progress resumes it here)
+      if (need && !arena_take(t, region, need, base)) {
+        // no room: nothing of this sub-bucket is written; it (and the rest of
+        // the bucket) runs again after the host compacts / grows the arena
+        // (sp.progress resumes it here)
         L.fail = 1;
         t.meta[M_FAIL] = 1;
-        atomicAdd((unsigned long long *)&t.meta[M_RNEED + region], (unsigned long long)tot);
+        atomicAdd((unsigned long long *)&t.meta[M_RNEED + region], (unsigned long long)need);
       }
       L.abase = base;
     }
     __syncthreads();
     if (L.fail) break;
-    // fresh-list offsets: exclusive scan of the groups' fresh rows (group order)
-    {
-      const uint32_t per = (ngrp + kBrNT - 1) / kBrNT;
-      const uint32_t g0 = threadIdx.x * per, g1 = g0 + per < ngrp ? g0 + per : ngrp;
-      uint64_t loc = 0;
-      for (uint32_t g = g0; g < g1; ++g) loc += L.tcnt[g];
-      const uint64_t incl = wave_incl_sum(loc);
-      __syncthreads();
-      if (lane == 63) L.wsum64[w] = incl;
-      __syncthreads();
-      uint64_t run = incl - loc;
-      for (int k = 0; k < w; ++k) run += L.wsum64[k];
-      for (uint32_t g = g0; g < g1; ++g) {
-        const uint32_t nc = L.tcnt[g];
-        L.tcnt[g] = nc ? (uint32_t)run + 1u : 0u;  // (row offset + 1 within the reservation; 0: in place)
-        run += nc;
-      }
-    }
-    __syncthreads();
     // 5. replay: one thread per key, its records in arrival order against its list
-    const bool mir = prog.n_slots <= kSessMirrorSlots;
-    for (uint32_t g = threadIdx.x; g < ngrp; g += kBrNT) {
+    for (uint32_t g0 = 0; g0 < ngrp; g0 += kBrNT) {
+      const uint32_t g = g0 + threadIdx.x;
+      if (g >= ngrp || L.tkey[g] == ~0u) continue;
       const uint32_t ks = L.tkey[g];
-      if (ks == ~0u) continue;
-      SessKey e = ss_load_entry(&t.kt[ks]);
-      uint64_t off = e.off, len = e.len;
-      uint32_t lcap = e.cap;
-      if (L.tcnt[g]) {
-        const uint64_t noff = L.abase + L.tcnt[g] - 1;
+      if (ngrp > kBrNT) E = ss_load_entry(&t.kt[ks]);
+      uint64_t off = E.off, len = E.len;
+      uint32_t lcap = E.cap;
+      const uint64_t want = len + L.gcnt[g];
+      if (want > lcap) {
+        const uint64_t noff = L.abase + L.gcur[g];
         for (uint64_t k = 0; k < len; ++k) ss_copy(t, noff + k, t, off + k);
         off = noff;
-        lcap = ss_grow_cap(len + L.gcnt[g]);
+        lcap = ss_grow_cap(want);
       }
       // the list's last session in registers (the entry's mirror, <= 2 slots):
       // a record at or after its start can reach no other session (the one
       // before ends more than gap before it), so it either merges into the
       // last session or follows it, without reading the list
-      bool lv = mir && e.mvalid && len > 0;
-      int64_t ls = e.ms, le = e.me, la[MS];
+      bool lv = mir && E.mvalid && len > 0;
+      int64_t ls = E.ms, le = E.me, la[MS];
 #pragma unroll
-      for (int s = 0; s < MS; ++s) la[s] = s < kSessMirrorSlots ? e.ma[s] : 0;
+      for (int s = 0; s < MS; ++s) la[s] = s < kSessMirrorSlots ? E.ma[s] : 0;
       const uint32_t st = L.gstart[g], c = L.gcnt[g];
       for (uint32_t x = st; x < st + c; ++x) {
         const uint32_t q = L.ord[x];
-        const uint64_t *rec = sp.srec + (uint64_t)L.rpos[q] * W;
+        const uint64_t *rec = CW ? &L.rw[q * CW] : sp.srec + (uint64_t)L.rpos[q] * W;
         const uint32_t i = L.ridx[q];
         const int64_t ts = (int64_t)rec[1];
         const uint64_t seq1 = (seq ? (uint64_t)seq[i] : p.rec_base + i) + 1;
@@ -2389,50 +2392,51 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
         for (int s = 0; s < MS; ++s)
           if (s < prog.n_slots) f[2 + s] = acc[s];
       }
-      e.off = off;
-      e.len = (uint32_t)len;
-      e.cap = lcap;
-      e.mvalid = lv && len > 0 ? 1u : 0u;
-      e.ms = ls;
-      e.me = le;
-      e.ma[0] = MS > 0 ? la[0] : 0;
-      e.ma[1] = MS > 1 ? la[1] : 0;
-      ss_store_entry(&t.kt[ks], e);
+      E.off = off;
+      E.len = (uint32_t)len;
+      E.cap = lcap;
+      E.mvalid = lv && len > 0 ? 1u : 0u;
+      E.ms = ls;
+      E.me = le;
+      E.ma[0] = MS > 0 ? la[0] : 0;
+      E.ma[1] = MS > 1 ? la[1] : 0;
+      ss_store_entry(&t.kt[ks], E);
     }
     // per-batch changelog (LAST / literal forms per batch): the keys' sessions stamped by this batch
     if (p.emit_mode == HSG_EMIT_PER_BATCH) {
-      uint64_t mine = 0;
-      for (uint32_t g = threadIdx.x; g < ngrp; g += kBrNT) {
-        if (L.tkey[g] == ~0u) continue;
-        const SessKey e = ss_load_entry(&t.kt[L.tkey[g]]);
-        for (uint64_t k = 0; k < e.len; ++k) mine += (uint32_t)ss_row(t, e.off + k)[2] == p.batch_id;
-      }
-      const uint64_t incl = wave_incl_sum(mine);
-      __syncthreads();
-      if (lane == 63) L.wsum64[w] = incl;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        uint64_t tot = 0;
-        for (int k = 0; k < kBrNT / 64; ++k) tot += L.wsum64[k];
-        L.abase = tot ? atomicAdd((unsigned long long *)&sc->out_rows, (unsigned long long)tot) : 0;
-        if (tot) atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)tot);
-      }
-      __syncthreads();
-      uint64_t o = out_base + L.abase + incl - mine;
-      for (int k = 0; k < w; ++k) o += L.wsum64[k];
-      for (uint32_t g = threadIdx.x; g < ngrp && mine; g += kBrNT) {
-        if (L.tkey[g] == ~0u) continue;
-        const SessKey e = ss_load_entry(&t.kt[L.tkey[g]]);
-        for (uint64_t k = 0; k < e.len; ++k) {
-          const uint64_t *row = ss_row(t, e.off + k);
-          if ((uint32_t)row[2] != p.batch_id) continue;
-          out.key[o] = e.key;
-          out.ws[o] = (int64_t)row[0];
-          out.we[o] = (int64_t)row[1];
-          out.src[o] = -1;
-          for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, (const int64_t *)row + 3);
-          if (out.form) out.form[o] = out_form(prog, (const int64_t *)row + 3);
-          ++o;
+      for (uint32_t g0 = 0; g0 < ngrp; g0 += kBrNT) {
+        const uint32_t g = g0 + threadIdx.x;
+        int64_t ks = -1;
+        SessKey E;
+        uint64_t mine = 0;
+        if (g < ngrp) {
+          bool ins = false;
+          ks = ss_find_or_insert(t, L.gkey[g], ins);  // (found: inserted above)
+          if (ks >= 0) {
+            E = ss_load_entry(&t.kt[ks]);
+            for (uint64_t k = 0; k < E.len; ++k) mine += (uint32_t)ss_row(t, E.off + k)[2] == p.batch_id;
+          }
+        }
+        uint64_t tot;
+        const uint64_t pre = block_excl(mine, tot);
+        if (threadIdx.x == 0) {
+          L.abase = tot ? atomicAdd((unsigned long long *)&sc->out_rows, (unsigned long long)tot) : 0;
+          if (tot) atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)tot);
+        }
+        __syncthreads();
+        uint64_t o = out_base + L.abase + pre;
+        if (mine) {
+          for (uint64_t k = 0; k < E.len; ++k) {
+            const uint64_t *row = ss_row(t, E.off + k);
+            if ((uint32_t)row[2] != p.batch_id) continue;
+            out.key[o] = E.key;
+            out.ws[o] = (int64_t)row[0];
+            out.we[o] = (int64_t)row[1];
+            out.src[o] = -1;
+            for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, (const int64_t *)row + 3);
+            if (out.form) out.form[o] = out_form(prog, (const int64_t *)row + 3);
+            ++o;
+          }
         }
       }
     }

@@ -271,6 +271,10 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
   }
   uint64_t rows = cfg.state_capacity ? cfg.state_capacity : (1ull << 21);
   d.cap = next_pow2(rows * 2);  // load factor <= 1/2
+  // hopping: a key's windows share its 8-row blocks, probed in steps of 8
+  // rows; past 1/2 load those chains dominate k_seg_apply (C3 at 71 %: 1.49
+  // ms per batch against 1.07 ms at 36 %), and 288 GB of HBM holds the rows
+  d.load8 = cfg.window_kind == HSG_HOPPING ? 4 : 6;
   if (cfg.window_kind == HSG_SESSION) {
     int rc = session_device_init(d, cfg, prog, rows, err);
     if (rc != HSG_OK) return rc;
@@ -732,7 +736,7 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       pp.chunk = kAggChunk;
       pp.big = d.agg_big ? 1 : 0;
       pp.defer = 1;
-      const uint64_t lim = d.cap - d.cap / 4;
+      const uint64_t lim = d.cap / 8 * d.load8;
       pp.room = lim > d.h_sc->live ? lim - d.h_sc->live : 0;
       pp.hold = !defer_sized && kb.n * d.wpr > pp.room ? 1 : 0;
       last_pp = pp;
@@ -808,7 +812,7 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     DTRY(hipMemcpyAsync(d.sc, d.h_sc, sizeof(DevScalars), hipMemcpyHostToDevice, d.stream));
     d.sc_clean = false;
     PartParams pp = last_pp;
-    const uint64_t lim = d.cap - d.cap / 4;
+    const uint64_t lim = d.cap / 8 * d.load8;
     pp.room = lim > keep.live ? lim - keep.live : 0;  // >= bound (tw_maintain)
     const bool emit_batch = cfg.emit_mode == HSG_EMIT_PER_BATCH;
     DTRY(hipEventRecord(d.ev_a, d.stream));

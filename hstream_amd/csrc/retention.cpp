@@ -127,7 +127,7 @@ int tw_maintain(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint
   const uint64_t bound = n_in * d.wpr < groups_bound ? n_in * d.wpr : groups_bound;
   // a region was full (overflow rows in use): rebuild with larger regions
   const bool widen = d.ovf_rows != 0;
-  if (!reopen && !widen && 4 * (live + bound) <= 3 * d.cap) return HSG_OK;
+  if (!reopen && !widen && 8 * (live + bound) <= (uint64_t)d.load8 * d.cap) return HSG_OK;
   wait_table_reset(d);
   const TwParams p = retention_params(cfg, wm_in);
   // small pinned block for the counters read back here
