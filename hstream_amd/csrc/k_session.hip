@@ -2143,7 +2143,7 @@ struct BrLds {
   uint64_t rw[CW ? kBrCap * CW : 1];
   uint64_t wsum64[kBrNT / 64];
   uint32_t ngrp;
-  uint64_t abase;
+  uint64_t abase, rbase;
   uint32_t fail;
 };
 
@@ -2289,18 +2289,27 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
     if (L.fail) break;
     // 5. replay: one thread per key, its records in arrival order against its list
     for (uint32_t g0 = 0; g0 < ngrp; g0 += kBrNT) {
-      const uint32_t g = g0 + threadIdx.x;
-      if (g >= ngrp || L.tkey[g] == ~0u) continue;
+    const uint32_t g = g0 + threadIdx.x;
+    uint64_t rl_src = 0, rl_dst = 0, rl_n = 0;  // this thread's moved list, if any
+    if (g < ngrp && L.tkey[g] != ~0u) {
       const uint32_t ks = L.tkey[g];
       if (ngrp > kBrNT) E = ss_load_entry(&t.kt[ks]);
       uint64_t off = E.off, len = E.len;
       uint32_t lcap = E.cap;
       const uint64_t want = len + L.gcnt[g];
+      // a list that outgrows its rows moves to fresh rows; its rows are not
+      // copied by this thread (a row-by-row copy holds the whole wave, and
+      // ~1 key in 8 per C4 batch moves) unless the slow path needs to read
+      // them: rows [0, pfx) -- those no record rewrote -- are listed for
+      // k_ss_reloc_copy after the kernel
+      const uint64_t old_off = off;
+      uint64_t pfx = 0;
+      bool pending = false;
       if (want > lcap) {
-        const uint64_t noff = L.abase + L.gcur[g];
-        for (uint64_t k = 0; k < len; ++k) ss_copy(t, noff + k, t, off + k);
-        off = noff;
+        off = L.abase + L.gcur[g];
         lcap = ss_grow_cap(want);
+        pfx = len;
+        pending = len > 0;
       }
       // the list's last session in registers (the entry's mirror, <= 2 slots):
       // a record at or after its start can reach no other session (the one
@@ -2331,6 +2340,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
             ss = ls;
             se = le > ts ? le : ts;
             ss_store<MS>(t, off + len - 1, ss, se, p.batch_id, acc);
+            pfx = len - 1 < pfx ? len - 1 : pfx;
           } else {  // a new last session
             ss_store<MS>(t, off + len, ss, se, p.batch_id, acc);
             len += 1;
@@ -2341,6 +2351,10 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
 #pragma unroll
           for (int s = 0; s < MS; ++s) la[s] = acc[s];
         } else {
+          if (pending) {  // the list is read from here on: its moved rows first
+            for (uint64_t k = 0; k < pfx; ++k) ss_copy(t, off + k, t, old_off + k);
+            pending = false;
+          }
           // first session with end >= lo (ends ascend: sessions are disjoint)
           uint64_t a = 0, z = len;
           while (a < z) {
@@ -2401,6 +2415,26 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       E.ma[0] = MS > 0 ? la[0] : 0;
       E.ma[1] = MS > 1 ? la[1] : 0;
       ss_store_entry(&t.kt[ks], E);
+      if (pending && pfx) {
+        rl_src = old_off;
+        rl_dst = off;
+        rl_n = pfx;
+      }
+    }
+    // the moved lists' prefixes to copy: one counter update per round
+    {
+      uint64_t rtot;
+      const uint64_t rpre = block_excl(rl_n ? 1u : 0u, rtot);
+      if (threadIdx.x == 0) L.rbase = rtot ? atomicAdd((unsigned long long *)&t.meta[M_RELOC], rtot) : 0;
+      __syncthreads();
+      if (rl_n) {
+        uint64_t *r = sp.reloc + 3 * (L.rbase + rpre);
+        r[0] = rl_src;
+        r[1] = rl_dst;
+        r[2] = rl_n;
+      }
+      __syncthreads();
+    }
     }
     // per-batch changelog (LAST / literal forms per batch): the keys' sessions stamped by this batch
     if (p.emit_mode == HSG_EMIT_PER_BATCH) {

@@ -107,6 +107,7 @@ static uint64_t ss_part_layout(uint64_t n, int words, SessPart *sp, char *m, boo
     x.tpartial = (uint64_t *)take((scan_partials_needed(tiles) + 8) * 8);
     x.subst = (uint32_t *)take(nb * 65 * 4);
     x.bperm = (uint32_t *)take(n * 4);
+    x.reloc = (uint64_t *)take(n * 24);
   } else {
     x.bigmask = (uint64_t *)take(nb * 8);
     x.touched = (uint32_t *)take(n * 4);
@@ -368,6 +369,12 @@ static int push_session_bucket(OpDevice &d, const hsg_op_config &cfg, const Prog
     DTRY(hipStreamSynchronize(d.stream));
     DTRY(hipGetLastError());
     if (d.h_meta[M_BRBIG]) return HSG_OK;  // (done stays false)
+    // the moved lists' prefixes (listed by the sub-buckets that ran), before
+    // anything else reads those lists: the next batch or a compaction
+    if (d.h_meta[M_RELOC]) {
+      launch_ss_reloc_copy(d.stream, d.ss, pt, n);
+      DTRY(hipMemsetAsync(d.ss.meta + M_RELOC, 0, sizeof(uint64_t), d.stream));
+    }
     if (!d.h_meta[M_FAIL]) break;
     if (attempt >= 8) {
       err = "session arena: no room after compaction";
