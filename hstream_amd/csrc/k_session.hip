@@ -2291,6 +2291,9 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
     for (uint32_t g0 = 0; g0 < ngrp; g0 += kBrNT) {
     const uint32_t g = g0 + threadIdx.x;
     uint64_t rl_src = 0, rl_dst = 0, rl_n = 0;  // this thread's moved list, if any
+    uint32_t emitted = 0;                         // sessions of the key this batch stamped
+    uint64_t klen = 0, koff = 0;
+    uint32_t kkey = 0;
     if (g < ngrp && L.tkey[g] != ~0u) {
       const uint32_t ks = L.tkey[g];
       if (ngrp > kBrNT) E = ss_load_entry(&t.kt[ks]);
@@ -2316,6 +2319,8 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       // before ends more than gap before it), so it either merges into the
       // last session or follows it, without reading the list
       bool lv = mir && E.mvalid && len > 0;
+      bool lst = false;  // the list's last session carries this batch's stamp (no session of the key
+                         // does before its records: one thread replays a key once per batch)
       int64_t ls = E.ms, le = E.me, la[MS];
 #pragma unroll
       for (int s = 0; s < MS; ++s) la[s] = s < kSessMirrorSlots ? E.ma[s] : 0;
@@ -2341,11 +2346,14 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
             se = le > ts ? le : ts;
             ss_store<MS>(t, off + len - 1, ss, se, p.batch_id, acc);
             pfx = len - 1 < pfx ? len - 1 : pfx;
+            emitted += lst ? 0u : 1u;
           } else {  // a new last session
             ss_store<MS>(t, off + len, ss, se, p.batch_id, acc);
             len += 1;
             live_delta += 1;
+            emitted += 1;
           }
+          lst = true;
           ls = ss;
           le = se;
 #pragma unroll
@@ -2365,16 +2373,19 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
           const uint64_t i0 = a;
           uint64_t i1 = i0;
           while (i1 < len && (int64_t)ss_row(t, off + i1)[0] <= hi) ++i1;
+          uint32_t sm = 0;  // merged sessions already stamped by this batch
           for (uint64_t k = i0; k < i1; ++k) {
             const uint64_t *row = ss_row(t, off + k);
             const int64_t cs = (int64_t)row[0], ce = (int64_t)row[1];
             ss = cs < ss ? cs : ss;
             se = ce > se ? ce : se;
+            sm += (uint32_t)row[2] == p.batch_id ? 1u : 0u;
             int64_t cur[MS];
             ss_load<MS>(t, off + k, cur);
             merge_row<MS>(prog, acc, cur);
           }
           const uint64_t mc = i1 - i0;
+          const bool to_end = i1 == len;  // the merged stretch reaches the last session
           if (mc == 0) {
             for (uint64_t k = len; k > i0; --k) ss_copy(t, off + k, t, off + k - 1);
             len += 1;
@@ -2384,6 +2395,8 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
           }
           live_delta += 1 - (int64_t)mc;
           ss_store<MS>(t, off + i0, ss, se, p.batch_id, acc);
+          emitted += 1u - sm;
+          if (to_end) lst = true;
           if (mir) {  // the last session again
             if (i0 + 1 == len) {
               ls = ss;
@@ -2415,6 +2428,9 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       E.ma[0] = MS > 0 ? la[0] : 0;
       E.ma[1] = MS > 1 ? la[1] : 0;
       ss_store_entry(&t.kt[ks], E);
+      klen = len;
+      koff = off;
+      kkey = E.key;
       if (pending && pfx) {
         rl_src = old_off;
         rl_dst = off;
@@ -2435,44 +2451,35 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       }
       __syncthreads();
     }
-    }
-    // per-batch changelog (LAST / literal forms per batch): the keys' sessions stamped by this batch
+    // per-batch changelog (LAST / literal forms, or every op with
+    // HSG_SS_REPLAY_ALL): the key's sessions this batch stamped, found from
+    // the end of its list (near-sorted arrivals stamp only its last ones;
+    // rows the slow path shifted were copied first, so every row read here
+    // is the kernel's or was in place)
     if (p.emit_mode == HSG_EMIT_PER_BATCH) {
-      for (uint32_t g0 = 0; g0 < ngrp; g0 += kBrNT) {
-        const uint32_t g = g0 + threadIdx.x;
-        int64_t ks = -1;
-        SessKey E;
-        uint64_t mine = 0;
-        if (g < ngrp) {
-          bool ins = false;
-          ks = ss_find_or_insert(t, L.gkey[g], ins);  // (found: inserted above)
-          if (ks >= 0) {
-            E = ss_load_entry(&t.kt[ks]);
-            for (uint64_t k = 0; k < E.len; ++k) mine += (uint32_t)ss_row(t, E.off + k)[2] == p.batch_id;
-          }
-        }
-        uint64_t tot;
-        const uint64_t pre = block_excl(mine, tot);
-        if (threadIdx.x == 0) {
-          L.abase = tot ? atomicAdd((unsigned long long *)&sc->out_rows, (unsigned long long)tot) : 0;
-          if (tot) atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)tot);
-        }
-        __syncthreads();
-        uint64_t o = out_base + L.abase + pre;
-        if (mine) {
-          for (uint64_t k = 0; k < E.len; ++k) {
-            const uint64_t *row = ss_row(t, E.off + k);
-            if ((uint32_t)row[2] != p.batch_id) continue;
-            out.key[o] = E.key;
-            out.ws[o] = (int64_t)row[0];
-            out.we[o] = (int64_t)row[1];
-            out.src[o] = -1;
-            for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, (const int64_t *)row + 3);
-            if (out.form) out.form[o] = out_form(prog, (const int64_t *)row + 3);
-            ++o;
-          }
-        }
+      uint64_t tot;
+      const uint64_t pre = block_excl(emitted, tot);
+      if (threadIdx.x == 0) {
+        L.rbase = tot ? atomicAdd((unsigned long long *)&sc->out_rows, (unsigned long long)tot) : 0;
+        if (tot) atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)tot);
       }
+      __syncthreads();
+      uint64_t o = out_base + L.rbase + pre;
+      uint32_t left = emitted;
+      for (uint64_t k = klen; k > 0 && left; --k) {
+        const uint64_t *row = ss_row(t, koff + k - 1);
+        if ((uint32_t)row[2] != p.batch_id) continue;
+        out.key[o] = kkey;
+        out.ws[o] = (int64_t)row[0];
+        out.we[o] = (int64_t)row[1];
+        out.src[o] = -1;
+        for (int j = 0; j < prog.n_out; ++j) out.agg[j][o] = out_value(prog, j, (const int64_t *)row + 3);
+        if (out.form) out.form[o] = out_form(prog, (const int64_t *)row + 3);
+        ++o;
+        --left;
+      }
+      __syncthreads();
+    }
     }
     __syncthreads();
     if (threadIdx.x == 0) sp.progress[bk] = (uint32_t)(sub + 1);
