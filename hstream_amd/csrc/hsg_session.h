@@ -100,14 +100,13 @@ struct SessPart {
   uint32_t *groups;    // [n][4] key groups: key, first record in srec, records, -
   uint8_t *done;       // [n / 256 + 1] apply blocks done (resumable)
   uint64_t *bigmask;   // [nb] sub-buckets left to k_ss_merge_big
-  uint64_t *scopy;     // [n][words] per bucket: its records grouped by sub-bucket (k_ss_sort)
+  uint64_t *scopy;     // [n][words] per bucket: its records grouped by sub-bucket (k_ss_sort, k_br_subhist)
   uint32_t *gsparse;   // [n][4] group records at their sub-bucket's record positions
   uint64_t *reloc;     // [n][3] relocated lists (old row, new row, rows of the prefix to copy)
   // bucket replay (per-record changelog, LAST, literal forms)
   uint32_t *tkeyed;    // [tiles] keyed records of each arrival tile (k_ss_phist)
   uint64_t *toff;      // [tiles + 1] exclusive prefix: the tile's first changelog row
   uint32_t *subst;     // [nb][65] each bucket's sub-bucket starts (k_br_subhist)
-  uint32_t *bperm;     // [n] record positions grouped by sub-bucket within each bucket
   int64_t *fin;        // [n][2 + n_slots] per arrival index: session start, end, state after the record
   uint64_t *tpartial;  // scan partials over the tiles
 };

@@ -2044,11 +2044,13 @@ void launch_br_scatter(hipStream_t s, const Batch &b, int np_log2, int bshift, u
   }
 }
 
-// Per bucket: its records' positions grouped by sub-bucket (sp.bperm, within
-// the bucket's own range) and the sub-bucket starts (sp.subst[b][0 .. 2^sl]);
-// a sub-bucket of more than kBrCap records flags the batch (M_BRBIG) before
+// Per bucket: its records grouped by sub-bucket (copied into sp.scopy over
+// the bucket's own range, so each sub-bucket pass of k_br_replay reads one
+// contiguous stretch) and the sub-bucket starts (sp.subst[b][0 .. 2^sl]); a
+// sub-bucket of more than kBrCap records flags the batch (M_BRBIG) before
 // any state is touched.
-__global__ __launch_bounds__(kBrSubNT) void k_br_subhist(SessTable t, int np_log2, int bshift, int W, SessPart sp) {
+template <int W>
+__global__ __launch_bounds__(kBrSubNT) void k_br_subhist(SessTable t, int np_log2, int bshift, SessPart sp) {
   __shared__ uint32_t cnt[1 << kBrMaxSubLog2];
   __shared__ uint32_t cur[1 << kBrMaxSubLog2];
   const uint32_t b = blockIdx.x;
@@ -2075,14 +2077,30 @@ __global__ __launch_bounds__(kBrSubNT) void k_br_subhist(SessTable t, int np_log
   }
   __syncthreads();
   for (uint64_t q = threadIdx.x; q < m; q += kBrSubNT) {
-    const uint32_t key = (uint32_t)sp.srec[(r0 + q) * W];
-    const uint32_t at = atomicAdd(&cur[ss_sub(key, hs, sl)], 1u);
-    sp.bperm[r0 + at] = (uint32_t)(r0 + q);
+    const uint64_t *src = sp.srec + (r0 + q) * W;
+    uint64_t v[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) v[k] = src[k];
+    const uint32_t at = atomicAdd(&cur[ss_sub((uint32_t)v[0], hs, sl)], 1u);
+    uint64_t *dst = sp.scopy + (r0 + at) * W;
+#pragma unroll
+    for (int k = 0; k < W; ++k) dst[k] = v[k];
   }
 }
 
 void launch_br_subhist(hipStream_t s, const SessTable &t, int np_log2, int bshift, int words, const SessPart &sp) {
-  hipLaunchKernelGGL(k_br_subhist, dim3(1u << np_log2), dim3(kBrSubNT), 0, s, t, np_log2, bshift, words, sp);
+  const dim3 g(1u << np_log2), th(kBrSubNT);
+  switch (words) {
+    case 3: hipLaunchKernelGGL(k_br_subhist<3>, g, th, 0, s, t, np_log2, bshift, sp); break;
+    case 4: hipLaunchKernelGGL(k_br_subhist<4>, g, th, 0, s, t, np_log2, bshift, sp); break;
+    case 5: hipLaunchKernelGGL(k_br_subhist<5>, g, th, 0, s, t, np_log2, bshift, sp); break;
+    case 6: hipLaunchKernelGGL(k_br_subhist<6>, g, th, 0, s, t, np_log2, bshift, sp); break;
+    case 7: hipLaunchKernelGGL(k_br_subhist<7>, g, th, 0, s, t, np_log2, bshift, sp); break;
+    case 8: hipLaunchKernelGGL(k_br_subhist<8>, g, th, 0, s, t, np_log2, bshift, sp); break;
+    case 9: hipLaunchKernelGGL(k_br_subhist<9>, g, th, 0, s, t, np_log2, bshift, sp); break;
+    case 10: hipLaunchKernelGGL(k_br_subhist<10>, g, th, 0, s, t, np_log2, bshift, sp); break;
+    default: hipLaunchKernelGGL(k_br_subhist<11>, g, th, 0, s, t, np_log2, bshift, sp); break;
+  }
 }
 
 // contribution of a bucket-replay record (present bits 32..39, literal-form
@@ -2187,8 +2205,8 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
     if (threadIdx.x == 0) L.fail = 0;
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < cnt; q += kBrNT) {
-      const uint32_t pos = sp.bperm[r0 + s0 + q];
-      const uint64_t *rec = sp.srec + (uint64_t)pos * W;
+      const uint32_t pos = (uint32_t)(r0 + s0 + q);
+      const uint64_t *rec = sp.scopy + (uint64_t)pos * W;
       const uint32_t key = (uint32_t)rec[0];
       L.ridx[q] = (uint32_t)rec[W - 1];
       L.rpos[q] = pos;
@@ -2327,7 +2345,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       const uint32_t st = L.gstart[g], c = L.gcnt[g];
       for (uint32_t x = st; x < st + c; ++x) {
         const uint32_t q = L.ord[x];
-        const uint64_t *rec = CW ? &L.rw[q * CW] : sp.srec + (uint64_t)L.rpos[q] * W;
+        const uint64_t *rec = CW ? &L.rw[q * CW] : sp.scopy + (uint64_t)L.rpos[q] * W;
         const uint32_t i = L.ridx[q];
         const int64_t ts = (int64_t)rec[1];
         const uint64_t seq1 = (seq ? (uint64_t)seq[i] : p.rec_base + i) + 1;

@@ -106,7 +106,7 @@ static uint64_t ss_part_layout(uint64_t n, int words, SessPart *sp, char *m, boo
     x.toff = (uint64_t *)take((tiles + 1) * 8);
     x.tpartial = (uint64_t *)take((scan_partials_needed(tiles) + 8) * 8);
     x.subst = (uint32_t *)take(nb * 65 * 4);
-    x.bperm = (uint32_t *)take(n * 4);
+    x.scopy = (uint64_t *)take(n * (uint64_t)words * 8);
     x.reloc = (uint64_t *)take(n * 24);
   } else {
     x.bigmask = (uint64_t *)take(nb * 8);
