@@ -218,6 +218,7 @@ EXPORTED_SYMBOLS = [
 # testing knobs (hsg_testing_set_knob)
 HSG_KNOB_XPART_LOG2 = 1
 HSG_KNOB_SESS_ARENA_MIN = 2
+HSG_KNOB_X_CLASSIC = 3
 
 
 # Every symbol include/hstream_ingest.h declares (host ingest, no GPU needed).

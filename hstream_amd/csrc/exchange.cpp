@@ -61,7 +61,9 @@ int exchange_device_init(OpDevice &d, const hsg_op_config &cfg, uint64_t batch_c
   d.x = x;
   const int G = d.nranks;
   const uint64_t n = batch_cap;
-  const uint64_t max_words = 2 + cfg.n_cols + 2;
+  // packed records of the classic path (key, ts, columns, seq, wm), or the
+  // columnar buffers of the fast / sequenced paths (+ valid bytes)
+  const uint64_t max_words = 2 + cfg.n_cols + 3;
   x->batch = n;
   DTRY(hipMalloc((void **)&x->owner, n * 4 + 4));
   DTRY(hipMalloc((void **)&x->idx, n * 4 + 4));
@@ -73,8 +75,8 @@ int exchange_device_init(OpDevice &d, const hsg_op_config &cfg, uint64_t batch_c
   DTRY(hipMalloc((void **)&x->info_all, (uint64_t)G * info_words(G) * 8));
   DTRY(hipHostMalloc((void **)&x->h_info, (uint64_t)G * info_words(G) * 8, hipHostMallocDefault));
   DTRY(hipMalloc((void **)&x->wm_local, n * 8 + 8));
-  DTRY(hipMalloc((void **)&x->send, n * max_words * 8 + 8));
-  DTRY(hipMalloc((void **)&x->recv, (uint64_t)G * n * max_words * 8 + 8));
+  DTRY(hipMalloc((void **)&x->send, n * max_words * 8 + 65536));
+  DTRY(hipMalloc((void **)&x->recv, (uint64_t)G * n * max_words * 8 + 65536));
   DTRY(hipMalloc((void **)&d.st_seq, (uint64_t)G * n * 8 + 8));
   DTRY(hipMalloc((void **)&d.st_wm, (uint64_t)G * n * 8 + 8));
   if (!d.h_tmp) DTRY(hipHostMalloc((void **)&d.h_tmp, 8 * sizeof(uint64_t), hipHostMallocDefault));
@@ -86,6 +88,7 @@ int exchange_device_init(OpDevice &d, const hsg_op_config &cfg, uint64_t batch_c
     const int64_t v = testing_knob(HSG_KNOB_XPART_LOG2);
     if (G == 1 && v >= 0 && v <= 6) d.xpart_log2 = (int)v;
   }
+  d.x_classic = testing_knob(HSG_KNOB_X_CLASSIC) > 0;
   d.bshift = d.xpart_log2 > 0 ? d.xpart_log2 : 0;
   if (d.bshift + kPartMaxLog2 > 60) d.bshift = 0;
   d.tw.bshift = d.bshift;  // table regions follow the local buckets
@@ -268,6 +271,9 @@ static int push_sharded_fast(OpDevice &d, const hsg_op_config &cfg, const Progra
 static int push_sharded_classic(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
                                 PushResult &r, std::string &err);
 
+static int push_sharded_seq(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
+                            PushResult &r, std::string &err);
+
 int push_sharded(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, PushResult &r,
                  std::string &err) {
   bool need_seq = cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.window_kind == HSG_SESSION;
@@ -277,7 +283,178 @@ int push_sharded(OpDevice &d, const hsg_op_config &cfg, const Program &prog, con
     int rc = push_sharded_fast(d, cfg, prog, a, r, err, fallback);
     if (rc != HSG_OK || !fallback) return rc;
   }
+  // (HSG_KNOB_X_CLASSIC: the packed classic exchange even where the
+  // sequenced columnar one applies; tests, A/B)
+  if (d.xpart_log2 >= 0 && d.part_mem && !d.x_classic) return push_sharded_seq(d, cfg, prog, a, r, err);
   return push_sharded_classic(d, cfg, prog, a, r, err);
+}
+
+// Sequenced exchange (per-record changelog, LAST, sessions, literal forms,
+// or a batch with late records; power-of-two ranks): the fast path's owner
+// partition and columnar all-to-all-v, with a stable scatter (each owner's
+// records in arrival order) that also sends every record's global sequence
+// number and, when some record may be late, its stream time. Rank slices
+// arrive in rank order, so the received columns are the owned records in
+// global arrival order: the single-GPU kernels give the single-stream result.
+// No radix sort, no packing, no unpack.
+static int push_sharded_seq(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,
+                            PushResult &r, std::string &err) {
+  XBuffers &x = *d.x;
+  const int G = a.nranks, me = a.rank;
+  const int IW = info_words(G);
+  const int xl = d.xpart_log2;
+  Comm *comm = a.comm;
+  hipStream_t s = d.stream;
+  if (a.batch->n > x.batch) {
+    err = "batch larger than batch_capacity";
+    return HSG_E_CAPACITY;
+  }
+  Batch kb;
+  int rc = stage_batch(d, a.batch, kb, err, a.staged_set);
+  if (rc != HSG_OK) return rc;
+  bool has_valid = false;
+  for (int c = 0; c < cfg.n_cols; ++c) has_valid = has_valid || kb.valid[c] != nullptr;
+  // records of every ts travel for sessions / unwindowed ops; for time
+  // windows a record before 0 has no window (windowsFor) and only moves
+  // stream time, which the all-gathered maxima carry
+  const bool all_ts = cfg.window_kind == HSG_SESSION || cfg.window_kind == HSG_UNWINDOWED;
+  const uint64_t n = kb.n;
+  DTRY(hipEventRecord(d.ev_c, s));
+  rc = clear_batch_scalars(d, err);
+  if (rc != HSG_OK) return rc;
+  // 1. owner counts per tile (+ ts extrema), owner-major run offsets, facts
+  launch_x_hist(s, kb, xl, all_ts, d.part.hist, d.part.text, d.sc);
+  PartParams xp;
+  memset(&xp, 0, sizeof(xp));
+  xp.np_log2 = xl;
+  xp.tiles = x_tiles(n);
+  launch_part_offsets(s, xp, d.part, d.sc);
+  launch_x_info(s, d.sc, d.part.bstart, xl, (uint32_t)G, n, has_valid, x.info, d.part.text, x_tiles(n));
+  // 2. all-gather the per-rank facts
+  rc = comm_allgather(comm, x.info, x.info_all, IW, ncclInt64, 8, s, err);
+  if (rc != HSG_OK) return rc;
+  DTRY(hipMemcpyAsync(x.h_info, x.info_all, (uint64_t)G * IW * 8, hipMemcpyDeviceToHost, s));
+  DTRY(hipStreamSynchronize(s));
+  const int64_t *H = x.h_info;
+  int64_t wm_global = a.wm_in, carry = a.wm_in, min_ts = INT64_MAX;
+  uint64_t seq_base = a.rec_base, total = 0;
+  bool any_valid = false;
+  for (int q = 0; q < G; ++q) {
+    const int64_t *I = H + (uint64_t)q * IW;
+    if (I[2] > 0) {
+      wm_global = I[0] > wm_global ? I[0] : wm_global;
+      if (q < me) carry = I[0] > carry ? I[0] : carry;
+      min_ts = I[1] < min_ts ? I[1] : min_ts;
+    }
+    if (q < me) seq_base += (uint64_t)I[2];
+    total += (uint64_t)I[2];
+    any_valid = any_valid || I[3] != 0;
+  }
+  const bool time_win = cfg.window_kind == HSG_TUMBLING || cfg.window_kind == HSG_HOPPING;
+  const bool may_be_late =
+      time_win && min_ts != INT64_MAX && wm_global > (int64_t)((uint64_t)min_ts + (uint64_t)cfg.grace_ms);
+  // per-record stream time in the global order (rare): tile maxima, their
+  // prefix seeded with the lower ranks' maxima, the inclusive scan per tile
+  if (may_be_late) {
+    const uint64_t tiles = (n + kTileRecords - 1) / kTileRecords;
+    launch_tile_stats(s, kb, d.tile_max, d.tile_min, tiles);
+    launch_tile_scan(s, d.tile_max, d.tile_min, d.tile_prefix, tiles, carry, 1, false, d.sc);
+    launch_x_recwm(s, kb, d.tile_prefix, x.wm_local);
+  }
+  // 3. stable columnar scatter by owner, one all-to-all-v per column
+  std::vector<size_t> scount(G), sdispl(G), rcount(G), rdispl(G);
+  uint64_t so = 0, ro = 0;
+  for (int q = 0; q < G; ++q) {
+    scount[q] = (size_t)H[(uint64_t)me * IW + 4 + q];
+    sdispl[q] = so;
+    so += scount[q];
+    rcount[q] = (size_t)H[(uint64_t)q * IW + 4 + me];
+    rdispl[q] = ro;
+    ro += rcount[q];
+  }
+  if (ro > d.batch_cap) {
+    err = "received more records than the op's capacity";
+    return HSG_E_CAPACITY;
+  }
+  const int C = cfg.n_cols;
+  auto carve = [&](void *base, uint64_t cap) {
+    XCols c;
+    memset(&c, 0, sizeof(c));
+    char *p = (char *)base;
+    auto take = [&](uint64_t bytes) {
+      char *q = p;
+      p += (bytes + 255) & ~255ull;
+      return q;
+    };
+    c.ts = (int64_t *)take(cap * 8);
+    for (int k = 0; k < C; ++k) c.col[k] = (int64_t *)take(cap * 8);
+    c.seq = (int64_t *)take(cap * 8);
+    c.wm = (int64_t *)take(cap * 8);
+    c.key = (uint32_t *)take(cap * 4);
+    for (int k = 0; k < C; ++k) c.valid[k] = (uint8_t *)take(cap);
+    return c;
+  };
+  const XCols snd = carve(x.send, x.batch), rcv = carve(x.recv, (uint64_t)G * x.batch);
+  launch_x_scatter_seq(s, kb, xl, all_ts, any_valid, C, d.part.offt, snd, seq_base,
+                       may_be_late ? x.wm_local : nullptr);
+  const size_t self_n = scount[me];
+  scount[me] = 0;
+  rcount[me] = 0;
+  XCols src = rcv;
+  if (G == 1) {
+    src = snd;
+  } else if (self_n) {
+    const size_t so_me = sdispl[me], ro_me = rdispl[me];
+    DTRY(hipMemcpyAsync(rcv.key + ro_me, snd.key + so_me, self_n * 4, hipMemcpyDeviceToDevice, s));
+    DTRY(hipMemcpyAsync(rcv.ts + ro_me, snd.ts + so_me, self_n * 8, hipMemcpyDeviceToDevice, s));
+    DTRY(hipMemcpyAsync(rcv.seq + ro_me, snd.seq + so_me, self_n * 8, hipMemcpyDeviceToDevice, s));
+    if (may_be_late) DTRY(hipMemcpyAsync(rcv.wm + ro_me, snd.wm + so_me, self_n * 8, hipMemcpyDeviceToDevice, s));
+    for (int k = 0; k < C; ++k) {
+      DTRY(hipMemcpyAsync(rcv.col[k] + ro_me, snd.col[k] + so_me, self_n * 8, hipMemcpyDeviceToDevice, s));
+      if (any_valid) DTRY(hipMemcpyAsync(rcv.valid[k] + ro_me, snd.valid[k] + so_me, self_n, hipMemcpyDeviceToDevice, s));
+    }
+  }
+  if (G > 1) {
+#define XA2A(buf, dt, el)                                                                              \
+  do {                                                                                                  \
+    rc = comm_alltoallv(comm, snd.buf, scount.data(), sdispl.data(), rcv.buf, rcount.data(), rdispl.data(), \
+                        dt, el, s, err);                                                                \
+    if (rc != HSG_OK) return rc;                                                                        \
+  } while (0)
+    if ((rc = comm_group_start(comm, err)) != HSG_OK) return rc;
+    XA2A(key, ncclUint32, 4);
+    XA2A(ts, ncclInt64, 8);
+    XA2A(seq, ncclInt64, 8);
+    if (may_be_late) XA2A(wm, ncclInt64, 8);
+    for (int k = 0; k < C; ++k) {
+      XA2A(col[k], ncclInt64, 8);
+      if (any_valid) XA2A(valid[k], ncclUint8, 1);
+    }
+    if ((rc = comm_group_end(comm, err)) != HSG_OK) return rc;
+#undef XA2A
+  }
+  DTRY(hipEventRecord(d.ev_d, s));
+  DTRY(hipGetLastError());
+  // 4. aggregate the owned records, in global arrival order
+  Batch rb;
+  memset(&rb, 0, sizeof(rb));
+  rb.n = ro;
+  rb.key = src.key;
+  rb.ts = src.ts;
+  for (int k = 0; k < C; ++k) {
+    rb.col[k] = src.col[k];
+    rb.valid[k] = any_valid ? src.valid[k] : nullptr;
+  }
+  PushArgs la = a;
+  la.wm_in = carry;  // any value <= the records' stream times keeps grace exact
+  rc = push_local(d, cfg, prog, la, rb, src.seq, may_be_late ? src.wm : nullptr, r, err);
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, d.ev_c, d.ev_d) == hipSuccess) r.exchange_ms = ms;
+  r.exchange_bytes = (uint64_t)(so - self_n) * (20 + 8 * C + (any_valid ? C : 0) + (may_be_late ? 8 : 0));
+  r.wm_out = wm_global;
+  r.owned = ro;
+  r.global_records = total;
+  return rc;
 }
 
 static int push_sharded_classic(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a,

@@ -217,13 +217,14 @@ extern "C" void hsg_engine_destroy(hsg_engine *e) {
 extern "C" const char *hsg_engine_last_error(const hsg_engine *e) { return e ? e->err.c_str() : "null engine"; }
 
 // testing knobs (include/hstream_gpu.h): process-wide, read at op creation
-static std::atomic<int64_t> g_knob_xpart{-1}, g_knob_arena{0};
+static std::atomic<int64_t> g_knob_xpart{-1}, g_knob_arena{0}, g_knob_xclassic{0};
 
 namespace hsg {
 int64_t testing_knob(int knob) {
   switch (knob) {
     case HSG_KNOB_XPART_LOG2: return g_knob_xpart.load();
     case HSG_KNOB_SESS_ARENA_MIN: return g_knob_arena.load();
+    case HSG_KNOB_X_CLASSIC: return g_knob_xclassic.load();
     default: return 0;
   }
 }
@@ -238,6 +239,10 @@ extern "C" int hsg_testing_set_knob(int32_t knob, int64_t value) {
     case HSG_KNOB_SESS_ARENA_MIN:
       if (value < 0) return HSG_E_INVALID;
       g_knob_arena.store(value);
+      return HSG_OK;
+    case HSG_KNOB_X_CLASSIC:
+      if (value < 0 || value > 1) return HSG_E_INVALID;
+      g_knob_xclassic.store(value);
       return HSG_OK;
     default: return HSG_E_INVALID;
   }

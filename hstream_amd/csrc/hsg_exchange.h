@@ -70,6 +70,8 @@ struct XCols {
   int64_t *ts;
   int64_t *col[kMaxCols];
   uint8_t *valid[kMaxCols];
+  int64_t *seq;  // sequenced exchange: the record's global arrival index (null: not sent)
+  int64_t *wm;   // sequenced exchange with late records: its stream time (null: not sent)
 };
 
 uint64_t x_tiles(uint64_t n);
@@ -79,6 +81,12 @@ void launch_x_info(hipStream_t s, DevScalars *sc, const uint64_t *bstart, int xl
                    bool has_valid, int64_t *info, const uint64_t *text, uint64_t tiles);
 void launch_x_scatter(hipStream_t s, const Batch &b, int xl, bool unwin, bool write_valid, int ncols,
                       const uint32_t *offt, const XCols &send);
+// the sequenced exchange's scatter: stable (each owner's records in arrival
+// order), with the global sequence (seq_base + index) and, when wm is given,
+// each record's stream time; all_ts: records of every ts travel (sessions,
+// unwindowed), else only ts >= 0 (time windows: the others have no window)
+void launch_x_scatter_seq(hipStream_t s, const Batch &b, int xl, bool all_ts, bool write_valid, int ncols,
+                          const uint32_t *offt, const XCols &send, uint64_t seq_base, const int64_t *wm);
 
 void launch_x_minmax(hipStream_t s, const int64_t *tmax, const int64_t *tmin, uint64_t n_tiles, uint64_t n,
                      int has_valid, int64_t *info);

@@ -124,6 +124,7 @@ struct OpDevice {
   int pane_S = 1;               // panes per window (0: one LDS entry per window)
   int bshift = 0;               // key-hash bits that pick the owner GPU (skipped by local buckets)
   int xpart_log2 = -1;          // owner partition of the fast exchange: log2(ranks), -1 = not a power of two
+  bool x_classic = false;       // HSG_KNOB_X_CLASSIC: sequenced batches take the packed classic exchange
   bool agg_big = true;          // aggregation variant of the next batch (big LDS table)
   bool pred_packed = false;     // launch prediction: the last batch was packed (wide variants not launched)
   bool pred_direct = false;     // launch prediction: the last batch's changelog came from the lean apply

@@ -240,6 +240,78 @@ __global__ __launch_bounds__(kXNT) void k_x_scatter(Batch b, int xl, int unwin, 
   }
 }
 
+// Stable variant (the sequenced exchange): records in arrival order (round r,
+// thread t) keep that order within each owner's run. Per round, a record's
+// place = the owner's records of earlier rounds (cnt) + of earlier waves in
+// this round (wcnt prefix) + of lower lanes of its wave (ballot match on the
+// owner bits); one wave-count table, three barriers per round.
+__global__ __launch_bounds__(kXNT) void k_x_scatter_seq(Batch b, int xl, int all_ts, int write_valid, int ncols,
+                                                        const uint32_t *offt, XCols send, uint64_t seq_base,
+                                                        const int64_t *wm) {
+  constexpr int NW = kXNT / 64;
+  __shared__ uint32_t cnt[kMaxRanks];
+  __shared__ uint32_t goff[kMaxRanks];
+  __shared__ uint32_t wcnt[NW][kMaxRanks];
+  const uint32_t P = 1u << xl;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint32_t o = threadIdx.x; o < P; o += kXNT) {
+    cnt[o] = 0;
+    goff[o] = offt[blockIdx.x * (uint64_t)P + o];
+  }
+  const uint64_t base = (uint64_t)blockIdx.x * kXT;
+  const uint64_t below = (1ull << lane) - 1ull;
+  for (int r = 0; r < kXT / kXNT; ++r) {
+    for (uint32_t k = threadIdx.x; k < (uint32_t)NW * P; k += kXNT) wcnt[k / P][k % P] = 0;
+    __syncthreads();
+    const uint64_t i = base + (uint64_t)r * kXNT + threadIdx.x;
+    bool go = false;
+    uint32_t o = 0;
+    if (i < b.n) {
+      const uint32_t key = b.key[i];
+      go = key != HSG_KEY_NONE && (all_ts || b.ts[i] >= 0);
+      if (go) o = owner_of(key, P, xl);
+    }
+    // lanes of this wave with the same owner
+    uint64_t peers = __ballot(go);
+    for (int bit = 0; bit < xl; ++bit) {
+      const uint64_t m = __ballot(go && ((o >> bit) & 1u));
+      peers &= ((o >> bit) & 1u) ? m : ~m;
+    }
+    const uint32_t rk = (uint32_t)__popcll(peers & below);
+    if (go && rk == 0) wcnt[w][o] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (go) {
+      uint32_t pre = cnt[o];
+      for (int k = 0; k < w; ++k) pre += wcnt[k][o];
+      const uint64_t d = (uint64_t)goff[o] + pre + rk;
+      send.key[d] = b.key[i];
+      send.ts[d] = b.ts[i];
+      for (int c = 0; c < ncols; ++c) {
+        send.col[c][d] = b.col[c][i];
+        // (the literal-form bit rides along: ops with literal forms use this exchange)
+        if (write_valid) send.valid[c][d] = b.valid[c] ? b.valid[c][i] : (uint8_t)1;
+      }
+      send.seq[d] = (int64_t)(seq_base + i);
+      if (wm) send.wm[d] = wm[i];
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < P; q += kXNT) {
+      uint32_t t = 0;
+      for (int k = 0; k < NW; ++k) t += wcnt[k][q];
+      cnt[q] += t;
+    }
+    __syncthreads();  // (the next round clears wcnt)
+  }
+}
+
+void launch_x_scatter_seq(hipStream_t s, const Batch &b, int xl, bool all_ts, bool write_valid, int ncols,
+                          const uint32_t *offt, const XCols &send, uint64_t seq_base, const int64_t *wm) {
+  const uint64_t tiles = x_tiles(b.n);
+  if (tiles)
+    hipLaunchKernelGGL(k_x_scatter_seq, dim3((unsigned)tiles), dim3(kXNT), 0, s, b, xl, all_ts ? 1 : 0,
+                       write_valid ? 1 : 0, ncols, offt, send, seq_base, wm);
+}
+
 uint64_t x_tiles(uint64_t n) { return (n + kXT - 1) / kXT; }
 
 void launch_x_hist(hipStream_t s, const Batch &b, int xl, bool unwin, uint32_t *hist, uint64_t *text, DevScalars *) {

@@ -27,9 +27,13 @@ __device__ inline bool arena_take(const SessTable &t, uint32_t r, uint64_t n, ui
 }
 __device__ inline uint32_t arena_region(uint32_t block) { return block % kArenaRegions; }
 
+// rows reserved for a list of `need` sessions: 4, 16, 64, then doubling. A
+// list that outgrows its rows moves (its rows are copied), so short lists,
+// which grow by a session every few batches, grow 4x: C4's lists (~33
+// sessions by the end of the stream) move twice instead of four times
 __device__ inline uint32_t ss_grow_cap(uint64_t need) {
   uint32_t c = 4;
-  while (c < need) c <<= 1;
+  while (c < need) c <<= (c < 64 ? 2 : 1);
   return c;
 }
 
@@ -2010,7 +2014,7 @@ void launch_ss_dump(hipStream_t s, const SessTable &t, const Program &prog, OutC
 // ---------------------------------------------------------------------------
 // Bucket replay (hsg_session.h): per-record changelog, LAST, literal forms.
 // ---------------------------------------------------------------------------
-constexpr int kBrNT = 512;
+constexpr int kBrNT = 1024;
 constexpr int kBrTab = 2 * kBrCap;  // LDS key table entries (load <= 1/2)
 constexpr int kBrMaxSubLog2 = 6;
 constexpr int kBrSubNT = 256;

@@ -55,7 +55,7 @@ class testing_knob:
     """Context manager over hsg_testing_set_knob (tests only): the knob holds
     for ops created inside the block, then returns to its default."""
 
-    DEFAULTS = {abi.HSG_KNOB_XPART_LOG2: -1, abi.HSG_KNOB_SESS_ARENA_MIN: 0}
+    DEFAULTS = {abi.HSG_KNOB_XPART_LOG2: -1, abi.HSG_KNOB_SESS_ARENA_MIN: 0, abi.HSG_KNOB_X_CLASSIC: 0}
 
     def __init__(self, knob, value):
         self.knob, self.value = knob, value

@@ -336,6 +336,8 @@ int  hsg_op_stats(const hsg_op *op, hsg_stats *out);
 #define HSG_KNOB_XPART_LOG2     1 /* a 1-rank exchange partitions its records into 2^v owner
                                      regions, all its own (0..6); -1 = log2(ranks)          */
 #define HSG_KNOB_SESS_ARENA_MIN 2 /* floor of the session arena in rows (> 0); 0 = 2^20      */
+#define HSG_KNOB_X_CLASSIC      3 /* 1: sequenced batches of a sharded op take the packed
+                                     classic exchange instead of the columnar one            */
 int  hsg_testing_set_knob(int32_t knob, int64_t value);
 
 #ifdef __cplusplus

@@ -271,21 +271,24 @@ def _x_specs():
     return out
 
 
-@pytest.mark.parametrize("xpart", [None, "2"], ids=["xpart1", "xpart4"])
+@pytest.mark.parametrize("xpart", [None, "2", "classic"], ids=["xpart1", "xpart4", "classic"])
 @pytest.mark.parametrize("late", [False, True], ids=["no_late", "late"])
 @pytest.mark.parametrize("spec", _x_specs())
 def test_exchange_path_single_rank(xeng, spec, late, xpart):
-    """xpart4: the fast exchange partitions the single rank's records into 4
-    owner regions (testing knob HSG_KNOB_XPART_LOG2 = 2), all sent to rank 0, so
-    the multi-owner offsets and scatter run with one GPU; late batches take the
-    classic path."""
+    """xpart4: the fast and the sequenced exchanges partition the single
+    rank's records into 4 owner regions (testing knob HSG_KNOB_XPART_LOG2 =
+    2), all sent to rank 0, so the multi-owner offsets and the (stable)
+    scatters run with one GPU; late batches, per-record changelogs, LAST and
+    sessions take the sequenced exchange; classic: the packed classic
+    exchange (HSG_KNOB_X_CLASSIC) for them instead."""
     from hstream_amd.engine import testing_knob
     batches = []
     for bi in range(3):
         key, ts, cols, valid = gen_small(2000 + bi, 4000, 29, col_types=spec.col_types, span=60_000,
                                          base=5_000_000 + bi * 60_000, very_late=late)
         batches.append((key, ts, cols, valid))
-    with testing_knob(abi.HSG_KNOB_XPART_LOG2, int(xpart) if xpart else -1):
+    with testing_knob(abi.HSG_KNOB_XPART_LOG2, int(xpart) if xpart and xpart != "classic" else -1), \
+            testing_knob(abi.HSG_KNOB_X_CLASSIC, 1 if xpart == "classic" else 0):
         g = xeng.op(spec)
     o = pyoracle.OracleOp(spec)
     f64 = spec.agg_is_f64()
