@@ -11,8 +11,13 @@ Protocol per global batch (rank r ingests slice r; slices are in rank order):
   fast path (no LAST, no per-record changelog, no sessions, and no record can
   be late): one all-to-all per column of (key, ts, col..., valid...) of the
   keyed records with ts >= 0, aggregated in any order at stream time = carry;
-  classic path otherwise: all-to-all of (key, ts, cols, valid, seq[, wm]),
-  each rank aggregates its owned records in global order.
+  sequenced path otherwise: the same columnar all-to-all with two more
+  columns, each record's global sequence number and (when some record may be
+  late) its stream time, the owner partition stable (arrival order kept), of
+  the keyed records with ts >= 0 (any ts for sessions and unwindowed ops);
+  each rank aggregates its owned records in global order. (A rank count that
+  is not a power of two, or HSG_KNOB_X_CLASSIC, takes the packed classic
+  exchange: the same records and sequence numbers, one packed all-to-all.)
 The per-rank aggregation here is the oracle, so this checks the protocol's
 claims (exact stream time and sequence numbers after the exchange, disjoint
 key ownership), not the GPU kernels (tests/test_gpu_parity.py does that)."""
@@ -97,14 +102,14 @@ SPECS = {
     "hopping_fast": OpSpec(abi.HSG_HOPPING, abi.HSG_EMIT_NONE, size_ms=9_000, advance_ms=3_000,
                            col_types=[abi.HSG_I64, abi.HSG_F64],
                            aggs=[a for a in ALL_AGG_SETS["mixed"] if a[0] != abi.HSG_LAST]),
-    # no LAST but a short grace: batches whose records may be late fall back to the classic exchange
+    # no LAST but a short grace: batches whose records may be late take the sequenced exchange
     "tumbling_fast_grace": OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=10_000, grace_ms=5_000,
                                   col_types=[abi.HSG_I64, abi.HSG_F64],
                                   aggs=[a for a in ALL_AGG_SETS["mixed"] if a[0] != abi.HSG_LAST]),
 }
 # the exchange each spec takes on these batches (very late records have ts < 0: never windowed)
-PATHS = {"hopping": "classic", "tumbling_batch": "classic", "session": "classic", "tumbling_fast": "fast",
-         "hopping_fast": "fast", "tumbling_fast_grace": "classic"}
+PATHS = {"hopping": "sequenced", "tumbling_batch": "sequenced", "session": "sequenced", "tumbling_fast": "fast",
+         "hopping_fast": "fast", "tumbling_fast_grace": "sequenced"}
 
 
 def fast_eligible(spec):
@@ -174,7 +179,8 @@ def _worker(rank, G, port, spec_name, late, q):
         else:
             rec_wm = np.maximum.accumulate(np.concatenate([[carry], ts]))[1:]
             seq = seq_base + np.arange(len(ts), dtype=np.int64)
-            own = np.where(keyed, owner_of(key, G), G)
+            all_ts = spec.window_kind in (abi.HSG_SESSION, abi.HSG_UNWINDOWED)
+            own = np.where(keyed & ((ts >= 0) | all_ts), owner_of(key, G), G)
             # stable partition by owner, drop HSG_KEY_NONE
             order = np.argsort(own, kind="stable")
             order = order[own[order] < G]
@@ -193,7 +199,7 @@ def _worker(rank, G, port, spec_name, late, q):
             r_valid = [got[:, 4].astype(np.uint8), got[:, 5].astype(np.uint8)]
             op.push_ex(r_key, got[:, 1].copy(), r_cols, r_valid, watermark=carry,
                        rec_wm=got[:, 7].copy() if may_be_late else None, seq=got[:, 6].copy())
-            paths.append("classic")
+            paths.append("sequenced")
         wm = wm_global
         rec_base += total
         rows_out = op.drain() if spec.emit_mode != abi.HSG_EMIT_NONE else None
