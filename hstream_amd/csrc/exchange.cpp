@@ -302,7 +302,10 @@ static int push_sharded_seq(OpDevice &d, const hsg_op_config &cfg, const Program
   XBuffers &x = *d.x;
   const int G = a.nranks, me = a.rank;
   const int IW = info_words(G);
-  const int xl = d.xpart_log2;
+  // one owner region per rank (not the testing knob's finer partition of a
+  // single rank): a rank's received columns are then its owned records in
+  // global arrival order (rank slices in rank order, each kept stable)
+  const int xl = log2_exact((uint32_t)G);
   Comm *comm = a.comm;
   hipStream_t s = d.stream;
   if (a.batch->n > x.batch) {

@@ -275,12 +275,13 @@ def _x_specs():
 @pytest.mark.parametrize("late", [False, True], ids=["no_late", "late"])
 @pytest.mark.parametrize("spec", _x_specs())
 def test_exchange_path_single_rank(xeng, spec, late, xpart):
-    """xpart4: the fast and the sequenced exchanges partition the single
-    rank's records into 4 owner regions (testing knob HSG_KNOB_XPART_LOG2 =
-    2), all sent to rank 0, so the multi-owner offsets and the (stable)
-    scatters run with one GPU; late batches, per-record changelogs, LAST and
-    sessions take the sequenced exchange; classic: the packed classic
-    exchange (HSG_KNOB_X_CLASSIC) for them instead."""
+    """xpart4: the fast exchange partitions the single rank's records into 4
+    owner regions (testing knob HSG_KNOB_XPART_LOG2 = 2), all sent to rank 0,
+    so the multi-owner offsets and scatter run with one GPU; late batches,
+    per-record changelogs, LAST and sessions take the sequenced exchange (one
+    owner region per rank, its stable scatter: tests/test_gpu_two_ranks.py
+    runs two owners); classic: the packed classic exchange
+    (HSG_KNOB_X_CLASSIC) for them instead."""
     from hstream_amd.engine import testing_knob
     batches = []
     for bi in range(3):
