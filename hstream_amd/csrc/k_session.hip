@@ -108,6 +108,32 @@ __device__ inline int64_t ss_find_or_insert(const SessTable &t, uint32_t key, bo
   return -1;
 }
 
+// The same, loading the key's whole entry with the probe (one round trip
+// when the key sits at its home slot, the common case): the found entry, or
+// a blank one for a key this call inserted.
+__device__ inline int64_t ss_find_entry(const SessTable &t, uint32_t key, SessKey &e, bool &inserted) {
+  uint64_t s = ss_home(t, key);
+  inserted = false;
+  for (uint64_t probe = 0; probe <= t.kmask; ++probe) {
+    e = ss_load_entry(&t.kt[s]);
+    if (e.key == key) return (int64_t)s;
+    if (e.key == kSessEmptyKey) {
+      const uint32_t old = atomicCAS(&t.kt[s].key, kSessEmptyKey, key);
+      if (old == kSessEmptyKey) {
+        inserted = true;
+        e = ss_blank(key);
+        return (int64_t)s;
+      }
+      if (old == key) {
+        e = ss_load_entry(&t.kt[s]);
+        return (int64_t)s;
+      }
+    }
+    s = (s + 1) & t.kmask;
+  }
+  return -1;
+}
+
 __global__ void k_ss_rehash(SessTable from, SessTable to) {
   const uint64_t cap = from.kmask + 1;
   for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap; s += (uint64_t)gridDim.x * blockDim.x) {
@@ -2014,7 +2040,7 @@ void launch_ss_dump(hipStream_t s, const SessTable &t, const Program &prog, OutC
 // ---------------------------------------------------------------------------
 // Bucket replay (hsg_session.h): per-record changelog, LAST, literal forms.
 // ---------------------------------------------------------------------------
-constexpr int kBrNT = 1024;
+constexpr int kBrNT = 512;
 constexpr int kBrTab = 2 * kBrCap;  // LDS key table entries (load <= 1/2)
 constexpr int kBrMaxSubLog2 = 6;
 constexpr int kBrSubNT = 256;
@@ -2279,12 +2305,11 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       uint32_t nc = 0;
       if (g < ngrp) {
         bool ins = false;
-        const int64_t ks = ss_find_or_insert(t, L.gkey[g], ins);
+        const int64_t ks = ss_find_entry(t, L.gkey[g], E, ins);
         inserted += ins ? 1u : 0u;
         if (ks < 0) {
           atomicOr(&sc->err, ERR_OOM);
         } else {
-          E = ss_load_entry(&t.kt[ks]);
           const uint64_t want = (uint64_t)E.len + L.gcnt[g];
           nc = want > E.cap ? ss_grow_cap(want) : 0u;
         }

@@ -161,7 +161,7 @@ def test_bucket_replay(eng, mode, gap):
 @pytest.mark.parametrize("mode", [abi.HSG_EMIT_PER_RECORD, abi.HSG_EMIT_PER_BATCH], ids=["changes", "per_batch_last"])
 def test_bucket_replay_hot_key_falls_back(eng, mode):
     """A key with more records in one batch than a bucket-replay sub-bucket
-    holds (kBrCap = 2048): the batch is flagged before any state changes and
+    holds (kBrCap = 1024): the batch is flagged before any state changes and
     runs on the sort-based replay instead; batches without one go back to
     the bucket replay. Same results either way."""
     aggs = ALL_AGG_SETS["mixed"] if mode == abi.HSG_EMIT_PER_RECORD else \
