@@ -2211,6 +2211,14 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
   const bool mir = prog.n_slots <= kSessMirrorSlots;
   int64_t live_delta = 0;
   uint64_t inserted = 0;
+  uint64_t ph[5] = {0, 0, 0, 0, 0}, pc = 0, nsp = 0;  // phase clocks (PHASES=1 builds), thread 0
+  auto tick = [&](int k) {
+    if constexpr (kPhaseClocks) {
+      const uint64_t c = phase_clock();
+      if (k >= 0) ph[k] += c - pc;
+      pc = c;
+    }
+  };
   // block-wide exclusive scan of one value per thread (every thread calls)
   auto block_excl = [&](uint64_t v, uint64_t &total) -> uint64_t {
     const uint64_t incl = wave_incl_sum(v);
@@ -2227,6 +2235,8 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
   };
   for (int sub = (int)sp.progress[bk]; sub < nsub; ++sub) {
     const uint32_t s0 = sp.subst[bk * 65ull + sub], cnt = sp.subst[bk * 65ull + sub + 1] - s0;
+    tick(-1);
+    ++nsp;
     // 1. group the sub-bucket's records by key (LDS hash table)
     for (int i = threadIdx.x; i < kBrTab; i += kBrNT) {
       L.tkey[i] = kSessEmptyKey;
@@ -2252,6 +2262,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       L.rtab[q] = (uint16_t)h;
     }
     __syncthreads();
+    tick(0);
     // 2. groups: the keys in table order, their segments (block scan over the table)
     {
       constexpr int PER = kBrTab / kBrNT;
@@ -2280,6 +2291,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       if (threadIdx.x == 0) L.ngrp = (uint32_t)(all >> 32);
     }
     __syncthreads();
+    tick(1);
     const uint32_t ngrp = L.ngrp;
     // 3. records into their group's segment, then ranked by arrival index
     for (uint32_t q = threadIdx.x; q < cnt; q += kBrNT) {
@@ -2333,6 +2345,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       L.abase = base;
     }
     __syncthreads();
+    tick(2);
     if (L.fail) break;
     // 5. replay: one thread per key, its records in arrival order against its list
     for (uint32_t g0 = 0; g0 < ngrp; g0 += kBrNT) {
@@ -2488,6 +2501,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
     {
       uint64_t rtot;
       const uint64_t rpre = block_excl(rl_n ? 1u : 0u, rtot);
+      tick(3);
       if (threadIdx.x == 0) L.rbase = rtot ? atomicAdd((unsigned long long *)&t.meta[M_RELOC], rtot) : 0;
       __syncthreads();
       if (rl_n) {
@@ -2529,7 +2543,15 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
     }
     }
     __syncthreads();
+    tick(4);
     if (threadIdx.x == 0) sp.progress[bk] = (uint32_t)(sub + 1);
+  }
+  if constexpr (kPhaseClocks) {
+    if (threadIdx.x == 0) {
+      for (int k = 0; k < 5; ++k) atomicAdd((unsigned long long *)&sc->scratch[24 + k], (unsigned long long)ph[k]);
+      atomicAdd((unsigned long long *)&sc->scratch[30], (unsigned long long)nsp);
+      sc->scratch[23] = 1;
+    }
   }
   const uint64_t ld = wave_sum_u64((uint64_t)live_delta);
   if (lane == 0 && ld) atomicAdd((unsigned long long *)&sc->live, (unsigned long long)ld);

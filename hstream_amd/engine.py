@@ -11,6 +11,9 @@ from . import abi
 from .columnar import OpHandle, OpSpec, declare_op_functions
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhstream_gpu.so")
+# diagnostics only: HSG_LIB_PATH names another build of the same library
+# (e.g. the PHASES=1 phase-clock build, tools/phases.sh)
+LIB_PATH = os.environ.get("HSG_LIB_PATH", LIB_PATH)
 _lib = None
 
 
