@@ -2087,12 +2087,12 @@ __global__ __launch_bounds__(kBrSubNT) void k_br_subhist(SessTable t, int np_log
   const uint64_t r0 = sp.bstart[b], m = sp.bstart[b + 1] - r0;
   const int sl = br_sub_log2(m), nsub = 1 << sl, hs = bshift + np_log2;
   if (threadIdx.x < (1 << kBrMaxSubLog2)) cnt[threadIdx.x] = 0;
-  __syncthreads();
+  lds_barrier();
   for (uint64_t q = threadIdx.x; q < m; q += kBrSubNT) {
     const uint32_t key = (uint32_t)sp.srec[(r0 + q) * W];
     atomicAdd(&cnt[ss_sub(key, hs, sl)], 1u);
   }
-  __syncthreads();
+  lds_barrier();
   if (threadIdx.x == 0) {
     uint32_t run = 0;
     bool big = false;
@@ -2105,7 +2105,7 @@ __global__ __launch_bounds__(kBrSubNT) void k_br_subhist(SessTable t, int np_log
     sp.subst[b * 65ull + nsub] = run;
     if (big) atomicOr((unsigned long long *)&t.meta[M_BRBIG], 1ull);
   }
-  __syncthreads();
+  lds_barrier();
   for (uint64_t q = threadIdx.x; q < m; q += kBrSubNT) {
     const uint64_t *src = sp.srec + (r0 + q) * W;
     uint64_t v[W];
@@ -2200,6 +2200,10 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
                                                      int bshift, SessPart sp, const int64_t *seq, OutCols out,
                                                      uint64_t out_base, DevScalars *sc) {
   __shared__ BrLds<W> L;
+  // every barrier here orders LDS only (lds_barrier): nothing in the
+  // workgroup reads back the rows, entries or states its threads store, so
+  // no barrier waits for those scattered stores (a __syncthreads would: its
+  // release waits for the wave's outstanding stores, ~10 us per sub-bucket)
   constexpr int CW = BrLds<W>::CW;
   if (t.meta[M_BRBIG] || t.meta[M_FAIL]) return;  // uniform: the other replay runs / the arena is refilled first
   const uint32_t bk = blockIdx.x;
@@ -2222,9 +2226,9 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
   // block-wide exclusive scan of one value per thread (every thread calls)
   auto block_excl = [&](uint64_t v, uint64_t &total) -> uint64_t {
     const uint64_t incl = wave_incl_sum(v);
-    __syncthreads();
+    lds_barrier();
     if (lane == 63) L.wsum64[w] = incl;
-    __syncthreads();
+    lds_barrier();
     uint64_t pre = incl - v;
     total = 0;
     for (int k = 0; k < kBrNT / 64; ++k) {
@@ -2243,7 +2247,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       L.tcnt[i] = 0;
     }
     if (threadIdx.x == 0) L.fail = 0;
-    __syncthreads();
+    lds_barrier();
     for (uint32_t q = threadIdx.x; q < cnt; q += kBrNT) {
       const uint32_t pos = (uint32_t)(r0 + s0 + q);
       const uint64_t *rec = sp.scopy + (uint64_t)pos * W;
@@ -2261,7 +2265,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       atomicAdd(&L.tcnt[h], 1u);
       L.rtab[q] = (uint16_t)h;
     }
-    __syncthreads();
+    lds_barrier();
     tick(0);
     // 2. groups: the keys in table order, their segments (block scan over the table)
     {
@@ -2290,7 +2294,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       }
       if (threadIdx.x == 0) L.ngrp = (uint32_t)(all >> 32);
     }
-    __syncthreads();
+    lds_barrier();
     tick(1);
     const uint32_t ngrp = L.ngrp;
     // 3. records into their group's segment, then ranked by arrival index
@@ -2299,7 +2303,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       L.seg[L.gstart[g] + atomicAdd(&L.gcur[g], 1u)] = (uint16_t)q;
       L.rtab[q] = (uint16_t)g;
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t x = threadIdx.x; x < cnt; x += kBrNT) {
       const uint32_t q = L.seg[x], g = L.rtab[q], st = L.gstart[g], c = L.gcnt[g], me = L.ridx[q];
       uint32_t rank = 0;
@@ -2344,7 +2348,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       }
       L.abase = base;
     }
-    __syncthreads();
+    lds_barrier();
     tick(2);
     if (L.fail) break;
     // 5. replay: one thread per key, its records in arrival order against its list
@@ -2503,14 +2507,14 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       const uint64_t rpre = block_excl(rl_n ? 1u : 0u, rtot);
       tick(3);
       if (threadIdx.x == 0) L.rbase = rtot ? atomicAdd((unsigned long long *)&t.meta[M_RELOC], rtot) : 0;
-      __syncthreads();
+      lds_barrier();
       if (rl_n) {
         uint64_t *r = sp.reloc + 3 * (L.rbase + rpre);
         r[0] = rl_src;
         r[1] = rl_dst;
         r[2] = rl_n;
       }
-      __syncthreads();
+      lds_barrier();
     }
     // per-batch changelog (LAST / literal forms, or every op with
     // HSG_SS_REPLAY_ALL): the key's sessions this batch stamped, found from
@@ -2524,7 +2528,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
         L.rbase = tot ? atomicAdd((unsigned long long *)&sc->out_rows, (unsigned long long)tot) : 0;
         if (tot) atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)tot);
       }
-      __syncthreads();
+      lds_barrier();
       uint64_t o = out_base + L.rbase + pre;
       uint32_t left = emitted;
       for (uint64_t k = klen; k > 0 && left; --k) {
@@ -2539,10 +2543,10 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
         ++o;
         --left;
       }
-      __syncthreads();
+      lds_barrier();
     }
     }
-    __syncthreads();
+    lds_barrier();
     tick(4);
     if (threadIdx.x == 0) sp.progress[bk] = (uint32_t)(sub + 1);
   }
@@ -2605,7 +2609,7 @@ __global__ __launch_bounds__(256) void k_br_emit(Batch b, SessParams p, Program 
     const uint64_t m = __ballot(keyed);
     const uint32_t pre = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
     if (lane == 0) sw[w] = (uint32_t)__popcll(m);
-    __syncthreads();
+    lds_barrier();  // (LDS only: the rows stored are read by no one here)
     uint32_t wpre = 0, tot = 0;
     for (int k = 0; k < 4; ++k) {
       wpre += k < w ? sw[k] : 0u;
@@ -2622,7 +2626,7 @@ __global__ __launch_bounds__(256) void k_br_emit(Batch b, SessParams p, Program 
       if (out.form) out.form[q] = out_form(prog, f + 2);
     }
     o += tot;
-    __syncthreads();
+    lds_barrier();
   }
 }
 
