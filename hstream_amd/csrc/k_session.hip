@@ -1547,7 +1547,9 @@ __global__ __launch_bounds__(kApNT) void k_ss_apply(SessParams p, SessTable t, P
   }
   const uint64_t lsum = wave_sum_u64((uint64_t)ld);
   if (lane == 0 && lsum) atomicAdd((unsigned long long *)&sc->live, (unsigned long long)lsum);
-  __syncthreads();
+  // (the done flag is read by a later launch only: no wait here for the
+  // block's scattered stores, which a __syncthreads would add)
+  lds_barrier();
   if (threadIdx.x == 0) sp.done[blk] = 1;
 }
 
