@@ -2042,7 +2042,19 @@ void launch_ss_dump(hipStream_t s, const SessTable &t, const Program &prog, OutC
 // ---------------------------------------------------------------------------
 // Bucket replay (hsg_session.h): per-record changelog, LAST, literal forms.
 // ---------------------------------------------------------------------------
-constexpr int kBrNT = 512;
+#ifndef HSG_BR_NT
+#define HSG_BR_NT 512
+#endif
+constexpr int kBrNT = HSG_BR_NT;
+// k_br_replay's register tail for records before the last session (ops of at
+// most this many slots; 0: off). Measured on C4 EMIT CHANGES: the tail cuts
+// the replay phase from 12.0 to 10.8 us per sub-pass, but its 166 VGPRs leave
+// room for one 512-thread workgroup per CU instead of two: 2.61 -> 4.19 ms per
+// batch. The replay is bound by how many sub-passes are in flight, not by one
+// sub-pass's latency, so it stays off.
+#ifndef HSG_BR_TAIL_MS
+#define HSG_BR_TAIL_MS 0
+#endif
 constexpr int kBrTab = 2 * kBrCap;  // LDS key table entries (load <= 1/2)
 constexpr int kBrMaxSubLog2 = 6;
 constexpr int kBrSubNT = 256;
@@ -2218,6 +2230,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
   int64_t live_delta = 0;
   uint64_t inserted = 0;
   uint64_t ph[5] = {0, 0, 0, 0, 0}, pc = 0, nsp = 0;  // phase clocks (PHASES=1 builds), thread 0
+  uint64_t n_slow = 0, n_deep = 0, n_grp = 0;  // PHASES=1: records off the mirror (past the tail), groups
   auto tick = [&](int k) {
     if constexpr (kPhaseClocks) {
       const uint64_t c = phase_clock();
@@ -2361,6 +2374,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
     uint64_t klen = 0, koff = 0;
     uint32_t kkey = 0;
     if (g < ngrp && L.tkey[g] != ~0u) {
+      n_grp += 1;
       const uint32_t ks = L.tkey[g];
       if (ngrp > kBrNT) E = ss_load_entry(&t.kt[ks]);
       uint64_t off = E.off, len = E.len;
@@ -2425,6 +2439,100 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
 #pragma unroll
           for (int s = 0; s < MS; ++s) la[s] = acc[s];
         } else {
+          n_slow += 1;
+          // a record before the last session: the list's tail rows (KT of
+          // them) in one round of loads; when the row before the tail ends
+          // before lo, every session the record reaches is among them, and the
+          // merge, the shift and the mirror run from registers (no dependent
+          // search, no load-then-store copies)
+          constexpr int KT = MS <= HSG_BR_TAIL_MS ? 4 : 0;
+          constexpr int RW = 3 + (MS <= 4 ? MS : 0);
+          bool done = false;
+          if constexpr (KT > 0) {
+            const uint64_t tb = len > (uint64_t)KT ? len - KT : 0;
+            uint64_t R[KT > 0 ? KT : 1][RW];
+#pragma unroll
+            for (int k = 0; k < KT; ++k) {
+              const uint64_t idx = tb + k;
+              const uint64_t *row = ss_row(t, (pending && idx < pfx ? old_off : off) + idx);
+#pragma unroll
+              for (int w2 = 0; w2 < RW; ++w2) R[k][w2] = idx < len && w2 < 3 + (int)t.ns ? row[w2] : 0;
+            }
+            if (tb == 0 || (int64_t)R[0][1] < lo) {
+              done = true;
+              // i0: first row ending at or after lo; i1: past the rows starting by hi
+              uint64_t i0 = len, i1;
+#pragma unroll
+              for (int k = KT - 1; k >= 0; --k)
+                if (tb + k < len && (int64_t)R[k][1] >= lo) i0 = tb + k;
+              uint64_t mc = 0;
+#pragma unroll
+              for (int k = 0; k < KT; ++k) mc += tb + k >= i0 && tb + k < len && (int64_t)R[k][0] <= hi ? 1u : 0u;
+              i1 = i0 + mc;
+              uint32_t sm = 0;
+              for (uint64_t j = i0; j < i1; ++j) {  // the merged rows, in end order
+                uint64_t cw[RW];
+#pragma unroll
+                for (int w2 = 0; w2 < RW; ++w2) {
+                  cw[w2] = 0;
+#pragma unroll
+                  for (int k = 0; k < KT; ++k) cw[w2] = tb + k == j ? R[k][w2] : cw[w2];
+                }
+                ss = (int64_t)cw[0] < ss ? (int64_t)cw[0] : ss;
+                se = (int64_t)cw[1] > se ? (int64_t)cw[1] : se;
+                sm += (uint32_t)cw[2] == p.batch_id ? 1u : 0u;
+                int64_t cur[MS];
+#pragma unroll
+                for (int s2 = 0; s2 < MS; ++s2) cur[s2] = s2 + 3 < RW ? (int64_t)cw[3 + s2] : 0;
+                merge_row<MS>(prog, acc, cur);
+              }
+              const bool to_end = i1 == len;
+              // the rows after the merged stretch move (up one for an insert,
+              // down mc - 1 for a merge of several), straight from registers;
+              // in a moved list they are written at their new place even when
+              // they keep their index (only rows before i0 are left to the copy)
+              const int64_t sh = mc == 0 ? 1 : 1 - (int64_t)mc;
+              if (sh != 0 || pending) {
+#pragma unroll
+                for (int k = 0; k < KT; ++k) {
+                  const uint64_t idx = tb + k;
+                  if (idx < i1 || idx >= len) continue;
+                  uint64_t *d = ss_row(t, off + (uint64_t)((int64_t)idx + sh));
+#pragma unroll
+                  for (int w2 = 0; w2 < RW; ++w2)
+                    if (w2 < 3 + (int)t.ns) d[w2] = R[k][w2];
+                }
+              }
+              // the last session before the update, if the mirror did not hold it
+              if (mir && !lv && len > 0 && !to_end) {
+#pragma unroll
+                for (int k = 0; k < KT; ++k)
+                  if (tb + k == len - 1) {
+                    ls = (int64_t)R[k][0];
+                    le = (int64_t)R[k][1];
+#pragma unroll
+                    for (int s2 = 0; s2 < MS; ++s2) la[s2] = s2 + 3 < RW ? (int64_t)R[k][3 + s2] : 0;
+                  }
+              }
+              len = (uint64_t)((int64_t)len + sh);
+              live_delta += 1 - (int64_t)mc;
+              ss_store<MS>(t, off + i0, ss, se, p.batch_id, acc);
+              pfx = i0 < pfx ? i0 : pfx;  // a moved list: rows from i0 on are written at their new place
+              emitted += 1u - sm;
+              if (to_end) lst = true;
+              if (mir) {
+                if (i0 + 1 == len) {
+                  ls = ss;
+                  le = se;
+#pragma unroll
+                  for (int s2 = 0; s2 < MS; ++s2) la[s2] = acc[s2];
+                }
+                lv = true;
+              }
+            }
+          }
+          if (!done) {
+          n_deep += 1;
           if (pending) {  // the list is read from here on: its moved rows first
             for (uint64_t k = 0; k < pfx; ++k) ss_copy(t, off + k, t, old_off + k);
             pending = false;
@@ -2476,6 +2584,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
               ss_load<MS>(t, off + len - 1, la);
             }
             lv = true;
+          }
           }
         }
         int64_t *f = sp.fin + (uint64_t)i * fs;
@@ -2557,6 +2666,11 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       for (int k = 0; k < 5; ++k) atomicAdd((unsigned long long *)&sc->scratch[24 + k], (unsigned long long)ph[k]);
       atomicAdd((unsigned long long *)&sc->scratch[30], (unsigned long long)nsp);
       sc->scratch[23] = 1;
+    }
+    const uint64_t a = wave_sum_u64(n_slow | n_deep << 32), z = wave_sum_u64(n_grp);
+    if (lane == 0) {
+      atomicAdd((unsigned long long *)&sc->scratch[43], (unsigned long long)a);
+      atomicAdd((unsigned long long *)&sc->scratch[44], (unsigned long long)z);
     }
   }
   const uint64_t ld = wave_sum_u64((uint64_t)live_delta);

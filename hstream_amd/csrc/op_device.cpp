@@ -656,6 +656,10 @@ int finish_batch(OpDevice &d, int64_t wm_in, uint64_t n, PushResult &r, std::str
     fprintf(stderr, "[hsg phases] bucket replay sub-passes=%llu load=%.2fus group=%.2fus rank+probe+reserve=%.2fus replay=%.2fus tail=%.2fus (per sub-pass)\n",
             (unsigned long long)s.scratch[30], s.scratch[24] * 0.01 / s.scratch[30], s.scratch[25] * 0.01 / s.scratch[30],
             s.scratch[26] * 0.01 / s.scratch[30], s.scratch[27] * 0.01 / s.scratch[30], s.scratch[28] * 0.01 / s.scratch[30]);
+  if (phases && s.scratch[30] && s.scratch[23] == 1)
+    fprintf(stderr, "[hsg phases] bucket replay records off the mirror=%llu (past the tail %llu) groups=%llu\n",
+            (unsigned long long)(s.scratch[43] & 0xFFFFFFFFu), (unsigned long long)(s.scratch[43] >> 32),
+            (unsigned long long)s.scratch[44]);
   else if (phases && s.scratch[30])
     fprintf(stderr, "[hsg phases] session sort wg=%llu buckets=%.1fus insert=%.1fus scan=%.1fus place=%.1fus keys=%.1fus total=%.1fus (per-wg avg)\n",
             (unsigned long long)s.scratch[30], s.scratch[24] * 0.01 / s.scratch[30], s.scratch[25] * 0.01 / s.scratch[30],
