@@ -610,7 +610,8 @@ def pipeline_name(cfg, emit):
     from hstream_amd import abi
     if cfg.window_kind == abi.HSG_SESSION:
         if emit == "per_record":
-            return "session replay (k_ss_slot, radix sort, k_ss_process)"
+            return ("session bucket replay (k_ss_phist, offsets, k_ss_pscatter, k_br_subhist, k_br_replay, "
+                    "k_ss_reloc_copy, k_br_emit)")
         return "session merge (k_ss_phist, offsets, k_ss_pscatter, k_ss_sort, k_ss_apply)"
     if emit == "per_record":
         if cfg.window_kind in (abi.HSG_TUMBLING, abi.HSG_UNWINDOWED):
