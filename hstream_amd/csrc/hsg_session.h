@@ -138,7 +138,10 @@ void launch_ss_emit(hipStream_t s, const SessTable &t, const Program &prog, cons
 // changelog is then written in arrival order (k_br_emit). A sub-bucket of more
 // than kBrCap records (a hot key) sets M_BRBIG before anything is modified,
 // and the batch takes the sort-based replay instead.
-constexpr int kBrCap = 1024;
+#ifndef HSG_BR_CAP
+#define HSG_BR_CAP 1024
+#endif
+constexpr int kBrCap = HSG_BR_CAP;
 int br_words(int n_cols);
 void launch_br_scatter(hipStream_t s, const Batch &b, int np_log2, int bshift, uint64_t tiles, int words,
                        const SessPart &sp);

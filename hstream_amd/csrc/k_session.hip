@@ -2052,6 +2052,9 @@ constexpr int kBrNT = HSG_BR_NT;
 // room for one 512-thread workgroup per CU instead of two: 2.61 -> 4.19 ms per
 // batch. The replay is bound by how many sub-passes are in flight, not by one
 // sub-pass's latency, so it stays off.
+#ifndef HSG_BR_WPE
+#define HSG_BR_WPE 1  // minimum waves per SIMD asked of the compiler for k_br_replay (1: none)
+#endif
 #ifndef HSG_BR_TAIL_MS
 #define HSG_BR_TAIL_MS 0
 #endif
@@ -2193,7 +2196,6 @@ struct BrLds {
   static constexpr int CW = W <= 5 ? W - 1 : 0;
   uint32_t tkey[kBrTab];  // key table
   uint32_t tcnt[kBrTab];  // records per key; after the grouping: the key's group
-  uint32_t rpos[kBrCap];  // record -> its position in sp.srec
   uint32_t ridx[kBrCap];  // record -> its arrival index
   uint16_t rtab[kBrCap];  // record -> its key's table entry, then its group
   uint16_t seg[kBrCap];   // records placed by group
@@ -2210,7 +2212,7 @@ struct BrLds {
 };
 
 template <int MS, int W>
-__global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, SessTable t, Program prog, int np_log2,
+__global__ __launch_bounds__(kBrNT) __attribute__((amdgpu_waves_per_eu(HSG_BR_WPE))) void k_br_replay(Batch b, SessParams p, SessTable t, Program prog, int np_log2,
                                                      int bshift, SessPart sp, const int64_t *seq, OutCols out,
                                                      uint64_t out_base, DevScalars *sc) {
   __shared__ BrLds<W> L;
@@ -2268,7 +2270,6 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       const uint64_t *rec = sp.scopy + (uint64_t)pos * W;
       const uint32_t key = (uint32_t)rec[0];
       L.ridx[q] = (uint32_t)rec[W - 1];
-      L.rpos[q] = pos;
 #pragma unroll
       for (int k = 0; k < CW; ++k) L.rw[q * CW + k] = rec[k];
       uint32_t h = (uint32_t)key_hash(key) & (kBrTab - 1);
@@ -2407,7 +2408,7 @@ __global__ __launch_bounds__(kBrNT) void k_br_replay(Batch b, SessParams p, Sess
       const uint32_t st = L.gstart[g], c = L.gcnt[g];
       for (uint32_t x = st; x < st + c; ++x) {
         const uint32_t q = L.ord[x];
-        const uint64_t *rec = CW ? &L.rw[q * CW] : sp.scopy + (uint64_t)L.rpos[q] * W;
+        const uint64_t *rec = CW ? &L.rw[q * CW] : sp.scopy + (r0 + s0 + q) * W;
         const uint32_t i = L.ridx[q];
         const int64_t ts = (int64_t)rec[1];
         const uint64_t seq1 = (seq ? (uint64_t)seq[i] : p.rec_base + i) + 1;
