@@ -172,7 +172,9 @@ def test_c3_full_hopping(eng):
     assert not bool((g[1:] == g[:-1]).any()), "a (key, window) with two rows"
     op.close()
     print({k: st[k] for k in ("state_rows", "table_slots", "grow_events", "overflow_rebuilds", "replays")})
-    assert st["table_slots"] <= (1 << 30), st
+    # hopping tables run at up to half load: 766M
+    # (key, window) rows fit 2^31 slots, sized by the groups, not the updates
+    assert st["table_slots"] <= (1 << 31) and 2 * st["state_rows"] <= st["table_slots"], st
 
 
 def test_c4_full_sessions_disjoint(eng):
