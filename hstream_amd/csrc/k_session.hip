@@ -970,9 +970,12 @@ __device__ __attribute__((always_inline)) inline void mg_apply(const PV &prog, c
 // sub-bucket with a key of more than kSoSmall records (hot keys), or more than
 // kSoCH records, is left to k_ss_merge_big (its bit in sp.bigmask).
 // ---------------------------------------------------------------------------
+#ifndef HSG_SO_CH_LOG2
+#define HSG_SO_CH_LOG2 10
+#endif
 constexpr int kSoNT = 512;
-constexpr int kSoCH = 1024;        // records per sub-bucket
-constexpr int kSoTabLog2 = 11;
+constexpr int kSoCH = 1 << HSG_SO_CH_LOG2;  // records per sub-bucket
+constexpr int kSoTabLog2 = HSG_SO_CH_LOG2 + 1;
 constexpr int kSoTab = 1 << kSoTabLog2;  // LDS hash table entries
 constexpr int kSoMaxSubLog2 = 6;   // up to 64 sub-buckets (buckets of < 2^16 records)
 constexpr int kSoSmall = 32;       // a key's records sorted by its own thread
