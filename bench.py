@@ -67,6 +67,10 @@ def parse():
     p.add_argument("--state-capacity", type=int, default=0,
                    help="hsg_op_config state_capacity (default 0: the engine sizes the table itself)")
     p.add_argument("--extra-steps", type=int, default=3, help="timed steps of the hbm_resident / per_record blocks")
+    p.add_argument("--no-sql-shape", action="store_true",
+                   help="skip the sql_shape block (the SQL drop-in's op shape: literal forms + a passthrough)")
+    p.add_argument("--sql-emit", default="both", choices=["both", "per_batch", "per_record"],
+                   help="emit modes of the sql_shape block")
     return p.parse_args()
 
 
@@ -207,6 +211,7 @@ def main():
                 "xgmi_frac": round(xb_all / elapsed / links, 6) if world > 1 else None}
 
     per_rec = None
+    sql = None
     table_slots, grow_events = int(st1["table_slots"]), int(st1["grow_events"])
     if world == 1 and not args.force_exchange:
         del dev_step
@@ -215,6 +220,8 @@ def main():
         if (not args.no_per_record and cfg.window_kind in (abi.HSG_TUMBLING, abi.HSG_UNWINDOWED)
                 and emit != abi.HSG_EMIT_PER_RECORD):
             per_rec = per_record_block(eng, cfg, keys, ts, cols, pieces, args)
+        if not args.no_sql_shape and cols and cfg.window_kind in (abi.HSG_TUMBLING, abi.HSG_UNWINDOWED):
+            sql = sql_shape_block(eng, cfg, keys, ts, cols, pieces, args)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -245,6 +252,7 @@ def main():
             "cpu_baseline": cpu,
             "hbm_resident": hbm,
             "per_record": per_rec,
+            "sql_shape": sql,
             "exchange": xchg,
             "agg_kernel_share": round(agg_s / elapsed, 4) if elapsed > 0 else None,
             "pairs_per_step": int((st1["pairs_total"] - st0["pairs_total"]) / max(1, args.steps)),
@@ -431,7 +439,7 @@ def host_steps(op, keys, ts, cols, pieces, spec, emit, world, args):
     return step, Info(info)
 
 
-def roofline(st0, st1, spec, emit):
+def roofline(st0, st1, spec, emit, valid_bytes=0, form_bytes=0):
     """Roofline of the batch pipeline: one "launch" = one batch through the
     partition + aggregation + changelog kernels, timed by HIP events on the
     op's stream (hsg_stats agg_kernel_ms). SURVEY.md 8(d) algorithmic bytes
@@ -443,9 +451,9 @@ def roofline(st0, st1, spec, emit):
     launches = st1["agg_kernel_launches"] - st0["agg_kernel_launches"]
     agg_s = (st1["agg_kernel_ms"] - st0["agg_kernel_ms"]) / 1e3
     ncol = len(spec.col_types)
-    rec_bytes = 4 + 8 + 8 * ncol
+    rec_bytes = 4 + 8 + 8 * ncol + valid_bytes
     row_bytes = st1["state_row_bytes"]
-    out_bytes = 4 + 8 + 8 + 8 * len(spec.aggs) if emit != abi.HSG_EMIT_NONE else 0
+    out_bytes = 4 + 8 + 8 + 8 * len(spec.aggs) + form_bytes if emit != abi.HSG_EMIT_NONE else 0
     touched = st1["touched_total"] - st0["touched_total"]
     pairs = st1["pairs_total"] - st0["pairs_total"]
     emitted = {abi.HSG_EMIT_PER_BATCH: touched, abi.HSG_EMIT_PER_RECORD: pairs}.get(emit, 0)
@@ -547,6 +555,88 @@ def per_record_block(eng, cfg, keys, ts, cols, pieces, args):
     return out
 
 
+def sql_shape_block(eng, cfg, keys, ts, cols, pieces, args):
+    """The SQL drop-in's op shape on the same workload: the query hstream-sql's
+    genGroupByNode dispatches for C2 -- `SELECT v, COUNT(*), SUM(v), AVG(v),
+    MIN(v), MAX(v) FROM s GROUP BY key, TUMBLING (60 s)` -- whose objectSerde
+    sink needs each value's Scientific literal form (HSG_OPF_LITERAL_FORMS:
+    MIN / MAX tie words, the SUM's decimal count, Codegen.hs:436-461) and
+    whose non-aggregate column `v` is a passthrough (HSG_LAST: the group's
+    last record, Codegen.hs:463-469). The records carry validity bytes as a
+    JSON decoder fills them (every field present; 1 in 16 literals decimal,
+    e.g. `5.0`: bit 1). HBM-resident input, per batch and EMIT CHANGES, each
+    with its roofline (B_alg adds the validity byte per record and the 4-byte
+    form word per changelog row) and the path that ran (hsg_stats)."""
+    import ctypes as C
+    import torch
+    from hstream_amd import abi
+    from hstream_amd.columnar import OpSpec, make_batch
+    dev = keys.device
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234)
+    valid = (1 + 2 * (torch.randint(0, 16, (keys.numel(),), device=dev, generator=g) == 0)).to(torch.uint8)
+    aggs = [(abi.HSG_LAST, 0)] + list(cfg.aggs)
+    modes = {"both": ("per_batch", "per_record")}.get(args.sql_emit, (args.sql_emit,))
+    out = {"query": f"SELECT v, COUNT(*), SUM(v), AVG(v), MIN(v), MAX(v) GROUP BY key, {workload_text(cfg).split(' ')[0]}"
+                    f" window (HSG_OPF_LITERAL_FORMS, v as HSG_LAST)",
+           "valid": "every field present, 1 in 16 literals decimal (bit 1)", "input": "HBM-resident device columns"}
+    k = max(1, args.extra_steps)
+    n_rank = sum(m for _, m in pieces)
+    torch.cuda.synchronize()
+    for mode in modes:
+        emit = abi.HSG_EMIT_PER_BATCH if mode == "per_batch" else abi.HSG_EMIT_PER_RECORD
+        spec = OpSpec(window_kind=cfg.window_kind, emit_mode=emit, size_ms=cfg.size_ms, advance_ms=cfg.advance_ms,
+                      col_types=[cfg.col_type], aggs=aggs, flags=abi.HSG_OPF_LITERAL_FORMS)
+        op = eng.op(spec)
+        cap = max(1, eng_out_capacity(op))
+        outs = {"key_id": torch.empty(cap, dtype=torch.int32, device=dev),
+                "win_start": torch.empty(cap, dtype=torch.int64, device=dev),
+                "win_end": torch.empty(cap, dtype=torch.int64, device=dev),
+                "src_index": torch.empty(cap, dtype=torch.int64, device=dev),
+                "aggs": [torch.empty(cap, dtype=torch.float64 if f else torch.int64, device=dev)
+                         for f in spec.agg_is_f64()],
+                "form": torch.empty(cap, dtype=torch.int32, device=dev)}
+        drain = make_device_drain(op, outs, cap, zero_copy=True)
+        descs = [make_batch(keys[s:s + m], ts[s:s + m], [c[s:s + m] for c in cols], [valid[s:s + m]],
+                            abi.HSG_MEM_DEVICE) for s, m in pieces]
+        push_fn = op._lib.hsg_push_batch
+        wm = C.c_int64(-1)
+
+        def step():
+            op.reset()
+            wm.value = -1
+            for b, _keep in descs:
+                rc = push_fn(op._h, C.byref(b), C.byref(wm))
+                if rc != abi.HSG_OK:
+                    op._check(rc, "push_batch")
+                drain()
+
+        step()
+        torch.cuda.synchronize()
+        st0 = op.stats()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        st1 = op.stats()
+        roof = roofline(st0, st1, spec, emit, valid_bytes=1, form_bytes=4)
+        roof["kernel"] = ("SQL lean pipeline (k_part_hist_opt, offsets + decide, k_part_scatter_st with the "
+                          "sequence word, k_agg_sql, k_sql_apply writing the changelog rows)" if mode == "per_batch"
+                          else "per-record changelog (k_part_hist_opt, offsets + decide, stable k_part_scatter_st "
+                               "with the sequence word, k_pr_bucket, k_pr_emit1)")
+        batches = st1["batches"] - st0["batches"]
+        out[mode] = {"value": round(n_rank * k / el, 1), "unit": "records/s", "steps": k,
+                     "ms_per_step": round(el * 1e3 / k, 3), "roofline": roof,
+                     "state_slots": int(st1["state_slots"]),
+                     "lean_batches": int(st1["lean_batches"] - st0["lean_batches"]), "batches": int(batches),
+                     "replays_onto_record_kernels": int(st1["replays"] - st0["replays"])}
+        del descs, drain, outs
+        op.close()
+        torch.cuda.empty_cache()
+    return out
+
+
 def workload_text(cfg):
     from hstream_amd import abi
     kind = {abi.HSG_TUMBLING: f"tumbling {cfg.size_ms // 1000}s", abi.HSG_HOPPING:
@@ -578,7 +668,8 @@ def make_device_drain(op, outs, cap, zero_copy=True, register=True):
     rows = abi.hsg_rows(capacity=cap, mem=abi.HSG_MEM_DEVICE, n_aggs=len(outs["aggs"]),
                         key_id=outs["key_id"].data_ptr(), win_start=outs["win_start"].data_ptr(),
                         win_end=outs["win_end"].data_ptr(), src_index=outs["src_index"].data_ptr(),
-                        aggs=C.cast(agg_ptrs, C.POINTER(C.c_void_p)))
+                        aggs=C.cast(agg_ptrs, C.POINTER(C.c_void_p)),
+                        form=outs["form"].data_ptr() if "form" in outs else None)
     got = C.c_uint64(0)
     if zero_copy:
         if register:

@@ -168,8 +168,15 @@ int comm_create(const uint8_t *id_bytes, int rank, int nranks, int device, int t
     }
     // the largest collective: the classic exchange's packed records (<= 12 words each)
     c->slot_bytes = batch_cap * 12 * 8 + 4096;
-    int rc = agree_alloc(c, err);
-    if (rc == HSG_OK) rc = host_open(name, rank, nranks, c->slot_bytes, &c->host, err);
+    // the rendezvous first, whatever the allocation below does: no rank
+    // skips a collective its peers have entered
+    int rc = host_open(name, rank, nranks, c->slot_bytes, &c->host, err);
+    std::string aerr;
+    const int arc = agree_alloc(c, aerr);
+    if (rc == HSG_OK && arc != HSG_OK) {
+      rc = arc;
+      err = aerr;
+    }
     if (rc != HSG_OK) {
       comm_destroy(c);
       return rc;
@@ -177,19 +184,26 @@ int comm_create(const uint8_t *id_bytes, int rank, int nranks, int device, int t
     *out = c;
     return HSG_OK;
   }
-  // the agreement buffer first: a failure here comes before any collective
-  int arc = agree_alloc(c, err);
-  if (arc != HSG_OK) {
-    comm_destroy(c);
-    return arc;
-  }
+  // the communicator init first, whatever the allocation of the agreement
+  // buffer does: every rank joins the collective init (a rank that returned
+  // before it would leave its peers waiting there). A rank whose 16-byte
+  // agreement buffer then fails to allocate returns the error; its peers see
+  // it at their first agreement (op creation), which that rank never joins --
+  // the caller must not go on with the engine on any rank then.
   ncclUniqueId id;
   memcpy(&id, id_bytes, sizeof(id));
-  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+  const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+  std::string aerr;
+  const int arc = agree_alloc(c, aerr);
   if (r != ncclSuccess) {
     err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
     comm_destroy(c);
     return HSG_E_COMM;
+  }
+  if (arc != HSG_OK) {
+    err = aerr;
+    comm_destroy(c);
+    return arc;
   }
   *out = c;
   return HSG_OK;

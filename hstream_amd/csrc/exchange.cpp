@@ -43,7 +43,48 @@ namespace hsg {
     }                                                                       \
   } while (0)
 
-static int info_words(int G) { return 4 + G; }
+// all-gathered facts per rank: [max ts, min keyed ts, n, has_valid,
+// records for each owner [G], changelog room, changelog row clamp]
+static int info_words(int G) { return 6 + G; }
+
+// This rank's changelog room (rows free in the changelog buffer) and the
+// clamp on the rows one batch can make here (per-batch time windows: the
+// table's slots), queued into its info words for the all-gather: every rank
+// then sees every rank's room and the records each one will own, and all of
+// them refuse the batch together before the all-to-all when any rank's room
+// is short (a rank that failed alone would leave its peers waiting in it).
+static int publish_room(OpDevice &d, const hsg_op_config &cfg, const PushArgs &a, int G, std::string &err) {
+  XBuffers &x = *d.x;
+  uint64_t room = UINT64_MAX, clamp = UINT64_MAX;
+  if (cfg.emit_mode != HSG_EMIT_NONE) {
+    room = d.out_cap > a.pending ? d.out_cap - a.pending : 0;
+    if (cfg.emit_mode == HSG_EMIT_PER_BATCH && cfg.window_kind != HSG_SESSION) clamp = d.cap;
+  }
+  x.h_room[0] = (int64_t)room;
+  x.h_room[1] = (int64_t)clamp;
+  // (pinned source: the push synchronises on the all-gather before the next
+  // batch rewrites it)
+  DTRY(hipMemcpyAsync(x.info + 4 + G, x.h_room, 16, hipMemcpyHostToDevice, d.stream));
+  return HSG_OK;
+}
+
+// the uniform refusal (same H on every rank): some rank's owned records could
+// write more changelog rows than its buffer has room for
+static int check_room(const OpDevice &d, const int64_t *H, int G, std::string &err) {
+  const int IW = info_words(G);
+  for (int q = 0; q < G; ++q) {
+    uint64_t ro = 0;
+    for (int p = 0; p < G; ++p) ro += (uint64_t)H[(uint64_t)p * IW + 4 + q];
+    uint64_t need = ro * d.wpr;
+    const uint64_t clamp = (uint64_t)H[(uint64_t)q * IW + 5 + G], room = (uint64_t)H[(uint64_t)q * IW + 4 + G];
+    if (need > clamp) need = clamp;
+    if (need > room) {
+      err = "changelog buffer full on rank " + std::to_string(q) + ": drain before pushing (out_capacity)";
+      return HSG_E_CAPACITY;  // the batch is applied on no rank
+    }
+  }
+  return HSG_OK;
+}
 
 static XLayout layout_for(const hsg_op_config &cfg, bool has_seq, bool has_wm, bool has_valid) {
   XLayout L;
@@ -74,6 +115,7 @@ int exchange_device_init(OpDevice &d, const hsg_op_config &cfg, uint64_t batch_c
   DTRY(hipMalloc((void **)&x->info, info_words(G) * 8));
   DTRY(hipMalloc((void **)&x->info_all, (uint64_t)G * info_words(G) * 8));
   DTRY(hipHostMalloc((void **)&x->h_info, (uint64_t)G * info_words(G) * 8, hipHostMallocDefault));
+  DTRY(hipHostMalloc((void **)&x->h_room, 16, hipHostMallocDefault));
   DTRY(hipMalloc((void **)&x->wm_local, n * 8 + 8));
   DTRY(hipMalloc((void **)&x->send, n * max_words * 8 + 65536));
   DTRY(hipMalloc((void **)&x->recv, (uint64_t)G * n * max_words * 8 + 65536));
@@ -107,6 +149,7 @@ void exchange_device_free(OpDevice &d) {
   hipFree(x->info);
   hipFree(x->info_all);
   hipHostFree(x->h_info);
+  hipHostFree(x->h_room);
   hipFree(x->wm_local);
   hipFree(x->send);
   hipFree(x->recv);
@@ -151,12 +194,14 @@ static int push_sharded_fast(OpDevice &d, const hsg_op_config &cfg, const Progra
   xp.tiles = x_tiles(n);
   launch_part_offsets(s, xp, d.part, d.sc);
   launch_x_info(s, d.sc, d.part.bstart, xl, (uint32_t)G, n, has_valid, x.info, d.part.text, x_tiles(n));
+  if ((rc = publish_room(d, cfg, a, G, err)) != HSG_OK) return rc;
   // 2. all-gather the per-rank facts
   rc = comm_allgather(comm, x.info, x.info_all, IW, ncclInt64, 8, s, err);
   if (rc != HSG_OK) return rc;
   DTRY(hipMemcpyAsync(x.h_info, x.info_all, (uint64_t)G * IW * 8, hipMemcpyDeviceToHost, s));
   DTRY(hipStreamSynchronize(s));
   const int64_t *H = x.h_info;
+  if ((rc = check_room(d, H, G, err)) != HSG_OK) return rc;
   int64_t wm_global = a.wm_in, carry = a.wm_in, min_ts = INT64_MAX;
   uint64_t total = 0;
   bool any_valid = false;
@@ -333,12 +378,14 @@ static int push_sharded_seq(OpDevice &d, const hsg_op_config &cfg, const Program
   xp.tiles = x_tiles(n);
   launch_part_offsets(s, xp, d.part, d.sc);
   launch_x_info(s, d.sc, d.part.bstart, xl, (uint32_t)G, n, has_valid, x.info, d.part.text, x_tiles(n));
+  if ((rc = publish_room(d, cfg, a, G, err)) != HSG_OK) return rc;
   // 2. all-gather the per-rank facts
   rc = comm_allgather(comm, x.info, x.info_all, IW, ncclInt64, 8, s, err);
   if (rc != HSG_OK) return rc;
   DTRY(hipMemcpyAsync(x.h_info, x.info_all, (uint64_t)G * IW * 8, hipMemcpyDeviceToHost, s));
   DTRY(hipStreamSynchronize(s));
   const int64_t *H = x.h_info;
+  if ((rc = check_room(d, H, G, err)) != HSG_OK) return rc;
   int64_t wm_global = a.wm_in, carry = a.wm_in, min_ts = INT64_MAX;
   uint64_t seq_base = a.rec_base, total = 0;
   bool any_valid = false;
@@ -485,6 +532,7 @@ static int push_sharded_classic(OpDevice &d, const hsg_op_config &cfg, const Pro
   DTRY(hipMemsetAsync(x.hist, 0, (kMaxRanks + 1) * 8, s));
   launch_x_owner(s, kb, (uint32_t)G, x.owner, x.idx, x.hist);
   DTRY(hipMemcpyAsync(x.info + 4, x.hist, (uint64_t)G * 8, hipMemcpyDeviceToDevice, s));
+  if ((rc = publish_room(d, cfg, a, G, err)) != HSG_OK) return rc;
   // stable partition by owner: one 8-bit radix pass of (owner, record index)
   int which = radix_sort_pairs(s, x.owner, x.idx, x.k1, x.v1, n, 8, x.sort_scratch);
   const uint32_t *sidx = which ? x.v1 : x.idx;
@@ -494,6 +542,7 @@ static int push_sharded_classic(OpDevice &d, const hsg_op_config &cfg, const Pro
   DTRY(hipMemcpyAsync(x.h_info, x.info_all, (uint64_t)G * IW * 8, hipMemcpyDeviceToHost, s));
   DTRY(hipStreamSynchronize(s));
   const int64_t *H = x.h_info;
+  if ((rc = check_room(d, H, G, err)) != HSG_OK) return rc;
   int64_t wm_global = a.wm_in, carry = a.wm_in, min_ts = INT64_MAX;
   uint64_t seq_base = a.rec_base, total = 0;
   bool any_valid = false;

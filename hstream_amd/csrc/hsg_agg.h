@@ -83,7 +83,9 @@ struct PRec {
     return v;
   }
   __device__ int64_t col(int c) const { return word(CB + c); }
-  __device__ int64_t seq1() const { return word(CB + C); }
+  // the sequence word (hsg_dev.h seq_word): seq + 1, decimal-literal bits
+  __device__ int64_t seq1() const { return (int64_t)((uint64_t)word(CB + C) & kSeqMask); }
+  __device__ bool dec(int c) const { return ((uint64_t)word(CB + C) >> (56 + c)) & 1ull; }
 };
 
 // contribution of the record to slot s (identity when absent)
@@ -103,6 +105,10 @@ __device__ inline int64_t prec_elem(const PG &prog, int s, const R &r) {
     case S_MIN_F:
     case S_MAX_F: return (int64_t)f64_ord(__builtin_bit_cast(double, r.col(c)));
     case S_LAST_SEQ: return r.seq1();
+    case S_CNT_DEC: return r.dec(c) ? 1 : 0;
+    case S_TIE_MIN:
+    case S_TIE_MAX:
+    case S_LAST_FORM: return (int64_t)(((uint64_t)r.seq1() << 1) | (r.dec(c) ? 0u : 1u));
     default: return 0;
   }
 }

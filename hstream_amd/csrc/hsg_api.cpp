@@ -144,6 +144,26 @@ int build_program(const hsg_op_config &cfg, const std::vector<int32_t> &col_type
   }
   prog.n_out = (int)aggs.size();
   for (int s = 0; s < prog.n_slots; ++s) prog.ties |= slot_is_tie(prog.slot_op[s]) ? 1 : 0;
+  // the per-record state projection (hsg_internal.h fin_*): the slots the
+  // outputs read, plus the form word, when that is smaller than the state
+  bool used[kMaxSlots] = {};
+  bool forms_any = false;
+  for (int j = 0; j < prog.n_out; ++j) {
+    used[prog.out_a[j]] = true;
+    if (prog.out_kind[j] == O_AVG_I || prog.out_kind[j] == O_AVG_F) used[prog.out_b[j]] = true;
+    forms_any |= prog.form_kind[j] != F_NONE;
+  }
+  int nf = 0;
+  for (int s = 0; s < prog.n_slots; ++s)
+    if (used[s]) prog.fin_slot[nf++] = s;
+  if (nf + (forms_any ? 1 : 0) < prog.n_slots) {
+    prog.fin_n = nf;
+    prog.fin_form = forms_any ? 1 : 0;
+  } else {
+    prog.fin_n = prog.n_slots;
+    prog.fin_form = 0;
+    for (int s = 0; s < prog.n_slots; ++s) prog.fin_slot[s] = s;
+  }
   return HSG_OK;
 }
 

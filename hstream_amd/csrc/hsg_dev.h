@@ -96,6 +96,18 @@ __device__ inline int64_t form_word(const Batch &b, int c, uint64_t i, uint64_t 
   return (int64_t)((seq1 << 1) | (rec_decimal(b, c, i) ? 0u : 1u));
 }
 
+// Sequence word of a partitioned record of an op with LAST / literal-form
+// slots (hsg_part.h): (global seq + 1) in the low 56 bits, bit 56 + c set when
+// column c's literal is decimal (bit 1 of its valid byte).
+constexpr uint64_t kSeqMask = (1ull << 56) - 1;
+__device__ inline uint64_t seq_word(const Batch &b, int C, int has_valid, int64_t seq, uint64_t i) {
+  uint64_t w = (uint64_t)(seq + 1) & kSeqMask;
+  if (has_valid)
+    for (int c = 0; c < C && c < 8; ++c)
+      if (b.valid[c] && (b.valid[c][i] & 2u)) w |= 1ull << (56 + c);
+  return w;
+}
+
 // Contribution of record i to state slot s (identity when the field is absent).
 __device__ inline int64_t slot_elem(const Program &prog, int s, const Batch &b, uint64_t i, uint64_t seq1) {
   const int op = prog.slot_op[s];

@@ -55,9 +55,11 @@ struct XBuffers {
   uint32_t *owner, *idx, *k1, *v1;  // [batch] partition sort
   void *sort_scratch;
   uint64_t *hist;                    // [kMaxRanks + 1]
-  int64_t *info;                     // [4 + kMaxRanks] this rank: max, min, n, has_valid, counts[G]
-  int64_t *info_all;                 // [G * (4 + kMaxRanks)]
+  int64_t *info;                     // [6 + G] this rank: max, min, n, has_valid, counts[G], changelog
+                                     // room, row clamp (exchange.cpp info_words)
+  int64_t *info_all;                 // [G * (6 + G)]
   int64_t *h_info;                   // pinned mirror of info_all
+  int64_t *h_room;                   // pinned: this rank's changelog room words, copied into info
   int64_t *wm_local;                 // [batch] per-record stream time before the exchange
   uint64_t *send;                    // [batch * max words]
   uint64_t *recv;                    // [G * batch * max words]

@@ -70,7 +70,16 @@ struct Program {
   int32_t form_a[kMaxAggs];
   int32_t slot_aux[kMaxSlots];  // S_TIE_*: the MIN / MAX slot the tie word belongs to
   int32_t ties;                 // the program has S_TIE_* slots
+  // per-record changelog of one-window ops (k_pr_bucket -> k_pr_emit1): each
+  // record's state as the outputs read it -- fin_n slots (fin_slot) and, with
+  // fin_form, the row's literal-form word -- when that is fewer words than
+  // the state (LAST's sequence, tie words, decimal counts stay behind)
+  int32_t fin_n;
+  int32_t fin_form;
+  int32_t fin_slot[kMaxSlots];
 };
+// words per record of that projection
+__host__ __device__ inline int prog_fin_words(const Program &p) { return p.fin_n + p.fin_form; }
 
 // u64 division by an invariant divisor (Granlund–Montgomery), exact for all n.
 struct Divider {
@@ -272,6 +281,9 @@ inline bool prog_needs_seq(const Program &p) {
     if (p.slot_op[s] == S_LAST_SEQ || slot_is_tie(p.slot_op[s]) || p.slot_op[s] == S_LAST_FORM) return true;
   return false;
 }
+// the partitioned records carry the sequence word (hsg_dev.h seq_word: global
+// seq + 1 and the decimal-literal bits) for these ops
+inline bool prog_part_seq(const Program &p) { return prog_needs_seq(p) || prog_has_forms(p); }
 inline bool prog_has_tie(const Program &p) {
   for (int s = 0; s < p.n_slots; ++s)
     if (slot_is_tie(p.slot_op[s])) return true;

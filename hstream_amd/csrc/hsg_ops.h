@@ -80,6 +80,9 @@ struct OpDevice {
   int32_t user_cols = 0;        // value columns of the caller's batches (n_cols: the kernels', internal)
   bool forms = false;           // HSG_OPF_LITERAL_FORMS: rows carry literal forms (hsg_rows.form)
   uint64_t wpr = 1;             // max windows per record
+  bool sql_lean = false;        // per-batch LAST / literal-form op on the SQL lean kernels (k_agg_sql.hip)
+  uint64_t *tkeys = nullptr;    // touched-list group keys across a mid-batch table rebuild (grow-only)
+  uint64_t tkeys_cap = 0;
   uint64_t n_tiles_cap = 0;
   int64_t *tile_max = nullptr, *tile_min = nullptr, *tile_prefix = nullptr;
   // staging (host batches, exchange receive side)

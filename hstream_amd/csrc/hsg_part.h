@@ -130,6 +130,15 @@ void launch_seg_apply(hipStream_t s, dim3 g, const Program &prog, const TwParams
 bool launch_part_agg_lean(hipStream_t s, dim3 g, const Program &prog, const TwParams &p, const PartParams &pp,
                           const TwTable &t, const PartBuffers &pb, DevScalars *sc, const OutCols *out,
                           uint64_t out_base, uint64_t out_cap);
+// The SQL drop-in's op shape (LAST / literal-form slots, k_agg_sql.hip) on
+// packed one-window batches: records with their sequence word, the full slot
+// algebra; false when the shape has no such variant. A batch the kernels
+// cannot finish exactly (a split bucket, an overflowing chunk) leaves
+// DevScalars::scratch[35] set and changes nothing: the careful path runs it.
+bool sql_lean_eligible(const Program &prog, const PartParams &pp);
+bool launch_part_agg_sql(hipStream_t s, dim3 g, const Program &prog, const TwParams &p, const PartParams &pp,
+                         const TwTable &t, const PartBuffers &pb, DevScalars *sc, const OutCols *out,
+                         uint64_t out_base, uint64_t out_cap);
 // per-batch changelog rows of the groups in pb.touched
 void launch_part_emit(hipStream_t s, const TwTable &t, const Program &prog, const TwParams &p, const PartBuffers &pb,
                       OutCols out, uint64_t out_base, uint64_t out_cap, DevScalars *sc);

@@ -208,7 +208,9 @@ __global__ void k_x_info(DevScalars *sc, const uint64_t *bstart, int xl, uint32_
   info[2] = (int64_t)n;
   info[3] = has_valid;
   const uint32_t per = (1u << xl) / G;  // owner regions per rank (1 unless a test partitions finer)
-  for (uint32_t q = 0; q < G; ++q) info[4 + q] = (int64_t)(bstart[(q + 1) * per] - bstart[q * per]);
+  // an empty slice: the offsets pipeline did not run (no tiles), so bstart
+  // still holds the previous batch's owner runs -- this rank sends nothing
+  for (uint32_t q = 0; q < G; ++q) info[4 + q] = n ? (int64_t)(bstart[(q + 1) * per] - bstart[q * per]) : 0;
 }
 
 // every sent record at offt[tile][owner] + its slot in the tile's run, columnar

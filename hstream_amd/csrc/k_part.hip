@@ -501,7 +501,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter(Batch b, TwParams p, Part
       } else if ((int)wc < 2 + C) {
         v = (uint64_t)b.col[wc - 2][i];
       } else {
-        v = (uint64_t)((seq ? seq[i] : (int64_t)(p.rec_base + i)) + 1);
+        v = seq_word(b, C, pp.has_valid, seq ? seq[i] : (int64_t)(p.rec_base + i), i);
       }
       pb.rec[dest * W + w] = v;
     }
@@ -635,7 +635,8 @@ void launch_part_decide_offsets(hipStream_t s, DevScalars *sc, const TwParams &p
   launch_part_offsets(s, pp, pb, sc, &a);
 }
 
-// Staged scatter for packed records of <= 2 words (<= 1 column, no LAST): the
+// Staged scatter for packed records of <= 2 words (<= 1 column, no LAST), or
+// 3 words (one column and the sequence word of LAST / literal-form ops): the
 // walk reads every input column once, in arrival order; each record's packed
 // words go to its bucket-sorted slot of an LDS copy of the tile, written out
 // with consecutive lanes on consecutive records of a run (16-byte stores).
@@ -645,7 +646,7 @@ void launch_part_decide_offsets(hipStream_t s, DevScalars *sc, const TwParams &p
 // The bucket of a staged record is recomputed from its key at write-out.
 template <int T, int W, bool STABLE>
 __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, PartParams pp, PartBuffers pb,
-                                                          DevScalars *sc) {
+                                                          const int64_t *__restrict__ seq, DevScalars *sc) {
   // STABLE: wave w's running count of bucket b over its rounds, then the
   // exclusive prefix of those counts over the waves
   __shared__ uint16_t wcnt[STABLE ? kPW : 1][1 << kPartMaxLog2];
@@ -685,6 +686,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
     uint32_t key[R];
     int64_t ts[R];
     uint64_t col[R];
+    uint64_t sqw[W == 3 ? R : 1];  // W == 3: the sequence word (seq + 1 | literal bits << 56)
     // STABLE: each wave takes R*64 consecutive records (64 per round), so a
     // record's arrival rank needs no block barrier per round
     auto rec_i = [&](int r) -> uint64_t {
@@ -696,7 +698,8 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
       const bool in = i < b.n;
       key[r] = in ? b.key[i] : HSG_KEY_NONE;
       ts[r] = in ? b.ts[i] : 0;
-      col[r] = (W == 2 && in) ? (uint64_t)b.col[0][i] : 0;
+      col[r] = (W >= 2 && in) ? (uint64_t)b.col[0][i] : 0;
+      if constexpr (W == 3) sqw[r] = in ? seq_word(b, 1, pp.has_valid, seq ? seq[i] : (int64_t)(p.rec_base + i), i) : 0;
     }
     __syncthreads();  // counters clear
     uint32_t slot[R];  // bucket << 16 | slot in the sub-tile's run of the bucket, ~0 = no window
@@ -723,7 +726,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
       slot[r] = (bk << 16) | pos;
       const uint64_t i = rec_i(r);
       uint64_t vb = 0;
-      if (W == 2 && !(pp.has_valid && b.valid[0] && !b.valid[0][i])) vb = 1;
+      if (W >= 2 && !(pp.has_valid && b.valid[0] && !b.valid[0][i])) vb = 1;
       ts[r] = (int64_t)((uint64_t)key[r] | ((uint64_t)((krel - kbase) & 0xFFFFu) << 32) | ((uint64_t)nwin << 48) |
                         (vb << 56));  // the packed header word, kept in the ts register
     }
@@ -771,7 +774,8 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
       if (pb.pos) pb.pos[rec_i(r)] = cursor[sb] + rk;
       const uint32_t q = lstart[sb] + rk;
       stage[q * W] = (uint64_t)ts[r];
-      if (W == 2) stage[q * W + 1] = col[r];
+      if (W >= 2) stage[q * W + 1] = col[r];
+      if constexpr (W == 3) stage[q * W + 2] = sqw[r];
     }
     __syncthreads();
     q1 = phase_clock();
@@ -780,7 +784,12 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
       const uint64_t h = stage[q * W];
       const uint32_t bk = bucket_of((uint32_t)h, pp.np_log2, pp.bshift);
       const uint64_t dest = (uint64_t)cursor[bk] + (q - lstart[bk]);
-      if (W == 2) {
+      if (W == 3) {
+        uint64_t *o = pb.rec + dest * 3;
+        o[0] = h;
+        o[1] = stage[q * W + 1];
+        o[2] = stage[q * W + 2];
+      } else if (W == 2) {
         const uint64_t cc = stage[q * W + 1];
         *(ulonglong2 *)(pb.rec + dest * 2) = make_ulonglong2(h, cc);
       } else {
@@ -809,16 +818,22 @@ void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const
                          DevScalars *sc, bool maybe_packed, bool wide) {
   if (!pp.tiles) return;
   const dim3 g((unsigned)pp.tiles);
-  const bool stage = maybe_packed && !pp.has_seq && pp.words - 1 <= 2;  // packed words <= 2
+  // packed words <= 2, or 3 with the sequence word (one column)
+  const bool stage = maybe_packed && ((!pp.has_seq && pp.words - 1 <= 2) || (pp.has_seq && pp.words - 1 == 3));
   // the per-record changelog (pb.pos) needs arrival order inside a bucket's runs
   const bool stable = pb.pos != nullptr;
   if (stage) {
-    if (pp.words - 1 == 2) {
-      if (stable) hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 2, true>), g, dim3(kPNT), 0, s, b, p, pp, pb, sc);
-      else hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 2, false>), g, dim3(kPNT), 0, s, b, p, pp, pb, sc);
+    const dim3 th(kPNT);
+    if (pp.words - 1 == 3) {
+      // (half tiles: 48 KB of staging, two workgroups per CU)
+      if (stable) hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 3, true>), g, th, 0, s, b, p, pp, pb, seq, sc);
+      else hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 3, false>), g, th, 0, s, b, p, pp, pb, seq, sc);
+    } else if (pp.words - 1 == 2) {
+      if (stable) hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 2, true>), g, th, 0, s, b, p, pp, pb, seq, sc);
+      else hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 2, false>), g, th, 0, s, b, p, pp, pb, seq, sc);
     } else {
-      if (stable) hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 1, true>), g, dim3(kPNT), 0, s, b, p, pp, pb, sc);
-      else hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 1, false>), g, dim3(kPNT), 0, s, b, p, pp, pb, sc);
+      if (stable) hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 1, true>), g, th, 0, s, b, p, pp, pb, seq, sc);
+      else hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 1, false>), g, th, 0, s, b, p, pp, pb, seq, sc);
     }
   }
   if (wide || !stage) {
@@ -1072,8 +1087,19 @@ bool launch_part_agg(hipStream_t s, const Program &prog, const TwParams &p, cons
                      uint64_t out_base, uint64_t out_cap, bool wide, bool *lean) {
   bool took_lean = false;
   if (lean) *lean = false;
-  if (!part_supported(prog)) return false;
   const uint64_t nb = 1ull << pp.np_log2;
+  if (sql_lean_eligible(prog, pp)) {
+    // the SQL op shape: its lean kernels only (a wide or refused batch runs on
+    // the careful path, op_device.cpp push_time_atomic)
+    if (!maybe_packed) return false;
+    hipLaunchKernelGGL(k_part_chunks, dim3(1), dim3(1024), 0, s, pb.bstart, pp.np_log2, pp.chunk, pb.chunk_start,
+                       pb.chunk_bucket, sc);
+    const dim3 g((unsigned)(nb + n / pp.chunk + 1));
+    launch_part_agg_sql(s, g, prog, p, pp, t, pb, sc, out, out_base, out_cap);
+    if (lean) *lean = true;
+    return true;
+  }
+  if (!part_supported(prog)) return false;
   hipLaunchKernelGGL(k_part_chunks, dim3(1), dim3(1024), 0, s, pb.bstart, pp.np_log2, pp.chunk, pb.chunk_start,
                      pb.chunk_bucket, sc);
   const dim3 g((unsigned)(nb + n / pp.chunk + 1));

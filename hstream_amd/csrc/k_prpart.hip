@@ -65,7 +65,9 @@ struct PrRecView {
   __device__ uint32_t nwin() const { return pk ? (uint32_t)((w[0] >> 48) & 0xFFull) : (uint32_t)w[1]; }
   __device__ bool present(int c) const { return pk ? (w[0] >> (56 + c)) & 1ull : (w[1] >> (32 + c)) & 1ull; }
   __device__ int64_t col(int c) const { return (int64_t)w[(pk ? 1 : 2) + c]; }
-  __device__ int64_t seq1() const { return (int64_t)w[(pk ? 1 : 2) + C]; }
+  // the sequence word (hsg_dev.h seq_word): seq + 1, decimal-literal bits
+  __device__ int64_t seq1() const { return (int64_t)(w[(pk ? 1 : 2) + C] & kSeqMask); }
+  __device__ bool dec(int c) const { return (w[(pk ? 1 : 2) + C] >> (56 + c)) & 1ull; }
 };
 
 // contribution of the record to every slot (identity when the field is absent)
@@ -98,6 +100,10 @@ __device__ inline void pr_elems(const Program &prog, const RV &r, int64_t (&e)[M
       case S_MIN_F:
       case S_MAX_F: e[s] = (int64_t)f64_ord(__builtin_bit_cast(double, r.col(c))); break;
       case S_LAST_SEQ: e[s] = r.seq1(); break;
+      case S_CNT_DEC: e[s] = r.dec(c) ? 1 : 0; break;
+      case S_TIE_MIN:
+      case S_TIE_MAX:
+      case S_LAST_FORM: e[s] = (int64_t)(((uint64_t)r.seq1() << 1) | (r.dec(c) ? 0u : 1u)); break;
       default: break;
     }
   }
@@ -831,6 +837,12 @@ constexpr int kPbNW = kPbNT / 64;
 // slot ops baked in: the common aggregate sets get straight-line combines)
 template <int MS, class PV>
 __device__ inline void combine_v(const PV &pv, int64_t (&a)[MS], const int64_t (&e)[MS]) {
+  if constexpr (std::is_same<PV, ProgRT>::value) {
+    // a runtime program: tie words, the LAST pair and the form slots
+    // (combine_row; the baked programs have none of them)
+    combine_row<MS>(pv.p, a, e);
+    return;
+  }
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
     if (s >= pv.n()) break;
@@ -879,6 +891,10 @@ __device__ inline void elems_v(const PV &pv, const RV &r, int64_t (&e)[MS]) {
       case S_MIN_F:
       case S_MAX_F: e[s] = (int64_t)f64_ord(__builtin_bit_cast(double, r.col(c))); break;
       case S_LAST_SEQ: e[s] = r.seq1(); break;
+      case S_CNT_DEC: e[s] = r.dec(c) ? 1 : 0; break;
+      case S_TIE_MIN:
+      case S_TIE_MAX:
+      case S_LAST_FORM: e[s] = (int64_t)(((uint64_t)r.seq1() << 1) | (r.dec(c) ? 0u : 1u)); break;
       default: break;
     }
   }
@@ -937,7 +953,9 @@ struct PrRecRegs {
     return (int64_t)(k == 0 ? r0 : k == 1 ? r1 : k == 2 ? r2 : r3);
   }
   __device__ int64_t col(int c) const { return word((pk ? 1 : 2) + c); }
-  __device__ int64_t seq1() const { return word((pk ? 1 : 2) + C); }
+  // the sequence word (hsg_dev.h seq_word): seq + 1, decimal-literal bits
+  __device__ int64_t seq1() const { return (int64_t)((uint64_t)word((pk ? 1 : 2) + C) & kSeqMask); }
+  __device__ bool dec(int c) const { return ((uint64_t)word((pk ? 1 : 2) + C) >> (56 + c)) & 1ull; }
 };
 
 template <int MS, int LT, bool REG, uint64_t SIG>
@@ -1225,10 +1243,20 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
         for (int s = 0; s < MS; ++s) fin[s] = carry[s];
         combine_v<MS>(pv, fin, pre);
         // at the record's partitioned position: consecutive lanes, consecutive rows
-        int64_t *o = pr.fin + i * (uint64_t)ns;
+        if constexpr (SIG != 0) {
+          int64_t *o = pr.fin + i * (uint64_t)ns;
 #pragma unroll
-        for (int s = 0; s < MS; ++s)
-          if (s < ns) o[s] = fin[s];
+          for (int s = 0; s < MS; ++s)
+            if (s < ns) o[s] = fin[s];
+        } else {
+          // the words the row's outputs read (hsg_internal.h fin_*)
+          const int fw = prog.fin_n + prog.fin_form;
+          int64_t *o = pr.fin + i * (uint64_t)fw;
+#pragma unroll
+          for (int k = 0; k < MS; ++k)
+            if (k < prog.fin_n) o[k] = reg_at<MS>(fin, prog.fin_slot[k]);
+          if (prog.fin_form) o[prog.fin_n] = (int64_t)out_form_reg<MS>(prog, fin);
+        }
       }
       if (owner) {
         if (last) {
@@ -1306,8 +1334,10 @@ __global__ __launch_bounds__(kE1NT) void k_pr_emit1(Batch bt, Program prog, TwPa
   const int64_t k_epoch = sc->k_epoch;
   const int64_t *wm = rec_wm ? rec_wm : (sc->no_late ? nullptr : pb.wm);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int ns = prog.n_slots;
-  const int fw = ns;
+  // the state words k_pr_bucket left per record (hsg_internal.h fin_*; the
+  // baked programs: the whole state)
+  const int fw = prog_fin_words(prog) ;
+  const bool proj = prog.fin_n != prog.n_slots || prog.fin_form;
   uint32_t err = 0;
   // consecutive tiles on one XCD: their rows of a bucket are neighbours in pr.fin
   const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);
@@ -1354,6 +1384,27 @@ __global__ __launch_bounds__(kE1NT) void k_pr_emit1(Batch bt, Program prog, TwPa
       }
 #pragma unroll
       for (int s = 0; s < MS; ++s) R[u][s] = s < fw ? f[s] : 0;
+    }
+    // a projected state: back to slot positions (the form word stays at fin_n)
+    uint32_t F[kE1];
+#pragma unroll
+    for (int u = 0; u < kE1; ++u) {
+      F[u] = 0;
+      if (!proj) continue;
+      F[u] = prog.fin_form ? (uint32_t)reg_at<MS>(R[u], prog.fin_n) : 0u;
+      int64_t T[MS];
+#pragma unroll
+      for (int s = 0; s < MS; ++s) T[s] = 0;
+#pragma unroll
+      for (int k = 0; k < MS; ++k)
+        if (k < prog.fin_n) {
+          const int at = prog.fin_slot[k];
+#pragma unroll
+          for (int s = 0; s < MS; ++s)
+            if (s == at) T[s] = R[u][k];
+        }
+#pragma unroll
+      for (int s = 0; s < MS; ++s) R[u][s] = T[s];
     }
 #pragma unroll
     for (int u = 0; u < kE1; ++u) {
@@ -1410,7 +1461,7 @@ __global__ __launch_bounds__(kE1NT) void k_pr_emit1(Batch bt, Program prog, TwPa
 #pragma unroll
       for (int jj = 0; jj < kMaxAggs; ++jj)
         if (jj < prog.n_out) out.agg[jj][ob] = out_value_reg<MS>(prog, jj, R[u]);
-      if (out.form) out.form[ob] = out_form_reg<MS>(prog, R[u]);
+      if (out.form) out.form[ob] = proj && prog.fin_form ? F[u] : out_form_reg<MS>(prog, R[u]);
     }
   }
   if (err) atomicOr(&sc->err, err);
@@ -1880,7 +1931,11 @@ void launch_pr_part(hipStream_t s, const Batch &b, const Program &prog, const Tw
   if (prog.n_slots <= 2) pr_launch<2>(s, b, prog, p, pp, t, pb, pr, wpr, rec_wm, seq, out, out_base, out_cap, sc);
   else if (prog.n_slots <= 4) pr_launch<4>(s, b, prog, p, pp, t, pb, pr, wpr, rec_wm, seq, out, out_base, out_cap, sc);
   else if (prog.n_slots <= 6) pr_launch<6>(s, b, prog, p, pp, t, pb, pr, wpr, rec_wm, seq, out, out_base, out_cap, sc);
-  else pr_launch<8>(s, b, prog, p, pp, t, pb, pr, wpr, rec_wm, seq, out, out_base, out_cap, sc);
+  else if (prog.n_slots <= 8) pr_launch<8>(s, b, prog, p, pp, t, pb, pr, wpr, rec_wm, seq, out, out_base, out_cap, sc);
+  // the SQL drop-in's op shape (literal forms, a passthrough: C2's five
+  // aggregates take 11 slots)
+  else if (prog.n_slots <= 12) pr_launch<12>(s, b, prog, p, pp, t, pb, pr, wpr, rec_wm, seq, out, out_base, out_cap, sc);
+  else pr_launch<16>(s, b, prog, p, pp, t, pb, pr, wpr, rec_wm, seq, out, out_base, out_cap, sc);
 }
 
 }  // namespace hsg

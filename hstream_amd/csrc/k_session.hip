@@ -2659,6 +2659,11 @@ __global__ __launch_bounds__(kBrNT) __attribute__((amdgpu_waves_per_eu(HSG_BR_WP
         --left;
       }
       lds_barrier();
+    } else {
+      // the resident sessions this batch read and wrote (U of SURVEY.md 8d's
+      // 2*U*R), counted as in per-batch mode: one atomic per wave
+      const uint64_t e = wave_sum_u64(emitted);
+      if ((threadIdx.x & 63) == 0 && e) atomicAdd((unsigned long long *)&sc->touched, (unsigned long long)e);
     }
     }
     lds_barrier();

@@ -99,7 +99,7 @@ static void free_out(OutCols &o) {
 int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err) {
   PartBuffers &pb = d.part;
   const uint64_t n = d.batch_cap;
-  const int words = part_words(cfg.n_cols, has_last(prog));
+  const int words = part_words(cfg.n_cols, prog_part_seq(prog));
   const uint64_t tiles = part_tiles(n, part_tile_for(words)) + 1;
   const uint64_t nh = (1ull << kPartMaxLog2) * tiles;
   uint64_t off = 0;
@@ -172,7 +172,7 @@ static void adapt_partitions(OpDevice &d, const hsg_op_config &cfg, const Progra
     return w > by_size ? w : by_size;
   };
   uint64_t want = need(false);
-  d.agg_big = want > (1ull << kPartMaxLog2);
+  d.agg_big = want > (1ull << kPartMaxLog2) && !d.sql_lean;  // (the SQL lean kernels: one LDS variant)
   if (d.agg_big) want = need(true);
   int l = 0;
   while ((1ull << l) < want && l < kPartMaxLog2) ++l;
@@ -311,6 +311,16 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
   } else if (cfg.emit_mode == HSG_EMIT_PER_RECORD || (cfg.window_kind == HSG_SESSION && !d.ss_merge)) {
     rc = perrecord_device_init(d, cfg, prog, err);
     if (rc != HSG_OK) return rc;
+  } else if ((cfg.window_kind == HSG_TUMBLING || cfg.window_kind == HSG_UNWINDOWED) && prog_part_seq(prog) &&
+             (cfg.n_cols == 1 || cfg.n_cols == 2) && prog.n_slots <= 16) {
+    // the SQL drop-in's op shape (LAST passthroughs, literal forms) of one-window
+    // ops: packed records with their sequence word on the SQL lean kernels
+    // (k_agg_sql.hip); a batch they refuse runs on the record kernels
+    d.use_part = true;
+    d.sql_lean = true;
+    d.pane_S = 1;
+    rc = part_device_init(d, cfg, prog, err);
+    if (rc != HSG_OK) return rc;
   } else if (part_supported(prog)) {
     d.use_part = true;
     {
@@ -380,6 +390,9 @@ void op_device_free(OpDevice &d) {
   d.scratch = nullptr;
   if (d.part_mem) hipFree(d.part_mem);
   d.part_mem = nullptr;
+  if (d.tkeys) hipFree(d.tkeys);
+  d.tkeys = nullptr;
+  d.tkeys_cap = 0;
   if (d.xsend) hipFree(d.xsend);
   if (d.xrecv) hipFree(d.xrecv);
   d.xsend = d.xrecv = nullptr;
@@ -695,7 +708,13 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
   // The first batch after create/reset has no epoch yet: k_epoch_first sets it
   // (device side) from the batch's first keyed record ahead of the optimistic
   // kernels, which then run as on every later batch.
-  const bool opt = d.use_part && !rec_wm && !has_last(prog) && cfg.grace_ms >= 0 && cfg.window_kind != HSG_SESSION;
+  // the SQL lean kernels (d.sql_lean) run only optimistic packed batches; a
+  // batch they refuse (late records, a wide layout, a split bucket or an
+  // overflowing chunk: scratch[35]) runs again on the record kernels
+  // (k_window.hip k_tw_agg and its LAST / tie resolution pass)
+  const bool sql = d.sql_lean;
+  const bool opt = d.use_part && !rec_wm && (!has_last(prog) || sql) && cfg.grace_ms >= 0 &&
+                   cfg.window_kind != HSG_SESSION;
   const bool need_epoch = !d.h_sc->epoch_set;
   // Table room (see table_bound_hint): the partition path's claiming kernels
   // check the batch against pp.room (3/4 load) before they claim anything --
@@ -718,6 +737,7 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
   PartParams last_pp;
   memset(&last_pp, 0, sizeof(last_pp));
   auto run = [&](bool optimistic) -> int {
+    skipped_wide = skipped_emit = false;  // (this run's launch prediction)
     int rc = clear_batch_scalars(d, err);
     if (rc != HSG_OK) return rc;
     if (!kb.n) return HSG_OK;
@@ -728,13 +748,14 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     if (!optimistic) launch_stream_time(d, cfg, kb, a.wm_in, p.adv);
     else if (need_epoch) launch_epoch_first(d.stream, kb, p.adv, d.sc);
     DTRY(hipEventRecord(d.ev_a, d.stream));
-    if (d.use_part) {
+    const bool part_now = d.use_part && (!sql || optimistic);
+    if (part_now) {
       PartParams pp;
       memset(&pp, 0, sizeof(pp));
       pp.np_log2 = d.np_log2;
       pp.bshift = d.bshift;
       for (int c = 0; c < cfg.n_cols; ++c) pp.has_valid |= kb.valid[c] != nullptr;
-      pp.has_seq = has_last(prog);
+      pp.has_seq = prog_part_seq(prog);
       pp.words = part_words(cfg.n_cols, pp.has_seq);
       pp.tile = part_tile_for(pp.words);
       pp.sub = optimistic ? kRowSub : 1;  // offsets rows of kRowSub tiles (the careful path: one)
@@ -756,7 +777,8 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       else
         launch_part_offsets(d.stream, pp, d.part, d.sc);
       skipped_wide = can_pack && d.pred_packed && part_lean_eligible(prog, pp);
-      launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc, can_pack, !skipped_wide);
+      // (the SQL kernels have no wide variant: a wide batch runs again carefully)
+      launch_part_scatter(d.stream, kb, p, pp, rec_wm, d.part.wm, seq, d.part, d.sc, can_pack, !skipped_wide && !sql);
       const bool emit_batch = cfg.emit_mode == HSG_EMIT_PER_BATCH;
       bool lean = false;
       wait_table_reset(d);  // the partition passes above do not touch the table
@@ -768,9 +790,10 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
       wait_table_reset(d);
       launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, false);
     }
-    if (has_last(prog)) launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, true);
+    if (has_last(prog) && !(sql && part_now))
+      launch_tw_agg(d.stream, kb, p, d.tw, prog, d.tile_prefix, rec_wm, seq, d.sc, true);
     if (cfg.emit_mode == HSG_EMIT_PER_BATCH) {
-      if (d.use_part) {
+      if (part_now) {
         if (!skipped_emit) launch_part_emit(d.stream, d.tw, prog, p, d.part, d.out, a.pending, d.out_cap, d.sc);
       } else {
         launch_tw_emit(d.stream, d.tw, d.tw.slots(), prog, p, 0, d.out, a.pending, d.out_cap, d.sc, d.emit,
@@ -798,17 +821,18 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     const uint64_t t0 = cfg.emit_mode == HSG_EMIT_PER_BATCH
                             ? (keep.scratch[1] < d.part.touched_cap ? keep.scratch[1] : d.part.touched_cap)
                             : 0;
-    uint64_t *tkeys = nullptr;
-    struct KeysFree {
-      uint64_t *&p;
-      ~KeysFree() {
-        if (p) hipFree(p);
-      }
-    } kf{tkeys};
-    if (t0) {
-      DTRY(hipMalloc((void **)&tkeys, t0 * sizeof(uint64_t)));
-      launch_touch_keys(d.stream, d.tw, d.part.touched, t0, tkeys);
+    // (a grow-only buffer kept with the op: no hipFree, and its device-wide
+    // synchronisation, on this path; tw_maintain's rebuild allocates anyway)
+    if (t0 > d.tkeys_cap) {
+      if (d.tkeys) hipFree(d.tkeys);
+      d.tkeys = nullptr;
+      d.tkeys_cap = 0;
+      const uint64_t want = t0 > d.part.touched_cap / 8 ? t0 : d.part.touched_cap / 8;
+      DTRY(hipMalloc((void **)&d.tkeys, want * sizeof(uint64_t)));
+      d.tkeys_cap = want;
     }
+    uint64_t *tkeys = d.tkeys;
+    if (t0) launch_touch_keys(d.stream, d.tw, d.part.touched, t0, tkeys);
     int rc = tw_maintain(d, cfg, prog, kb.n, a.wm_in, a.pending, err, bound);
     if (rc != HSG_OK) return rc;
     if (t0) launch_touch_slots(d.stream, d.tw, tkeys, t0, d.part.touched);
@@ -874,7 +898,14 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
   const uint64_t live0 = d.h_sc->live;  // rows before the batch (after its tw_maintain)
   int rc = run_room(opt);
   if (rc != HSG_OK) return rc;
-  if (opt && kb.n && d.h_sc->redo) {
+  const bool sql_refused = sql && opt && kb.n && (!d.h_sc->packed || d.h_sc->scratch[35]);
+  if (sql_refused) d.replays += 1;  // (hsg_stats: a lean SQL batch is counted in lean_batches)
+  if (opt && kb.n && (d.h_sc->redo || sql_refused)) {
+    if (sql) {
+      // the record kernels check no table room: the batch's worst case first
+      rc = tw_maintain(d, cfg, prog, kb.n, a.wm_in, a.pending, err, UINT64_MAX);
+      if (rc != HSG_OK) return rc;
+    }
     rc = run_room(false);
   } else if (kb.n && skipped_wide && !d.h_sc->packed) {
     d.pred_packed = false;  // a wide batch: nothing was aggregated, run it with every variant
@@ -882,7 +913,7 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     rc = run_room(opt);
   }
   const uint64_t groups = d.h_sc->scratch[0];
-  if (kb.n && d.use_part) {
+  if (kb.n && d.use_part && !(sql && (d.h_sc->redo || sql_refused))) {
     d.pred_packed = d.h_sc->packed != 0;
     const uint64_t how = d.h_sc->scratch[2];  // 1/2 lean, 3/4 deferred; odd: changelog written directly
     d.pred_direct = how == 1 || how == 3;
@@ -933,6 +964,7 @@ static uint64_t table_bound_hint(const OpDevice &d, const hsg_op_config &cfg, co
   // deferred ones: a superset of its new groups); the first batch, whose
   // in-kernel updates have no check of their own, gets the worst case
   if (defer_room_checked(d, cfg, prog)) return d.defer_pred ? d.defer_pred : UINT64_MAX;
+  if (d.sql_lean) return cfg.grace_ms >= 0 ? d.lean_pred : UINT64_MAX;  // k_sql_apply checks its partials
   if (!d.use_part || has_last(prog) || cfg.emit_mode == HSG_EMIT_PER_RECORD || cfg.grace_ms < 0 ||
       cfg.window_kind == HSG_SESSION || cfg.n_cols > 8 || d.wpr >= 256)
     return UINT64_MAX;
@@ -953,9 +985,11 @@ int op_push(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const Pu
     int rc = tw_maintain(d, cfg, prog, b->n, a.wm_in, a.pending, err, table_bound_hint(d, cfg, prog));
     if (rc != HSG_OK) return rc;
   }
-  // the changelog must have room for the worst case of this batch
-  if (cfg.emit_mode != HSG_EMIT_NONE) {
-    uint64_t bound = b->n * (uint64_t)a.nranks * d.wpr;
+  // the changelog must have room for the worst case of this batch (sharded
+  // ops: decided after the all-gather, from the records each rank will own and
+  // every rank's room, uniformly on all ranks -- exchange.cpp check_room)
+  if (cfg.emit_mode != HSG_EMIT_NONE && !a.comm) {
+    uint64_t bound = b->n * d.wpr;
     if (cfg.emit_mode == HSG_EMIT_PER_BATCH && cfg.window_kind != HSG_SESSION && bound > d.cap) bound = d.cap;
     if (a.pending + bound > d.out_cap) {
       err = "changelog buffer full: drain before pushing (out_capacity)";

@@ -90,10 +90,13 @@ int perrecord_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &
 // Per-record changelog on the partitioned pipeline (k_prpart.hip): ops with
 // <= 8 state slots and < 256 windows per record. Others: the sort path below.
 // ---------------------------------------------------------------------------
-// LAST, or literal-form slots: the records' global sequence numbers are needed
-static bool has_last_slot(const Program &prog) { return prog_needs_seq(prog); }
+// LAST, or literal-form slots: the records' sequence words (global seq +
+// literal bits) ride in the partitioned records
+static bool has_last_slot(const Program &prog) { return prog_part_seq(prog); }
 
-bool perrecord_part_eligible(const Program &prog, uint64_t wpr) { return part_supported(prog) && wpr < 256; }
+// the per-record kernels fold with the full slot algebra (combine_row: the
+// LAST pair, tie words, literal-form slots), up to 16 slots
+bool perrecord_part_eligible(const Program &prog, uint64_t wpr) { return prog.n_slots <= 16 && wpr < 256; }
 
 int perrecord_part_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, std::string &err) {
   int rc = part_device_init(d, cfg, prog, err);
@@ -116,7 +119,7 @@ int perrecord_part_init(OpDevice &d, const hsg_op_config &cfg, const Program &pr
     x.ccnt = c.take<uint32_t>(chunks);
     x.counter = c.take<uint64_t>(8);
     x.partial = c.take<uint64_t>(scan_partials_needed(tiles) + 8);
-    x.fin = c.take<int64_t>(wpr == 1 ? n * ns : 1);
+    x.fin = c.take<int64_t>(wpr == 1 ? n * (uint64_t)prog_fin_words(prog) : 1);
     x.krec = c.take<uint64_t>(wpr == 1 ? 1 : n * (uint64_t)part_words(cfg.n_cols, true));
     x.kpos = c.take<uint32_t>(wpr == 1 ? 1 : n);
     x.roff = c.take<uint64_t>(wpr == 1 ? 1 : n);

@@ -306,6 +306,38 @@ def test_exchange_path_single_rank(xeng, spec, late, xpart):
     assert st["records_owned"] == sum(int((b[0] != abi.HSG_KEY_NONE).sum()) for b in batches)
 
 
+@pytest.mark.parametrize("xpart", [None, "2", "classic"], ids=["xpart1", "xpart4", "classic"])
+@pytest.mark.parametrize("spec", _x_specs())
+def test_exchange_path_empty_batch_between(xeng, spec, xpart):
+    """An empty batch between non-empty ones through the exchange path: the
+    empty slice runs no offsets pipeline, so its owner counts must be zero,
+    not the previous batch's (the stale runs were sent again and
+    re-aggregated)."""
+    from hstream_amd.engine import testing_knob
+    batches = []
+    for bi in range(3):
+        key, ts, cols, valid = gen_small(2100 + bi, 4000, 29, col_types=spec.col_types, span=60_000,
+                                         base=5_000_000 + bi * 60_000, very_late=False)
+        batches.append((key, ts, cols, valid))
+    key, ts, cols, valid = batches[0]
+    batches.insert(1, (key[:0], ts[:0], [c[:0] for c in cols], [v[:0] for v in valid]))
+    with testing_knob(abi.HSG_KNOB_XPART_LOG2, int(xpart) if xpart and xpart != "classic" else -1), \
+            testing_knob(abi.HSG_KNOB_X_CLASSIC, 1 if xpart == "classic" else 0):
+        g = xeng.op(spec)
+    o = pyoracle.OracleOp(spec)
+    f64 = spec.agg_is_f64()
+    wg = wo = -1
+    for bi, (key, ts, cols, valid) in enumerate(batches):
+        wg = g.push(key, ts, cols, valid, watermark=wg)
+        wo = o.push(key, ts, cols, valid, watermark=wo)
+        assert wg == wo
+        if spec.emit_mode != abi.HSG_EMIT_NONE:
+            rows_equal(g.drain(), o.drain(), f64, ordered=spec.emit_mode == abi.HSG_EMIT_PER_RECORD,
+                       what=f"batch {bi}")
+    rows_equal(g.dump_state(), o.dump_state(), f64, what="state")
+    assert g.stats()["records_owned"] == sum(int((b[0] != abi.HSG_KEY_NONE).sum()) for b in batches)
+
+
 @pytest.mark.parametrize("kind,kw", [(abi.HSG_TUMBLING, dict(size_ms=10_000)),
                                      (abi.HSG_HOPPING, dict(size_ms=10_000, advance_ms=3_000)),
                                      (abi.HSG_UNWINDOWED, {})], ids=["tumbling", "hopping", "unwindowed"])

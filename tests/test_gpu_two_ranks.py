@@ -43,6 +43,18 @@ def _rows(spec, r):
              tuple(a[i].item() for a in r.aggs)) for i in range(len(r))]
 
 
+def _slices(G, late):
+    """the protocol test's batches; "empty": rank 0's slice of the middle batch
+    is empty (between non-empty ones: its owner runs must not be the previous
+    batch's)"""
+    if late != "empty":
+        return _batches(G, late)
+    out = _batches(G, False)
+    key, ts, cols, valid = out[1][0]
+    out[1][0] = (key[:0], ts[:0], [c[:0] for c in cols], [v[:0] for v in valid])
+    return out
+
+
 def _gpu_worker(rank, G, name, spec_name, late, q):
     try:
         from hstream_amd.engine import Engine
@@ -51,7 +63,7 @@ def _gpu_worker(rank, G, name, spec_name, late, q):
         spec = GPU_SPECS[spec_name]
         op = eng.op(spec)
         wm, results = -1, []
-        for slices in _batches(G, late):
+        for slices in _slices(G, late):
             key, ts, cols, valid = slices[rank]
             wm = op.push(key, ts, cols, valid, watermark=wm)
             results.append(None if spec.emit_mode == abi.HSG_EMIT_NONE else _rows(spec, op.drain()))
@@ -68,7 +80,7 @@ def _single(spec_name, G, late):
     spec = GPU_SPECS[spec_name]
     op = pyoracle.OracleOp(spec)
     wm, results = -1, []
-    for slices in _batches(G, late):
+    for slices in _slices(G, late):
         key = np.concatenate([s[0] for s in slices])
         ts = np.concatenate([s[1] for s in slices])
         cols = [np.concatenate([s[2][c] for s in slices]) for c in range(2)]
@@ -78,7 +90,7 @@ def _single(spec_name, G, late):
     return wm, results, op.dump_state().tuples()
 
 
-@pytest.mark.parametrize("late", [False, True], ids=["no_late", "late"])
+@pytest.mark.parametrize("late", [False, True, "empty"], ids=["no_late", "late", "empty_slice"])
 @pytest.mark.parametrize("spec_name", list(GPU_SPECS))
 def test_two_ranks_equal_single_stream(spec_name, late):
     import multiprocessing as mp
