@@ -28,31 +28,73 @@ struct ProgRT {
   __device__ int col(int s) const { return p.slot_col[s]; }
 };
 
-template <uint64_t SIG>
+template <uint64_t SIG, uint64_t SIG2 = 0>
 struct ProgSig {
+  // slot s's 7-bit code: slots 0..8 in SIG, 9..17 in SIG2 (programs of more
+  // than 9 slots: the SQL drop-in's shape, literal forms and a passthrough)
+  static constexpr uint32_t code(int s) {
+    return s < 9 ? (uint32_t)((SIG >> (7 * s)) & 127u) : (uint32_t)((SIG2 >> (7 * (s - 9))) & 127u);
+  }
   static constexpr int count() {
     int k = 0;
-    while (k < 8 && ((SIG >> (7 * k)) & 15u) != 0) ++k;
+    while (k < 18 && (code(k) & 15u) != 0) ++k;
     return k;
+  }
+  static constexpr int op_of(int s) { return (int)(code(s) & 15u) - 1; }
+  static constexpr int col_of(int s) { return (int)((code(s) >> 4) & 7u); }
+  // the MIN / MAX slot a tie-word slot breaks ties of (build_program: the
+  // one MIN (MAX) slot over the same column)
+  static constexpr int aux_of(int s) {
+    const int want = op_of(s) == S_TIE_MIN ? 0 : 1;
+    for (int k = 0; k < count(); ++k) {
+      const int o = op_of(k);
+      const bool mn = o == S_MIN_I || o == S_MIN_F, mx = o == S_MAX_I || o == S_MAX_F;
+      if (((want == 0 && mn) || (want == 1 && mx)) && col_of(k) == col_of(s)) return k;
+    }
+    return 0;
+  }
+  static constexpr bool has_ties() {
+    for (int k = 0; k < count(); ++k)
+      if (op_of(k) == S_TIE_MIN || op_of(k) == S_TIE_MAX) return true;
+    return false;
   }
   __device__ ProgSig() {}
   __device__ explicit ProgSig(const Program &) {}
   __device__ constexpr int n() const { return count(); }
-  __device__ constexpr int op(int s) const { return (int)((SIG >> (7 * s)) & 15u) - 1; }
-  __device__ constexpr int col(int s) const { return (int)((SIG >> (7 * s + 4)) & 7u); }
+  __device__ constexpr int op(int s) const { return op_of(s); }
+  __device__ constexpr int col(int s) const { return col_of(s); }
 };
 
-template <uint64_t SIG>
-using ProgView = typename std::conditional<SIG == 0, ProgRT, ProgSig<SIG>>::type;
+template <uint64_t SIG, uint64_t SIG2 = 0>
+using ProgView = typename std::conditional<SIG == 0, ProgRT, ProgSig<SIG, SIG2>>::type;
 
-// signature of a runtime program (0: not expressible)
-inline uint64_t program_sig(const Program &p) {
-  if (p.n_slots > 8) return 0;
-  uint64_t sig = 0;
+// tie-word helpers over either view
+__device__ inline int pv_aux(const ProgRT &pv, int s) { return pv.p.slot_aux[s]; }
+__device__ inline bool pv_ties(const ProgRT &pv) { return pv.p.ties != 0; }
+template <uint64_t SIG, uint64_t SIG2>
+__device__ constexpr int pv_aux(const ProgSig<SIG, SIG2> &, int s) { return ProgSig<SIG, SIG2>::aux_of(s); }
+template <uint64_t SIG, uint64_t SIG2>
+__device__ constexpr bool pv_ties(const ProgSig<SIG, SIG2> &) { return ProgSig<SIG, SIG2>::has_ties(); }
+
+// signature of a runtime program (0: not expressible); slots past the ninth
+// go to *sig2 when it is given (else such a program has no signature)
+inline uint64_t program_sig(const Program &p, uint64_t *sig2 = nullptr) {
+  if (p.n_slots > (sig2 ? 18 : 8)) return 0;
+  uint64_t sig = 0, hi = 0;
   for (int s = 0; s < p.n_slots; ++s) {
     if (p.slot_op[s] < 0 || p.slot_op[s] > 14 || p.slot_col[s] < 0 || p.slot_col[s] > 7) return 0;
-    sig |= (uint64_t)((p.slot_op[s] + 1) | (p.slot_col[s] << 4)) << (7 * s);
+    // (a tie word's MIN / MAX slot is implied: the one over its column)
+    if (slot_is_tie(p.slot_op[s])) {
+      const int v = p.slot_aux[s], vo = p.slot_op[v];
+      const bool ok = p.slot_col[v] == p.slot_col[s] &&
+                      (p.slot_op[s] == S_TIE_MIN ? (vo == S_MIN_I || vo == S_MIN_F) : (vo == S_MAX_I || vo == S_MAX_F));
+      if (!ok) return 0;
+    }
+    const uint64_t c = (uint64_t)((p.slot_op[s] + 1) | (p.slot_col[s] << 4));
+    if (s < 9) sig |= c << (7 * s);
+    else hi |= c << (7 * (s - 9));
   }
+  if (sig2) *sig2 = hi;
   return sig;
 }
 
@@ -829,6 +871,29 @@ constexpr uint64_t kSigCnt = sig_ops({S_CNT_ALL});
 constexpr uint64_t kSigCntSumI = sig_ops({S_CNT_ALL, S_SUM_I});
 constexpr uint64_t kSigCntSumF = sig_ops({S_CNT_ALL, S_SUM_F});
 constexpr uint64_t kSigSumMaxI = sig_ops({S_SUM_I, S_MAX_I});
+// the SQL drop-in's C2 query, `SELECT v, COUNT(*), SUM(v), AVG(v), MIN(v),
+// MAX(v)` with literal forms (build_program's slot order): the passthrough's
+// LAST pair and form, COUNT(*), SUM and its decimal count, COUNT(v), MIN / MAX
+// with their tie words -- eleven slots, the last two in the second word
+constexpr uint64_t sig_ops_at(std::initializer_list<int> ops, int first) {
+  uint64_t sig = 0;
+  int k = 0;
+  for (int op : ops) {
+    if (k >= first && k < first + 9) sig |= (uint64_t)(op + 1) << (7 * (k - first));
+    ++k;
+  }
+  return sig;
+}
+#define HSG_SQL_C2_OPS(SUM, MIN, MAX) \
+  {S_LAST_SEQ, S_LAST_VAL, S_LAST_FORM, S_CNT_ALL, SUM, S_CNT_DEC, S_CNT, MIN, S_TIE_MIN, MAX, S_TIE_MAX}
+constexpr uint64_t kSigSqlI = sig_ops_at(HSG_SQL_C2_OPS(S_SUM_I, S_MIN_I, S_MAX_I), 0);
+constexpr uint64_t kSigSqlI2 = sig_ops_at(HSG_SQL_C2_OPS(S_SUM_I, S_MIN_I, S_MAX_I), 9);
+constexpr uint64_t kSigSqlF = sig_ops_at(HSG_SQL_C2_OPS(S_SUM_F, S_MIN_F, S_MAX_F), 0);
+constexpr uint64_t kSigSqlF2 = sig_ops_at(HSG_SQL_C2_OPS(S_SUM_F, S_MIN_F, S_MAX_F), 9);
+#undef HSG_SQL_C2_OPS
+static_assert(ProgSig<kSigSqlI, kSigSqlI2>::count() == 11 && ProgSig<kSigSqlI, kSigSqlI2>::aux_of(8) == 7 &&
+                  ProgSig<kSigSqlI, kSigSqlI2>::aux_of(10) == 9,
+              "SQL C2 signature");
 
 // the state-slot class (k_agg_s{2,4,6,8}.hip) a program of n slots runs in
 constexpr int ms_class(int n) { return n <= 2 ? 2 : n <= 4 ? 4 : n <= 6 ? 6 : 8; }

@@ -81,6 +81,7 @@ struct OpDevice {
   bool forms = false;           // HSG_OPF_LITERAL_FORMS: rows carry literal forms (hsg_rows.form)
   uint64_t wpr = 1;             // max windows per record
   bool sql_lean = false;        // per-batch LAST / literal-form op on the SQL lean kernels (k_agg_sql.hip)
+  int sql_skip = 0;             // batches left that skip the SQL lean kernels (refused at the most buckets)
   uint64_t *tkeys = nullptr;    // touched-list group keys across a mid-batch table rebuild (grow-only)
   uint64_t tkeys_cap = 0;
   uint64_t n_tiles_cap = 0;

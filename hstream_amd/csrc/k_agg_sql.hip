@@ -81,15 +81,15 @@ __device__ inline bool sql_chunk(const PartParams &pp, const PartBuffers &pb, ui
 }
 
 // phase 1 of one record on LDS entry e (slot-major, ST entries per slot)
-template <int MS, int ST, int W>
-__device__ inline void sql_phase1(const Program &prog, int64_t *__restrict__ agg, const PRec<W, true> &r,
+template <int MS, int ST, int W, class PV>
+__device__ inline void sql_phase1(const PV &pv, int64_t *__restrict__ agg, const PRec<W, true> &r,
                                   uint32_t skip) {
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
-    if (s >= prog.n_slots) break;
-    const int op = prog.slot_op[s];
+    if (s >= pv.n()) break;
+    const int op = pv.op(s);
     if (op == S_LAST_VAL || slot_is_tie(op) || ((skip >> s) & 1u)) continue;
-    const int c = prog.slot_col[s];
+    const int c = pv.col(s);
     if (op != S_CNT_ALL && !r.present(c)) continue;
     int64_t *a = agg + s * ST;
     unsigned long long *u = (unsigned long long *)a;
@@ -130,10 +130,11 @@ __device__ inline void sql_phase1(const Program &prog, int64_t *__restrict__ agg
         // (to "no word yet": above every word for a MIN's atomic min -- its
         // identity, seq 0, is the initial value's word and would win every
         // tie -- below every word for a MAX's atomic max)
-        if (moved && prog.ties) {
-          for (int k = 0; k < prog.n_slots && k < MS; ++k)
-            if (slot_is_tie(prog.slot_op[k]) && prog.slot_aux[k] == s)
-              agg[k * ST] = prog.slot_op[k] == S_TIE_MIN ? (int64_t)~0ull : 0;
+        if (moved && pv_ties(pv)) {
+#pragma unroll
+          for (int k = 0; k < MS; ++k)
+            if (k < pv.n() && slot_is_tie(pv.op(k)) && pv_aux(pv, k) == s)
+              agg[k * ST] = pv.op(k) == S_TIE_MIN ? (int64_t)~0ull : 0;
         }
         break;
       }
@@ -143,19 +144,19 @@ __device__ inline void sql_phase1(const Program &prog, int64_t *__restrict__ agg
 
 // phase 2: the LAST value of the group's last record, the tie words of the
 // records holding the group's extreme
-template <int MS, int ST, int W>
-__device__ inline void sql_phase2(const Program &prog, int64_t *__restrict__ agg, const PRec<W, true> &r) {
+template <int MS, int ST, int W, class PV>
+__device__ inline void sql_phase2(const PV &pv, int64_t *__restrict__ agg, const PRec<W, true> &r) {
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
-    if (s >= prog.n_slots) break;
-    const int op = prog.slot_op[s];
-    const int c = prog.slot_col[s];
+    if (s >= pv.n()) break;
+    const int op = pv.op(s);
+    const int c = pv.col(s);
     if (op == S_LAST_VAL) {
       // the preceding slot is its LAST_SEQ (build_program last_pair)
       if (s > 0 && r.present(c) && (uint64_t)agg[(s - 1) * ST] == (uint64_t)r.seq1()) agg[s * ST] = r.col(c);
     } else if (slot_is_tie(op)) {
       if (!r.present(c)) continue;
-      const int v = prog.slot_aux[s], vop = prog.slot_op[v];
+      const int v = pv_aux(pv, s), vop = pv.op(v);
       const int64_t x = r.col(c);
       const int64_t xv = (vop == S_MIN_F || vop == S_MAX_F) ? (int64_t)f64_ord(__builtin_bit_cast(double, x)) : x;
       if (agg[v * ST] != xv) continue;
@@ -167,10 +168,11 @@ __device__ inline void sql_phase2(const Program &prog, int64_t *__restrict__ agg
   }
 }
 
-template <int MS, int E, int NT, int W>
+template <int MS, int E, int NT, int W, uint64_t SIG = 0, uint64_t SIG2 = 0>
 __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwTable t, PartBuffers pb,
                                                 DevScalars *sc) {
-  constexpr int RB = 2;  // records per thread per block
+  const ProgView<SIG, SIG2> pv(prog);  // the SQL C2 query's slot program baked in (else the runtime one)
+  constexpr int RB = 4;  // records per thread per block (one block in flight beside it)
   __shared__ uint64_t lkey[E];
   __shared__ int64_t lagg[MS * E];
   __shared__ uint32_t s_cnt, s_ovf, s_fill;
@@ -180,7 +182,7 @@ __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwT
   uint64_t r0, r1;
   bool exclusive;
   if (!sql_chunk(pp, pb, r0, r1, exclusive)) return;  // uniform
-  const int ns = prog.n_slots;
+  const int ns = pv.n();
   const int PW = 1 + ns;  // partial words
   const int C = W - 2;    // packed: header, C columns, sequence word
   const uint32_t kbase = (uint32_t)sc->kbase;
@@ -194,18 +196,18 @@ __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwT
   int cnt_all_slot = -1;
   uint32_t skip = 0;
   for (int s = 0; s < ns && s < MS; ++s)
-    if (prog.slot_op[s] == S_CNT_ALL && cnt_all_slot < 0) cnt_all_slot = s;
+    if (pv.op(s) == S_CNT_ALL && cnt_all_slot < 0) cnt_all_slot = s;
   if (!pp.has_valid && cnt_all_slot >= 0)
     for (int s = 0; s < ns && s < MS; ++s)
-      if (prog.slot_op[s] == S_CNT) skip |= 1u << s;
-  bool two = prog.ties != 0, need2 = prog.ties != 0;
-  for (int s = 0; s < ns && s < MS; ++s) need2 |= prog.slot_op[s] == S_LAST_VAL;
+      if (pv.op(s) == S_CNT) skip |= 1u << s;
+  bool two = pv_ties(pv), need2 = pv_ties(pv);
+  for (int s = 0; s < ns && s < MS; ++s) need2 |= pv.op(s) == S_LAST_VAL;
   for (int k = threadIdx.x; k < kSqlSortBins; k += NT) s_bin[k] = 0;
   for (int e = threadIdx.x; e < E; e += NT) {
     lkey[e] = kEmpty;
 #pragma unroll
     for (int s = 0; s < MS; ++s)
-      if (s < ns) lagg[s * E + e] = slot_identity_dev(prog.slot_op[s]);
+      if (s < ns) lagg[s * E + e] = slot_identity_dev(pv.op(s));
   }
   if (threadIdx.x == 0) {
     s_cnt = 0;
@@ -214,17 +216,24 @@ __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwT
   }
   __syncthreads();
 
-  for (uint64_t s0 = r0; s0 < r1; s0 += (uint64_t)RB * NT) {
-    PRec<W, true> rec[RB];
-    int ent[RB];
+  // records: block k holds records r0 + k*RB*NT + u*NT + tid; the next block's
+  // loads are issued before the current one is processed (k_agg_lean.hip)
+  PRec<W, true> rec[RB], nxt[RB];
+  auto load = [&](uint64_t s0, PRec<W, true>(&d)[RB]) {
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
       const uint64_t i = s0 + (uint64_t)u * NT + threadIdx.x;
-      rec[u].C = C;
+      d[u].C = C;
 #pragma unroll
-      for (int q = 0; q < W; ++q) rec[u].w[q] = i < r1 ? pb.rec[i * W + q] : 0;
-      if (i >= r1) rec[u].w[0] = kEmpty;
+      for (int q = 0; q < W; ++q) d[u].w[q] = i < r1 ? pb.rec[i * W + q] : 0;
+      if (i >= r1) d[u].w[0] = kEmpty;
     }
+  };
+  load(r0, rec);
+  for (uint64_t s0 = r0; s0 < r1; s0 += (uint64_t)RB * NT) {
+    const bool more = s0 + (uint64_t)RB * NT < r1;  // uniform
+    if (more) load(s0 + (uint64_t)RB * NT, nxt);
+    int ent[RB];
     // phase 1
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
@@ -252,7 +261,7 @@ __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwT
         }
         h = (h + 1) & (E - 1);
       }
-      if (ent[u] >= 0) sql_phase1<MS, E, W>(prog, &lagg[ent[u]], r, skip);
+      if (ent[u] >= 0) sql_phase1<MS, E, W>(pv, &lagg[ent[u]], r, skip);
       else s_ovf = 1;  // the table is full: the batch takes the careful path
     }
     if (need2) {
@@ -260,8 +269,12 @@ __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwT
       // phase 2
 #pragma unroll
       for (int u = 0; u < RB; ++u)
-        if (ent[u] >= 0) sql_phase2<MS, E, W>(prog, &lagg[ent[u]], rec[u]);
+        if (ent[u] >= 0) sql_phase2<MS, E, W>(pv, &lagg[ent[u]], rec[u]);
       if (two) lds_barrier();
+    }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < RB; ++u) rec[u] = nxt[u];
     }
   }
   __syncthreads();
@@ -486,14 +499,14 @@ bool sql_lean_eligible(const Program &prog, const PartParams &pp) {
   return pp.pane_S == 1 && pp.rbits == 0 && pp.has_seq && (pp.words == 4 || pp.words == 5) && prog.n_slots <= 16;
 }
 
-template <int MS, int E, int NT>
+template <int MS, int E, int NT, uint64_t SIG = 0, uint64_t SIG2 = 0>
 static void sql_launch(hipStream_t s, dim3 g, const Program &prog, const TwParams &p, const PartParams &pp,
                        const TwTable &t, const PartBuffers &pb, DevScalars *sc, const OutCols &out, uint64_t out_base,
                        uint64_t out_cap) {
   if (pp.words - 1 == 3)
-    hipLaunchKernelGGL((k_agg_sql<MS, E, NT, 3>), g, dim3(NT), 0, s, prog, pp, t, pb, sc);
+    hipLaunchKernelGGL((k_agg_sql<MS, E, NT, 3, SIG, SIG2>), g, dim3(NT), 0, s, prog, pp, t, pb, sc);
   else
-    hipLaunchKernelGGL((k_agg_sql<MS, E, NT, 4>), g, dim3(NT), 0, s, prog, pp, t, pb, sc);
+    hipLaunchKernelGGL((k_agg_sql<MS, E, NT, 4, SIG, SIG2>), g, dim3(NT), 0, s, prog, pp, t, pb, sc);
   hipLaunchKernelGGL((k_sql_apply<MS>), g, dim3(256), 0, s, prog, p, pp, t, pb, out, out_base, out_cap, sc);
 }
 
@@ -507,7 +520,17 @@ bool launch_part_agg_sql(hipStream_t s, dim3 g, const Program &prog, const TwPar
   // 1024 LDS entries (part_lds_entries: buckets of <= 512 groups): 8 + 8 MS
   // bytes each, one 1024-thread workgroup per CU at 12 slots
   if (prog.n_slots <= 8) sql_launch<8, 1024, 512>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
-  else if (prog.n_slots <= 12) sql_launch<12, 1024, 1024>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
+  else if (prog.n_slots <= 12) {
+    // the SQL drop-in's C2 query: its slot program baked in
+    uint64_t hi = 0;
+    const uint64_t sq = program_sig(prog, &hi);
+    if (sq == kSigSqlI && hi == kSigSqlI2)
+      sql_launch<12, 1024, 1024, kSigSqlI, kSigSqlI2>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
+    else if (sq == kSigSqlF && hi == kSigSqlF2)
+      sql_launch<12, 1024, 1024, kSigSqlF, kSigSqlF2>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
+    else
+      sql_launch<12, 1024, 1024>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
+  }
   else sql_launch<16, 1024, 1024>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
   return true;
 }

@@ -17,6 +17,7 @@
 // Window assignment and grace follow TimeWindowedStream.hs:86-103 / :105-117
 // exactly as in k_window.hip (rejected windows are always the earliest ones, so
 // the accepted windows of a record are one consecutive run).
+#include <cstdlib>
 #include <cstring>
 
 #include "hsg_dev.h"
@@ -654,6 +655,10 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
   __shared__ uint32_t cnt2[1 << (kPartMaxLog2 - 1)];  // two u16 counts per word, then the u16 run starts
   __shared__ uint32_t cursor[1 << kPartMaxLog2];      // the row's next output slot per bucket
   __shared__ uint32_t swave[kPNT / 64];
+  // W == 3: each staged record's output slot, so the write-out can go word by
+  // word (consecutive lanes, consecutive 8-byte words of a run) instead of
+  // three 8-byte stores 24 bytes apart per lane
+  __shared__ uint32_t sdest[W == 3 ? T : 1];
   if (sc->redo || !sc->packed) return;  // uniform: the gather variant runs
   constexpr int R = T / kPNT;
   const int nb = 1 << pp.np_log2;
@@ -780,16 +785,22 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
     __syncthreads();
     q1 = phase_clock();
     // write-out: record q goes to the row's slot for its bucket + (q - run start)
-    for (uint32_t q = threadIdx.x; q < placed; q += kPNT) {
+    if constexpr (W == 3) {
+      for (uint32_t q = threadIdx.x; q < placed; q += kPNT) {
+        const uint32_t bk = bucket_of((uint32_t)stage[q * W], pp.np_log2, pp.bshift);
+        sdest[q] = cursor[bk] + (q - lstart[bk]);
+      }
+      lds_barrier();
+      for (uint32_t w = threadIdx.x; w < placed * 3; w += kPNT) {
+        const uint32_t q = w / 3, j = w - 3 * q;
+        pb.rec[(uint64_t)sdest[q] * 3 + j] = stage[w];
+      }
+    }
+    for (uint32_t q = threadIdx.x; W != 3 && q < placed; q += kPNT) {
       const uint64_t h = stage[q * W];
       const uint32_t bk = bucket_of((uint32_t)h, pp.np_log2, pp.bshift);
       const uint64_t dest = (uint64_t)cursor[bk] + (q - lstart[bk]);
-      if (W == 3) {
-        uint64_t *o = pb.rec + dest * 3;
-        o[0] = h;
-        o[1] = stage[q * W + 1];
-        o[2] = stage[q * W + 2];
-      } else if (W == 2) {
+      if (W == 2) {
         const uint64_t cc = stage[q * W + 1];
         *(ulonglong2 *)(pb.rec + dest * 2) = make_ulonglong2(h, cc);
       } else {
@@ -825,8 +836,11 @@ void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const
   if (stage) {
     const dim3 th(kPNT);
     if (pp.words - 1 == 3) {
-      // (half tiles: 48 KB of staging, two workgroups per CU)
+      // (half tiles: 48 KB of staging, two workgroups per CU; HSG_SCATTER3_WHOLE:
+      // whole tiles, one workgroup per CU, an A/B knob)
+      static const bool whole = getenv("HSG_SCATTER3_WHOLE") != nullptr;
       if (stable) hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 3, true>), g, th, 0, s, b, p, pp, pb, seq, sc);
+      else if (whole) hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 3, false>), g, th, 0, s, b, p, pp, pb, seq, sc);
       else hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 3, false>), g, th, 0, s, b, p, pp, pb, seq, sc);
     } else if (pp.words - 1 == 2) {
       if (stable) hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 2, true>), g, th, 0, s, b, p, pp, pb, seq, sc);

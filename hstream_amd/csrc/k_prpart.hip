@@ -839,9 +839,22 @@ template <int MS, class PV>
 __device__ inline void combine_v(const PV &pv, int64_t (&a)[MS], const int64_t (&e)[MS]) {
   if constexpr (std::is_same<PV, ProgRT>::value) {
     // a runtime program: tie words, the LAST pair and the form slots
-    // (combine_row; the baked programs have none of them)
+    // (combine_row)
     combine_row<MS>(pv.p, a, e);
     return;
+  } else {
+    // a baked program with tie words (the SQL shape): the words first, against
+    // the MIN / MAX values before the combine (as combine_row)
+    if constexpr (PV::has_ties()) {
+#pragma unroll
+      for (int s = 0; s < MS; ++s) {
+        if (s >= pv.n()) break;
+        const int op = pv.op(s);
+        if (op != S_TIE_MIN && op != S_TIE_MAX) continue;
+        const int v = PV::aux_of(s);
+        a[s] = tie_combine(op, pv.op(v), reg_at<MS>(a, v), reg_at<MS>(e, v), a[s], e[s]);
+      }
+    }
   }
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
@@ -958,10 +971,10 @@ struct PrRecRegs {
   __device__ bool dec(int c) const { return ((uint64_t)word((pk ? 1 : 2) + C) >> (56 + c)) & 1ull; }
 };
 
-template <int MS, int LT, bool REG, uint64_t SIG>
+template <int MS, int LT, bool REG, uint64_t SIG, uint64_t SIG2 = 0>
 __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, PartParams pp, TwTable t,
                                                      PartBuffers pb, PrPart pr, DevScalars *sc) {
-  const ProgView<SIG> pv(prog);
+  const ProgView<SIG, SIG2> pv(prog);
   constexpr int TAB = 1 << LT;
   constexpr int EPT = TAB / kPbNT;  // table entries per thread
   constexpr int PF = 8;             // record loads in flight per thread in the one-pass insert
@@ -1243,7 +1256,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
         for (int s = 0; s < MS; ++s) fin[s] = carry[s];
         combine_v<MS>(pv, fin, pre);
         // at the record's partitioned position: consecutive lanes, consecutive rows
-        if constexpr (SIG != 0) {
+        if (SIG != 0 && prog.fin_n == ns && !prog.fin_form) {  // (uniform: no projection)
           int64_t *o = pr.fin + i * (uint64_t)ns;
 #pragma unroll
           for (int s = 0; s < MS; ++s)
@@ -1866,6 +1879,18 @@ static void pr_launch(hipStream_t s, const Batch &b, const Program &prog, const 
         done = true;
       } else if (reg && sig == kSigSumMaxI) {
         hipLaunchKernelGGL((k_pr_bucket<MS, LT, true, kSigSumMaxI>), gb, tb, 0, s, prog, p, pp, t, pb, pr, sc);
+        done = true;
+      }
+    }
+    if constexpr (MS == 12) {
+      // the SQL drop-in's C2 query (literal forms, a passthrough)
+      uint64_t hi = 0;
+      const uint64_t sq = program_sig(prog, &hi);
+      if (reg && sq == kSigSqlI && hi == kSigSqlI2) {
+        hipLaunchKernelGGL((k_pr_bucket<MS, LT, true, kSigSqlI, kSigSqlI2>), gb, tb, 0, s, prog, p, pp, t, pb, pr, sc);
+        done = true;
+      } else if (reg && sq == kSigSqlF && hi == kSigSqlF2) {
+        hipLaunchKernelGGL((k_pr_bucket<MS, LT, true, kSigSqlF, kSigSqlF2>), gb, tb, 0, s, prog, p, pp, t, pb, pr, sc);
         done = true;
       }
     }

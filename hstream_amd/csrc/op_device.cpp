@@ -896,9 +896,18 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     return rc;
   };
   const uint64_t live0 = d.h_sc->live;  // rows before the batch (after its tw_maintain)
-  int rc = run_room(opt);
+  // a run of SQL refusals at the most buckets there are (groups beyond what the
+  // LDS tables hold): the careful path directly for a while
+  const bool sql_try = !sql || d.sql_skip == 0;
+  if (!sql_try) d.sql_skip -= 1;
+  int rc = run_room(opt && sql_try);
   if (rc != HSG_OK) return rc;
-  const bool sql_refused = sql && opt && kb.n && (!d.h_sc->packed || d.h_sc->scratch[35]);
+  const bool sql_refused = sql && opt && sql_try && kb.n && (!d.h_sc->packed || d.h_sc->scratch[35]);
+  // (a refusal is a split bucket or a chunk whose groups overflowed its LDS
+  // table: more buckets for the next batch -- the careful run below leaves no
+  // group count to size them by)
+  const bool sql_ovf = sql_refused && d.h_sc->packed && d.h_sc->scratch[35];
+  const int np_refused = d.np_log2;
   if (sql_refused) d.replays += 1;  // (hsg_stats: a lean SQL batch is counted in lean_batches)
   if (opt && kb.n && (d.h_sc->redo || sql_refused)) {
     if (sql) {
@@ -948,6 +957,12 @@ static int push_time_atomic(OpDevice &d, const hsg_op_config &cfg, const Program
     if (hipEventElapsedTime(&ms, d.ev_a, d.ev_b) == hipSuccess) r.agg_ms = ms;
     r.agg_launches = 1;
     if (d.use_part) adapt_partitions(d, cfg, prog, groups, kb.n);
+    if (sql_ovf) {
+      const int want = np_refused + 1 < kPartMaxLog2 ? np_refused + 1 : kPartMaxLog2;
+      if (d.np_log2 < want) d.np_log2 = want;
+      // already at the most buckets: give the lean SQL kernels a rest
+      if (np_refused >= kPartMaxLog2) d.sql_skip = 16;
+    }
   }
   r.touched = cfg.emit_mode == HSG_EMIT_PER_BATCH ? r.out_rows : d.h_sc->scratch[0];
   return rc;
