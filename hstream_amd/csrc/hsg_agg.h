@@ -53,6 +53,14 @@ struct ProgSig {
     }
     return 0;
   }
+  // the LAST_FORM slot over the column of LAST_SEQ slot s (-1: none): its
+  // word is (seq + 1) << 1 | bit over the same present records, so the
+  // LAST_SEQ slot is that word >> 1 and needs no update of its own
+  static constexpr int last_form_of(int s) {
+    for (int k = 0; k < count(); ++k)
+      if (op_of(k) == S_LAST_FORM && col_of(k) == col_of(s)) return k;
+    return -1;
+  }
   static constexpr bool has_ties() {
     for (int k = 0; k < count(); ++k)
       if (op_of(k) == S_TIE_MIN || op_of(k) == S_TIE_MAX) return true;
@@ -75,6 +83,9 @@ template <uint64_t SIG, uint64_t SIG2>
 __device__ constexpr int pv_aux(const ProgSig<SIG, SIG2> &, int s) { return ProgSig<SIG, SIG2>::aux_of(s); }
 template <uint64_t SIG, uint64_t SIG2>
 __device__ constexpr bool pv_ties(const ProgSig<SIG, SIG2> &) { return ProgSig<SIG, SIG2>::has_ties(); }
+__device__ inline int pv_last_form(const ProgRT &, int) { return -1; }
+template <uint64_t SIG, uint64_t SIG2>
+__device__ constexpr int pv_last_form(const ProgSig<SIG, SIG2> &, int s) { return ProgSig<SIG, SIG2>::last_form_of(s); }
 
 // signature of a runtime program (0: not expressible); slots past the ninth
 // go to *sig2 when it is given (else such a program has no signature)

@@ -89,6 +89,7 @@ __device__ inline void sql_phase1(const PV &pv, int64_t *__restrict__ agg, const
     if (s >= pv.n()) break;
     const int op = pv.op(s);
     if (op == S_LAST_VAL || slot_is_tie(op) || ((skip >> s) & 1u)) continue;
+    if (op == S_LAST_SEQ && pv_last_form(pv, s) >= 0) continue;  // derived from the LAST_FORM word
     const int c = pv.col(s);
     if (op != S_CNT_ALL && !r.present(c)) continue;
     int64_t *a = agg + s * ST;
@@ -153,7 +154,9 @@ __device__ inline void sql_phase2(const PV &pv, int64_t *__restrict__ agg, const
     const int c = pv.col(s);
     if (op == S_LAST_VAL) {
       // the preceding slot is its LAST_SEQ (build_program last_pair)
-      if (s > 0 && r.present(c) && (uint64_t)agg[(s - 1) * ST] == (uint64_t)r.seq1()) agg[s * ST] = r.col(c);
+      const int lf = s > 0 ? pv_last_form(pv, s - 1) : -1;
+      const uint64_t last = lf >= 0 ? (uint64_t)agg[lf * ST] >> 1 : (uint64_t)agg[(s - 1) * ST];
+      if (s > 0 && r.present(c) && last == (uint64_t)r.seq1()) agg[s * ST] = r.col(c);
     } else if (slot_is_tie(op)) {
       if (!r.present(c)) continue;
       const int v = pv_aux(pv, s), vop = pv.op(v);
@@ -278,6 +281,14 @@ __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwT
     }
   }
   __syncthreads();
+  // LAST_SEQ slots kept only through their LAST_FORM word
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    if (s >= ns || pv.op(s) != S_LAST_SEQ) continue;
+    const int lf = pv_last_form(pv, s);
+    if (lf < 0) continue;
+    for (int e = threadIdx.x; e < E; e += NT) lagg[s * E + e] = (int64_t)((uint64_t)lagg[lf * E + e] >> 1);
+  }
   if (s_ovf) {  // uniform (read after the barrier)
     if (threadIdx.x == 0) atomicOr((unsigned long long *)&sc->scratch[35], 1ull);
     return;

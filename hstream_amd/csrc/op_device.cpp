@@ -319,6 +319,9 @@ int op_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog, u
     d.use_part = true;
     d.sql_lean = true;
     d.pane_S = 1;
+    // no group count before the first batch: the most buckets (a bucket whose
+    // groups overflow its LDS table sends the batch to the careful path)
+    d.np_log2 = kPartMaxLog2;
     rc = part_device_init(d, cfg, prog, err);
     if (rc != HSG_OK) return rc;
   } else if (part_supported(prog)) {
