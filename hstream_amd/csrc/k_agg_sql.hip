@@ -56,6 +56,15 @@ __device__ inline uint32_t sql_home(uint32_t key, uint32_t w) {
   return h >> (32 - LOG2E);
 }
 
+// key-hash round of (key, window) among 2^rb (bits independent of sql_home's)
+__device__ inline uint32_t sql_round(uint32_t key, uint32_t w, int rb) {
+  uint32_t h = key * 0x85EBCA6Bu ^ w * 0xC2B2AE35u;
+  h ^= h >> 13;
+  h *= 0x27D4EB2Du;
+  h ^= h >> 15;
+  return h >> (32 - rb);
+}
+
 constexpr int kSqlSortBins = 1024;
 // a partial's HBM home row bin (k_agg_lean.hip lean_sort_bin)
 __device__ inline uint32_t sql_sort_bin(const TwTable &t, const PartParams &pp, uint64_t g) {
@@ -171,6 +180,40 @@ __device__ inline void sql_phase2(const PV &pv, int64_t *__restrict__ agg, const
   }
 }
 
+// one record's contribution to every slot, as a partial of its own (a record
+// whose group found no room in the chunk's LDS table): the state of a group
+// holding only this record
+template <int MS, int W, class PV>
+__device__ inline void sql_elems(const PV &pv, const PRec<W, true> &r, uint32_t skip, int64_t (&v)[MS]) {
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    v[s] = 0;
+    if (s >= pv.n()) continue;
+    const int op = pv.op(s), c = pv.col(s);
+    if (op == S_CNT_ALL || ((skip >> s) & 1u)) {  // (skip: COUNT(col) without validity arrays)
+      v[s] = 1;
+      continue;
+    }
+    if (!r.present(c)) {
+      v[s] = slot_identity_dev(op);
+      continue;
+    }
+    const int64_t x = r.col(c);
+    const uint64_t w = ((uint64_t)r.seq1() << 1) | (r.dec(c) ? 0u : 1u);
+    switch (op) {
+      case S_CNT: v[s] = 1; break;
+      case S_CNT_DEC: v[s] = r.dec(c) ? 1 : 0; break;
+      case S_MIN_F:
+      case S_MAX_F: v[s] = (int64_t)f64_ord(__builtin_bit_cast(double, x)); break;
+      case S_LAST_SEQ: v[s] = r.seq1(); break;
+      case S_LAST_FORM:
+      case S_TIE_MIN:
+      case S_TIE_MAX: v[s] = (int64_t)w; break;
+      default: v[s] = x; break;  // SUM, MIN / MAX (i64), LAST_VAL
+    }
+  }
+}
+
 template <int MS, int E, int NT, int W, uint64_t SIG = 0, uint64_t SIG2 = 0>
 __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwTable t, PartBuffers pb,
                                                 DevScalars *sc) {
@@ -178,7 +221,7 @@ __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwT
   constexpr int RB = 4;  // records per thread per block (one block in flight beside it)
   __shared__ uint64_t lkey[E];
   __shared__ int64_t lagg[MS * E];
-  __shared__ uint32_t s_cnt, s_ovf, s_fill;
+  __shared__ uint32_t s_cnt, s_ovf, s_fill, s_full;
   __shared__ uint32_t s_bin[kSqlSortBins];
   __shared__ uint32_t s_wsum[NT / 64];
   if (sc->redo || !sc->packed) return;  // uniform: the careful path runs the batch
@@ -189,12 +232,10 @@ __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwT
   const int PW = 1 + ns;  // partial words
   const int C = W - 2;    // packed: header, C columns, sequence word
   const uint32_t kbase = (uint32_t)sc->kbase;
-  if (!exclusive) {
-    // a bucket split over workgroups: its groups' partials would meet in HBM
-    // out of order (uniform)
-    if (threadIdx.x == 0) atomicOr((unsigned long long *)&sc->scratch[35], 1ull);
-    return;
-  }
+  uint64_t *const pane = pb.pane + r0 * (uint64_t)PW;
+  // (a bucket split over workgroups, or a record of a chunk whose LDS table is
+  // full: several partials of one group, which k_sql_apply combines under the
+  // row's lock)
   // without validity arrays COUNT(col) = COUNT(*): not kept in LDS
   int cnt_all_slot = -1;
   uint32_t skip = 0;
@@ -205,157 +246,204 @@ __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwT
       if (pv.op(s) == S_CNT) skip |= 1u << s;
   bool two = pv_ties(pv), need2 = pv_ties(pv);
   for (int s = 0; s < ns && s < MS; ++s) need2 |= pv.op(s) == S_LAST_VAL;
-  for (int k = threadIdx.x; k < kSqlSortBins; k += NT) s_bin[k] = 0;
-  for (int e = threadIdx.x; e < E; e += NT) {
-    lkey[e] = kEmpty;
-#pragma unroll
-    for (int s = 0; s < MS; ++s)
-      if (s < ns) lagg[s * E + e] = slot_identity_dev(pv.op(s));
-  }
+  // key-hash rounds: round k takes the groups whose round hash is k (one
+  // pass over the chunk's records each), so a chunk with more groups than
+  // the LDS table holds still gives one partial per group; the host's hint
+  // (pp.rbits, from the last batch's groups per bucket) sets the first split,
+  // a round whose groups overflow the table is split in two and run again
+  constexpr int kMaxRb = 6;
+  int rb = pp.rbits < kMaxRb ? pp.rbits : kMaxRb;
   if (threadIdx.x == 0) {
     s_cnt = 0;
-    s_fill = 0;
     s_ovf = 0;
   }
-  __syncthreads();
-
-  // records: block k holds records r0 + k*RB*NT + u*NT + tid; the next block's
-  // loads are issued before the current one is processed (k_agg_lean.hip)
-  PRec<W, true> rec[RB], nxt[RB];
-  auto load = [&](uint64_t s0, PRec<W, true>(&d)[RB]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t round = 0;
+  while (round < (1u << rb)) {  // uniform
+    for (int k = threadIdx.x; k < kSqlSortBins; k += NT) s_bin[k] = 0;
+    for (int e = threadIdx.x; e < E; e += NT) {
+      lkey[e] = kEmpty;
 #pragma unroll
-    for (int u = 0; u < RB; ++u) {
-      const uint64_t i = s0 + (uint64_t)u * NT + threadIdx.x;
-      d[u].C = C;
-#pragma unroll
-      for (int q = 0; q < W; ++q) d[u].w[q] = i < r1 ? pb.rec[i * W + q] : 0;
-      if (i >= r1) d[u].w[0] = kEmpty;
+      for (int s = 0; s < MS; ++s)
+        if (s < ns) lagg[s * E + e] = slot_identity_dev(pv.op(s));
     }
-  };
-  load(r0, rec);
-  for (uint64_t s0 = r0; s0 < r1; s0 += (uint64_t)RB * NT) {
-    const bool more = s0 + (uint64_t)RB * NT < r1;  // uniform
-    if (more) load(s0 + (uint64_t)RB * NT, nxt);
-    int ent[RB];
-    // phase 1
+    if (threadIdx.x == 0) {
+      s_fill = 0;
+      s_full = 0;
+    }
+    __syncthreads();
+    const bool last_try = rb >= kMaxRb;  // (then a record that finds no room is a partial of its own)
+
+    // records: block k holds records r0 + k*RB*NT + u*NT + tid; the next block's
+    // loads are issued before the current one is processed (k_agg_lean.hip)
+    PRec<W, true> rec[RB], nxt[RB];
+    auto load = [&](uint64_t s0, PRec<W, true>(&d)[RB]) {
 #pragma unroll
-    for (int u = 0; u < RB; ++u) {
-      ent[u] = -1;
-      const PRec<W, true> &r = rec[u];
-      if (r.w[0] == kEmpty) continue;
-      const uint32_t key = r.key(), kw = r.krel(kbase);
-      const uint64_t g = ((uint64_t)key << 32) | kw;
-      uint32_t h = sql_home<E>(key, kw);
-      for (int probe = 0; probe < E; ++probe) {
-        const uint64_t c = lkey[h];
-        if (c == g) {
-          ent[u] = (int)h;
-          break;
-        }
-        if (c == kEmpty) {
-          if (*(volatile uint32_t *)&s_fill >= (uint32_t)(E - E / 8)) break;  // full: g is not in the table
-          const uint64_t old =
-              atomicCAS((unsigned long long *)&lkey[h], (unsigned long long)kEmpty, (unsigned long long)g);
-          if (old == kEmpty) atomicAdd(&s_fill, 1u);
-          if (old == kEmpty || old == g) {
+      for (int u = 0; u < RB; ++u) {
+        const uint64_t i = s0 + (uint64_t)u * NT + threadIdx.x;
+        d[u].C = C;
+#pragma unroll
+        for (int q = 0; q < W; ++q) d[u].w[q] = i < r1 ? pb.rec[i * W + q] : 0;
+        if (i >= r1) d[u].w[0] = kEmpty;
+      }
+    };
+    load(r0, rec);
+    for (uint64_t s0 = r0; s0 < r1; s0 += (uint64_t)RB * NT) {
+      const bool more = s0 + (uint64_t)RB * NT < r1;  // uniform
+      if (more) load(s0 + (uint64_t)RB * NT, nxt);
+      int ent[RB];
+      // phase 1
+#pragma unroll
+      for (int u = 0; u < RB; ++u) {
+        ent[u] = -1;
+        const PRec<W, true> &r = rec[u];
+        if (r.w[0] == kEmpty) continue;
+        const uint32_t key = r.key(), kw = r.krel(kbase);
+        if (rb && sql_round(key, kw, rb) != round) continue;  // another round's group
+        const uint64_t g = ((uint64_t)key << 32) | kw;
+        uint32_t h = sql_home<E>(key, kw);
+        for (int probe = 0; probe < E; ++probe) {
+          const uint64_t c = lkey[h];
+          if (c == g) {
             ent[u] = (int)h;
             break;
           }
+          if (c == kEmpty) {
+            if (*(volatile uint32_t *)&s_fill >= (uint32_t)(E - E / 8)) break;  // full: g is not in the table
+            const uint64_t old =
+                atomicCAS((unsigned long long *)&lkey[h], (unsigned long long)kEmpty, (unsigned long long)g);
+            if (old == kEmpty) atomicAdd(&s_fill, 1u);
+            if (old == kEmpty || old == g) {
+              ent[u] = (int)h;
+              break;
+            }
+          }
+          h = (h + 1) & (E - 1);
         }
-        h = (h + 1) & (E - 1);
+        if (ent[u] >= 0) {
+          sql_phase1<MS, E, W>(pv, &lagg[ent[u]], r, skip);
+        } else if (!last_try) {
+          s_full = 1;  // this round is split and run again
+        } else {
+          // no finer split left: this record is a partial of its own
+          int64_t v[MS];
+          sql_elems<MS, W>(pv, r, skip, v);
+          const uint32_t q = atomicAdd(&s_cnt, 1u);
+          uint64_t *o = pane + (uint64_t)q * PW;
+          o[0] = g;
+#pragma unroll
+          for (int s = 0; s < MS; ++s)
+            if (s < ns) o[1 + s] = (uint64_t)v[s];
+          s_ovf = 1;
+        }
       }
-      if (ent[u] >= 0) sql_phase1<MS, E, W>(pv, &lagg[ent[u]], r, skip);
-      else s_ovf = 1;  // the table is full: the batch takes the careful path
-    }
-    if (need2) {
-      lds_barrier();
-      // phase 2
+      if (need2) {
+        lds_barrier();
+        // phase 2
 #pragma unroll
-      for (int u = 0; u < RB; ++u)
-        if (ent[u] >= 0) sql_phase2<MS, E, W>(pv, &lagg[ent[u]], rec[u]);
-      if (two) lds_barrier();
-    }
-    if (more) {
+        for (int u = 0; u < RB; ++u)
+          if (ent[u] >= 0) sql_phase2<MS, E, W>(pv, &lagg[ent[u]], rec[u]);
+        if (two) lds_barrier();
+      }
+      if (more) {
 #pragma unroll
-      for (int u = 0; u < RB; ++u) rec[u] = nxt[u];
+        for (int u = 0; u < RB; ++u) rec[u] = nxt[u];
+      }
     }
-  }
-  __syncthreads();
-  // LAST_SEQ slots kept only through their LAST_FORM word
+    __syncthreads();
+    if (s_full) {  // uniform (read after the barrier): nothing of this round was written
+      rb += 1;
+      round *= 2;
+      __syncthreads();  // every thread has read s_full before the reset above rewrites it
+      continue;
+    }
+    // LAST_SEQ slots kept only through their LAST_FORM word
 #pragma unroll
-  for (int s = 0; s < MS; ++s) {
-    if (s >= ns || pv.op(s) != S_LAST_SEQ) continue;
-    const int lf = pv_last_form(pv, s);
-    if (lf < 0) continue;
-    for (int e = threadIdx.x; e < E; e += NT) lagg[s * E + e] = (int64_t)((uint64_t)lagg[lf * E + e] >> 1);
-  }
-  if (s_ovf) {  // uniform (read after the barrier)
-    if (threadIdx.x == 0) atomicOr((unsigned long long *)&sc->scratch[35], 1ull);
-    return;
-  }
+    for (int s = 0; s < MS; ++s) {
+      if (s >= ns || pv.op(s) != S_LAST_SEQ) continue;
+      const int lf = pv_last_form(pv, s);
+      if (lf < 0) continue;
+      for (int e = threadIdx.x; e < E; e += NT) lagg[s * E + e] = (int64_t)((uint64_t)lagg[lf * E + e] >> 1);
+    }
 
-  // live entries -> partials, in the order of their HBM home rows (counting
-  // sort over kSqlSortBins bins)
-  constexpr int PER = E / NT;
-  uint32_t bin[PER], rank[PER];
+    // live entries -> partials, in the order of their HBM home rows (counting
+    // sort over kSqlSortBins bins), after the partials written so far
+    constexpr int PER = E / NT;
+    uint32_t bin[PER], rank[PER];
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const uint64_t g = lkey[k * NT + threadIdx.x];
-    bin[k] = g != kEmpty ? sql_sort_bin(t, pp, g) : ~0u;
-    rank[k] = g != kEmpty ? atomicAdd(&s_bin[bin[k]], 1u) : 0u;
-  }
-  __syncthreads();
-  constexpr int BPT = kSqlSortBins / NT > 0 ? kSqlSortBins / NT : 1;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t loc = 0;
-  if (threadIdx.x * BPT < kSqlSortBins) {
-#pragma unroll
-    for (int k = 0; k < BPT; ++k) loc += s_bin[threadIdx.x * BPT + k];
-  }
-  const uint32_t incl = (uint32_t)wave_incl_sum((uint64_t)loc);
-  if (lane == 63) s_wsum[wv] = incl;
-  __syncthreads();
-  uint32_t run = incl - loc;
-  for (int k = 0; k < wv; ++k) run += s_wsum[k];
-  uint32_t total = 0;
-  for (int k = 0; k < NT / 64; ++k) total += s_wsum[k];
-  __syncthreads();
-  if (threadIdx.x * BPT < kSqlSortBins) {
-#pragma unroll
-    for (int k = 0; k < BPT; ++k) {
-      const uint32_t c = s_bin[threadIdx.x * BPT + k];
-      s_bin[threadIdx.x * BPT + k] = run;
-      run += c;
+    for (int k = 0; k < PER; ++k) {
+      const uint64_t g = lkey[k * NT + threadIdx.x];
+      bin[k] = g != kEmpty ? sql_sort_bin(t, pp, g) : ~0u;
+      rank[k] = g != kEmpty ? atomicAdd(&s_bin[bin[k]], 1u) : 0u;
     }
+    __syncthreads();
+    constexpr int BPT = kSqlSortBins / NT > 0 ? kSqlSortBins / NT : 1;
+    uint32_t loc = 0;
+    if (threadIdx.x * BPT < kSqlSortBins) {
+#pragma unroll
+      for (int k = 0; k < BPT; ++k) loc += s_bin[threadIdx.x * BPT + k];
+    }
+    const uint32_t incl = (uint32_t)wave_incl_sum((uint64_t)loc);
+    if (lane == 63) s_wsum[wv] = incl;
+    __syncthreads();
+    uint32_t run = incl - loc + s_cnt;
+    for (int k = 0; k < wv; ++k) run += s_wsum[k];
+    uint32_t live = 0;
+    for (int k = 0; k < NT / 64; ++k) live += s_wsum[k];
+    __syncthreads();
+    if (threadIdx.x * BPT < kSqlSortBins) {
+#pragma unroll
+      for (int k = 0; k < BPT; ++k) {
+        const uint32_t c = s_bin[threadIdx.x * BPT + k];
+        s_bin[threadIdx.x * BPT + k] = run;
+        run += c;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (bin[k] == ~0u) continue;
+      const int e = k * NT + threadIdx.x;
+      const uint32_t q = s_bin[bin[k]] + rank[k];
+      uint64_t *o = pane + (uint64_t)q * PW;
+      o[0] = lkey[e];
+      const int64_t call = cnt_all_slot >= 0 ? lagg[cnt_all_slot * E + e] : 0;
+#pragma unroll
+      for (int s = 0; s < MS; ++s)
+        if (s < ns) o[1 + s] = (uint64_t)(((skip >> s) & 1u) ? call : lagg[s * E + e]);
+    }
+    __syncthreads();  // the flush has read the table (and s_cnt)
+    if (threadIdx.x == 0) s_cnt += live;
+    ++round;
   }
   __syncthreads();
-  uint64_t *const pane = pb.pane + r0 * (uint64_t)PW;
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    if (bin[k] == ~0u) continue;
-    const int e = k * NT + threadIdx.x;
-    const uint32_t q = s_bin[bin[k]] + rank[k];
-    uint64_t *o = pane + (uint64_t)q * PW;
-    o[0] = lkey[e];
-    const int64_t call = cnt_all_slot >= 0 ? lagg[cnt_all_slot * E + e] : 0;
-#pragma unroll
-    for (int s = 0; s < MS; ++s)
-      if (s < ns) o[1 + s] = (uint64_t)(((skip >> s) & 1u) ? call : lagg[s * E + e]);
-  }
   if (threadIdx.x == 0) {
+    const uint32_t total = s_cnt;
     atomicAdd((unsigned long long *)&sc->scratch[31], (unsigned long long)total);  // the apply's room check
+    // count | record partials << 31 | split bucket << 30: a workgroup with
+    // either applies under the rows' locks, and the batch's changelog then
+    // comes from the touched list
+    const uint32_t fl = (s_ovf ? 1u << 31 : 0u) | (exclusive ? 0u : 1u << 30);
     pb.pane_info[2 * blockIdx.x] = r0;
-    pb.pane_info[2 * blockIdx.x + 1] = (uint64_t)total;
-    pb.pane_cnt[blockIdx.x] = total;
+    pb.pane_info[2 * blockIdx.x + 1] = (uint64_t)total | ((uint64_t)fl << 32);
+    pb.pane_cnt[blockIdx.x] = total | fl;
   }
 }
 
 // One workgroup per aggregation workgroup: its partials into the HBM table.
-// Every group of the batch has exactly one partial (k_agg_sql refused split
-// buckets and overflowing chunks), so each thread owns its group's row: find
-// or claim it (the bucket's regions are this workgroup's; claims arbitrated
-// in an LDS claim set when the region bits allow, k_agg_lean.hip), combine
-// with the full slot algebra and write the row and its changelog row.
+// A workgroup whose bucket is its own and which wrote no record partials has
+// exactly one partial per group, so each thread owns its group's row: find or
+// claim it (the bucket's regions are this workgroup's; claims arbitrated in an
+// LDS claim set when the region bits allow, k_agg_lean.hip), combine with the
+// full slot algebra and write the row. Otherwise (a split bucket, a chunk
+// whose LDS table filled) several partials of one group meet here, from this
+// and other workgroups: each is combined into the row under the row's lock
+// (the high half of its stamp word), with agent-scope loads and stores (no
+// stale L2 line across XCDs) and an order-free combine (the LAST pair by its
+// sequence, tie words by their rule, the rest commutative). When every
+// workgroup is of the first kind the changelog rows are written here;
+// otherwise each partial leaves a touched-list entry (the group's slot on its
+// first update of the batch, by the stamp) and the emit chain writes them.
 constexpr int kSqlClaimSet = 4096;
 __device__ inline bool sql_claim_insert(uint32_t *cset, uint32_t slot) {
   uint32_t h = (slot * 0x9E3779B1u) >> (32 - 12);
@@ -386,11 +474,27 @@ __device__ inline int64_t sql_claim_lds(const TwTable &t, uint64_t g, uint32_t *
   return tw_ovf_claim(t, g, fresh);  // the region's sub-table is full
 }
 
+// a <- a (+) e in any order: combine_row with the LAST pair kept by sequence
+template <int MS>
+__device__ inline void sql_combine_any(const Program &prog, int64_t (&a)[MS], const int64_t (&e)[MS]) {
+  int64_t f[MS];
+#pragma unroll
+  for (int s = 0; s < MS; ++s) f[s] = e[s];
+#pragma unroll
+  for (int s = 0; s < MS; ++s)
+    if (s + 1 < MS && s < prog.n_slots && prog.slot_op[s] == S_LAST_SEQ && (uint64_t)e[s] <= (uint64_t)a[s]) {
+      f[s] = 0;  // combine_row then keeps a's pair
+      f[s + 1] = 0;
+    }
+  combine_row<MS>(prog, a, f);
+}
+
 template <int MS>
 __global__ __launch_bounds__(256) void k_sql_apply(Program prog, TwParams p, PartParams pp, TwTable t, PartBuffers pb,
                                                    OutCols out, uint64_t out_base, uint64_t out_cap,
                                                    DevScalars *sc) {
   __shared__ uint64_t s_red[4], s_tot[4];
+  __shared__ uint32_t s_fl[4];
   __shared__ uint32_t cset[kSqlClaimSet];
   if (sc->redo || !sc->packed || sc->scratch[35]) return;  // uniform: the careful path runs the batch
   // the batch's groups (at most its partials) may not fit the table at the
@@ -407,34 +511,49 @@ __global__ __launch_bounds__(256) void k_sql_apply(Program prog, TwParams p, Par
   const uint64_t PW = 1 + (uint64_t)ns;
   const uint64_t base = pb.pane_info[2 * blockIdx.x];
   const uint32_t cnt = (uint32_t)pb.pane_info[2 * blockIdx.x + 1];
-  const bool plain_claim = pp.np_log2 <= t.rbits && pp.bshift == t.bshift;
+  const bool shared = (pb.pane_info[2 * blockIdx.x + 1] >> 62) != 0;  // record partials or a split bucket
+  const bool plain_claim = !shared && pp.np_log2 <= t.rbits && pp.bshift == t.bshift;
   const bool lds_claim = plain_claim && cnt <= kSqlClaimSet / 2 && t.mask < 0xFFFFFFFFull;
   if (lds_claim)
     for (int k = threadIdx.x; k < kSqlClaimSet; k += 256) cset[k] = 0;
-  // every workgroup's partial count: this one's changelog position and the total
+  // every workgroup's partial count: this one's changelog / touched-list
+  // position, the total, and whether any workgroup shares groups
   const int nb = 1 << pp.np_log2;
   const uint32_t nch = pb.chunk_start[nb];
   uint64_t before = 0, total = 0;
+  uint32_t anyfl = 0;
   for (uint32_t k = threadIdx.x; k < nch; k += 256) {
-    const uint64_t c = pb.pane_cnt[k];
+    const uint32_t w = pb.pane_cnt[k];
+    const uint64_t c = w & 0x3FFFFFFFu;
+    anyfl |= w >> 30;
     total += c;
     if (k < blockIdx.x) before += c;
   }
   before = wave_sum_u64(before);
   total = wave_sum_u64(total);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) anyfl |= __shfl_xor(anyfl, o, 64);
   if ((threadIdx.x & 63) == 0) {
     s_red[threadIdx.x >> 6] = before;
     s_tot[threadIdx.x >> 6] = total;
+    s_fl[threadIdx.x >> 6] = anyfl;
   }
   __syncthreads();
   before = s_red[0] + s_red[1] + s_red[2] + s_red[3];
   total = s_tot[0] + s_tot[1] + s_tot[2] + s_tot[3];
+  const bool direct = (s_fl[0] | s_fl[1] | s_fl[2] | s_fl[3]) == 0;  // uniform over the batch
   const bool has_out = out.key != nullptr;
   if (threadIdx.x == 0 && blockIdx.x + 1 == nch) {
     // last workgroup: batch totals (every placed record updates one group)
-    sc->scratch[1] = 0;
-    sc->scratch[3] = has_out ? total : 0;
-    sc->scratch[2] = 1;
+    if (direct) {
+      sc->scratch[1] = 0;
+      sc->scratch[3] = has_out ? total : 0;
+      sc->scratch[2] = 1;
+    } else {
+      sc->scratch[1] = total;  // the touched list: one entry per partial
+      sc->scratch[3] = 0;
+      sc->scratch[2] = 2;
+    }
     sc->scratch[0] = total;
     sc->pairs = pb.bstart[nb];
   }
@@ -455,24 +574,64 @@ __global__ __launch_bounds__(256) void k_sql_apply(Program prog, TwParams p, Par
                                        : tw_find_or_insert(t, g, fresh);
     if (slot < 0) {
       err |= ERR_OOM;
+      if (!direct) pb.touched[before + q] = kTouchSkip;
       continue;
     }
     int64_t *row = t.aggs(slot);
     uint32_t *stp = t.stamp(slot);
-    if (fresh == f0) {
-      // an existing group (its window's earlier batches): the row first, then
-      // this batch's partial (later in arrival order)
-      int64_t c[MS];
+    bool first = true;
+    if (shared) {
+      // under the row's lock: one holder at a time, and a lane that takes it
+      // finishes and releases it in the same pass (lanes of one wave never
+      // wait on each other)
+      // (a done flag, not a break out of the loop: the critical section must
+      // stay inside the loop, where the compiler cannot move it past the
+      // spinning lanes; a bound on the passes turns a lost lock into an error
+      // instead of a hang)
+      uint32_t *lk = stp + 1;
+      bool done = false;
+      for (uint32_t pass = 0; !done; ++pass) {
+        if (pass > (1u << 24)) {
+          err |= ERR_OOM;
+          break;
+        }
+        if (atomicCAS(lk, 0u, 1u) == 0u) {
+          int64_t c[MS];
 #pragma unroll
-      for (int s = 0; s < MS; ++s) c[s] = s < ns ? __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-      combine_row<MS>(prog, c, v);
+          for (int s = 0; s < MS; ++s)
+            c[s] = s < ns ? __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+          sql_combine_any<MS>(prog, c, v);
 #pragma unroll
-      for (int s = 0; s < MS; ++s) v[s] = c[s];
+          for (int s = 0; s < MS; ++s)
+            if (s < ns) __hip_atomic_store(row + s, c[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          first = __hip_atomic_load(stp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != bid;
+          if (first) __hip_atomic_store(stp, bid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the row's stores before the release
+          atomicExch(lk, 0u);
+          done = true;
+        }
+      }
+    } else {
+      if (fresh == f0) {
+        // an existing group (its window's earlier batches): the row first, then
+        // this batch's partial (later in arrival order)
+        int64_t c[MS];
+#pragma unroll
+        for (int s = 0; s < MS; ++s) c[s] = s < ns ? __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        combine_row<MS>(prog, c, v);
+#pragma unroll
+        for (int s = 0; s < MS; ++s) v[s] = c[s];
+      }
+#pragma unroll
+      for (int s = 0; s < MS; ++s)
+        if (s < ns) row[s] = v[s];
+      if (!direct) first = *stp != bid;
+      *stp = bid;
     }
-#pragma unroll
-    for (int s = 0; s < MS; ++s)
-      if (s < ns) row[s] = v[s];
-    *stp = bid;
+    if (!direct) {
+      pb.touched[before + q] = first ? (uint32_t)slot : kTouchSkip;
+      continue;
+    }
     if (has_out) {
       // v is the group's state after this batch: its changelog row
       const uint64_t o = out_base + before + q;
@@ -507,7 +666,7 @@ __global__ __launch_bounds__(256) void k_sql_apply(Program prog, TwParams p, Par
 // the op shape this path takes: one-window packed records with the sequence
 // word (<= 2 columns), the full slot program in LDS (<= 16 slots)
 bool sql_lean_eligible(const Program &prog, const PartParams &pp) {
-  return pp.pane_S == 1 && pp.rbits == 0 && pp.has_seq && (pp.words == 4 || pp.words == 5) && prog.n_slots <= 16;
+  return pp.pane_S == 1 && pp.has_seq && (pp.words == 4 || pp.words == 5) && prog.n_slots <= 16;
 }
 
 template <int MS, int E, int NT, uint64_t SIG = 0, uint64_t SIG2 = 0>

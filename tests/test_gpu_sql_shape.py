@@ -150,3 +150,63 @@ def test_sql_shape_c2_reduced(emit, f64):
         assert st["lean_batches"] == nb and st["replays"] == 0, st
     g.close()
     eng.close()
+
+
+@pytest.mark.parametrize("f64", [False, True], ids=["i64", "f64"])
+def test_sql_shape_hot_keys_and_full_tables(f64):
+    """The SQL shape on skewed keys (BASELINE C5's shape, reduced): a hot key
+    whose bucket is split over several aggregation workgroups, and buckets
+    with more groups than a chunk's LDS table holds (each such record a
+    partial of its own). Both meet in k_sql_apply under the rows' locks, in
+    any order; the changelog then comes from the touched list. Every batch
+    stays on the SQL lean kernels; values, forms and ties match the oracle
+    and the reference's sequential fold."""
+    import pyoracle
+    from hstream_amd.engine import Engine
+    nb, per = 2, 1_500_000
+    total = nb * per
+    ct = abi.HSG_F64 if f64 else abi.HSG_I64
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=60_000, col_types=[ct], aggs=AGGS,
+                  flags=abi.HSG_OPF_LITERAL_FORMS)
+    rng = np.random.default_rng(11 + f64)
+    batches = []
+    for b in range(nb):
+        _k, t, c, va = _gen(21 + f64, per, b * per, total, 4096, f64)
+        z = rng.zipf(1.2, size=per)
+        key = np.where(z <= 400_000, z, rng.integers(1, 400_000, size=per)).astype(np.uint32)
+        batches.append((key, t, c, va))
+    key = np.concatenate([b[0] for b in batches])
+    ts = np.concatenate([b[1] for b in batches])
+    v = np.concatenate([b[2] for b in batches])
+    valid = np.concatenate([b[3] for b in batches])
+    gid = key.astype(np.int64) * 1_000_000 + (ts // 60_000 - TS0 // 60_000)
+    fw = _prefix_forms(gid, v, valid, f64)
+    eng = Engine(device=0, batch_capacity=per)
+    g = eng.op(spec)
+    o = pyoracle.OracleOp(spec)
+    f64s = spec.agg_is_f64()
+    wg = wo = -1
+    for bi, (k, t, c, va) in enumerate(batches):
+        wg = g.push(k, t, [c], [va], watermark=wg)
+        wo = o.push(k, t, [c], [va], watermark=wo)
+        assert wg == wo
+        a, b = g.drain(), o.drain()
+        rows_equal(a, b, f64s, what=f"batch {bi}")
+        base = bi * per
+        gg = gid[base:base + per]
+        # the state after a group's last record of the batch: its last index
+        order = np.argsort(gg, kind="stable")
+        last_of = {}
+        sg = gg[order]
+        ends = np.r_[np.nonzero(sg[1:] != sg[:-1])[0], len(sg) - 1]
+        for e in ends:
+            last_of[int(sg[e])] = base + int(order[e])
+        a = a.sorted()
+        want = np.array([fw[last_of[int(kk) * 1_000_000 + (int(ws) // 60_000 - TS0 // 60_000)]]
+                         for kk, ws in zip(a.key_id, a.win_start)], np.uint32)
+        np.testing.assert_array_equal(a.form, want, err_msg=f"batch {bi}: forms")
+    rows_equal(g.dump_state(), o.dump_state(), f64s, what="state")
+    st = g.stats()
+    assert st["lean_batches"] == nb, st
+    g.close()
+    eng.close()

@@ -3,7 +3,7 @@
 # (kernel statistics per line under gpurun_out/prof/NAME_*)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 if [ -n "$T" ]; then
-  timeout -k 10 ${TT:-900} python -u -m pytest $T -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pt_ab.log 2>&1
+  timeout -k 10 ${TT:-900} python -u -m pytest $T -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/pt_ab.log 2>&1
   rc=$?; tail -3 gpurun_out/pt_ab.log; [ $rc -eq 0 ] || exit $rc
 fi
 IFS=';' read -ra LINES <<< "$AB"
