@@ -71,6 +71,8 @@ def parse():
                    help="skip the sql_shape block (the SQL drop-in's op shape: literal forms + a passthrough)")
     p.add_argument("--sql-emit", default="both", choices=["both", "per_batch", "per_record"],
                    help="emit modes of the sql_shape block")
+    p.add_argument("--only-sql", action="store_true",
+                   help="profiling aid: only the sql_shape block (HBM-resident), no headline line")
     return p.parse_args()
 
 
@@ -152,6 +154,16 @@ def main():
             el = float(tt.item())
         return el, st0, st1
 
+    if args.only_sql:
+        # (profiling aid: the SQL op shape's kernels alone, e.g. for PMC traffic)
+        op.close()
+        sql = sql_shape_block(eng, cfg, keys, ts, cols, pieces, args)
+        if rank == 0:
+            print(json.dumps({"metric": "records/sec windowed GROUP BY (sql_shape only)", "value": None,
+                              "config": {"workload": f"{cfg.name}: {workload_text(cfg)}"}, "sql_shape": sql}),
+                  flush=True)
+        eng.close()
+        return
     dev_step = device_steps(op, keys, ts, cols, pieces, emit, args)
     hbm = None
     if args.input == "host":
