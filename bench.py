@@ -637,6 +637,9 @@ def sql_shape_block(eng, cfg, keys, ts, cols, pieces, args):
                           "sequence word, k_agg_sql, k_sql_apply writing the changelog rows)" if mode == "per_batch"
                           else "per-record changelog (k_part_hist_opt, offsets + decide, stable k_part_scatter_st "
                                "with the sequence word, k_pr_bucket, k_pr_emit1)")
+        tr = sql_traffic(cfg, mode)
+        if tr:
+            roof["traffic"], roof["traffic_source"] = tr
         batches = st1["batches"] - st0["batches"]
         out[mode] = {"value": round(n_rank * k / el, 1), "unit": "records/s", "steps": k,
                      "ms_per_step": round(el * 1e3 / k, 3), "roofline": roof,
@@ -647,6 +650,20 @@ def sql_shape_block(eng, cfg, keys, ts, cols, pieces, args):
         op.close()
         torch.cuda.empty_cache()
     return out
+
+
+def sql_traffic(cfg, mode):
+    """Per-batch HBM bytes of the SQL op shape's pipeline on this config from
+    the committed PMC summary (tools/gpu_r6_profile.sh ->
+    profiles/<round>/traffic_<config>_sql[_pr].json), else None."""
+    import glob
+    name = f"traffic_{cfg.name.lower()}_sql{'_pr' if mode == 'per_record' else ''}.json"
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)))
+    if not paths:
+        return None
+    with open(paths[-1]) as f:
+        d = json.load(f)
+    return int(d["hbm_bytes_per_batch"]), os.path.relpath(paths[-1], ROOT)
 
 
 def workload_text(cfg):
@@ -745,7 +762,7 @@ def committed_traffic(args, world):
     with open(paths[-1]) as f:
         d = json.load(f)
     # flags that only switch the extra blocks off measure the same pipeline
-    extra = {"--no-host-input", "--no-per-record", "--no-hbm", "--input", "hbm"}
+    extra = {"--no-host-input", "--no-per-record", "--no-hbm", "--no-sql-shape", "--input", "hbm"}
     words = [w for w in d.get("bench_args", "").split() if w not in extra]
     want = ["--config", args.config]
     if pr:
