@@ -172,7 +172,14 @@ static void adapt_partitions(OpDevice &d, const hsg_op_config &cfg, const Progra
     return w > by_size ? w : by_size;
   };
   uint64_t want = need(false);
-  d.agg_big = want > (1ull << kPartMaxLog2) && !d.sql_lean;  // (the SQL lean kernels: one LDS variant)
+  // one-window ops of more than two slots take the big table whatever the
+  // group count: half the buckets, so the scatter's runs per (tile, bucket)
+  // are twice as long and the (tile, bucket) offsets matrix half the size
+  // (C2: scatter 164 -> 137 us, aggregation 113 -> 126 us, 30.5 -> 32.3 G
+  // records/s HBM-resident); HSG_AGG_SMALL keeps the small table (A/B)
+  static const bool keep_small = getenv("HSG_AGG_SMALL") != nullptr;
+  const bool prefer_big = !keep_small && cfg.window_kind != HSG_HOPPING && d.pane_S == 1 && prog.n_slots > 2;
+  d.agg_big = (want > (1ull << kPartMaxLog2) || prefer_big) && !d.sql_lean;  // (the SQL lean kernels: one LDS variant)
   if (d.agg_big) want = need(true);
   int l = 0;
   while ((1ull << l) < want && l < kPartMaxLog2) ++l;
