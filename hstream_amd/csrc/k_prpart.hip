@@ -734,7 +734,8 @@ __global__ __launch_bounds__(kPrEmitThreads) void k_pr_emit(Batch bt, Program pr
     }
     roff[threadIdx.x] = before;
     if (threadIdx.x == kPrEmitThreads - 1) roff[kPrEmitThreads] = before + n;
-    rpos[threadIdx.x] = n ? pr.kpos[pr.pos[i]] : 0u;  // (k_pr_keysort's place of the record)
+    // (k_pr_keysort's place of the record; one-window ops: no key grouping)
+    rpos[threadIdx.x] = n ? (pr.kpos ? pr.kpos[pr.pos[i]] : pr.pos[i]) : 0u;
     rkey[threadIdx.x] = key;
     rwin[threadIdx.x] = a;
     lds_barrier();
@@ -987,7 +988,7 @@ __global__ __launch_bounds__(kPbNT) void k_pr_bucket(Program prog, TwParams p, P
   __shared__ uint8_t widx[kPbNW][CAP];     // per wave: 1 + owner lane of each group in the step, 0 = none
   __shared__ uint32_t s_fill;
   __shared__ uint64_t s_red[2][kPbNW];
-  if (sc->redo) return;  // uniform: the optimistic pass found late records (bucket starts are stale)
+  if (sc->redo || pr.counter[1]) return;  // uniform: stale bucket starts / a hot bucket: the chunked path runs
   const uint32_t b = blockIdx.x;
   const uint64_t r0 = pb.bstart[b], r1 = pb.bstart[b + 1];
   if (r0 >= r1) return;  // uniform
@@ -1343,7 +1344,7 @@ __global__ __launch_bounds__(kE1NT) void k_pr_emit1(Batch bt, Program prog, TwPa
                                                              const int64_t *__restrict__ seq, OutCols out,
                                                              uint64_t out_base, uint64_t out_cap, DevScalars *sc) {
   __shared__ uint32_t sw[kE1][kE1NT / 64];
-  if (sc->redo) return;  // uniform
+  if (sc->redo || pr.counter[1]) return;  // uniform (a hot bucket: the chunked path's k_pr_emit)
   const int64_t k_epoch = sc->k_epoch;
   const int64_t *wm = rec_wm ? rec_wm : (sc->no_late ? nullptr : pb.wm);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1832,6 +1833,19 @@ __global__ __launch_bounds__(kPkNT) void k_pr_keys(Program prog, TwParams p, Par
   }
 }
 
+// One-window ops: a bucket of more than kPrHot records (a very hot key) would
+// serialise k_pr_bucket on one workgroup; counter[1] then sends the batch to
+// the chunked path (k_pr_local / k_pr_carry / k_pr_emit over the bucket's
+// arrival-order records, chunks in parallel, carries in order)
+constexpr uint64_t kPrHot = 65536;
+__global__ __launch_bounds__(256) void k_pr_hot(const uint64_t *bstart, int nb, const DevScalars *sc, PrPart pr) {
+  if (sc->redo) return;
+  uint32_t hot = 0;
+  for (int b = threadIdx.x; b < nb; b += 256) hot |= bstart[b + 1] - bstart[b] > kPrHot ? 1u : 0u;
+  hot = __syncthreads_or(hot);
+  if (threadIdx.x == 0 && hot) pr.counter[1] = 1;
+}
+
 // k_pr_emit1's program: with a projected per-record state (hsg_internal.h
 // fin_*) the outputs read the projected words, so their slot indices are
 // remapped to those words' positions (fin_n / fin_form stay: they tell the
@@ -1857,6 +1871,7 @@ static void pr_launch(hipStream_t s, const Batch &b, const Program &prog, const 
                       const int64_t *seq, const OutCols &out, uint64_t out_base, uint64_t out_cap, DevScalars *sc) {
   const uint64_t nb = 1ull << pp.np_log2;
   if (wpr == 1) {
+    hipLaunchKernelGGL(k_pr_hot, dim3(1), dim3(256), 0, s, pb.bstart, (int)nb, sc, pr);
     // LDS: 10 B per table slot, 8 MS + 4 + 4 per group (half the slots), staging 2 KB per state slot
     constexpr int LT = MS <= 6 ? 10 : 9;
     const dim3 gb((unsigned)nb), tb(kPbNT);
@@ -1915,6 +1930,16 @@ static void pr_launch(hipStream_t s, const Batch &b, const Program &prog, const 
     else if (fw <= 8 && MS >= 8) HSG_E1(8);
     else HSG_E1(MS);
 #undef HSG_E1
+    // ... or, with a hot bucket, the chunked path over the arrival-order
+    // records (each kernel returns at once otherwise)
+    const uint64_t nchunks = nb + b.n / pp.chunk + 1;
+    const dim3 g((unsigned)(nchunks < 4096 ? nchunks : 4096));
+    PrPart pr1 = pr;
+    pr1.kpos = nullptr;  // (no key grouping: a record's pairs sit at its partitioned position)
+    hipLaunchKernelGGL(k_pr_local<MS>, g, dim3(kPrNT), 0, s, prog, pp, pb, pr1, wpr, sc);
+    hipLaunchKernelGGL(k_pr_carry<MS>, dim3((unsigned)nb), dim3(256), 0, s, prog, p, pp, t, pb, pr1, sc);
+    hipLaunchKernelGGL(k_pr_emit<MS>, ge, dim3(kPrEmitThreads), 0, s, b, prog, p, pp, pb, pr1, wpr, rec_wm, seq, out,
+                       out_base, out_cap, sc);
     return;
   }
   const uint64_t nchunks = nb + b.n / pp.chunk + 1;  // >= the partition's chunks

@@ -195,7 +195,7 @@ static int push_time_perrecord_part(OpDevice &d, const hsg_op_config &cfg, const
     // k_pr_carry / k_pr_emit) even when every bucket fits the key sort (tests, A/B)
     static const bool chunked = getenv("HSG_PR_CHUNKED") != nullptr;
     if (wpr != 1 && chunked) DTRY(hipMemsetAsync(d.prp.counter + 1, 1, 1, d.stream));
-    if (wpr != 1) launch_part_chunks(d.stream, pp, d.part, d.sc);
+    launch_part_chunks(d.stream, pp, d.part, d.sc);  // (one-window ops: for a hot bucket's chunked path)
     launch_pr_part(d.stream, kb, prog, p, pp, d.tw, d.part, d.prp, wpr, rec_wm, seq, d.out, a.pending, d.out_cap,
                    d.sc);
     DTRY(hipEventRecord(d.ev_b, d.stream));

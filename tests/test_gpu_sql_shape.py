@@ -210,3 +210,50 @@ def test_sql_shape_hot_keys_and_full_tables(f64):
     assert st["lean_batches"] == nb, st
     g.close()
     eng.close()
+
+
+@pytest.mark.parametrize("shape", ["sql", "plain"])
+def test_per_record_hot_key_chunked(shape):
+    """EMIT CHANGES of a one-window op with a hot key (its partition bucket far
+    over kPrHot records): the batch takes the chunked path (chunks of the
+    bucket in parallel, carries in order) instead of one workgroup walking
+    the bucket. Every row, in arrival order, against the oracle; forms of
+    the SQL shape against the reference's sequential fold."""
+    import pyoracle
+    from hstream_amd.engine import Engine
+    nb, per = 2, 1_000_000
+    total = nb * per
+    aggs = AGGS if shape == "sql" else [(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0), (abi.HSG_MAX, 0)]
+    flags = abi.HSG_OPF_LITERAL_FORMS if shape == "sql" else 0
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_RECORD, size_ms=60_000, col_types=[abi.HSG_I64], aggs=aggs,
+                  flags=flags)
+    rng = np.random.default_rng(31)
+    batches = []
+    for b in range(nb):
+        _k, t, c, va = _gen(41, per, b * per, total, 4096, False)
+        z = rng.zipf(1.2, size=per)
+        key = np.where(z <= 200_000, z, rng.integers(1, 200_000, size=per)).astype(np.uint32)
+        batches.append((key, t, c, va))
+    eng = Engine(device=0, batch_capacity=per)
+    g = eng.op(spec)
+    o = pyoracle.OracleOp(spec)
+    f64s = spec.agg_is_f64()
+    fw = None
+    if shape == "sql":
+        key = np.concatenate([b[0] for b in batches])
+        ts = np.concatenate([b[1] for b in batches])
+        gid = key.astype(np.int64) * 1_000_000 + (ts // 60_000 - TS0 // 60_000)
+        fw = _prefix_forms(gid, np.concatenate([b[2] for b in batches]), np.concatenate([b[3] for b in batches]),
+                           False)
+    wg = wo = -1
+    for bi, (k, t, c, va) in enumerate(batches):
+        wg = g.push(k, t, [c], [va], watermark=wg)
+        wo = o.push(k, t, [c], [va], watermark=wo)
+        assert wg == wo
+        a, b = g.drain(), o.drain()
+        rows_equal(a, b, f64s, ordered=True, what=f"batch {bi}")
+        if fw is not None:
+            np.testing.assert_array_equal(a.form, fw[a.src_index], err_msg=f"batch {bi}: forms")
+    rows_equal(g.dump_state(), o.dump_state(), f64s, what="state")
+    g.close()
+    eng.close()
