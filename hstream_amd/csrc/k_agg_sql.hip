@@ -89,19 +89,84 @@ __device__ inline bool sql_chunk(const PartParams &pp, const PartBuffers &pb, ui
   return true;
 }
 
-// phase 1 of one record on LDS entry e (slot-major, ST entries per slot)
+// LDS columns of the state slots. A runtime program keeps one column per
+// slot. A baked program (the SQL C2 query) packs its counts -- COUNT(*),
+// COUNT(col), the SUM's decimal count, each < 2^21 in a chunk of <= 2^15
+// records -- into one column updated by one atomic, and keeps no LAST
+// sequence column (that word is the LAST_FORM word >> 1): 8 columns instead
+// of 11, so a 2048-entry table fits the LDS beside its keys.
+template <class PV>
+struct SqlLay {
+  static constexpr bool kPacked = false;
+  static constexpr int ncols(int ms) { return ms; }
+  __device__ static int col(const PV &, int s) { return s; }
+  __device__ static int field(const PV &, int) { return -1; }
+  __device__ static bool derived(const PV &, int) { return false; }
+};
+template <uint64_t A, uint64_t B>
+struct SqlLay<ProgSig<A, B>> {
+  using P = ProgSig<A, B>;
+  static constexpr bool kPacked = true;
+  static constexpr int field_of(int s) {
+    return P::op_of(s) == S_CNT_ALL ? 0 : P::op_of(s) == S_CNT ? 1 : P::op_of(s) == S_CNT_DEC ? 2 : -1;
+  }
+  static constexpr bool derived_of(int s) { return P::op_of(s) == S_LAST_SEQ && P::last_form_of(s) >= 0; }
+  static constexpr int col_of(int s) {
+    if (field_of(s) >= 0) return 0;
+    if (derived_of(s)) return -1;
+    int c = 1;
+    for (int k = 0; k < s; ++k)
+      if (field_of(k) < 0 && !derived_of(k)) ++c;
+    return c;
+  }
+  static constexpr int ncols(int) {
+    int c = 1;
+    for (int k = 0; k < P::count(); ++k)
+      if (field_of(k) < 0 && !derived_of(k)) ++c;
+    return c;
+  }
+  static constexpr bool packable() {  // one slot of each count op at most
+    int n[3] = {0, 0, 0};
+    for (int k = 0; k < P::count(); ++k)
+      if (field_of(k) >= 0) ++n[field_of(k)];
+    return n[0] <= 1 && n[1] <= 1 && n[2] <= 1;
+  }
+  __device__ static constexpr int col(const P &, int s) { return col_of(s); }
+  __device__ static constexpr int field(const P &, int s) { return field_of(s); }
+  __device__ static constexpr bool derived(const P &, int s) { return derived_of(s); }
+};
+static_assert(SqlLay<ProgSig<kSigSqlI, kSigSqlI2>>::ncols(12) == 8 && SqlLay<ProgSig<kSigSqlI, kSigSqlI2>>::packable(),
+              "SQL C2 LDS layout");
+constexpr int kCntBits = 21;
+
+// phase 1 of one record on LDS entry e (column-major, ST entries per column)
 template <int MS, int ST, int W, class PV>
 __device__ inline void sql_phase1(const PV &pv, int64_t *__restrict__ agg, const PRec<W, true> &r,
                                   uint32_t skip) {
+  using Lay = SqlLay<PV>;
+  if constexpr (Lay::kPacked) {
+    // every count slot in one atomic on column 0
+    uint64_t add = 0;
+#pragma unroll
+    for (int s = 0; s < MS; ++s) {
+      if (s >= pv.n()) break;
+      const int f = Lay::field(pv, s), c = pv.col(s);
+      if (f == 0) add += 1ull;
+      if (f == 1 && r.present(c)) add += 1ull << kCntBits;
+      if (f == 2 && r.present(c) && r.dec(c)) add += 1ull << (2 * kCntBits);
+    }
+    if (add) atomicAdd((unsigned long long *)agg, (unsigned long long)add);
+  }
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
     if (s >= pv.n()) break;
     const int op = pv.op(s);
     if (op == S_LAST_VAL || slot_is_tie(op) || ((skip >> s) & 1u)) continue;
+    if (Lay::field(pv, s) >= 0 || Lay::derived(pv, s)) continue;  // (packed counts / derived LAST sequence)
     if (op == S_LAST_SEQ && pv_last_form(pv, s) >= 0) continue;  // derived from the LAST_FORM word
     const int c = pv.col(s);
     if (op != S_CNT_ALL && !r.present(c)) continue;
-    int64_t *a = agg + s * ST;
+    int64_t *a = agg + Lay::col(pv, s) * ST;
     unsigned long long *u = (unsigned long long *)a;
     switch (op) {
       case S_CNT_ALL:
@@ -144,7 +209,7 @@ __device__ inline void sql_phase1(const PV &pv, int64_t *__restrict__ agg, const
 #pragma unroll
           for (int k = 0; k < MS; ++k)
             if (k < pv.n() && slot_is_tie(pv.op(k)) && pv_aux(pv, k) == s)
-              agg[k * ST] = pv.op(k) == S_TIE_MIN ? (int64_t)~0ull : 0;
+              agg[Lay::col(pv, k) * ST] = pv.op(k) == S_TIE_MIN ? (int64_t)~0ull : 0;
         }
         break;
       }
@@ -156,6 +221,7 @@ __device__ inline void sql_phase1(const PV &pv, int64_t *__restrict__ agg, const
 // records holding the group's extreme
 template <int MS, int ST, int W, class PV>
 __device__ inline void sql_phase2(const PV &pv, int64_t *__restrict__ agg, const PRec<W, true> &r) {
+  using Lay = SqlLay<PV>;
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
     if (s >= pv.n()) break;
@@ -164,16 +230,17 @@ __device__ inline void sql_phase2(const PV &pv, int64_t *__restrict__ agg, const
     if (op == S_LAST_VAL) {
       // the preceding slot is its LAST_SEQ (build_program last_pair)
       const int lf = s > 0 ? pv_last_form(pv, s - 1) : -1;
-      const uint64_t last = lf >= 0 ? (uint64_t)agg[lf * ST] >> 1 : (uint64_t)agg[(s - 1) * ST];
-      if (s > 0 && r.present(c) && last == (uint64_t)r.seq1()) agg[s * ST] = r.col(c);
+      const uint64_t last =
+          lf >= 0 ? (uint64_t)agg[Lay::col(pv, lf) * ST] >> 1 : (uint64_t)agg[Lay::col(pv, s - 1) * ST];
+      if (s > 0 && r.present(c) && last == (uint64_t)r.seq1()) agg[Lay::col(pv, s) * ST] = r.col(c);
     } else if (slot_is_tie(op)) {
       if (!r.present(c)) continue;
       const int v = pv_aux(pv, s), vop = pv.op(v);
       const int64_t x = r.col(c);
       const int64_t xv = (vop == S_MIN_F || vop == S_MAX_F) ? (int64_t)f64_ord(__builtin_bit_cast(double, x)) : x;
-      if (agg[v * ST] != xv) continue;
+      if (agg[Lay::col(pv, v) * ST] != xv) continue;
       const uint64_t w = ((uint64_t)r.seq1() << 1) | (r.dec(c) ? 0u : 1u);
-      unsigned long long *u = (unsigned long long *)(agg + s * ST);
+      unsigned long long *u = (unsigned long long *)(agg + Lay::col(pv, s) * ST);
       if (op == S_TIE_MIN) atomicMin(u, (unsigned long long)w);
       else atomicMax(u, (unsigned long long)w);
     }
@@ -220,7 +287,9 @@ __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwT
   const ProgView<SIG, SIG2> pv(prog);  // the SQL C2 query's slot program baked in (else the runtime one)
   constexpr int RB = 4;  // records per thread per block (one block in flight beside it)
   __shared__ uint64_t lkey[E];
-  __shared__ int64_t lagg[MS * E];
+  using Lay = SqlLay<ProgView<SIG, SIG2>>;
+  constexpr int NC = Lay::ncols(MS);  // LDS columns
+  __shared__ int64_t lagg[NC * E];
   __shared__ uint32_t s_cnt, s_ovf, s_fill, s_full;
   __shared__ uint32_t s_bin[kSqlSortBins];
   __shared__ uint32_t s_wsum[NT / 64];
@@ -264,8 +333,10 @@ __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwT
     for (int e = threadIdx.x; e < E; e += NT) {
       lkey[e] = kEmpty;
 #pragma unroll
-      for (int s = 0; s < MS; ++s)
-        if (s < ns) lagg[s * E + e] = slot_identity_dev(pv.op(s));
+      for (int s = 0; s < MS; ++s) {
+        if (s >= ns || Lay::derived(pv, s)) continue;
+        lagg[Lay::col(pv, s) * E + e] = Lay::field(pv, s) >= 0 ? 0 : slot_identity_dev(pv.op(s));
+      }
     }
     if (threadIdx.x == 0) {
       s_fill = 0;
@@ -357,10 +428,11 @@ __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwT
       __syncthreads();  // every thread has read s_full before the reset above rewrites it
       continue;
     }
-    // LAST_SEQ slots kept only through their LAST_FORM word
+    // LAST_SEQ slots kept only through their LAST_FORM word (a runtime
+    // program's column; the packed layout has none: the flush derives it)
 #pragma unroll
     for (int s = 0; s < MS; ++s) {
-      if (s >= ns || pv.op(s) != S_LAST_SEQ) continue;
+      if (Lay::kPacked || s >= ns || pv.op(s) != S_LAST_SEQ) continue;
       const int lf = pv_last_form(pv, s);
       if (lf < 0) continue;
       for (int e = threadIdx.x; e < E; e += NT) lagg[s * E + e] = (int64_t)((uint64_t)lagg[lf * E + e] >> 1);
@@ -407,10 +479,24 @@ __global__ __launch_bounds__(NT) void k_agg_sql(Program prog, PartParams pp, TwT
       const uint32_t q = s_bin[bin[k]] + rank[k];
       uint64_t *o = pane + (uint64_t)q * PW;
       o[0] = lkey[e];
-      const int64_t call = cnt_all_slot >= 0 ? lagg[cnt_all_slot * E + e] : 0;
+      if constexpr (Lay::kPacked) {
+        const uint64_t cw = (uint64_t)lagg[e];  // the packed counts (column 0)
 #pragma unroll
-      for (int s = 0; s < MS; ++s)
-        if (s < ns) o[1 + s] = (uint64_t)(((skip >> s) & 1u) ? call : lagg[s * E + e]);
+        for (int s = 0; s < MS; ++s) {
+          if (s >= ns) continue;
+          const int f = Lay::field(pv, s);
+          uint64_t x;
+          if (f >= 0) x = (cw >> (kCntBits * f)) & ((1ull << kCntBits) - 1);
+          else if (Lay::derived(pv, s)) x = (uint64_t)lagg[Lay::col(pv, pv_last_form(pv, s)) * E + e] >> 1;
+          else x = (uint64_t)lagg[Lay::col(pv, s) * E + e];
+          o[1 + s] = x;
+        }
+      } else {
+        const int64_t call = cnt_all_slot >= 0 ? lagg[cnt_all_slot * E + e] : 0;
+#pragma unroll
+        for (int s = 0; s < MS; ++s)
+          if (s < ns) o[1 + s] = (uint64_t)(((skip >> s) & 1u) ? call : lagg[s * E + e]);
+      }
     }
     __syncthreads();  // the flush has read the table (and s_cnt)
     if (threadIdx.x == 0) s_cnt += live;
@@ -663,6 +749,14 @@ __global__ __launch_bounds__(256) void k_sql_apply(Program prog, TwParams p, Par
   }
 }
 
+// LDS entries of the SQL lean kernel for this program (op_device.cpp
+// adapt_partitions: buckets of at most half a table of groups)
+uint64_t sql_lds_entries(const Program &prog) {
+  uint64_t hi = 0;
+  const uint64_t sq = program_sig(prog, &hi);
+  return ((sq == kSigSqlI && hi == kSigSqlI2) || (sq == kSigSqlF && hi == kSigSqlF2)) ? 2048 : 1024;
+}
+
 // the op shape this path takes: one-window packed records with the sequence
 // word (<= 2 columns), the full slot program in LDS (<= 16 slots)
 bool sql_lean_eligible(const Program &prog, const PartParams &pp) {
@@ -694,10 +788,11 @@ bool launch_part_agg_sql(hipStream_t s, dim3 g, const Program &prog, const TwPar
     // the SQL drop-in's C2 query: its slot program baked in
     uint64_t hi = 0;
     const uint64_t sq = program_sig(prog, &hi);
+    // (its packed LDS layout: a 2048-entry table, buckets of twice the groups)
     if (sq == kSigSqlI && hi == kSigSqlI2)
-      sql_launch<12, 1024, 1024, kSigSqlI, kSigSqlI2>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
+      sql_launch<12, 2048, 1024, kSigSqlI, kSigSqlI2>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
     else if (sq == kSigSqlF && hi == kSigSqlF2)
-      sql_launch<12, 1024, 1024, kSigSqlF, kSigSqlF2>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
+      sql_launch<12, 2048, 1024, kSigSqlF, kSigSqlF2>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
     else
       sql_launch<12, 1024, 1024>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
   }

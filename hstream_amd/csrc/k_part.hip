@@ -649,15 +649,22 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
                                                           const int64_t *__restrict__ seq, DevScalars *sc) {
   // STABLE: wave w's running count of bucket b over its rounds, then the
   // exclusive prefix of those counts over the waves
+  // SEQ3: the SQL op shape's one-window records [header][value][sequence
+  // word] staged as two words -- the header carries the record's tile-local
+  // index in its window-count field (one window: rebuilt at write-out) and
+  // the decimal bit, the sequence word is made at write-out -- so whole tiles
+  // fit two workgroups per CU
+  constexpr bool SEQ3 = W == 3 && !STABLE;
+  constexpr int SW = SEQ3 ? 2 : W;  // staged words per record
   __shared__ uint16_t wcnt[STABLE ? kPW : 1][1 << kPartMaxLog2];
-  __shared__ uint64_t stage[T * W];
+  __shared__ uint64_t stage[T * SW];
   __shared__ uint32_t cnt2[1 << (kPartMaxLog2 - 1)];  // two u16 counts per word, then the u16 run starts
   __shared__ uint32_t cursor[1 << kPartMaxLog2];      // the row's next output slot per bucket
   __shared__ uint32_t swave[kPNT / 64];
   // W == 3: each staged record's output slot, so the write-out can go word by
   // word (consecutive lanes, consecutive 8-byte words of a run) instead of
   // three 8-byte stores 24 bytes apart per lane
-  __shared__ uint32_t sdest[W == 3 ? T : 1];
+  __shared__ uint32_t sdest[W == 3 && !SEQ3 ? T : 1];
   if (sc->redo || !sc->packed) return;  // uniform: the gather variant runs
   constexpr int R = T / kPNT;
   const int nb = 1 << pp.np_log2;
@@ -690,7 +697,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
     uint32_t key[R];
     int64_t ts[R];
     uint64_t col[R];
-    uint64_t sqw[W == 3 ? R : 1];  // W == 3: the sequence word (seq + 1 | literal bits << 56)
+    uint64_t sqw[W == 3 ? R : 1];  // W == 3: the sequence word (seq + 1 | literal bits << 56); SEQ3: the decimal bit
     // STABLE: each wave takes R*64 consecutive records (64 per round), so a
     // record's arrival rank needs no block barrier per round
     auto rec_i = [&](int r) -> uint64_t {
@@ -703,7 +710,8 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
       key[r] = in ? b.key[i] : HSG_KEY_NONE;
       ts[r] = in ? b.ts[i] : 0;
       col[r] = (W >= 2 && in) ? (uint64_t)b.col[0][i] : 0;
-      if constexpr (W == 3) sqw[r] = in ? seq_word(b, 1, pp.has_valid, seq ? seq[i] : (int64_t)(p.rec_base + i), i) : 0;
+      if constexpr (SEQ3) sqw[r] = in && pp.has_valid && b.valid[0] && (b.valid[0][i] & 2u) ? 1u : 0u;
+      else if constexpr (W == 3) sqw[r] = in ? seq_word(b, 1, pp.has_valid, seq ? seq[i] : (int64_t)(p.rec_base + i), i) : 0;
     }
     __syncthreads();  // counters clear
     uint32_t slot[R];  // bucket << 16 | slot in the sub-tile's run of the bucket, ~0 = no window
@@ -731,8 +739,16 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
       const uint64_t i = rec_i(r);
       uint64_t vb = 0;
       if (W >= 2 && !(pp.has_valid && b.valid[0] && !b.valid[0][i])) vb = 1;
-      ts[r] = (int64_t)((uint64_t)key[r] | ((uint64_t)((krel - kbase) & 0xFFFFu) << 32) | ((uint64_t)nwin << 48) |
-                        (vb << 56));  // the packed header word, kept in the ts register
+      if constexpr (SEQ3) {
+        // (one window per record on this path: tumbling / unwindowed)
+        if (nwin != 1) err |= ERR_RANGE;
+        const uint64_t local = i - base;  // < T: 12 bits
+        ts[r] = (int64_t)((uint64_t)key[r] | ((uint64_t)((krel - kbase) & 0xFFFFu) << 32) | (local << 48) |
+                          (vb << 60) | (sqw[r] << 61));
+      } else {
+        ts[r] = (int64_t)((uint64_t)key[r] | ((uint64_t)((krel - kbase) & 0xFFFFu) << 32) | ((uint64_t)nwin << 48) |
+                          (vb << 56));  // the packed header word, kept in the ts register
+      }
     }
     __syncthreads();
     // sub-tile-local exclusive scan of the bucket counts -> run starts (in place)
@@ -777,14 +793,34 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
       const uint32_t rk = (slot[r] & 0xFFFFu) + (STABLE ? (uint32_t)wcnt[wv][sb] : 0u);
       if (pb.pos) pb.pos[rec_i(r)] = cursor[sb] + rk;
       const uint32_t q = lstart[sb] + rk;
-      stage[q * W] = (uint64_t)ts[r];
-      if (W >= 2) stage[q * W + 1] = col[r];
-      if constexpr (W == 3) stage[q * W + 2] = sqw[r];
+      stage[q * SW] = (uint64_t)ts[r];
+      if (W >= 2) stage[q * SW + 1] = col[r];
+      if constexpr (W == 3 && !SEQ3) stage[q * W + 2] = sqw[r];
     }
     __syncthreads();
     q1 = phase_clock();
     // write-out: record q goes to the row's slot for its bucket + (q - run start)
-    if constexpr (W == 3) {
+    if constexpr (SEQ3) {
+      // word by word: the header rebuilt (one window, the present bit), the
+      // value, the sequence word (seq + 1 | decimal bit << 56)
+      for (uint32_t w = threadIdx.x; w < placed * 3; w += kPNT) {
+        const uint32_t q = w / 3, j = w - 3 * q;
+        const uint64_t h = stage[q * 2];
+        const uint32_t bk = bucket_of((uint32_t)h, pp.np_log2, pp.bshift);
+        const uint64_t dest = (uint64_t)cursor[bk] + (q - lstart[bk]);
+        uint64_t v;
+        if (j == 0) {
+          v = (h & 0x0000FFFFFFFFFFFFull) | (1ull << 48) | (((h >> 60) & 1ull) << 56);
+        } else if (j == 1) {
+          v = stage[q * 2 + 1];
+        } else {
+          const uint64_t i = base + ((h >> 48) & 0xFFFull);
+          v = ((uint64_t)((seq ? seq[i] : (int64_t)(p.rec_base + i)) + 1) & kSeqMask) | (((h >> 61) & 1ull) << 56);
+        }
+        pb.rec[dest * 3 + j] = v;
+      }
+    }
+    if constexpr (W == 3 && !SEQ3) {
       for (uint32_t q = threadIdx.x; q < placed; q += kPNT) {
         const uint32_t bk = bucket_of((uint32_t)stage[q * W], pp.np_log2, pp.bshift);
         sdest[q] = cursor[bk] + (q - lstart[bk]);
@@ -835,10 +871,13 @@ void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const
   if (stage) {
     const dim3 th(kPNT);
     if (pp.words - 1 == 3) {
-      // (half tiles: 48 KB of staging, two workgroups per CU; whole tiles, one
-      // workgroup per CU, measured 0.43 against 0.34 ms per C2 SQL batch)
+      // (the stable variant on half tiles: 48 KB of staging, two workgroups
+      // per CU; the per-batch one stages two words per record -- SEQ3 -- and
+      // takes whole tiles at two workgroups per CU; three staged words on
+      // whole tiles, one workgroup per CU, measured 0.43 against 0.34 ms per
+      // C2 SQL batch on half tiles)
       if (stable) hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 3, true>), g, th, 0, s, b, p, pp, pb, seq, sc);
-      else hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 3, false>), g, th, 0, s, b, p, pp, pb, seq, sc);
+      else hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 3, false>), g, th, 0, s, b, p, pp, pb, seq, sc);
     } else if (pp.words - 1 == 2) {
       if (stable) hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 2, true>), g, th, 0, s, b, p, pp, pb, seq, sc);
       else hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 2, false>), g, th, 0, s, b, p, pp, pb, seq, sc);

@@ -164,10 +164,13 @@ int part_device_init(OpDevice &d, const hsg_op_config &cfg, const Program &prog,
 // (two workgroups per CU) when that needs at most 2^kPartMaxLog2 buckets;
 // fewer buckets mean longer coalesced runs in the scatter. When the bucket
 // count is at its maximum, key-hash rounds split a bucket's groups instead.
+uint64_t sql_lds_entries(const Program &prog);  // k_agg_sql.hip
+
 static void adapt_partitions(OpDevice &d, const hsg_op_config &cfg, const Program &prog, uint64_t groups, uint64_t n) {
   const uint64_t by_size = (n + kAggChunk / 2 - 1) / (kAggChunk / 2);  // buckets of <= half a chunk on average
+  auto entries = [&](bool big) { return d.sql_lean ? sql_lds_entries(prog) : part_lds_entries(prog, big); };
   auto need = [&](bool big) {
-    const uint64_t per = part_lds_entries(prog, big) / 2;
+    const uint64_t per = entries(big) / 2;
     uint64_t w = (groups + per - 1) / per;
     return w > by_size ? w : by_size;
   };
@@ -185,7 +188,7 @@ static void adapt_partitions(OpDevice &d, const hsg_op_config &cfg, const Progra
   while ((1ull << l) < want && l < kPartMaxLog2) ++l;
   d.np_log2 = l < 4 ? 4 : l;
   const uint64_t per_bucket = groups >> d.np_log2;
-  const uint64_t fit = part_lds_entries(prog, d.agg_big) * 6 / 10;
+  const uint64_t fit = entries(d.agg_big) * 6 / 10;
   int rb = 0;
   while ((fit << rb) < per_bucket && rb < 4) ++rb;
   d.rbits = d.pane_S ? rb : 0;
