@@ -644,7 +644,7 @@ void launch_part_decide_offsets(hipStream_t s, DevScalars *sc, const TwParams &p
 // misses (PMC) and waited on them. LDS: the tile (T x W words), two u16
 // counters per u32, u16 run starts: 72 KiB at W = 2, two workgroups per CU.
 // The bucket of a staged record is recomputed from its key at write-out.
-template <int T, int W, bool STABLE>
+template <int T, int W, bool STABLE, bool ONEWIN = false>
 __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, PartParams pp, PartBuffers pb,
                                                           const int64_t *__restrict__ seq, DevScalars *sc) {
   // STABLE: wave w's running count of bucket b over its rounds, then the
@@ -654,7 +654,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
   // index in its window-count field (one window: rebuilt at write-out) and
   // the decimal bit, the sequence word is made at write-out -- so whole tiles
   // fit two workgroups per CU
-  constexpr bool SEQ3 = W == 3 && !STABLE;
+  constexpr bool SEQ3 = W == 3 && ONEWIN;
   constexpr int SW = SEQ3 ? 2 : W;  // staged words per record
   __shared__ uint16_t wcnt[STABLE ? kPW : 1][1 << kPartMaxLog2];
   __shared__ uint64_t stage[T * SW];
@@ -742,7 +742,7 @@ __global__ __launch_bounds__(kPNT) void k_part_scatter_st(Batch b, TwParams p, P
       if constexpr (SEQ3) {
         // (one window per record on this path: tumbling / unwindowed)
         if (nwin != 1) err |= ERR_RANGE;
-        const uint64_t local = i - base;  // < T: 12 bits
+        const uint64_t local = i - base;  // < T <= 4096: 12 bits
         ts[r] = (int64_t)((uint64_t)key[r] | ((uint64_t)((krel - kbase) & 0xFFFFu) << 32) | (local << 48) |
                           (vb << 60) | (sqw[r] << 61));
       } else {
@@ -876,8 +876,16 @@ void launch_part_scatter(hipStream_t s, const Batch &b, const TwParams &p, const
       // takes whole tiles at two workgroups per CU; three staged words on
       // whole tiles, one workgroup per CU, measured 0.43 against 0.34 ms per
       // C2 SQL batch on half tiles)
-      if (stable) hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 3, true>), g, th, 0, s, b, p, pp, pb, seq, sc);
-      else hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 3, false>), g, th, 0, s, b, p, pp, pb, seq, sc);
+      // (SEQ3 needs one window per record: tumbling / unwindowed ops)
+      const bool onewin = p.kind == HSG_TUMBLING || p.kind == HSG_UNWINDOWED;
+      if (stable && onewin)
+        hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 3, true, true>), g, th, 0, s, b, p, pp, pb, seq, sc);
+      else if (stable)
+        hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 3, true>), g, th, 0, s, b, p, pp, pb, seq, sc);
+      else if (onewin)
+        hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 3, false, true>), g, th, 0, s, b, p, pp, pb, seq, sc);
+      else
+        hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 3, false>), g, th, 0, s, b, p, pp, pb, seq, sc);
     } else if (pp.words - 1 == 2) {
       if (stable) hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs / 2, 2, true>), g, th, 0, s, b, p, pp, pb, seq, sc);
       else hipLaunchKernelGGL((k_part_scatter_st<kPartTileRecs, 2, false>), g, th, 0, s, b, p, pp, pb, seq, sc);
