@@ -776,4 +776,16 @@ int op_sink_info(const hsg_op *op, int *device, int *n_aggs, uint32_t *f64_mask,
 namespace hsg {
 // For the join (join.cpp): the engine's device.
 int engine_device(const hsg_engine *e) { return e ? e->device : 0; }
+int engine_split_comm(hsg_engine *e, Comm **out, int *rank, int *nranks, std::string &err) {
+  *out = nullptr;
+  *rank = e ? e->rank : 0;
+  *nranks = e ? e->nranks : 1;
+  if (!e || e->nranks <= 1 || !e->comm) {
+    *rank = 0;
+    *nranks = 1;
+    return HSG_OK;
+  }
+  std::lock_guard<std::mutex> lk(e->mu);
+  return comm_split(e->comm, out, err);
+}
 }  // namespace hsg

@@ -39,7 +39,19 @@ struct JoinBatchDev {
   const uint32_t *jkey;
   const int64_t *ts;
   const uint64_t *handle;
+  uint32_t rank;    // sharded joins (nranks > 1): this rank stores and probes the
+  uint32_t nranks;  // records whose key it owns (join_owner); every record's timestamp
+                    // still enters the timestamp set (side | 4 marks a record owned elsewhere)
 };
+
+// the rank that stores and probes record key k
+__host__ __device__ inline uint32_t join_owner(uint32_t k, uint32_t nranks) {
+  return nranks > 1 ? (uint32_t)((key_hash(k) >> 32) % nranks) : 0u;
+}
+// the rank slices of an all-gathered batch (G slots of `stride` records, slice q
+// holding n_q at off[q] .. off[q + 1] of the global batch) -> the global batch
+void launch_join_compact(hipStream_t s, const JoinBatchDev &slots, uint64_t stride, const int64_t *off, int G,
+                         uint64_t n, uint8_t *side, uint32_t *key, uint32_t *jkey, int64_t *ts, uint64_t *handle);
 
 struct JoinOut {
   uint64_t *this_h;

@@ -8,8 +8,10 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/hstream_join.h"
+#include "hsg_exchange.h"
 #include "hsg_join.h"
 #include "hsg_sort.h"
 
@@ -18,6 +20,9 @@ using namespace hsg;
 namespace hsg {
 // hsg_api.cpp
 int engine_device(const hsg_engine *e);
+// a communicator of the engine's ranks for one sharded object (nullptr, rank
+// 0 of 1 on a single-rank engine)
+int engine_split_comm(hsg_engine *e, Comm **out, int *rank, int *nranks, std::string &err);
 }
 
 struct hsg_join {
@@ -49,6 +54,23 @@ struct hsg_join {
   // output rows
   JoinOut out = {};
   uint64_t out_cap = 0, pending = 0;
+  // sharded (the engine's ranks > 1): each rank pushes its slice of the
+  // poll batch; the slices are all-gathered into the global batch (rank
+  // order = arrival order), every rank keeps the whole timestamp set (the
+  // end-point rule reads any key's entries) and stores / probes the records
+  // whose key it owns (join_owner), so its rows are those records' rows
+  Comm *comm = nullptr;
+  int rank = 0, nranks = 1;
+  int64_t *d_n = nullptr, *d_nall = nullptr, *h_nall = nullptr;  // slice sizes (device, all-gathered, pinned)
+  int64_t *d_off = nullptr;                                       // [G + 1] slice offsets
+  uint8_t *r_side = nullptr;                                      // [G * batch_cap] all-gathered slots
+  uint32_t *r_key = nullptr, *r_jkey = nullptr;
+  int64_t *r_ts = nullptr;
+  uint64_t *r_handle = nullptr;
+  uint8_t *g_side = nullptr;                                      // [G * batch_cap] the global batch
+  uint32_t *g_key = nullptr, *g_jkey = nullptr;
+  int64_t *g_ts = nullptr;
+  uint64_t *g_handle = nullptr;
 };
 
 namespace {
@@ -80,6 +102,11 @@ void free_join(hsg_join *j) {
                   j->T, j->Tn, j->Tm, j->flag, j->soff, j->partial, j->tot, j->out.this_h, j->out.other_h,
                   j->out.jkey, j->out.ts};
   for (void *p : ptrs) dfree(p);
+  void *xptrs[] = {j->d_n, j->d_nall, j->d_off, j->r_side, j->r_key, j->r_jkey, j->r_ts, j->r_handle,
+                   j->g_side, j->g_key, j->g_jkey, j->g_ts, j->g_handle};
+  for (void *p : xptrs) dfree(p);
+  if (j->h_nall) hipHostFree(j->h_nall);
+  if (j->comm) comm_destroy(j->comm);
   if (j->h_tot) hipHostFree(j->h_tot);
   if (j->stream) hipStreamDestroy(j->stream);
   delete j;
@@ -186,7 +213,17 @@ extern "C" int hsg_join_create(hsg_engine *eng, const hsg_join_config *cfg, hsg_
   j->before = cfg->before_ms;
   j->after = cfg->after_ms;
   j->batch_cap = cfg->batch_capacity;
-  const uint64_t n = j->batch_cap;
+  {
+    std::string err;
+    const int rc = engine_split_comm(eng, &j->comm, &j->rank, &j->nranks, err);
+    if (rc != HSG_OK) {
+      free_join(j);
+      return rc;
+    }
+  }
+  const int G = j->nranks;
+  // (sharded: the global batch holds every rank's slice)
+  const uint64_t n = j->batch_cap * (uint64_t)G;
   hipError_t e = hipSetDevice(j->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&j->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = dmalloc(j->st_side, n);
@@ -208,6 +245,22 @@ extern "C" int hsg_join_create(hsg_engine *eng, const hsg_join_config *cfg, hsg_
   if (e == hipSuccess) e = hipMalloc(&j->sort_scratch, sort_scratch_bytes(n));
   if (e == hipSuccess) e = dmalloc(j->tot, 4);
   if (e == hipSuccess) e = hipHostMalloc((void **)&j->h_tot, 4 * sizeof(uint64_t), hipHostMallocDefault);
+  if (G > 1) {
+    if (e == hipSuccess) e = dmalloc(j->d_n, 1);
+    if (e == hipSuccess) e = dmalloc(j->d_nall, G);
+    if (e == hipSuccess) e = dmalloc(j->d_off, G + 1);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&j->h_nall, (G + 1) * sizeof(int64_t), hipHostMallocDefault);
+    if (e == hipSuccess) e = dmalloc(j->r_side, n);
+    if (e == hipSuccess) e = dmalloc(j->r_key, n);
+    if (e == hipSuccess) e = dmalloc(j->r_jkey, n);
+    if (e == hipSuccess) e = dmalloc(j->r_ts, n);
+    if (e == hipSuccess) e = dmalloc(j->r_handle, n);
+    if (e == hipSuccess) e = dmalloc(j->g_side, n);
+    if (e == hipSuccess) e = dmalloc(j->g_key, n);
+    if (e == hipSuccess) e = dmalloc(j->g_jkey, n);
+    if (e == hipSuccess) e = dmalloc(j->g_ts, n);
+    if (e == hipSuccess) e = dmalloc(j->g_handle, n);
+  }
   if (e != hipSuccess) {
     free_join(j);
     return e == hipErrorOutOfMemory ? HSG_E_OOM : HSG_E_DEVICE;
@@ -233,20 +286,20 @@ extern "C" int hsg_join_push(hsg_join *j, const hsg_join_batch *b) {
     return HSG_E_CAPACITY;
   }
   if (b->mem != HSG_MEM_HOST && b->mem != HSG_MEM_DEVICE) return HSG_E_INVALID;
-  const uint64_t n = b->n;
+  uint64_t n = b->n;
   if (n && (!b->side || !b->key_id || !b->join_key || !b->ts || !b->handle)) return HSG_E_INVALID;
-  if (!n) return HSG_OK;
+  if (!n && j->nranks == 1) return HSG_OK;  // (sharded: every rank joins the all-gather, empty slice or not)
   try {
     JTRY(hipSetDevice(j->device));
     hipStream_t s = j->stream;
-    int rc = ensure_state(j, j->nR + n, j->nT + n);
-    if (rc != HSG_OK) return rc;
     JoinBatchDev db;
     db.n = n;
-    if (b->mem == HSG_MEM_DEVICE) {
+    db.rank = (uint32_t)j->rank;
+    db.nranks = (uint32_t)j->nranks;
+    if (b->mem == HSG_MEM_DEVICE && j->nranks == 1) {
       db.side = b->side, db.key = b->key_id, db.jkey = b->join_key, db.ts = b->ts, db.handle = b->handle;
-    } else {
-      const hipMemcpyKind k = hipMemcpyHostToDevice;
+    } else if (n) {
+      const hipMemcpyKind k = b->mem == HSG_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
       JTRY(hipMemcpyAsync(j->st_side, b->side, n, k, s));
       JTRY(hipMemcpyAsync(j->st_key, b->key_id, n * 4, k, s));
       JTRY(hipMemcpyAsync(j->st_jkey, b->join_key, n * 4, k, s));
@@ -254,6 +307,50 @@ extern "C" int hsg_join_push(hsg_join *j, const hsg_join_batch *b) {
       JTRY(hipMemcpyAsync(j->st_handle, b->handle, n * 8, k, s));
       db.side = j->st_side, db.key = j->st_key, db.jkey = j->st_jkey, db.ts = j->st_ts, db.handle = j->st_handle;
     }
+    if (j->nranks > 1) {
+      // every rank's slice size, then the slices (padded to the largest) and
+      // the global batch in rank order
+      const int G = j->nranks;
+      j->h_nall[0] = (int64_t)n;
+      JTRY(hipMemcpyAsync(j->d_n, j->h_nall, 8, hipMemcpyHostToDevice, s));
+      int rc = comm_allgather(j->comm, j->d_n, j->d_nall, 1, ncclInt64, 8, s, j->err);
+      if (rc != HSG_OK) return rc;
+      JTRY(hipMemcpyAsync(j->h_nall, j->d_nall, G * 8, hipMemcpyDeviceToHost, s));
+      JTRY(hipStreamSynchronize(s));
+      uint64_t mx = 0, tot = 0;
+      std::vector<int64_t> off(G + 1, 0);
+      for (int q = 0; q < G; ++q) {
+        const uint64_t nq = (uint64_t)j->h_nall[q];
+        mx = nq > mx ? nq : mx;
+        off[q] = (int64_t)tot;
+        tot += nq;
+      }
+      off[G] = (int64_t)tot;
+      if (!tot) return HSG_OK;  // (every rank saw the same sizes)
+      if (mx > j->batch_cap) {
+        j->err = "a rank's batch is larger than batch_capacity";
+        return HSG_E_CAPACITY;
+      }
+      JTRY(hipMemcpyAsync(j->d_off, off.data(), (G + 1) * 8, hipMemcpyHostToDevice, s));
+      JTRY(hipStreamSynchronize(s));  // (off is a host temporary)
+      if ((rc = comm_group_start(j->comm, j->err)) != HSG_OK) return rc;
+      if ((rc = comm_allgather(j->comm, j->st_side, j->r_side, mx, ncclUint8, 1, s, j->err)) != HSG_OK) return rc;
+      if ((rc = comm_allgather(j->comm, j->st_key, j->r_key, mx, ncclUint32, 4, s, j->err)) != HSG_OK) return rc;
+      if ((rc = comm_allgather(j->comm, j->st_jkey, j->r_jkey, mx, ncclUint32, 4, s, j->err)) != HSG_OK) return rc;
+      if ((rc = comm_allgather(j->comm, j->st_ts, j->r_ts, mx, ncclInt64, 8, s, j->err)) != HSG_OK) return rc;
+      if ((rc = comm_allgather(j->comm, j->st_handle, j->r_handle, mx, ncclUint64, 8, s, j->err)) != HSG_OK)
+        return rc;
+      if ((rc = comm_group_end(j->comm, j->err)) != HSG_OK) return rc;
+      JoinBatchDev slots = db;
+      slots.side = j->r_side, slots.key = j->r_key, slots.jkey = j->r_jkey, slots.ts = j->r_ts,
+      slots.handle = j->r_handle;
+      launch_join_compact(s, slots, mx, j->d_off, G, tot, j->g_side, j->g_key, j->g_jkey, j->g_ts, j->g_handle);
+      n = tot;
+      db.n = n;
+      db.side = j->g_side, db.key = j->g_key, db.jkey = j->g_jkey, db.ts = j->g_ts, db.handle = j->g_handle;
+    }
+    int rc = ensure_state(j, j->nR + n, j->nT + n);
+    if (rc != HSG_OK) return rc;
     launch_join_build(s, db, j->braw);
     // 1. the batch by (record key, side, ts, arrival), merged into the state
     static const int m_passes[4] = {0, 1, 2, 3};

@@ -51,7 +51,8 @@ __global__ void k_join_build(JoinBatchDev b, JEnt *out) {
     e.jkey = b.jkey[i];
     e.ts = b.ts[i];
     e.handle = b.handle[i];
-    e.side = e.k == HSG_KEY_NONE ? 2u : (b.side[i] ? 1u : 0u);
+    const bool own = b.nranks <= 1 || join_owner(e.k, b.nranks) == b.rank;
+    e.side = e.k == HSG_KEY_NONE ? 2u : ((b.side[i] ? 1u : 0u) | (own ? 0u : 4u));
     e.arr = (uint32_t)i + 1;
     out[i] = e;
   }
@@ -95,14 +96,17 @@ __global__ void k_join_merge_b(const JEnt *R, uint64_t nR, const JEnt *B, uint64
 __global__ void k_join_tflags(const JEnt *Bt, uint64_t n, uint32_t *flag) {
   GRID_LOOP(i, n) {
     const JEnt &x = Bt[i];
-    flag[i] = x.side < 2 && (i == 0 || Bt[i - 1].side != x.side || Bt[i - 1].ts != x.ts) ? 1u : 0u;
+    // (a record another rank owns keeps its timestamp here: side & 3; the
+    // 2-bit side sort pass already ordered the batch by it)
+    const uint32_t sd = x.side & 3u;
+    flag[i] = sd < 2 && (i == 0 || (Bt[i - 1].side & 3u) != sd || Bt[i - 1].ts != x.ts) ? 1u : 0u;
   }
 }
 __global__ void k_join_twrite(const JEnt *Bt, uint64_t n, const uint32_t *flag, const uint64_t *off, TEnt *out) {
   GRID_LOOP(i, n) {
     if (!flag[i]) continue;
     TEnt t;
-    t.side = Bt[i].side;
+    t.side = Bt[i].side & 3u;
     t.arr = Bt[i].arr;  // the group is in arrival order: its first is the smallest
     t.ts = Bt[i].ts;
     out[off[i]] = t;
@@ -219,6 +223,24 @@ __global__ void k_join_tkeep_write(const TEnt *T, uint64_t n, const uint32_t *fl
   do { if (n) hipLaunchKernelGGL(k, dim3(grid_for(n, 256)), dim3(256), 0, s, __VA_ARGS__); } while (0)
 
 void launch_join_build(hipStream_t s, const JoinBatchDev &b, JEnt *out) { LAUNCH(k_join_build, b.n, b, out); }
+
+__global__ void k_join_compact(JoinBatchDev slots, uint64_t stride, const int64_t *off, int G, uint64_t n,
+                               uint8_t *side, uint32_t *key, uint32_t *jkey, int64_t *ts, uint64_t *handle) {
+  GRID_LOOP(i, n) {
+    int q = 0;
+    while (q + 1 < G && (uint64_t)off[q + 1] <= i) ++q;
+    const uint64_t src = (uint64_t)q * stride + (i - (uint64_t)off[q]);
+    side[i] = slots.side[src];
+    key[i] = slots.key[src];
+    jkey[i] = slots.jkey[src];
+    ts[i] = slots.ts[src];
+    handle[i] = slots.handle[src];
+  }
+}
+void launch_join_compact(hipStream_t s, const JoinBatchDev &slots, uint64_t stride, const int64_t *off, int G,
+                         uint64_t n, uint8_t *side, uint32_t *key, uint32_t *jkey, int64_t *ts, uint64_t *handle) {
+  LAUNCH(k_join_compact, n, slots, stride, off, G, n, side, key, jkey, ts, handle);
+}
 void launch_join_sortkey(hipStream_t s, const JEnt *e, const uint32_t *perm, uint64_t n, int pass, uint32_t *key) {
   LAUNCH(k_join_sortkey, n, e, perm, n, pass, key);
 }

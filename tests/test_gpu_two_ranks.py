@@ -131,3 +131,102 @@ def test_two_ranks_equal_single_stream(spec_name, late):
         assert len(rows) == len(ref), (bi, len(rows), len(ref))
         for a, b in zip(rows, ref):
             assert a[:4] == b[:4] and _close(a[4], b[4]), (bi, a, b)
+
+
+# ---------------------------------------------------------------------------
+# the stream-stream join, sharded over two ranks (one GPU, host transport)
+# ---------------------------------------------------------------------------
+def _join_gen(seed, n, nkeys=40, grid=5, span=40_000):
+    rng = np.random.default_rng(seed)
+    side = (rng.random(n) < 0.5).astype(np.uint8)
+    key = rng.integers(0, nkeys, n).astype(np.uint32)
+    key[rng.random(n) < 0.01] = abi.HSG_KEY_NONE
+    jk = rng.integers(0, 3, n).astype(np.uint32)
+    jk[rng.random(n) < 0.03] = abi.HSG_KEY_NONE
+    ts = ((np.arange(n) * span) // n + rng.integers(0, 400, n)) // grid * grid
+    ts = ts.astype(np.int64) + 1_700_000_000_000
+    # handles name the record globally (the caller's values stay where they are)
+    handle = np.arange(n, dtype=np.uint64) + (np.uint64(seed) << np.uint64(32))
+    return side, key, jk, ts, handle
+
+
+JOIN_CASES = {"w100_50": (100, 50, 5), "w0_0": (0, 0, 1), "w250_0": (250, 0, 25)}
+
+
+def _join_slices(case, G):
+    """batches of the stream, each cut into G consecutive rank slices (rank
+    order = arrival order); the second batch's slice of rank 0 is empty"""
+    before, after, grid = JOIN_CASES[case]
+    side, key, jk, ts, h = _join_gen(before * 7 + after + grid, 12_000, grid=grid)
+    out = []
+    for bi, s0 in enumerate(range(0, len(ts), 3_000)):
+        b = [a[s0:s0 + 3_000] for a in (side, key, jk, ts, h)]
+        cuts = np.linspace(0, len(b[0]), G + 1).astype(int)
+        if bi == 1:
+            cuts[1] = 0
+        out.append([tuple(a[cuts[r]:cuts[r + 1]] for a in b) for r in range(G)])
+    return before, after, out
+
+
+def _join_worker(rank, G, name, case, q):
+    try:
+        from hstream_amd.engine import Engine
+        from hstream_amd.join import Join
+        eng = Engine(device=0, rank=rank, nranks=G, comm_id=name, batch_capacity=1 << 13,
+                     transport=abi.HSG_TRANSPORT_HOST)
+        before, after, batches = _join_slices(case, G)
+        j = Join(eng, before, after, batch_capacity=1 << 12)
+        rows = []
+        for slices in batches:
+            j.push(*slices[rank])
+            th, oh, k, t = j.drain()
+            rows.append(list(zip(th.tolist(), oh.tolist(), k.tolist(), t.tolist())))
+        st = j.state_rows()
+        j.close()
+        eng.close()
+        q.put((rank, rows, st))
+    except Exception as e:
+        q.put((rank, "error", repr(e)))
+
+
+@pytest.mark.parametrize("case", list(JOIN_CASES))
+def test_two_ranks_join_equal_single_stream(case):
+    """Each rank pushes its slice of every poll batch; the slices are
+    all-gathered, every rank keeps the whole timestamp set and stores /
+    probes the records whose key it owns. The union of the two ranks' rows
+    (each rank's in arrival order) is the single-stream join's, and the two
+    stores hold the single store's entries between them."""
+    import multiprocessing as mp
+    import joinref
+    G = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = f"hsgj-{os.getpid()}-{uuid.uuid4().hex[:12]}"
+    procs = [ctx.Process(target=_join_worker, args=(r, G, name, case, q)) for r in range(G)]
+    for p in procs:
+        p.start()
+    try:
+        outs = [q.get(timeout=100) for _ in range(G)]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    errs = [o for o in outs if o[1] == "error"]
+    assert not errs, errs
+    outs.sort(key=lambda o: o[0])
+    before, after, batches = _join_slices(case, G)
+    ref = joinref.JoinRef(before, after)
+    total = 0
+    for bi, slices in enumerate(batches):
+        whole = [np.concatenate([s[a] for s in slices]) for a in range(5)]
+        exp = ref.push(*whole)
+        got = outs[0][1][bi] + outs[1][1][bi]
+        assert sorted(got) == sorted(exp), (bi, len(got), len(exp))
+        # each rank's rows in the single stream's order
+        for r in range(G):
+            mine = [x for x in exp if x in set(outs[r][1][bi])]
+            assert outs[r][1][bi] == mine, (bi, r)
+        total += len(exp)
+    assert outs[0][2] + outs[1][2] == ref.state_rows()
+    assert total > 0 or JOIN_CASES[case][:2] == (0, 0)
