@@ -64,7 +64,7 @@ __global__ void k_join_sortkey(const JEnt *e, const uint32_t *perm, uint64_t n, 
     uint32_t v;
     if (pass == 0) v = (uint32_t)(uint64_t)x.ts;
     else if (pass == 1) v = (uint32_t)((uint64_t)x.ts >> 32) ^ 0x80000000u;
-    else if (pass == 2) v = x.side;
+    else if (pass == 2) v = x.side & 3u;  // (a record another rank owns sorts by its side: all of its key's are)
     else v = x.k;
     key[i] = v;
   }
