@@ -11,7 +11,7 @@ ARGS="$*"
 run() { n=$1; shift; if [ -z "$ARGS" ] || [[ " $ARGS " == *" $n "* ]]; then b $n "$@" || exit $?; fi; }
 run c2_default --steps 5 --warmup 2 --cpu-seconds 10
 run c2f --config C2f --steps 5 --warmup 2 --cpu-seconds 10 --no-per-record
-run c5 --config C5 --steps 3 --warmup 1 --cpu-seconds 10 --no-per-record
+run c5 --config C5 --steps 3 --warmup 1 --cpu-seconds 10
 run c3 --config C3 --steps 2 --warmup 1 --cpu-seconds 10 --no-per-record
 run c4 --config C4 --steps 2 --warmup 1 --cpu-seconds 10 --no-per-record
 run c3_pr --config C3 --emit per_record --records 100663296 --steps 2 --warmup 1 --cpu-seconds 10 --no-per-record
