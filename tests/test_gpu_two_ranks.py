@@ -230,3 +230,112 @@ def test_two_ranks_join_equal_single_stream(case):
         total += len(exp)
     assert outs[0][2] + outs[1][2] == ref.state_rows()
     assert total > 0 or JOIN_CASES[case][:2] == (0, 0)
+
+
+# ---------------------------------------------------------------------------
+# literal forms through the exchange: the decimal bits ride the
+# sequenced exchange's valid bytes (bit 1) and the classic exchange's packed
+# word; the sharded result, forms included, equals one GPU fed the whole
+# stream (whose forms tests/test_sink.py and test_gpu_sql_shape.py pin
+# against the reference's sequential fold)
+# ---------------------------------------------------------------------------
+FORM_AGGS = [(abi.HSG_LAST, 0), (abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0), (abi.HSG_MIN, 1), (abi.HSG_MAX, 0),
+             (abi.HSG_SUM, 1)]
+FORM_SPECS = {
+    "tumbling_batch": OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=10_000,
+                             col_types=[abi.HSG_I64, abi.HSG_F64], aggs=FORM_AGGS, flags=abi.HSG_OPF_LITERAL_FORMS),
+    "tumbling_changes": OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_RECORD, size_ms=10_000,
+                               col_types=[abi.HSG_I64, abi.HSG_F64], aggs=FORM_AGGS, flags=abi.HSG_OPF_LITERAL_FORMS),
+    "session_batch": OpSpec(abi.HSG_SESSION, abi.HSG_EMIT_PER_BATCH, gap_ms=2_000,
+                            col_types=[abi.HSG_I64, abi.HSG_F64], aggs=FORM_AGGS, flags=abi.HSG_OPF_LITERAL_FORMS),
+    "session_changes": OpSpec(abi.HSG_SESSION, abi.HSG_EMIT_PER_RECORD, gap_ms=2_000,
+                              col_types=[abi.HSG_I64, abi.HSG_F64], aggs=FORM_AGGS, flags=abi.HSG_OPF_LITERAL_FORMS),
+}
+
+
+def _form_slices(G):
+    """the protocol batches with decimal literals (valid bit 1) on 1 in 4
+    present values and a narrow value range (ties)"""
+    rng = np.random.default_rng(77)
+    out = []
+    for slices in _batches(G, False):
+        ns = []
+        for key, ts, cols, valid in slices:
+            c0 = (cols[0] % 7).astype(np.int64)
+            c1 = np.round(cols[1] % 5.0, 1)
+            v = [(va | ((rng.random(len(va)) < 0.25) & (va != 0)).astype(np.uint8) << 1).astype(np.uint8)
+                 for va in valid]
+            ns.append((key, ts, [c0, c1], v))
+        out.append(ns)
+    return out
+
+
+def _form_rows(spec, r):
+    src = [-1] * len(r) if spec.emit_mode == abi.HSG_EMIT_PER_BATCH else r.src_index.tolist()
+    return [(int(r.key_id[i]), int(r.win_start[i]), int(r.win_end[i]), int(src[i]), int(r.form[i]),
+             tuple(a[i].item() for a in r.aggs)) for i in range(len(r))]
+
+
+def _form_worker(rank, G, name, spec_name, classic, q):
+    try:
+        from hstream_amd.engine import Engine, testing_knob
+        eng = Engine(device=0, rank=rank, nranks=G, comm_id=name, batch_capacity=1 << 13,
+                     transport=abi.HSG_TRANSPORT_HOST)
+        spec = FORM_SPECS[spec_name]
+        with testing_knob(abi.HSG_KNOB_X_CLASSIC, 1 if classic else 0):
+            op = eng.op(spec)
+        wm, results = -1, []
+        for slices in _form_slices(G):
+            key, ts, cols, valid = slices[rank]
+            wm = op.push(key, ts, cols, valid, watermark=wm)
+            results.append(_form_rows(spec, op.drain()))
+        op.close()
+        eng.close()
+        q.put((rank, wm, results))
+    except Exception as e:
+        q.put((rank, "error", repr(e)))
+
+
+@pytest.mark.parametrize("classic", [False, True], ids=["sequenced", "classic"])
+@pytest.mark.parametrize("spec_name", list(FORM_SPECS))
+def test_two_ranks_literal_forms(spec_name, classic):
+    import multiprocessing as mp
+    from hstream_amd.engine import Engine
+    G = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = f"hsgf-{os.getpid()}-{uuid.uuid4().hex[:12]}"
+    procs = [ctx.Process(target=_form_worker, args=(r, G, name, spec_name, classic, q)) for r in range(G)]
+    for p in procs:
+        p.start()
+    try:
+        outs = [q.get(timeout=100) for _ in range(G)]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    errs = [o for o in outs if o[1] == "error"]
+    assert not errs, errs
+    outs.sort(key=lambda o: o[0])
+    # one GPU fed the whole stream
+    spec = FORM_SPECS[spec_name]
+    eng = Engine(device=0, batch_capacity=1 << 14)
+    op = eng.op(spec)
+    wm, ref = -1, []
+    for slices in _form_slices(G):
+        key = np.concatenate([s[0] for s in slices])
+        ts = np.concatenate([s[1] for s in slices])
+        cols = [np.concatenate([s[2][c] for s in slices]) for c in range(2)]
+        valid = [np.concatenate([s[3][c] for s in slices]) for c in range(2)]
+        wm = op.push(key, ts, cols, valid, watermark=wm)
+        ref.append(_form_rows(spec, op.drain()))
+    op.close()
+    eng.close()
+    assert all(o[1] == wm for o in outs)
+    for bi in range(len(ref)):
+        got = sorted(outs[0][2][bi] + outs[1][2][bi], key=lambda t: (t[3], t[1], t[0], t[2], t[4], repr(t[5])))
+        exp = sorted(ref[bi], key=lambda t: (t[3], t[1], t[0], t[2], t[4], repr(t[5])))
+        assert len(got) == len(exp), (bi, len(got), len(exp))
+        for a, b in zip(got, exp):
+            assert a[:5] == b[:5] and _close(a[5], b[5]), (bi, a, b)
