@@ -180,6 +180,8 @@ static void adapt_partitions(OpDevice &d, const hsg_op_config &cfg, const Progra
   // are twice as long and the (tile, bucket) offsets matrix half the size
   // (C2: scatter 164 -> 137 us, aggregation 113 -> 126 us, 30.5 -> 32.3 G
   // records/s HBM-resident); HSG_AGG_SMALL keeps the small table (A/B)
+  // (two-slot ops -- C5's SUM / MAX -- measured the same on either table:
+  // 23.25 against 23.31 G records/s; hopping ops already take the big one)
   static const bool keep_small = getenv("HSG_AGG_SMALL") != nullptr;
   const bool prefer_big = !keep_small && cfg.window_kind != HSG_HOPPING && d.pane_S == 1 && prog.n_slots > 2;
   d.agg_big = (want > (1ull << kPartMaxLog2) || prefer_big) && !d.sql_lean;  // (the SQL lean kernels: one LDS variant)
