@@ -295,6 +295,8 @@ struct RowPtrs {
   int64_t *p[kMaxAggs];
 };
 void launch_clear_scalars(hipStream_t s, DevScalars *sc);
+// copy into the pinned host mirror h, then clear (the end of a push)
+void launch_fetch_clear_scalars(hipStream_t s, DevScalars *sc, DevScalars *h);
 void launch_copy_rows(hipStream_t s, const OutCols &src, uint64_t from, uint64_t n, int n_aggs, uint32_t *key,
                       int64_t *ws, int64_t *we, int64_t *si, const RowPtrs &aggs, uint32_t *form = nullptr);
 void launch_fill_u64(hipStream_t s, uint64_t *p, uint64_t n, uint64_t v);

@@ -76,6 +76,7 @@ struct OpDevice {
   DevScalars *sc = nullptr;     // device
   DevScalars *h_sc = nullptr;   // pinned host mirror
   bool sc_clean = false;        // per-batch scalars already cleared on the stream
+  hipEvent_t ev_fetch = nullptr;  // after the fetch of the scalars (fetch_scalars)
   uint64_t batch_cap = 0;       // records this op can take in one push (after exchange)
   int32_t user_cols = 0;        // value columns of the caller's batches (n_cols: the kernels', internal)
   bool forms = false;           // HSG_OPF_LITERAL_FORMS: rows carry literal forms (hsg_rows.form)

@@ -144,6 +144,30 @@ __global__ void k_clear_scalars(DevScalars *sc) {
 }
 void launch_clear_scalars(hipStream_t s, DevScalars *sc) { hipLaunchKernelGGL(k_clear_scalars, dim3(1), dim3(64), 0, s, sc); }
 
+// The end of every push: the scalars into the pinned host mirror (one 8-byte
+// word per lane, vector stores), then the per-batch ones cleared for the next
+// batch -- one launch where a copy and a clear took two.
+__global__ void k_fetch_clear_scalars(DevScalars *sc, DevScalars *h) {
+  static_assert(sizeof(DevScalars) == 64 * 8, "one word per lane");
+  const int t = threadIdx.x;
+  reinterpret_cast<uint64_t *>(h)[t] = reinterpret_cast<const uint64_t *>(sc)[t];
+  __syncthreads();
+  if (t == 0) {
+    sc->err = 0;
+    sc->pairs = 0;
+    sc->late = 0;
+    sc->out_rows = 0;
+    sc->touched = 0;
+    sc->redo = 0;
+    sc->packed = 0;
+    sc->kbase = 0;
+  }
+  if (t < kScratchWords) sc->scratch[t] = 0;
+}
+void launch_fetch_clear_scalars(hipStream_t s, DevScalars *sc, DevScalars *h) {
+  hipLaunchKernelGGL(k_fetch_clear_scalars, dim3(1), dim3(64), 0, s, sc, h);
+}
+
 // changelog rows [from, from + n) of src into device columns (null = skip), one launch
 __global__ void k_copy_rows(OutCols src, uint64_t from, uint64_t n, int n_aggs, uint32_t *key, int64_t *ws, int64_t *we,
                             int64_t *si, RowPtrs aggs, uint32_t *form) {
