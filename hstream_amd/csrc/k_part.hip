@@ -941,14 +941,54 @@ __global__ __launch_bounds__(256) void k_part_colsum(const uint32_t *__restrict_
   if (w == 0 && b < nb) segsum[(uint64_t)b * nseg + blockIdx.y] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
 
+// FUSED (segment sums of at most kColFused entries): no separate scan -- a
+// workgroup's base is the sum of the contiguous bucket-major prefix of the
+// segment sums before its 64 buckets (<= 64 KiB of L2 reads), plus a wave
+// scan of its buckets' totals and the bucket's own earlier segments; three
+// launches fewer per batch.
+constexpr uint64_t kColFused = 16384;
+template <bool FUSED>
 __global__ __launch_bounds__(256) void k_part_colscan(const uint32_t *__restrict__ hist, uint64_t tiles, int nb,
                                                       uint32_t nseg, const uint64_t *__restrict__ segoff,
+                                                      const uint32_t *__restrict__ segsum,
                                                       uint32_t *__restrict__ offt, uint64_t *__restrict__ bstart,
                                                       const DevScalars *sc) {
   __shared__ uint32_t red[4][64];
+  __shared__ uint64_t s_pre[4];
   if (sc->redo) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int b = blockIdx.x * 64 + lane;
+  uint64_t base = 0;  // FUSED: segoff[b * nseg + blockIdx.y]
+  if constexpr (FUSED) {
+    // (16-byte loads, all in flight at once: pre_n is a multiple of 64)
+    constexpr int NQ = (int)(kColFused / 4 / 256);
+    const uint32_t n4 = (uint32_t)((uint64_t)blockIdx.x * 64 * nseg / 4);
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(segsum);
+    uint4 qv[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const uint32_t i = threadIdx.x + (uint32_t)k * 256;
+      qv[k] = i < n4 ? s4[i] : make_uint4(0, 0, 0, 0);
+    }
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) acc += (uint64_t)qv[k].x + qv[k].y + qv[k].z + qv[k].w;
+    acc = wave_incl_sum(acc);
+    if (lane == 63) s_pre[w] = acc;
+    uint64_t tot = 0, mine = 0;
+    if (b < nb)
+      for (uint32_t q = 0; q < nseg; ++q) {
+        const uint32_t v = segsum[(uint64_t)b * nseg + q];
+        tot += v;
+        if (q < blockIdx.y) mine += v;
+      }
+    const uint64_t incl = wave_incl_sum(tot);
+    __syncthreads();
+    const uint64_t pre = s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3];
+    base = pre + (incl - tot) + mine;
+    // records placed: the last bucket block's end
+    if (blockIdx.x == gridDim.x - 1 && blockIdx.y == 0 && threadIdx.x == 63) bstart[nb] = pre + incl;
+  }
   const uint64_t t0 = (uint64_t)blockIdx.y * kColSeg, t1 = t0 + kColSeg < tiles ? t0 + kColSeg : tiles;
   // each wave a quarter of the segment's tiles: their sum, then the running
   // prefix (the second read is served by L2); loads unrolled so that many
@@ -965,7 +1005,8 @@ __global__ __launch_bounds__(256) void k_part_colscan(const uint32_t *__restrict
   red[w][lane] = sum;
   __syncthreads();
   if (b >= nb) return;
-  uint64_t run = segoff[(uint64_t)b * nseg + blockIdx.y];
+  uint64_t run = FUSED ? base : segoff[(uint64_t)b * nseg + blockIdx.y];
+  const uint64_t b0 = run;  // blockIdx.y == 0: the bucket's start
   for (int k = 0; k < w; ++k) run += red[k][lane];
   uint32_t *op = offt + r0 * nb + b;
 #pragma unroll 16
@@ -973,7 +1014,7 @@ __global__ __launch_bounds__(256) void k_part_colscan(const uint32_t *__restrict
     op[(uint64_t)k * nb] = (uint32_t)run;
     run += hp[(uint64_t)k * nb];
   }
-  if (blockIdx.y == 0 && w == 0) bstart[b] = segoff[(uint64_t)b * nseg];
+  if (blockIdx.y == 0 && w == 0) bstart[b] = b0;
 }
 
 void launch_part_offsets(hipStream_t s, const PartParams &pp, const PartBuffers &pb, DevScalars *sc,
@@ -986,9 +1027,14 @@ void launch_part_offsets(hipStream_t s, const PartParams &pp, const PartBuffers 
   memset(&off, 0, sizeof(off));
   hipLaunchKernelGGL(k_part_colsum, dim3(g.x + 1, g.y), dim3(256), 0, s, pb.hist, pp.tiles, nb, nseg, pb.segsum, sc,
                      da ? *da : off);
+  if ((uint64_t)nb * nseg <= kColFused) {
+    hipLaunchKernelGGL(k_part_colscan<true>, g, dim3(256), 0, s, pb.hist, pp.tiles, nb, nseg, nullptr, pb.segsum,
+                       pb.offt, pb.bstart, sc);
+    return;
+  }
   scan_excl_u32(s, pb.segsum, pb.segoff, (uint64_t)nb * nseg, pb.partial, pb.bstart + nb);
-  hipLaunchKernelGGL(k_part_colscan, g, dim3(256), 0, s, pb.hist, pp.tiles, nb, nseg, pb.segoff, pb.offt, pb.bstart,
-                     sc);
+  hipLaunchKernelGGL(k_part_colscan<false>, g, dim3(256), 0, s, pb.hist, pp.tiles, nb, nseg, pb.segoff, pb.segsum,
+                     pb.offt, pb.bstart, sc);
 }
 
 // ---------------------------------------------------------------------------

@@ -74,6 +74,16 @@ def test_c4_sessions_reduced(eng, mode):
     _drive_cfg(eng, cfg, spec, cfg.n, 1 << 18, faithful_sessions=False)
 
 
+def test_c2_one_bench_batch_exact(eng):
+    """One 2^24-record C2 batch, the bench's batch size (4096 partition tiles:
+    the offsets' segment sums take the one-workgroup scan of up to 2^15
+    elements), row for row against the oracle."""
+    cfg = datagen.CONFIGS["C2"]
+    n = 1 << 24
+    spec = cfg.spec(abi.HSG_EMIT_PER_BATCH, state_capacity=cfg.keys * 64)
+    _drive_cfg(eng, cfg, spec, n, n)
+
+
 def test_c5_zipf_reduced(eng):
     cfg = datagen.CONFIGS["C5"]
     n = 2_000_000
