@@ -943,10 +943,10 @@ __global__ __launch_bounds__(256) void k_part_colsum(const uint32_t *__restrict_
 
 // FUSED (segment sums of at most kColFused entries): no separate scan -- a
 // workgroup's base is the sum of the contiguous bucket-major prefix of the
-// segment sums before its 64 buckets (<= 64 KiB of L2 reads), plus a wave
+// segment sums before its 64 buckets (<= 128 KiB of L2 reads), plus a wave
 // scan of its buckets' totals and the bucket's own earlier segments; three
 // launches fewer per batch.
-constexpr uint64_t kColFused = 16384;
+constexpr uint64_t kColFused = 32768;
 template <bool FUSED>
 __global__ __launch_bounds__(256) void k_part_colscan(const uint32_t *__restrict__ hist, uint64_t tiles, int nb,
                                                       uint32_t nseg, const uint64_t *__restrict__ segoff,
@@ -960,19 +960,21 @@ __global__ __launch_bounds__(256) void k_part_colscan(const uint32_t *__restrict
   const int b = blockIdx.x * 64 + lane;
   uint64_t base = 0;  // FUSED: segoff[b * nseg + blockIdx.y]
   if constexpr (FUSED) {
-    // (16-byte loads, all in flight at once: pre_n is a multiple of 64)
-    constexpr int NQ = (int)(kColFused / 4 / 256);
+    // (16-byte loads, 16 per thread in flight at once: pre_n is a multiple of 64)
+    constexpr int NQ = 16;
     const uint32_t n4 = (uint32_t)((uint64_t)blockIdx.x * 64 * nseg / 4);
     const uint4 *s4 = reinterpret_cast<const uint4 *>(segsum);
-    uint4 qv[NQ];
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) {
-      const uint32_t i = threadIdx.x + (uint32_t)k * 256;
-      qv[k] = i < n4 ? s4[i] : make_uint4(0, 0, 0, 0);
-    }
     uint64_t acc = 0;
+    for (uint32_t i0 = 0; i0 < n4; i0 += NQ * 256) {
+      uint4 qv[NQ];
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) acc += (uint64_t)qv[k].x + qv[k].y + qv[k].z + qv[k].w;
+      for (int k = 0; k < NQ; ++k) {
+        const uint32_t i = i0 + threadIdx.x + (uint32_t)k * 256;
+        qv[k] = i < n4 ? s4[i] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) acc += (uint64_t)qv[k].x + qv[k].y + qv[k].z + qv[k].w;
+    }
     acc = wave_incl_sum(acc);
     if (lane == 63) s_pre[w] = acc;
     uint64_t tot = 0, mine = 0;
