@@ -905,6 +905,11 @@ constexpr uint64_t kSigSqlF2 = sig_ops_at(HSG_SQL_C2_OPS(S_SUM_F, S_MIN_F, S_MAX
 static_assert(ProgSig<kSigSqlI, kSigSqlI2>::count() == 11 && ProgSig<kSigSqlI, kSigSqlI2>::aux_of(8) == 7 &&
                   ProgSig<kSigSqlI, kSigSqlI2>::aux_of(10) == 9,
               "SQL C2 signature");
+// and its C5 query, `SELECT v, SUM(v), MAX(v)` of an i64 column: seven slots
+constexpr uint64_t kSigSqlSumMaxI =
+    sig_ops_at({S_LAST_SEQ, S_LAST_VAL, S_LAST_FORM, S_SUM_I, S_CNT_DEC, S_MAX_I, S_TIE_MAX}, 0);
+static_assert(ProgSig<kSigSqlSumMaxI, 0>::count() == 7 && ProgSig<kSigSqlSumMaxI, 0>::aux_of(6) == 5,
+              "SQL C5 signature");
 
 // the state-slot class (k_agg_s{2,4,6,8}.hip) a program of n slots runs in
 constexpr int ms_class(int n) { return n <= 2 ? 2 : n <= 4 ? 4 : n <= 6 ? 6 : 8; }

@@ -137,6 +137,8 @@ struct SqlLay<ProgSig<A, B>> {
 };
 static_assert(SqlLay<ProgSig<kSigSqlI, kSigSqlI2>>::ncols(12) == 8 && SqlLay<ProgSig<kSigSqlI, kSigSqlI2>>::packable(),
               "SQL C2 LDS layout");
+static_assert(SqlLay<ProgSig<kSigSqlSumMaxI, 0>>::ncols(8) == 6 && SqlLay<ProgSig<kSigSqlSumMaxI, 0>>::packable(),
+              "SQL C5 LDS layout");
 constexpr int kCntBits = 21;
 
 // phase 1 of one record on LDS entry e (column-major, ST entries per column)
@@ -754,7 +756,9 @@ __global__ __launch_bounds__(256) void k_sql_apply(Program prog, TwParams p, Par
 uint64_t sql_lds_entries(const Program &prog) {
   uint64_t hi = 0;
   const uint64_t sq = program_sig(prog, &hi);
-  return ((sq == kSigSqlI && hi == kSigSqlI2) || (sq == kSigSqlF && hi == kSigSqlF2)) ? 2048 : 1024;
+  return ((sq == kSigSqlI && hi == kSigSqlI2) || (sq == kSigSqlF && hi == kSigSqlF2) || (sq == kSigSqlSumMaxI && !hi))
+             ? 2048
+             : 1024;
 }
 
 // the op shape this path takes: one-window packed records with the sequence
@@ -783,12 +787,16 @@ bool launch_part_agg_sql(hipStream_t s, dim3 g, const Program &prog, const TwPar
   if (out) oc = *out;
   // 1024 LDS entries (part_lds_entries: buckets of <= 512 groups): 8 + 8 MS
   // bytes each, one 1024-thread workgroup per CU at 12 slots
-  if (prog.n_slots <= 8) sql_launch<8, 1024, 512>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
-  else if (prog.n_slots <= 12) {
-    // the SQL drop-in's C2 query: its slot program baked in
-    uint64_t hi = 0;
-    const uint64_t sq = program_sig(prog, &hi);
-    // (its packed LDS layout: a 2048-entry table, buckets of twice the groups)
+  // the SQL drop-in's C2 and C5 queries: their slot programs baked in, in
+  // the packed LDS layout (a 2048-entry table, buckets of twice the groups)
+  uint64_t hi = 0;
+  const uint64_t sq = program_sig(prog, &hi);
+  if (prog.n_slots <= 8) {
+    if (sq == kSigSqlSumMaxI && !hi)
+      sql_launch<8, 2048, 1024, kSigSqlSumMaxI, 0>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
+    else
+      sql_launch<8, 1024, 512>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
+  } else if (prog.n_slots <= 12) {
     if (sq == kSigSqlI && hi == kSigSqlI2)
       sql_launch<12, 2048, 1024, kSigSqlI, kSigSqlI2>(s, g, prog, p, pp, t, pb, sc, oc, out_base, out_cap);
     else if (sq == kSigSqlF && hi == kSigSqlF2)

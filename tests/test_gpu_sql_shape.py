@@ -56,7 +56,7 @@ def _gen(seed, n, start, total, nkeys, f64, absent=0.03, dec=0.3, vr=40):
     return key, ts.astype(np.int64), v, valid
 
 
-def _prefix_forms(gid, v, valid, f64):
+def _prefix_forms(gid, v, valid, f64, aggs=AGGS):
     """Literal-form word (hsg_rows.form) of each record's group right after
     the record, in arrival order: the reference's sequential fold."""
     import pandas as pd
@@ -91,7 +91,7 @@ def _prefix_forms(gid, v, valid, f64):
 
     per = {"sum": (sum_dec == 0).astype(np.int64), "min": bits(tmin), "max": bits(tmax), "last": bits(tlast)}
     word = np.zeros(n, np.int64)
-    for j, (k, _c) in enumerate(AGGS):
+    for j, (k, _c) in enumerate(aggs):
         if k in FORM:
             word |= per[FORM[k]] << (2 * j)
     out = np.empty(n, np.uint32)
@@ -152,21 +152,28 @@ def test_sql_shape_c2_reduced(emit, f64):
     eng.close()
 
 
+# BASELINE C5's query in the SQL shape, `SELECT v, SUM(v), MAX(v)` (a baked
+# slot program of its own in k_agg_sql)
+AGGS_C5 = [(abi.HSG_LAST, 0), (abi.HSG_SUM, 0), (abi.HSG_MAX, 0)]
+
+
+@pytest.mark.parametrize("query", ["c2", "c5"])
 @pytest.mark.parametrize("f64", [False, True], ids=["i64", "f64"])
-def test_sql_shape_hot_keys_and_full_tables(f64):
+def test_sql_shape_hot_keys_and_full_tables(f64, query):
     """The SQL shape on skewed keys (BASELINE C5's shape, reduced): a hot key
     whose bucket is split over several aggregation workgroups, and buckets
     with more groups than a chunk's LDS table holds (each such record a
     partial of its own). Both meet in k_sql_apply under the rows' locks, in
     any order; the changelog then comes from the touched list. Every batch
     stays on the SQL lean kernels; values, forms and ties match the oracle
-    and the reference's sequential fold."""
+    and the reference's sequential fold. Both the C2 query and C5's."""
     import pyoracle
     from hstream_amd.engine import Engine
     nb, per = 2, 1_500_000
     total = nb * per
     ct = abi.HSG_F64 if f64 else abi.HSG_I64
-    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=60_000, col_types=[ct], aggs=AGGS,
+    aggs = AGGS if query == "c2" else AGGS_C5
+    spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_BATCH, size_ms=60_000, col_types=[ct], aggs=aggs,
                   flags=abi.HSG_OPF_LITERAL_FORMS)
     rng = np.random.default_rng(11 + f64)
     batches = []
@@ -180,7 +187,7 @@ def test_sql_shape_hot_keys_and_full_tables(f64):
     v = np.concatenate([b[2] for b in batches])
     valid = np.concatenate([b[3] for b in batches])
     gid = key.astype(np.int64) * 1_000_000 + (ts // 60_000 - TS0 // 60_000)
-    fw = _prefix_forms(gid, v, valid, f64)
+    fw = _prefix_forms(gid, v, valid, f64, aggs)
     eng = Engine(device=0, batch_capacity=per)
     g = eng.op(spec)
     o = pyoracle.OracleOp(spec)
