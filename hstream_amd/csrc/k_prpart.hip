@@ -1900,6 +1900,15 @@ static void pr_launch(hipStream_t s, const Batch &b, const Program &prog, const 
         done = true;
       }
     }
+    if constexpr (MS == 8) {
+      // the SQL drop-in's C5 query (its 7 slots exactly)
+      uint64_t hi = 0;
+      const uint64_t sq = program_sig(prog, &hi);
+      if (reg && sq == kSigSqlSumMaxI && !hi) {
+        hipLaunchKernelGGL((k_pr_bucket<7, LT, true, kSigSqlSumMaxI, 0>), gb, tb, 0, s, prog, p, pp, t, pb, pr, sc);
+        done = true;
+      }
+    }
     if constexpr (MS == 12) {
       // the SQL drop-in's C2 query (literal forms, a passthrough)
       uint64_t hi = 0;

@@ -219,7 +219,7 @@ def test_sql_shape_hot_keys_and_full_tables(f64, query):
     eng.close()
 
 
-@pytest.mark.parametrize("shape", ["sql", "plain"])
+@pytest.mark.parametrize("shape", ["sql", "sql_c5", "plain"])
 def test_per_record_hot_key_chunked(shape):
     """EMIT CHANGES of a one-window op with a hot key (its partition bucket far
     over kPrHot records): the batch takes the chunked path (chunks of the
@@ -230,8 +230,8 @@ def test_per_record_hot_key_chunked(shape):
     from hstream_amd.engine import Engine
     nb, per = 2, 1_000_000
     total = nb * per
-    aggs = AGGS if shape == "sql" else [(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0), (abi.HSG_MAX, 0)]
-    flags = abi.HSG_OPF_LITERAL_FORMS if shape == "sql" else 0
+    aggs = {"sql": AGGS, "sql_c5": AGGS_C5}.get(shape, [(abi.HSG_COUNT_ALL, 0), (abi.HSG_SUM, 0), (abi.HSG_MAX, 0)])
+    flags = abi.HSG_OPF_LITERAL_FORMS if shape != "plain" else 0
     spec = OpSpec(abi.HSG_TUMBLING, abi.HSG_EMIT_PER_RECORD, size_ms=60_000, col_types=[abi.HSG_I64], aggs=aggs,
                   flags=flags)
     rng = np.random.default_rng(31)
@@ -246,12 +246,12 @@ def test_per_record_hot_key_chunked(shape):
     o = pyoracle.OracleOp(spec)
     f64s = spec.agg_is_f64()
     fw = None
-    if shape == "sql":
+    if shape != "plain":
         key = np.concatenate([b[0] for b in batches])
         ts = np.concatenate([b[1] for b in batches])
         gid = key.astype(np.int64) * 1_000_000 + (ts // 60_000 - TS0 // 60_000)
         fw = _prefix_forms(gid, np.concatenate([b[2] for b in batches]), np.concatenate([b[3] for b in batches]),
-                           False)
+                           False, aggs)
     wg = wo = -1
     for bi, (k, t, c, va) in enumerate(batches):
         wg = g.push(k, t, [c], [va], watermark=wg)
