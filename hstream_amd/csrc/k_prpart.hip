@@ -547,14 +547,17 @@ __global__ __launch_bounds__(256) void k_pr_carry(Program prog, TwParams p, Part
   const uint32_t bid = (uint32_t)p.batch_id;
   uint32_t fresh = 0, err = 0;
   uint64_t touched = 0;
-  for (uint32_t c = c0; c < c1; ++c) {
-    const uint32_t base = pr.cbase[c], cnt = pr.ccnt[c];
-    // CU partials per thread and pass: their group keys, totals and home-slot
-    // keys loaded together (one wait instead of one per partial)
-    constexpr int CU = 4;
-    for (uint32_t e0 = threadIdx.x; e0 < cnt; e0 += 256 * CU) {
-    uint64_t gk[CU], hk[CU];
-    int64_t tt[CU][MS];
+  // The chunks of a bucket form a chain (each reads the rows the one before
+  // it wrote), so the latency per chunk is the bucket's time -- a hot key's
+  // bucket has ~10^3 chunks. Per pass of CU partials per thread: the partials
+  // were loaded during the previous pass (prefetch, overlapping its store
+  // drain), and each one's home row -- key, stamp and slots share a line --
+  // is loaded in one go: one round trip plus the drain per chunk where the
+  // partial, home-key and row loads took three.
+  constexpr int CU = 4;
+  uint64_t gk[CU];
+  int64_t tt[CU][MS];
+  auto load_pass = [&](uint32_t base, uint32_t cnt, uint32_t e0) {
 #pragma unroll
     for (int u = 0; u < CU; ++u) {
       const uint32_t e = e0 + u * 256;
@@ -562,11 +565,29 @@ __global__ __launch_bounds__(256) void k_pr_carry(Program prog, TwParams p, Part
 #pragma unroll
       for (int s = 0; s < MS; ++s) tt[u][s] = (e < cnt && s < ns) ? pr.part[(uint64_t)(base + e) * ns + s] : 0;
     }
+  };
+  uint32_t c = c0, pass = 0, base = 0, cnt = 0;
+  if (c < c1) {
+    base = pr.cbase[c];
+    cnt = pr.ccnt[c];
+    load_pass(base, cnt, threadIdx.x);
+  }
+  while (c < c1) {
+    const uint32_t e0 = threadIdx.x + pass * (256 * CU);
+    uint64_t hk[CU];
+    uint32_t hst[CU];
+    int64_t hrow[CU][MS];
 #pragma unroll
-    for (int u = 0; u < CU; ++u)
-      hk[u] = gk[u] != kEmpty ? __hip_atomic_load(t.key(tw_region_base(t, gk[u]) + tw_home_in(t, gk[u])),
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                              : kEmpty;
+    for (int u = 0; u < CU; ++u) {
+      hk[u] = kEmpty;
+      if (gk[u] == kEmpty) continue;
+      const uint64_t hs = tw_region_base(t, gk[u]) + tw_home_in(t, gk[u]);
+      hk[u] = __hip_atomic_load(t.key(hs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      hst[u] = __hip_atomic_load(t.stamp(hs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int s = 0; s < MS; ++s)
+        hrow[u][s] = s < ns ? __hip_atomic_load(t.aggs(hs) + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    }
 #pragma unroll
     for (int u = 0; u < CU; ++u) {
       const uint32_t e = e0 + u * 256;
@@ -581,8 +602,15 @@ __global__ __launch_bounds__(256) void k_pr_carry(Program prog, TwParams p, Part
       uint64_t sl = tw_home_in(t, g);
       const uint64_t step = tw_step(t), np = (t.rmask + 1) / step;
       int64_t slot = -1;
-      bool isnew = false;
-      if (hk[u] == g) slot = (int64_t)(rb + sl);  // found at its home slot (the usual case)
+      bool isnew = false, loaded = false;
+      uint32_t st = 0;
+      if (hk[u] == g) {  // found at its home slot (the usual case), its row loaded with the key
+        slot = (int64_t)(rb + sl);
+        loaded = true;
+        st = hst[u];
+#pragma unroll
+        for (int s = 0; s < MS; ++s) cur[s] = hrow[u][s];
+      }
       for (uint64_t probe = 0; slot < 0 && probe < np && probe < kMaxProbes; ++probe) {
         uint64_t *kp = t.key(rb + sl);
         const uint64_t k = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -618,12 +646,12 @@ __global__ __launch_bounds__(256) void k_pr_carry(Program prog, TwParams p, Part
         uint32_t *stp = t.stamp(slot);
         if (isnew) {
           identity_row<MS>(prog, cur);
-        } else {
+        } else if (!loaded) {
 #pragma unroll
           for (int s = 0; s < MS; ++s)
             cur[s] = s < ns ? __hip_atomic_load(row + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+          st = __hip_atomic_load(stp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        const uint32_t st = isnew ? 0u : __hip_atomic_load(stp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int64_t nv[MS];
 #pragma unroll
         for (int s = 0; s < MS; ++s) nv[s] = cur[s];
@@ -631,7 +659,7 @@ __global__ __launch_bounds__(256) void k_pr_carry(Program prog, TwParams p, Part
 #pragma unroll
         for (int s = 0; s < MS; ++s)
           if (s < ns) row[s] = nv[s];
-        if (st != bid) {
+        if (st != bid) {  // (a new row: st = 0)
           *stp = bid;
           touched += 1;
         }
@@ -640,13 +668,30 @@ __global__ __launch_bounds__(256) void k_pr_carry(Program prog, TwParams p, Part
       for (int s = 0; s < MS; ++s)
         if (s < ns) pr.part[(uint64_t)gi * ns + s] = cur[s];
     }
+    // the next pass (uniform): more of this chunk, else the next chunk --
+    // its partials loaded now, beside this pass's stores
+    uint32_t nc = c, npass = pass + 1;
+    if ((uint64_t)npass * (256 * CU) >= cnt) {
+      nc = c + 1;
+      npass = 0;
     }
-    // this chunk's rows in L2 before the next chunk reads them: the same
-    // workgroup (one CU, one L2) reads them back with L1-bypassing loads, so
-    // draining the stores is enough (no device-scope fence: a whole-L2 write-
-    // back per chunk)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (nc < c1) {
+      if (nc != c) {
+        base = pr.cbase[nc];
+        cnt = pr.ccnt[nc];
+      }
+      load_pass(base, cnt, threadIdx.x + npass * (256 * CU));
+    }
+    if (nc != c) {
+      // this chunk's rows in L2 before the next chunk reads them: the same
+      // workgroup (one CU, one L2) reads them back with L1-bypassing loads, so
+      // draining the stores is enough (no device-scope fence: a whole-L2 write-
+      // back per chunk)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    c = nc;
+    pass = npass;
   }
   if (err) atomicOr(&sc->err, err);
   const uint64_t f = wave_sum_u64(fresh), tc = wave_sum_u64(touched);
