@@ -199,7 +199,7 @@ static int push_sharded_fast(OpDevice &d, const hsg_op_config &cfg, const Progra
   rc = comm_allgather(comm, x.info, x.info_all, IW, ncclInt64, 8, s, err);
   if (rc != HSG_OK) return rc;
   DTRY(hipMemcpyAsync(x.h_info, x.info_all, (uint64_t)G * IW * 8, hipMemcpyDeviceToHost, s));
-  DTRY(hipStreamSynchronize(s));
+  if ((rc = poll_stream(d, s, err)) != HSG_OK) return rc;
   const int64_t *H = x.h_info;
   if ((rc = check_room(d, H, G, err)) != HSG_OK) return rc;
   int64_t wm_global = a.wm_in, carry = a.wm_in, min_ts = INT64_MAX;
@@ -383,7 +383,7 @@ static int push_sharded_seq(OpDevice &d, const hsg_op_config &cfg, const Program
   rc = comm_allgather(comm, x.info, x.info_all, IW, ncclInt64, 8, s, err);
   if (rc != HSG_OK) return rc;
   DTRY(hipMemcpyAsync(x.h_info, x.info_all, (uint64_t)G * IW * 8, hipMemcpyDeviceToHost, s));
-  DTRY(hipStreamSynchronize(s));
+  if ((rc = poll_stream(d, s, err)) != HSG_OK) return rc;
   const int64_t *H = x.h_info;
   if ((rc = check_room(d, H, G, err)) != HSG_OK) return rc;
   int64_t wm_global = a.wm_in, carry = a.wm_in, min_ts = INT64_MAX;
@@ -540,7 +540,7 @@ static int push_sharded_classic(OpDevice &d, const hsg_op_config &cfg, const Pro
   rc = comm_allgather(comm, x.info, x.info_all, IW, ncclInt64, 8, s, err);
   if (rc != HSG_OK) return rc;
   DTRY(hipMemcpyAsync(x.h_info, x.info_all, (uint64_t)G * IW * 8, hipMemcpyDeviceToHost, s));
-  DTRY(hipStreamSynchronize(s));
+  if ((rc = poll_stream(d, s, err)) != HSG_OK) return rc;
   const int64_t *H = x.h_info;
   if ((rc = check_room(d, H, G, err)) != HSG_OK) return rc;
   int64_t wm_global = a.wm_in, carry = a.wm_in, min_ts = INT64_MAX;

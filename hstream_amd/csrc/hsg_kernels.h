@@ -13,6 +13,8 @@ int stage_batch(OpDevice &d, const hsg_batch *b, Batch &kb, std::string &err, in
 TwParams make_tw_params(const hsg_op_config &cfg, const PushArgs &a);
 void launch_stream_time(OpDevice &d, const hsg_op_config &cfg, const Batch &kb, int64_t wm_in, int64_t adv);
 int fetch_scalars(OpDevice &d, std::string &err);
+// wait for stream s: poll an event (5 ms), then block
+int poll_stream(OpDevice &d, hipStream_t s, std::string &err);
 int clear_batch_scalars(OpDevice &d, std::string &err);
 int finish_batch(OpDevice &d, int64_t wm_in, uint64_t n, PushResult &r, std::string &err);
 int push_local(OpDevice &d, const hsg_op_config &cfg, const Program &prog, const PushArgs &a, const Batch &kb,

@@ -628,25 +628,30 @@ void launch_stream_time(OpDevice &d, const hsg_op_config &cfg, const Batch &kb, 
 // Copies the scalars to the host mirror, then (same stream, before the host
 // waits) clears the per-batch ones for the next batch, so a push does not
 // start with a dependent launch.
+// The host waits on the stream inside every push (here, and on the exchange's
+// all-gathered facts), so the wake-up latency is GPU idle time: poll an event
+// for up to 5 ms (a batch's pipeline is well under that), then block.
+int poll_stream(OpDevice &d, hipStream_t s, std::string &err) {
+  DTRY(hipEventRecord(d.ev_fetch, s));
+  const auto t0 = std::chrono::steady_clock::now();
+  hipError_t e;
+  while ((e = hipEventQuery(d.ev_fetch)) == hipErrorNotReady) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) {
+      e = hipEventSynchronize(d.ev_fetch);
+      break;
+    }
+  }
+  DTRY(e);
+  return HSG_OK;
+}
+
 int fetch_scalars(OpDevice &d, std::string &err) {
   launch_fetch_clear_scalars(d.stream, d.sc, d.h_sc);
   DTRY(hipGetLastError());
-  // The host waits on every push, so the wake-up latency is GPU idle time:
-  // poll the event for up to 5 ms (a batch's pipeline is well under that),
-  // then block. Against hipStreamSynchronize plus a separate copy and clear:
-  // C2 34.7 -> 34.8 G, C5 24.2 -> 24.5 G records/s HBM-resident (profiles/r06).
-  DTRY(hipEventRecord(d.ev_fetch, d.stream));
-  {
-    const auto t0 = std::chrono::steady_clock::now();
-    hipError_t e;
-    while ((e = hipEventQuery(d.ev_fetch)) == hipErrorNotReady) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) {
-        e = hipEventSynchronize(d.ev_fetch);
-        break;
-      }
-    }
-    DTRY(e);
-  }
+  // (against hipStreamSynchronize plus a separate copy and clear: C2 34.7 ->
+  // 34.8 G, C5 24.2 -> 24.5 G records/s HBM-resident, profiles/r06)
+  const int rc = poll_stream(d, d.stream, err);
+  if (rc != HSG_OK) return rc;
   for (int k = 0; k < 8; ++k) d.h_sc->live += d.h_sc->live_x[k];  // device: live + shards
   d.ovf_rows += d.h_sc->scratch[33];  // groups a full region sent to the overflow rows (cleared above)
   d.sc_clean = true;
